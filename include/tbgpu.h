@@ -1,0 +1,302 @@
+/*
+ * tbgpu.h — C ABI of the MI355X-native TigerBeetle commit engine.
+ *
+ * This is the drop-in boundary for the `create_accounts` / `create_transfers`
+ * arms of `StateMachine.commit` (reference: src/state_machine.zig:894-928,
+ * `execute` :1002-1088).  A thin Zig `extern "C"` shim in
+ * src/state_machine.zig binds these symbols.
+ *
+ * Plain C: fixed-layout structs, pointers and sizes.  No torch, no HIP types.
+ *
+ * Struct layouts are byte-identical to the reference's extern structs
+ *   Account               src/tigerbeetle.zig:7-40      (tb_client.h:26-40)
+ *   Transfer              src/tigerbeetle.zig:80-105    (tb_client.h:51-65)
+ *   CreateAccountsResult  src/tigerbeetle.zig:247-255   (tb_client.h:150-153)
+ *   CreateTransfersResult src/tigerbeetle.zig:257-265   (tb_client.h:155-158)
+ * and the result codes are the reference enums (src/tigerbeetle.zig:125-245),
+ * whose numeric value equals their precedence index.
+ */
+#ifndef TBGPU_H
+#define TBGPU_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* u128 as two little-endian u64 words (the reference targets little-endian only,
+ * src/tigerbeetle.zig:306-309). */
+typedef struct tb_uint128_t { uint64_t lo, hi; } tb_uint128_t;
+
+typedef struct tb_account_t {
+    tb_uint128_t id;
+    tb_uint128_t debits_pending;
+    tb_uint128_t debits_posted;
+    tb_uint128_t credits_pending;
+    tb_uint128_t credits_posted;
+    tb_uint128_t user_data_128;
+    uint64_t user_data_64;
+    uint32_t user_data_32;
+    uint32_t reserved;
+    uint32_t ledger;
+    uint16_t code;
+    uint16_t flags;
+    uint64_t timestamp;
+} tb_account_t;
+
+typedef struct tb_transfer_t {
+    tb_uint128_t id;
+    tb_uint128_t debit_account_id;
+    tb_uint128_t credit_account_id;
+    tb_uint128_t amount;
+    tb_uint128_t pending_id;
+    tb_uint128_t user_data_128;
+    uint64_t user_data_64;
+    uint32_t user_data_32;
+    uint32_t timeout;
+    uint32_t ledger;
+    uint16_t code;
+    uint16_t flags;
+    uint64_t timestamp;
+} tb_transfer_t;
+
+/* {index, result}: sparse, only non-ok events, ascending index. */
+typedef struct tb_create_accounts_result_t { uint32_t index; uint32_t result; } tb_create_accounts_result_t;
+typedef struct tb_create_transfers_result_t { uint32_t index; uint32_t result; } tb_create_transfers_result_t;
+
+/* AccountHistoryGrooveValue, src/state_machine.zig:275-294 (256 B). */
+typedef struct tb_account_history_t {
+    tb_uint128_t dr_account_id;
+    tb_uint128_t dr_debits_pending;
+    tb_uint128_t dr_debits_posted;
+    tb_uint128_t dr_credits_pending;
+    tb_uint128_t dr_credits_posted;
+    tb_uint128_t cr_account_id;
+    tb_uint128_t cr_debits_pending;
+    tb_uint128_t cr_debits_posted;
+    tb_uint128_t cr_credits_pending;
+    tb_uint128_t cr_credits_posted;
+    uint64_t timestamp;
+    uint8_t reserved[88];
+} tb_account_history_t;
+
+/* AccountFlags, src/tigerbeetle.zig:42-63 */
+enum {
+    TB_ACCOUNT_LINKED = 1 << 0,
+    TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS = 1 << 1,
+    TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS = 1 << 2,
+    TB_ACCOUNT_HISTORY = 1 << 3,
+};
+/* TransferFlags, src/tigerbeetle.zig:107-120 */
+enum {
+    TB_TRANSFER_LINKED = 1 << 0,
+    TB_TRANSFER_PENDING = 1 << 1,
+    TB_TRANSFER_POST_PENDING_TRANSFER = 1 << 2,
+    TB_TRANSFER_VOID_PENDING_TRANSFER = 1 << 3,
+    TB_TRANSFER_BALANCING_DEBIT = 1 << 4,
+    TB_TRANSFER_BALANCING_CREDIT = 1 << 5,
+};
+
+/* CreateAccountResult, src/tigerbeetle.zig:125-160 */
+enum {
+    TB_CREATE_ACCOUNT_OK = 0,
+    TB_CREATE_ACCOUNT_LINKED_EVENT_FAILED = 1,
+    TB_CREATE_ACCOUNT_LINKED_EVENT_CHAIN_OPEN = 2,
+    TB_CREATE_ACCOUNT_TIMESTAMP_MUST_BE_ZERO = 3,
+    TB_CREATE_ACCOUNT_RESERVED_FIELD = 4,
+    TB_CREATE_ACCOUNT_RESERVED_FLAG = 5,
+    TB_CREATE_ACCOUNT_ID_MUST_NOT_BE_ZERO = 6,
+    TB_CREATE_ACCOUNT_ID_MUST_NOT_BE_INT_MAX = 7,
+    TB_CREATE_ACCOUNT_FLAGS_ARE_MUTUALLY_EXCLUSIVE = 8,
+    TB_CREATE_ACCOUNT_DEBITS_PENDING_MUST_BE_ZERO = 9,
+    TB_CREATE_ACCOUNT_DEBITS_POSTED_MUST_BE_ZERO = 10,
+    TB_CREATE_ACCOUNT_CREDITS_PENDING_MUST_BE_ZERO = 11,
+    TB_CREATE_ACCOUNT_CREDITS_POSTED_MUST_BE_ZERO = 12,
+    TB_CREATE_ACCOUNT_LEDGER_MUST_NOT_BE_ZERO = 13,
+    TB_CREATE_ACCOUNT_CODE_MUST_NOT_BE_ZERO = 14,
+    TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_FLAGS = 15,
+    TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_USER_DATA_128 = 16,
+    TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_USER_DATA_64 = 17,
+    TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_USER_DATA_32 = 18,
+    TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_LEDGER = 19,
+    TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_CODE = 20,
+    TB_CREATE_ACCOUNT_EXISTS = 21,
+};
+
+/* CreateTransferResult, src/tigerbeetle.zig:165-245 */
+enum {
+    TB_CREATE_TRANSFER_OK = 0,
+    TB_CREATE_TRANSFER_LINKED_EVENT_FAILED = 1,
+    TB_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN = 2,
+    TB_CREATE_TRANSFER_TIMESTAMP_MUST_BE_ZERO = 3,
+    TB_CREATE_TRANSFER_RESERVED_FLAG = 4,
+    TB_CREATE_TRANSFER_ID_MUST_NOT_BE_ZERO = 5,
+    TB_CREATE_TRANSFER_ID_MUST_NOT_BE_INT_MAX = 6,
+    TB_CREATE_TRANSFER_FLAGS_ARE_MUTUALLY_EXCLUSIVE = 7,
+    TB_CREATE_TRANSFER_DEBIT_ACCOUNT_ID_MUST_NOT_BE_ZERO = 8,
+    TB_CREATE_TRANSFER_DEBIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX = 9,
+    TB_CREATE_TRANSFER_CREDIT_ACCOUNT_ID_MUST_NOT_BE_ZERO = 10,
+    TB_CREATE_TRANSFER_CREDIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX = 11,
+    TB_CREATE_TRANSFER_ACCOUNTS_MUST_BE_DIFFERENT = 12,
+    TB_CREATE_TRANSFER_PENDING_ID_MUST_BE_ZERO = 13,
+    TB_CREATE_TRANSFER_PENDING_ID_MUST_NOT_BE_ZERO = 14,
+    TB_CREATE_TRANSFER_PENDING_ID_MUST_NOT_BE_INT_MAX = 15,
+    TB_CREATE_TRANSFER_PENDING_ID_MUST_BE_DIFFERENT = 16,
+    TB_CREATE_TRANSFER_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER = 17,
+    TB_CREATE_TRANSFER_AMOUNT_MUST_NOT_BE_ZERO = 18,
+    TB_CREATE_TRANSFER_LEDGER_MUST_NOT_BE_ZERO = 19,
+    TB_CREATE_TRANSFER_CODE_MUST_NOT_BE_ZERO = 20,
+    TB_CREATE_TRANSFER_DEBIT_ACCOUNT_NOT_FOUND = 21,
+    TB_CREATE_TRANSFER_CREDIT_ACCOUNT_NOT_FOUND = 22,
+    TB_CREATE_TRANSFER_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER = 23,
+    TB_CREATE_TRANSFER_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS = 24,
+    TB_CREATE_TRANSFER_PENDING_TRANSFER_NOT_FOUND = 25,
+    TB_CREATE_TRANSFER_PENDING_TRANSFER_NOT_PENDING = 26,
+    TB_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_DEBIT_ACCOUNT_ID = 27,
+    TB_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_CREDIT_ACCOUNT_ID = 28,
+    TB_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_LEDGER = 29,
+    TB_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_CODE = 30,
+    TB_CREATE_TRANSFER_EXCEEDS_PENDING_TRANSFER_AMOUNT = 31,
+    TB_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_AMOUNT = 32,
+    TB_CREATE_TRANSFER_PENDING_TRANSFER_ALREADY_POSTED = 33,
+    TB_CREATE_TRANSFER_PENDING_TRANSFER_ALREADY_VOIDED = 34,
+    TB_CREATE_TRANSFER_PENDING_TRANSFER_EXPIRED = 35,
+    TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_FLAGS = 36,
+    TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_DEBIT_ACCOUNT_ID = 37,
+    TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_CREDIT_ACCOUNT_ID = 38,
+    TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_AMOUNT = 39,
+    TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_PENDING_ID = 40,
+    TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_128 = 41,
+    TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_64 = 42,
+    TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_32 = 43,
+    TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_TIMEOUT = 44,
+    TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_CODE = 45,
+    TB_CREATE_TRANSFER_EXISTS = 46,
+    TB_CREATE_TRANSFER_OVERFLOWS_DEBITS_PENDING = 47,
+    TB_CREATE_TRANSFER_OVERFLOWS_CREDITS_PENDING = 48,
+    TB_CREATE_TRANSFER_OVERFLOWS_DEBITS_POSTED = 49,
+    TB_CREATE_TRANSFER_OVERFLOWS_CREDITS_POSTED = 50,
+    TB_CREATE_TRANSFER_OVERFLOWS_DEBITS = 51,
+    TB_CREATE_TRANSFER_OVERFLOWS_CREDITS = 52,
+    TB_CREATE_TRANSFER_OVERFLOWS_TIMEOUT = 53,
+    TB_CREATE_TRANSFER_EXCEEDS_CREDITS = 54,
+    TB_CREATE_TRANSFER_EXCEEDS_DEBITS = 55,
+};
+
+/* constants.batch_max.create_transfers with production constants:
+ * (message_size_max 1 MiB - 256 B header) / 128 B (src/state_machine.zig:53-76). */
+#define TBGPU_BATCH_MAX 8190u
+
+/* ------------------------------------------------------------------------ */
+/* Engine                                                                    */
+/* ------------------------------------------------------------------------ */
+
+typedef struct tbgpu_ctx tbgpu_ctx;
+
+/* Options replace StateMachine.Options (src/state_machine.zig:328-334): the
+ * cache sizes become HBM table capacities. Zero means "default". */
+typedef struct tbgpu_options {
+    int32_t  device;              /* HIP device ordinal */
+    uint32_t reserved0;
+    uint64_t accounts_max;        /* accounts the ctx must hold                     */
+    uint64_t transfers_max;       /* stored transfers (rows) the ctx must hold      */
+    uint64_t history_max;         /* account-history rows                            */
+    uint64_t events_per_call_max; /* events one (multi-batch) call may carry        */
+    uint32_t flags;               /* TBGPU_OPT_*                                    */
+    uint32_t reserved1;
+} tbgpu_options;
+
+enum {
+    TBGPU_OPT_FORCE_GENERAL = 1u << 0, /* disable the balance-insensitive fast path (tests) */
+};
+
+/* Replaces StateMachine.init/deinit (src/state_machine.zig:418-451).
+ * Returns 0 on success; on failure *out is NULL and the return is a negative errno-like code. */
+int  tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options);
+void tbgpu_deinit(tbgpu_ctx* ctx);
+/* StateMachine.reset (src/state_machine.zig:453): forget all state. */
+void tbgpu_reset(tbgpu_ctx* ctx);
+
+/* execute(.create_accounts) — src/state_machine.zig:1002-1088, :1198-1237.
+ * `timestamp` is the prepare timestamp handed to commit (the events get
+ * timestamp - n + index + 1). Returns the number of sparse results written
+ * (reply bytes = 8 * count). Host buffers, 16-byte aligned, caller-owned. */
+uint32_t tbgpu_create_accounts(tbgpu_ctx* ctx, uint64_t timestamp,
+                               const tb_account_t* events, uint32_t count,
+                               tb_create_accounts_result_t* results);
+
+/* execute(.create_transfers) — src/state_machine.zig:1002-1088, :1239-1573. */
+uint32_t tbgpu_create_transfers(tbgpu_ctx* ctx, uint64_t timestamp,
+                                const tb_transfer_t* events, uint32_t count,
+                                tb_create_transfers_result_t* results);
+
+/* Streaming form: `batch_count` consecutive commits of create_transfers, with
+ * identical results to calling tbgpu_create_transfers once per batch in order.
+ * Batch b has `counts[b]` events starting after the previous batch's events and
+ * prepare timestamp `timestamps[b]`.  Results of batch b are written at
+ * `results + (sum of counts before b)`; `result_counts[b]` receives its count.
+ * Returns the total number of results. */
+uint64_t tbgpu_create_transfers_batches(tbgpu_ctx* ctx, uint32_t batch_count,
+                                        const uint64_t* timestamps, const uint32_t* counts,
+                                        const tb_transfer_t* events,
+                                        tb_create_transfers_result_t* results,
+                                        uint32_t* result_counts);
+
+/* Same with the events already resident in device memory (HBM) and results left
+ * in device memory (same layout).  `timestamps`/`counts`/`result_counts` are host
+ * arrays.  `stream` is a hipStream_t passed as void* (NULL = the ctx stream). */
+uint64_t tbgpu_create_transfers_batches_device(tbgpu_ctx* ctx, uint32_t batch_count,
+                                               const uint64_t* timestamps, const uint32_t* counts,
+                                               const void* events_device,
+                                               void* results_device,
+                                               uint32_t* result_counts);
+
+uint64_t tbgpu_create_accounts_batches(tbgpu_ctx* ctx, uint32_t batch_count,
+                                       const uint64_t* timestamps, const uint32_t* counts,
+                                       const tb_account_t* events,
+                                       tb_create_accounts_result_t* results,
+                                       uint32_t* result_counts);
+
+/* execute_lookup_accounts / execute_lookup_transfers (src/state_machine.zig:1091-1126):
+ * found objects are written densely in request order; returns the count. */
+uint32_t tbgpu_lookup_accounts(tbgpu_ctx* ctx, const tb_uint128_t* ids, uint32_t count, tb_account_t* out);
+uint32_t tbgpu_lookup_transfers(tbgpu_ctx* ctx, const tb_uint128_t* ids, uint32_t count, tb_transfer_t* out);
+
+/* Test harness `setup` action (src/state_machine.zig:1892-1908): overwrite an
+ * existing account's four balances.  Returns 0, or -1 if the account is missing. */
+int tbgpu_test_set_balances(tbgpu_ctx* ctx, tb_uint128_t id,
+                            tb_uint128_t debits_pending, tb_uint128_t debits_posted,
+                            tb_uint128_t credits_pending, tb_uint128_t credits_posted);
+
+/* State export for parity checks (not on the reference's hot path). */
+uint64_t tbgpu_account_count(tbgpu_ctx* ctx);
+uint64_t tbgpu_transfer_count(tbgpu_ctx* ctx);
+uint64_t tbgpu_history_count(tbgpu_ctx* ctx);
+/* Stored transfers in commit order (rows [first, first+count)). */
+uint64_t tbgpu_export_transfers(tbgpu_ctx* ctx, uint64_t first, uint64_t count, tb_transfer_t* out);
+/* All accounts, in unspecified order. `capacity` bounds `out`. */
+uint64_t tbgpu_export_accounts(tbgpu_ctx* ctx, tb_account_t* out, uint64_t capacity);
+uint64_t tbgpu_export_history(tbgpu_ctx* ctx, uint64_t first, uint64_t count, tb_account_history_t* out);
+/* Posted groove (src/state_machine.zig:235-248): fulfillment of the pending transfer
+ * with this id: -1 none/not found, 0 posted, 1 voided. */
+int tbgpu_get_posted(tbgpu_ctx* ctx, tb_uint128_t pending_id);
+/* StateMachine.commit_timestamp (src/state_machine.zig:375). */
+uint64_t tbgpu_commit_timestamp(tbgpu_ctx* ctx);
+
+/* Diagnostics: statistics of the last call and the last error message. */
+typedef struct tbgpu_stats {
+    uint64_t events;          /* events in the last call                        */
+    uint32_t iterations;      /* fixed-point passes of the last call            */
+    uint32_t path;            /* 0 general (scan + rescan), 1 fast (no rescan)  */
+    uint64_t sorts;           /* side sorts performed                           */
+    double   device_ms;       /* HIP-event time of the last call's device work  */
+} tbgpu_stats;
+void tbgpu_last_stats(tbgpu_ctx* ctx, tbgpu_stats* out);
+int  tbgpu_last_error(tbgpu_ctx* ctx, char* buf, uint32_t len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TBGPU_H */

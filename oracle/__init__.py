@@ -1,0 +1,185 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes binding of the CPU oracle (oracle.c).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from tigerbeetle_amd.types import (ACCOUNT_DTYPE, HISTORY_DTYPE, RESULT_DTYPE, TRANSFER_DTYPE,
+                                   U64_MAX, u128_array)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+
+class U128(ctypes.Structure):
+    _fields_ = [("lo", ctypes.c_uint64), ("hi", ctypes.c_uint64)]
+
+
+def u128(v: int) -> U128:
+    return U128(v & U64_MAX, v >> 64)
+
+
+def build(force: bool = False) -> str:
+    """Compile oracle.c with gcc (oracle/Makefile)."""
+    if force or not os.path.exists(_LIB_PATH) or \
+            os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "oracle.c")):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_LIB_PATH)
+        vp, u32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
+        L.orc_new.restype = vp
+        L.orc_new.argtypes = [u64, u64]
+        L.orc_free.argtypes = [vp]
+        for name in ("orc_create_accounts", "orc_create_transfers"):
+            getattr(L, name).restype = u32
+            getattr(L, name).argtypes = [vp, u64, vp, u32, vp]
+        L.orc_create_transfers_batches.restype = u64
+        L.orc_create_transfers_batches.argtypes = [vp, u32, vp, vp, vp, vp, vp, ctypes.POINTER(ctypes.c_double)]
+        L.orc_create_accounts_batches.restype = u64
+        L.orc_create_accounts_batches.argtypes = [vp, u32, vp, vp, vp, vp, vp]
+        for name in ("orc_lookup_accounts", "orc_lookup_transfers"):
+            getattr(L, name).restype = u32
+            getattr(L, name).argtypes = [vp, vp, u32, vp]
+        L.orc_set_balances.restype = ctypes.c_int
+        L.orc_set_balances.argtypes = [vp, U128, U128, U128, U128, U128]
+        for name in ("orc_account_count", "orc_transfer_count", "orc_history_count", "orc_commit_timestamp"):
+            getattr(L, name).restype = u64
+            getattr(L, name).argtypes = [vp]
+        L.orc_export_accounts.restype = u64
+        L.orc_export_accounts.argtypes = [vp, vp, u64]
+        L.orc_export_transfers.restype = u64
+        L.orc_export_transfers.argtypes = [vp, u64, u64, vp]
+        L.orc_export_history.restype = u64
+        L.orc_export_history.argtypes = [vp, u64, u64, vp]
+        L.orc_get_posted.restype = ctypes.c_int
+        L.orc_get_posted.argtypes = [vp, U128]
+        L.orc_sum_overflows_u64.restype = ctypes.c_int
+        L.orc_sum_overflows_u64.argtypes = [u64, u64]
+        L.orc_sum_overflows_u128.restype = ctypes.c_int
+        L.orc_sum_overflows_u128.argtypes = [U128, U128]
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Oracle:
+    """Sequential reference semantics (one create_* per event, in order)."""
+
+    name = "oracle"
+
+    def __init__(self, accounts_hint: int = 1024, transfers_hint: int = 1024):
+        self._L = lib()
+        self._h = self._L.orc_new(accounts_hint, transfers_hint)
+
+    def close(self):
+        if self._h:
+            self._L.orc_free(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def create_accounts(self, timestamp: int, events: np.ndarray) -> np.ndarray:
+        events = np.ascontiguousarray(events, dtype=ACCOUNT_DTYPE)
+        out = np.zeros(max(len(events), 1), dtype=RESULT_DTYPE)
+        n = self._L.orc_create_accounts(self._h, timestamp, _ptr(events), len(events), _ptr(out))
+        return out[:n].copy()
+
+    def create_transfers(self, timestamp: int, events: np.ndarray) -> np.ndarray:
+        events = np.ascontiguousarray(events, dtype=TRANSFER_DTYPE)
+        out = np.zeros(max(len(events), 1), dtype=RESULT_DTYPE)
+        n = self._L.orc_create_transfers(self._h, timestamp, _ptr(events), len(events), _ptr(out))
+        return out[:n].copy()
+
+    def create_transfers_batches(self, timestamps, counts, events):
+        """Returns (results laid out per batch at the batch's event offset, result_counts, seconds)."""
+        ts = np.ascontiguousarray(timestamps, dtype=np.uint64)
+        cs = np.ascontiguousarray(counts, dtype=np.uint32)
+        events = np.ascontiguousarray(events, dtype=TRANSFER_DTYPE)
+        out = np.zeros(max(len(events), 1), dtype=RESULT_DTYPE)
+        rc = np.zeros(len(cs), dtype=np.uint32)
+        el = ctypes.c_double(0.0)
+        self._L.orc_create_transfers_batches(self._h, len(cs), _ptr(ts), _ptr(cs), _ptr(events), _ptr(out),
+                                             _ptr(rc), ctypes.byref(el))
+        return out, rc, el.value
+
+    def create_accounts_batches(self, timestamps, counts, events):
+        ts = np.ascontiguousarray(timestamps, dtype=np.uint64)
+        cs = np.ascontiguousarray(counts, dtype=np.uint32)
+        events = np.ascontiguousarray(events, dtype=ACCOUNT_DTYPE)
+        out = np.zeros(max(len(events), 1), dtype=RESULT_DTYPE)
+        rc = np.zeros(len(cs), dtype=np.uint32)
+        self._L.orc_create_accounts_batches(self._h, len(cs), _ptr(ts), _ptr(cs), _ptr(events), _ptr(out), _ptr(rc))
+        return out, rc
+
+    def lookup_accounts(self, ids) -> np.ndarray:
+        q = u128_array(list(ids))
+        out = np.zeros(max(len(q), 1), dtype=ACCOUNT_DTYPE)
+        n = self._L.orc_lookup_accounts(self._h, _ptr(q), len(q), _ptr(out))
+        return out[:n].copy()
+
+    def lookup_transfers(self, ids) -> np.ndarray:
+        q = u128_array(list(ids))
+        out = np.zeros(max(len(q), 1), dtype=TRANSFER_DTYPE)
+        n = self._L.orc_lookup_transfers(self._h, _ptr(q), len(q), _ptr(out))
+        return out[:n].copy()
+
+    def set_balances(self, id_, dp, dpo, cp, cpo) -> None:
+        rc = self._L.orc_set_balances(self._h, u128(id_), u128(dp), u128(dpo), u128(cp), u128(cpo))
+        assert rc == 0, "setup: account not found"
+
+    def account_count(self) -> int:
+        return self._L.orc_account_count(self._h)
+
+    def transfer_count(self) -> int:
+        return self._L.orc_transfer_count(self._h)
+
+    def history_count(self) -> int:
+        return self._L.orc_history_count(self._h)
+
+    def commit_timestamp(self) -> int:
+        return self._L.orc_commit_timestamp(self._h)
+
+    def export_accounts(self) -> np.ndarray:
+        n = self.account_count()
+        out = np.zeros(max(n, 1), dtype=ACCOUNT_DTYPE)
+        self._L.orc_export_accounts(self._h, _ptr(out), n)
+        return out[:n]
+
+    def export_transfers(self, first: int = 0, count: int | None = None) -> np.ndarray:
+        total = self.transfer_count()
+        count = total - first if count is None else count
+        out = np.zeros(max(count, 1), dtype=TRANSFER_DTYPE)
+        n = self._L.orc_export_transfers(self._h, first, count, _ptr(out))
+        return out[:n]
+
+    def export_history(self) -> np.ndarray:
+        n = self.history_count()
+        out = np.zeros(max(n, 1), dtype=HISTORY_DTYPE)
+        self._L.orc_export_history(self._h, 0, n, _ptr(out))
+        return out[:n]
+
+    def get_posted(self, pending_id: int) -> int:
+        return self._L.orc_get_posted(self._h, u128(pending_id))
+
+
+def sum_overflows(bits: int, a: int, b: int) -> bool:
+    L = lib()
+    if bits == 64:
+        return bool(L.orc_sum_overflows_u64(a, b))
+    return bool(L.orc_sum_overflows_u128(u128(a), u128(b)))

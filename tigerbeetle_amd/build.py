@@ -1,0 +1,69 @@
+"""Build libtbgpu.so (HIP for gfx950) in-tree, and the test oracle.
+
+    python -m tigerbeetle_amd.build
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+BUILD = os.path.join(PKG, "build")
+LIB = os.path.join(PKG, "libtbgpu.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("TBGPU_ARCH", "gfx950")
+CXXFLAGS = ["-std=c++17", "-O3", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+            "-Wno-unused-result", "-munsafe-fp-atomics"]
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_lib(verbose: bool = False, force: bool = False) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    sources = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    headers = sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(ROOT, "include", "tbgpu.h")]
+    objs = []
+    jobs = []
+    for src in sources:
+        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if force or _stale(obj, [src] + headers):
+            jobs.append([HIPCC, *CXXFLAGS, "-c", src, "-o", obj])
+    with cf.ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
+        for cmd, r in zip(jobs, ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), jobs)):
+            if verbose or r.returncode != 0:
+                sys.stderr.write(" ".join(cmd) + "\n" + r.stdout + r.stderr)
+            if r.returncode != 0:
+                raise RuntimeError(f"hipcc failed for {cmd[-3]}")
+    if force or jobs or _stale(LIB, objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            sys.stderr.write(r.stdout + r.stderr)
+            raise RuntimeError("link failed")
+    return LIB
+
+
+def build_oracle() -> str:
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    return os.path.join(ROOT, "oracle", "liboracle.so")
+
+
+def build_all(verbose: bool = False) -> None:
+    build_lib(verbose=verbose)
+    build_oracle()
+
+
+if __name__ == "__main__":
+    build_all(verbose="-v" in sys.argv)
+    print(LIB)

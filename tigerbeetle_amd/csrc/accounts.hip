@@ -1,0 +1,292 @@
+// accounts.hip — create_accounts as a batch-parallel fixed point, plus the
+// lookup / maintenance kernels.
+//
+// create_account (src/state_machine.zig:1198-1225) depends on earlier events
+// only through the id (a second create of the same id in the batch sees the
+// first) and through linked chains, so the same Jacobi sweep as transfers.hip
+// applies without the balance scan.
+#include "common.h"
+#include "engine.h"
+#include "transfers.h"
+
+namespace {
+
+__device__ __forceinline__ u32 ac_batch_of(const u32* __restrict__ b_start, u32 nb, u32 i) {
+    u32 lo = 0, hi = nb;
+    while (hi - lo > 1) {
+        const u32 mid = (lo + hi) >> 1;
+        if (b_start[mid] <= i) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ u32 ac_gtab_insert(const AcArgs& C, u128 key, u32 i) {
+    const u32 claim = i + 1;
+    u64 h = hash128(key) & C.gmask;
+    for (;;) {
+        u32 cur = C.gclaim[h];
+        if (cur == 0) {
+            const u32 prev = atomicCAS(&C.gclaim[h], 0u, claim);
+            if (prev == 0) return (u32)h;
+            cur = prev;
+        }
+        if (C.ev[cur - 1].id == key) return (u32)h;
+        h = (h + 1) & C.gmask;
+    }
+}
+
+__global__ void ac_classify(Tables T, AcArgs C) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= C.n) return;
+    const u32 b = ac_batch_of(C.b_start, C.nb, i);
+    const u32 bs = C.b_start[b], be = C.b_start[b + 1];
+    const u32 nbatch = be - bs, k = i - bs;
+    const Account a = C.ev[i];
+    C.ts[i] = C.b_ts[b] - nbatch + k + 1;
+    u32 s = i;
+    while (s > bs && (C.ev[s - 1].flags & AF_LINKED)) s--;
+    u32 e = i;
+    while (e + 1 < be && (C.ev[e].flags & AF_LINKED)) e++;
+    C.cs[i] = s;
+    C.ce[i] = e;
+    u32 fl = (s != e) ? FL_CHAINS : 0u;
+    u8 sres;
+    u32 pre = NONE32, gslot = NONE32;
+    // execute (:1018-1035) then create_account's static checks (:1201-1216)
+    if ((a.flags & AF_LINKED) && k == nbatch - 1) sres = TB_CREATE_ACCOUNT_LINKED_EVENT_CHAIN_OPEN;
+    else if (a.timestamp != 0) sres = TB_CREATE_ACCOUNT_TIMESTAMP_MUST_BE_ZERO;
+    else if (a.reserved != 0) sres = TB_CREATE_ACCOUNT_RESERVED_FIELD;
+    else if (a.flags & 0xFFF0u) sres = TB_CREATE_ACCOUNT_RESERVED_FLAG;
+    else if (a.id == 0) sres = TB_CREATE_ACCOUNT_ID_MUST_NOT_BE_ZERO;
+    else if (a.id == U128_MAX) sres = TB_CREATE_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
+    else if ((a.flags & AF_DNEC) && (a.flags & AF_CNED)) sres = TB_CREATE_ACCOUNT_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+    else if (a.debits_pending != 0) sres = TB_CREATE_ACCOUNT_DEBITS_PENDING_MUST_BE_ZERO;
+    else if (a.debits_posted != 0) sres = TB_CREATE_ACCOUNT_DEBITS_POSTED_MUST_BE_ZERO;
+    else if (a.credits_pending != 0) sres = TB_CREATE_ACCOUNT_CREDITS_PENDING_MUST_BE_ZERO;
+    else if (a.credits_posted != 0) sres = TB_CREATE_ACCOUNT_CREDITS_POSTED_MUST_BE_ZERO;
+    else if (a.ledger == 0) sres = TB_CREATE_ACCOUNT_LEDGER_MUST_NOT_BE_ZERO;
+    else if (a.code == 0) sres = TB_CREATE_ACCOUNT_CODE_MUST_NOT_BE_ZERO;
+    else {
+        sres = SRES_DYN;
+        pre = acc_probe(T.acc, T.acc_mask, a.id);
+        gslot = ac_gtab_insert(C, a.id, i);
+        atomicAdd(&C.gcnt_id[gslot], 1u);
+    }
+    C.sres[i] = sres;
+    C.pre[i] = pre;
+    C.gslot[i] = gslot;
+    C.prev_id[i] = NONE32;
+    if (fl) atomicOr(&C.counters[CNT_FLAGS], fl);
+}
+
+__global__ void ac_group1(AcArgs C) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= C.n) return;
+    const u32 g = C.gslot[i];
+    if (g != NONE32 && C.gcnt_id[g] > 1) atomicOr(&C.counters[CNT_FLAGS], (u32)FL_MULTI_ID);
+}
+
+__global__ void ac_group_keys(AcArgs C, u32 invalid, u32* keys, u32* vals) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= C.n) return;
+    const u32 g = C.gslot[i];
+    keys[i] = g == NONE32 ? invalid : g;
+    vals[i] = i;
+}
+
+__global__ void ac_group_prev(AcArgs C, u32 invalid, const u32* ks, const u32* vs) {
+    const u32 q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= C.n) return;
+    const u32 key = ks[q];
+    if (key >= invalid) return;
+    C.prev_id[vs[q]] = (q == 0 || ks[q - 1] != key) ? NONE32 : vs[q - 1];
+}
+
+__global__ void ac_init(AcArgs C, u8* res, u8* ok, u32* cfail) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= C.n) return;
+    const u8 sr = C.sres[i];
+    u8 r = sr;
+    if (sr == SRES_DYN) r = C.pre[i] != NONE32 ? TB_CREATE_ACCOUNT_EXISTS : TB_CREATE_ACCOUNT_OK;
+    res[i] = r;
+    ok[i] = r == 0 ? 1 : 0;
+    if (r != 0 && C.cs[i] != C.ce[i]) atomicMin(&cfail[C.cs[i]], i);
+}
+
+__global__ void ac_finalize(AcArgs C, u8* ok, const u32* cfail) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= C.n) return;
+    const u8 o = ok[i] & 1;
+    const u32 cs = C.cs[i];
+    const bool persisted = cs == C.ce[i] || cfail[cs] == NONE32;
+    ok[i] = o | ((o && persisted) ? 2 : 0);
+}
+
+// create_account_exists (src/state_machine.zig:1227-1237)
+__device__ __forceinline__ u8 account_exists(const Account& a, const Account& e) {
+    if (a.flags != e.flags) return TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_FLAGS;
+    if (a.user_data_128 != e.user_data_128) return TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_USER_DATA_128;
+    if (a.user_data_64 != e.user_data_64) return TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_USER_DATA_64;
+    if (a.user_data_32 != e.user_data_32) return TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_USER_DATA_32;
+    if (a.ledger != e.ledger) return TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_LEDGER;
+    if (a.code != e.code) return TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_CODE;
+    return TB_CREATE_ACCOUNT_EXISTS;
+}
+
+__global__ void ac_evaluate(Tables T, AcArgs C, const u8* res_s, const u8* ok_s, u8* res_d, u8* ok_d, u32* cfail_d) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= C.n) return;
+    const u8 sr = C.sres[i];
+    u8 r = sr;
+    const u32 csi = C.cs[i];
+    if (sr == SRES_DYN) {
+        const Account a = C.ev[i];
+        u32 e = NONE32;
+        for (u32 j = C.prev_id[i]; j != NONE32; j = C.prev_id[j]) {
+            const u8 o = ok_s[j];
+            if (C.cs[j] == csi ? (o & 1) : (o & 2)) { e = j; break; }
+        }
+        if (e != NONE32) r = account_exists(a, C.ev[e]);
+        else if (C.pre[i] != NONE32) r = account_exists(a, T.acc[C.pre[i]]);
+        else r = TB_CREATE_ACCOUNT_OK;
+    }
+    res_d[i] = r;
+    ok_d[i] = r == 0 ? 1 : 0;
+    if (r != 0 && csi != C.ce[i]) atomicMin(&cfail_d[csi], i);
+    if (r != res_s[i]) atomicAdd(&C.counters[CNT_CHANGES], 1u);
+}
+
+__global__ void ac_mask(AcArgs C, const u8* res, const u8* ok, const u32* cfail, u8* fres, u8* mask) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= C.n) return;
+    const u32 cs = C.cs[i];
+    const u32 cf = cs != C.ce[i] ? cfail[cs] : NONE32;
+    u8 r;
+    if (C.sres[i] == TB_CREATE_ACCOUNT_LINKED_EVENT_CHAIN_OPEN) r = TB_CREATE_ACCOUNT_LINKED_EVENT_CHAIN_OPEN;
+    else if (cf < i) r = TB_CREATE_ACCOUNT_LINKED_EVENT_FAILED;
+    else if (res[i] != 0) r = res[i];
+    else if (cf != NONE32) r = TB_CREATE_ACCOUNT_LINKED_EVENT_FAILED;
+    else r = TB_CREATE_ACCOUNT_OK;
+    fres[i] = r;
+    mask[i] = ((ok[i] & 2) ? 1 : 0) | (r != 0 ? 2 : 0);
+}
+
+__global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const uint4* rk,
+                         tb_create_accounts_result_t* results) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= C.n) return;
+    const u8 r = fres[i];
+    if (r != 0) {
+        const u32 b = ac_batch_of(C.b_start, C.nb, i);
+        const u32 bs = C.b_start[b];
+        results[bs + (rk[i].y - rk[bs].y)] = {i - bs, (u32)r};
+        return;
+    }
+    if (!(ok[i] & 2)) return;
+    Account a = C.ev[i];
+    a.timestamp = C.ts[i];
+    // accounts.insert: claim an empty slot by its timestamp word, then publish.
+    u64 h = hash128(a.id) & T.acc_mask;
+    for (;;) {
+        unsigned long long prev =
+            atomicCAS((unsigned long long*)&T.acc[h].timestamp, 0ull, (unsigned long long)a.timestamp);
+        if (prev == 0) break;
+        h = (h + 1) & T.acc_mask;
+    }
+    Account& dst = T.acc[h];
+    dst.id = a.id;
+    dst.debits_pending = a.debits_pending;
+    dst.debits_posted = a.debits_posted;
+    dst.credits_pending = a.credits_pending;
+    dst.credits_posted = a.credits_posted;
+    dst.user_data_128 = a.user_data_128;
+    dst.user_data_64 = a.user_data_64;
+    dst.user_data_32 = a.user_data_32;
+    dst.reserved = a.reserved;
+    dst.ledger = a.ledger;
+    dst.code = a.code;
+    dst.flags = a.flags;
+    atomicMax((unsigned long long*)T.commit_ts, (unsigned long long)a.timestamp);
+}
+
+__global__ void ac_batch_counts(const u32* b_start, u32 nb, const uint4* rk, u32* counts) {
+    const u32 b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < nb) counts[b] = rk[b_start[b + 1]].y - rk[b_start[b]].y;
+}
+
+// ------------------------------------------------------------- lookups ----
+__global__ void k_lookup_accounts(Tables T, const u128* ids, u32 n, Account* out, u8* found) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u32 s = acc_probe(T.acc, T.acc_mask, ids[i]);
+    found[i] = s != NONE32;
+    if (s != NONE32) out[i] = T.acc[s];
+}
+__global__ void k_lookup_transfers(Tables T, const u128* ids, u32 n, Transfer* out, u8* found) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u32 r = xidx_probe(T.xidx, T.xidx_mask, ids[i]);
+    found[i] = r != NONE32;
+    if (r != NONE32) out[i] = T.xrows[r];
+}
+__global__ void k_set_balances(Tables T, u128 id, Bal4 b, int* status) {
+    const u32 s = acc_probe(T.acc, T.acc_mask, id);
+    if (s == NONE32) { *status = -1; return; }
+    Account& a = T.acc[s];
+    a.debits_pending = b.dp;
+    a.debits_posted = b.dpo;
+    a.credits_pending = b.cp;
+    a.credits_posted = b.cpo;
+    *status = 0;
+}
+__global__ void k_get_posted(Tables T, u128 id, int* status) {
+    const u32 r = xidx_probe(T.xidx, T.xidx_mask, id);
+    if (r == NONE32) { *status = -1; return; }
+    const u8 f = T.xful[r];
+    *status = f == 0 ? -1 : (f == 1 ? 0 : 1);
+}
+
+}  // namespace
+
+#define GRID(n) (u32)(((n) + 255) / 256), 256, 0, stream
+
+void ac_launch_classify(const Tables& T, const AcArgs& C, hipStream_t stream) {
+    ac_classify<<<GRID(C.n)>>>(T, C);
+    ac_group1<<<GRID(C.n)>>>(C);
+}
+void ac_launch_group_sort(const AcArgs& C, u32 invalid, int bits, u32* k_in, u32* v_in, u32* k_out, u32* v_out,
+                          SortScratch& ss, hipStream_t stream) {
+    ac_group_keys<<<GRID(C.n)>>>(C, invalid, k_in, v_in);
+    radix_sort_pairs(k_in, v_in, k_out, v_out, C.n, bits, ss, stream);
+    ac_group_prev<<<GRID(C.n)>>>(C, invalid, k_out, v_out);
+}
+void ac_launch_init(const AcArgs& C, u8* res, u8* ok, u32* cfail, hipStream_t stream) {
+    ac_init<<<GRID(C.n)>>>(C, res, ok, cfail);
+    ac_finalize<<<GRID(C.n)>>>(C, ok, cfail);
+}
+void ac_launch_evaluate(const Tables& T, const AcArgs& C, const u8* res_s, const u8* ok_s, u8* res_d, u8* ok_d,
+                        u32* cfail_d, hipStream_t stream) {
+    ac_evaluate<<<GRID(C.n)>>>(T, C, res_s, ok_s, res_d, ok_d, cfail_d);
+    ac_finalize<<<GRID(C.n)>>>(C, ok_d, cfail_d);
+}
+void ac_launch_mask(const AcArgs& C, const u8* res, const u8* ok, const u32* cfail, u8* fres, u8* mask,
+                    hipStream_t stream) {
+    ac_mask<<<GRID(C.n)>>>(C, res, ok, cfail, fres, mask);
+}
+void ac_launch_apply(const Tables& T, const AcArgs& C, const u8* ok, const u8* fres, const uint4* rk,
+                     tb_create_accounts_result_t* results, u32* counts, hipStream_t stream) {
+    ac_apply<<<GRID(C.n)>>>(T, C, ok, fres, rk, results);
+    ac_batch_counts<<<GRID(C.nb)>>>(C.b_start, C.nb, rk, counts);
+}
+void launch_lookup_accounts(const Tables& T, const u128* ids, u32 n, Account* out, u8* found, hipStream_t stream) {
+    if (n) k_lookup_accounts<<<GRID(n)>>>(T, ids, n, out, found);
+}
+void launch_lookup_transfers(const Tables& T, const u128* ids, u32 n, Transfer* out, u8* found, hipStream_t stream) {
+    if (n) k_lookup_transfers<<<GRID(n)>>>(T, ids, n, out, found);
+}
+void launch_set_balances(const Tables& T, u128 id, Bal4 b, int* status, hipStream_t stream) {
+    k_set_balances<<<1, 1, 0, stream>>>(T, id, b, status);
+}
+void launch_get_posted(const Tables& T, u128 id, int* status, hipStream_t stream) {
+    k_get_posted<<<1, 1, 0, stream>>>(T, id, status);
+}

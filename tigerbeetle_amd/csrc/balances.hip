@@ -1,0 +1,231 @@
+// balances.hip — segmented u128 balance scan over account-sorted event sides.
+//
+// Every transfer has a debit side and a credit side.  After sorting the sides by
+// (account slot, batch index), the running balances an event sees are a prefix
+// sum over its account's earlier sides (src/state_machine.zig:1286-1340 read
+// dr/cr balances, :1330-1340 update them).  Visibility follows `execute`'s
+// linked-chain scopes (:1018-1083): a side counts with its FINAL status (chain
+// persisted) for readers outside its chain, and with its EVALUATED status for
+// later members of the same chain (their scope still holds its effects).  So
+//
+//   before(q) = init(account) + F_excl(q) + H_excl(q)
+//
+// F sums final-ok deltas, segmented by account; H sums (eval-ok but not final)
+// deltas, segmented by (account, chain).  Both are one scan with a two-level
+// segmented operator; H is compiled out when the call has no chains.
+//
+// Traffic per side: 8 B key/value + ~33 B delta gather + 64 B init gather
+// (L2-local: consecutive sides share the account row) + 64 B output.
+#include "common.h"
+#include "engine.h"
+
+namespace {
+
+constexpr int BS_THREADS = 256;
+constexpr int BS_IPT = 4;
+constexpr int BS_TILE = BS_THREADS * BS_IPT;
+
+struct SE {
+    Bal4 F, H;
+    u32 fl;  // bit0: account segment starts here, bit1: chain group starts here
+};
+
+__device__ __forceinline__ void zero(Bal4& b) { b.dp = b.dpo = b.cp = b.cpo = 0; }
+__device__ __forceinline__ Bal4 add(const Bal4& a, const Bal4& b) {
+    Bal4 r;
+    r.dp = a.dp + b.dp;
+    r.dpo = a.dpo + b.dpo;
+    r.cp = a.cp + b.cp;
+    r.cpo = a.cpo + b.cpo;
+    return r;
+}
+
+template <bool HAS_H>
+__device__ __forceinline__ SE combine(const SE& a, const SE& b) {
+    SE c;
+    c.F = (b.fl & 1) ? b.F : add(a.F, b.F);
+    if (HAS_H) c.H = (b.fl & 2) ? b.H : add(a.H, b.H);
+    c.fl = a.fl | b.fl;
+    return c;
+}
+
+template <bool HAS_H>
+__device__ __forceinline__ SE identity() {
+    SE e;
+    zero(e.F);
+    if (HAS_H) zero(e.H);
+    e.fl = 0;
+    return e;
+}
+
+// Load sorted position q as a scan element.  Invalid (inert) sides sort last and
+// contribute nothing; they are marked as segment starts so they never leak.
+template <bool HAS_H>
+__device__ __forceinline__ SE load_elem(const SideScanArgs& A, u64 q, u32 invalid) {
+    SE e;
+    const u32 key = A.skey[q];
+    if (key >= invalid) {
+        e = identity<HAS_H>();
+        e.fl = 3;
+        return e;
+    }
+    const u32 sv = A.sval[q];
+    const u32 i = sv >> 1;
+    bool f_start = true, h_start = true;
+    if (q > 0) {
+        const u32 pkey = A.skey[q - 1];
+        f_start = pkey != key;
+        h_start = f_start || A.cs[A.sval[q - 1] >> 1] != A.cs[i];
+    }
+    e.fl = (f_start ? 1u : 0u) | (h_start ? 2u : 0u);
+    const u8 ok = A.ok[i];
+    u128 dpe = A.dpend[i], dpo = A.dpost[i];
+    zero(e.F);
+    if (HAS_H) zero(e.H);
+    if (ok & 2) {
+        if (sv & 1) { e.F.cp = dpe; e.F.cpo = dpo; } else { e.F.dp = dpe; e.F.dpo = dpo; }
+    } else if (HAS_H && (ok & 1)) {
+        if (sv & 1) { e.H.cp = dpe; e.H.cpo = dpo; } else { e.H.dp = dpe; e.H.dpo = dpo; }
+    }
+    return e;
+}
+
+// Exclusive segmented scan of one value per thread across the workgroup.
+template <bool HAS_H>
+__device__ SE block_excl(SE v, SE* sh, SE* total) {
+    const u32 tid = threadIdx.x;
+    sh[tid] = v;
+    __syncthreads();
+    for (u32 off = 1; off < BS_THREADS; off <<= 1) {
+        SE o;
+        const bool take = tid >= off;
+        if (take) o = sh[tid - off];
+        __syncthreads();
+        if (take) sh[tid] = combine<HAS_H>(o, sh[tid]);
+        __syncthreads();
+    }
+    SE excl = tid ? sh[tid - 1] : identity<HAS_H>();
+    *total = sh[BS_THREADS - 1];
+    __syncthreads();
+    return excl;
+}
+
+template <bool HAS_H>
+__global__ __launch_bounds__(BS_THREADS) void bs_reduce(SideScanArgs A, u64 m, u32 invalid, SE* __restrict__ tagg) {
+    __shared__ SE sh[BS_THREADS];
+    const u64 base = (u64)blockIdx.x * BS_TILE + (u64)threadIdx.x * BS_IPT;
+    SE acc = identity<HAS_H>();
+    for (int k = 0; k < BS_IPT; k++)
+        if (base + k < m) acc = combine<HAS_H>(acc, load_elem<HAS_H>(A, base + k, invalid));
+    SE total;
+    block_excl<HAS_H>(acc, sh, &total);
+    if (threadIdx.x == 0) tagg[blockIdx.x] = total;
+}
+
+template <bool HAS_H>
+__global__ __launch_bounds__(BS_THREADS) void bs_tiles(SE* __restrict__ tagg, u64 ntiles) {
+    __shared__ SE sh[BS_THREADS];
+    const u32 tid = threadIdx.x;
+    const u64 chunk = (ntiles + BS_THREADS - 1) / BS_THREADS;
+    const u64 lo = (u64)tid * chunk;
+    const u64 hi = lo + chunk < ntiles ? lo + chunk : ntiles;
+    SE acc = identity<HAS_H>();
+    for (u64 t = lo; t < hi; t++) acc = combine<HAS_H>(acc, tagg[t]);
+    SE total;
+    SE run = block_excl<HAS_H>(acc, sh, &total);
+    for (u64 t = lo; t < hi; t++) {
+        SE v = tagg[t];
+        tagg[t] = run;
+        run = combine<HAS_H>(run, v);
+    }
+}
+
+template <bool HAS_H>
+__global__ __launch_bounds__(BS_THREADS) void bs_down(SideScanArgs A, u64 m, u32 invalid, const SE* __restrict__ tagg,
+                                                      const Account* __restrict__ acc, Bal4* __restrict__ bb) {
+    __shared__ SE sh[BS_THREADS];
+    const u64 base = (u64)blockIdx.x * BS_TILE + (u64)threadIdx.x * BS_IPT;
+    SE acc_t = identity<HAS_H>();
+    for (int k = 0; k < BS_IPT; k++)
+        if (base + k < m) acc_t = combine<HAS_H>(acc_t, load_elem<HAS_H>(A, base + k, invalid));
+    SE total;
+    SE run = combine<HAS_H>(tagg[blockIdx.x], block_excl<HAS_H>(acc_t, sh, &total));
+    for (int k = 0; k < BS_IPT; k++) {
+        const u64 q = base + k;
+        if (q >= m) break;
+        SE e = load_elem<HAS_H>(A, q, invalid);
+        const u32 key = A.skey[q];
+        if (key < invalid) {
+            const Account& a = acc[key];
+            Bal4 out;
+            out.dp = a.debits_pending;
+            out.dpo = a.debits_posted;
+            out.cp = a.credits_pending;
+            out.cpo = a.credits_posted;
+            if (!(e.fl & 1)) out = add(out, run.F);
+            if (HAS_H && !(e.fl & 2)) out = add(out, run.H);
+            bb[q] = out;
+        }
+        run = combine<HAS_H>(run, e);
+    }
+}
+
+// After convergence: the last side of each account segment writes the account's
+// final balances: before(q) minus the in-chain H part, plus its own final delta.
+__global__ void bs_final(SideScanArgs A, u64 m, u32 invalid, const Bal4* __restrict__ bb, Account* __restrict__ acc) {
+    const u64 q = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= m) return;
+    const u32 key = A.skey[q];
+    if (key >= invalid) return;
+    if (q + 1 < m && A.skey[q + 1] == key) return;
+    Bal4 tot = bb[q];
+    const u32 i = A.sval[q] >> 1;
+    // remove the H contribution (same account, same chain, eval-ok & !final-ok)
+    for (u64 p = q; p > 0;) {
+        --p;
+        if (A.skey[p] != key) break;
+        const u32 j = A.sval[p] >> 1;
+        if (A.cs[j] != A.cs[i]) break;
+        const u8 ok = A.ok[j];
+        if ((ok & 1) && !(ok & 2)) {
+            if (A.sval[p] & 1) { tot.cp -= A.dpend[j]; tot.cpo -= A.dpost[j]; }
+            else { tot.dp -= A.dpend[j]; tot.dpo -= A.dpost[j]; }
+        }
+    }
+    if (A.ok[i] & 2) {
+        if (A.sval[q] & 1) { tot.cp += A.dpend[i]; tot.cpo += A.dpost[i]; }
+        else { tot.dp += A.dpend[i]; tot.dpo += A.dpost[i]; }
+    }
+    Account& a = acc[key];
+    a.debits_pending = tot.dp;
+    a.debits_posted = tot.dpo;
+    a.credits_pending = tot.cp;
+    a.credits_posted = tot.cpo;
+}
+
+}  // namespace
+
+u64 side_scan_tile_bytes(u64 capacity) { return ((capacity + BS_TILE - 1) / BS_TILE + 1) * sizeof(SE); }
+
+void side_scan(const SideScanArgs& A, u64 m, u32 invalid, bool has_chains, void* tile_scratch, const Account* acc,
+               Bal4* bb, hipStream_t stream) {
+    if (m == 0) return;
+    const u64 ntiles = (m + BS_TILE - 1) / BS_TILE;
+    SE* tagg = (SE*)tile_scratch;
+    if (has_chains) {
+        bs_reduce<true><<<(u32)ntiles, BS_THREADS, 0, stream>>>(A, m, invalid, tagg);
+        bs_tiles<true><<<1, BS_THREADS, 0, stream>>>(tagg, ntiles);
+        bs_down<true><<<(u32)ntiles, BS_THREADS, 0, stream>>>(A, m, invalid, tagg, acc, bb);
+    } else {
+        bs_reduce<false><<<(u32)ntiles, BS_THREADS, 0, stream>>>(A, m, invalid, tagg);
+        bs_tiles<false><<<1, BS_THREADS, 0, stream>>>(tagg, ntiles);
+        bs_down<false><<<(u32)ntiles, BS_THREADS, 0, stream>>>(A, m, invalid, tagg, acc, bb);
+    }
+    HIP_CHECK(hipGetLastError());
+}
+
+void side_final_balances(const SideScanArgs& A, u64 m, u32 invalid, const Bal4* bb, Account* acc, hipStream_t stream) {
+    if (m == 0) return;
+    bs_final<<<(u32)((m + 255) / 256), 256, 0, stream>>>(A, m, invalid, bb, acc);
+    HIP_CHECK(hipGetLastError());
+}

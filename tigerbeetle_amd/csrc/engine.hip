@@ -1,0 +1,617 @@
+// engine.hip — host runtime of the commit engine and the C-ABI (include/tbgpu.h).
+//
+// A ctx owns the HBM state that replaces the StateMachine's forest for the hot
+// path (accounts, transfers + id index, posted groove, account history) and the
+// per-call scratch.  Each create_* call (one batch, or several consecutive
+// batches streamed together) runs:
+//
+//   classify (static checks + probes) -> group same-id / same-pending events ->
+//   fixed point { sides -> sort -> balance scan -> evaluate } -> apply
+//
+// See transfers.hip for why the fixed point reproduces execute() exactly.
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+#include "engine.h"
+#include "transfers.h"
+
+[[noreturn]] void tbgpu_fatal(const char* what, const char* why, const char* file, int line) {
+    fprintf(stderr, "tbgpu: fatal: %s: %s (%s:%d)\n", what, why, file, line);
+    fflush(stderr);
+    abort();
+}
+
+namespace {
+
+u64 pow2_at_least(u64 x) {
+    u64 p = 16;
+    while (p < x) p <<= 1;
+    return p;
+}
+int log2u(u64 x) {
+    int b = 0;
+    while ((1ull << b) < x) b++;
+    return b;
+}
+
+template <typename T>
+T* dalloc(u64 count, u64* total) {
+    void* p = nullptr;
+    const u64 bytes = std::max<u64>(count * sizeof(T), 16);
+    HIP_CHECK(hipMalloc(&p, bytes));
+    *total += bytes;
+    return (T*)p;
+}
+
+}  // namespace
+
+struct tbgpu_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    tbgpu_options opt{};
+    Tables T{};
+    u64 acc_cap = 0, xrow_cap = 0, xidx_cap = 0, hist_cap = 0;
+    u64 accounts_max = 0;
+    u64 n_accounts = 0, n_rows = 0, n_hist = 0;
+    u64 bytes = 0;
+
+    // per-call scratch (nmax events, bmax batches)
+    u64 nmax = 0, bmax = 0, gcap = 0;
+    u8* ev_buf = nullptr;  // nmax * 128
+    u32* b_start = nullptr;
+    u64* b_ts = nullptr;
+    u64* ts = nullptr;
+    u32 *cs = nullptr, *ce = nullptr;
+    u8* sres = nullptr;
+    u32 *dslot, *cslot, *pre_e, *pre_p, *pp_dslot, *pp_cslot, *gslot, *pslot, *prev_id, *pend_last, *prev_pend;
+    u32 *gclaim, *gcnt_id, *gcnt_pd, *gmem, *gbeg, *gend;
+    EvalState st[2];
+    u32 *skey, *sval, *skey_s, *sval_s, *spos;
+    Bal4* bb = nullptr;
+    SortScratch ss{};
+    void* side_tiles = nullptr;
+    Scan3Scratch sc{};
+    u8 *fres, *mask;
+    uint4* ranks = nullptr;
+    u8* res_buf = nullptr;  // nmax * 8 results
+    u32* counts = nullptr;
+    u32* counters = nullptr;
+    int* status = nullptr;
+    u32* h_counters = nullptr;  // pinned
+    hipEvent_t ev0, ev1;
+    tbgpu_stats stats{};
+    char err[256] = {0};
+};
+
+static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
+    u64& B = c->bytes;
+    c->nmax = nmax;
+    c->bmax = nmax + 2;
+    c->gcap = pow2_at_least(4 * nmax);
+    const u64 n = nmax, m = 2 * nmax;
+    c->ev_buf = dalloc<u8>(n * 128, &B);
+    c->b_start = dalloc<u32>(c->bmax + 1, &B);
+    c->b_ts = dalloc<u64>(c->bmax, &B);
+    c->ts = dalloc<u64>(n, &B);
+    c->cs = dalloc<u32>(n, &B);
+    c->ce = dalloc<u32>(n, &B);
+    c->sres = dalloc<u8>(n, &B);
+    u32** u32s[] = {&c->dslot, &c->cslot, &c->pre_e, &c->pre_p, &c->pp_dslot, &c->pp_cslot,
+                    &c->gslot, &c->pslot, &c->prev_id, &c->pend_last, &c->prev_pend};
+    for (u32** p : u32s) *p = dalloc<u32>(n, &B);
+    u32** g32s[] = {&c->gclaim, &c->gcnt_id, &c->gcnt_pd, &c->gmem, &c->gbeg, &c->gend};
+    for (u32** p : g32s) *p = dalloc<u32>(c->gcap, &B);
+    for (EvalState& s : c->st) {
+        s.res = dalloc<u8>(n, &B);
+        s.ok = dalloc<u8>(n, &B);
+        s.pref = dalloc<u32>(n, &B);
+        s.cfail = dalloc<u32>(n, &B);
+        s.amt = dalloc<u128>(n, &B);
+        s.pamt = dalloc<u128>(n, &B);
+        s.dpend = dalloc<u128>(n, &B);
+        s.dpost = dalloc<u128>(n, &B);
+    }
+    c->skey = dalloc<u32>(m, &B);
+    c->sval = dalloc<u32>(m, &B);
+    c->skey_s = dalloc<u32>(m, &B);
+    c->sval_s = dalloc<u32>(m, &B);
+    c->spos = dalloc<u32>(m, &B);
+    c->bb = dalloc<Bal4>(m, &B);
+    c->ss.keys_tmp = dalloc<u32>(m, &B);
+    c->ss.vals_tmp = dalloc<u32>(m, &B);
+    c->ss.hist = dalloc<u32>(radix_sort_hist_words(m), &B);
+    c->ss.capacity = m;
+    c->side_tiles = dalloc<u8>(side_scan_tile_bytes(m), &B);
+    c->sc.tile_sums = dalloc<uint4>(scan3_tile_words(n), &B);
+    c->sc.capacity = n;
+    c->fres = dalloc<u8>(n, &B);
+    c->mask = dalloc<u8>(n, &B);
+    c->ranks = dalloc<uint4>(n + 1, &B);
+    c->res_buf = dalloc<u8>(n * 8, &B);
+    c->counts = dalloc<u32>(c->bmax, &B);
+    c->counters = dalloc<u32>(CNT_COUNT, &B);
+    c->status = dalloc<int>(4, &B);
+    HIP_CHECK(hipHostMalloc((void**)&c->h_counters, CNT_COUNT * sizeof(u32), hipHostMallocDefault));
+}
+
+static void set_err(tbgpu_ctx* c, const char* msg) {
+    snprintf(c->err, sizeof c->err, "%s", msg);
+}
+
+extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
+    *out = nullptr;
+    tbgpu_options o{};
+    if (options) o = *options;
+    if (!o.accounts_max) o.accounts_max = 1u << 20;
+    if (!o.transfers_max) o.transfers_max = 1u << 24;
+    if (!o.history_max) o.history_max = 1u << 16;
+    if (!o.events_per_call_max) o.events_per_call_max = 1u << 20;
+    if (o.events_per_call_max < TBGPU_BATCH_MAX) o.events_per_call_max = TBGPU_BATCH_MAX;
+    if (o.transfers_max >= 0x7FFFFFFFull || o.events_per_call_max >= (1ull << 29)) return -22;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return -19;  // ENODEV
+    if (o.device < 0 || o.device >= ndev) return -19;
+    tbgpu_ctx* c = new tbgpu_ctx();
+    c->opt = o;
+    c->device = o.device;
+    HIP_CHECK(hipSetDevice(c->device));
+    HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreate(&c->ev0));
+    HIP_CHECK(hipEventCreate(&c->ev1));
+    c->accounts_max = o.accounts_max;
+    c->acc_cap = pow2_at_least(2 * o.accounts_max);
+    c->xrow_cap = o.transfers_max;
+    c->xidx_cap = pow2_at_least(2 * o.transfers_max);
+    c->hist_cap = o.history_max;
+    u64& B = c->bytes;
+    c->T.acc = dalloc<Account>(c->acc_cap, &B);
+    c->T.acc_mask = c->acc_cap - 1;
+    c->T.xrows = dalloc<Transfer>(c->xrow_cap, &B);
+    c->T.xful = dalloc<u8>(c->xrow_cap, &B);
+    c->T.xidx = dalloc<IdSlot>(c->xidx_cap, &B);
+    c->T.xidx_mask = c->xidx_cap - 1;
+    c->T.hrows = dalloc<History>(c->hist_cap, &B);
+    c->T.commit_ts = dalloc<u64>(2, &B);
+    alloc_scratch(c, o.events_per_call_max);
+    tbgpu_reset(c);
+    *out = c;
+    return 0;
+}
+
+extern "C" void tbgpu_reset(tbgpu_ctx* c) {
+    HIP_CHECK(hipSetDevice(c->device));
+    HIP_CHECK(hipMemsetAsync(c->T.acc, 0, c->acc_cap * sizeof(Account), c->stream));
+    HIP_CHECK(hipMemsetAsync(c->T.xful, 0, c->xrow_cap, c->stream));
+    HIP_CHECK(hipMemsetAsync(c->T.xidx, 0, c->xidx_cap * sizeof(IdSlot), c->stream));
+    HIP_CHECK(hipMemsetAsync(c->T.commit_ts, 0, 2 * sizeof(u64), c->stream));
+    HIP_CHECK(hipStreamSynchronize(c->stream));
+    c->n_accounts = c->n_rows = c->n_hist = 0;
+}
+
+extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    // Free every device allocation by walking the struct's pointers.
+    void* ptrs[] = {c->T.acc, c->T.xrows, c->T.xful, c->T.xidx, c->T.hrows, c->T.commit_ts, c->ev_buf,
+                    c->b_start, c->b_ts, c->ts, c->cs, c->ce, c->sres, c->dslot, c->cslot, c->pre_e, c->pre_p,
+                    c->pp_dslot, c->pp_cslot, c->gslot, c->pslot, c->prev_id, c->pend_last, c->prev_pend,
+                    c->gclaim, c->gcnt_id, c->gcnt_pd, c->gmem, c->gbeg, c->gend, c->skey, c->sval, c->skey_s,
+                    c->sval_s, c->spos, c->bb, c->ss.keys_tmp, c->ss.vals_tmp, c->ss.hist, c->side_tiles,
+                    c->sc.tile_sums, c->fres, c->mask, c->ranks, c->res_buf, c->counts, c->counters, c->status};
+    for (void* p : ptrs) if (p) (void)hipFree(p);
+    for (EvalState& s : c->st) {
+        void* q[] = {s.res, s.ok, s.pref, s.cfail, s.amt, s.pamt, s.dpend, s.dpost};
+        for (void* p : q) if (p) (void)hipFree(p);
+    }
+    if (c->h_counters) (void)hipHostFree(c->h_counters);
+    (void)hipEventDestroy(c->ev0);
+    (void)hipEventDestroy(c->ev1);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+// ------------------------------------------------------------ helpers -----
+
+static void read_counters(tbgpu_ctx* c) {
+    HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, CNT_COUNT * sizeof(u32), hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(hipStreamSynchronize(c->stream));
+}
+
+// Splits batches [b0, b_end) into chunks of whole batches of <= nmax events.
+static u32 chunk_end(const tbgpu_ctx* c, const uint32_t* counts, u32 b0, u32 nb) {
+    u64 ev = 0;
+    u32 b = b0;
+    while (b < nb && b - b0 < c->bmax - 2) {
+        if (ev + counts[b] > c->nmax) break;
+        ev += counts[b];
+        b++;
+    }
+    if (b == b0) tbgpu_fatal("batches", "a single batch exceeds events_per_call_max", __FILE__, __LINE__);
+    return b;
+}
+
+static void upload_batches(tbgpu_ctx* c, const uint64_t* timestamps, const uint32_t* counts, u32 nb,
+                           std::vector<u32>& starts) {
+    starts.resize(nb + 1);
+    starts[0] = 0;
+    for (u32 b = 0; b < nb; b++) starts[b + 1] = starts[b] + counts[b];
+    HIP_CHECK(hipMemcpyAsync(c->b_start, starts.data(), (nb + 1) * sizeof(u32), hipMemcpyHostToDevice, c->stream));
+    HIP_CHECK(hipMemcpyAsync(c->b_ts, timestamps, nb * sizeof(u64), hipMemcpyHostToDevice, c->stream));
+}
+
+static TrArgs make_tr_args(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb) {
+    TrArgs C{};
+    C.ev = ev; C.n = n; C.nb = nb;
+    C.b_start = c->b_start; C.b_ts = c->b_ts;
+    C.ts = c->ts; C.cs = c->cs; C.ce = c->ce; C.sres = c->sres;
+    C.dslot = c->dslot; C.cslot = c->cslot; C.pre_e = c->pre_e; C.pre_p = c->pre_p;
+    C.pp_dslot = c->pp_dslot; C.pp_cslot = c->pp_cslot; C.gslot = c->gslot; C.pslot = c->pslot;
+    C.prev_id = c->prev_id; C.pend_last = c->pend_last; C.prev_pend = c->prev_pend;
+    C.gclaim = c->gclaim; C.gcnt_id = c->gcnt_id; C.gcnt_pd = c->gcnt_pd; C.gmem = c->gmem;
+    C.gbeg = c->gbeg; C.gend = c->gend; C.gmembers = c->sval_s;
+    // group table sized for this call: >= 2x the keys (ids + pending ids <= 2n)
+    const u64 g = std::min<u64>(c->gcap, pow2_at_least(4ull * std::max<u32>(n, 1)));
+    C.gmask = g - 1;
+    C.counters = c->counters;
+    return C;
+}
+
+// One chunk of create_transfers: events already at `ev` on the device.
+static void run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
+                                tb_create_transfers_result_t* results_dev, u32* counts_host) {
+    hipStream_t s = c->stream;
+    TrArgs C = make_tr_args(c, ev, n, nb);
+    const u64 g = C.gmask + 1;
+    const u32 inv_acc = (u32)c->acc_cap;
+    const int bits_acc = log2u(c->acc_cap + 1);
+    const u32 inv_g = (u32)g;
+    const int bits_g = log2u(g + 1);
+    c->stats.iterations = 0;
+    c->stats.sorts = 0;
+    c->stats.path = 0;
+    if (n == 0) {
+        std::fill(counts_host, counts_host + nb, 0u);
+        return;
+    }
+    HIP_CHECK(hipMemsetAsync(c->counters, 0, CNT_COUNT * sizeof(u32), s));
+    HIP_CHECK(hipMemsetAsync(c->gclaim, 0, g * sizeof(u32), s));
+    HIP_CHECK(hipMemsetAsync(c->gcnt_id, 0, g * sizeof(u32), s));
+    HIP_CHECK(hipMemsetAsync(c->gcnt_pd, 0, g * sizeof(u32), s));
+    tr_launch_classify(c->T, C, s);
+    read_counters(c);
+    const u32 flags = c->h_counters[CNT_FLAGS];
+    if (flags & FL_MULTI_ID) {
+        tr_launch_group_sort(C, 0, inv_g, bits_g, c->skey, c->sval, c->skey_s, c->sval_s, c->ss, s);
+        c->stats.sorts++;
+    }
+    if (flags & FL_POSTVOID) tr_launch_group2(C, s);
+    if (flags & FL_MULTI_PEND) {
+        tr_launch_group_sort(C, 1, inv_g, bits_g, c->skey, c->sval, c->skey_s, c->sval_s, c->ss, s);
+        c->stats.sorts++;
+    }
+    const bool chains = flags & FL_CHAINS;
+    const bool keys_dynamic = flags & FL_POSTVOID;
+
+    EvalState* A = &c->st[0];
+    EvalState* Bst = &c->st[1];
+    HIP_CHECK(hipMemsetAsync(A->cfail, 0xFF, n * sizeof(u32), s));
+    tr_launch_init(c->T, C, *A, s);
+
+    const u64 m = 2ull * n;
+    SideScanArgs SA{};
+    SA.skey = c->skey_s; SA.sval = c->sval_s; SA.cs = c->cs;
+    u32 it = 0;
+    for (;; it++) {
+        if (it > n + 2) tbgpu_fatal("create_transfers", "fixed point did not converge", __FILE__, __LINE__);
+        HIP_CHECK(hipMemsetAsync(c->counters + CNT_CHANGES, 0, 2 * sizeof(u32), s));
+        tr_launch_sides(C, *A, inv_acc, c->skey, c->sval, s);
+        bool sort = it == 0;
+        if (!sort && keys_dynamic) {
+            read_counters(c);
+            sort = c->h_counters[CNT_KEYS] != 0;
+        }
+        if (sort) {
+            radix_sort_pairs(c->skey, c->sval, c->skey_s, c->sval_s, m, bits_acc, c->ss, s);
+            tr_launch_side_pos(c->sval_s, m, c->spos, s);
+            c->stats.sorts++;
+        }
+        SA.ok = A->ok; SA.dpend = A->dpend; SA.dpost = A->dpost;
+        side_scan(SA, m, inv_acc, chains, c->side_tiles, c->T.acc, c->bb, s);
+        HIP_CHECK(hipMemsetAsync(Bst->cfail, 0xFF, n * sizeof(u32), s));
+        tr_launch_evaluate(c->T, C, *A, *Bst, c->spos, c->bb, s);
+        read_counters(c);
+        std::swap(A, Bst);
+        if (c->h_counters[CNT_CHANGES] == 0) break;
+    }
+    c->stats.iterations = it + 1;
+
+    // apply: ranks of stored rows / results / history rows
+    tr_launch_mask(c->T, C, *A, c->fres, c->mask, s);
+    scan3_exclusive(c->mask, c->ranks, n, c->sc, s);
+    uint4 tot;
+    HIP_CHECK(hipMemcpyAsync(&tot, c->ranks + n, sizeof(uint4), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (c->n_rows + tot.x > c->xrow_cap) tbgpu_fatal("create_transfers", "transfers_max exceeded", __FILE__, __LINE__);
+    if (c->n_hist + tot.z > c->hist_cap) tbgpu_fatal("create_transfers", "history_max exceeded", __FILE__, __LINE__);
+    SA.ok = A->ok; SA.dpend = A->dpend; SA.dpost = A->dpost;
+    tr_launch_apply(c->T, C, *A, c->fres, c->ranks, c->spos, c->bb, c->n_rows, c->n_hist, results_dev, c->counts, s);
+    side_final_balances(SA, m, inv_acc, c->bb, c->T.acc, s);
+    HIP_CHECK(hipMemcpyAsync(counts_host, c->counts, nb * sizeof(u32), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    c->n_rows += tot.x;
+    c->n_hist += tot.z;
+}
+
+static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t* timestamps, const uint32_t* counts,
+                                  const Transfer* ev_src, bool src_device, tb_create_transfers_result_t* results,
+                                  bool dst_device, uint32_t* result_counts) {
+    HIP_CHECK(hipSetDevice(c->device));
+    HIP_CHECK(hipEventRecord(c->ev0, c->stream));
+    std::vector<u32> starts;
+    u64 total = 0, ev_off = 0, events = 0;
+    u32 iters = 0;
+    u64 sorts = 0;
+    for (u32 b0 = 0; b0 < nb_total || (nb_total == 0 && false);) {
+        const u32 b1 = chunk_end(c, counts, b0, nb_total);
+        const u32 nb = b1 - b0;
+        upload_batches(c, timestamps + b0, counts + b0, nb, starts);
+        const u32 n = starts[nb];
+        const Transfer* ev;
+        if (src_device) {
+            ev = ev_src + ev_off;
+        } else {
+            HIP_CHECK(hipMemcpyAsync(c->ev_buf, ev_src + ev_off, (u64)n * 128, hipMemcpyHostToDevice, c->stream));
+            ev = (const Transfer*)c->ev_buf;
+        }
+        tb_create_transfers_result_t* rdev =
+            dst_device ? results + ev_off : (tb_create_transfers_result_t*)c->res_buf;
+        run_transfers_chunk(c, ev, n, nb, rdev, result_counts + b0);
+        if (!dst_device) {
+            // copy each batch's results (they sit at the batch's event offset)
+            u64 bytes = 0;
+            for (u32 b = 0; b < nb; b++) {
+                if (result_counts[b0 + b] == 0) continue;
+                bytes = (u64)starts[b] * 8;
+                HIP_CHECK(hipMemcpyAsync((u8*)(results + ev_off) + bytes, c->res_buf + bytes,
+                                         (u64)result_counts[b0 + b] * 8, hipMemcpyDeviceToHost, c->stream));
+            }
+            HIP_CHECK(hipStreamSynchronize(c->stream));
+        }
+        for (u32 b = 0; b < nb; b++) total += result_counts[b0 + b];
+        iters = std::max(iters, c->stats.iterations);
+        sorts += c->stats.sorts;
+        ev_off += n;
+        events += n;
+        b0 = b1;
+    }
+    HIP_CHECK(hipEventRecord(c->ev1, c->stream));
+    HIP_CHECK(hipEventSynchronize(c->ev1));
+    float ms = 0;
+    HIP_CHECK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    c->stats.events = events;
+    c->stats.iterations = iters;
+    c->stats.sorts = sorts;
+    c->stats.device_ms = ms;
+    return total;
+}
+
+extern "C" uint32_t tbgpu_create_transfers(tbgpu_ctx* c, uint64_t timestamp, const tb_transfer_t* events,
+                                           uint32_t count, tb_create_transfers_result_t* results) {
+    uint32_t rc = 0;
+    const uint64_t ts = timestamp;
+    return (uint32_t)transfers_batches(c, 1, &ts, &count, (const Transfer*)events, false, results, false, &rc);
+}
+
+extern "C" uint64_t tbgpu_create_transfers_batches(tbgpu_ctx* c, uint32_t batch_count, const uint64_t* timestamps,
+                                                   const uint32_t* counts, const tb_transfer_t* events,
+                                                   tb_create_transfers_result_t* results, uint32_t* result_counts) {
+    return transfers_batches(c, batch_count, timestamps, counts, (const Transfer*)events, false, results, false,
+                             result_counts);
+}
+
+extern "C" uint64_t tbgpu_create_transfers_batches_device(tbgpu_ctx* c, uint32_t batch_count,
+                                                          const uint64_t* timestamps, const uint32_t* counts,
+                                                          const void* events_device, void* results_device,
+                                                          uint32_t* result_counts) {
+    return transfers_batches(c, batch_count, timestamps, counts, (const Transfer*)events_device, true,
+                             (tb_create_transfers_result_t*)results_device, true, result_counts);
+}
+
+// ------------------------------------------------------- create_accounts --
+
+static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
+                               tb_create_accounts_result_t* results_dev, u32* counts_host) {
+    hipStream_t s = c->stream;
+    if (n == 0) {
+        std::fill(counts_host, counts_host + nb, 0u);
+        return;
+    }
+    AcArgs C{};
+    C.ev = ev; C.n = n; C.nb = nb; C.b_start = c->b_start; C.b_ts = c->b_ts;
+    C.ts = c->ts; C.cs = c->cs; C.ce = c->ce; C.sres = c->sres; C.pre = c->pre_e;
+    C.gslot = c->gslot; C.prev_id = c->prev_id; C.gclaim = c->gclaim; C.gcnt_id = c->gcnt_id;
+    const u64 g = std::min<u64>(c->gcap, pow2_at_least(4ull * n));
+    C.gmask = g - 1;
+    C.counters = c->counters;
+    HIP_CHECK(hipMemsetAsync(c->counters, 0, CNT_COUNT * sizeof(u32), s));
+    HIP_CHECK(hipMemsetAsync(c->gclaim, 0, g * sizeof(u32), s));
+    HIP_CHECK(hipMemsetAsync(c->gcnt_id, 0, g * sizeof(u32), s));
+    ac_launch_classify(c->T, C, s);
+    read_counters(c);
+    if (c->h_counters[CNT_FLAGS] & FL_MULTI_ID)
+        ac_launch_group_sort(C, (u32)g, log2u(g + 1), c->skey, c->sval, c->skey_s, c->sval_s, c->ss, s);
+    EvalState* A = &c->st[0];
+    EvalState* Bst = &c->st[1];
+    HIP_CHECK(hipMemsetAsync(A->cfail, 0xFF, n * sizeof(u32), s));
+    ac_launch_init(C, A->res, A->ok, A->cfail, s);
+    u32 it = 0;
+    for (;; it++) {
+        if (it > n + 2) tbgpu_fatal("create_accounts", "fixed point did not converge", __FILE__, __LINE__);
+        HIP_CHECK(hipMemsetAsync(c->counters + CNT_CHANGES, 0, sizeof(u32), s));
+        HIP_CHECK(hipMemsetAsync(Bst->cfail, 0xFF, n * sizeof(u32), s));
+        ac_launch_evaluate(c->T, C, A->res, A->ok, Bst->res, Bst->ok, Bst->cfail, s);
+        read_counters(c);
+        std::swap(A, Bst);
+        if (c->h_counters[CNT_CHANGES] == 0) break;
+    }
+    c->stats.iterations = it + 1;
+    ac_launch_mask(C, A->res, A->ok, A->cfail, c->fres, c->mask, s);
+    scan3_exclusive(c->mask, c->ranks, n, c->sc, s);
+    uint4 tot;
+    HIP_CHECK(hipMemcpyAsync(&tot, c->ranks + n, sizeof(uint4), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (c->n_accounts + tot.x > c->accounts_max) tbgpu_fatal("create_accounts", "accounts_max exceeded", __FILE__, __LINE__);
+    ac_launch_apply(c->T, C, A->ok, c->fres, c->ranks, results_dev, c->counts, s);
+    HIP_CHECK(hipMemcpyAsync(counts_host, c->counts, nb * sizeof(u32), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    c->n_accounts += tot.x;
+}
+
+extern "C" uint64_t tbgpu_create_accounts_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t* timestamps,
+                                                  const uint32_t* counts, const tb_account_t* events,
+                                                  tb_create_accounts_result_t* results, uint32_t* result_counts) {
+    HIP_CHECK(hipSetDevice(c->device));
+    std::vector<u32> starts;
+    u64 total = 0, ev_off = 0;
+    for (u32 b0 = 0; b0 < nb_total;) {
+        const u32 b1 = chunk_end(c, counts, b0, nb_total);
+        const u32 nb = b1 - b0;
+        upload_batches(c, timestamps + b0, counts + b0, nb, starts);
+        const u32 n = starts[nb];
+        HIP_CHECK(hipMemcpyAsync(c->ev_buf, events + ev_off, (u64)n * 128, hipMemcpyHostToDevice, c->stream));
+        run_accounts_chunk(c, (const Account*)c->ev_buf, n, nb, (tb_create_accounts_result_t*)c->res_buf,
+                           result_counts + b0);
+        for (u32 b = 0; b < nb; b++) {
+            if (result_counts[b0 + b] == 0) continue;
+            const u64 off = (u64)starts[b] * 8;
+            HIP_CHECK(hipMemcpyAsync((u8*)(results + ev_off) + off, c->res_buf + off, (u64)result_counts[b0 + b] * 8,
+                                     hipMemcpyDeviceToHost, c->stream));
+            total += result_counts[b0 + b];
+        }
+        HIP_CHECK(hipStreamSynchronize(c->stream));
+        ev_off += n;
+        b0 = b1;
+    }
+    return total;
+}
+
+extern "C" uint32_t tbgpu_create_accounts(tbgpu_ctx* c, uint64_t timestamp, const tb_account_t* events,
+                                          uint32_t count, tb_create_accounts_result_t* results) {
+    uint32_t rc = 0;
+    return (uint32_t)tbgpu_create_accounts_batches(c, 1, &timestamp, &count, events, results, &rc);
+}
+
+// ------------------------------------------------------------- lookups ----
+
+template <typename Row, typename Launch>
+static uint32_t lookup(tbgpu_ctx* c, const tb_uint128_t* ids, uint32_t count, Row* out, Launch launch) {
+    HIP_CHECK(hipSetDevice(c->device));
+    uint32_t found_total = 0;
+    std::vector<Row> rows;
+    std::vector<u8> found;
+    const u32 step = (u32)std::min<u64>(c->nmax, 1u << 20);
+    for (u32 off = 0; off < count; off += step) {
+        const u32 k = std::min(step, count - off);
+        u128* d_ids = (u128*)c->ev_buf;  // k * 16 <= nmax * 128
+        Row* d_out = (Row*)c->bb;        // 2 * nmax * 64 bytes >= k * 128
+        u8* d_found = c->fres;
+        HIP_CHECK(hipMemcpyAsync(d_ids, ids + off, (u64)k * 16, hipMemcpyHostToDevice, c->stream));
+        launch(d_ids, k, d_out, d_found);
+        rows.resize(k);
+        found.resize(k);
+        HIP_CHECK(hipMemcpyAsync(rows.data(), d_out, (u64)k * sizeof(Row), hipMemcpyDeviceToHost, c->stream));
+        HIP_CHECK(hipMemcpyAsync(found.data(), d_found, k, hipMemcpyDeviceToHost, c->stream));
+        HIP_CHECK(hipStreamSynchronize(c->stream));
+        for (u32 i = 0; i < k; i++)
+            if (found[i]) memcpy(&out[found_total++], &rows[i], sizeof(Row));
+    }
+    return found_total;
+}
+
+extern "C" uint32_t tbgpu_lookup_accounts(tbgpu_ctx* c, const tb_uint128_t* ids, uint32_t count, tb_account_t* out) {
+    return lookup(c, ids, count, (Account*)out, [&](const u128* d, u32 k, Account* o, u8* f) {
+        launch_lookup_accounts(c->T, d, k, o, f, c->stream);
+    });
+}
+
+extern "C" uint32_t tbgpu_lookup_transfers(tbgpu_ctx* c, const tb_uint128_t* ids, uint32_t count, tb_transfer_t* out) {
+    return lookup(c, ids, count, (Transfer*)out, [&](const u128* d, u32 k, Transfer* o, u8* f) {
+        launch_lookup_transfers(c->T, d, k, o, f, c->stream);
+    });
+}
+
+static u128 to128(tb_uint128_t x) { return ((u128)x.hi << 64) | x.lo; }
+
+extern "C" int tbgpu_test_set_balances(tbgpu_ctx* c, tb_uint128_t id, tb_uint128_t dp, tb_uint128_t dpo,
+                                       tb_uint128_t cp, tb_uint128_t cpo) {
+    HIP_CHECK(hipSetDevice(c->device));
+    Bal4 b{to128(dp), to128(dpo), to128(cp), to128(cpo)};
+    launch_set_balances(c->T, to128(id), b, c->status, c->stream);
+    int st = 0;
+    HIP_CHECK(hipMemcpyAsync(&st, c->status, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(hipStreamSynchronize(c->stream));
+    return st;
+}
+
+extern "C" int tbgpu_get_posted(tbgpu_ctx* c, tb_uint128_t pending_id) {
+    HIP_CHECK(hipSetDevice(c->device));
+    launch_get_posted(c->T, to128(pending_id), c->status, c->stream);
+    int st = 0;
+    HIP_CHECK(hipMemcpyAsync(&st, c->status, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(hipStreamSynchronize(c->stream));
+    return st;
+}
+
+extern "C" uint64_t tbgpu_account_count(tbgpu_ctx* c) { return c->n_accounts; }
+extern "C" uint64_t tbgpu_transfer_count(tbgpu_ctx* c) { return c->n_rows; }
+extern "C" uint64_t tbgpu_history_count(tbgpu_ctx* c) { return c->n_hist; }
+
+extern "C" uint64_t tbgpu_export_transfers(tbgpu_ctx* c, uint64_t first, uint64_t count, tb_transfer_t* out) {
+    HIP_CHECK(hipSetDevice(c->device));
+    if (first >= c->n_rows) return 0;
+    count = std::min<u64>(count, c->n_rows - first);
+    HIP_CHECK(hipMemcpy(out, c->T.xrows + first, count * sizeof(Transfer), hipMemcpyDeviceToHost));
+    return count;
+}
+
+extern "C" uint64_t tbgpu_export_history(tbgpu_ctx* c, uint64_t first, uint64_t count, tb_account_history_t* out) {
+    HIP_CHECK(hipSetDevice(c->device));
+    if (first >= c->n_hist) return 0;
+    count = std::min<u64>(count, c->n_hist - first);
+    HIP_CHECK(hipMemcpy(out, c->T.hrows + first, count * sizeof(History), hipMemcpyDeviceToHost));
+    return count;
+}
+
+extern "C" uint64_t tbgpu_export_accounts(tbgpu_ctx* c, tb_account_t* out, uint64_t capacity) {
+    HIP_CHECK(hipSetDevice(c->device));
+    const u64 chunk = 1u << 16;
+    std::vector<Account> buf(chunk);
+    u64 n = 0;
+    for (u64 off = 0; off < c->acc_cap && n < capacity; off += chunk) {
+        const u64 k = std::min(chunk, c->acc_cap - off);
+        HIP_CHECK(hipMemcpy(buf.data(), c->T.acc + off, k * sizeof(Account), hipMemcpyDeviceToHost));
+        for (u64 i = 0; i < k && n < capacity; i++)
+            if (buf[i].timestamp != 0) memcpy(&out[n++], &buf[i], sizeof(Account));
+    }
+    return n;
+}
+
+extern "C" uint64_t tbgpu_commit_timestamp(tbgpu_ctx* c) {
+    HIP_CHECK(hipSetDevice(c->device));
+    u64 v = 0;
+    HIP_CHECK(hipMemcpy(&v, c->T.commit_ts, sizeof(u64), hipMemcpyDeviceToHost));
+    return v;
+}
+
+extern "C" void tbgpu_last_stats(tbgpu_ctx* c, tbgpu_stats* out) { *out = c->stats; }
+
+extern "C" int tbgpu_last_error(tbgpu_ctx* c, char* buf, uint32_t len) {
+    if (!buf || !len) return 0;
+    snprintf(buf, len, "%s", c ? c->err : "no ctx");
+    return (int)strlen(buf);
+}

@@ -1,0 +1,85 @@
+// transfers.h — per-call arguments of the create_transfers kernels.
+#pragma once
+#include "engine.h"
+
+struct TrArgs {
+    const Transfer* ev;   // events of the call (all batches), in HBM
+    u32 n;                // event count
+    u32 nb;               // batch count
+    const u32* b_start;   // [nb + 1] event offset of each batch
+    const u64* b_ts;      // [nb] prepare timestamp of each batch
+    u64* ts;              // assigned event timestamps
+    u32* cs;              // linked-chain start (== index for standalone events)
+    u32* ce;              // linked-chain end (inclusive)
+    u8* sres;             // static result or SRES_DYN
+    u32* dslot;           // debit / credit account slots (regular transfers)
+    u32* cslot;
+    u32* pre_e;           // committed row with the same id, or NONE32
+    u32* pre_p;           // committed row with id == pending_id, or NONE32
+    u32* pp_dslot;        // account slots of that committed pending transfer
+    u32* pp_cslot;
+    u32* gslot;           // group-table slot of the id / of the pending_id
+    u32* pslot;
+    u32* prev_id;         // previous dynamic event with the same id
+    u32* pend_last;       // last earlier dynamic event whose id == pending_id
+    u32* prev_pend;       // previous dynamic post/void with the same pending_id
+    u32* gclaim;          // group table: claim words, member counts, ranges
+    u32* gcnt_id;
+    u32* gcnt_pd;
+    u32* gmem;
+    u32* gbeg;
+    u32* gend;
+    const u32* gmembers;  // id-sorted members (valid when FL_MULTI_ID)
+    u64 gmask;
+    u32* counters;
+};
+
+void tr_launch_classify(const Tables& T, const TrArgs& C, hipStream_t stream);
+void tr_launch_group_sort(const TrArgs& C, u32 kind, u32 invalid, int bits, u32* k_in, u32* v_in, u32* k_out,
+                          u32* v_out, SortScratch& ss, hipStream_t stream);
+void tr_launch_group2(const TrArgs& C, hipStream_t stream);
+void tr_launch_init(const Tables& T, const TrArgs& C, const EvalState& D, hipStream_t stream);
+void tr_launch_sides(const TrArgs& C, const EvalState& S, u32 invalid, u32* skey, u32* sval, hipStream_t stream);
+void tr_launch_side_pos(const u32* sval_s, u64 m, u32* spos, hipStream_t stream);
+void tr_launch_evaluate(const Tables& T, const TrArgs& C, const EvalState& S, const EvalState& D, const u32* spos,
+                        const Bal4* bb, hipStream_t stream);
+void tr_launch_mask(const Tables& T, const TrArgs& C, const EvalState& S, u8* fres, u8* mask, hipStream_t stream);
+void tr_launch_apply(const Tables& T, const TrArgs& C, const EvalState& S, const u8* fres, const uint4* rk,
+                     const u32* spos, const Bal4* bb, u64 row_base, u64 hist_base,
+                     tb_create_transfers_result_t* results, u32* counts, hipStream_t stream);
+
+// create_accounts (accounts.hip)
+struct AcArgs {
+    const Account* ev;
+    u32 n;
+    u32 nb;
+    const u32* b_start;
+    const u64* b_ts;
+    u64* ts;
+    u32* cs;
+    u32* ce;
+    u8* sres;
+    u32* pre;       // slot of an existing account with the same id
+    u32* gslot;
+    u32* prev_id;
+    u32* gclaim;
+    u32* gcnt_id;
+    u64 gmask;
+    u32* counters;
+};
+void ac_launch_classify(const Tables& T, const AcArgs& C, hipStream_t stream);
+void ac_launch_group_sort(const AcArgs& C, u32 invalid, int bits, u32* k_in, u32* v_in, u32* k_out, u32* v_out,
+                          SortScratch& ss, hipStream_t stream);
+void ac_launch_init(const AcArgs& C, u8* res, u8* ok, u32* cfail, hipStream_t stream);
+void ac_launch_evaluate(const Tables& T, const AcArgs& C, const u8* res_s, const u8* ok_s, u8* res_d, u8* ok_d,
+                        u32* cfail_d, hipStream_t stream);
+void ac_launch_mask(const AcArgs& C, const u8* res, const u8* ok, const u32* cfail, u8* fres, u8* mask,
+                    hipStream_t stream);
+void ac_launch_apply(const Tables& T, const AcArgs& C, const u8* ok, const u8* fres, const uint4* rk,
+                     tb_create_accounts_result_t* results, u32* counts, hipStream_t stream);
+
+// lookups / maintenance (accounts.hip)
+void launch_lookup_accounts(const Tables& T, const u128* ids, u32 n, Account* out, u8* found, hipStream_t stream);
+void launch_lookup_transfers(const Tables& T, const u128* ids, u32 n, Transfer* out, u8* found, hipStream_t stream);
+void launch_set_balances(const Tables& T, u128 id, Bal4 b, int* status, hipStream_t stream);
+void launch_get_posted(const Tables& T, u128 id, int* status, hipStream_t stream);

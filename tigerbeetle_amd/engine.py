@@ -1,0 +1,227 @@
+"""ctypes binding of libtbgpu.so — the C-ABI in include/tbgpu.h.
+
+This is the product path: every call goes to the HIP engine on the GPU.  There
+is no CPU fallback; loading fails loudly when the library is missing and
+``Engine()`` fails loudly when no GPU is visible.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import numpy as np
+
+from .types import (ACCOUNT_DTYPE, HISTORY_DTYPE, RESULT_DTYPE, TRANSFER_DTYPE, U64_MAX, u128_array)
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+LIB_PATH = os.path.join(PKG, "libtbgpu.so")
+HEADER = os.path.join(ROOT, "include", "tbgpu.h")
+_lib = None
+
+
+class U128(ctypes.Structure):
+    _fields_ = [("lo", ctypes.c_uint64), ("hi", ctypes.c_uint64)]
+
+
+def u128(v: int) -> U128:
+    return U128(v & U64_MAX, v >> 64)
+
+
+class Options(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("reserved0", ctypes.c_uint32), ("accounts_max", ctypes.c_uint64),
+                ("transfers_max", ctypes.c_uint64), ("history_max", ctypes.c_uint64),
+                ("events_per_call_max", ctypes.c_uint64), ("flags", ctypes.c_uint32),
+                ("reserved1", ctypes.c_uint32)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("events", ctypes.c_uint64), ("iterations", ctypes.c_uint32), ("path", ctypes.c_uint32),
+                ("sorts", ctypes.c_uint64), ("device_ms", ctypes.c_double)]
+
+
+OPT_FORCE_GENERAL = 1
+
+
+def header_symbols() -> list[str]:
+    """Every function the C-ABI header declares."""
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(tbgpu_[a-z0-9_]+)\s*\(", text)))
+
+
+def lib():
+    """Load libtbgpu.so (built in-tree by tigerbeetle_amd.build)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: run `python -m tigerbeetle_amd.build` (no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
+    L.tbgpu_init.restype = ctypes.c_int
+    L.tbgpu_init.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(Options)]
+    L.tbgpu_deinit.argtypes = [vp]
+    L.tbgpu_reset.argtypes = [vp]
+    for name in ("tbgpu_create_accounts", "tbgpu_create_transfers"):
+        getattr(L, name).restype = u32
+        getattr(L, name).argtypes = [vp, u64, vp, u32, vp]
+    for name in ("tbgpu_create_transfers_batches", "tbgpu_create_accounts_batches",
+                 "tbgpu_create_transfers_batches_device"):
+        getattr(L, name).restype = u64
+        getattr(L, name).argtypes = [vp, u32, vp, vp, vp, vp, vp]
+    for name in ("tbgpu_lookup_accounts", "tbgpu_lookup_transfers"):
+        getattr(L, name).restype = u32
+        getattr(L, name).argtypes = [vp, vp, u32, vp]
+    L.tbgpu_test_set_balances.restype = ctypes.c_int
+    L.tbgpu_test_set_balances.argtypes = [vp, U128, U128, U128, U128, U128]
+    for name in ("tbgpu_account_count", "tbgpu_transfer_count", "tbgpu_history_count", "tbgpu_commit_timestamp"):
+        getattr(L, name).restype = u64
+        getattr(L, name).argtypes = [vp]
+    L.tbgpu_export_transfers.restype = u64
+    L.tbgpu_export_transfers.argtypes = [vp, u64, u64, vp]
+    L.tbgpu_export_history.restype = u64
+    L.tbgpu_export_history.argtypes = [vp, u64, u64, vp]
+    L.tbgpu_export_accounts.restype = u64
+    L.tbgpu_export_accounts.argtypes = [vp, vp, u64]
+    L.tbgpu_get_posted.restype = ctypes.c_int
+    L.tbgpu_get_posted.argtypes = [vp, U128]
+    L.tbgpu_last_stats.argtypes = [vp, ctypes.POINTER(Stats)]
+    L.tbgpu_last_error.restype = ctypes.c_int
+    L.tbgpu_last_error.argtypes = [vp, ctypes.c_char_p, u32]
+    _lib = L
+    return L
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Engine:
+    """One commit-engine context on one GPU (a StateMachine's hot-path state)."""
+
+    name = "gpu"
+
+    def __init__(self, device: int = 0, accounts_max: int = 1 << 16, transfers_max: int = 1 << 20,
+                 history_max: int = 1 << 16, events_per_call_max: int = 1 << 17, force_general: bool = False):
+        self._L = lib()
+        opt = Options(device=device, accounts_max=accounts_max, transfers_max=transfers_max,
+                      history_max=history_max, events_per_call_max=events_per_call_max,
+                      flags=OPT_FORCE_GENERAL if force_general else 0)
+        h = ctypes.c_void_p()
+        rc = self._L.tbgpu_init(ctypes.byref(h), ctypes.byref(opt))
+        if rc != 0:
+            raise RuntimeError(f"tbgpu_init failed ({rc}): no usable GPU (the engine has no CPU fallback)")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.tbgpu_deinit(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self):
+        self._L.tbgpu_reset(self._h)
+
+    # -- commit -------------------------------------------------------------
+    def create_accounts(self, timestamp: int, events: np.ndarray) -> np.ndarray:
+        events = np.ascontiguousarray(events, dtype=ACCOUNT_DTYPE)
+        out = np.zeros(max(len(events), 1), dtype=RESULT_DTYPE)
+        n = self._L.tbgpu_create_accounts(self._h, timestamp, _ptr(events), len(events), _ptr(out))
+        return out[:n].copy()
+
+    def create_transfers(self, timestamp: int, events: np.ndarray) -> np.ndarray:
+        events = np.ascontiguousarray(events, dtype=TRANSFER_DTYPE)
+        out = np.zeros(max(len(events), 1), dtype=RESULT_DTYPE)
+        n = self._L.tbgpu_create_transfers(self._h, timestamp, _ptr(events), len(events), _ptr(out))
+        return out[:n].copy()
+
+    def create_transfers_batches(self, timestamps, counts, events):
+        ts = np.ascontiguousarray(timestamps, dtype=np.uint64)
+        cs = np.ascontiguousarray(counts, dtype=np.uint32)
+        events = np.ascontiguousarray(events, dtype=TRANSFER_DTYPE)
+        out = np.zeros(max(len(events), 1), dtype=RESULT_DTYPE)
+        rc = np.zeros(len(cs), dtype=np.uint32)
+        self._L.tbgpu_create_transfers_batches(self._h, len(cs), _ptr(ts), _ptr(cs), _ptr(events), _ptr(out),
+                                               _ptr(rc))
+        return out, rc, self.stats().device_ms / 1e3
+
+    def create_transfers_batches_device(self, timestamps, counts, events_ptr: int, results_ptr: int):
+        ts = np.ascontiguousarray(timestamps, dtype=np.uint64)
+        cs = np.ascontiguousarray(counts, dtype=np.uint32)
+        rc = np.zeros(len(cs), dtype=np.uint32)
+        total = self._L.tbgpu_create_transfers_batches_device(self._h, len(cs), _ptr(ts), _ptr(cs),
+                                                              ctypes.c_void_p(events_ptr),
+                                                              ctypes.c_void_p(results_ptr), _ptr(rc))
+        return total, rc
+
+    def create_accounts_batches(self, timestamps, counts, events):
+        ts = np.ascontiguousarray(timestamps, dtype=np.uint64)
+        cs = np.ascontiguousarray(counts, dtype=np.uint32)
+        events = np.ascontiguousarray(events, dtype=ACCOUNT_DTYPE)
+        out = np.zeros(max(len(events), 1), dtype=RESULT_DTYPE)
+        rc = np.zeros(len(cs), dtype=np.uint32)
+        self._L.tbgpu_create_accounts_batches(self._h, len(cs), _ptr(ts), _ptr(cs), _ptr(events), _ptr(out),
+                                              _ptr(rc))
+        return out, rc
+
+    # -- queries --------------------------------------------------------------
+    def lookup_accounts(self, ids) -> np.ndarray:
+        q = u128_array(list(ids))
+        out = np.zeros(max(len(q), 1), dtype=ACCOUNT_DTYPE)
+        n = self._L.tbgpu_lookup_accounts(self._h, _ptr(q), len(q), _ptr(out))
+        return out[:n].copy()
+
+    def lookup_transfers(self, ids) -> np.ndarray:
+        q = u128_array(list(ids))
+        out = np.zeros(max(len(q), 1), dtype=TRANSFER_DTYPE)
+        n = self._L.tbgpu_lookup_transfers(self._h, _ptr(q), len(q), _ptr(out))
+        return out[:n].copy()
+
+    def set_balances(self, id_, dp, dpo, cp, cpo) -> None:
+        rc = self._L.tbgpu_test_set_balances(self._h, u128(id_), u128(dp), u128(dpo), u128(cp), u128(cpo))
+        assert rc == 0, "setup: account not found"
+
+    def account_count(self) -> int:
+        return self._L.tbgpu_account_count(self._h)
+
+    def transfer_count(self) -> int:
+        return self._L.tbgpu_transfer_count(self._h)
+
+    def history_count(self) -> int:
+        return self._L.tbgpu_history_count(self._h)
+
+    def commit_timestamp(self) -> int:
+        return self._L.tbgpu_commit_timestamp(self._h)
+
+    def export_accounts(self) -> np.ndarray:
+        n = self.account_count()
+        out = np.zeros(max(n, 1), dtype=ACCOUNT_DTYPE)
+        k = self._L.tbgpu_export_accounts(self._h, _ptr(out), n)
+        return out[:k]
+
+    def export_transfers(self, first: int = 0, count: int | None = None) -> np.ndarray:
+        total = self.transfer_count()
+        count = total - first if count is None else count
+        out = np.zeros(max(count, 1), dtype=TRANSFER_DTYPE)
+        n = self._L.tbgpu_export_transfers(self._h, first, count, _ptr(out))
+        return out[:n]
+
+    def export_history(self) -> np.ndarray:
+        n = self.history_count()
+        out = np.zeros(max(n, 1), dtype=HISTORY_DTYPE)
+        self._L.tbgpu_export_history(self._h, 0, n, _ptr(out))
+        return out[:n]
+
+    def get_posted(self, pending_id: int) -> int:
+        return self._L.tbgpu_get_posted(self._h, u128(pending_id))
+
+    def stats(self) -> Stats:
+        s = Stats()
+        self._L.tbgpu_last_stats(self._h, ctypes.byref(s))
+        return s

@@ -1,0 +1,310 @@
+"""Deterministic synthetic workloads for BASELINE.json's configs.
+
+config 1  `tigerbeetle benchmark` defaults (src/tigerbeetle/benchmark_load.zig:209-330):
+          10k accounts (ledger 2, code 1), uniform random debit/credit pairs,
+          amount = floor(Exp(1) * 10000) +| 1, code = rand_u16 +| 1, flags 0,
+          ids = transfer index + 1 (identity IdPermutation).
+config 2  1M accounts on one ledger, debit/credit ranks drawn independently from
+          Zipf(s = 0.99), rank -> id through a fixed random permutation.
+config 3  flag-heavy mix: limit accounts, pending / post / void, balancing,
+          linked chains, duplicate ids and invalid fields, periodic ticks.
+config 4  1000 ledgers x 10k accounts, uniform pairs within a ledger, 1%
+          cross-ledger linked pairs (ledger-sharded across GPUs).
+
+The reference draws from Zig's std.rand; only the *distributions* are
+reproduced (numpy PCG64 streams, seed 42 by default).  Timestamps follow the
+reference test harness (src/state_machine.zig:1973-1978): before each commit
+prepare_timestamp += 1 + len(batch) and the commit timestamp is that value.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from .types import ACCOUNT_DTYPE, BATCH_MAX, TRANSFER_DTYPE, U64_MAX, AccountFlags, TransferFlags
+
+NS_PER_S = 1_000_000_000
+
+
+@dataclass
+class Workload:
+    name: str
+    accounts: np.ndarray
+    account_counts: np.ndarray
+    transfers: np.ndarray
+    transfer_counts: np.ndarray
+    # extra prepare_timestamp ticks applied before transfer batch b (harness `tick`)
+    ticks: dict = field(default_factory=dict)
+
+    def timestamps(self, start: int = 0):
+        """Commit timestamps for the account batches then the transfer batches."""
+        t = start
+        acc_ts = np.zeros(len(self.account_counts), dtype=np.uint64)
+        for b, n in enumerate(self.account_counts):
+            t += 1 + int(n)
+            acc_ts[b] = t
+        tr_ts = np.zeros(len(self.transfer_counts), dtype=np.uint64)
+        for b, n in enumerate(self.transfer_counts):
+            t += self.ticks.get(b, 0)
+            t += 1 + int(n)
+            tr_ts[b] = t
+        return acc_ts, tr_ts
+
+
+def _batches(total: int, size: int = BATCH_MAX) -> np.ndarray:
+    n_full, rem = divmod(total, size)
+    c = [size] * n_full + ([rem] if rem else [])
+    return np.array(c, dtype=np.uint32)
+
+
+def _set128(arr, name, lo, hi=None):
+    arr[name + "_lo"] = lo
+    arr[name + "_hi"] = 0 if hi is None else hi
+
+
+def _amounts(rng, n):
+    # random_int_exponential(u64, 10_000) +| 1  (src/testing/fuzz.zig:16-24)
+    a = np.floor(rng.exponential(1.0, n) * 10_000.0)
+    return np.minimum(a, float(U64_MAX - 1)).astype(np.uint64) + np.uint64(1)
+
+
+def _codes(rng, n):
+    c = rng.integers(0, 1 << 16, n, dtype=np.uint32) + 1
+    return np.minimum(c, 0xFFFF).astype(np.uint16)  # +| saturating
+
+
+def make_accounts(ids: np.ndarray, ledger, code=1, flags=None) -> np.ndarray:
+    a = np.zeros(len(ids), dtype=ACCOUNT_DTYPE)
+    _set128(a, "id", ids.astype(np.uint64))
+    a["ledger"] = ledger
+    a["code"] = code
+    if flags is not None:
+        a["flags"] = flags
+    return a
+
+
+def _transfers(rng, ids, dr, cr, ledger):
+    n = len(ids)
+    t = np.zeros(n, dtype=TRANSFER_DTYPE)
+    _set128(t, "id", ids.astype(np.uint64))
+    _set128(t, "debit_account_id", dr.astype(np.uint64))
+    _set128(t, "credit_account_id", cr.astype(np.uint64))
+    _set128(t, "user_data_128", rng.integers(0, U64_MAX, n, dtype=np.uint64, endpoint=True),
+            rng.integers(0, U64_MAX, n, dtype=np.uint64, endpoint=True))
+    t["user_data_64"] = rng.integers(0, U64_MAX, n, dtype=np.uint64, endpoint=True)
+    t["user_data_32"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    t["ledger"] = ledger
+    t["code"] = _codes(rng, n)
+    _set128(t, "amount", _amounts(rng, n))
+    return t
+
+
+def config1(transfer_count: int = 10_000_000, account_count: int = 10_000, seed: int = 42,
+            batch: int = BATCH_MAX) -> Workload:
+    rng = np.random.default_rng(seed)
+    acc_ids = np.arange(1, account_count + 1, dtype=np.uint64)
+    accounts = make_accounts(acc_ids, ledger=2)
+    dr = rng.integers(0, account_count, transfer_count, dtype=np.uint64)
+    cr = rng.integers(0, account_count, transfer_count, dtype=np.uint64)
+    cr = np.where(dr == cr, (cr + 1) % account_count, cr)  # benchmark_load.zig:291-295
+    ids = np.arange(1, transfer_count + 1, dtype=np.uint64)
+    transfers = _transfers(rng, ids, dr + 1, cr + 1, ledger=2)
+    return Workload("config1", accounts, _batches(account_count), transfers, _batches(transfer_count, batch))
+
+
+def zipf_sampler(rng, n: int, s: float):
+    w = 1.0 / np.power(np.arange(1, n + 1, dtype=np.float64), s)
+    cdf = np.cumsum(w)
+    cdf /= cdf[-1]
+
+    def draw(k):
+        return np.minimum(np.searchsorted(cdf, rng.random(k), side="right"), n - 1).astype(np.uint64)
+    return draw
+
+
+def config2(transfer_count: int = 8_190_000, account_count: int = 1_000_000, seed: int = 42, s: float = 0.99,
+            batch: int = BATCH_MAX) -> Workload:
+    rng = np.random.default_rng(seed)
+    perm = rng.permutation(account_count).astype(np.uint64)  # rank -> account index
+    acc_ids = np.arange(1, account_count + 1, dtype=np.uint64)
+    accounts = make_accounts(acc_ids, ledger=1)
+    draw = zipf_sampler(rng, account_count, s)
+    dr = perm[draw(transfer_count)]
+    cr = perm[draw(transfer_count)]
+    cr = np.where(dr == cr, (cr + 1) % account_count, cr)
+    ids = np.arange(1, transfer_count + 1, dtype=np.uint64)
+    transfers = _transfers(rng, ids, dr + 1, cr + 1, ledger=1)
+    return Workload("config2", accounts, _batches(account_count), transfers, _batches(transfer_count, batch))
+
+
+def config4(transfer_count: int = 16_380_000, ledgers: int = 1000, accounts_per_ledger: int = 10_000,
+            seed: int = 42, cross_ledger_pairs: float = 0.01, batch: int = BATCH_MAX) -> Workload:
+    """Ledger-sharded workload.  Account id = ledger * 2^32 + k (k in 1..accounts_per_ledger)."""
+    rng = np.random.default_rng(seed)
+    led = np.repeat(np.arange(1, ledgers + 1, dtype=np.uint64), accounts_per_ledger)
+    k = np.tile(np.arange(1, accounts_per_ledger + 1, dtype=np.uint64), ledgers)
+    accounts = make_accounts((led << np.uint64(32)) | k, ledger=led.astype(np.uint32))
+    tl = rng.integers(1, ledgers + 1, transfer_count, dtype=np.uint64)
+    dr = rng.integers(0, accounts_per_ledger, transfer_count, dtype=np.uint64)
+    cr = rng.integers(0, accounts_per_ledger, transfer_count, dtype=np.uint64)
+    cr = np.where(dr == cr, (cr + 1) % accounts_per_ledger, cr)
+    ids = np.arange(1, transfer_count + 1, dtype=np.uint64)
+    transfers = _transfers(rng, ids, (tl << np.uint64(32)) | (dr + 1), (tl << np.uint64(32)) | (cr + 1),
+                           ledger=tl.astype(np.uint32))
+    # cross-ledger linked pairs (currency exchange, docs/reference/transfers.md:282): event i and
+    # i+1 linked, the second moved to another ledger.
+    n_pairs = int(transfer_count * cross_ledger_pairs / 2)
+    if n_pairs:
+        starts = rng.choice(np.arange(0, transfer_count - 1, 2), size=n_pairs, replace=False)
+        starts = starts[(starts % batch) != batch - 1]
+        t0 = transfers[starts]
+        t0["flags"] |= TransferFlags.linked
+        transfers[starts] = t0
+        other = (tl[starts] % ledgers) + 1
+        t1 = transfers[starts + 1]
+        t1["ledger"] = other.astype(np.uint32)
+        _set128(t1, "debit_account_id", (other << np.uint64(32)) | (dr[starts + 1] + 1))
+        _set128(t1, "credit_account_id", (other << np.uint64(32)) | (cr[starts + 1] + 1))
+        transfers[starts + 1] = t1
+    return Workload("config4", accounts, _batches(len(accounts)), transfers, _batches(transfer_count, batch))
+
+
+def config3(batches: int = 200, batch: int = BATCH_MAX, account_count: int = 10_000, seed: int = 42,
+            tick_every: int = 50, tick_ns: int = 60 * NS_PER_S) -> Workload:
+    """Flag-heavy mix.
+
+    Per event: single-phase 45%, pending 20% (timeout 0 or Exp(5 s)+1), post 15%
+    (partial 1..p.amount or 0 = inherit), void 10%, balancing debit/credit 5% each.
+    ~25% of events in linked chains of length 2-8, ~1% duplicate ids, ~1%
+    invalid fields.  The first batch funds the limit accounts.
+    """
+    rng = np.random.default_rng(seed)
+    acc_ids = np.arange(1, account_count + 1, dtype=np.uint64)
+    roll = rng.random(account_count)
+    aflags = np.where(roll < 0.30, int(AccountFlags.debits_must_not_exceed_credits),
+                      np.where(roll < 0.40, int(AccountFlags.credits_must_not_exceed_debits), 0)).astype(np.uint16)
+    hist = rng.random(account_count) < 0.02
+    aflags = aflags | np.where(hist, int(AccountFlags.history), 0).astype(np.uint16)
+    accounts = make_accounts(acc_ids, ledger=1, flags=aflags)
+    free = np.nonzero((aflags & 6) == 0)[0]
+    dnec = np.nonzero(aflags & 2)[0]
+    cned = np.nonzero(aflags & 4)[0]
+
+    out = []
+    counts = []
+    next_id = 1
+    pendings: list[tuple[int, int]] = []  # (id, amount)
+    recent_ids: list[int] = []
+
+    def rand_free():
+        return int(free[rng.integers(0, len(free))])
+
+    # funding batch(es): credit every D<C account, debit every C<D account
+    fund = []
+    for a in dnec:
+        fund.append((rand_free(), int(a), int(rng.integers(5_000, 50_000))))
+    for a in cned:
+        fund.append((int(a), rand_free(), int(rng.integers(5_000, 50_000))))
+    for s in range(0, len(fund), batch):
+        part = fund[s:s + batch]
+        t = np.zeros(len(part), dtype=TRANSFER_DTYPE)
+        for j, (d, c, amt) in enumerate(part):
+            t[j]["id_lo"] = next_id
+            next_id += 1
+            t[j]["debit_account_id_lo"] = d + 1
+            t[j]["credit_account_id_lo"] = c + 1
+            t[j]["amount_lo"] = amt
+            t[j]["ledger"] = 1
+            t[j]["code"] = 1
+        out.append(t)
+        counts.append(len(part))
+
+    ticks = {}
+    for b in range(batches):
+        if tick_every and b > 0 and b % tick_every == 0:
+            ticks[len(counts)] = tick_ns
+        t = np.zeros(batch, dtype=TRANSFER_DTYPE)
+        kinds = rng.choice(6, size=batch, p=[0.45, 0.20, 0.15, 0.10, 0.05, 0.05])
+        new_pend = []
+        for j in range(batch):
+            r = t[j]
+            k = kinds[j]
+            tid = next_id
+            next_id += 1
+            if rng.random() < 0.01 and recent_ids:
+                tid = recent_ids[int(rng.integers(0, len(recent_ids)))]  # duplicate id
+            r["id_lo"] = tid
+            r["ledger"] = 1
+            r["code"] = int(rng.integers(1, 100))
+            r["user_data_64"] = int(rng.integers(0, 3))
+            d = int(rng.integers(0, account_count))
+            c = int(rng.integers(0, account_count - 1))
+            c = c + 1 if c >= d else c
+            amt = int(np.floor(rng.exponential(1.0) * 3000)) + 1
+            if k in (2, 3) and pendings:  # post / void an earlier pending
+                pid, pamt = pendings[int(rng.integers(0, len(pendings)))]
+                r["pending_id_lo"] = pid
+                r["flags"] = int(TransferFlags.post_pending_transfer if k == 2 else TransferFlags.void_pending_transfer)
+                if k == 2:
+                    roll = rng.random()
+                    r["amount_lo"] = 0 if roll < 0.3 else int(rng.integers(1, max(2, pamt + 1)))
+                else:
+                    r["amount_lo"] = 0 if rng.random() < 0.5 else pamt
+                r["ledger"] = 0 if rng.random() < 0.5 else 1
+                r["code"] = 0
+            else:
+                r["debit_account_id_lo"] = d + 1
+                r["credit_account_id_lo"] = c + 1
+                r["amount_lo"] = amt
+                if k == 1:
+                    r["flags"] = int(TransferFlags.pending)
+                    r["timeout"] = 0 if rng.random() < 0.5 else int(np.floor(rng.exponential(5.0))) + 1
+                    new_pend.append((tid, amt))
+                elif k == 4:
+                    r["flags"] = int(TransferFlags.balancing_debit)
+                    if rng.random() < 0.5:
+                        r["amount_lo"] = 0
+                elif k == 5:
+                    r["flags"] = int(TransferFlags.balancing_credit)
+                    if rng.random() < 0.5:
+                        r["amount_lo"] = 0
+            if rng.random() < 0.01:  # invalid field
+                which = int(rng.integers(0, 4))
+                if which == 0:
+                    r["ledger"] = 0 if not (int(r["flags"]) & 12) else 7
+                elif which == 1:
+                    r["code"] = 0 if not (int(r["flags"]) & 12) else 7
+                elif which == 2:
+                    r["timeout"] = 5 if not (int(r["flags"]) & 2) else r["timeout"]
+                else:
+                    r["debit_account_id_lo"] = account_count + 77
+            recent_ids.append(tid)
+        # linked chains covering ~25% of events
+        j = 0
+        while j < batch - 1:
+            if rng.random() < 0.25 / 5.0:
+                ln = int(rng.integers(2, 9))
+                ln = min(ln, batch - j)
+                for q in range(j, j + ln - 1):
+                    t[q]["flags"] |= int(TransferFlags.linked)
+                j += ln
+            else:
+                j += 1
+        # an occasional open chain at the batch end
+        if rng.random() < 0.02:
+            t[batch - 1]["flags"] |= int(TransferFlags.linked)
+        out.append(t)
+        counts.append(batch)
+        pendings.extend(new_pend)
+        if len(pendings) > 50_000:
+            pendings = pendings[-50_000:]
+        if len(recent_ids) > 20_000:
+            recent_ids = recent_ids[-20_000:]
+    transfers = np.concatenate(out)
+    return Workload("config3", accounts, _batches(account_count), transfers, np.array(counts, dtype=np.uint32),
+                    ticks)
+
+
+def make(config: int, **kw) -> Workload:
+    return {1: config1, 2: config2, 3: config3, 4: config4}[config](**kw)

@@ -156,7 +156,7 @@ __global__ void ac_evaluate(Tables T, AcArgs C, const u8* res_s, const u8* ok_s,
     if (r != res_s[i]) atomicAdd(&C.counters[CNT_CHANGES], 1u);
 }
 
-__global__ void ac_mask(AcArgs C, const u8* res, const u8* ok, const u32* cfail, u8* fres, u8* mask) {
+__global__ void ac_mask(AcArgs C, const u8* res, const u8* ok, const u32* cfail, u8* fres, u8* mask, u64* commit_ts) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= C.n) return;
     const u32 cs = C.cs[i];
@@ -169,6 +169,8 @@ __global__ void ac_mask(AcArgs C, const u8* res, const u8* ok, const u32* cfail,
     else r = TB_CREATE_ACCOUNT_OK;
     fres[i] = r;
     mask[i] = ((ok[i] & 2) ? 1 : 0) | (r != 0 ? 2 : 0);
+    if ((ok[i] & 1) && (cf == NONE32 || i < cf))  // commit_timestamp survives rollback (:1223)
+        atomicMax((unsigned long long*)commit_ts, (unsigned long long)C.ts[i]);
 }
 
 __global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const uint4* rk,
@@ -206,7 +208,6 @@ __global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const
     dst.ledger = a.ledger;
     dst.code = a.code;
     dst.flags = a.flags;
-    atomicMax((unsigned long long*)T.commit_ts, (unsigned long long)a.timestamp);
 }
 
 __global__ void ac_batch_counts(const u32* b_start, u32 nb, const uint4* rk, u32* counts) {
@@ -269,9 +270,9 @@ void ac_launch_evaluate(const Tables& T, const AcArgs& C, const u8* res_s, const
     ac_evaluate<<<GRID(C.n)>>>(T, C, res_s, ok_s, res_d, ok_d, cfail_d);
     ac_finalize<<<GRID(C.n)>>>(C, ok_d, cfail_d);
 }
-void ac_launch_mask(const AcArgs& C, const u8* res, const u8* ok, const u32* cfail, u8* fres, u8* mask,
-                    hipStream_t stream) {
-    ac_mask<<<GRID(C.n)>>>(C, res, ok, cfail, fres, mask);
+void ac_launch_mask(const Tables& T, const AcArgs& C, const u8* res, const u8* ok, const u32* cfail, u8* fres,
+                    u8* mask, hipStream_t stream) {
+    ac_mask<<<GRID(C.n)>>>(C, res, ok, cfail, fres, mask, T.commit_ts);
 }
 void ac_launch_apply(const Tables& T, const AcArgs& C, const u8* ok, const u8* fres, const uint4* rk,
                      tb_create_accounts_result_t* results, u32* counts, hipStream_t stream) {

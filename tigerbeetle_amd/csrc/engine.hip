@@ -460,7 +460,7 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
         if (c->h_counters[CNT_CHANGES] == 0) break;
     }
     c->stats.iterations = it + 1;
-    ac_launch_mask(C, A->res, A->ok, A->cfail, c->fres, c->mask, s);
+    ac_launch_mask(c->T, C, A->res, A->ok, A->cfail, c->fres, c->mask, s);
     scan3_exclusive(c->mask, c->ranks, n, c->sc, s);
     uint4 tot;
     HIP_CHECK(hipMemcpyAsync(&tot, c->ranks + n, sizeof(uint4), hipMemcpyDeviceToHost, s));

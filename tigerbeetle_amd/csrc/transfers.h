@@ -73,8 +73,8 @@ void ac_launch_group_sort(const AcArgs& C, u32 invalid, int bits, u32* k_in, u32
 void ac_launch_init(const AcArgs& C, u8* res, u8* ok, u32* cfail, hipStream_t stream);
 void ac_launch_evaluate(const Tables& T, const AcArgs& C, const u8* res_s, const u8* ok_s, u8* res_d, u8* ok_d,
                         u32* cfail_d, hipStream_t stream);
-void ac_launch_mask(const AcArgs& C, const u8* res, const u8* ok, const u32* cfail, u8* fres, u8* mask,
-                    hipStream_t stream);
+void ac_launch_mask(const Tables& T, const AcArgs& C, const u8* res, const u8* ok, const u32* cfail, u8* fres,
+                    u8* mask, hipStream_t stream);
 void ac_launch_apply(const Tables& T, const AcArgs& C, const u8* ok, const u8* fres, const uint4* rk,
                      tb_create_accounts_result_t* results, u32* counts, hipStream_t stream);
 

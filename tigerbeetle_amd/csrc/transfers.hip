@@ -564,6 +564,10 @@ __global__ void tr_mask(Tables T, TrArgs C, EvalState S, u8* fres, u8* mask) {
         hist = (T.acc[C.dslot[i]].flags | T.acc[C.cslot[i]].flags) & AF_HISTORY;
     fres[i] = r;
     mask[i] = (ok ? 1 : 0) | (r != 0 ? 2 : 0) | (hist ? 4 : 0);
+    // commit_timestamp is a plain field, not undone by scope_close(.discard): every
+    // create_transfer that returned ok before its chain broke advanced it (:1366).
+    if ((S.ok[i] & 1) && (cf == NONE32 || i < cf))
+        atomicMax((unsigned long long*)T.commit_ts, (unsigned long long)C.ts[i]);
 }
 
 __global__ void tr_apply(Tables T, TrArgs C, EvalState S, const u8* __restrict__ fres, const uint4* __restrict__ rk,
@@ -613,7 +617,6 @@ __global__ void tr_apply(Tables T, TrArgs C, EvalState S, const u8* __restrict__
             T.hrows[hist_base + q.z] = h;
         }
     }
-    atomicMax((unsigned long long*)T.commit_ts, (unsigned long long)s.timestamp);
 }
 
 __global__ void batch_counts(const u32* b_start, u32 nb, const uint4* rk, u32* counts) {

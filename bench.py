@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Committed transfers/s of the MI355X commit engine (BASELINE.json metric).
+
+One *step* = one streamed create_transfers call over `--batches-per-step`
+consecutive 8190-transfer batches, with the events already resident in HBM
+(tbgpu_create_transfers_batches_device).  Results are bit-identical to one
+StateMachine.commit per batch (tests/test_gpu_parity.py).
+
+Default workload: BASELINE config 2 (configs[1]) — 1M accounts on one ledger,
+Zipf(0.99) debit/credit accounts, 8190-transfer batches.  With --gpus N > 1
+(torchrun, one process per GPU) every rank owns its own ledger shard (weak
+scaling, no data-path collective): the ledger partition of SURVEY.md §8e with
+the routing already applied.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+ALGO_BYTES_PER_TRANSFER = 680  # 128 ev + 128 row + 2x128 acct + 2x64 bal + 16 probe + 24 insert
+HBM_PEAK_GBPS = 8000.0         # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", type=int, default=2, choices=(1, 2))
+    ap.add_argument("--batches-per-step", type=int, default=200)
+    ap.add_argument("--accounts", type=int, default=None)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--verify", action="store_true", help="check every result is ok (config 1/2 never fail)")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch  # device memory + torch.distributed plumbing (loaded before libtbgpu: one HIP runtime)
+    import torch.distributed as dist
+    from tigerbeetle_amd import workload
+    from tigerbeetle_amd.engine import PHASES, Engine
+    from tigerbeetle_amd.types import BATCH_MAX
+
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    B, K, W = args.batches_per_step, args.steps, args.warmup
+    n_batches = (K + W) * B
+    n_transfers = n_batches * BATCH_MAX
+    t_gen = time.time()
+    if args.config == 2:
+        acc_n = args.accounts or 1_000_000
+        w = workload.config2(transfer_count=n_transfers, account_count=acc_n, seed=42 + rank)
+    else:
+        acc_n = args.accounts or 10_000
+        w = workload.config1(transfer_count=n_transfers, account_count=acc_n, seed=42 + rank)
+    log(f"[rank {rank}] generated {n_transfers} transfers / {acc_n} accounts in {time.time() - t_gen:.1f}s")
+
+    eng = Engine(device=local_rank, accounts_max=acc_n, transfers_max=n_transfers + 1024,
+                 history_max=1024, events_per_call_max=B * BATCH_MAX)
+    ats, tts = w.timestamps()
+    _, rc = eng.create_accounts_batches(ats, w.account_counts, w.accounts)
+    assert int(rc.sum()) == 0, "account creation failed"
+
+    dev = torch.device("cuda", local_rank)
+    ev_dev = torch.from_numpy(w.transfers.view(np.uint8)).to(dev)
+    res_dev = torch.empty(B * BATCH_MAX * 8, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    counts = w.transfer_counts
+    ev_base = ev_dev.data_ptr()
+    res_ptr = res_dev.data_ptr()
+
+    def step(k):
+        b0 = k * B
+        off = int(counts[:b0].sum()) * 128
+        total, rcs = eng.create_transfers_batches_device(tts[b0:b0 + B], counts[b0:b0 + B], ev_base + off, res_ptr)
+        return int(total)
+
+    for k in range(W):
+        step(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    eng.set_profiling(True)
+    phase = np.zeros(8)
+    dev_ms = 0.0
+    iters = []
+    non_ok = 0
+    t0 = time.perf_counter()
+    for k in range(W, W + K):
+        non_ok += step(k)
+        st = eng.stats()
+        phase += np.array(st.phase_ms[:8])
+        dev_ms += st.device_ms
+        iters.append(st.iterations)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    eng.set_profiling(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        nk = torch.tensor([non_ok], dtype=torch.int64, device=dev)
+        dist.all_reduce(nk)
+        non_ok = int(nk.item())
+    per_rank = K * B * BATCH_MAX
+    total = per_rank * world
+    value = total / elapsed
+    ms_per_step = elapsed / K * 1e3
+
+    # Roofline: the dominant phase, priced with its algorithmic bytes per transfer.
+    names = list(PHASES)
+    dom = int(np.argmax(phase[:len(names)]))
+    phase_ms_per_step = {names[i]: round(phase[i] / K, 4) for i in range(len(names))}
+    e2e_gbps = value / world * ALGO_BYTES_PER_TRANSFER / 1e9
+    roofline = {
+        "bound": "hbm",
+        "achieved": round(e2e_gbps, 2),
+        "peak": HBM_PEAK_GBPS,
+        "unit": "GB/s",
+        "frac": round(e2e_gbps / HBM_PEAK_GBPS, 5),
+        "traffic": None,
+        "basis": "680 B/transfer (SURVEY.md §8d) x per-GPU committed transfers/s over the whole step",
+        "dominant_phase": names[dom],
+        "phase_ms_per_step": phase_ms_per_step,
+        "device_ms_per_step": round(dev_ms / K, 4),
+    }
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        import oracle  # the CPU baseline leg (test infrastructure, never the product path)
+        orc = oracle.Oracle(acc_n, 4 << 20)
+        orc.create_accounts_batches(ats, w.account_counts, w.accounts)
+        done, spent, b = 0, 0.0, 0
+        while spent < args.cpu_seconds and b < len(counts):
+            k = min(16, len(counts) - b)
+            off = int(counts[:b].sum())
+            n = int(counts[b:b + k].sum())
+            _, _, el = orc.create_transfers_batches(tts[b:b + k], counts[b:b + k], w.transfers[off:off + n])
+            done += n
+            spent += el
+            b += k
+        cpu = {"value": round(done / spent, 1), "unit": "transfers/s", "cores": 1, "kind": "port",
+               "sample": f"oracle/oracle.c commit loop (single thread), first {b} batches ({done} transfers) "
+                         f"of the same config-{args.config} stream after creating the {acc_n} accounts; "
+                         f"{spent:.1f}s of CPU work on {cpu_model()}"}
+
+    if rank == 0:
+        line = {
+            "metric": "committed transfers/sec (whole node), 8190-transfer batches; % HBM roofline",
+            "value": round(value, 1),
+            "unit": "transfers/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u128",
+            "data": "synthetic",
+            "config": {"workload": f"config{args.config}: {acc_n} accounts, "
+                                   + ("Zipf(0.99) pairs on 1 ledger" if args.config == 2 else "uniform pairs")
+                                   + f", {B} x 8190-transfer batches per step (streamed, HBM-resident)",
+                       "batches_per_step": B, "transfers_per_step_per_gpu": B * BATCH_MAX,
+                       "parallelism": f"ledger-shard x{world}"},
+            "non_ok_results": non_ok,
+            "fixed_point_passes": max(iters) if iters else 0,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -244,9 +244,11 @@ uint64_t tbgpu_create_transfers_batches(tbgpu_ctx* ctx, uint32_t batch_count,
                                         tb_create_transfers_result_t* results,
                                         uint32_t* result_counts);
 
-/* Same with the events already resident in device memory (HBM) and results left
- * in device memory (same layout).  `timestamps`/`counts`/`result_counts` are host
- * arrays.  `stream` is a hipStream_t passed as void* (NULL = the ctx stream). */
+/* Same with the events already resident in device memory (HBM) and the replies
+ * left in device memory.  On the device the replies are concatenated: batch b's
+ * `result_counts[b]` results follow batch b-1's (the streaming reply format);
+ * each result's `index` is relative to its own batch.  `timestamps`, `counts`
+ * and `result_counts` are host arrays. */
 uint64_t tbgpu_create_transfers_batches_device(tbgpu_ctx* ctx, uint32_t batch_count,
                                                const uint64_t* timestamps, const uint32_t* counts,
                                                const void* events_device,
@@ -292,8 +294,14 @@ typedef struct tbgpu_stats {
     uint32_t path;            /* 0 general (scan + rescan), 1 fast (no rescan)  */
     uint64_t sorts;           /* side sorts performed                           */
     double   device_ms;       /* HIP-event time of the last call's device work  */
+    /* With profiling on: HIP-event time per phase of the last call, on the ctx
+     * stream: [0] upload [1] classify+group [2] sort [3] balance scan
+     * [4] evaluate [5] apply [6] reserved [7] reserved. */
+    double   phase_ms[8];
 } tbgpu_stats;
 void tbgpu_last_stats(tbgpu_ctx* ctx, tbgpu_stats* out);
+/* Enable per-phase HIP-event timing (adds a few event records per call). */
+void tbgpu_set_profiling(tbgpu_ctx* ctx, int enable);
 int  tbgpu_last_error(tbgpu_ctx* ctx, char* buf, uint32_t len);
 
 #ifdef __cplusplus

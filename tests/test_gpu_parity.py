@@ -21,6 +21,11 @@ def _engine(**kw):
     return Engine(**args)
 
 
+@pytest.fixture(params=[False, True], ids=["auto", "general"])
+def force_general(request):
+    return request.param
+
+
 def _parity(w, split=None, **kw):
     orc = oracle.Oracle(len(w.accounts), len(w.transfers))
     gpu = _engine(**kw)
@@ -35,28 +40,28 @@ def _parity(w, split=None, **kw):
         gpu.close()
 
 
-def test_config1_small():
-    _parity(workload.config1(transfer_count=50_000, account_count=1000))
+def test_config1_small(force_general):
+    _parity(workload.config1(transfer_count=50_000, account_count=1000), force_general=force_general)
 
 
-def test_config1_batch_by_batch():
-    _parity(workload.config1(transfer_count=20_000, account_count=500), split=1)
+def test_config1_batch_by_batch(force_general):
+    _parity(workload.config1(transfer_count=20_000, account_count=500), split=1, force_general=force_general)
 
 
-def test_config2_small_zipf():
-    _parity(workload.config2(transfer_count=100_000, account_count=20_000))
+def test_config2_small_zipf(force_general):
+    _parity(workload.config2(transfer_count=100_000, account_count=20_000), force_general=force_general)
 
 
-def test_config3_flag_mix():
-    _parity(workload.config3(batches=6, batch=2000, account_count=2000))
+def test_config3_flag_mix(force_general):
+    _parity(workload.config3(batches=6, batch=2000, account_count=2000), force_general=force_general)
 
 
-def test_config3_batch_by_batch():
-    _parity(workload.config3(batches=4, batch=1000, account_count=500, seed=7), split=1)
+def test_config3_batch_by_batch(force_general):
+    _parity(workload.config3(batches=4, batch=1000, account_count=500, seed=7), split=1, force_general=force_general)
 
 
-def test_config3_full_batches():
-    _parity(workload.config3(batches=4, account_count=10_000, seed=3))
+def test_config3_full_batches(force_general):
+    _parity(workload.config3(batches=4, account_count=10_000, seed=3), force_general=force_general)
 
 
 def test_posted_groove():
@@ -83,5 +88,49 @@ def test_lookups_match():
         assert gpu.lookup_accounts(ids).tobytes() == orc.lookup_accounts(ids).tobytes()
         tids = list(range(0, 6000, 7)) + [(1 << 128) - 1]
         assert gpu.lookup_transfers(tids).tobytes() == orc.lookup_transfers(tids).tobytes()
+    finally:
+        gpu.close()
+
+
+def test_fast_path_is_taken_for_plain_batches():
+    w = workload.config2(transfer_count=30_000, account_count=5_000)
+    gpu = _engine()
+    try:
+        run_workload(gpu, w)
+        st = gpu.stats()
+        assert st.path == 1 and st.iterations == 1
+    finally:
+        gpu.close()
+
+
+def test_fast_path_falls_back_exactly():
+    """Plain batches followed by one duplicate id: the fast attempt undoes its deltas."""
+    w = workload.config1(transfer_count=20_000, account_count=300, seed=9)
+    t = w.transfers.copy()
+    t[15_000]["id_lo"] = t[14_000]["id_lo"]  # duplicate inside one call
+    t[16_000]["amount_lo"] = 0               # a static failure next to it
+    w.transfers = t
+    _parity(w)
+
+
+def test_overflow_guard_routes_to_general():
+    """Huge balances (high words >= 2^62) are never handled by the fast path."""
+    from table import check
+    text = """
+account A1 0 0 0 0 _ _ _ _ L1 C1 _ _ _ _ _ ok
+account A2 0 0 0 0 _ _ _ _ L1 C1 _ _ _ _ _ ok
+commit create_accounts
+setup A1 0 -10 0 0
+setup A2 0 0 0 -20
+transfer T1 A1 A2 5 _ _ _ _ _ L1 C1 _ _ _ _ _ _ _ _ ok
+transfer T2 A1 A2 6 _ _ _ _ _ L1 C1 _ _ _ _ _ _ _ _ overflows_debits_posted
+transfer T3 A2 A1 9 _ _ _ _ _ L1 C1 _ _ _ _ _ _ _ _ ok
+commit create_transfers
+lookup_account A1 0 -5 0 9
+commit lookup_accounts
+"""
+    gpu = _engine()
+    try:
+        check(gpu, text)
     finally:
         gpu.close()

@@ -181,7 +181,7 @@ __global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const
     if (r != 0) {
         const u32 b = ac_batch_of(C.b_start, C.nb, i);
         const u32 bs = C.b_start[b];
-        results[bs + (rk[i].y - rk[bs].y)] = {i - bs, (u32)r};
+        results[rk[i].y] = {i - bs, (u32)r};  // concatenated replies
         return;
     }
     if (!(ok[i] & 2)) return;

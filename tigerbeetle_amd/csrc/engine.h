@@ -82,6 +82,7 @@ enum {
     CNT_FLAGS = 0,      // FL_* bits
     CNT_CHANGES = 1,    // fixed-point: events whose state changed this pass
     CNT_KEYS = 2,       // side keys changed since the last sort
+    CNT_OK = 3,         // fast path: accepted events
     CNT_COUNT = 16,
 };
 enum {
@@ -93,4 +94,6 @@ enum {
     FL_MULTI_PEND = 1u << 5,  // two post/voids name the same pending id
     FL_PENDING = 1u << 6,     // pending transfers present
     FL_HISTORY = 1u << 7,     // an account with flags.history is touched
+    FL_SLOW = 1u << 8,        // fast path: some event needs the fixed point
+    FL_ERROR = 1u << 9,       // device-side protocol error (bounded spin expired)
 };

@@ -18,6 +18,7 @@
 #include "common.h"
 #include "engine.h"
 #include "transfers.h"
+#include "fast.h"
 
 [[noreturn]] void tbgpu_fatal(const char* what, const char* why, const char* file, int line) {
     fprintf(stderr, "tbgpu: fatal: %s: %s (%s:%d)\n", what, why, file, line);
@@ -82,7 +83,20 @@ struct tbgpu_ctx {
     u32* counters = nullptr;
     int* status = nullptr;
     u32* h_counters = nullptr;  // pinned
+    // fast path (fast.hip)
+    u64* f_gtab = nullptr;
+    u64 f_gcap = 0;
+    u32 f_epoch = 0;
+    u64* f_tiles = nullptr;
+    u32* f_tile_counter = nullptr;
+    u128* f_keys = nullptr;
+    u32* f_rows = nullptr;
     hipEvent_t ev0, ev1;
+    // phase profiler: consecutive marks on the ctx stream; segment k belongs to
+    // the phase opened by mark k.
+    bool prof = false;
+    std::vector<hipEvent_t> prof_pool;
+    std::vector<int> prof_phase;
     tbgpu_stats stats{};
     char err[256] = {0};
 };
@@ -135,11 +149,48 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->counts = dalloc<u32>(c->bmax, &B);
     c->counters = dalloc<u32>(CNT_COUNT, &B);
     c->status = dalloc<int>(4, &B);
+    c->f_gcap = pow2_at_least(2 * nmax);
+    c->f_gtab = dalloc<u64>(c->f_gcap, &B);
+    HIP_CHECK(hipMemset(c->f_gtab, 0, c->f_gcap * sizeof(u64)));
+    c->f_tiles = dalloc<u64>(fp_tiles(nmax) + 1, &B);
+    c->f_tile_counter = dalloc<u32>(4, &B);
+    c->f_keys = dalloc<u128>(n, &B);
+    c->f_rows = dalloc<u32>(n, &B);
     HIP_CHECK(hipHostMalloc((void**)&c->h_counters, CNT_COUNT * sizeof(u32), hipHostMallocDefault));
 }
 
-static void set_err(tbgpu_ctx* c, const char* msg) {
-    snprintf(c->err, sizeof c->err, "%s", msg);
+enum { PH_UPLOAD = 0, PH_CLASSIFY = 1, PH_SORT = 2, PH_SCAN = 3, PH_EVAL = 4, PH_APPLY = 5, PH_END = -1 };
+
+static void prof_mark(tbgpu_ctx* c, int phase) {
+    if (!c->prof) return;
+    const size_t k = c->prof_phase.size();
+    if (k >= c->prof_pool.size()) return;  // pool exhausted: stop recording
+    HIP_CHECK(hipEventRecord(c->prof_pool[k], c->stream));
+    c->prof_phase.push_back(phase);
+}
+
+static void prof_collect(tbgpu_ctx* c) {
+    for (double& v : c->stats.phase_ms) v = 0;
+    if (!c->prof || c->prof_phase.size() < 2) { c->prof_phase.clear(); return; }
+    HIP_CHECK(hipEventSynchronize(c->prof_pool[c->prof_phase.size() - 1]));
+    for (size_t k = 0; k + 1 < c->prof_phase.size(); k++) {
+        const int ph = c->prof_phase[k];
+        if (ph < 0 || ph >= 8) continue;
+        float ms = 0;
+        HIP_CHECK(hipEventElapsedTime(&ms, c->prof_pool[k], c->prof_pool[k + 1]));
+        c->stats.phase_ms[ph] += ms;
+    }
+    c->prof_phase.clear();
+}
+
+extern "C" void tbgpu_set_profiling(tbgpu_ctx* c, int enable) {
+    HIP_CHECK(hipSetDevice(c->device));
+    c->prof = enable != 0;
+    if (c->prof && c->prof_pool.empty()) {
+        c->prof_pool.resize(4096);
+        for (hipEvent_t& e : c->prof_pool) HIP_CHECK(hipEventCreate(&e));
+    }
+    c->prof_phase.clear();
 }
 
 extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
@@ -202,13 +253,15 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
                     c->pp_dslot, c->pp_cslot, c->gslot, c->pslot, c->prev_id, c->pend_last, c->prev_pend,
                     c->gclaim, c->gcnt_id, c->gcnt_pd, c->gmem, c->gbeg, c->gend, c->skey, c->sval, c->skey_s,
                     c->sval_s, c->spos, c->bb, c->ss.keys_tmp, c->ss.vals_tmp, c->ss.hist, c->side_tiles,
-                    c->sc.tile_sums, c->fres, c->mask, c->ranks, c->res_buf, c->counts, c->counters, c->status};
+                    c->sc.tile_sums, c->fres, c->mask, c->ranks, c->res_buf, c->counts, c->counters, c->status,
+                    c->f_gtab, c->f_tiles, c->f_tile_counter, c->f_keys, c->f_rows};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     for (EvalState& s : c->st) {
         void* q[] = {s.res, s.ok, s.pref, s.cfail, s.amt, s.pamt, s.dpend, s.dpost};
         for (void* p : q) if (p) (void)hipFree(p);
     }
     if (c->h_counters) (void)hipHostFree(c->h_counters);
+    for (hipEvent_t e : c->prof_pool) (void)hipEventDestroy(e);
     (void)hipEventDestroy(c->ev0);
     (void)hipEventDestroy(c->ev1);
     (void)hipStreamDestroy(c->stream);
@@ -244,6 +297,23 @@ static void upload_batches(tbgpu_ctx* c, const uint64_t* timestamps, const uint3
     HIP_CHECK(hipMemcpyAsync(c->b_ts, timestamps, nb * sizeof(u64), hipMemcpyHostToDevice, c->stream));
 }
 
+// Device replies are concatenated across the chunk's batches; the host C-ABI
+// places batch b's reply at the batch's event offset.
+static void copy_results_to_batches(tbgpu_ctx* c, u32 nb, const std::vector<u32>& starts, const u32* counts,
+                                    u8* dst_chunk) {
+    u64 total = 0;
+    for (u32 b = 0; b < nb; b++) total += counts[b];
+    if (total == 0) return;
+    std::vector<u8> tmp(total * 8);
+    HIP_CHECK(hipMemcpyAsync(tmp.data(), c->res_buf, total * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(hipStreamSynchronize(c->stream));
+    u64 off = 0;
+    for (u32 b = 0; b < nb; b++) {
+        memcpy(dst_chunk + (u64)starts[b] * 8, tmp.data() + off * 8, (u64)counts[b] * 8);
+        off += counts[b];
+    }
+}
+
 static TrArgs make_tr_args(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb) {
     TrArgs C{};
     C.ev = ev; C.n = n; C.nb = nb;
@@ -259,6 +329,52 @@ static TrArgs make_tr_args(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb) {
     C.gmask = g - 1;
     C.counters = c->counters;
     return C;
+}
+
+// Single-pass attempt (fast.hip).  Returns false, with every balance delta
+// undone, when some event needs the fixed point.
+static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tb_create_transfers_result_t* results_dev,
+                     u32* counts_host) {
+    hipStream_t s = c->stream;
+    if (++c->f_epoch == 0) {  // epoch wrapped: clear the claim table once
+        HIP_CHECK(hipMemsetAsync(c->f_gtab, 0, c->f_gcap * sizeof(u64), s));
+        c->f_epoch = 1;
+    }
+    FastArgs F{};
+    F.ev = ev; F.n = n; F.nb = nb; F.b_start = c->b_start; F.b_ts = c->b_ts;
+    F.gtab = c->f_gtab;
+    F.gmask = std::min<u64>(c->f_gcap, pow2_at_least(2ull * n)) - 1;
+    F.epoch = (u64)c->f_epoch << 32;
+    F.fres = c->fres;
+    F.counters = c->counters;
+    F.tile_status = c->f_tiles;
+    F.tile_counter = c->f_tile_counter;
+    F.batch_counts = c->counts;
+    F.results = results_dev;
+    F.row_base = c->n_rows;
+    F.keys = c->f_keys;
+    F.rows = c->f_rows;
+    if (c->n_rows + n > c->xrow_cap) return false;  // let the general path report capacity exactly
+    prof_mark(c, PH_CLASSIFY);
+    HIP_CHECK(hipMemsetAsync(c->counters, 0, CNT_COUNT * sizeof(u32), s));
+    HIP_CHECK(hipMemsetAsync(c->f_tiles, 0, fp_tiles(n) * sizeof(u64), s));
+    HIP_CHECK(hipMemsetAsync(c->f_tile_counter, 0, sizeof(u32), s));
+    HIP_CHECK(hipMemsetAsync(c->counts, 0, nb * sizeof(u32), s));
+    fp_launch_commit(c->T, F, s);
+    prof_mark(c, PH_END);
+    read_counters(c);
+    const u32 flags = c->h_counters[CNT_FLAGS];
+    if (flags & FL_ERROR) tbgpu_fatal("create_transfers", "fast path look-back did not complete", __FILE__, __LINE__);
+    if (flags & FL_SLOW) {
+        fp_launch_undo(c->T, F, s);
+        return false;
+    }
+    HIP_CHECK(hipMemcpyAsync(counts_host, c->counts, nb * sizeof(u32), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    c->n_rows += c->h_counters[CNT_OK];
+    c->stats.path = 1;
+    c->stats.iterations = 1;
+    return true;
 }
 
 // One chunk of create_transfers: events already at `ev` on the device.
@@ -278,6 +394,8 @@ static void run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
         std::fill(counts_host, counts_host + nb, 0u);
         return;
     }
+    if (!(c->opt.flags & TBGPU_OPT_FORCE_GENERAL) && try_fast(c, ev, n, nb, results_dev, counts_host)) return;
+    prof_mark(c, PH_CLASSIFY);
     HIP_CHECK(hipMemsetAsync(c->counters, 0, CNT_COUNT * sizeof(u32), s));
     HIP_CHECK(hipMemsetAsync(c->gclaim, 0, g * sizeof(u32), s));
     HIP_CHECK(hipMemsetAsync(c->gcnt_id, 0, g * sizeof(u32), s));
@@ -316,12 +434,15 @@ static void run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
             sort = c->h_counters[CNT_KEYS] != 0;
         }
         if (sort) {
+            prof_mark(c, PH_SORT);
             radix_sort_pairs(c->skey, c->sval, c->skey_s, c->sval_s, m, bits_acc, c->ss, s);
             tr_launch_side_pos(c->sval_s, m, c->spos, s);
             c->stats.sorts++;
         }
+        prof_mark(c, PH_SCAN);
         SA.ok = A->ok; SA.dpend = A->dpend; SA.dpost = A->dpost;
         side_scan(SA, m, inv_acc, chains, c->side_tiles, c->T.acc, c->bb, s);
+        prof_mark(c, PH_EVAL);
         HIP_CHECK(hipMemsetAsync(Bst->cfail, 0xFF, n * sizeof(u32), s));
         tr_launch_evaluate(c->T, C, *A, *Bst, c->spos, c->bb, s);
         read_counters(c);
@@ -331,6 +452,7 @@ static void run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
     c->stats.iterations = it + 1;
 
     // apply: ranks of stored rows / results / history rows
+    prof_mark(c, PH_APPLY);
     tr_launch_mask(c->T, C, *A, c->fres, c->mask, s);
     scan3_exclusive(c->mask, c->ranks, n, c->sc, s);
     uint4 tot;
@@ -341,6 +463,7 @@ static void run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
     SA.ok = A->ok; SA.dpend = A->dpend; SA.dpost = A->dpost;
     tr_launch_apply(c->T, C, *A, c->fres, c->ranks, c->spos, c->bb, c->n_rows, c->n_hist, results_dev, c->counts, s);
     side_final_balances(SA, m, inv_acc, c->bb, c->T.acc, s);
+    prof_mark(c, PH_END);
     HIP_CHECK(hipMemcpyAsync(counts_host, c->counts, nb * sizeof(u32), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     c->n_rows += tot.x;
@@ -356,9 +479,10 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
     u64 total = 0, ev_off = 0, events = 0;
     u32 iters = 0;
     u64 sorts = 0;
-    for (u32 b0 = 0; b0 < nb_total || (nb_total == 0 && false);) {
+    for (u32 b0 = 0; b0 < nb_total;) {
         const u32 b1 = chunk_end(c, counts, b0, nb_total);
         const u32 nb = b1 - b0;
+        prof_mark(c, PH_UPLOAD);
         upload_batches(c, timestamps + b0, counts + b0, nb, starts);
         const u32 n = starts[nb];
         const Transfer* ev;
@@ -369,19 +493,9 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
             ev = (const Transfer*)c->ev_buf;
         }
         tb_create_transfers_result_t* rdev =
-            dst_device ? results + ev_off : (tb_create_transfers_result_t*)c->res_buf;
+            dst_device ? results + total : (tb_create_transfers_result_t*)c->res_buf;
         run_transfers_chunk(c, ev, n, nb, rdev, result_counts + b0);
-        if (!dst_device) {
-            // copy each batch's results (they sit at the batch's event offset)
-            u64 bytes = 0;
-            for (u32 b = 0; b < nb; b++) {
-                if (result_counts[b0 + b] == 0) continue;
-                bytes = (u64)starts[b] * 8;
-                HIP_CHECK(hipMemcpyAsync((u8*)(results + ev_off) + bytes, c->res_buf + bytes,
-                                         (u64)result_counts[b0 + b] * 8, hipMemcpyDeviceToHost, c->stream));
-            }
-            HIP_CHECK(hipStreamSynchronize(c->stream));
-        }
+        if (!dst_device) copy_results_to_batches(c, nb, starts, result_counts + b0, (u8*)(results + ev_off));
         for (u32 b = 0; b < nb; b++) total += result_counts[b0 + b];
         iters = std::max(iters, c->stats.iterations);
         sorts += c->stats.sorts;
@@ -393,6 +507,7 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
     HIP_CHECK(hipEventSynchronize(c->ev1));
     float ms = 0;
     HIP_CHECK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    prof_collect(c);
     c->stats.events = events;
     c->stats.iterations = iters;
     c->stats.sorts = sorts;
@@ -486,14 +601,8 @@ extern "C" uint64_t tbgpu_create_accounts_batches(tbgpu_ctx* c, uint32_t nb_tota
         HIP_CHECK(hipMemcpyAsync(c->ev_buf, events + ev_off, (u64)n * 128, hipMemcpyHostToDevice, c->stream));
         run_accounts_chunk(c, (const Account*)c->ev_buf, n, nb, (tb_create_accounts_result_t*)c->res_buf,
                            result_counts + b0);
-        for (u32 b = 0; b < nb; b++) {
-            if (result_counts[b0 + b] == 0) continue;
-            const u64 off = (u64)starts[b] * 8;
-            HIP_CHECK(hipMemcpyAsync((u8*)(results + ev_off) + off, c->res_buf + off, (u64)result_counts[b0 + b] * 8,
-                                     hipMemcpyDeviceToHost, c->stream));
-            total += result_counts[b0 + b];
-        }
-        HIP_CHECK(hipStreamSynchronize(c->stream));
+        copy_results_to_batches(c, nb, starts, result_counts + b0, (u8*)(results + ev_off));
+        for (u32 b = 0; b < nb; b++) total += result_counts[b0 + b];
         ev_off += n;
         b0 = b1;
     }

@@ -1,0 +1,289 @@
+// fast.hip — single-pass create_transfers for balance-insensitive calls.
+//
+// When no event of a call can observe another event of the same call, the
+// sequential loop of `execute` (src/state_machine.zig:1018-1083) degenerates to
+// independent events: every result is decided by the pre-call state alone and
+// every account's final balance is its initial balance plus the sum of its
+// accepted deltas.  That holds when the call has
+//   - no linked chains (no scope rollback),
+//   - no post/void (no pending resolution) and no balancing transfers (no
+//     amount clamped from a running balance),
+//   - no account with debits/credits_must_not_exceed_* (no limit check) or
+//     history (no per-event balance snapshot),
+//   - no id committed twice (no intra-call `exists`),
+//   - no possible u128 overflow: amounts < 2^64 and the high words of every
+//     touched balance < 2^62, so no prefix sum of < 2^32 events can reach the
+//     overflow checks of :1308-1318.
+// Every event checks its own eligibility; one ineligible event flags the call
+// (FL_SLOW), its balance deltas are subtracted again (fp_undo, exact modular
+// inverse) and the call is redone by the general fixed-point path.
+//
+// fp_commit: classify + balance deltas (u64 atomics with carry) + decoupled
+// look-back rank of accepted events and failures + stored rows + replies.
+// fp_index:  publish the accepted ids in the transfer-id index.
+#include "common.h"
+#include "engine.h"
+#include "fast.h"
+
+namespace {
+
+constexpr int FP_THREADS = 256;
+constexpr u8 FRES_SLOW = 0xFE;
+constexpr u64 ST_AGG = 1ull << 62;
+constexpr u64 ST_INC = 2ull << 62;
+constexpr u64 ST_VAL = (1ull << 62) - 1;
+
+__device__ __forceinline__ u32 fp_batch_of(const u32* __restrict__ b_start, u32 nb, u32 i) {
+    u32 lo = 0, hi = nb;
+    while (hi - lo > 1) {
+        const u32 mid = (lo + hi) >> 1;
+        if (b_start[mid] <= i) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// u128 += a (a < 2^64) with u64 atomics: the carry out of the low word is exact
+// because each atomic returns the word it was applied to.
+__device__ __forceinline__ void atomic_add_u128_small(u128* p, u64 a) {
+    u64* w = (u64*)p;
+    const u64 old = atomicAdd((unsigned long long*)&w[0], (unsigned long long)a);
+    if (old + a < old) atomicAdd((unsigned long long*)&w[1], 1ull);
+}
+__device__ __forceinline__ void atomic_sub_u128_small(u128* p, u64 a) {
+    u64* w = (u64*)p;
+    const u64 old = atomicSub((unsigned long long*)&w[0], (unsigned long long)a);
+    if (old < a) atomicSub((unsigned long long*)&w[1], 1ull);
+}
+
+// Call-local duplicate detection: claims are (epoch << 32 | event + 1), so the
+// table never needs clearing between calls.
+__device__ __forceinline__ bool gtab_claim_is_dup(const FastArgs& F, u128 id, u32 i) {
+    const u64 mine = F.epoch | (u64)(i + 1);
+    u64 h = hash128(id) & F.gmask;
+    for (;;) {
+        u64 cur = __hip_atomic_load(&F.gtab[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((cur & 0xFFFFFFFF00000000ull) != F.epoch) {
+            const u64 prev = atomicCAS((unsigned long long*)&F.gtab[h], cur, mine);
+            if (prev == cur) return false;
+            cur = prev;
+            if ((cur & 0xFFFFFFFF00000000ull) != F.epoch) continue;  // raced with a stale slot: retry
+        }
+        const u32 other = (u32)cur - 1;
+        if (F.ev[other].id == id) return true;
+        h = (h + 1) & F.gmask;
+    }
+}
+
+// create_transfer_exists (src/state_machine.zig:1370-1389)
+__device__ __forceinline__ u8 fp_exists(const Transfer& t, const Transfer& e) {
+    if (t.flags != e.flags) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_FLAGS;
+    if (t.debit_account_id != e.debit_account_id) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_DEBIT_ACCOUNT_ID;
+    if (t.credit_account_id != e.credit_account_id) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_CREDIT_ACCOUNT_ID;
+    if (t.amount != e.amount) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_AMOUNT;
+    if (t.user_data_128 != e.user_data_128) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_128;
+    if (t.user_data_64 != e.user_data_64) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_64;
+    if (t.user_data_32 != e.user_data_32) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_32;
+    if (t.timeout != e.timeout) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_TIMEOUT;
+    if (t.code != e.code) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_CODE;
+    return TB_CREATE_TRANSFER_EXISTS;
+}
+
+// Result of one event against the pre-call state, or FRES_SLOW.
+__device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, const Transfer& t, u32 i, u64 ts,
+                                          u32* dslot_out, u32* cslot_out) {
+    const u16 f = t.flags;
+    if (f & TF_LINKED) return FRES_SLOW;  // linked chain
+    if (t.timestamp != 0) return TB_CREATE_TRANSFER_TIMESTAMP_MUST_BE_ZERO;
+    if (f & 0xFFC0u) return TB_CREATE_TRANSFER_RESERVED_FLAG;
+    if (t.id == 0) return TB_CREATE_TRANSFER_ID_MUST_NOT_BE_ZERO;
+    if (t.id == U128_MAX) return TB_CREATE_TRANSFER_ID_MUST_NOT_BE_INT_MAX;
+    if (f & (TF_POST | TF_VOID)) {
+        if ((f & TF_POST) && (f & TF_VOID)) return TB_CREATE_TRANSFER_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+        if (f & (TF_PENDING | TF_BDR | TF_BCR)) return TB_CREATE_TRANSFER_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+        if (t.pending_id == 0) return TB_CREATE_TRANSFER_PENDING_ID_MUST_NOT_BE_ZERO;
+        if (t.pending_id == U128_MAX) return TB_CREATE_TRANSFER_PENDING_ID_MUST_NOT_BE_INT_MAX;
+        if (t.pending_id == t.id) return TB_CREATE_TRANSFER_PENDING_ID_MUST_BE_DIFFERENT;
+        if (t.timeout != 0) return TB_CREATE_TRANSFER_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
+        return FRES_SLOW;  // resolves a pending transfer
+    }
+    if (t.debit_account_id == 0) return TB_CREATE_TRANSFER_DEBIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
+    if (t.debit_account_id == U128_MAX) return TB_CREATE_TRANSFER_DEBIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
+    if (t.credit_account_id == 0) return TB_CREATE_TRANSFER_CREDIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
+    if (t.credit_account_id == U128_MAX) return TB_CREATE_TRANSFER_CREDIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
+    if (t.credit_account_id == t.debit_account_id) return TB_CREATE_TRANSFER_ACCOUNTS_MUST_BE_DIFFERENT;
+    if (t.pending_id != 0) return TB_CREATE_TRANSFER_PENDING_ID_MUST_BE_ZERO;
+    if (!(f & TF_PENDING) && t.timeout != 0) return TB_CREATE_TRANSFER_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
+    if (!(f & (TF_BDR | TF_BCR)) && t.amount == 0) return TB_CREATE_TRANSFER_AMOUNT_MUST_NOT_BE_ZERO;
+    if (t.ledger == 0) return TB_CREATE_TRANSFER_LEDGER_MUST_NOT_BE_ZERO;
+    if (t.code == 0) return TB_CREATE_TRANSFER_CODE_MUST_NOT_BE_ZERO;
+    const u32 ds = acc_probe(T.acc, T.acc_mask, t.debit_account_id);
+    if (ds == NONE32) return TB_CREATE_TRANSFER_DEBIT_ACCOUNT_NOT_FOUND;
+    const u32 cs = acc_probe(T.acc, T.acc_mask, t.credit_account_id);
+    if (cs == NONE32) return TB_CREATE_TRANSFER_CREDIT_ACCOUNT_NOT_FOUND;
+    const Account& dr = T.acc[ds];
+    const Account& cr = T.acc[cs];
+    if (dr.ledger != cr.ledger) return TB_CREATE_TRANSFER_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
+    if (t.ledger != dr.ledger) return TB_CREATE_TRANSFER_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
+    if (f & (TF_BDR | TF_BCR)) return FRES_SLOW;                                  // balancing
+    if ((dr.flags | cr.flags) & (AF_DNEC | AF_CNED | AF_HISTORY)) return FRES_SLOW;  // limits / history
+    const u32 pre = xidx_probe(T.xidx, T.xidx_mask, t.id);
+    if (pre != NONE32) return fp_exists(t, T.xrows[pre]);
+    if (gtab_claim_is_dup(F, t.id, i)) return FRES_SLOW;                           // id repeats in the call
+    // overflow impossible: amount < 2^64 and the touched balances' high words < 2^62
+    const u64 lim = 1ull << 62;
+    if ((u64)(t.amount >> 64) != 0) return FRES_SLOW;
+    if ((u64)(dr.debits_pending >> 64) >= lim || (u64)(dr.debits_posted >> 64) >= lim) return FRES_SLOW;
+    if ((u64)(cr.credits_pending >> 64) >= lim || (u64)(cr.credits_posted >> 64) >= lim) return FRES_SLOW;
+    if (sum_overflows64(ts, (u64)t.timeout * NS_PER_S)) return TB_CREATE_TRANSFER_OVERFLOWS_TIMEOUT;
+    *dslot_out = ds;
+    *cslot_out = cs;
+    return TB_CREATE_TRANSFER_OK;
+}
+
+__global__ __launch_bounds__(FP_THREADS) void fp_commit(Tables T, FastArgs F) {
+    __shared__ u32 s_tile;
+    __shared__ u32 s_wok[FP_THREADS / 64], s_wbad[FP_THREADS / 64];
+    __shared__ u64 s_excl;
+    __shared__ u64 s_maxts[FP_THREADS / 64];
+    const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) s_tile = atomicAdd(F.tile_counter, 1u);
+    __syncthreads();
+    const u32 tile = s_tile;
+    const u32 i = tile * FP_THREADS + tid;
+    const bool valid = i < F.n;
+
+    Transfer t;
+    u8 r = FRES_SLOW;
+    u32 b = 0, ds = NONE32, cs = NONE32;
+    u64 ts = 0;
+    if (valid) {
+        b = fp_batch_of(F.b_start, F.nb, i);
+        const u32 bs = F.b_start[b], nbatch = F.b_start[b + 1] - bs;
+        ts = F.b_ts[b] - nbatch + (i - bs) + 1;
+        t = F.ev[i];
+        r = fp_classify(T, F, t, i, ts, &ds, &cs);
+        F.fres[i] = r;
+        if (r == TB_CREATE_TRANSFER_OK) {
+            const u64 a = (u64)t.amount;
+            if (t.flags & TF_PENDING) {
+                atomic_add_u128_small(&T.acc[ds].debits_pending, a);
+                atomic_add_u128_small(&T.acc[cs].credits_pending, a);
+            } else {
+                atomic_add_u128_small(&T.acc[ds].debits_posted, a);
+                atomic_add_u128_small(&T.acc[cs].credits_posted, a);
+            }
+        } else if (r == FRES_SLOW) {
+            atomicOr(&F.counters[CNT_FLAGS], (u32)FL_SLOW);
+        }
+    }
+    const bool ok = valid && r == TB_CREATE_TRANSFER_OK;
+    const bool bad = valid && r != TB_CREATE_TRANSFER_OK;
+
+    // rank accepted events (stored rows) and failures (replies) across the call
+    const u64 lt = __lanemask_lt();
+    const u64 okm = __ballot(ok), badm = __ballot(bad);
+    u64 mts = ok ? ts : 0;
+    for (int off = 32; off > 0; off >>= 1) mts = max(mts, (u64)__shfl_xor((unsigned long long)mts, off));
+    if (lane == 0) {
+        s_wok[wave] = __popcll(okm);
+        s_wbad[wave] = __popcll(badm);
+        s_maxts[wave] = mts;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        u64 agg_ok = 0, agg_bad = 0, maxts = 0;
+        for (int w = 0; w < FP_THREADS / 64; w++) {
+            agg_ok += s_wok[w];
+            agg_bad += s_wbad[w];
+            maxts = max(maxts, s_maxts[w]);
+        }
+        const u64 agg = agg_ok | (agg_bad << 31);
+        u64 excl = 0;
+        if (tile == 0) {
+            __hip_atomic_store(&F.tile_status[0], ST_INC | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(&F.tile_status[tile], ST_AGG | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            u32 j = tile - 1;
+            u32 spins = 0;
+            for (;;) {
+                const u64 s = __hip_atomic_load(&F.tile_status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((s & ~ST_VAL) == 0) {
+                    if (++spins > (1u << 26)) { atomicOr(&F.counters[CNT_FLAGS], (u32)FL_ERROR); break; }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                excl += s & ST_VAL;
+                if (s & ST_INC) break;
+                if (j == 0) break;
+                j--;
+            }
+            __hip_atomic_store(&F.tile_status[tile], ST_INC | (excl + agg), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_excl = excl;
+        if (agg_ok) {
+            atomicAdd(&F.counters[CNT_OK], (u32)agg_ok);
+            atomicMax((unsigned long long*)T.commit_ts, (unsigned long long)maxts);
+        }
+    }
+    __syncthreads();
+    const u64 excl = s_excl;
+    u32 wok = 0, wbad = 0;
+    for (u32 w = 0; w < wave; w++) { wok += s_wok[w]; wbad += s_wbad[w]; }
+    if (ok) {
+        const u64 row = F.row_base + (excl & 0x7FFFFFFFull) + wok + __popcll(okm & lt);
+        Transfer s = t;
+        s.timestamp = ts;
+        T.xrows[row] = s;  // speculative until fp_index publishes the id
+        F.keys[i] = t.id;
+        F.rows[i] = (u32)row;
+    } else if (valid) {
+        F.rows[i] = NONE32;
+        if (bad) {
+            const u64 pos = (excl >> 31) + wbad + __popcll(badm & lt);
+            F.results[pos] = {i - F.b_start[b], (u32)r};
+            atomicAdd(&F.batch_counts[b], 1u);
+        }
+    }
+}
+
+__global__ void fp_index(Tables T, FastArgs F) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= F.n) return;
+    if (F.counters[CNT_FLAGS] & (FL_SLOW | FL_ERROR)) return;
+    const u32 row = F.rows[i];
+    if (row != NONE32) xidx_insert(T.xidx, T.xidx_mask, F.keys[i], row);
+}
+
+// Exact inverse of fp_commit's balance deltas, before the general path redoes the call.
+__global__ void fp_undo(Tables T, FastArgs F) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= F.n) return;
+    if (F.fres[i] != TB_CREATE_TRANSFER_OK) return;
+    const Transfer& t = F.ev[i];
+    const u32 ds = acc_probe(T.acc, T.acc_mask, t.debit_account_id);
+    const u32 cs = acc_probe(T.acc, T.acc_mask, t.credit_account_id);
+    const u64 a = (u64)t.amount;
+    if (t.flags & TF_PENDING) {
+        atomic_sub_u128_small(&T.acc[ds].debits_pending, a);
+        atomic_sub_u128_small(&T.acc[cs].credits_pending, a);
+    } else {
+        atomic_sub_u128_small(&T.acc[ds].debits_posted, a);
+        atomic_sub_u128_small(&T.acc[cs].credits_posted, a);
+    }
+}
+
+}  // namespace
+
+void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream) {
+    fp_commit<<<(F.n + FP_THREADS - 1) / FP_THREADS, FP_THREADS, 0, stream>>>(T, F);
+    fp_index<<<(F.n + 255) / 256, 256, 0, stream>>>(T, F);
+    HIP_CHECK(hipGetLastError());
+}
+
+void fp_launch_undo(const Tables& T, const FastArgs& F, hipStream_t stream) {
+    fp_undo<<<(F.n + 255) / 256, 256, 0, stream>>>(T, F);
+    HIP_CHECK(hipGetLastError());
+}
+
+u64 fp_tiles(u64 n) { return (n + FP_THREADS - 1) / FP_THREADS; }

@@ -578,9 +578,9 @@ __global__ void tr_apply(Tables T, TrArgs C, EvalState S, const u8* __restrict__
     const u8 r = fres[i];
     const uint4 q = rk[i];
     if (r != 0) {
+        // replies of consecutive batches are concatenated: global non-ok rank
         const u32 b = batch_of(C.b_start, C.nb, i);
-        const u32 bs = C.b_start[b];
-        results[bs + (q.y - rk[bs].y)] = {i - bs, (u32)r};
+        results[q.y] = {i - C.b_start[b], (u32)r};
         return;
     }
     if (!(S.ok[i] & 2)) return;

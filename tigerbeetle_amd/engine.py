@@ -38,7 +38,9 @@ class Options(ctypes.Structure):
 
 class Stats(ctypes.Structure):
     _fields_ = [("events", ctypes.c_uint64), ("iterations", ctypes.c_uint32), ("path", ctypes.c_uint32),
-                ("sorts", ctypes.c_uint64), ("device_ms", ctypes.c_double)]
+                ("sorts", ctypes.c_uint64), ("device_ms", ctypes.c_double), ("phase_ms", ctypes.c_double * 8)]
+
+PHASES = ("upload", "classify", "sort", "scan", "evaluate", "apply")
 
 
 OPT_FORCE_GENERAL = 1
@@ -87,6 +89,7 @@ def lib():
     L.tbgpu_get_posted.restype = ctypes.c_int
     L.tbgpu_get_posted.argtypes = [vp, U128]
     L.tbgpu_last_stats.argtypes = [vp, ctypes.POINTER(Stats)]
+    L.tbgpu_set_profiling.argtypes = [vp, ctypes.c_int]
     L.tbgpu_last_error.restype = ctypes.c_int
     L.tbgpu_last_error.argtypes = [vp, ctypes.c_char_p, u32]
     _lib = L
@@ -220,6 +223,9 @@ class Engine:
 
     def get_posted(self, pending_id: int) -> int:
         return self._L.tbgpu_get_posted(self._h, u128(pending_id))
+
+    def set_profiling(self, enable: bool) -> None:
+        self._L.tbgpu_set_profiling(self._h, 1 if enable else 0)
 
     def stats(self) -> Stats:
         s = Stats()

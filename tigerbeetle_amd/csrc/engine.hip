@@ -159,7 +159,7 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     HIP_CHECK(hipHostMalloc((void**)&c->h_counters, CNT_COUNT * sizeof(u32), hipHostMallocDefault));
 }
 
-enum { PH_UPLOAD = 0, PH_CLASSIFY = 1, PH_SORT = 2, PH_SCAN = 3, PH_EVAL = 4, PH_APPLY = 5, PH_END = -1 };
+enum { PH_UPLOAD = 0, PH_CLASSIFY = 1, PH_SORT = 2, PH_SCAN = 3, PH_EVAL = 4, PH_APPLY = 5, PH_INDEX = 6, PH_PREP = 7, PH_END = -1 };
 
 static void prof_mark(tbgpu_ctx* c, int phase) {
     if (!c->prof) return;
@@ -355,12 +355,15 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tb_create_
     F.keys = c->f_keys;
     F.rows = c->f_rows;
     if (c->n_rows + n > c->xrow_cap) return false;  // let the general path report capacity exactly
-    prof_mark(c, PH_CLASSIFY);
+    prof_mark(c, PH_PREP);
     HIP_CHECK(hipMemsetAsync(c->counters, 0, CNT_COUNT * sizeof(u32), s));
     HIP_CHECK(hipMemsetAsync(c->f_tiles, 0, fp_tiles(n) * sizeof(u64), s));
     HIP_CHECK(hipMemsetAsync(c->f_tile_counter, 0, sizeof(u32), s));
     HIP_CHECK(hipMemsetAsync(c->counts, 0, nb * sizeof(u32), s));
+    prof_mark(c, PH_CLASSIFY);
     fp_launch_commit(c->T, F, s);
+    prof_mark(c, PH_INDEX);
+    fp_launch_index(c->T, F, s);
     prof_mark(c, PH_END);
     read_counters(c);
     const u32 flags = c->h_counters[CNT_FLAGS];

@@ -23,5 +23,6 @@ struct FastArgs {
 };
 
 void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream);
+void fp_launch_index(const Tables& T, const FastArgs& F, hipStream_t stream);
 void fp_launch_undo(const Tables& T, const FastArgs& F, hipStream_t stream);
 u64 fp_tiles(u64 n);

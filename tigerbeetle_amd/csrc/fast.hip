@@ -27,7 +27,9 @@
 
 namespace {
 
-constexpr int FP_THREADS = 256;
+constexpr int FP_THREADS = 1024;  // one event per thread, one tile per workgroup
+constexpr int AGG_SLOTS = 4096;   // LDS aggregation table (>= 2x the 2048 sides of a tile)
+constexpr u32 AGG_EMPTY = 0xFFFFFFFFu;
 constexpr u8 FRES_SLOW = 0xFE;
 constexpr u64 ST_AGG = 1ull << 62;
 constexpr u64 ST_INC = 2ull << 62;
@@ -42,13 +44,6 @@ __device__ __forceinline__ u32 fp_batch_of(const u32* __restrict__ b_start, u32 
     return lo;
 }
 
-// u128 += a (a < 2^64) with u64 atomics: the carry out of the low word is exact
-// because each atomic returns the word it was applied to.
-__device__ __forceinline__ void atomic_add_u128_small(u128* p, u64 a) {
-    u64* w = (u64*)p;
-    const u64 old = atomicAdd((unsigned long long*)&w[0], (unsigned long long)a);
-    if (old + a < old) atomicAdd((unsigned long long*)&w[1], 1ull);
-}
 __device__ __forceinline__ void atomic_sub_u128_small(u128* p, u64 a) {
     u64* w = (u64*)p;
     const u64 old = atomicSub((unsigned long long*)&w[0], (unsigned long long)a);
@@ -140,13 +135,44 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
     return TB_CREATE_TRANSFER_OK;
 }
 
+// Balance field of an account row: 0 debits_pending, 1 debits_posted,
+// 2 credits_pending, 3 credits_posted (offsets 16, 32, 48, 64).
+__device__ __forceinline__ u128* acc_field(const Tables& T, u32 key) {
+    return &(&T.acc[key >> 2].debits_pending)[key & 3];
+}
+
+// Add `a` to the tile's LDS partial sum for `key` (= slot * 4 + field).  Sums
+// are 64-bit with a carry counter, so no precision is lost.
+__device__ __forceinline__ void agg_add(u32* keys, u64* sums, u32* carries, u32 key, u64 a) {
+    u32 h = (u32)(mix64(key) & (AGG_SLOTS - 1));
+    for (;;) {
+        u32 k = keys[h];
+        if (k == AGG_EMPTY) {
+            k = atomicCAS(&keys[h], AGG_EMPTY, key);
+            if (k == AGG_EMPTY) k = key;
+        }
+        if (k == key) break;
+        h = (h + 1) & (AGG_SLOTS - 1);
+    }
+    const u64 old = atomicAdd((unsigned long long*)&sums[h], (unsigned long long)a);
+    if (old + a < old) atomicAdd(&carries[h], 1u);
+}
+
 __global__ __launch_bounds__(FP_THREADS) void fp_commit(Tables T, FastArgs F) {
     __shared__ u32 s_tile;
     __shared__ u32 s_wok[FP_THREADS / 64], s_wbad[FP_THREADS / 64];
     __shared__ u64 s_excl;
     __shared__ u64 s_maxts[FP_THREADS / 64];
+    __shared__ u32 s_keys[AGG_SLOTS];
+    __shared__ u64 s_sums[AGG_SLOTS];
+    __shared__ u32 s_carry[AGG_SLOTS];
     const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid == 0) s_tile = atomicAdd(F.tile_counter, 1u);
+    for (u32 h = tid; h < AGG_SLOTS; h += FP_THREADS) {
+        s_keys[h] = AGG_EMPTY;
+        s_sums[h] = 0;
+        s_carry[h] = 0;
+    }
     __syncthreads();
     const u32 tile = s_tile;
     const u32 i = tile * FP_THREADS + tid;
@@ -164,20 +190,28 @@ __global__ __launch_bounds__(FP_THREADS) void fp_commit(Tables T, FastArgs F) {
         r = fp_classify(T, F, t, i, ts, &ds, &cs);
         F.fres[i] = r;
         if (r == TB_CREATE_TRANSFER_OK) {
+            // tile-local aggregation first: a hot account costs one global atomic per tile
             const u64 a = (u64)t.amount;
-            if (t.flags & TF_PENDING) {
-                atomic_add_u128_small(&T.acc[ds].debits_pending, a);
-                atomic_add_u128_small(&T.acc[cs].credits_pending, a);
-            } else {
-                atomic_add_u128_small(&T.acc[ds].debits_posted, a);
-                atomic_add_u128_small(&T.acc[cs].credits_posted, a);
-            }
+            const u32 pend = (t.flags & TF_PENDING) ? 0u : 1u;
+            agg_add(s_keys, s_sums, s_carry, ds * 4 + pend, a);
+            agg_add(s_keys, s_sums, s_carry, cs * 4 + 2 + pend, a);
         } else if (r == FRES_SLOW) {
             atomicOr(&F.counters[CNT_FLAGS], (u32)FL_SLOW);
         }
     }
     const bool ok = valid && r == TB_CREATE_TRANSFER_OK;
     const bool bad = valid && r != TB_CREATE_TRANSFER_OK;
+    __syncthreads();
+    // flush the tile's partial sums: u128 += (carry:sum) with u64 atomics
+    for (u32 h = tid; h < AGG_SLOTS; h += FP_THREADS) {
+        const u32 key = s_keys[h];
+        if (key == AGG_EMPTY) continue;
+        u64* w = (u64*)acc_field(T, key);
+        const u64 a = s_sums[h];
+        const u64 old = atomicAdd((unsigned long long*)&w[0], (unsigned long long)a);
+        const u64 c = (u64)s_carry[h] + (old + a < old ? 1 : 0);
+        if (c) atomicAdd((unsigned long long*)&w[1], (unsigned long long)c);
+    }
 
     // rank accepted events (stored rows) and failures (replies) across the call
     const u64 lt = __lanemask_lt();
@@ -277,6 +311,10 @@ __global__ void fp_undo(Tables T, FastArgs F) {
 
 void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream) {
     fp_commit<<<(F.n + FP_THREADS - 1) / FP_THREADS, FP_THREADS, 0, stream>>>(T, F);
+    HIP_CHECK(hipGetLastError());
+}
+
+void fp_launch_index(const Tables& T, const FastArgs& F, hipStream_t stream) {
     fp_index<<<(F.n + 255) / 256, 256, 0, stream>>>(T, F);
     HIP_CHECK(hipGetLastError());
 }

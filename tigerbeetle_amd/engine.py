@@ -40,7 +40,7 @@ class Stats(ctypes.Structure):
     _fields_ = [("events", ctypes.c_uint64), ("iterations", ctypes.c_uint32), ("path", ctypes.c_uint32),
                 ("sorts", ctypes.c_uint64), ("device_ms", ctypes.c_double), ("phase_ms", ctypes.c_double * 8)]
 
-PHASES = ("upload", "classify", "sort", "scan", "evaluate", "apply")
+PHASES = ("upload", "classify", "sort", "scan", "evaluate", "apply", "index", "prep")
 
 
 OPT_FORCE_GENERAL = 1

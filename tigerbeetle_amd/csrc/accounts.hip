@@ -238,6 +238,9 @@ __global__ void k_set_balances(Tables T, u128 id, Bal4 b, int* status) {
     a.debits_posted = b.dpo;
     a.credits_pending = b.cp;
     a.credits_posted = b.cpo;
+    const u64 lim = 1ull << 62;
+    if ((u64)(b.dp >> 64) >= lim || (u64)(b.dpo >> 64) >= lim || (u64)(b.cp >> 64) >= lim || (u64)(b.cpo >> 64) >= lim)
+        atomicOr(T.big, 1u);
     *status = 0;
 }
 __global__ void k_get_posted(Tables T, u128 id, int* status) {

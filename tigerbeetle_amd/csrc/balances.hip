@@ -172,7 +172,8 @@ __global__ __launch_bounds__(BS_THREADS) void bs_down(SideScanArgs A, u64 m, u32
 
 // After convergence: the last side of each account segment writes the account's
 // final balances: before(q) minus the in-chain H part, plus its own final delta.
-__global__ void bs_final(SideScanArgs A, u64 m, u32 invalid, const Bal4* __restrict__ bb, Account* __restrict__ acc) {
+__global__ void bs_final(SideScanArgs A, u64 m, u32 invalid, const Bal4* __restrict__ bb, Account* __restrict__ acc,
+                         u32* big) {
     const u64 q = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= m) return;
     const u32 key = A.skey[q];
@@ -201,6 +202,10 @@ __global__ void bs_final(SideScanArgs A, u64 m, u32 invalid, const Bal4* __restr
     a.debits_posted = tot.dpo;
     a.credits_pending = tot.cp;
     a.credits_posted = tot.cpo;
+    const u64 lim = 1ull << 62;
+    if ((u64)(tot.dp >> 64) >= lim || (u64)(tot.dpo >> 64) >= lim || (u64)(tot.cp >> 64) >= lim ||
+        (u64)(tot.cpo >> 64) >= lim)
+        atomicOr(big, 1u);
 }
 
 }  // namespace
@@ -224,8 +229,9 @@ void side_scan(const SideScanArgs& A, u64 m, u32 invalid, bool has_chains, void*
     HIP_CHECK(hipGetLastError());
 }
 
-void side_final_balances(const SideScanArgs& A, u64 m, u32 invalid, const Bal4* bb, Account* acc, hipStream_t stream) {
+void side_final_balances(const SideScanArgs& A, u64 m, u32 invalid, const Bal4* bb, Account* acc, u32* big,
+                         hipStream_t stream) {
     if (m == 0) return;
-    bs_final<<<(u32)((m + 255) / 256), 256, 0, stream>>>(A, m, invalid, bb, acc);
+    bs_final<<<(u32)((m + 255) / 256), 256, 0, stream>>>(A, m, invalid, bb, acc, big);
     HIP_CHECK(hipGetLastError());
 }

@@ -13,7 +13,27 @@ struct Tables {
     u64 xidx_mask;
     History* hrows;    // account-history groove rows, append-only
     u64* commit_ts;    // device copy of StateMachine.commit_timestamp (atomicMax)
+    // Componentwise range of the ids in xidx: [0] max lo, [1] max hi, [2] min lo,
+    // [3] min hi.  An id outside it is absent without a probe (the LSM key-range
+    // short-circuit of src/lsm/tree.zig:289-300, why sequential ids are cheap).
+    u64* idr;
+    // Set once any balance high word reaches 2^62: until then a call of < 2^32
+    // events with amounts < 2^64 cannot overflow a u128 sum (fast.hip).
+    u32* big;
 };
+
+__device__ __forceinline__ bool xidx_maybe_present(const Tables& T, u128 id) {
+    const u64 lo = (u64)id, hi = (u64)(id >> 64);
+    return lo <= T.idr[0] && hi <= T.idr[1] && lo >= T.idr[2] && hi >= T.idr[3];
+}
+
+__device__ __forceinline__ void xidx_range_add(const Tables& T, u128 id) {
+    const u64 lo = (u64)id, hi = (u64)(id >> 64);
+    atomicMax((unsigned long long*)&T.idr[0], (unsigned long long)lo);
+    atomicMax((unsigned long long*)&T.idr[1], (unsigned long long)hi);
+    atomicMin((unsigned long long*)&T.idr[2], (unsigned long long)lo);
+    atomicMin((unsigned long long*)&T.idr[3], (unsigned long long)hi);
+}
 
 // One double-buffered fixed-point state (see transfers.hip).
 struct EvalState {
@@ -39,7 +59,8 @@ struct SideScanArgs {
 u64 side_scan_tile_bytes(u64 capacity);
 void side_scan(const SideScanArgs& A, u64 m, u32 invalid, bool has_chains, void* tile_scratch, const Account* acc,
                Bal4* bb, hipStream_t stream);
-void side_final_balances(const SideScanArgs& A, u64 m, u32 invalid, const Bal4* bb, Account* acc, hipStream_t stream);
+void side_final_balances(const SideScanArgs& A, u64 m, u32 invalid, const Bal4* bb, Account* acc, u32* big,
+                         hipStream_t stream);
 
 // Device probes shared by the kernels.
 __device__ __forceinline__ u32 acc_probe(const Account* __restrict__ acc, u64 mask, u128 id) {

@@ -91,6 +91,7 @@ struct tbgpu_ctx {
     u32* f_tile_counter = nullptr;
     u128* f_keys = nullptr;
     u32* f_rows = nullptr;
+    u64* f_tile_idr = nullptr;
     hipEvent_t ev0, ev1;
     // phase profiler: consecutive marks on the ctx stream; segment k belongs to
     // the phase opened by mark k.
@@ -156,6 +157,7 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->f_tile_counter = dalloc<u32>(4, &B);
     c->f_keys = dalloc<u128>(n, &B);
     c->f_rows = dalloc<u32>(n, &B);
+    c->f_tile_idr = dalloc<u64>(4 * (fp_tiles(nmax) + 1), &B);
     HIP_CHECK(hipHostMalloc((void**)&c->h_counters, CNT_COUNT * sizeof(u32), hipHostMallocDefault));
 }
 
@@ -227,6 +229,8 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     c->T.xidx_mask = c->xidx_cap - 1;
     c->T.hrows = dalloc<History>(c->hist_cap, &B);
     c->T.commit_ts = dalloc<u64>(2, &B);
+    c->T.idr = dalloc<u64>(4, &B);
+    c->T.big = dalloc<u32>(4, &B);
     alloc_scratch(c, o.events_per_call_max);
     tbgpu_reset(c);
     *out = c;
@@ -239,6 +243,9 @@ extern "C" void tbgpu_reset(tbgpu_ctx* c) {
     HIP_CHECK(hipMemsetAsync(c->T.xful, 0, c->xrow_cap, c->stream));
     HIP_CHECK(hipMemsetAsync(c->T.xidx, 0, c->xidx_cap * sizeof(IdSlot), c->stream));
     HIP_CHECK(hipMemsetAsync(c->T.commit_ts, 0, 2 * sizeof(u64), c->stream));
+    HIP_CHECK(hipMemsetAsync(c->T.idr, 0, 2 * sizeof(u64), c->stream));                  // max = 0
+    HIP_CHECK(hipMemsetAsync(c->T.idr + 2, 0xFF, 2 * sizeof(u64), c->stream));           // min = ~0
+    HIP_CHECK(hipMemsetAsync(c->T.big, 0, sizeof(u32), c->stream));
     HIP_CHECK(hipStreamSynchronize(c->stream));
     c->n_accounts = c->n_rows = c->n_hist = 0;
 }
@@ -248,13 +255,13 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     // Free every device allocation by walking the struct's pointers.
-    void* ptrs[] = {c->T.acc, c->T.xrows, c->T.xful, c->T.xidx, c->T.hrows, c->T.commit_ts, c->ev_buf,
+    void* ptrs[] = {c->T.acc, c->T.xrows, c->T.xful, c->T.xidx, c->T.hrows, c->T.commit_ts, c->T.idr, c->T.big, c->ev_buf,
                     c->b_start, c->b_ts, c->ts, c->cs, c->ce, c->sres, c->dslot, c->cslot, c->pre_e, c->pre_p,
                     c->pp_dslot, c->pp_cslot, c->gslot, c->pslot, c->prev_id, c->pend_last, c->prev_pend,
                     c->gclaim, c->gcnt_id, c->gcnt_pd, c->gmem, c->gbeg, c->gend, c->skey, c->sval, c->skey_s,
                     c->sval_s, c->spos, c->bb, c->ss.keys_tmp, c->ss.vals_tmp, c->ss.hist, c->side_tiles,
                     c->sc.tile_sums, c->fres, c->mask, c->ranks, c->res_buf, c->counts, c->counters, c->status,
-                    c->f_gtab, c->f_tiles, c->f_tile_counter, c->f_keys, c->f_rows};
+                    c->f_gtab, c->f_tiles, c->f_tile_counter, c->f_keys, c->f_rows, c->f_tile_idr};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     for (EvalState& s : c->st) {
         void* q[] = {s.res, s.ok, s.pref, s.cfail, s.amt, s.pamt, s.dpend, s.dpost};
@@ -354,6 +361,7 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tb_create_
     F.row_base = c->n_rows;
     F.keys = c->f_keys;
     F.rows = c->f_rows;
+    F.tile_idr = c->f_tile_idr;
     if (c->n_rows + n > c->xrow_cap) return false;  // let the general path report capacity exactly
     prof_mark(c, PH_PREP);
     HIP_CHECK(hipMemsetAsync(c->counters, 0, CNT_COUNT * sizeof(u32), s));
@@ -465,7 +473,7 @@ static void run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
     if (c->n_hist + tot.z > c->hist_cap) tbgpu_fatal("create_transfers", "history_max exceeded", __FILE__, __LINE__);
     SA.ok = A->ok; SA.dpend = A->dpend; SA.dpost = A->dpost;
     tr_launch_apply(c->T, C, *A, c->fres, c->ranks, c->spos, c->bb, c->n_rows, c->n_hist, results_dev, c->counts, s);
-    side_final_balances(SA, m, inv_acc, c->bb, c->T.acc, s);
+    side_final_balances(SA, m, inv_acc, c->bb, c->T.acc, c->T.big, s);
     prof_mark(c, PH_END);
     HIP_CHECK(hipMemcpyAsync(counts_host, c->counts, nb * sizeof(u32), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));

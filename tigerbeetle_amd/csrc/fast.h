@@ -20,6 +20,7 @@ struct FastArgs {
     u64 row_base;
     u128* keys;         // accepted ids, for fp_index
     u32* rows;          // stored row per event or NONE32
+    u64* tile_idr;      // per tile: componentwise max lo, max hi, min lo, min hi of accepted ids
 };
 
 void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream);

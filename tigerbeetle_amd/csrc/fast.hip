@@ -27,8 +27,8 @@
 
 namespace {
 
-constexpr int FP_THREADS = 1024;  // one event per thread, one tile per workgroup
-constexpr int AGG_SLOTS = 4096;   // LDS aggregation table (>= 2x the 2048 sides of a tile)
+constexpr int FP_THREADS = 512;   // one event per thread, one tile per workgroup (2 per CU)
+constexpr int AGG_SLOTS = 2048;   // LDS aggregation table (>= 2x the 1024 sides of a tile)
 constexpr u32 AGG_EMPTY = 0xFFFFFFFFu;
 constexpr u8 FRES_SLOW = 0xFE;
 constexpr u64 ST_AGG = 1ull << 62;
@@ -83,9 +83,97 @@ __device__ __forceinline__ u8 fp_exists(const Transfer& t, const Transfer& e) {
     return TB_CREATE_TRANSFER_EXISTS;
 }
 
-// Result of one event against the pre-call state, or FRES_SLOW.
+// Continue an account probe after a first-slot miss.
+__device__ __forceinline__ u32 acc_probe_from(const Tables& T, u64 h, u128 id) {
+    for (;;) {
+        h = (h + 1) & T.acc_mask;
+        const Account& a = T.acc[h];
+        if (a.timestamp == 0) return NONE32;
+        if (a.id == id) return (u32)h;
+    }
+}
+
+__device__ __forceinline__ u32 xidx_probe_from(const Tables& T, u64 h, u128 id) {
+    const u64 lo = (u64)id, hi = (u64)(id >> 64);
+    for (;;) {
+        h = (h + 1) & T.xidx_mask;
+        const IdSlot& s = T.xidx[h];
+        if (s.ref == 0) return NONE32;
+        if (s.key_lo == lo && s.key_hi == hi) return (u32)(s.ref - 1);
+    }
+}
+
+__device__ __forceinline__ u8 fp_classify_guarded(const Tables& T, const FastArgs& F, const Transfer& t, u32 i,
+                                                  u64 ts, u32* dslot_out, u32* cslot_out);
+
+// Result of one event against the pre-call state, or FRES_SLOW.  The debit and
+// credit account rows, the transfer-id slot and the duplicate claim are all
+// issued before any of them is consumed (they are independent; only the
+// precedence of the resulting checks is ordered), so one event costs about one
+// memory round trip instead of four.
 __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, const Transfer& t, u32 i, u64 ts,
                                           u32* dslot_out, u32* cslot_out) {
+    const u16 f = t.flags;
+    if (f & (TF_LINKED | TF_BDR | TF_BCR | TF_POST | TF_VOID) || *T.big)
+        return fp_classify_guarded(T, F, t, i, ts, dslot_out, cslot_out);
+    // speculative first-slot reads (hash tables at load <= 0.5: usually the hit)
+    const u64 hd = hash128(t.debit_account_id) & T.acc_mask;
+    const u64 hc = hash128(t.credit_account_id) & T.acc_mask;
+    const Account& A = T.acc[hd];
+    const Account& B = T.acc[hc];
+    const u64 a_ts = A.timestamp, b_ts = B.timestamp;
+    const u128 a_id = A.id, b_id = B.id;
+    const bool maybe = xidx_maybe_present(T, t.id);
+    const u64 hx = hash128(t.id) & T.xidx_mask;
+    u64 x_ref = 0, x_lo = 0, x_hi = 0;
+    if (maybe) {
+        x_ref = T.xidx[hx].ref;
+        x_lo = T.xidx[hx].key_lo;
+        x_hi = T.xidx[hx].key_hi;
+    }
+    const bool plausible = t.id != 0 && t.id != U128_MAX;
+    const bool dup = plausible && gtab_claim_is_dup(F, t.id, i);  // a false positive only costs the slow path
+    if (t.timestamp != 0) return TB_CREATE_TRANSFER_TIMESTAMP_MUST_BE_ZERO;
+    if (f & 0xFFC0u) return TB_CREATE_TRANSFER_RESERVED_FLAG;
+    if (t.id == 0) return TB_CREATE_TRANSFER_ID_MUST_NOT_BE_ZERO;
+    if (t.id == U128_MAX) return TB_CREATE_TRANSFER_ID_MUST_NOT_BE_INT_MAX;
+    if (t.debit_account_id == 0) return TB_CREATE_TRANSFER_DEBIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
+    if (t.debit_account_id == U128_MAX) return TB_CREATE_TRANSFER_DEBIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
+    if (t.credit_account_id == 0) return TB_CREATE_TRANSFER_CREDIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
+    if (t.credit_account_id == U128_MAX) return TB_CREATE_TRANSFER_CREDIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
+    if (t.credit_account_id == t.debit_account_id) return TB_CREATE_TRANSFER_ACCOUNTS_MUST_BE_DIFFERENT;
+    if (t.pending_id != 0) return TB_CREATE_TRANSFER_PENDING_ID_MUST_BE_ZERO;
+    if (!(f & TF_PENDING) && t.timeout != 0) return TB_CREATE_TRANSFER_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
+    if (t.amount == 0) return TB_CREATE_TRANSFER_AMOUNT_MUST_NOT_BE_ZERO;
+    if (t.ledger == 0) return TB_CREATE_TRANSFER_LEDGER_MUST_NOT_BE_ZERO;
+    if (t.code == 0) return TB_CREATE_TRANSFER_CODE_MUST_NOT_BE_ZERO;
+    const u32 ds = a_ts == 0 ? NONE32 : (a_id == t.debit_account_id ? (u32)hd : acc_probe_from(T, hd, t.debit_account_id));
+    if (ds == NONE32) return TB_CREATE_TRANSFER_DEBIT_ACCOUNT_NOT_FOUND;
+    const u32 cs = b_ts == 0 ? NONE32 : (b_id == t.credit_account_id ? (u32)hc : acc_probe_from(T, hc, t.credit_account_id));
+    if (cs == NONE32) return TB_CREATE_TRANSFER_CREDIT_ACCOUNT_NOT_FOUND;
+    const Account& dr = T.acc[ds];
+    const Account& cr = T.acc[cs];
+    if (dr.ledger != cr.ledger) return TB_CREATE_TRANSFER_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
+    if (t.ledger != dr.ledger) return TB_CREATE_TRANSFER_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
+    if ((dr.flags | cr.flags) & (AF_DNEC | AF_CNED | AF_HISTORY)) return FRES_SLOW;  // limits / history
+    if (maybe && x_ref != 0) {
+        const u32 pre = (x_lo == (u64)t.id && x_hi == (u64)(t.id >> 64)) ? (u32)(x_ref - 1)
+                                                                          : xidx_probe_from(T, hx, t.id);
+        if (pre != NONE32) return fp_exists(t, T.xrows[pre]);
+    }
+    if (dup) return FRES_SLOW;  // the id repeats in the call
+    // u128 overflow is impossible: amount < 2^64, balances < 2^126 (T.big clear), < 2^32 events
+    if ((u64)(t.amount >> 64) != 0) return FRES_SLOW;
+    if (sum_overflows64(ts, (u64)t.timeout * NS_PER_S)) return TB_CREATE_TRANSFER_OVERFLOWS_TIMEOUT;
+    *dslot_out = ds;
+    *cslot_out = cs;
+    return TB_CREATE_TRANSFER_OK;
+}
+
+// The static checks that precede what makes an event ineligible (their results
+// are exact); otherwise FRES_SLOW.
+__device__ __forceinline__ u8 fp_classify_guarded(const Tables& T, const FastArgs& F, const Transfer& t, u32 i,
+                                                       u64 ts, u32* dslot_out, u32* cslot_out) {
     const u16 f = t.flags;
     if (f & TF_LINKED) return FRES_SLOW;  // linked chain
     if (t.timestamp != 0) return TB_CREATE_TRANSFER_TIMESTAMP_MUST_BE_ZERO;
@@ -163,6 +251,7 @@ __global__ __launch_bounds__(FP_THREADS) void fp_commit(Tables T, FastArgs F) {
     __shared__ u32 s_wok[FP_THREADS / 64], s_wbad[FP_THREADS / 64];
     __shared__ u64 s_excl;
     __shared__ u64 s_maxts[FP_THREADS / 64];
+    __shared__ u64 s_idr[FP_THREADS / 64][4];
     __shared__ u32 s_keys[AGG_SLOTS];
     __shared__ u64 s_sums[AGG_SLOTS];
     __shared__ u32 s_carry[AGG_SLOTS];
@@ -201,17 +290,6 @@ __global__ __launch_bounds__(FP_THREADS) void fp_commit(Tables T, FastArgs F) {
     }
     const bool ok = valid && r == TB_CREATE_TRANSFER_OK;
     const bool bad = valid && r != TB_CREATE_TRANSFER_OK;
-    __syncthreads();
-    // flush the tile's partial sums: u128 += (carry:sum) with u64 atomics
-    for (u32 h = tid; h < AGG_SLOTS; h += FP_THREADS) {
-        const u32 key = s_keys[h];
-        if (key == AGG_EMPTY) continue;
-        u64* w = (u64*)acc_field(T, key);
-        const u64 a = s_sums[h];
-        const u64 old = atomicAdd((unsigned long long*)&w[0], (unsigned long long)a);
-        const u64 c = (u64)s_carry[h] + (old + a < old ? 1 : 0);
-        if (c) atomicAdd((unsigned long long*)&w[1], (unsigned long long)c);
-    }
 
     // rank accepted events (stored rows) and failures (replies) across the call
     const u64 lt = __lanemask_lt();
@@ -223,41 +301,97 @@ __global__ __launch_bounds__(FP_THREADS) void fp_commit(Tables T, FastArgs F) {
         s_wbad[wave] = __popcll(badm);
         s_maxts[wave] = mts;
     }
-    __syncthreads();
-    if (tid == 0) {
-        u64 agg_ok = 0, agg_bad = 0, maxts = 0;
+    // componentwise id range of the tile's accepted ids (for the index key-range filter)
+    {
+        u64 mxl = ok ? (u64)t.id : 0, mxh = ok ? (u64)(t.id >> 64) : 0;
+        u64 mnl = ok ? (u64)t.id : ~0ull, mnh = ok ? (u64)(t.id >> 64) : ~0ull;
+        for (int off = 32; off > 0; off >>= 1) {
+            mxl = max(mxl, (u64)__shfl_xor((unsigned long long)mxl, off));
+            mxh = max(mxh, (u64)__shfl_xor((unsigned long long)mxh, off));
+            mnl = min(mnl, (u64)__shfl_xor((unsigned long long)mnl, off));
+            mnh = min(mnh, (u64)__shfl_xor((unsigned long long)mnh, off));
+        }
+        if (lane == 0) {
+            s_idr[wave][0] = mxl;
+            s_idr[wave][1] = mxh;
+            s_idr[wave][2] = mnl;
+            s_idr[wave][3] = mnh;
+        }
+    }
+    __syncthreads();  // LDS sums and per-wave counts complete
+    u64 agg_ok = 0, agg_bad = 0, maxts = 0;
+    if (wave == 0) {
         for (int w = 0; w < FP_THREADS / 64; w++) {
             agg_ok += s_wok[w];
             agg_bad += s_wbad[w];
             maxts = max(maxts, s_maxts[w]);
         }
+        // publish this tile's aggregate before anything else, so successors can pass it
+        if (lane == 0)
+            __hip_atomic_store(&F.tile_status[tile], (tile == 0 ? ST_INC : ST_AGG) | agg_ok | (agg_bad << 31),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane < 4) {
+            u64 v = s_idr[0][lane];
+            for (int w = 1; w < FP_THREADS / 64; w++) v = lane < 2 ? max(v, s_idr[w][lane]) : min(v, s_idr[w][lane]);
+            F.tile_idr[4 * tile + lane] = v;
+        }
+    }
+    // flush the tile's partial sums: u128 += (carry:sum) with u64 atomics
+    for (u32 h = tid; h < AGG_SLOTS; h += FP_THREADS) {
+        const u32 key = s_keys[h];
+        if (key == AGG_EMPTY) continue;
+        u64* w = (u64*)acc_field(T, key);
+        const u64 a = s_sums[h];
+        const u64 old = atomicAdd((unsigned long long*)&w[0], (unsigned long long)a);
+        const u64 c = (u64)s_carry[h] + (old + a < old ? 1 : 0);
+        if (c) {
+            const u64 hi = atomicAdd((unsigned long long*)&w[1], (unsigned long long)c);
+            if (hi + c >= (1ull << 62)) atomicOr(T.big, 1u);  // later calls must prove no overflow
+        }
+    }
+    if (wave == 0) {
+        // decoupled look-back, 64 predecessors per step (lane l reads tile top - l)
         const u64 agg = agg_ok | (agg_bad << 31);
         u64 excl = 0;
-        if (tile == 0) {
-            __hip_atomic_store(&F.tile_status[0], ST_INC | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(&F.tile_status[tile], ST_AGG | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            u32 j = tile - 1;
-            u32 spins = 0;
-            for (;;) {
-                const u64 s = __hip_atomic_load(&F.tile_status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((s & ~ST_VAL) == 0) {
-                    if (++spins > (1u << 26)) { atomicOr(&F.counters[CNT_FLAGS], (u32)FL_ERROR); break; }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
+        if (tile > 0) {
+            long long top = (long long)tile - 1;
+            for (bool done = false; !done;) {
+                const long long j = top - lane;
+                u64 st = ST_INC;  // before tile 0: an inclusive prefix of zero
+                if (j >= 0) {
+                    u32 spins = 0;
+                    for (;;) {
+                        st = __hip_atomic_load(&F.tile_status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (st & ~ST_VAL) break;
+                        if (++spins > (1u << 24)) {
+                            atomicOr(&F.counters[CNT_FLAGS], (u32)FL_ERROR);
+                            st = ST_INC;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
                 }
-                excl += s & ST_VAL;
-                if (s & ST_INC) break;
-                if (j == 0) break;
-                j--;
+                const u64 incm = __ballot((st & ST_INC) != 0);
+                u32 take = 64;
+                if (incm) {
+                    take = (u32)__ffsll((unsigned long long)incm);  // nearest inclusive predecessor
+                    done = true;
+                }
+                u64 v = lane < take ? (st & ST_VAL) : 0;
+                for (int off = 32; off > 0; off >>= 1) v += (u64)__shfl_xor((unsigned long long)v, off);
+                excl += v;
+                top -= 64;
             }
-            __hip_atomic_store(&F.tile_status[tile], ST_INC | (excl + agg), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0)
+                __hip_atomic_store(&F.tile_status[tile], ST_INC | (excl + agg), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
-        s_excl = excl;
-        if (agg_ok) {
-            atomicAdd(&F.counters[CNT_OK], (u32)agg_ok);
-            atomicMax((unsigned long long*)T.commit_ts, (unsigned long long)maxts);
+        if (lane == 0) {
+            s_excl = excl;
+            if (agg_ok) {
+                atomicAdd(&F.counters[CNT_OK], (u32)agg_ok);
+                atomicMax((unsigned long long*)T.commit_ts, (unsigned long long)maxts);
+            }
         }
     }
     __syncthreads();
@@ -282,9 +416,32 @@ __global__ __launch_bounds__(FP_THREADS) void fp_commit(Tables T, FastArgs F) {
 }
 
 __global__ void fp_index(Tables T, FastArgs F) {
-    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= F.n) return;
     if (F.counters[CNT_FLAGS] & (FL_SLOW | FL_ERROR)) return;
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x < 64) {
+        // fold the tiles' id ranges into the index's key range (one wave)
+        const u32 lane = threadIdx.x, ntiles = (F.n + FP_THREADS - 1) / FP_THREADS;
+        u64 r[4] = {0, 0, ~0ull, ~0ull};
+        for (u32 k = lane; k < ntiles; k += 64) {
+            r[0] = max(r[0], F.tile_idr[4 * k + 0]);
+            r[1] = max(r[1], F.tile_idr[4 * k + 1]);
+            r[2] = min(r[2], F.tile_idr[4 * k + 2]);
+            r[3] = min(r[3], F.tile_idr[4 * k + 3]);
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            r[0] = max(r[0], (u64)__shfl_xor((unsigned long long)r[0], off));
+            r[1] = max(r[1], (u64)__shfl_xor((unsigned long long)r[1], off));
+            r[2] = min(r[2], (u64)__shfl_xor((unsigned long long)r[2], off));
+            r[3] = min(r[3], (u64)__shfl_xor((unsigned long long)r[3], off));
+        }
+        if (lane == 0) {
+            atomicMax((unsigned long long*)&T.idr[0], (unsigned long long)r[0]);
+            atomicMax((unsigned long long*)&T.idr[1], (unsigned long long)r[1]);
+            atomicMin((unsigned long long*)&T.idr[2], (unsigned long long)r[2]);
+            atomicMin((unsigned long long*)&T.idr[3], (unsigned long long)r[3]);
+        }
+    }
+    if (i >= F.n) return;
     const u32 row = F.rows[i];
     if (row != NONE32) xidx_insert(T.xidx, T.xidx_mask, F.keys[i], row);
 }

@@ -619,6 +619,27 @@ __global__ void tr_apply(Tables T, TrArgs C, EvalState S, const u8* __restrict__
     }
 }
 
+// Widen the index's componentwise key range by the stored ids (one atomic per
+// wave and word; every lane of every wave takes part).
+__global__ void tr_range(Tables T, TrArgs C, EvalState S) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool ok = i < C.n && (S.ok[i] & 2);
+    const u128 id = ok ? C.ev[i].id : 0;
+    u64 r[4] = {ok ? (u64)id : 0, ok ? (u64)(id >> 64) : 0, ok ? (u64)id : ~0ull, ok ? (u64)(id >> 64) : ~0ull};
+    for (int off = 32; off > 0; off >>= 1) {
+        r[0] = max(r[0], (u64)__shfl_xor((unsigned long long)r[0], off));
+        r[1] = max(r[1], (u64)__shfl_xor((unsigned long long)r[1], off));
+        r[2] = min(r[2], (u64)__shfl_xor((unsigned long long)r[2], off));
+        r[3] = min(r[3], (u64)__shfl_xor((unsigned long long)r[3], off));
+    }
+    if ((threadIdx.x & 63) == 0 && r[0] | r[1] | ~r[2] | ~r[3]) {
+        atomicMax((unsigned long long*)&T.idr[0], (unsigned long long)r[0]);
+        atomicMax((unsigned long long*)&T.idr[1], (unsigned long long)r[1]);
+        atomicMin((unsigned long long*)&T.idr[2], (unsigned long long)r[2]);
+        atomicMin((unsigned long long*)&T.idr[3], (unsigned long long)r[3]);
+    }
+}
+
 __global__ void batch_counts(const u32* b_start, u32 nb, const uint4* rk, u32* counts) {
     const u32 b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b < nb) counts[b] = rk[b_start[b + 1]].y - rk[b_start[b]].y;
@@ -663,5 +684,6 @@ void tr_launch_apply(const Tables& T, const TrArgs& C, const EvalState& S, const
                      const u32* spos, const Bal4* bb, u64 row_base, u64 hist_base,
                      tb_create_transfers_result_t* results, u32* counts, hipStream_t stream) {
     tr_apply<<<GRID(C.n)>>>(T, C, S, fres, rk, spos, bb, row_base, hist_base, results);
+    tr_range<<<GRID(C.n)>>>(T, C, S);
     batch_counts<<<GRID(C.nb)>>>(C.b_start, C.nb, rk, counts);
 }

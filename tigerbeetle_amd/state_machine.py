@@ -1,0 +1,64 @@
+"""Host-side mirror of the reference ``StateMachine`` interface for the hot path.
+
+The reference replica drives its state machine through ``prepare`` / ``prefetch`` /
+``commit`` (src/state_machine.zig:503-928).  This class keeps those names, argument
+meanings and reply format, and routes create_accounts / create_transfers and the two
+lookups to the HIP engine (libtbgpu.so).  Inputs and outputs are raw message bodies
+(``bytes`` of 128-byte events / 8-byte results), exactly like the reference.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .engine import Engine
+from .types import ACCOUNT_DTYPE, RESULT_DTYPE, TRANSFER_DTYPE, U128_DTYPE, Operation
+
+MESSAGE_BODY_SIZE_MAX = (1 << 20) - 256  # constants.message_body_size_max (src/constants.zig:204)
+
+
+class StateMachine:
+    """``StateMachineType(Storage, config)`` for the operations this engine owns."""
+
+    Operation = Operation
+
+    def __init__(self, engine: Engine | None = None, **engine_options):
+        self.engine = engine or Engine(**engine_options)
+        self.prepare_timestamp = 0
+        self.commit_timestamp = 0
+
+    # src/state_machine.zig:503-512
+    def prepare(self, operation: Operation, input: bytes) -> None:
+        if operation in (Operation.create_accounts, Operation.create_transfers):
+            self.prepare_timestamp += len(input) // 128
+
+    # src/state_machine.zig:514-576 — the HBM tables need no prefetch; the callback
+    # still runs (the reference delivers it asynchronously via the grid's next tick).
+    def prefetch(self, callback, op: int, operation: Operation, input: bytes) -> None:
+        callback(self)
+
+    # src/state_machine.zig:894-928
+    def commit(self, client: int, op: int, timestamp: int, operation: Operation, input: bytes) -> bytes:
+        assert op != 0
+        assert timestamp > self.commit_timestamp
+        if operation == Operation.create_accounts:
+            events = np.frombuffer(input, dtype=ACCOUNT_DTYPE)
+            out = self.engine.create_accounts(timestamp, events)
+        elif operation == Operation.create_transfers:
+            events = np.frombuffer(input, dtype=TRANSFER_DTYPE)
+            out = self.engine.create_transfers(timestamp, events)
+        elif operation == Operation.lookup_accounts:
+            ids = np.frombuffer(input, dtype=U128_DTYPE)
+            out = self.engine.lookup_accounts([(int(x["hi"]) << 64) | int(x["lo"]) for x in ids])
+            out = out[:MESSAGE_BODY_SIZE_MAX // 128]
+        elif operation == Operation.lookup_transfers:
+            ids = np.frombuffer(input, dtype=U128_DTYPE)
+            out = self.engine.lookup_transfers([(int(x["hi"]) << 64) | int(x["lo"]) for x in ids])
+            out = out[:MESSAGE_BODY_SIZE_MAX // 128]
+        else:
+            raise NotImplementedError(f"{operation.name} is not served by the GPU engine (SURVEY.md §8f)")
+        self.commit_timestamp = max(self.commit_timestamp, self.engine.commit_timestamp())
+        return out.tobytes()
+
+    @staticmethod
+    def results(reply: bytes) -> np.ndarray:
+        return np.frombuffer(reply, dtype=RESULT_DTYPE)

@@ -1,0 +1,23 @@
+"""Timing-only ablation of the fast-path kernel (cdna_hip_programming.md §7, step 2).
+
+Runs the bench workload once per TBGPU_ABLATE mask in fresh processes and prints
+the per-phase device time; results of ablated runs are wrong by construction.
+"""
+import json
+import os
+import subprocess
+import sys
+
+MASKS = {"full": 0, "no-dup": 1, "no-balances": 2, "no-rows": 4, "no-lookback": 8,
+         "no-dup+bal+rows+lb": 15}
+args = sys.argv[1:] or ["--steps", "5", "--warmup", "1", "--batches-per-step", "100", "--no-cpu"]
+for name, m in MASKS.items():
+    env = dict(os.environ, TBGPU_ABLATE=str(m))
+    r = subprocess.run([sys.executable, "bench.py", *args], env=env, capture_output=True, text=True)
+    try:
+        line = json.loads(r.stdout.strip().splitlines()[-1])
+        ph = line["roofline"]["phase_ms_per_step"]
+        print(f"{name:22s} value={line['value']/1e9:6.3f} G/s  commit={ph['classify']:.4f} ms  "
+              f"index={ph['index']:.4f} ms  step={line['ms_per_step']:.4f} ms", flush=True)
+    except Exception:
+        print(name, "failed", r.stderr[-500:], flush=True)

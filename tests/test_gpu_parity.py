@@ -134,3 +134,19 @@ commit lookup_accounts
         check(gpu, text)
     finally:
         gpu.close()
+
+
+def test_random_id_order():
+    """Ids in random order (benchmark --id-order=random): the fast path must run its
+    in-call duplicate check and still match the oracle, with and without repeats."""
+    w = workload.config1(transfer_count=40_000, account_count=700, seed=13)
+    rng = np.random.default_rng(1)
+    t = w.transfers.copy()
+    t["id_lo"] = rng.permutation(t["id_lo"])
+    w.transfers = t
+    st = _parity(w)
+    assert st.path == 1
+    t2 = t.copy()
+    t2[30_000]["id_lo"] = t2[29_999]["id_lo"]  # a repeat inside the last call
+    w.transfers = t2
+    _parity(w)

@@ -117,4 +117,5 @@ enum {
     FL_HISTORY = 1u << 7,     // an account with flags.history is touched
     FL_SLOW = 1u << 8,        // fast path: some event needs the fixed point
     FL_ERROR = 1u << 9,       // device-side protocol error (bounded spin expired)
+    FL_NONMONO = 1u << 10,    // fast path: ids of the call are not strictly increasing
 };

@@ -84,9 +84,9 @@ struct tbgpu_ctx {
     int* status = nullptr;
     u32* h_counters = nullptr;  // pinned
     // fast path (fast.hip)
-    u64* f_gtab = nullptr;
+    u32* f_gtab = nullptr;
+    u32* f_gpos = nullptr;
     u64 f_gcap = 0;
-    u32 f_epoch = 0;
     u64* f_tiles = nullptr;
     u32* f_tile_counter = nullptr;
     u128* f_keys = nullptr;
@@ -151,8 +151,9 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->counters = dalloc<u32>(CNT_COUNT, &B);
     c->status = dalloc<int>(4, &B);
     c->f_gcap = pow2_at_least(2 * nmax);
-    c->f_gtab = dalloc<u64>(c->f_gcap, &B);
-    HIP_CHECK(hipMemset(c->f_gtab, 0, c->f_gcap * sizeof(u64)));
+    c->f_gtab = dalloc<u32>(c->f_gcap, &B);
+    HIP_CHECK(hipMemset(c->f_gtab, 0, c->f_gcap * sizeof(u32)));
+    c->f_gpos = dalloc<u32>(n, &B);
     c->f_tiles = dalloc<u64>(fp_tiles(nmax) + 1, &B);
     c->f_tile_counter = dalloc<u32>(4, &B);
     c->f_keys = dalloc<u128>(n, &B);
@@ -261,7 +262,8 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
                     c->gclaim, c->gcnt_id, c->gcnt_pd, c->gmem, c->gbeg, c->gend, c->skey, c->sval, c->skey_s,
                     c->sval_s, c->spos, c->bb, c->ss.keys_tmp, c->ss.vals_tmp, c->ss.hist, c->side_tiles,
                     c->sc.tile_sums, c->fres, c->mask, c->ranks, c->res_buf, c->counts, c->counters, c->status,
-                    c->f_gtab, c->f_tiles, c->f_tile_counter, c->f_keys, c->f_rows, c->f_tile_idr};
+                    c->f_gtab, c->f_gpos, c->f_tiles, c->f_tile_counter, c->f_keys, c->f_rows,
+                    c->f_tile_idr};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     for (EvalState& s : c->st) {
         void* q[] = {s.res, s.ok, s.pref, s.cfail, s.amt, s.pamt, s.dpend, s.dpost};
@@ -343,15 +345,11 @@ static TrArgs make_tr_args(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb) {
 static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tb_create_transfers_result_t* results_dev,
                      u32* counts_host) {
     hipStream_t s = c->stream;
-    if (++c->f_epoch == 0) {  // epoch wrapped: clear the claim table once
-        HIP_CHECK(hipMemsetAsync(c->f_gtab, 0, c->f_gcap * sizeof(u64), s));
-        c->f_epoch = 1;
-    }
     FastArgs F{};
     F.ev = ev; F.n = n; F.nb = nb; F.b_start = c->b_start; F.b_ts = c->b_ts;
     F.gtab = c->f_gtab;
+    F.gpos = c->f_gpos;
     F.gmask = std::min<u64>(c->f_gcap, pow2_at_least(2ull * n)) - 1;
-    F.epoch = (u64)c->f_epoch << 32;
     F.fres = c->fres;
     F.counters = c->counters;
     F.tile_status = c->f_tiles;
@@ -362,6 +360,11 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tb_create_
     F.keys = c->f_keys;
     F.rows = c->f_rows;
     F.tile_idr = c->f_tile_idr;
+    static const u32 ablate = [] {  // timing-only ablation (profiles/ablate.py); never set in production
+        const char* e = getenv("TBGPU_ABLATE");
+        return e ? (u32)strtoul(e, nullptr, 0) : 0u;
+    }();
+    F.ablate = ablate;
     if (c->n_rows + n > c->xrow_cap) return false;  // let the general path report capacity exactly
     prof_mark(c, PH_PREP);
     HIP_CHECK(hipMemsetAsync(c->counters, 0, CNT_COUNT * sizeof(u32), s));

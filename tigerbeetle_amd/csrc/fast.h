@@ -8,9 +8,9 @@ struct FastArgs {
     u32 nb;
     const u32* b_start;
     const u64* b_ts;
-    u64* gtab;          // epoch-tagged duplicate-id claims
+    u32* gtab;          // duplicate-id claims (event + 1), all-zero between calls
+    u32* gpos;          // slot each event claimed (cleared again by fp_index)
     u64 gmask;
-    u64 epoch;          // (call epoch) << 32, never 0
     u8* fres;           // per-event result (0 = accepted, deltas applied)
     u32* counters;
     u64* tile_status;   // decoupled look-back: [flag:2 | failures:31 | accepted:31]
@@ -21,7 +21,9 @@ struct FastArgs {
     u128* keys;         // accepted ids, for fp_index
     u32* rows;          // stored row per event or NONE32
     u64* tile_idr;      // per tile: componentwise max lo, max hi, min lo, min hi of accepted ids
+    u32 ablate;         // timing-only builds (TBGPU_ABLATE): skip parts of the work; results wrong
 };
+enum { ABL_DUP = 1, ABL_BALANCES = 2, ABL_ROWS = 4, ABL_LOOKBACK = 8, ABL_EVENT = 16 };
 
 void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream);
 void fp_launch_index(const Tables& T, const FastArgs& F, hipStream_t stream);

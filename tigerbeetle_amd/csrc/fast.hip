@@ -50,21 +50,23 @@ __device__ __forceinline__ void atomic_sub_u128_small(u128* p, u64 a) {
     if (old < a) atomicSub((unsigned long long*)&w[1], 1ull);
 }
 
-// Call-local duplicate detection: claims are (epoch << 32 | event + 1), so the
-// table never needs clearing between calls.
+// Call-local duplicate detection among accepted ids (only run when the call's ids
+// are not strictly increasing).  Linear probing with claims (event + 1) placed in
+// the first empty slot: a later claimant of the same id meets the earlier claim
+// before any empty slot.  Every claimed slot is cleared again by fp_index, so the
+// table is all-zero at the start of each call.
 __device__ __forceinline__ bool gtab_claim_is_dup(const FastArgs& F, u128 id, u32 i) {
-    const u64 mine = F.epoch | (u64)(i + 1);
     u64 h = hash128(id) & F.gmask;
     for (;;) {
-        u64 cur = __hip_atomic_load(&F.gtab[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((cur & 0xFFFFFFFF00000000ull) != F.epoch) {
-            const u64 prev = atomicCAS((unsigned long long*)&F.gtab[h], cur, mine);
-            if (prev == cur) return false;
-            cur = prev;
-            if ((cur & 0xFFFFFFFF00000000ull) != F.epoch) continue;  // raced with a stale slot: retry
+        const u32 prev = atomicCAS(&F.gtab[h], 0u, i + 1);
+        if (prev == 0) {
+            F.gpos[i] = (u32)h;
+            return false;
         }
-        const u32 other = (u32)cur - 1;
-        if (F.ev[other].id == id) return true;
+        if (F.keys[prev - 1] == id) {
+            F.gpos[i] = NONE32;
+            return true;
+        }
         h = (h + 1) & F.gmask;
     }
 }
@@ -131,8 +133,6 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
         x_lo = T.xidx[hx].key_lo;
         x_hi = T.xidx[hx].key_hi;
     }
-    const bool plausible = t.id != 0 && t.id != U128_MAX;
-    const bool dup = plausible && gtab_claim_is_dup(F, t.id, i);  // a false positive only costs the slow path
     if (t.timestamp != 0) return TB_CREATE_TRANSFER_TIMESTAMP_MUST_BE_ZERO;
     if (f & 0xFFC0u) return TB_CREATE_TRANSFER_RESERVED_FLAG;
     if (t.id == 0) return TB_CREATE_TRANSFER_ID_MUST_NOT_BE_ZERO;
@@ -161,7 +161,7 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
                                                                           : xidx_probe_from(T, hx, t.id);
         if (pre != NONE32) return fp_exists(t, T.xrows[pre]);
     }
-    if (dup) return FRES_SLOW;  // the id repeats in the call
+    // an id repeated within the call is caught by fp_dupcheck (only when ids are not increasing)
     // u128 overflow is impossible: amount < 2^64, balances < 2^126 (T.big clear), < 2^32 events
     if ((u64)(t.amount >> 64) != 0) return FRES_SLOW;
     if (sum_overflows64(ts, (u64)t.timeout * NS_PER_S)) return TB_CREATE_TRANSFER_OVERFLOWS_TIMEOUT;
@@ -282,14 +282,34 @@ __global__ __launch_bounds__(FP_THREADS) void fp_commit(Tables T, FastArgs F) {
             // tile-local aggregation first: a hot account costs one global atomic per tile
             const u64 a = (u64)t.amount;
             const u32 pend = (t.flags & TF_PENDING) ? 0u : 1u;
-            agg_add(s_keys, s_sums, s_carry, ds * 4 + pend, a);
-            agg_add(s_keys, s_sums, s_carry, cs * 4 + 2 + pend, a);
+            if (!(F.ablate & ABL_BALANCES)) {
+                agg_add(s_keys, s_sums, s_carry, ds * 4 + pend, a);
+                agg_add(s_keys, s_sums, s_carry, cs * 4 + 2 + pend, a);
+            }
         } else if (r == FRES_SLOW) {
             atomicOr(&F.counters[CNT_FLAGS], (u32)FL_SLOW);
         }
     }
     const bool ok = valid && r == TB_CREATE_TRANSFER_OK;
     const bool bad = valid && r != TB_CREATE_TRANSFER_OK;
+
+    // Strictly increasing ids across the whole call cannot repeat: then fp_dupcheck
+    // has nothing to do (sequential ids, the benchmark's default id order).
+    {
+        const u64 lo = valid ? (u64)t.id : ~0ull, hi = valid ? (u64)(t.id >> 64) : ~0ull;
+        u64 plo = __shfl_up((unsigned long long)lo, 1), phi = __shfl_up((unsigned long long)hi, 1);
+        if (lane == 0) {
+            if (i > 0 && valid) {
+                const u128 p = F.ev[i - 1].id;
+                plo = (u64)p;
+                phi = (u64)(p >> 64);
+            } else {
+                plo = phi = 0;
+            }
+        }
+        const bool up = !valid || i == 0 || hi > phi || (hi == phi && lo > plo);
+        if (__ballot(!up) && lane == 0) atomicOr(&F.counters[CNT_FLAGS], (u32)FL_NONMONO);
+    }
 
     // rank accepted events (stored rows) and failures (replies) across the call
     const u64 lt = __lanemask_lt();
@@ -336,24 +356,40 @@ __global__ __launch_bounds__(FP_THREADS) void fp_commit(Tables T, FastArgs F) {
             F.tile_idr[4 * tile + lane] = v;
         }
     }
-    // flush the tile's partial sums: u128 += (carry:sum) with u64 atomics
-    for (u32 h = tid; h < AGG_SLOTS; h += FP_THREADS) {
-        const u32 key = s_keys[h];
-        if (key == AGG_EMPTY) continue;
-        u64* w = (u64*)acc_field(T, key);
-        const u64 a = s_sums[h];
-        const u64 old = atomicAdd((unsigned long long*)&w[0], (unsigned long long)a);
-        const u64 c = (u64)s_carry[h] + (old + a < old ? 1 : 0);
-        if (c) {
-            const u64 hi = atomicAdd((unsigned long long*)&w[1], (unsigned long long)c);
-            if (hi + c >= (1ull << 62)) atomicOr(T.big, 1u);  // later calls must prove no overflow
+    // flush the tile's partial sums: u128 += (carry:sum) with u64 atomics.  All of a
+    // thread's low-word atomics are issued before any returns (memory-level
+    // parallelism); the rare carries follow.
+    {
+        constexpr int PER = AGG_SLOTS / FP_THREADS;
+        u64* wp[PER];
+        u64 av[PER], old[PER];
+        u32 cv[PER];
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const u32 h = tid + k * FP_THREADS;
+            const u32 key = s_keys[h];
+            wp[k] = key == AGG_EMPTY ? nullptr : (u64*)acc_field(T, key);
+            av[k] = s_sums[h];
+            cv[k] = s_carry[h];
+        }
+#pragma unroll
+        for (int k = 0; k < PER; k++)
+            old[k] = wp[k] ? atomicAdd((unsigned long long*)&wp[k][0], (unsigned long long)av[k]) : 0;
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            if (!wp[k]) continue;
+            const u64 c = (u64)cv[k] + (old[k] + av[k] < old[k] ? 1 : 0);
+            if (c) {
+                const u64 hi = atomicAdd((unsigned long long*)&wp[k][1], (unsigned long long)c);
+                if (hi + c >= (1ull << 62)) atomicOr(T.big, 1u);  // later calls must prove no overflow
+            }
         }
     }
     if (wave == 0) {
         // decoupled look-back, 64 predecessors per step (lane l reads tile top - l)
         const u64 agg = agg_ok | (agg_bad << 31);
         u64 excl = 0;
-        if (tile > 0) {
+        if (tile > 0 && !(F.ablate & ABL_LOOKBACK)) {
             long long top = (long long)tile - 1;
             for (bool done = false; !done;) {
                 const long long j = top - lane;
@@ -402,7 +438,7 @@ __global__ __launch_bounds__(FP_THREADS) void fp_commit(Tables T, FastArgs F) {
         const u64 row = F.row_base + (excl & 0x7FFFFFFFull) + wok + __popcll(okm & lt);
         Transfer s = t;
         s.timestamp = ts;
-        T.xrows[row] = s;  // speculative until fp_index publishes the id
+        if (!(F.ablate & ABL_ROWS)) T.xrows[row] = s;  // speculative until fp_index publishes the id
         F.keys[i] = t.id;
         F.rows[i] = (u32)row;
     } else if (valid) {
@@ -415,9 +451,26 @@ __global__ __launch_bounds__(FP_THREADS) void fp_commit(Tables T, FastArgs F) {
     }
 }
 
-__global__ void fp_index(Tables T, FastArgs F) {
-    if (F.counters[CNT_FLAGS] & (FL_SLOW | FL_ERROR)) return;
+// Only when the call's ids were not increasing: claim every accepted id once.
+__global__ void fp_dupcheck(Tables T, FastArgs F) {
+    // Every event records its claim (or NONE) so fp_index can clear the table.
+    if (!(F.counters[CNT_FLAGS] & FL_NONMONO)) return;
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= F.n) return;
+    F.gpos[i] = NONE32;
+    if (F.rows[i] == NONE32) return;
+    if (gtab_claim_is_dup(F, F.keys[i], i)) atomicOr(&F.counters[CNT_FLAGS], (u32)FL_SLOW);
+}
+
+__global__ void fp_index(Tables T, FastArgs F) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    const u32 flags = F.counters[CNT_FLAGS];
+    if ((flags & FL_NONMONO) && i < F.n) {
+        // leave the claim table all-zero for the next call (also when falling back)
+        const u32 g = F.gpos[i];
+        if (g != NONE32) F.gtab[g] = 0;
+    }
+    if (flags & (FL_SLOW | FL_ERROR)) return;
     if (blockIdx.x == 0 && threadIdx.x < 64) {
         // fold the tiles' id ranges into the index's key range (one wave)
         const u32 lane = threadIdx.x, ntiles = (F.n + FP_THREADS - 1) / FP_THREADS;
@@ -472,6 +525,7 @@ void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream) {
 }
 
 void fp_launch_index(const Tables& T, const FastArgs& F, hipStream_t stream) {
+    fp_dupcheck<<<(F.n + 255) / 256, 256, 0, stream>>>(T, F);
     fp_index<<<(F.n + 255) / 256, 256, 0, stream>>>(T, F);
     HIP_CHECK(hipGetLastError());
 }

@@ -68,7 +68,7 @@ __global__ void ac_classify(Tables T, AcArgs C) {
     else if (a.code == 0) sres = TB_CREATE_ACCOUNT_CODE_MUST_NOT_BE_ZERO;
     else {
         sres = SRES_DYN;
-        pre = acc_probe(T.acc, T.acc_mask, a.id);
+        pre = acc_probe(T.aidx, T.aidx_mask, a.id);
         gslot = ac_gtab_insert(C, a.id, i);
         atomicAdd(&C.gcnt_id[gslot], 1u);
     }
@@ -173,7 +173,7 @@ __global__ void ac_mask(AcArgs C, const u8* res, const u8* ok, const u32* cfail,
         atomicMax((unsigned long long*)commit_ts, (unsigned long long)C.ts[i]);
 }
 
-__global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const uint4* rk,
+__global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const uint4* rk, u64 row_base,
                          tb_create_accounts_result_t* results) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= C.n) return;
@@ -187,27 +187,18 @@ __global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const
     if (!(ok[i] & 2)) return;
     Account a = C.ev[i];
     a.timestamp = C.ts[i];
-    // accounts.insert: claim an empty slot by its timestamp word, then publish.
-    u64 h = hash128(a.id) & T.acc_mask;
-    for (;;) {
-        unsigned long long prev =
-            atomicCAS((unsigned long long*)&T.acc[h].timestamp, 0ull, (unsigned long long)a.timestamp);
-        if (prev == 0) break;
-        h = (h + 1) & T.acc_mask;
-    }
-    Account& dst = T.acc[h];
-    dst.id = a.id;
-    dst.debits_pending = a.debits_pending;
-    dst.debits_posted = a.debits_posted;
-    dst.credits_pending = a.credits_pending;
-    dst.credits_posted = a.credits_posted;
-    dst.user_data_128 = a.user_data_128;
-    dst.user_data_64 = a.user_data_64;
-    dst.user_data_32 = a.user_data_32;
-    dst.reserved = a.reserved;
-    dst.ledger = a.ledger;
-    dst.code = a.code;
-    dst.flags = a.flags;
+    // accounts.insert: the row is the event's rank among the persisted accounts
+    // (creation order); the index slot is claimed by CAS on its row word.
+    const u32 row = (u32)(row_base + rk[i].x);
+    T.acc[row] = a;
+    u64 h = hash128(a.id) & T.aidx_mask;
+    while (atomicCAS(&T.aidx[h].row1, 0u, row + 1) != 0) h = (h + 1) & T.aidx_mask;
+    AccIdx& e = T.aidx[h];
+    e.id_lo = (u64)a.id;
+    e.id_hi = (u64)(a.id >> 64);
+    e.ledger = a.ledger;
+    e.flags = a.flags;
+    e.code = a.code;
 }
 
 __global__ void ac_batch_counts(const u32* b_start, u32 nb, const uint4* rk, u32* counts) {
@@ -219,19 +210,19 @@ __global__ void ac_batch_counts(const u32* b_start, u32 nb, const uint4* rk, u32
 __global__ void k_lookup_accounts(Tables T, const u128* ids, u32 n, Account* out, u8* found) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const u32 s = acc_probe(T.acc, T.acc_mask, ids[i]);
+    const u32 s = acc_probe(T.aidx, T.aidx_mask, ids[i]);
     found[i] = s != NONE32;
     if (s != NONE32) out[i] = T.acc[s];
 }
 __global__ void k_lookup_transfers(Tables T, const u128* ids, u32 n, Transfer* out, u8* found) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const u32 r = xidx_probe(T.xidx, T.xidx_mask, ids[i]);
+    const u32 r = xidx_probe(T, ids[i]);
     found[i] = r != NONE32;
     if (r != NONE32) out[i] = T.xrows[r];
 }
 __global__ void k_set_balances(Tables T, u128 id, Bal4 b, int* status) {
-    const u32 s = acc_probe(T.acc, T.acc_mask, id);
+    const u32 s = acc_probe(T.aidx, T.aidx_mask, id);
     if (s == NONE32) { *status = -1; return; }
     Account& a = T.acc[s];
     a.debits_pending = b.dp;
@@ -244,7 +235,7 @@ __global__ void k_set_balances(Tables T, u128 id, Bal4 b, int* status) {
     *status = 0;
 }
 __global__ void k_get_posted(Tables T, u128 id, int* status) {
-    const u32 r = xidx_probe(T.xidx, T.xidx_mask, id);
+    const u32 r = xidx_probe(T, id);
     if (r == NONE32) { *status = -1; return; }
     const u8 f = T.xful[r];
     *status = f == 0 ? -1 : (f == 1 ? 0 : 1);
@@ -277,9 +268,9 @@ void ac_launch_mask(const Tables& T, const AcArgs& C, const u8* res, const u8* o
                     u8* mask, hipStream_t stream) {
     ac_mask<<<GRID(C.n)>>>(C, res, ok, cfail, fres, mask, T.commit_ts);
 }
-void ac_launch_apply(const Tables& T, const AcArgs& C, const u8* ok, const u8* fres, const uint4* rk,
+void ac_launch_apply(const Tables& T, const AcArgs& C, const u8* ok, const u8* fres, const uint4* rk, u64 row_base,
                      tb_create_accounts_result_t* results, u32* counts, hipStream_t stream) {
-    ac_apply<<<GRID(C.n)>>>(T, C, ok, fres, rk, results);
+    ac_apply<<<GRID(C.n)>>>(T, C, ok, fres, rk, row_base, results);
     ac_batch_counts<<<GRID(C.nb)>>>(C.b_start, C.nb, rk, counts);
 }
 void launch_lookup_accounts(const Tables& T, const u128* ids, u32 n, Account* out, u8* found, hipStream_t stream) {

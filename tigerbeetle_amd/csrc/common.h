@@ -46,13 +46,6 @@ static_assert(sizeof(History) == 256, "History layout");
 static_assert(sizeof(Account) == sizeof(tb_account_t), "ABI");
 static_assert(sizeof(Transfer) == sizeof(tb_transfer_t), "ABI");
 
-// Transfer-id index slot: u128 key + row reference (row + 1; 0 = empty).
-struct alignas(32) IdSlot {
-    u64 key_lo, key_hi;
-    u64 ref;
-    u64 pad;
-};
-
 // Four balances of an account (the scan state).
 struct Bal4 {
     u128 dp, dpo, cp, cpo;

@@ -2,14 +2,30 @@
 #pragma once
 #include "common.h"
 
+// Account id index entry: 32 bytes, so the index of 1M accounts (at load 0.5)
+// is 64 MB and stays resident in the 256 MB Infinity Cache while the 128-byte
+// rows live densely elsewhere.  ledger and flags are immutable after
+// create_account, so the state-independent checks of create_transfer
+// (src/state_machine.zig:1273-1281) never touch the row.
+struct alignas(32) AccIdx {
+    u64 id_lo, id_hi;
+    u32 row1;    // dense row + 1; 0 = empty slot
+    u32 ledger;
+    u16 flags;
+    u16 code;
+    u32 pad;
+};
+static_assert(sizeof(AccIdx) == 32, "AccIdx layout");
+
 // HBM-resident state owned by a ctx (replaces the grooves' object caches and
 // LSM trees for the hot path: src/lsm/groove.zig:623-1006).
 struct Tables {
-    Account* acc;      // open-addressed by id; empty slot <=> timestamp == 0
-    u64 acc_mask;      // capacity - 1 (power of two)
+    Account* acc;      // dense account rows, index = account row (creation order)
+    AccIdx* aidx;      // open-addressed account id -> row
+    u64 aidx_mask;     // capacity - 1 (power of two)
     Transfer* xrows;   // stored transfers, append-only, commit order
     u8* xful;          // posted groove by pending row: 0 none, 1 posted, 2 voided
-    IdSlot* xidx;      // transfer id -> row index
+    u32* xidx;         // transfer id -> row + 1 (the key is read from xrows)
     u64 xidx_mask;
     History* hrows;    // account-history groove rows, append-only
     u64* commit_ts;    // device copy of StateMachine.commit_timestamp (atomicMax)
@@ -27,14 +43,6 @@ __device__ __forceinline__ bool xidx_maybe_present(const Tables& T, u128 id) {
     return lo <= T.idr[0] && hi <= T.idr[1] && lo >= T.idr[2] && hi >= T.idr[3];
 }
 
-__device__ __forceinline__ void xidx_range_add(const Tables& T, u128 id) {
-    const u64 lo = (u64)id, hi = (u64)(id >> 64);
-    atomicMax((unsigned long long*)&T.idr[0], (unsigned long long)lo);
-    atomicMax((unsigned long long*)&T.idr[1], (unsigned long long)hi);
-    atomicMin((unsigned long long*)&T.idr[2], (unsigned long long)lo);
-    atomicMin((unsigned long long*)&T.idr[3], (unsigned long long)hi);
-}
-
 // One double-buffered fixed-point state (see transfers.hip).
 struct EvalState {
     u8* res;     // own evaluation result (0 = ok)
@@ -48,7 +56,7 @@ struct EvalState {
 };
 
 struct SideScanArgs {
-    const u32* skey;  // sorted side keys (account slot; >= invalid for inert)
+    const u32* skey;  // sorted side keys (account row; >= invalid for inert)
     const u32* sval;  // sorted side ids (2*event + 0 debit / 1 credit)
     const u32* cs;    // chain start per event
     const u8* ok;
@@ -62,40 +70,32 @@ void side_scan(const SideScanArgs& A, u64 m, u32 invalid, bool has_chains, void*
 void side_final_balances(const SideScanArgs& A, u64 m, u32 invalid, const Bal4* bb, Account* acc, u32* big,
                          hipStream_t stream);
 
-// Device probes shared by the kernels.
-__device__ __forceinline__ u32 acc_probe(const Account* __restrict__ acc, u64 mask, u128 id) {
-    u64 h = hash128(id) & mask;
+// Device probes shared by the kernels.  acc_probe returns the account ROW.
+__device__ __forceinline__ u32 acc_probe(const AccIdx* __restrict__ aidx, u64 mask, u128 id) {
+    const u64 lo = (u64)id, hi = (u64)(id >> 64);
+    u64 h = hash128(lo, hi) & mask;
     for (;;) {
-        const Account& a = acc[h];
-        if (a.timestamp == 0) return NONE32;
-        if (a.id == id) return (u32)h;
+        const AccIdx& e = aidx[h];
+        if (e.row1 == 0) return NONE32;
+        if (e.id_lo == lo && e.id_hi == hi) return e.row1 - 1;
         h = (h + 1) & mask;
     }
 }
 
-__device__ __forceinline__ u32 xidx_probe(const IdSlot* __restrict__ x, u64 mask, u128 id) {
-    const u64 lo = (u64)id, hi = (u64)(id >> 64);
-    u64 h = hash128(lo, hi) & mask;
+__device__ __forceinline__ u32 xidx_probe(const Tables& T, u128 id) {
+    u64 h = hash128(id) & T.xidx_mask;
     for (;;) {
-        const IdSlot& s = x[h];
-        if (s.ref == 0) return NONE32;
-        if (s.key_lo == lo && s.key_hi == hi) return (u32)(s.ref - 1);
-        h = (h + 1) & mask;
+        const u32 r1 = T.xidx[h];
+        if (r1 == 0) return NONE32;
+        if (T.xrows[r1 - 1].id == id) return r1 - 1;
+        h = (h + 1) & T.xidx_mask;
     }
 }
 
-__device__ __forceinline__ void xidx_insert(IdSlot* __restrict__ x, u64 mask, u128 id, u32 row) {
-    const u64 lo = (u64)id, hi = (u64)(id >> 64);
-    u64 h = hash128(lo, hi) & mask;
-    for (;;) {
-        unsigned long long prev = atomicCAS((unsigned long long*)&x[h].ref, 0ull, (unsigned long long)row + 1);
-        if (prev == 0) {
-            x[h].key_lo = lo;
-            x[h].key_hi = hi;
-            return;
-        }
-        h = (h + 1) & mask;
-    }
+// Inserts never compare keys: a call inserts ids that are absent and distinct.
+__device__ __forceinline__ void xidx_insert(const Tables& T, u128 id, u32 row) {
+    u64 h = hash128(id) & T.xidx_mask;
+    while (atomicCAS(&T.xidx[h], 0u, row + 1) != 0) h = (h + 1) & T.xidx_mask;
 }
 
 // Counter words (device u32[16]) used for host decisions.

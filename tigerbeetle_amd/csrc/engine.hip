@@ -55,7 +55,7 @@ struct tbgpu_ctx {
     hipStream_t stream = nullptr;
     tbgpu_options opt{};
     Tables T{};
-    u64 acc_cap = 0, xrow_cap = 0, xidx_cap = 0, hist_cap = 0;
+    u64 aidx_cap = 0, xrow_cap = 0, xidx_cap = 0, hist_cap = 0;
     u64 accounts_max = 0;
     u64 n_accounts = 0, n_rows = 0, n_hist = 0;
     u64 bytes = 0;
@@ -217,16 +217,17 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     HIP_CHECK(hipEventCreate(&c->ev0));
     HIP_CHECK(hipEventCreate(&c->ev1));
     c->accounts_max = o.accounts_max;
-    c->acc_cap = pow2_at_least(2 * o.accounts_max);
+    c->aidx_cap = pow2_at_least(2 * o.accounts_max);
     c->xrow_cap = o.transfers_max;
     c->xidx_cap = pow2_at_least(2 * o.transfers_max);
     c->hist_cap = o.history_max;
     u64& B = c->bytes;
-    c->T.acc = dalloc<Account>(c->acc_cap, &B);
-    c->T.acc_mask = c->acc_cap - 1;
+    c->T.acc = dalloc<Account>(o.accounts_max, &B);
+    c->T.aidx = dalloc<AccIdx>(c->aidx_cap, &B);
+    c->T.aidx_mask = c->aidx_cap - 1;
     c->T.xrows = dalloc<Transfer>(c->xrow_cap, &B);
     c->T.xful = dalloc<u8>(c->xrow_cap, &B);
-    c->T.xidx = dalloc<IdSlot>(c->xidx_cap, &B);
+    c->T.xidx = dalloc<u32>(c->xidx_cap, &B);
     c->T.xidx_mask = c->xidx_cap - 1;
     c->T.hrows = dalloc<History>(c->hist_cap, &B);
     c->T.commit_ts = dalloc<u64>(2, &B);
@@ -240,9 +241,9 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
 
 extern "C" void tbgpu_reset(tbgpu_ctx* c) {
     HIP_CHECK(hipSetDevice(c->device));
-    HIP_CHECK(hipMemsetAsync(c->T.acc, 0, c->acc_cap * sizeof(Account), c->stream));
+    HIP_CHECK(hipMemsetAsync(c->T.aidx, 0, c->aidx_cap * sizeof(AccIdx), c->stream));
     HIP_CHECK(hipMemsetAsync(c->T.xful, 0, c->xrow_cap, c->stream));
-    HIP_CHECK(hipMemsetAsync(c->T.xidx, 0, c->xidx_cap * sizeof(IdSlot), c->stream));
+    HIP_CHECK(hipMemsetAsync(c->T.xidx, 0, c->xidx_cap * sizeof(u32), c->stream));
     HIP_CHECK(hipMemsetAsync(c->T.commit_ts, 0, 2 * sizeof(u64), c->stream));
     HIP_CHECK(hipMemsetAsync(c->T.idr, 0, 2 * sizeof(u64), c->stream));                  // max = 0
     HIP_CHECK(hipMemsetAsync(c->T.idr + 2, 0xFF, 2 * sizeof(u64), c->stream));           // min = ~0
@@ -256,7 +257,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     // Free every device allocation by walking the struct's pointers.
-    void* ptrs[] = {c->T.acc, c->T.xrows, c->T.xful, c->T.xidx, c->T.hrows, c->T.commit_ts, c->T.idr, c->T.big, c->ev_buf,
+    void* ptrs[] = {c->T.acc, c->T.aidx, c->T.xrows, c->T.xful, c->T.xidx, c->T.hrows, c->T.commit_ts, c->T.idr, c->T.big, c->ev_buf,
                     c->b_start, c->b_ts, c->ts, c->cs, c->ce, c->sres, c->dslot, c->cslot, c->pre_e, c->pre_p,
                     c->pp_dslot, c->pp_cslot, c->gslot, c->pslot, c->prev_id, c->pend_last, c->prev_pend,
                     c->gclaim, c->gcnt_id, c->gcnt_pd, c->gmem, c->gbeg, c->gend, c->skey, c->sval, c->skey_s,
@@ -397,8 +398,8 @@ static void run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
     hipStream_t s = c->stream;
     TrArgs C = make_tr_args(c, ev, n, nb);
     const u64 g = C.gmask + 1;
-    const u32 inv_acc = (u32)c->acc_cap;
-    const int bits_acc = log2u(c->acc_cap + 1);
+    const u32 inv_acc = (u32)c->accounts_max;  // side keys are account rows
+    const int bits_acc = log2u(c->accounts_max + 1);
     const u32 inv_g = (u32)g;
     const int bits_g = log2u(g + 1);
     c->stats.iterations = 0;
@@ -595,7 +596,7 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
     HIP_CHECK(hipMemcpyAsync(&tot, c->ranks + n, sizeof(uint4), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     if (c->n_accounts + tot.x > c->accounts_max) tbgpu_fatal("create_accounts", "accounts_max exceeded", __FILE__, __LINE__);
-    ac_launch_apply(c->T, C, A->ok, c->fres, c->ranks, results_dev, c->counts, s);
+    ac_launch_apply(c->T, C, A->ok, c->fres, c->ranks, c->n_accounts, results_dev, c->counts, s);
     HIP_CHECK(hipMemcpyAsync(counts_host, c->counts, nb * sizeof(u32), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     c->n_accounts += tot.x;
@@ -712,15 +713,8 @@ extern "C" uint64_t tbgpu_export_history(tbgpu_ctx* c, uint64_t first, uint64_t 
 
 extern "C" uint64_t tbgpu_export_accounts(tbgpu_ctx* c, tb_account_t* out, uint64_t capacity) {
     HIP_CHECK(hipSetDevice(c->device));
-    const u64 chunk = 1u << 16;
-    std::vector<Account> buf(chunk);
-    u64 n = 0;
-    for (u64 off = 0; off < c->acc_cap && n < capacity; off += chunk) {
-        const u64 k = std::min(chunk, c->acc_cap - off);
-        HIP_CHECK(hipMemcpy(buf.data(), c->T.acc + off, k * sizeof(Account), hipMemcpyDeviceToHost));
-        for (u64 i = 0; i < k && n < capacity; i++)
-            if (buf[i].timestamp != 0) memcpy(&out[n++], &buf[i], sizeof(Account));
-    }
+    const u64 n = std::min<u64>(capacity, c->n_accounts);  // dense rows, creation order
+    if (n) HIP_CHECK(hipMemcpy(out, c->T.acc, n * sizeof(Account), hipMemcpyDeviceToHost));
     return n;
 }
 

@@ -85,23 +85,22 @@ __device__ __forceinline__ u8 fp_exists(const Transfer& t, const Transfer& e) {
     return TB_CREATE_TRANSFER_EXISTS;
 }
 
-// Continue an account probe after a first-slot miss.
-__device__ __forceinline__ u32 acc_probe_from(const Tables& T, u64 h, u128 id) {
+// Continue an account index probe after a first-slot miss; returns the slot.
+__device__ __forceinline__ u64 aidx_probe_from(const Tables& T, u64 h, u128 id) {
+    const u64 lo = (u64)id, hi = (u64)(id >> 64);
     for (;;) {
-        h = (h + 1) & T.acc_mask;
-        const Account& a = T.acc[h];
-        if (a.timestamp == 0) return NONE32;
-        if (a.id == id) return (u32)h;
+        h = (h + 1) & T.aidx_mask;
+        const AccIdx& e = T.aidx[h];
+        if (e.row1 == 0 || (e.id_lo == lo && e.id_hi == hi)) return h;
     }
 }
 
 __device__ __forceinline__ u32 xidx_probe_from(const Tables& T, u64 h, u128 id) {
-    const u64 lo = (u64)id, hi = (u64)(id >> 64);
     for (;;) {
         h = (h + 1) & T.xidx_mask;
-        const IdSlot& s = T.xidx[h];
-        if (s.ref == 0) return NONE32;
-        if (s.key_lo == lo && s.key_hi == hi) return (u32)(s.ref - 1);
+        const u32 r1 = T.xidx[h];
+        if (r1 == 0) return NONE32;
+        if (T.xrows[r1 - 1].id == id) return r1 - 1;
     }
 }
 
@@ -118,21 +117,16 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
     const u16 f = t.flags;
     if (f & (TF_LINKED | TF_BDR | TF_BCR | TF_POST | TF_VOID) || *T.big)
         return fp_classify_guarded(T, F, t, i, ts, dslot_out, cslot_out);
-    // speculative first-slot reads (hash tables at load <= 0.5: usually the hit)
-    const u64 hd = hash128(t.debit_account_id) & T.acc_mask;
-    const u64 hc = hash128(t.credit_account_id) & T.acc_mask;
-    const Account& A = T.acc[hd];
-    const Account& B = T.acc[hc];
-    const u64 a_ts = A.timestamp, b_ts = B.timestamp;
-    const u128 a_id = A.id, b_id = B.id;
+    // speculative first-slot reads (hash tables at load <= 0.5: usually the hit).
+    // The 32-byte account index entries carry ledger and flags, so the rows
+    // themselves are only touched by the balance atomics.
+    u64 hd = hash128(t.debit_account_id) & T.aidx_mask;
+    u64 hc = hash128(t.credit_account_id) & T.aidx_mask;
+    AccIdx A = T.aidx[hd];
+    AccIdx B = T.aidx[hc];
     const bool maybe = xidx_maybe_present(T, t.id);
     const u64 hx = hash128(t.id) & T.xidx_mask;
-    u64 x_ref = 0, x_lo = 0, x_hi = 0;
-    if (maybe) {
-        x_ref = T.xidx[hx].ref;
-        x_lo = T.xidx[hx].key_lo;
-        x_hi = T.xidx[hx].key_hi;
-    }
+    const u32 x_r1 = maybe ? T.xidx[hx] : 0u;
     if (t.timestamp != 0) return TB_CREATE_TRANSFER_TIMESTAMP_MUST_BE_ZERO;
     if (f & 0xFFC0u) return TB_CREATE_TRANSFER_RESERVED_FLAG;
     if (t.id == 0) return TB_CREATE_TRANSFER_ID_MUST_NOT_BE_ZERO;
@@ -147,20 +141,20 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
     if (t.amount == 0) return TB_CREATE_TRANSFER_AMOUNT_MUST_NOT_BE_ZERO;
     if (t.ledger == 0) return TB_CREATE_TRANSFER_LEDGER_MUST_NOT_BE_ZERO;
     if (t.code == 0) return TB_CREATE_TRANSFER_CODE_MUST_NOT_BE_ZERO;
-    const u32 ds = a_ts == 0 ? NONE32 : (a_id == t.debit_account_id ? (u32)hd : acc_probe_from(T, hd, t.debit_account_id));
-    if (ds == NONE32) return TB_CREATE_TRANSFER_DEBIT_ACCOUNT_NOT_FOUND;
-    const u32 cs = b_ts == 0 ? NONE32 : (b_id == t.credit_account_id ? (u32)hc : acc_probe_from(T, hc, t.credit_account_id));
-    if (cs == NONE32) return TB_CREATE_TRANSFER_CREDIT_ACCOUNT_NOT_FOUND;
-    const Account& dr = T.acc[ds];
-    const Account& cr = T.acc[cs];
-    if (dr.ledger != cr.ledger) return TB_CREATE_TRANSFER_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
-    if (t.ledger != dr.ledger) return TB_CREATE_TRANSFER_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
-    if ((dr.flags | cr.flags) & (AF_DNEC | AF_CNED | AF_HISTORY)) return FRES_SLOW;  // limits / history
-    if (maybe && x_ref != 0) {
-        const u32 pre = (x_lo == (u64)t.id && x_hi == (u64)(t.id >> 64)) ? (u32)(x_ref - 1)
-                                                                          : xidx_probe_from(T, hx, t.id);
+    const u64 dlo = (u64)t.debit_account_id, dhi = (u64)(t.debit_account_id >> 64);
+    if (A.row1 != 0 && (A.id_lo != dlo || A.id_hi != dhi)) A = T.aidx[aidx_probe_from(T, hd, t.debit_account_id)];
+    if (A.row1 == 0) return TB_CREATE_TRANSFER_DEBIT_ACCOUNT_NOT_FOUND;
+    const u64 clo = (u64)t.credit_account_id, chi = (u64)(t.credit_account_id >> 64);
+    if (B.row1 != 0 && (B.id_lo != clo || B.id_hi != chi)) B = T.aidx[aidx_probe_from(T, hc, t.credit_account_id)];
+    if (B.row1 == 0) return TB_CREATE_TRANSFER_CREDIT_ACCOUNT_NOT_FOUND;
+    if (A.ledger != B.ledger) return TB_CREATE_TRANSFER_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
+    if (t.ledger != A.ledger) return TB_CREATE_TRANSFER_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
+    if ((A.flags | B.flags) & (AF_DNEC | AF_CNED | AF_HISTORY)) return FRES_SLOW;  // limits / history
+    if (x_r1 != 0) {
+        const u32 pre = T.xrows[x_r1 - 1].id == t.id ? x_r1 - 1 : xidx_probe_from(T, hx, t.id);
         if (pre != NONE32) return fp_exists(t, T.xrows[pre]);
     }
+    const u32 ds = A.row1 - 1, cs = B.row1 - 1;
     // an id repeated within the call is caught by fp_dupcheck (only when ids are not increasing)
     // u128 overflow is impossible: amount < 2^64, balances < 2^126 (T.big clear), < 2^32 events
     if ((u64)(t.amount >> 64) != 0) return FRES_SLOW;
@@ -199,9 +193,9 @@ __device__ __forceinline__ u8 fp_classify_guarded(const Tables& T, const FastArg
     if (!(f & (TF_BDR | TF_BCR)) && t.amount == 0) return TB_CREATE_TRANSFER_AMOUNT_MUST_NOT_BE_ZERO;
     if (t.ledger == 0) return TB_CREATE_TRANSFER_LEDGER_MUST_NOT_BE_ZERO;
     if (t.code == 0) return TB_CREATE_TRANSFER_CODE_MUST_NOT_BE_ZERO;
-    const u32 ds = acc_probe(T.acc, T.acc_mask, t.debit_account_id);
+    const u32 ds = acc_probe(T.aidx, T.aidx_mask, t.debit_account_id);
     if (ds == NONE32) return TB_CREATE_TRANSFER_DEBIT_ACCOUNT_NOT_FOUND;
-    const u32 cs = acc_probe(T.acc, T.acc_mask, t.credit_account_id);
+    const u32 cs = acc_probe(T.aidx, T.aidx_mask, t.credit_account_id);
     if (cs == NONE32) return TB_CREATE_TRANSFER_CREDIT_ACCOUNT_NOT_FOUND;
     const Account& dr = T.acc[ds];
     const Account& cr = T.acc[cs];
@@ -209,7 +203,7 @@ __device__ __forceinline__ u8 fp_classify_guarded(const Tables& T, const FastArg
     if (t.ledger != dr.ledger) return TB_CREATE_TRANSFER_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
     if (f & (TF_BDR | TF_BCR)) return FRES_SLOW;                                  // balancing
     if ((dr.flags | cr.flags) & (AF_DNEC | AF_CNED | AF_HISTORY)) return FRES_SLOW;  // limits / history
-    const u32 pre = xidx_probe(T.xidx, T.xidx_mask, t.id);
+    const u32 pre = xidx_probe(T, t.id);
     if (pre != NONE32) return fp_exists(t, T.xrows[pre]);
     if (gtab_claim_is_dup(F, t.id, i)) return FRES_SLOW;                           // id repeats in the call
     // overflow impossible: amount < 2^64 and the touched balances' high words < 2^62
@@ -496,7 +490,7 @@ __global__ void fp_index(Tables T, FastArgs F) {
     }
     if (i >= F.n) return;
     const u32 row = F.rows[i];
-    if (row != NONE32) xidx_insert(T.xidx, T.xidx_mask, F.keys[i], row);
+    if (row != NONE32) xidx_insert(T, F.keys[i], row);
 }
 
 // Exact inverse of fp_commit's balance deltas, before the general path redoes the call.
@@ -505,8 +499,8 @@ __global__ void fp_undo(Tables T, FastArgs F) {
     if (i >= F.n) return;
     if (F.fres[i] != TB_CREATE_TRANSFER_OK) return;
     const Transfer& t = F.ev[i];
-    const u32 ds = acc_probe(T.acc, T.acc_mask, t.debit_account_id);
-    const u32 cs = acc_probe(T.acc, T.acc_mask, t.credit_account_id);
+    const u32 ds = acc_probe(T.aidx, T.aidx_mask, t.debit_account_id);
+    const u32 cs = acc_probe(T.aidx, T.aidx_mask, t.credit_account_id);
     const u64 a = (u64)t.amount;
     if (t.flags & TF_PENDING) {
         atomic_sub_u128_small(&T.acc[ds].debits_pending, a);

@@ -75,7 +75,7 @@ void ac_launch_evaluate(const Tables& T, const AcArgs& C, const u8* res_s, const
                         u32* cfail_d, hipStream_t stream);
 void ac_launch_mask(const Tables& T, const AcArgs& C, const u8* res, const u8* ok, const u32* cfail, u8* fres,
                     u8* mask, hipStream_t stream);
-void ac_launch_apply(const Tables& T, const AcArgs& C, const u8* ok, const u8* fres, const uint4* rk,
+void ac_launch_apply(const Tables& T, const AcArgs& C, const u8* ok, const u8* fres, const uint4* rk, u64 row_base,
                      tb_create_accounts_result_t* results, u32* counts, hipStream_t stream);
 
 // lookups / maintenance (accounts.hip)

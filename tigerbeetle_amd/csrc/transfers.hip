@@ -114,12 +114,12 @@ __global__ void tr_classify(Tables T, TrArgs C) {
         else {
             sres = SRES_DYN;
             fl |= FL_POSTVOID;
-            pre_e = xidx_probe(T.xidx, T.xidx_mask, t.id);
-            pre_p = xidx_probe(T.xidx, T.xidx_mask, t.pending_id);
+            pre_e = xidx_probe(T, t.id);
+            pre_p = xidx_probe(T, t.pending_id);
             if (pre_p != NONE32) {
                 const Transfer& p = T.xrows[pre_p];
-                ppd = acc_probe(T.acc, T.acc_mask, p.debit_account_id);
-                ppc = acc_probe(T.acc, T.acc_mask, p.credit_account_id);
+                ppd = acc_probe(T.aidx, T.aidx_mask, p.debit_account_id);
+                ppc = acc_probe(T.aidx, T.aidx_mask, p.credit_account_id);
             }
             gslot = gtab_find_or_insert(C, t.id, i, 0);
             pslot = gtab_find_or_insert(C, t.pending_id, i, 1);
@@ -144,9 +144,9 @@ __global__ void tr_classify(Tables T, TrArgs C) {
         sres = TB_CREATE_TRANSFER_LEDGER_MUST_NOT_BE_ZERO;
     } else if (t.code == 0) {
         sres = TB_CREATE_TRANSFER_CODE_MUST_NOT_BE_ZERO;
-    } else if ((dslot = acc_probe(T.acc, T.acc_mask, t.debit_account_id)) == NONE32) {
+    } else if ((dslot = acc_probe(T.aidx, T.aidx_mask, t.debit_account_id)) == NONE32) {
         sres = TB_CREATE_TRANSFER_DEBIT_ACCOUNT_NOT_FOUND;
-    } else if ((cslot = acc_probe(T.acc, T.acc_mask, t.credit_account_id)) == NONE32) {
+    } else if ((cslot = acc_probe(T.aidx, T.aidx_mask, t.credit_account_id)) == NONE32) {
         sres = TB_CREATE_TRANSFER_CREDIT_ACCOUNT_NOT_FOUND;
     } else {
         const Account& dr = T.acc[dslot];
@@ -155,7 +155,7 @@ __global__ void tr_classify(Tables T, TrArgs C) {
         else if (t.ledger != dr.ledger) sres = TB_CREATE_TRANSFER_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
         else {
             sres = SRES_DYN;
-            pre_e = xidx_probe(T.xidx, T.xidx_mask, t.id);
+            pre_e = xidx_probe(T, t.id);
             gslot = gtab_find_or_insert(C, t.id, i, 0);
             if (f & (TF_BDR | TF_BCR)) fl |= FL_BALANCING;
             if (f & TF_PENDING) fl |= FL_PENDING;
@@ -588,7 +588,7 @@ __global__ void tr_apply(Tables T, TrArgs C, EvalState S, const u8* __restrict__
     const u64 row = row_base + q.x;
     const Transfer s = load_ref(T, C, S, i);
     T.xrows[row] = s;
-    xidx_insert(T.xidx, T.xidx_mask, t.id, (u32)row);
+    xidx_insert(T, t.id, (u32)row);
     if (t.flags & (TF_POST | TF_VOID)) {
         const u32 p = S.pref[i];
         const u64 prow = (p & PREF_ROW) ? (u64)(p & ~PREF_ROW) : row_base + rk[p].x;

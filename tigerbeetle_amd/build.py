@@ -28,30 +28,41 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_lib(verbose: bool = False, force: bool = False) -> str:
-    os.makedirs(BUILD, exist_ok=True)
+def build_lib(verbose: bool = False, force: bool = False, defines=(), build_dir: str = BUILD,
+              lib: str = LIB) -> str:
+    """Compile csrc/*.hip and link `lib`.  `defines` (e.g. ["FP_WAVES_PER_EU=8"]) and
+    a separate `build_dir`/`lib` build timing variants for experiments; the product
+    library is the default one."""
+    os.makedirs(build_dir, exist_ok=True)
     sources = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     headers = sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(ROOT, "include", "tbgpu.h")]
     objs = []
     jobs = []
     for src in sources:
-        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        obj = os.path.join(build_dir, os.path.basename(src) + ".o")
         objs.append(obj)
         if force or _stale(obj, [src] + headers):
-            jobs.append([HIPCC, *CXXFLAGS, "-c", src, "-o", obj])
+            jobs.append([HIPCC, *CXXFLAGS, *[f"-D{d}" for d in defines], "-c", src, "-o", obj])
     with cf.ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
         for cmd, r in zip(jobs, ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), jobs)):
             if verbose or r.returncode != 0:
                 sys.stderr.write(" ".join(cmd) + "\n" + r.stdout + r.stderr)
             if r.returncode != 0:
                 raise RuntimeError(f"hipcc failed for {cmd[-3]}")
-    if force or jobs or _stale(LIB, objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
+    if force or jobs or _stale(lib, objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             sys.stderr.write(r.stdout + r.stderr)
             raise RuntimeError("link failed")
-    return LIB
+    return lib
+
+
+def build_variant(name: str, defines) -> str:
+    """build/var_<name>/libtbgpu.so, loaded instead of the product library when
+    TBGPU_LIB points at it (profiles/variants.py)."""
+    d = os.path.join(BUILD, "var_" + name)
+    return build_lib(defines=defines, build_dir=d, lib=os.path.join(d, "libtbgpu.so"), force=True)
 
 
 def build_oracle() -> str:

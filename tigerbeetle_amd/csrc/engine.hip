@@ -83,6 +83,9 @@ struct tbgpu_ctx {
     u32* counters = nullptr;
     int* status = nullptr;
     u32* h_counters = nullptr;  // pinned
+    u32* h_counts = nullptr;    // pinned, bmax
+    u64* h_stage_ts = nullptr;  // pinned, bmax
+    u32* h_stage_start = nullptr;  // pinned, bmax + 1
     // fast path (fast.hip)
     u32* f_gtab = nullptr;
     u32* f_gpos = nullptr;
@@ -160,6 +163,9 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->f_rows = dalloc<u32>(n, &B);
     c->f_tile_idr = dalloc<u64>(4 * (fp_tiles(nmax) + 1), &B);
     HIP_CHECK(hipHostMalloc((void**)&c->h_counters, CNT_COUNT * sizeof(u32), hipHostMallocDefault));
+    HIP_CHECK(hipHostMalloc((void**)&c->h_counts, c->bmax * sizeof(u32), hipHostMallocDefault));
+    HIP_CHECK(hipHostMalloc((void**)&c->h_stage_ts, c->bmax * sizeof(u64), hipHostMallocDefault));
+    HIP_CHECK(hipHostMalloc((void**)&c->h_stage_start, (c->bmax + 1) * sizeof(u32), hipHostMallocDefault));
 }
 
 enum { PH_UPLOAD = 0, PH_CLASSIFY = 1, PH_SORT = 2, PH_SCAN = 3, PH_EVAL = 4, PH_APPLY = 5, PH_INDEX = 6, PH_PREP = 7, PH_END = -1 };
@@ -271,6 +277,9 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
         for (void* p : q) if (p) (void)hipFree(p);
     }
     if (c->h_counters) (void)hipHostFree(c->h_counters);
+    if (c->h_counts) (void)hipHostFree(c->h_counts);
+    if (c->h_stage_ts) (void)hipHostFree(c->h_stage_ts);
+    if (c->h_stage_start) (void)hipHostFree(c->h_stage_start);
     for (hipEvent_t e : c->prof_pool) (void)hipEventDestroy(e);
     (void)hipEventDestroy(c->ev0);
     (void)hipEventDestroy(c->ev1);
@@ -303,8 +312,12 @@ static void upload_batches(tbgpu_ctx* c, const uint64_t* timestamps, const uint3
     starts.resize(nb + 1);
     starts[0] = 0;
     for (u32 b = 0; b < nb; b++) starts[b + 1] = starts[b] + counts[b];
-    HIP_CHECK(hipMemcpyAsync(c->b_start, starts.data(), (nb + 1) * sizeof(u32), hipMemcpyHostToDevice, c->stream));
-    HIP_CHECK(hipMemcpyAsync(c->b_ts, timestamps, nb * sizeof(u64), hipMemcpyHostToDevice, c->stream));
+    // staged through pinned memory so the copies are truly asynchronous (every
+    // call synchronizes before the staging buffer is reused)
+    memcpy(c->h_stage_ts, timestamps, nb * sizeof(u64));
+    memcpy(c->h_stage_start, starts.data(), (nb + 1) * sizeof(u32));
+    HIP_CHECK(hipMemcpyAsync(c->b_start, c->h_stage_start, (nb + 1) * sizeof(u32), hipMemcpyHostToDevice, c->stream));
+    HIP_CHECK(hipMemcpyAsync(c->b_ts, c->h_stage_ts, nb * sizeof(u64), hipMemcpyHostToDevice, c->stream));
 }
 
 // Device replies are concatenated across the chunk's batches; the host C-ABI
@@ -368,24 +381,23 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tb_create_
     F.ablate = ablate;
     if (c->n_rows + n > c->xrow_cap) return false;  // let the general path report capacity exactly
     prof_mark(c, PH_PREP);
-    HIP_CHECK(hipMemsetAsync(c->counters, 0, CNT_COUNT * sizeof(u32), s));
-    HIP_CHECK(hipMemsetAsync(c->f_tiles, 0, fp_tiles(n) * sizeof(u64), s));
-    HIP_CHECK(hipMemsetAsync(c->f_tile_counter, 0, sizeof(u32), s));
-    HIP_CHECK(hipMemsetAsync(c->counts, 0, nb * sizeof(u32), s));
+    fp_launch_prep(F, s);
     prof_mark(c, PH_CLASSIFY);
     fp_launch_commit(c->T, F, s);
     prof_mark(c, PH_INDEX);
     fp_launch_index(c->T, F, s);
     prof_mark(c, PH_END);
-    read_counters(c);
+    // one round trip: the flags decide whether the reply counts are valid
+    HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, CNT_COUNT * sizeof(u32), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(c->h_counts, c->counts, nb * sizeof(u32), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
     const u32 flags = c->h_counters[CNT_FLAGS];
     if (flags & FL_ERROR) tbgpu_fatal("create_transfers", "fast path look-back did not complete", __FILE__, __LINE__);
     if (flags & FL_SLOW) {
         fp_launch_undo(c->T, F, s);
         return false;
     }
-    HIP_CHECK(hipMemcpyAsync(counts_host, c->counts, nb * sizeof(u32), hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+    memcpy(counts_host, c->h_counts, nb * sizeof(u32));
     c->n_rows += c->h_counters[CNT_OK];
     c->stats.path = 1;
     c->stats.iterations = 1;

@@ -27,8 +27,11 @@
 
 namespace {
 
-constexpr int FP_THREADS = 512;   // one event per thread, one tile per workgroup (2 per CU)
-constexpr int AGG_SLOTS = 2048;   // LDS aggregation table (>= 2x the 1024 sides of a tile)
+#ifndef FP_TILE
+#define FP_TILE 512
+#endif
+constexpr int FP_THREADS = FP_TILE;        // one event per thread, one tile per workgroup
+constexpr int AGG_SLOTS = 4 * FP_THREADS;  // LDS aggregation table (2x the sides of a tile)
 constexpr u32 AGG_EMPTY = 0xFFFFFFFFu;
 constexpr u8 FRES_SLOW = 0xFE;
 constexpr u64 ST_AGG = 1ull << 62;
@@ -240,7 +243,10 @@ __device__ __forceinline__ void agg_add(u32* keys, u64* sums, u32* carries, u32 
     if (old + a < old) atomicAdd(&carries[h], 1u);
 }
 
-__global__ __launch_bounds__(FP_THREADS) void fp_commit(Tables T, FastArgs F) {
+#ifndef FP_WAVES_PER_EU
+#define FP_WAVES_PER_EU 7
+#endif
+__global__ __launch_bounds__(FP_THREADS) __attribute__((amdgpu_waves_per_eu(FP_WAVES_PER_EU))) void fp_commit(Tables T, FastArgs F) {
     __shared__ u32 s_tile;
     __shared__ u32 s_wok[FP_THREADS / 64], s_wbad[FP_THREADS / 64];
     __shared__ u64 s_excl;
@@ -249,6 +255,8 @@ __global__ __launch_bounds__(FP_THREADS) void fp_commit(Tables T, FastArgs F) {
     __shared__ u32 s_keys[AGG_SLOTS];
     __shared__ u64 s_sums[AGG_SLOTS];
     __shared__ u32 s_carry[AGG_SLOTS];
+    __shared__ u32 s_row[FP_THREADS];  // stored row per event of the tile, or NONE32
+    __shared__ u64 s_ts[FP_THREADS];
     const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid == 0) s_tile = atomicAdd(F.tile_counter, 1u);
     for (u32 h = tid; h < AGG_SLOTS; h += FP_THREADS) {
@@ -265,14 +273,19 @@ __global__ __launch_bounds__(FP_THREADS) void fp_commit(Tables T, FastArgs F) {
     u8 r = FRES_SLOW;
     u32 b = 0, ds = NONE32, cs = NONE32;
     u64 ts = 0;
+    // batch of the event: one uniform binary search per wave, then a short walk
+    // (a wave spans 64 events, so usually zero or one batch boundary)
+    const u32 i0 = __builtin_amdgcn_readfirstlane(tile * FP_THREADS + wave * 64);
+    if (i0 < F.n) b = fp_batch_of(F.b_start, F.nb, i0);
     if (valid) {
-        b = fp_batch_of(F.b_start, F.nb, i);
+        while (F.b_start[b + 1] <= i) b++;
         const u32 bs = F.b_start[b], nbatch = F.b_start[b + 1] - bs;
         ts = F.b_ts[b] - nbatch + (i - bs) + 1;
         t = F.ev[i];
         r = fp_classify(T, F, t, i, ts, &ds, &cs);
         F.fres[i] = r;
         if (r == TB_CREATE_TRANSFER_OK) {
+            F.keys[i] = t.id;
             // tile-local aggregation first: a hot account costs one global atomic per tile
             const u64 a = (u64)t.amount;
             const u32 pend = (t.flags & TF_PENDING) ? 0u : 1u;
@@ -353,11 +366,11 @@ __global__ __launch_bounds__(FP_THREADS) void fp_commit(Tables T, FastArgs F) {
     // flush the tile's partial sums: u128 += (carry:sum) with u64 atomics.  All of a
     // thread's low-word atomics are issued before any returns (memory-level
     // parallelism); the rare carries follow.
+    constexpr int PER = AGG_SLOTS / FP_THREADS;
+    u64* wp[PER];
+    u64 av[PER], old[PER];
+    u32 cv[PER];
     {
-        constexpr int PER = AGG_SLOTS / FP_THREADS;
-        u64* wp[PER];
-        u64 av[PER], old[PER];
-        u32 cv[PER];
 #pragma unroll
         for (int k = 0; k < PER; k++) {
             const u32 h = tid + k * FP_THREADS;
@@ -369,15 +382,6 @@ __global__ __launch_bounds__(FP_THREADS) void fp_commit(Tables T, FastArgs F) {
 #pragma unroll
         for (int k = 0; k < PER; k++)
             old[k] = wp[k] ? atomicAdd((unsigned long long*)&wp[k][0], (unsigned long long)av[k]) : 0;
-#pragma unroll
-        for (int k = 0; k < PER; k++) {
-            if (!wp[k]) continue;
-            const u64 c = (u64)cv[k] + (old[k] + av[k] < old[k] ? 1 : 0);
-            if (c) {
-                const u64 hi = atomicAdd((unsigned long long*)&wp[k][1], (unsigned long long)c);
-                if (hi + c >= (1ull << 62)) atomicOr(T.big, 1u);  // later calls must prove no overflow
-            }
-        }
     }
     if (wave == 0) {
         // decoupled look-back, 64 predecessors per step (lane l reads tile top - l)
@@ -428,19 +432,48 @@ __global__ __launch_bounds__(FP_THREADS) void fp_commit(Tables T, FastArgs F) {
     const u64 excl = s_excl;
     u32 wok = 0, wbad = 0;
     for (u32 w = 0; w < wave; w++) { wok += s_wok[w]; wbad += s_wbad[w]; }
+    u32 row = NONE32;
     if (ok) {
-        const u64 row = F.row_base + (excl & 0x7FFFFFFFull) + wok + __popcll(okm & lt);
-        Transfer s = t;
-        s.timestamp = ts;
-        if (!(F.ablate & ABL_ROWS)) T.xrows[row] = s;  // speculative until fp_index publishes the id
-        F.keys[i] = t.id;
-        F.rows[i] = (u32)row;
-    } else if (valid) {
-        F.rows[i] = NONE32;
-        if (bad) {
-            const u64 pos = (excl >> 31) + wbad + __popcll(badm & lt);
-            F.results[pos] = {i - F.b_start[b], (u32)r};
-            atomicAdd(&F.batch_counts[b], 1u);
+        row = (u32)(F.row_base + (excl & 0x7FFFFFFFull) + wok + __popcll(okm & lt));
+    } else if (bad) {
+        const u64 pos = (excl >> 31) + wbad + __popcll(badm & lt);
+        F.results[pos] = {i - F.b_start[b], (u32)r};
+        atomicAdd(&F.batch_counts[b], 1u);
+    }
+    if (valid) F.rows[i] = row;
+    s_row[tid] = row;
+    s_ts[tid] = ts;
+    __syncthreads();
+    // Stored rows: the tile's events copied to their rows with whole-wave 1-KB
+    // accesses (lane = one 16-byte chunk; 8 chunks per 128-byte transfer), the
+    // timestamp chunk patched.  The second read of the events hits the L2.
+    if (!(F.ablate & ABL_ROWS)) {
+        const u32 base = tile * FP_THREADS;
+        const u32 nt = min((u32)FP_THREADS, F.n - base);
+        const uint4* src = (const uint4*)(F.ev + base);
+        uint4* dst = (uint4*)T.xrows;
+        for (u32 c = tid; c < nt * 8; c += FP_THREADS) {
+            const u32 e = c >> 3, part = c & 7;
+            const u32 rw = s_row[e];
+            if (rw == NONE32) continue;
+            uint4 v = src[c];
+            if (part == 7) {  // bytes 112..127: ledger, code, flags, timestamp
+                const u64 t8 = s_ts[e];
+                v.z = (u32)t8;
+                v.w = (u32)(t8 >> 32);
+            }
+            dst[(u64)rw * 8 + part] = v;
+        }
+    }
+    // carries of the flushed sums, last: the atomics' return latency hides behind
+    // the look-back and the row stores
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        if (!wp[k]) continue;
+        const u64 c = (u64)cv[k] + (old[k] + av[k] < old[k] ? 1 : 0);
+        if (c) {
+            const u64 hi = atomicAdd((unsigned long long*)&wp[k][1], (unsigned long long)c);
+            if (hi + c >= (1ull << 62)) atomicOr(T.big, 1u);  // later calls must prove no overflow
         }
     }
 }
@@ -493,6 +526,16 @@ __global__ void fp_index(Tables T, FastArgs F) {
     if (row != NONE32) xidx_insert(T, F.keys[i], row);
 }
 
+// Per-call reset of the fast path's counters, look-back tiles and reply counts
+// (one launch instead of four fills).
+__global__ void fp_prep(FastArgs F, u32 ntiles) {
+    const u32 k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < CNT_COUNT) F.counters[k] = 0;
+    if (k == 0) *F.tile_counter = 0;
+    if (k < ntiles) F.tile_status[k] = 0;
+    if (k < F.nb) F.batch_counts[k] = 0;
+}
+
 // Exact inverse of fp_commit's balance deltas, before the general path redoes the call.
 __global__ void fp_undo(Tables T, FastArgs F) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -512,6 +555,13 @@ __global__ void fp_undo(Tables T, FastArgs F) {
 }
 
 }  // namespace
+
+void fp_launch_prep(const FastArgs& F, hipStream_t stream) {
+    const u32 ntiles = (u32)fp_tiles(F.n);
+    const u32 m = std::max<u32>(std::max<u32>(ntiles, F.nb), CNT_COUNT);
+    fp_prep<<<(m + 255) / 256, 256, 0, stream>>>(F, ntiles);
+    HIP_CHECK(hipGetLastError());
+}
 
 void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream) {
     fp_commit<<<(F.n + FP_THREADS - 1) / FP_THREADS, FP_THREADS, 0, stream>>>(T, F);

@@ -16,7 +16,8 @@ from .types import (ACCOUNT_DTYPE, HISTORY_DTYPE, RESULT_DTYPE, TRANSFER_DTYPE, 
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
-LIB_PATH = os.path.join(PKG, "libtbgpu.so")
+# TBGPU_LIB: a timing variant built by build.build_variant (experiments only)
+LIB_PATH = os.environ.get("TBGPU_LIB") or os.path.join(PKG, "libtbgpu.so")
 HEADER = os.path.join(ROOT, "include", "tbgpu.h")
 _lib = None
 

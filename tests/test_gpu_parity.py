@@ -150,3 +150,19 @@ def test_random_id_order():
     t2[30_000]["id_lo"] = t2[29_999]["id_lo"]  # a repeat inside the last call
     w.transfers = t2
     _parity(w)
+
+
+def test_fast_path_with_failures():
+    """Static failures, unknown accounts and re-submitted ids stay on the fast path:
+    rows are re-placed at their ranks (fp_fix) and the replies are exact."""
+    w = workload.config1(transfer_count=30_000, account_count=400, seed=21)
+    t = w.transfers.copy()
+    t[100]["amount_lo"] = 0                          # amount_must_not_be_zero
+    t[9_000]["debit_account_id_lo"] = 10_000_000     # debit_account_not_found
+    t[12_345]["ledger"] = 0                          # ledger_must_not_be_zero
+    t[29_000:29_100] = t[0:100]                      # exists (same ids, earlier calls)
+    t[29_100]["id_lo"] = t[5]["id_lo"]               # exists_with_different_* (other fields)
+    w.transfers = t
+    st = _parity(w, split=1)
+    assert st.path == 1
+    st = _parity(w, split=2)

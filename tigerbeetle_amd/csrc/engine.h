@@ -82,20 +82,32 @@ __device__ __forceinline__ u32 acc_probe(const AccIdx* __restrict__ aidx, u64 ma
     }
 }
 
+// Transfer-id index hash: runs of 16 consecutive ids share one 64-byte line of
+// slots in id order (the benchmark's sequential ids insert with whole-line
+// writes); the run itself is placed by a full 128-bit mix, so random ids spread
+// as with any hash.  Probing steps a whole line (XIDX_STEP), keeping each id's
+// offset, so a run that meets an occupied line moves on together instead of
+// walking through the other run slot by slot.  The mask is >= 16 (pow2_at_least).
+constexpr u64 XIDX_STEP = 16;
+__device__ __forceinline__ u64 xidx_hash(u128 id) {
+    const u64 lo = (u64)id, hi = (u64)(id >> 64);
+    return (hash128(lo >> 4, hi) << 4) | (lo & 15);
+}
+
 __device__ __forceinline__ u32 xidx_probe(const Tables& T, u128 id) {
-    u64 h = hash128(id) & T.xidx_mask;
+    u64 h = xidx_hash(id) & T.xidx_mask;
     for (;;) {
         const u32 r1 = T.xidx[h];
         if (r1 == 0) return NONE32;
         if (T.xrows[r1 - 1].id == id) return r1 - 1;
-        h = (h + 1) & T.xidx_mask;
+        h = (h + XIDX_STEP) & T.xidx_mask;
     }
 }
 
 // Inserts never compare keys: a call inserts ids that are absent and distinct.
 __device__ __forceinline__ void xidx_insert(const Tables& T, u128 id, u32 row) {
-    u64 h = hash128(id) & T.xidx_mask;
-    while (atomicCAS(&T.xidx[h], 0u, row + 1) != 0) h = (h + 1) & T.xidx_mask;
+    u64 h = xidx_hash(id) & T.xidx_mask;
+    while (atomicCAS(&T.xidx[h], 0u, row + 1) != 0) h = (h + XIDX_STEP) & T.xidx_mask;
 }
 
 // Counter words (device u32[16]) used for host decisions.
@@ -104,6 +116,7 @@ enum {
     CNT_CHANGES = 1,    // fixed-point: events whose state changed this pass
     CNT_KEYS = 2,       // side keys changed since the last sort
     CNT_OK = 3,         // fast path: accepted events
+    CNT_BAD = 4,        // fast path: events with a result other than ok
     CNT_COUNT = 16,
 };
 enum {

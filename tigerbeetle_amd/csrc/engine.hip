@@ -90,8 +90,6 @@ struct tbgpu_ctx {
     u32* f_gtab = nullptr;
     u32* f_gpos = nullptr;
     u64 f_gcap = 0;
-    u64* f_tiles = nullptr;
-    u32* f_tile_counter = nullptr;
     u128* f_keys = nullptr;
     u32* f_rows = nullptr;
     u64* f_tile_idr = nullptr;
@@ -157,8 +155,6 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->f_gtab = dalloc<u32>(c->f_gcap, &B);
     HIP_CHECK(hipMemset(c->f_gtab, 0, c->f_gcap * sizeof(u32)));
     c->f_gpos = dalloc<u32>(n, &B);
-    c->f_tiles = dalloc<u64>(fp_tiles(nmax) + 1, &B);
-    c->f_tile_counter = dalloc<u32>(4, &B);
     c->f_keys = dalloc<u128>(n, &B);
     c->f_rows = dalloc<u32>(n, &B);
     c->f_tile_idr = dalloc<u64>(4 * (fp_tiles(nmax) + 1), &B);
@@ -269,7 +265,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
                     c->gclaim, c->gcnt_id, c->gcnt_pd, c->gmem, c->gbeg, c->gend, c->skey, c->sval, c->skey_s,
                     c->sval_s, c->spos, c->bb, c->ss.keys_tmp, c->ss.vals_tmp, c->ss.hist, c->side_tiles,
                     c->sc.tile_sums, c->fres, c->mask, c->ranks, c->res_buf, c->counts, c->counters, c->status,
-                    c->f_gtab, c->f_gpos, c->f_tiles, c->f_tile_counter, c->f_keys, c->f_rows,
+                    c->f_gtab, c->f_gpos, c->f_keys, c->f_rows,
                     c->f_tile_idr};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     for (EvalState& s : c->st) {
@@ -366,8 +362,6 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tb_create_
     F.gmask = std::min<u64>(c->f_gcap, pow2_at_least(2ull * n)) - 1;
     F.fres = c->fres;
     F.counters = c->counters;
-    F.tile_status = c->f_tiles;
-    F.tile_counter = c->f_tile_counter;
     F.batch_counts = c->counts;
     F.results = results_dev;
     F.row_base = c->n_rows;
@@ -396,6 +390,13 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tb_create_
     if (flags & FL_SLOW) {
         fp_launch_undo(c->T, F, s);
         return false;
+    }
+    if (c->h_counters[CNT_BAD]) {
+        // failures: rows to their ranks, replies, then the index on the final rows
+        prof_mark(c, PH_APPLY);
+        fp_launch_fix(c->T, F, c->mask, c->ranks, c->sc, s);
+        prof_mark(c, PH_END);
+        HIP_CHECK(hipStreamSynchronize(s));
     }
     memcpy(counts_host, c->h_counts, nb * sizeof(u32));
     c->n_rows += c->h_counters[CNT_OK];

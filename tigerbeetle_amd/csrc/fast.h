@@ -13,13 +13,11 @@ struct FastArgs {
     u64 gmask;
     u8* fres;           // per-event result (0 = accepted, deltas applied)
     u32* counters;
-    u64* tile_status;   // decoupled look-back: [flag:2 | failures:31 | accepted:31]
-    u32* tile_counter;
     u32* batch_counts;  // failures per batch
     tb_create_transfers_result_t* results;  // replies, concatenated across batches
     u64 row_base;
     u128* keys;         // accepted ids, for fp_index
-    u32* rows;          // stored row per event or NONE32
+    u32* rows;          // stored row per accepted event (written by fp_fix only)
     u64* tile_idr;      // per tile: componentwise max lo, max hi, min lo, min hi of accepted ids
     u32 ablate;         // timing-only builds (TBGPU_ABLATE): skip parts of the work; results wrong
 };
@@ -28,5 +26,6 @@ enum { ABL_DUP = 1, ABL_BALANCES = 2, ABL_ROWS = 4, ABL_LOOKBACK = 8, ABL_EVENT 
 void fp_launch_prep(const FastArgs& F, hipStream_t stream);
 void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream);
 void fp_launch_index(const Tables& T, const FastArgs& F, hipStream_t stream);
+void fp_launch_fix(const Tables& T, const FastArgs& F, u8* mask, uint4* ranks, Scan3Scratch& sc, hipStream_t stream);
 void fp_launch_undo(const Tables& T, const FastArgs& F, hipStream_t stream);
 u64 fp_tiles(u64 n);

@@ -18,9 +18,12 @@
 // (FL_SLOW), its balance deltas are subtracted again (fp_undo, exact modular
 // inverse) and the call is redone by the general fixed-point path.
 //
-// fp_commit: classify + balance deltas (u64 atomics with carry) + decoupled
-// look-back rank of accepted events and failures + stored rows + replies.
+// fp_commit: classify + balance deltas (LDS-aggregated, u64 atomics with carry)
+//            + optimistic stored rows at row_base + event.
 // fp_index:  publish the accepted ids in the transfer-id index.
+// With failures (results other than ok, the rare case for this path) fp_mask +
+// scan3 + fp_fix place the rows at their ranks and write the sparse replies, then
+// fp_index runs on the final rows.
 #include "common.h"
 #include "engine.h"
 #include "fast.h"
@@ -34,9 +37,6 @@ constexpr int FP_THREADS = FP_TILE;        // one event per thread, one tile per
 constexpr int AGG_SLOTS = 4 * FP_THREADS;  // LDS aggregation table (2x the sides of a tile)
 constexpr u32 AGG_EMPTY = 0xFFFFFFFFu;
 constexpr u8 FRES_SLOW = 0xFE;
-constexpr u64 ST_AGG = 1ull << 62;
-constexpr u64 ST_INC = 2ull << 62;
-constexpr u64 ST_VAL = (1ull << 62) - 1;
 
 __device__ __forceinline__ u32 fp_batch_of(const u32* __restrict__ b_start, u32 nb, u32 i) {
     u32 lo = 0, hi = nb;
@@ -100,7 +100,7 @@ __device__ __forceinline__ u64 aidx_probe_from(const Tables& T, u64 h, u128 id) 
 
 __device__ __forceinline__ u32 xidx_probe_from(const Tables& T, u64 h, u128 id) {
     for (;;) {
-        h = (h + 1) & T.xidx_mask;
+        h = (h + XIDX_STEP) & T.xidx_mask;
         const u32 r1 = T.xidx[h];
         if (r1 == 0) return NONE32;
         if (T.xrows[r1 - 1].id == id) return r1 - 1;
@@ -128,7 +128,7 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
     AccIdx A = T.aidx[hd];
     AccIdx B = T.aidx[hc];
     const bool maybe = xidx_maybe_present(T, t.id);
-    const u64 hx = hash128(t.id) & T.xidx_mask;
+    const u64 hx = xidx_hash(t.id) & T.xidx_mask;
     const u32 x_r1 = maybe ? T.xidx[hx] : 0u;
     if (t.timestamp != 0) return TB_CREATE_TRANSFER_TIMESTAMP_MUST_BE_ZERO;
     if (f & 0xFFC0u) return TB_CREATE_TRANSFER_RESERVED_FLAG;
@@ -246,33 +246,32 @@ __device__ __forceinline__ void agg_add(u32* keys, u64* sums, u32* carries, u32 
 #ifndef FP_WAVES_PER_EU
 #define FP_WAVES_PER_EU 7
 #endif
-__global__ __launch_bounds__(FP_THREADS) __attribute__((amdgpu_waves_per_eu(FP_WAVES_PER_EU))) void fp_commit(Tables T, FastArgs F) {
-    __shared__ u32 s_tile;
-    __shared__ u32 s_wok[FP_THREADS / 64], s_wbad[FP_THREADS / 64];
-    __shared__ u64 s_excl;
+// One tile of FP_THREADS events per workgroup.  Rows are stored optimistically at
+// row_base + event (every event accepted, the benchmark's case); failures are
+// counted and, if there are any, fp_fix moves the rows to their ranks afterwards.
+__global__ __launch_bounds__(FP_THREADS) __attribute__((amdgpu_waves_per_eu(FP_WAVES_PER_EU)))
+void fp_commit(Tables T, FastArgs F) {
     __shared__ u64 s_maxts[FP_THREADS / 64];
+    __shared__ u32 s_cnt[FP_THREADS / 64][2];
     __shared__ u64 s_idr[FP_THREADS / 64][4];
     __shared__ u32 s_keys[AGG_SLOTS];
     __shared__ u64 s_sums[AGG_SLOTS];
     __shared__ u32 s_carry[AGG_SLOTS];
-    __shared__ u32 s_row[FP_THREADS];  // stored row per event of the tile, or NONE32
-    __shared__ u64 s_ts[FP_THREADS];
     const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid == 0) s_tile = atomicAdd(F.tile_counter, 1u);
     for (u32 h = tid; h < AGG_SLOTS; h += FP_THREADS) {
         s_keys[h] = AGG_EMPTY;
         s_sums[h] = 0;
         s_carry[h] = 0;
     }
     __syncthreads();
-    const u32 tile = s_tile;
+    const u32 tile = blockIdx.x;
     const u32 i = tile * FP_THREADS + tid;
     const bool valid = i < F.n;
 
-    Transfer t;
     u8 r = FRES_SLOW;
-    u32 b = 0, ds = NONE32, cs = NONE32;
+    u32 b = 0;
     u64 ts = 0;
+    u128 id = 0;
     // batch of the event: one uniform binary search per wave, then a short walk
     // (a wave spans 64 events, so usually zero or one batch boundary)
     const u32 i0 = __builtin_amdgcn_readfirstlane(tile * FP_THREADS + wave * 64);
@@ -281,7 +280,9 @@ __global__ __launch_bounds__(FP_THREADS) __attribute__((amdgpu_waves_per_eu(FP_W
         while (F.b_start[b + 1] <= i) b++;
         const u32 bs = F.b_start[b], nbatch = F.b_start[b + 1] - bs;
         ts = F.b_ts[b] - nbatch + (i - bs) + 1;
-        t = F.ev[i];
+        Transfer t = F.ev[i];
+        id = t.id;
+        u32 ds = NONE32, cs = NONE32;
         r = fp_classify(T, F, t, i, ts, &ds, &cs);
         F.fres[i] = r;
         if (r == TB_CREATE_TRANSFER_OK) {
@@ -293,8 +294,13 @@ __global__ __launch_bounds__(FP_THREADS) __attribute__((amdgpu_waves_per_eu(FP_W
                 agg_add(s_keys, s_sums, s_carry, ds * 4 + pend, a);
                 agg_add(s_keys, s_sums, s_carry, cs * 4 + 2 + pend, a);
             }
+            // optimistic stored row (every predecessor accepted); fp_fix re-places it otherwise
+            t.timestamp = ts;
+            if (!(F.ablate & ABL_ROWS)) T.xrows[F.row_base + i] = t;
         } else if (r == FRES_SLOW) {
             atomicOr(&F.counters[CNT_FLAGS], (u32)FL_SLOW);
+        } else {
+            atomicAdd(&F.batch_counts[b], 1u);
         }
     }
     const bool ok = valid && r == TB_CREATE_TRANSFER_OK;
@@ -303,7 +309,7 @@ __global__ __launch_bounds__(FP_THREADS) __attribute__((amdgpu_waves_per_eu(FP_W
     // Strictly increasing ids across the whole call cannot repeat: then fp_dupcheck
     // has nothing to do (sequential ids, the benchmark's default id order).
     {
-        const u64 lo = valid ? (u64)t.id : ~0ull, hi = valid ? (u64)(t.id >> 64) : ~0ull;
+        const u64 lo = valid ? (u64)id : ~0ull, hi = valid ? (u64)(id >> 64) : ~0ull;
         u64 plo = __shfl_up((unsigned long long)lo, 1), phi = __shfl_up((unsigned long long)hi, 1);
         if (lane == 0) {
             if (i > 0 && valid) {
@@ -317,50 +323,47 @@ __global__ __launch_bounds__(FP_THREADS) __attribute__((amdgpu_waves_per_eu(FP_W
         const bool up = !valid || i == 0 || hi > phi || (hi == phi && lo > plo);
         if (__ballot(!up) && lane == 0) atomicOr(&F.counters[CNT_FLAGS], (u32)FL_NONMONO);
     }
-
-    // rank accepted events (stored rows) and failures (replies) across the call
-    const u64 lt = __lanemask_lt();
     const u64 okm = __ballot(ok), badm = __ballot(bad);
     u64 mts = ok ? ts : 0;
     for (int off = 32; off > 0; off >>= 1) mts = max(mts, (u64)__shfl_xor((unsigned long long)mts, off));
-    if (lane == 0) {
-        s_wok[wave] = __popcll(okm);
-        s_wbad[wave] = __popcll(badm);
-        s_maxts[wave] = mts;
-    }
     // componentwise id range of the tile's accepted ids (for the index key-range filter)
-    {
-        u64 mxl = ok ? (u64)t.id : 0, mxh = ok ? (u64)(t.id >> 64) : 0;
-        u64 mnl = ok ? (u64)t.id : ~0ull, mnh = ok ? (u64)(t.id >> 64) : ~0ull;
-        for (int off = 32; off > 0; off >>= 1) {
-            mxl = max(mxl, (u64)__shfl_xor((unsigned long long)mxl, off));
-            mxh = max(mxh, (u64)__shfl_xor((unsigned long long)mxh, off));
-            mnl = min(mnl, (u64)__shfl_xor((unsigned long long)mnl, off));
-            mnh = min(mnh, (u64)__shfl_xor((unsigned long long)mnh, off));
-        }
-        if (lane == 0) {
-            s_idr[wave][0] = mxl;
-            s_idr[wave][1] = mxh;
-            s_idr[wave][2] = mnl;
-            s_idr[wave][3] = mnh;
-        }
+    u64 mxl = ok ? (u64)id : 0, mxh = ok ? (u64)(id >> 64) : 0;
+    u64 mnl = ok ? (u64)id : ~0ull, mnh = ok ? (u64)(id >> 64) : ~0ull;
+    for (int off = 32; off > 0; off >>= 1) {
+        mxl = max(mxl, (u64)__shfl_xor((unsigned long long)mxl, off));
+        mxh = max(mxh, (u64)__shfl_xor((unsigned long long)mxh, off));
+        mnl = min(mnl, (u64)__shfl_xor((unsigned long long)mnl, off));
+        mnh = min(mnh, (u64)__shfl_xor((unsigned long long)mnh, off));
     }
-    __syncthreads();  // LDS sums and per-wave counts complete
-    u64 agg_ok = 0, agg_bad = 0, maxts = 0;
+    if (lane == 0) {
+        s_maxts[wave] = mts;
+        s_cnt[wave][0] = __popcll(okm);
+        s_cnt[wave][1] = __popcll(badm);
+        s_idr[wave][0] = mxl;
+        s_idr[wave][1] = mxh;
+        s_idr[wave][2] = mnl;
+        s_idr[wave][3] = mnh;
+    }
+    __syncthreads();  // LDS sums and per-wave figures complete
     if (wave == 0) {
-        for (int w = 0; w < FP_THREADS / 64; w++) {
-            agg_ok += s_wok[w];
-            agg_bad += s_wbad[w];
-            maxts = max(maxts, s_maxts[w]);
-        }
-        // publish this tile's aggregate before anything else, so successors can pass it
-        if (lane == 0)
-            __hip_atomic_store(&F.tile_status[tile], (tile == 0 ? ST_INC : ST_AGG) | agg_ok | (agg_bad << 31),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (lane < 4) {
             u64 v = s_idr[0][lane];
             for (int w = 1; w < FP_THREADS / 64; w++) v = lane < 2 ? max(v, s_idr[w][lane]) : min(v, s_idr[w][lane]);
             F.tile_idr[4 * tile + lane] = v;
+        }
+        if (lane == 0) {
+            u32 nok = 0, nbad = 0;
+            u64 maxts = 0;
+            for (int w = 0; w < FP_THREADS / 64; w++) {
+                nok += s_cnt[w][0];
+                nbad += s_cnt[w][1];
+                maxts = max(maxts, s_maxts[w]);
+            }
+            if (nok) {
+                atomicAdd(&F.counters[CNT_OK], nok);
+                atomicMax((unsigned long long*)T.commit_ts, (unsigned long long)maxts);
+            }
+            if (nbad) atomicAdd(&F.counters[CNT_BAD], nbad);
         }
     }
     // flush the tile's partial sums: u128 += (carry:sum) with u64 atomics.  All of a
@@ -370,103 +373,17 @@ __global__ __launch_bounds__(FP_THREADS) __attribute__((amdgpu_waves_per_eu(FP_W
     u64* wp[PER];
     u64 av[PER], old[PER];
     u32 cv[PER];
-    {
 #pragma unroll
-        for (int k = 0; k < PER; k++) {
-            const u32 h = tid + k * FP_THREADS;
-            const u32 key = s_keys[h];
-            wp[k] = key == AGG_EMPTY ? nullptr : (u64*)acc_field(T, key);
-            av[k] = s_sums[h];
-            cv[k] = s_carry[h];
-        }
+    for (int k = 0; k < PER; k++) {
+        const u32 h = tid + k * FP_THREADS;
+        const u32 key = s_keys[h];
+        wp[k] = key == AGG_EMPTY ? nullptr : (u64*)acc_field(T, key);
+        av[k] = s_sums[h];
+        cv[k] = s_carry[h];
+    }
 #pragma unroll
-        for (int k = 0; k < PER; k++)
-            old[k] = wp[k] ? atomicAdd((unsigned long long*)&wp[k][0], (unsigned long long)av[k]) : 0;
-    }
-    if (wave == 0) {
-        // decoupled look-back, 64 predecessors per step (lane l reads tile top - l)
-        const u64 agg = agg_ok | (agg_bad << 31);
-        u64 excl = 0;
-        if (tile > 0 && !(F.ablate & ABL_LOOKBACK)) {
-            long long top = (long long)tile - 1;
-            for (bool done = false; !done;) {
-                const long long j = top - lane;
-                u64 st = ST_INC;  // before tile 0: an inclusive prefix of zero
-                if (j >= 0) {
-                    u32 spins = 0;
-                    for (;;) {
-                        st = __hip_atomic_load(&F.tile_status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (st & ~ST_VAL) break;
-                        if (++spins > (1u << 24)) {
-                            atomicOr(&F.counters[CNT_FLAGS], (u32)FL_ERROR);
-                            st = ST_INC;
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(1);
-                    }
-                }
-                const u64 incm = __ballot((st & ST_INC) != 0);
-                u32 take = 64;
-                if (incm) {
-                    take = (u32)__ffsll((unsigned long long)incm);  // nearest inclusive predecessor
-                    done = true;
-                }
-                u64 v = lane < take ? (st & ST_VAL) : 0;
-                for (int off = 32; off > 0; off >>= 1) v += (u64)__shfl_xor((unsigned long long)v, off);
-                excl += v;
-                top -= 64;
-            }
-            if (lane == 0)
-                __hip_atomic_store(&F.tile_status[tile], ST_INC | (excl + agg), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (lane == 0) {
-            s_excl = excl;
-            if (agg_ok) {
-                atomicAdd(&F.counters[CNT_OK], (u32)agg_ok);
-                atomicMax((unsigned long long*)T.commit_ts, (unsigned long long)maxts);
-            }
-        }
-    }
-    __syncthreads();
-    const u64 excl = s_excl;
-    u32 wok = 0, wbad = 0;
-    for (u32 w = 0; w < wave; w++) { wok += s_wok[w]; wbad += s_wbad[w]; }
-    u32 row = NONE32;
-    if (ok) {
-        row = (u32)(F.row_base + (excl & 0x7FFFFFFFull) + wok + __popcll(okm & lt));
-    } else if (bad) {
-        const u64 pos = (excl >> 31) + wbad + __popcll(badm & lt);
-        F.results[pos] = {i - F.b_start[b], (u32)r};
-        atomicAdd(&F.batch_counts[b], 1u);
-    }
-    if (valid) F.rows[i] = row;
-    s_row[tid] = row;
-    s_ts[tid] = ts;
-    __syncthreads();
-    // Stored rows: the tile's events copied to their rows with whole-wave 1-KB
-    // accesses (lane = one 16-byte chunk; 8 chunks per 128-byte transfer), the
-    // timestamp chunk patched.  The second read of the events hits the L2.
-    if (!(F.ablate & ABL_ROWS)) {
-        const u32 base = tile * FP_THREADS;
-        const u32 nt = min((u32)FP_THREADS, F.n - base);
-        const uint4* src = (const uint4*)(F.ev + base);
-        uint4* dst = (uint4*)T.xrows;
-        for (u32 c = tid; c < nt * 8; c += FP_THREADS) {
-            const u32 e = c >> 3, part = c & 7;
-            const u32 rw = s_row[e];
-            if (rw == NONE32) continue;
-            uint4 v = src[c];
-            if (part == 7) {  // bytes 112..127: ledger, code, flags, timestamp
-                const u64 t8 = s_ts[e];
-                v.z = (u32)t8;
-                v.w = (u32)(t8 >> 32);
-            }
-            dst[(u64)rw * 8 + part] = v;
-        }
-    }
-    // carries of the flushed sums, last: the atomics' return latency hides behind
-    // the look-back and the row stores
+    for (int k = 0; k < PER; k++)
+        old[k] = wp[k] ? atomicAdd((unsigned long long*)&wp[k][0], (unsigned long long)av[k]) : 0;
 #pragma unroll
     for (int k = 0; k < PER; k++) {
         if (!wp[k]) continue;
@@ -485,19 +402,23 @@ __global__ void fp_dupcheck(Tables T, FastArgs F) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= F.n) return;
     F.gpos[i] = NONE32;
-    if (F.rows[i] == NONE32) return;
+    if (F.fres[i] != TB_CREATE_TRANSFER_OK) return;
     if (gtab_claim_is_dup(F, F.keys[i], i)) atomicOr(&F.counters[CNT_FLAGS], (u32)FL_SLOW);
 }
 
-__global__ void fp_index(Tables T, FastArgs F) {
+// Publish the accepted ids.  fixed = false: the launch right after fp_commit, which
+// stands down when the call had failures (rows not final yet) and always clears the
+// duplicate claims; fixed = true: after fp_fix, rows from F.rows.
+__global__ void fp_index(Tables T, FastArgs F, bool fixed) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     const u32 flags = F.counters[CNT_FLAGS];
-    if ((flags & FL_NONMONO) && i < F.n) {
+    if (!fixed && (flags & FL_NONMONO) && i < F.n) {
         // leave the claim table all-zero for the next call (also when falling back)
         const u32 g = F.gpos[i];
         if (g != NONE32) F.gtab[g] = 0;
     }
     if (flags & (FL_SLOW | FL_ERROR)) return;
+    if (!fixed && F.counters[CNT_BAD] != 0) return;
     if (blockIdx.x == 0 && threadIdx.x < 64) {
         // fold the tiles' id ranges into the index's key range (one wave)
         const u32 lane = threadIdx.x, ntiles = (F.n + FP_THREADS - 1) / FP_THREADS;
@@ -522,17 +443,39 @@ __global__ void fp_index(Tables T, FastArgs F) {
         }
     }
     if (i >= F.n) return;
-    const u32 row = F.rows[i];
-    if (row != NONE32) xidx_insert(T, F.keys[i], row);
+    if (F.fres[i] != TB_CREATE_TRANSFER_OK) return;
+    xidx_insert(T, F.keys[i], fixed ? F.rows[i] : (u32)(F.row_base + i));
 }
 
-// Per-call reset of the fast path's counters, look-back tiles and reply counts
-// (one launch instead of four fills).
-__global__ void fp_prep(FastArgs F, u32 ntiles) {
+// With failures: mask for the rank scan (bit0 accepted, bit1 failed).
+__global__ void fp_mask(FastArgs F, u8* mask) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < F.n) mask[i] = F.fres[i] == TB_CREATE_TRANSFER_OK ? 1 : 2;
+}
+
+// With failures: stored rows at their ranks (re-copied from the events, so the
+// order of the writes does not matter) and the sparse replies.
+__global__ void fp_fix(FastArgs F, Tables T, const uint4* rk) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= F.n) return;
+    const u32 b = fp_batch_of(F.b_start, F.nb, i);
+    const u32 bs = F.b_start[b];
+    const u8 r = F.fres[i];
+    if (r != TB_CREATE_TRANSFER_OK) {
+        F.results[rk[i].y] = {i - bs, (u32)r};  // concatenated replies
+        return;
+    }
+    const u32 row = (u32)(F.row_base + rk[i].x);
+    Transfer t = F.ev[i];
+    t.timestamp = F.b_ts[b] - (F.b_start[b + 1] - bs) + (i - bs) + 1;
+    T.xrows[row] = t;
+    F.rows[i] = row;
+}
+
+// Per-call reset of the fast path's counters and reply counts.
+__global__ void fp_prep(FastArgs F) {
     const u32 k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k < CNT_COUNT) F.counters[k] = 0;
-    if (k == 0) *F.tile_counter = 0;
-    if (k < ntiles) F.tile_status[k] = 0;
     if (k < F.nb) F.batch_counts[k] = 0;
 }
 
@@ -556,10 +499,10 @@ __global__ void fp_undo(Tables T, FastArgs F) {
 
 }  // namespace
 
+#define GRID(n) (u32)(((n) + 255) / 256), 256, 0, stream
+
 void fp_launch_prep(const FastArgs& F, hipStream_t stream) {
-    const u32 ntiles = (u32)fp_tiles(F.n);
-    const u32 m = std::max<u32>(std::max<u32>(ntiles, F.nb), CNT_COUNT);
-    fp_prep<<<(m + 255) / 256, 256, 0, stream>>>(F, ntiles);
+    fp_prep<<<GRID(std::max<u32>(F.nb, CNT_COUNT))>>>(F);
     HIP_CHECK(hipGetLastError());
 }
 
@@ -569,13 +512,21 @@ void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream) {
 }
 
 void fp_launch_index(const Tables& T, const FastArgs& F, hipStream_t stream) {
-    fp_dupcheck<<<(F.n + 255) / 256, 256, 0, stream>>>(T, F);
-    fp_index<<<(F.n + 255) / 256, 256, 0, stream>>>(T, F);
+    fp_dupcheck<<<GRID(F.n)>>>(T, F);
+    fp_index<<<GRID(F.n)>>>(T, F, false);
+    HIP_CHECK(hipGetLastError());
+}
+
+void fp_launch_fix(const Tables& T, const FastArgs& F, u8* mask, uint4* ranks, Scan3Scratch& sc, hipStream_t stream) {
+    fp_mask<<<GRID(F.n)>>>(F, mask);
+    scan3_exclusive(mask, ranks, F.n, sc, stream);
+    fp_fix<<<GRID(F.n)>>>(F, T, ranks);
+    fp_index<<<GRID(F.n)>>>(T, F, true);
     HIP_CHECK(hipGetLastError());
 }
 
 void fp_launch_undo(const Tables& T, const FastArgs& F, hipStream_t stream) {
-    fp_undo<<<(F.n + 255) / 256, 256, 0, stream>>>(T, F);
+    fp_undo<<<GRID(F.n)>>>(T, F);
     HIP_CHECK(hipGetLastError());
 }
 

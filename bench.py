@@ -47,6 +47,24 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
+def pmc_traffic(kernel: str, events_per_launch: float):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
+    (profiles/rNN/traffic.json, written by profiles/collect.sh on the same bench command:
+    2 x FETCH_SIZE + WRITE_SIZE per dispatch, MI355X_MICROARCH.md's gfx950 correction),
+    scaled to this run's events per launch.  None when no summary matches."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")), reverse=True):
+        try:
+            d = json.load(open(f))[kernel]
+        except (OSError, KeyError, ValueError):
+            continue
+        per_ev = d["traffic_bytes"] / d["events_per_launch"]
+        return round(per_ev * events_per_launch), (
+            f"{os.path.relpath(f, ROOT)}: {per_ev:.1f} B/transfer (2xFETCH_SIZE+WRITE_SIZE, "
+            f"rocprofv3 --pmc passes of this bench) x {events_per_launch:.0f} transfers per launch")
+    return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -149,6 +167,7 @@ def main():
     phase_ms_per_step = {names[i]: round(phase[i] / K, 4) for i in range(len(names))}
     commit_ms = phase[names.index("classify")] / K
     achieved = per_rank / K * COMMIT_BYTES_PER_TRANSFER / (commit_ms * 1e-3) / 1e9 if commit_ms > 0 else 0.0
+    traffic, traffic_src = pmc_traffic("fp_commit", per_rank / K)
     e2e_gbps = value / world * ALGO_BYTES_PER_TRANSFER / 1e9
     roofline = {
         "bound": "hbm",
@@ -156,7 +175,8 @@ def main():
         "peak": HBM_PEAK_GBPS,
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBPS, 5),
-        "traffic": None,
+        "traffic": traffic,
+        "traffic_source": traffic_src,
         "kernel": "fp_commit",
         "basis": f"{COMMIT_BYTES_PER_TRANSFER} B/transfer x {B * BATCH_MAX} transfers per launch "
                  f"/ fp_commit launch time ({commit_ms:.4f} ms, HIP events on the engine stream)",

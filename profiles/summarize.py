@@ -35,3 +35,18 @@ if ev:
         if fm + wm < ev:  # kernels that do not scale with the call
             continue
         print(f"{k:40s} fetch={fm/ev:7.1f} B (x2: {2*fm/ev:7.1f})  write={wm/ev:7.1f} B")
+    # Per-launch HBM traffic of every kernel that scales with the call, for bench.py's
+    # roofline.traffic: 2 x FETCH_SIZE (gfx950 half-count of wide reads) + WRITE_SIZE.
+    # Random 8/16/32-B accesses are uncalibrated (MI355X_MICROARCH.md), and Infinity-Cache
+    # hits are counted as fabric traffic, so this is an upper-bound estimate of HBM bytes.
+    import json
+    res = {}
+    for k in sorted({k for k, _ in agg}):
+        f, w = agg.get((k, "FETCH_SIZE")), agg.get((k, "WRITE_SIZE"))
+        if not f or not w or k.startswith("__amd"):
+            continue
+        fm, wm = sum(f) / len(f) * 1024, sum(w) / len(w) * 1024
+        res[k] = {"fetch_bytes_raw": fm, "write_bytes": wm, "traffic_bytes": 2 * fm + wm,
+                  "events_per_launch": ev}
+    if len(sys.argv) > 3:
+        json.dump(res, open(sys.argv[3], "w"), indent=1)

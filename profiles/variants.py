@@ -24,7 +24,7 @@ for spec in argv:
             print(name, "missing", lib, flush=True)
             continue
         env["TBGPU_LIB"] = lib
-    vals, commits, idx = [], [], []
+    vals, commits, idx, app = [], [], [], []
     for _ in range(reps):
         r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *bench_args], env=env,
                            capture_output=True, text=True, cwd=ROOT)
@@ -37,6 +37,7 @@ for spec in argv:
         vals.append(line["value"] / 1e9)
         commits.append(ph["classify"])
         idx.append(ph["index"])
+        app.append(ph["apply"])
     if vals:
         print(f"{name:12s} value max={max(vals):.3f} G/s  commit min={min(commits):.4f} ms  "
-              f"index min={min(idx):.4f} ms  all={[round(v, 3) for v in vals]}", flush=True)
+              f"apply min={min(app):.4f} ms  index min={min(idx):.4f} ms  all={[round(v, 3) for v in vals]}", flush=True)

@@ -381,6 +381,14 @@ void fp_commit(Tables T, FastArgs F) {
         av[k] = s_sums[h];
         cv[k] = s_carry[h];
     }
+#if defined(FP_NOFLUSH)  // timing-only variants (profiles/variants.py); results wrong
+    return;
+#elif defined(FP_NORET)
+#pragma unroll
+    for (int k = 0; k < PER; k++)
+        if (wp[k]) __hip_atomic_fetch_add((unsigned long long*)&wp[k][0], (unsigned long long)av[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+#endif
 #pragma unroll
     for (int k = 0; k < PER; k++)
         old[k] = wp[k] ? atomicAdd((unsigned long long*)&wp[k][0], (unsigned long long)av[k]) : 0;

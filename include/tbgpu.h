@@ -261,6 +261,45 @@ uint64_t tbgpu_create_accounts_batches(tbgpu_ctx* ctx, uint32_t batch_count,
                                        tb_create_accounts_result_t* results,
                                        uint32_t* result_counts);
 
+/* ------------------------------------------------------------------------ */
+/* Sharded commit (the ledger router is tigerbeetle_amd/shard.py) */
+/* ------------------------------------------------------------------------ */
+/* The reference has one state machine; sharded by ledger, each GPU's ctx commits
+ * the owner's sub-sequence of a routed step.  These entry points have no single
+ * reference counterpart: they carry what `execute` (src/state_machine.zig:1018-1083)
+ * derives from a batch's position -- the event timestamps and the linked-chain
+ * bounds -- for sub-batches whose events are not contiguous in their batch. */
+enum {
+    /* The chain this event belongs to continues on another shard after it: the
+     * event closes the local part of the chain (no linked_event_chain_open). */
+    TBGPU_CTL_CHAIN_END = 1u << 0,
+    /* The chain broke on another shard before this event: not evaluated, result
+     * linked_event_failed (execute's chain_broken arm, :1037-1040). */
+    TBGPU_CTL_SKIP = 1u << 1,
+};
+
+/* create_transfers over `batch_count` owner sub-batches.  `event_timestamps[i]`
+ * is event i's timestamp (T - n + index + 1 of its source batch).  `ctl` (may be
+ * NULL) holds TBGPU_CTL_* bits per event.  With `dry_run` nonzero the replies and
+ * the would-be commit timestamp are computed and nothing is stored (one call must
+ * then fit events_per_call_max).  `*commit_timestamp` receives the ctx's commit
+ * timestamp after the call (or, dry, what it would be).  Replies as in
+ * tbgpu_create_transfers_batches (host buffers). */
+uint64_t tbgpu_create_transfers_routed(tbgpu_ctx* ctx, uint32_t batch_count, const uint32_t* counts,
+                                       const tb_transfer_t* events, const uint64_t* event_timestamps,
+                                       const uint8_t* ctl, int dry_run,
+                                       tb_create_transfers_result_t* results, uint32_t* result_counts,
+                                       uint64_t* commit_timestamp);
+
+/* Copy committed transfers of another shard into this ctx's transfer table and id
+ * index, without balance or posted effects: the `exists` comparisons of
+ * :1370-1389 / :1500-1561 then see a colliding id committed elsewhere.  Returns 0. */
+int tbgpu_import_transfers(tbgpu_ctx* ctx, const tb_transfer_t* rows, uint32_t count);
+
+/* commit_timestamp = max(commit_timestamp, timestamp): the node-wide commit
+ * timestamp is the max over shards (:1366 advances it per created transfer). */
+void tbgpu_advance_commit_timestamp(tbgpu_ctx* ctx, uint64_t timestamp);
+
 /* execute_lookup_accounts / execute_lookup_transfers (src/state_machine.zig:1091-1126):
  * found objects are written densely in request order; returns the count. */
 uint32_t tbgpu_lookup_accounts(tbgpu_ctx* ctx, const tb_uint128_t* ids, uint32_t count, tb_account_t* out);

@@ -66,6 +66,12 @@ def lib():
         L.orc_export_history.argtypes = [vp, u64, u64, vp]
         L.orc_get_posted.restype = ctypes.c_int
         L.orc_get_posted.argtypes = [vp, U128]
+        L.orc_create_transfers_routed.restype = u64
+        L.orc_create_transfers_routed.argtypes = [vp, u32, vp, vp, vp, vp, ctypes.c_int, vp, vp,
+                                                  ctypes.POINTER(ctypes.c_uint64)]
+        L.orc_import_transfers.restype = ctypes.c_int
+        L.orc_import_transfers.argtypes = [vp, vp, u32]
+        L.orc_advance_commit_timestamp.argtypes = [vp, u64]
         L.orc_sum_overflows_u64.restype = ctypes.c_int
         L.orc_sum_overflows_u64.argtypes = [u64, u64]
         L.orc_sum_overflows_u128.restype = ctypes.c_int
@@ -117,6 +123,29 @@ class Oracle:
         self._L.orc_create_transfers_batches(self._h, len(cs), _ptr(ts), _ptr(cs), _ptr(events), _ptr(out),
                                              _ptr(rc), ctypes.byref(el))
         return out, rc, el.value
+
+    def create_transfers_routed(self, counts, events, event_ts, ctl=None, dry_run=False):
+        """Routed sub-batches (sharded commit, include/tbgpu.h): returns (results at each
+        sub-batch's event offset, result_counts, commit_timestamp after the call)."""
+        cs = np.ascontiguousarray(counts, dtype=np.uint32)
+        events = np.ascontiguousarray(events, dtype=TRANSFER_DTYPE)
+        ts = np.ascontiguousarray(event_ts, dtype=np.uint64)
+        c = None if ctl is None else np.ascontiguousarray(ctl, dtype=np.uint8)
+        out = np.zeros(max(len(events), 1), dtype=RESULT_DTYPE)
+        rc = np.zeros(len(cs), dtype=np.uint32)
+        cts = ctypes.c_uint64(0)
+        self._L.orc_create_transfers_routed(self._h, len(cs), _ptr(cs), _ptr(events), _ptr(ts),
+                                            None if c is None else _ptr(c), int(bool(dry_run)), _ptr(out),
+                                            _ptr(rc), ctypes.byref(cts))
+        return out, rc, cts.value
+
+    def import_transfers(self, rows: np.ndarray) -> None:
+        rows = np.ascontiguousarray(rows, dtype=TRANSFER_DTYPE)
+        if len(rows):
+            self._L.orc_import_transfers(self._h, _ptr(rows), len(rows))
+
+    def advance_commit_timestamp(self, ts: int) -> None:
+        self._L.orc_advance_commit_timestamp(self._h, int(ts))
 
     def create_accounts_batches(self, timestamps, counts, events):
         ts = np.ascontiguousarray(timestamps, dtype=np.uint64)

@@ -514,8 +514,12 @@ typedef uint32_t (*create_fn)(orc_t*, const void* event);
 static uint32_t create_account_v(orc_t* o, const void* e) { return create_account(o, (const tb_account_t*)e); }
 static uint32_t create_transfer_v(orc_t* o, const void* e) { return create_transfer(o, (const tb_transfer_t*)e); }
 
-static uint32_t execute(orc_t* o, uint64_t timestamp, const uint8_t* events, uint32_t n, size_t size,
-                        create_fn create, uint32_t* results /* pairs {index,result} */) {
+/* `ev_ts` / `ctl` (may be NULL): the routed form used by the sharded commit
+ * (include/tbgpu.h, tbgpu_create_transfers_routed) -- per-event timestamps and
+ * TBGPU_CTL_* chain control.  NULL reproduces execute exactly. */
+static uint32_t execute_ex(orc_t* o, uint64_t timestamp, const uint8_t* events, uint32_t n, size_t size,
+                           create_fn create, uint32_t* results /* pairs {index,result} */,
+                           const uint64_t* ev_ts, const uint8_t* ctl) {
     uint32_t count = 0;
     int64_t chain = -1;
     int chain_broken = 0;
@@ -525,17 +529,19 @@ static uint32_t execute(orc_t* o, uint64_t timestamp, const uint8_t* events, uin
         /* flags and timestamp share the layout tail for both structs */
         uint16_t flags; memcpy(&flags, event + 118, 2);
         uint64_t ts; memcpy(&ts, event + 120, 8);
-        const int linked = flags & 1; /* AccountFlags.linked / TransferFlags.linked */
+        /* AccountFlags.linked / TransferFlags.linked; a routed chain part ends where
+         * the router closed it (the chain continues on another shard) */
+        const int linked = (flags & 1) && !(ctl && (ctl[index] & TBGPU_CTL_CHAIN_END));
         uint32_t result;
         if (linked && chain < 0) { chain = index; assert(!chain_broken); scope_open(o); }
         if (linked && index == n - 1) {
             result = TB_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN; /* == account code 2 */
-        } else if (chain_broken) {
+        } else if (chain_broken || (ctl && (ctl[index] & TBGPU_CTL_SKIP))) {
             result = TB_CREATE_TRANSFER_LINKED_EVENT_FAILED;
         } else if (ts != 0) {
             result = TB_CREATE_TRANSFER_TIMESTAMP_MUST_BE_ZERO;
         } else {
-            ts = timestamp - n + index + 1;
+            ts = ev_ts ? ev_ts[index] : timestamp - n + index + 1;
             memcpy(event + 120, &ts, 8);
             result = create(o, event);
         }
@@ -566,6 +572,11 @@ static uint32_t execute(orc_t* o, uint64_t timestamp, const uint8_t* events, uin
     }
     assert(chain < 0 && !chain_broken);
     return count;
+}
+
+static uint32_t execute(orc_t* o, uint64_t timestamp, const uint8_t* events, uint32_t n, size_t size,
+                        create_fn create, uint32_t* results) {
+    return execute_ex(o, timestamp, events, n, size, create, results, NULL, NULL);
 }
 
 /* ------------------------------------------------------------------ API --- */
@@ -686,3 +697,70 @@ uint64_t orc_commit_timestamp(orc_t* o) { return o->commit_timestamp; }
 
 int orc_sum_overflows_u64(uint64_t a, uint64_t b) { return sum_overflows_u64(a, b); }
 int orc_sum_overflows_u128(tb_uint128_t a, tb_uint128_t b) { return sum_overflows_u128(G(a), G(b)); }
+
+/* ------------------------------------------------------- sharded commit --- */
+
+static void map_copy(map_t* dst, const map_t* src) {
+    *dst = *src;
+    dst->keys = (u128*)malloc(src->cap * sizeof(u128));
+    dst->vals = (uint64_t*)malloc(src->cap * sizeof(uint64_t));
+    dst->used = (uint8_t*)malloc(src->cap);
+    memcpy(dst->keys, src->keys, src->cap * sizeof(u128));
+    memcpy(dst->vals, src->vals, src->cap * sizeof(uint64_t));
+    memcpy(dst->used, src->used, src->cap);
+}
+
+static void* dup_array(const void* p, uint64_t cap, size_t elem) {
+    void* q = malloc((cap ? cap : 1) * elem);
+    if (p && cap) memcpy(q, p, cap * elem);
+    return q;
+}
+
+/* Deep copy: a dry run executes on a clone (tbgpu_create_transfers_routed). */
+static orc_t* orc_clone(const orc_t* o) {
+    orc_t* c = (orc_t*)calloc(1, sizeof(orc_t));
+    *c = *o;
+    map_copy(&c->account_map, &o->account_map);
+    map_copy(&c->transfer_map, &o->transfer_map);
+    map_copy(&c->posted_map, &o->posted_map);
+    c->accounts = (tb_account_t*)dup_array(o->accounts, o->accounts_cap, sizeof(tb_account_t));
+    c->transfers = (tb_transfer_t*)dup_array(o->transfers, o->transfers_cap, sizeof(tb_transfer_t));
+    c->history = (tb_account_history_t*)dup_array(o->history, o->history_cap, sizeof(tb_account_history_t));
+    c->undo = (undo_t*)dup_array(o->undo, o->undo_cap, sizeof(undo_t));
+    return c;
+}
+
+uint64_t orc_create_transfers_routed(orc_t* o, uint32_t batch_count, const uint32_t* counts,
+                                     const tb_transfer_t* events, const uint64_t* event_ts, const uint8_t* ctl,
+                                     int dry_run, tb_create_transfers_result_t* results, uint32_t* result_counts,
+                                     uint64_t* commit_timestamp) {
+    orc_t* x = dry_run ? orc_clone(o) : o;
+    uint64_t off = 0, total = 0;
+    for (uint32_t b = 0; b < batch_count; b++) {
+        uint32_t c = execute_ex(x, 0, (const uint8_t*)(events + off), counts[b], sizeof(tb_transfer_t),
+                                create_transfer_v, (uint32_t*)(results + off), event_ts + off,
+                                ctl ? ctl + off : NULL);
+        result_counts[b] = c;
+        total += c;
+        off += counts[b];
+    }
+    if (commit_timestamp) *commit_timestamp = x->commit_timestamp;
+    if (dry_run) orc_free(x);
+    return total;
+}
+
+int orc_import_transfers(orc_t* o, const tb_transfer_t* rows, uint32_t count) {
+    for (uint32_t i = 0; i < count; i++) {
+        if (map_get(&o->transfer_map, G(rows[i].id), NULL)) continue;  /* already held */
+        o->transfers = (tb_transfer_t*)grow(o->transfers, &o->transfers_cap, o->transfers_len + 1,
+                                            sizeof(tb_transfer_t));
+        o->transfers[o->transfers_len] = rows[i];
+        map_put_new(&o->transfer_map, G(rows[i].id), o->transfers_len);
+        o->transfers_len++;
+    }
+    return 0;
+}
+
+void orc_advance_commit_timestamp(orc_t* o, uint64_t timestamp) {
+    if (timestamp > o->commit_timestamp) o->commit_timestamp = timestamp;
+}

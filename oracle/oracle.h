@@ -41,6 +41,16 @@ uint64_t orc_create_accounts_batches(orc_t* o, uint32_t batch_count, const uint6
                                      const uint32_t* counts, const tb_account_t* events,
                                      tb_create_accounts_result_t* results, uint32_t* result_counts);
 
+/* Sharded commit: the routed form of create_transfers and its helpers, with the
+ * semantics of tbgpu_create_transfers_routed / tbgpu_import_transfers /
+ * tbgpu_advance_commit_timestamp (include/tbgpu.h). */
+uint64_t orc_create_transfers_routed(orc_t* o, uint32_t batch_count, const uint32_t* counts,
+                                     const tb_transfer_t* events, const uint64_t* event_ts, const uint8_t* ctl,
+                                     int dry_run, tb_create_transfers_result_t* results, uint32_t* result_counts,
+                                     uint64_t* commit_timestamp);
+int orc_import_transfers(orc_t* o, const tb_transfer_t* rows, uint32_t count);
+void orc_advance_commit_timestamp(orc_t* o, uint64_t timestamp);
+
 uint32_t orc_lookup_accounts(orc_t* o, const tb_uint128_t* ids, uint32_t count, tb_account_t* out);
 uint32_t orc_lookup_transfers(orc_t* o, const tb_uint128_t* ids, uint32_t count, tb_transfer_t* out);
 int orc_set_balances(orc_t* o, tb_uint128_t id, tb_uint128_t dp, tb_uint128_t dpo, tb_uint128_t cp,

@@ -1,0 +1,19 @@
+"""Sharded commit with the HIP engine as every rank's shard backend (2 ranks on one
+GPU, gloo for the router's collectives): tbgpu_create_transfers_routed with chain
+control and dry runs, and tbgpu_import_transfers, against the single CPU state
+machine over the router's global order (tests/test_shard.py for the protocol)."""
+import pytest
+
+from tests.test_shard import _check
+
+
+@pytest.mark.gpu
+def test_gpu_sharded_flag_mix():
+    stats = _check(("mix", 21, 2, 3, 2), 2, kind="gpu")
+    assert stats["dry_rounds"] > 0
+
+
+@pytest.mark.gpu
+def test_gpu_sharded_config4():
+    stats = _check(("c4", 5, 2, 2, 2), 2, kind="gpu")
+    assert stats["dry_rounds"] > 0

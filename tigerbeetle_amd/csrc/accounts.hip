@@ -241,6 +241,20 @@ __global__ void k_get_posted(Tables T, u128 id, int* status) {
     *status = f == 0 ? -1 : (f == 1 ? 0 : 1);
 }
 
+// Foreign rows (tbgpu_import_transfers): stored rows + id index + key range, no
+// balance or posted effects.
+__global__ void import_transfers(Tables T, const Transfer* rows, u32 n, u64 row_base) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Transfer t = rows[i];
+    T.xrows[row_base + i] = t;
+    xidx_insert(T, t.id, (u32)(row_base + i));
+    atomicMax((unsigned long long*)&T.idr[0], (unsigned long long)(u64)t.id);
+    atomicMax((unsigned long long*)&T.idr[1], (unsigned long long)(u64)(t.id >> 64));
+    atomicMin((unsigned long long*)&T.idr[2], (unsigned long long)(u64)t.id);
+    atomicMin((unsigned long long*)&T.idr[3], (unsigned long long)(u64)(t.id >> 64));
+}
+
 }  // namespace
 
 #define GRID(n) (u32)(((n) + 255) / 256), 256, 0, stream
@@ -284,4 +298,9 @@ void launch_set_balances(const Tables& T, u128 id, Bal4 b, int* status, hipStrea
 }
 void launch_get_posted(const Tables& T, u128 id, int* status, hipStream_t stream) {
     k_get_posted<<<1, 1, 0, stream>>>(T, id, status);
+}
+
+void launch_import_transfers(const Tables& T, const Transfer* rows, u32 n, u64 row_base, hipStream_t stream) {
+    import_transfers<<<(n + 255) / 256, 256, 0, stream>>>(T, rows, n, row_base);
+    HIP_CHECK(hipGetLastError());
 }

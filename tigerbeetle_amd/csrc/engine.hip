@@ -93,6 +93,14 @@ struct tbgpu_ctx {
     u128* f_keys = nullptr;
     u32* f_rows = nullptr;
     u64* f_tile_idr = nullptr;
+    // routed (sharded) calls: per-event timestamps / chain control of the current
+    // chunk in device memory (null for ordinary calls), dry-run flag and sink
+    u64* rt_ts_buf = nullptr;
+    u8* rt_ctl_buf = nullptr;
+    u64* rt_dry_ts = nullptr;
+    const u64* rt_ev_ts = nullptr;
+    const u8* rt_ctl = nullptr;
+    bool rt_dry = false;
     hipEvent_t ev0, ev1;
     // phase profiler: consecutive marks on the ctx stream; segment k belongs to
     // the phase opened by mark k.
@@ -158,6 +166,9 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->f_keys = dalloc<u128>(n, &B);
     c->f_rows = dalloc<u32>(n, &B);
     c->f_tile_idr = dalloc<u64>(4 * (fp_tiles(nmax) + 1), &B);
+    c->rt_ts_buf = dalloc<u64>(n, &B);
+    c->rt_ctl_buf = dalloc<u8>(n, &B);
+    c->rt_dry_ts = dalloc<u64>(1, &B);
     HIP_CHECK(hipHostMalloc((void**)&c->h_counters, CNT_COUNT * sizeof(u32), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc((void**)&c->h_counts, c->bmax * sizeof(u32), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc((void**)&c->h_stage_ts, c->bmax * sizeof(u64), hipHostMallocDefault));
@@ -266,7 +277,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
                     c->sval_s, c->spos, c->bb, c->ss.keys_tmp, c->ss.vals_tmp, c->ss.hist, c->side_tiles,
                     c->sc.tile_sums, c->fres, c->mask, c->ranks, c->res_buf, c->counts, c->counters, c->status,
                     c->f_gtab, c->f_gpos, c->f_keys, c->f_rows,
-                    c->f_tile_idr};
+                    c->f_tile_idr, c->rt_ts_buf, c->rt_ctl_buf, c->rt_dry_ts};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     for (EvalState& s : c->st) {
         void* q[] = {s.res, s.ok, s.pref, s.cfail, s.amt, s.pamt, s.dpend, s.dpost};
@@ -347,6 +358,10 @@ static TrArgs make_tr_args(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb) {
     const u64 g = std::min<u64>(c->gcap, pow2_at_least(4ull * std::max<u32>(n, 1)));
     C.gmask = g - 1;
     C.counters = c->counters;
+    C.ev_ts = c->rt_ev_ts;
+    C.ctl = c->rt_ctl;
+    C.dry = c->rt_dry ? 1u : 0u;
+    C.commit_ts = c->rt_dry ? c->rt_dry_ts : c->T.commit_ts;
     return C;
 }
 
@@ -356,7 +371,7 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tb_create_
                      u32* counts_host) {
     hipStream_t s = c->stream;
     FastArgs F{};
-    F.ev = ev; F.n = n; F.nb = nb; F.b_start = c->b_start; F.b_ts = c->b_ts;
+    F.ev = ev; F.n = n; F.nb = nb; F.b_start = c->b_start; F.b_ts = c->b_ts; F.ev_ts = c->rt_ev_ts;
     F.gtab = c->f_gtab;
     F.gpos = c->f_gpos;
     F.gmask = std::min<u64>(c->f_gcap, pow2_at_least(2ull * n)) - 1;
@@ -422,7 +437,10 @@ static void run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
         std::fill(counts_host, counts_host + nb, 0u);
         return;
     }
-    if (!(c->opt.flags & TBGPU_OPT_FORCE_GENERAL) && try_fast(c, ev, n, nb, results_dev, counts_host)) return;
+    // the fast path knows no chains, so calls carrying chain control or a dry run
+    // take the fixed point
+    const bool fast_ok = !(c->opt.flags & TBGPU_OPT_FORCE_GENERAL) && !c->rt_ctl && !c->rt_dry;
+    if (fast_ok && try_fast(c, ev, n, nb, results_dev, counts_host)) return;
     prof_mark(c, PH_CLASSIFY);
     HIP_CHECK(hipMemsetAsync(c->counters, 0, CNT_COUNT * sizeof(u32), s));
     HIP_CHECK(hipMemsetAsync(c->gclaim, 0, g * sizeof(u32), s));
@@ -490,17 +508,19 @@ static void run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
     if (c->n_hist + tot.z > c->hist_cap) tbgpu_fatal("create_transfers", "history_max exceeded", __FILE__, __LINE__);
     SA.ok = A->ok; SA.dpend = A->dpend; SA.dpost = A->dpost;
     tr_launch_apply(c->T, C, *A, c->fres, c->ranks, c->spos, c->bb, c->n_rows, c->n_hist, results_dev, c->counts, s);
-    side_final_balances(SA, m, inv_acc, c->bb, c->T.acc, c->T.big, s);
+    if (!c->rt_dry) side_final_balances(SA, m, inv_acc, c->bb, c->T.acc, c->T.big, s);
     prof_mark(c, PH_END);
     HIP_CHECK(hipMemcpyAsync(counts_host, c->counts, nb * sizeof(u32), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
+    if (c->rt_dry) return;
     c->n_rows += tot.x;
     c->n_hist += tot.z;
 }
 
 static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t* timestamps, const uint32_t* counts,
                                   const Transfer* ev_src, bool src_device, tb_create_transfers_result_t* results,
-                                  bool dst_device, uint32_t* result_counts) {
+                                  bool dst_device, uint32_t* result_counts, const uint64_t* ev_ts_host = nullptr,
+                                  const uint8_t* ctl_host = nullptr) {
     HIP_CHECK(hipSetDevice(c->device));
     HIP_CHECK(hipEventRecord(c->ev0, c->stream));
     std::vector<u32> starts;
@@ -519,6 +539,16 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         } else {
             HIP_CHECK(hipMemcpyAsync(c->ev_buf, ev_src + ev_off, (u64)n * 128, hipMemcpyHostToDevice, c->stream));
             ev = (const Transfer*)c->ev_buf;
+        }
+        c->rt_ev_ts = nullptr;
+        c->rt_ctl = nullptr;
+        if (ev_ts_host) {
+            HIP_CHECK(hipMemcpyAsync(c->rt_ts_buf, ev_ts_host + ev_off, (u64)n * 8, hipMemcpyHostToDevice, c->stream));
+            c->rt_ev_ts = c->rt_ts_buf;
+        }
+        if (ctl_host) {
+            HIP_CHECK(hipMemcpyAsync(c->rt_ctl_buf, ctl_host + ev_off, n, hipMemcpyHostToDevice, c->stream));
+            c->rt_ctl = c->rt_ctl_buf;
         }
         tb_create_transfers_result_t* rdev =
             dst_device ? results + total : (tb_create_transfers_result_t*)c->res_buf;
@@ -541,6 +571,72 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
     c->stats.sorts = sorts;
     c->stats.device_ms = ms;
     return total;
+}
+
+extern "C" uint64_t tbgpu_create_transfers_routed(tbgpu_ctx* c, uint32_t batch_count, const uint32_t* counts,
+                                                  const tb_transfer_t* events, const uint64_t* event_timestamps,
+                                                  const uint8_t* ctl, int dry_run,
+                                                  tb_create_transfers_result_t* results, uint32_t* result_counts,
+                                                  uint64_t* commit_timestamp) {
+    HIP_CHECK(hipSetDevice(c->device));
+    u64 n = 0;
+    for (u32 b = 0; b < batch_count; b++) n += counts[b];
+    if (dry_run && (n > c->nmax || batch_count > c->bmax - 2))
+        tbgpu_fatal("create_transfers_routed", "a dry run must fit one call (events_per_call_max)", __FILE__, __LINE__);
+    // the batch timestamps only order the batches here: every event carries its own
+    std::vector<u64> bts(batch_count, 0);
+    for (u32 b = 0; b < batch_count; b++) bts[b] = counts[b] ? event_timestamps[0] : 0;
+    c->rt_dry = dry_run != 0;
+    if (c->rt_dry) {
+        HIP_CHECK(hipMemcpyAsync(c->rt_dry_ts, c->T.commit_ts, sizeof(u64), hipMemcpyDeviceToDevice, c->stream));
+    }
+    const u64 total = transfers_batches(c, batch_count, bts.data(), counts, (const Transfer*)events, false, results,
+                                        false, result_counts, event_timestamps, ctl);
+    c->rt_ev_ts = nullptr;
+    c->rt_ctl = nullptr;
+    u64 ts = 0;
+    HIP_CHECK(hipMemcpy(&ts, c->rt_dry ? c->rt_dry_ts : c->T.commit_ts, sizeof(u64), hipMemcpyDeviceToHost));
+    c->rt_dry = false;
+    if (commit_timestamp) *commit_timestamp = ts;
+    return total;
+}
+
+extern "C" int tbgpu_import_transfers(tbgpu_ctx* c, const tb_transfer_t* rows, uint32_t count) {
+    HIP_CHECK(hipSetDevice(c->device));
+    if (count == 0) return 0;
+    // rows already held (committed here or imported before) are skipped: rows are
+    // immutable, and the id index must hold each id once
+    std::vector<tb_uint128_t> ids(count);
+    for (u32 i = 0; i < count; i++) ids[i] = rows[i].id;
+    std::vector<tb_transfer_t> found(count);
+    const u32 held = tbgpu_lookup_transfers(c, ids.data(), count, found.data());
+    std::vector<tb_transfer_t> keep;
+    keep.reserve(count);
+    for (u32 i = 0, f = 0; i < count; i++) {
+        if (f < held && found[f].id.lo == rows[i].id.lo && found[f].id.hi == rows[i].id.hi) { f++; continue; }
+        bool dup = false;  // a repeated id within this call
+        for (const tb_transfer_t& k : keep) dup |= k.id.lo == rows[i].id.lo && k.id.hi == rows[i].id.hi;
+        if (!dup) keep.push_back(rows[i]);
+    }
+    const u64 n = keep.size();
+    if (c->n_rows + n > c->xrow_cap) tbgpu_fatal("import_transfers", "transfers_max exceeded", __FILE__, __LINE__);
+    u64 off = 0;
+    while (off < n) {
+        const u32 k = (u32)std::min<u64>(n - off, c->nmax);
+        HIP_CHECK(hipMemcpyAsync(c->ev_buf, keep.data() + off, (u64)k * 128, hipMemcpyHostToDevice, c->stream));
+        launch_import_transfers(c->T, (const Transfer*)c->ev_buf, k, c->n_rows, c->stream);
+        HIP_CHECK(hipStreamSynchronize(c->stream));
+        c->n_rows += k;
+        off += k;
+    }
+    return 0;
+}
+
+extern "C" void tbgpu_advance_commit_timestamp(tbgpu_ctx* c, uint64_t timestamp) {
+    HIP_CHECK(hipSetDevice(c->device));
+    u64 v = 0;
+    HIP_CHECK(hipMemcpy(&v, c->T.commit_ts, sizeof(u64), hipMemcpyDeviceToHost));
+    if (timestamp > v) HIP_CHECK(hipMemcpy(c->T.commit_ts, &timestamp, sizeof(u64), hipMemcpyHostToDevice));
 }
 
 extern "C" uint32_t tbgpu_create_transfers(tbgpu_ctx* c, uint64_t timestamp, const tb_transfer_t* events,

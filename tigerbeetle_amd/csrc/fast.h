@@ -8,6 +8,7 @@ struct FastArgs {
     u32 nb;
     const u32* b_start;
     const u64* b_ts;
+    const u64* ev_ts;   // [n] event timestamps (routed sub-batches) or null
     u32* gtab;          // duplicate-id claims (event + 1), all-zero between calls
     u32* gpos;          // slot each event claimed (cleared again by fp_index)
     u64 gmask;

@@ -279,7 +279,7 @@ void fp_commit(Tables T, FastArgs F) {
     if (valid) {
         while (F.b_start[b + 1] <= i) b++;
         const u32 bs = F.b_start[b], nbatch = F.b_start[b + 1] - bs;
-        ts = F.b_ts[b] - nbatch + (i - bs) + 1;
+        ts = F.ev_ts ? F.ev_ts[i] : F.b_ts[b] - nbatch + (i - bs) + 1;
         Transfer t = F.ev[i];
         id = t.id;
         u32 ds = NONE32, cs = NONE32;
@@ -475,7 +475,7 @@ __global__ void fp_fix(FastArgs F, Tables T, const uint4* rk) {
     }
     const u32 row = (u32)(F.row_base + rk[i].x);
     Transfer t = F.ev[i];
-    t.timestamp = F.b_ts[b] - (F.b_start[b + 1] - bs) + (i - bs) + 1;
+    t.timestamp = F.ev_ts ? F.ev_ts[i] : F.b_ts[b] - (F.b_start[b + 1] - bs) + (i - bs) + 1;
     T.xrows[row] = t;
     F.rows[i] = row;
 }

@@ -8,6 +8,10 @@ struct TrArgs {
     u32 nb;               // batch count
     const u32* b_start;   // [nb + 1] event offset of each batch
     const u64* b_ts;      // [nb] prepare timestamp of each batch
+    const u64* ev_ts;     // [n] event timestamps (routed sub-batches) or null
+    const u8* ctl;        // [n] TBGPU_CTL_* bits (chains spanning shards) or null
+    u64* commit_ts;       // commit_timestamp sink (T.commit_ts, or a scratch word when dry)
+    u32 dry;              // dry run: replies only, no state change
     u64* ts;              // assigned event timestamps
     u32* cs;              // linked-chain start (== index for standalone events)
     u32* ce;              // linked-chain end (inclusive)
@@ -82,4 +86,5 @@ void ac_launch_apply(const Tables& T, const AcArgs& C, const u8* ok, const u8* f
 void launch_lookup_accounts(const Tables& T, const u128* ids, u32 n, Account* out, u8* found, hipStream_t stream);
 void launch_lookup_transfers(const Tables& T, const u128* ids, u32 n, Transfer* out, u8* found, hipStream_t stream);
 void launch_set_balances(const Tables& T, u128 id, Bal4 b, int* status, hipStream_t stream);
+void launch_import_transfers(const Tables& T, const Transfer* rows, u32 n, u64 row_base, hipStream_t stream);
 void launch_get_posted(const Tables& T, u128 id, int* status, hipStream_t stream);

@@ -77,13 +77,18 @@ __global__ void tr_classify(Tables T, TrArgs C) {
     const u32 bs = C.b_start[b], be = C.b_start[b + 1];
     const u32 nbatch = be - bs, k = i - bs;
     const Transfer t = C.ev[i];
-    const u64 ts = C.b_ts[b] - nbatch + k + 1;
+    const u64 ts = C.ev_ts ? C.ev_ts[i] : C.b_ts[b] - nbatch + k + 1;
     C.ts[i] = ts;
 
+    // chain bounds: `linked` unless the router closed the local part of a chain
+    // that continues on another shard (TBGPU_CTL_CHAIN_END)
+    auto linked = [&](u32 j) {
+        return (C.ev[j].flags & TF_LINKED) && !(C.ctl && (C.ctl[j] & TBGPU_CTL_CHAIN_END));
+    };
     u32 s = i;
-    while (s > bs && (C.ev[s - 1].flags & TF_LINKED)) s--;
+    while (s > bs && linked(s - 1)) s--;
     u32 e = i;
-    while (e + 1 < be && (C.ev[e].flags & TF_LINKED)) e++;
+    while (e + 1 < be && linked(e)) e++;
     C.cs[i] = s;
     C.ce[i] = e;
     u32 fl = (s != e) ? FL_CHAINS : 0u;
@@ -92,8 +97,10 @@ __global__ void tr_classify(Tables T, TrArgs C) {
     u32 gslot = NONE32, pslot = NONE32;
     u8 sres;
     const u16 f = t.flags;
-    if ((f & TF_LINKED) && k == nbatch - 1) {
+    if (linked(i) && k == nbatch - 1) {
         sres = TB_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN;
+    } else if (C.ctl && (C.ctl[i] & TBGPU_CTL_SKIP)) {
+        sres = TB_CREATE_TRANSFER_LINKED_EVENT_FAILED;  // chain broken on another shard
     } else if (t.timestamp != 0) {
         sres = TB_CREATE_TRANSFER_TIMESTAMP_MUST_BE_ZERO;
     } else if (f & 0xFFC0u) {
@@ -567,7 +574,7 @@ __global__ void tr_mask(Tables T, TrArgs C, EvalState S, u8* fres, u8* mask) {
     // commit_timestamp is a plain field, not undone by scope_close(.discard): every
     // create_transfer that returned ok before its chain broke advanced it (:1366).
     if ((S.ok[i] & 1) && (cf == NONE32 || i < cf))
-        atomicMax((unsigned long long*)T.commit_ts, (unsigned long long)C.ts[i]);
+        atomicMax((unsigned long long*)C.commit_ts, (unsigned long long)C.ts[i]);
 }
 
 __global__ void tr_apply(Tables T, TrArgs C, EvalState S, const u8* __restrict__ fres, const uint4* __restrict__ rk,
@@ -583,7 +590,7 @@ __global__ void tr_apply(Tables T, TrArgs C, EvalState S, const u8* __restrict__
         results[q.y] = {i - C.b_start[b], (u32)r};
         return;
     }
-    if (!(S.ok[i] & 2)) return;
+    if (C.dry || !(S.ok[i] & 2)) return;
     const Transfer t = C.ev[i];
     const u64 row = row_base + q.x;
     const Transfer s = load_ref(T, C, S, i);
@@ -684,6 +691,6 @@ void tr_launch_apply(const Tables& T, const TrArgs& C, const EvalState& S, const
                      const u32* spos, const Bal4* bb, u64 row_base, u64 hist_base,
                      tb_create_transfers_result_t* results, u32* counts, hipStream_t stream) {
     tr_apply<<<GRID(C.n)>>>(T, C, S, fres, rk, spos, bb, row_base, hist_base, results);
-    tr_range<<<GRID(C.n)>>>(T, C, S);
+    if (!C.dry) tr_range<<<GRID(C.n)>>>(T, C, S);
     batch_counts<<<GRID(C.nb)>>>(C.b_start, C.nb, rk, counts);
 }

@@ -91,6 +91,12 @@ def lib():
     L.tbgpu_get_posted.argtypes = [vp, U128]
     L.tbgpu_last_stats.argtypes = [vp, ctypes.POINTER(Stats)]
     L.tbgpu_set_profiling.argtypes = [vp, ctypes.c_int]
+    L.tbgpu_create_transfers_routed.restype = u64
+    L.tbgpu_create_transfers_routed.argtypes = [vp, u32, vp, vp, vp, vp, ctypes.c_int, vp, vp,
+                                                ctypes.POINTER(ctypes.c_uint64)]
+    L.tbgpu_import_transfers.restype = ctypes.c_int
+    L.tbgpu_import_transfers.argtypes = [vp, vp, u32]
+    L.tbgpu_advance_commit_timestamp.argtypes = [vp, u64]
     L.tbgpu_last_error.restype = ctypes.c_int
     L.tbgpu_last_error.argtypes = [vp, ctypes.c_char_p, u32]
     _lib = L
@@ -163,6 +169,29 @@ class Engine:
                                                               ctypes.c_void_p(events_ptr),
                                                               ctypes.c_void_p(results_ptr), _ptr(rc))
         return total, rc
+
+    def create_transfers_routed(self, counts, events, event_ts, ctl=None, dry_run=False):
+        """Owner sub-batches of a routed step (tbgpu_create_transfers_routed): returns
+        (results at each sub-batch's event offset, result_counts, commit_timestamp)."""
+        cs = np.ascontiguousarray(counts, dtype=np.uint32)
+        events = np.ascontiguousarray(events, dtype=TRANSFER_DTYPE)
+        ts = np.ascontiguousarray(event_ts, dtype=np.uint64)
+        c = None if ctl is None else np.ascontiguousarray(ctl, dtype=np.uint8)
+        out = np.zeros(max(len(events), 1), dtype=RESULT_DTYPE)
+        rc = np.zeros(len(cs), dtype=np.uint32)
+        cts = ctypes.c_uint64(0)
+        self._L.tbgpu_create_transfers_routed(self._h, len(cs), _ptr(cs), _ptr(events), _ptr(ts),
+                                              None if c is None else _ptr(c), int(bool(dry_run)), _ptr(out),
+                                              _ptr(rc), ctypes.byref(cts))
+        return out, rc, cts.value
+
+    def import_transfers(self, rows: np.ndarray) -> None:
+        rows = np.ascontiguousarray(rows, dtype=TRANSFER_DTYPE)
+        if len(rows):
+            self._L.tbgpu_import_transfers(self._h, _ptr(rows), len(rows))
+
+    def advance_commit_timestamp(self, ts: int) -> None:
+        self._L.tbgpu_advance_commit_timestamp(self._h, int(ts))
 
     def create_accounts_batches(self, timestamps, counts, events):
         ts = np.ascontiguousarray(timestamps, dtype=np.uint64)

@@ -1,0 +1,578 @@
+"""Ledger-sharded commit across GPUs: one process per GPU.
+
+The reference has a single state machine that commits batches one at a time
+(`StateMachine.commit`, src/state_machine.zig:894-928).  Here the state is
+partitioned by ledger -- a valid transfer has `dr.ledger == cr.ledger ==
+t.ledger` (:1280-1281) -- and each rank's engine owns the balances, stored
+transfers and posted entries of its ledgers.  Results are those of the single
+sequential state machine committing the step's batches in global order
+(rank 0's batches, then rank 1's, ...), bit for bit; the tests check this
+against one CPU oracle fed the same global sequence.
+
+Per step (`create_transfers`):
+
+1. Timestamps.  The batch counts are all-gathered; batch g of the global order
+   gets T_g = T_{g-1} + 1 + n_g (the harness rule, src/state_machine.zig:1973)
+   and event i of it T_g - n_g + i + 1 (execute, :1031).
+2. Id directory round.  Transfer ids are hash-partitioned over ranks ("homes").
+   Each event sends its id (and, for post/void, its pending id) to its home,
+   which answers in global order: committed on shard O (EXISTS), first seen
+   earlier in this step (DUP, with that event's route) or new.  Pending ids
+   resolve the same way to the shard holding (or creating) the pending.
+3. Routing.  Regular transfers go to owner(t.ledger); a transfer whose id is
+   committed on O goes to O (it can only fail there, with `exists*` or an
+   earlier code, so no balance moves); post/void goes to the pending's shard,
+   with a colliding committed id imported there (tbgpu_import_transfers) for the
+   `exists` comparison.  Events that fail state-independently stay with their
+   chain.  Accounts are replicated on every rank (create_accounts runs
+   everywhere), so the account checks (:1273-1281) are exact on any shard.
+4. Exchange.  Events travel to their owners with one all-to-all (RCCL over
+   xGMI on GPUs, gloo in the CPU tests); each owner commits its sub-batches in
+   global order with tbgpu_create_transfers_routed (per-event timestamps).
+5. Chains spanning shards.  Each shard commits its part of such a chain as a
+   chain of its own (TBGPU_CTL_CHAIN_END).  While any exist, rounds of dry runs
+   find every part's first failure; the all-gathered minimum is the chain's
+   break, after which members are skipped (TBGPU_CTL_SKIP) and parts that lie
+   wholly before it are doomed by a synthetic skipped member.  The rounds stop
+   when no break moves (a Jacobi fixed point over the step, as in the engine's
+   own general path), then the step commits for real.
+6. Hazards.  A duplicate id whose first occurrence (in another chain) routes
+   to a shard that does not own the later event's ledger, or a post/void of a
+   transfer created by a post/void in the same step, depends on an outcome on
+   another shard: the step is split before the hazard's chain, the prefix
+   commits, and the rest is routed again.
+7. Replies go back to the source ranks with a second all-to-all; committed
+   ids are registered with their homes; commit_timestamp is the max over
+   shards and is propagated to every engine.
+
+The backend of a rank is anything with the engine's commit API: the HIP
+engine (`tigerbeetle_amd.engine.Engine`) on GPUs; the CPU tests use the
+oracle per rank (test infrastructure) as the shard backend and a separate
+oracle as the checker.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from .types import ACCOUNT_DTYPE, RESULT_DTYPE, TRANSFER_DTYPE, TransferFlags
+
+CTL_CHAIN_END = 1  # include/tbgpu.h TBGPU_CTL_CHAIN_END
+CTL_SKIP = 2       # include/tbgpu.h TBGPU_CTL_SKIP
+LINKED_EVENT_FAILED = 1
+LINKED = int(TransferFlags.linked)
+POST_VOID = int(TransferFlags.post_pending_transfer | TransferFlags.void_pending_transfer)
+ANY = -1           # route: state-independent failure, any shard computes it
+PV = -2            # directory hint of a post/void: its shard is that of its pending
+MAX_ROUNDS = 64
+
+# directory replies
+NEW, EXISTS, DUP, PEND, PEND_NONE, PEND_HAZARD = range(6)
+
+
+def _id(lo, hi) -> int:
+    return (int(hi) << 64) | int(lo)
+
+
+def _home(key: int, world: int) -> int:
+    z = (key ^ (key >> 64)) & 0xFFFFFFFFFFFFFFFF
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9 & 0xFFFFFFFFFFFFFFFF
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EB & 0xFFFFFFFFFFFFFFFF
+    return (z ^ (z >> 31)) % world
+
+
+class Comm:
+    """The collectives the router needs, over a torch.distributed group (gloo on
+    CPU, nccl = RCCL on GPU: tensors then live on the rank's device)."""
+
+    def __init__(self, rank: int, world: int, group=None, device=None):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.rank, self.world, self.group = rank, world, group
+        self.device = device if device is not None else torch.device("cpu")
+
+    def all_gather_object(self, obj):
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj, group=self.group)
+        return out
+
+    def alltoallv(self, parts: list[np.ndarray]) -> list[np.ndarray]:
+        """parts[d]: bytes (uint8 array) for rank d.  Returns the parts received, by source."""
+        torch = self.torch
+        sizes = torch.tensor([len(p) for p in parts], dtype=torch.int64, device=self.device)
+        rsizes = torch.empty_like(sizes)
+        self.dist.all_to_all_single(rsizes, sizes, group=self.group)
+        rs = rsizes.cpu().tolist()
+        src = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+        inp = torch.from_numpy(np.ascontiguousarray(src, dtype=np.uint8)).to(self.device)
+        out = torch.empty(sum(rs), dtype=torch.uint8, device=self.device)
+        self.dist.all_to_all_single(out, inp, rs, [len(p) for p in parts], group=self.group)
+        o = out.cpu().numpy()
+        res, off = [], 0
+        for n in rs:
+            res.append(o[off:off + n])
+            off += n
+        return res
+
+    def allreduce_max(self, v: int) -> int:
+        return max(self.all_gather_object(int(v)))
+
+
+@dataclass
+class _Event:
+    """Routing view of one event of the step (global order = index in the step)."""
+    src: int        # source rank
+    batch: int      # source rank's batch index
+    index: int      # index in that batch
+    g: int          # global batch number within the step
+
+
+class ShardedStateMachine:
+    """create_accounts / create_transfers for one rank of a ledger-sharded node."""
+
+    def __init__(self, backend, comm: Comm, owner_of_ledger=None):
+        self.backend = backend
+        self.comm = comm
+        self.rank, self.world = comm.rank, comm.world
+        self.owner_of_ledger = owner_of_ledger or (lambda ledger: int(ledger) % self.world)
+        self.prepare_timestamp = 0
+        self.commit_timestamp = 0
+        self.committed = {}     # home part of the id directory: transfer id -> owning shard
+        self.stats = {"steps": 0, "splits": 0, "dry_rounds": 0, "cross_chains": 0, "imports": 0}
+
+    # ------------------------------------------------------------ accounts --
+    def create_accounts(self, batches: list[np.ndarray]) -> list[np.ndarray]:
+        """Every rank commits every rank's account batches (replicated accounts):
+        the account checks of create_transfer are then exact on any shard."""
+        allb = self.comm.all_gather_object([np.ascontiguousarray(b, ACCOUNT_DTYPE).tobytes() for b in batches])
+        flat, counts, ts, owner = [], [], [], []
+        for r, bl in enumerate(allb):
+            for j, raw in enumerate(bl):
+                ev = np.frombuffer(raw, dtype=ACCOUNT_DTYPE)
+                self.prepare_timestamp += 1 + len(ev)
+                flat.append(ev)
+                counts.append(len(ev))
+                ts.append(self.prepare_timestamp)
+                owner.append((r, j))
+        if not counts:
+            return []
+        events = np.concatenate(flat) if flat else np.zeros(0, ACCOUNT_DTYPE)
+        out, rc = self.backend.create_accounts_batches(np.array(ts, np.uint64), np.array(counts, np.uint32),
+                                                       events)
+        self._sync_commit_timestamp()
+        mine, off = [], 0
+        for (r, j), c, k in zip(owner, counts, rc):
+            if r == self.rank:
+                mine.append(out[off:off + int(k)].copy())
+            off += c
+        return mine
+
+    # ----------------------------------------------------------- transfers --
+    def create_transfers(self, batches: list[np.ndarray]) -> list[np.ndarray]:
+        """One routed step over this rank's batches; returns this rank's replies."""
+        batches = [np.ascontiguousarray(b, TRANSFER_DTYPE) for b in batches]
+        counts_all = self.comm.all_gather_object([len(b) for b in batches])
+        # global order and timestamps (identical on every rank)
+        glob = [(r, j, c) for r, cl in enumerate(counts_all) for j, c in enumerate(cl)]
+        T = []
+        for r, j, c in glob:
+            self.prepare_timestamp += 1 + c
+            T.append(self.prepare_timestamp)
+        gidx = {(r, j): g for g, (r, j, c) in enumerate(glob)}
+        # the step's events in global order, addressed by (g, index)
+        my_events = {gidx[(self.rank, j)]: b for j, b in enumerate(batches)}
+        replies = {g: [] for g in my_events}
+        start = (0, 0)  # resume point (global batch, index) after a hazard split
+        while True:
+            self.stats["steps"] += 1
+            split = self._round(glob, T, my_events, replies, start)
+            if split is None:
+                break
+            self.stats["splits"] += 1
+            start = split
+        self._sync_commit_timestamp()
+        out = []
+        for j in range(len(batches)):
+            r = replies[gidx[(self.rank, j)]]
+            a = np.array(sorted(r), dtype=np.uint32).reshape(-1, 2)
+            res = np.zeros(len(a), dtype=RESULT_DTYPE)
+            if len(a):
+                res["index"], res["result"] = a[:, 0], a[:, 1]
+            out.append(res)
+        return out
+
+    def _sync_commit_timestamp(self):
+        ts = self.comm.allreduce_max(self.backend.commit_timestamp())
+        self.backend.advance_commit_timestamp(ts)
+        self.commit_timestamp = ts
+
+    # One routing + commit round over the step's events at or after `start`.
+    # Returns None when they all committed, else the split point where the next
+    # round resumes (the prefix before it committed).
+    def _round(self, glob, T, my_events, replies, start):
+        W, me = self.world, self.rank
+        g0, i0 = start
+        # ---- 1. local view of my events in the remaining range
+        loc = []   # (g, i) of my remaining events, in global order
+        for g in sorted(my_events):
+            if g < g0:
+                continue
+            n = len(my_events[g])
+            for i in range(i0 if g == g0 else 0, n):
+                loc.append((g, i))
+        ev = {k: my_events[k[0]][k[1]] for k in loc}
+
+        # ---- 2. id directory round
+        reqs = [[] for _ in range(W)]
+        for (g, i) in loc:
+            t = ev[(g, i)]
+            x = _id(t["id_lo"], t["id_hi"])
+            f = int(t["flags"])
+            pv = bool(f & POST_VOID)
+            if x == 0 or x == (1 << 128) - 1:
+                continue  # fails statically (:1250-1251): no directory entry
+            hint = PV if pv else (self.owner_of_ledger(t["ledger"]) if int(t["ledger"]) else ANY)
+            reqs[_home(x, W)].append((g, i, 0, x, hint))
+            if pv:
+                p = _id(t["pending_id_lo"], t["pending_id_hi"])
+                if p != 0 and p != (1 << 128) - 1 and p != x:
+                    reqs[_home(p, W)].append((g, i, 1, p, ANY))
+        got = self._exchange_objects(reqs)
+        # home: answer in global order (kind 0 before kind 1 of the same event)
+        recs = sorted(((g, i, k, key, hint, src) for src, lst in enumerate(got) for (g, i, k, key, hint) in lst),
+                      key=lambda r: (r[0], r[1], r[2]))
+        first = {}  # key -> (g, i, route hint) of its first occurrence this round
+        ans = [[] for _ in range(W)]
+        for (g, i, k, key, hint, src) in recs:
+            if k == 0:
+                if key in self.committed:
+                    a = (EXISTS, self.committed[key], None)
+                elif key in first:
+                    fg, fi, fh = first[key]
+                    a = (DUP, fh, (fg, fi))
+                else:
+                    first[key] = (g, i, hint)
+                    a = (NEW, None, None)
+            else:
+                if key in self.committed:
+                    a = (PEND, self.committed[key], None)
+                elif key in first and first[key][:2] < (g, i):
+                    fg, fi, fh = first[key]
+                    a = (PEND_HAZARD, None, (fg, fi)) if fh in (ANY, PV) else (PEND, fh, (fg, fi))
+                else:
+                    a = (PEND_NONE, None, None)
+            ans[src].append((g, i, k, a))
+        back = self._exchange_objects(ans)
+        dir_id, dir_p = {}, {}
+        for lst in back:
+            for (g, i, k, a) in lst:
+                (dir_id if k == 0 else dir_p)[(g, i)] = a
+
+        # ---- 3. routing of my events
+        route, hazard = {}, None
+        chain_of = self._chains(loc, ev)
+        for (g, i) in loc:
+            t = ev[(g, i)]
+            f = int(t["flags"])
+            a_id = dir_id.get((g, i), (NEW, None, None))
+            if f & POST_VOID:
+                a_p = dir_p.get((g, i), (PEND_NONE, None, None))
+                if a_p[0] == PEND:
+                    r = a_p[1]
+                elif a_p[0] == PEND_HAZARD:
+                    fg, fi = a_p[2]
+                    if (fg, fi) in chain_of and chain_of[(fg, fi)] == chain_of[(g, i)]:
+                        r = ("follow", (fg, fi))   # same chain: it can only fail; go where the creator goes
+                    else:
+                        hazard = self._min(hazard, (g, i))
+                        r = ANY
+                else:
+                    r = ANY  # pending_transfer_not_found or an earlier static failure
+                if a_id[0] == DUP and (a_id[1] != r or a_id[1] in (ANY, PV)):
+                    fg, fi = a_id[2]
+                    if (fg, fi) in chain_of and chain_of[(fg, fi)] == chain_of[(g, i)]:
+                        r = ("follow", (fg, fi))   # same chain: it can only fail; go with the first
+                    else:
+                        hazard = self._min(hazard, (g, i))
+                route[(g, i)] = r
+            else:
+                own = self.owner_of_ledger(t["ledger"]) if int(t["ledger"]) else ANY
+                if a_id[0] == EXISTS:
+                    r = a_id[1]
+                elif a_id[0] == DUP:
+                    fg, fi = a_id[2]
+                    same_chain = (fg, fi) in chain_of and chain_of[(fg, fi)] == chain_of[(g, i)]
+                    if same_chain:
+                        r = ("follow", (fg, fi))   # it can only fail: go where the first goes
+                    elif a_id[1] == ANY or own == ANY:
+                        r = own                    # the first fails statically / so does this one
+                    elif a_id[1] == own:
+                        r = own
+                    else:
+                        hazard = self._min(hazard, (g, i))
+                        r = own
+                else:
+                    r = own
+                route[(g, i)] = r
+        # resolve "follow" routes (same chain, so same source) and ANY inside chains
+        for k in loc:
+            seen = 0
+            while isinstance(route[k], tuple) and seen < len(loc):
+                route[k] = route[route[k][1]]
+                seen += 1
+            if isinstance(route[k], tuple):
+                route[k] = ANY
+        for members in self._chain_members(loc, chain_of).values():
+            owners = [route[m] for m in members if route[m] != ANY]
+            fill = owners[0] if owners else me
+            for m in members:
+                if route[m] == ANY:
+                    route[m] = fill
+        # post/void whose id is committed on another shard: import that row
+        imports = []
+        for (g, i) in loc:
+            t = ev[(g, i)]
+            if int(t["flags"]) & POST_VOID:
+                a_id = dir_id.get((g, i), (NEW, None, None))
+                if a_id[0] == EXISTS and a_id[1] != route[(g, i)]:
+                    imports.append((_id(t["id_lo"], t["id_hi"]), a_id[1], route[(g, i)]))
+
+        # ---- 4. hazards: the earliest one over all ranks splits the step
+        hz = [h for h in self.comm.all_gather_object(
+            None if hazard is None else self._chain_start(hazard, ev, my_events)) if h is not None]
+        stop = min(hz) if hz else None
+        if stop is not None and stop <= (g0, i0):
+            raise RuntimeError("sharded commit: unresolvable cross-shard dependency at the resume point")
+        if stop is not None:
+            loc = [k for k in loc if k < stop]
+        self._do_imports(imports)  # rows are immutable: importing one early is harmless
+
+        # ---- 5. exchange events to owners (global order is preserved per source)
+        parts = [[] for _ in range(W)]
+        meta = [[] for _ in range(W)]
+        for k in loc:
+            d = route[k]
+            parts[d].append(ev[k])
+            meta[d].append((k[0], k[1], chain_of[k]))
+        recv = self._exchange_events(parts)
+        recv_meta = self._exchange_objects(meta)
+        mine = []   # (g, i, chain key, event) received, in global order
+        for src in range(W):
+            for (g, i, c), e in zip(recv_meta[src], recv[src]):
+                mine.append((g, i, c, e))
+        mine.sort(key=lambda x: (x[0], x[1]))
+
+        # cross-shard chains: chain key -> set of owners (all-gathered)
+        my_chains = {}
+        for k in loc:
+            my_chains.setdefault(chain_of[k], set()).add(route[k])
+        span = {}
+        for d in self.comm.all_gather_object({c: sorted(o) for c, o in my_chains.items() if len(o) > 1}):
+            span.update(d)
+        self.stats["cross_chains"] += len(span) if self.rank == 0 else 0
+        last_member = {}
+        for d in self.comm.all_gather_object({c: max(k for k in loc if chain_of[k] == c) for c in span
+                                              if any(chain_of[k] == c for k in loc)}):
+            for c, m in d.items():
+                last_member[c] = max(last_member.get(c, m), m)
+
+        # ---- 6. commit (dry rounds while chains span shards)
+        brk = {}   # chain key -> (g, i) of its first failure (global)
+        rounds = 0
+        while True:
+            sub = self._build_sub(mine, T, glob, span, last_member, brk)
+            dry = bool(span)
+            res = self._commit(sub, dry)
+            if not dry:
+                break
+            rounds += 1
+            self.stats["dry_rounds"] += 1
+            fails = {}
+            for (g, i, c), code in res:
+                if c in span and code not in (0, LINKED_EVENT_FAILED):
+                    if c not in fails or (g, i) < fails[c]:
+                        fails[c] = (g, i)
+            nb = {}
+            for d in self.comm.all_gather_object(fails):
+                for c, p in d.items():
+                    if c not in nb or p < nb[c]:
+                        nb[c] = p
+            if nb == brk:
+                sub = self._build_sub(mine, T, glob, span, last_member, brk)
+                res2 = self._commit(sub, False)
+                assert sorted(res2) == sorted(res), "sharded commit: dry run and commit disagree"
+                res = res2
+                break
+            if rounds >= MAX_ROUNDS:
+                raise RuntimeError("sharded commit: cross-shard chains did not converge")
+            brk = nb
+
+        # ---- 7. replies to sources, committed ids to homes
+        rep = [[] for _ in range(W)]
+        homes = [[] for _ in range(W)]
+        failed = {(g, i) for (g, i, c), code in res if code != 0}
+        for (g, i, c), code in res:
+            if code != 0:
+                rep[glob[g][0]].append((g, i, code))
+        for (g, i, c, e) in mine:
+            if (g, i) not in failed:
+                x = _id(e["id_lo"], e["id_hi"])
+                homes[_home(x, W)].append((x, self.rank))
+        for lst in self._exchange_objects(rep):
+            for (g, i, code) in lst:
+                replies[g].append((i, code))
+        for lst in self._exchange_objects(homes):
+            for (x, o) in lst:
+                self.committed[x] = o
+        if stop is None:
+            return None
+        return stop
+
+    # ----------------------------------------------------------- helpers --
+    @staticmethod
+    def _min(a, b):
+        return b if a is None or b < a else a
+
+    @staticmethod
+    def _chains(loc, ev):
+        """Chain key (g, first index) of each event: a run of `linked` events plus the
+        event that ends it, within one batch (execute, :1018-1035)."""
+        out = {}
+        cur = None
+        prev_g = None
+        for (g, i) in loc:
+            if g != prev_g:
+                cur = None
+                prev_g = g
+            if cur is None:
+                cur = (g, i)
+            out[(g, i)] = cur
+            if not (int(ev[(g, i)]["flags"]) & LINKED):
+                cur = None
+        return out
+
+    @staticmethod
+    def _chain_members(loc, chain_of):
+        m = {}
+        for k in loc:
+            m.setdefault(chain_of[k], []).append(k)
+        return m
+
+    @staticmethod
+    def _chain_start(k, ev, my_events):
+        g, i = k
+        b = my_events[g]
+        while i > 0 and int(b[i - 1]["flags"]) & LINKED:
+            i -= 1
+        return (g, i)
+
+    def _exchange_objects(self, parts):
+        import pickle
+        enc = [np.frombuffer(pickle.dumps(p), dtype=np.uint8) for p in parts]
+        return [pickle.loads(x.tobytes()) for x in self.comm.alltoallv(enc)]
+
+    def _exchange_events(self, parts):
+        enc = [np.ascontiguousarray(np.array(p, dtype=TRANSFER_DTYPE) if p else np.zeros(0, TRANSFER_DTYPE))
+               .view(np.uint8).reshape(-1) for p in parts]
+        return [x.view(TRANSFER_DTYPE) if len(x) else np.zeros(0, TRANSFER_DTYPE) for x in self.comm.alltoallv(enc)]
+
+    def _do_imports(self, imports):
+        """imports: (id, holder shard, destination shard) requested by this rank."""
+        reqs = [[] for _ in range(self.world)]
+        for (x, holder, dest) in sorted(set(imports)):
+            reqs[holder].append((x, dest))
+        got = self._exchange_objects(reqs)
+        send = [[] for _ in range(self.world)]
+        for lst in got:
+            for (x, dest) in lst:
+                row = self.backend.lookup_transfers([x])
+                assert len(row) == 1, "directory names a shard that does not hold the transfer"
+                send[dest].append(row[0])
+        rows, seen = [], set()
+        for lst in self._exchange_events(send):
+            for r in lst:
+                x = _id(r["id_lo"], r["id_hi"])
+                if x not in seen:
+                    seen.add(x)
+                    rows.append(r)
+        if rows:
+            self.backend.import_transfers(np.array(rows, dtype=TRANSFER_DTYPE))
+            self.stats["imports"] += len(rows)
+
+    def _build_sub(self, mine, T, glob, span, last_member, brk):
+        """Owner sub-batches (one per source batch, global order) with chain control."""
+        evs, ts, ctl, keys, counts = [], [], [], [], []
+        cur_g, cnt = None, 0
+        by_chain = {}
+        for idx, (g, i, c, e) in enumerate(mine):
+            by_chain.setdefault(c, []).append(idx)
+        last_local = {c: lst[-1] for c, lst in by_chain.items()}
+        for idx, (g, i, c, e) in enumerate(mine):
+            if g != cur_g:
+                if cur_g is not None:
+                    counts.append(cnt)
+                cur_g, cnt = g, 0
+            n_g = glob[g][2]
+            t_i = T[g] - n_g + i + 1
+            b = 0
+            doom = False
+            if c in span:
+                q = brk.get(c)
+                if q is not None and (g, i) > q:
+                    b |= CTL_SKIP
+                if idx == last_local[c] and (g, i) != last_member[c]:
+                    b |= CTL_CHAIN_END
+                    if q is not None and (g, i) < q:
+                        doom = True   # the chain breaks after this part: roll it back
+            if doom:
+                evs.append(e)
+                ts.append(t_i)
+                ctl.append(0)   # stays linked: the synthetic member closes the part
+                keys.append((g, i, c))
+                evs.append(e)
+                ts.append(t_i)
+                ctl.append(CTL_SKIP | CTL_CHAIN_END)
+                keys.append(None)
+                cnt += 2
+            else:
+                evs.append(e)
+                ts.append(t_i)
+                ctl.append(b)
+                keys.append((g, i, c))
+                cnt += 1
+        if cur_g is not None:
+            counts.append(cnt)
+        return evs, ts, ctl, keys, counts
+
+    def _commit(self, sub, dry):
+        evs, ts, ctl, keys, counts = sub
+        if not counts:
+            return []
+        events = np.array(evs, dtype=TRANSFER_DTYPE)
+        c = np.array(ctl, dtype=np.uint8)
+        out, rc, _ = self.backend.create_transfers_routed(np.array(counts, np.uint32), events,
+                                                          np.array(ts, np.uint64), c if c.any() else None, dry)
+        res, off = [], 0
+        for n, k in zip(counts, rc):
+            got = {int(r["index"]): int(r["result"]) for r in out[off:off + int(k)]}
+            for j in range(n):
+                key = keys[off + j]
+                if key is not None:
+                    res.append((key, got.get(j, 0)))
+            off += n
+        return res
+
+    # -------------------------------------------------------------- export --
+    def export_state(self):
+        """Collective.  (accounts of the ledgers this shard owns, transfers committed
+        on this shard -- imported copies excluded): for parity checks."""
+        owners = {}
+        for d in self.comm.all_gather_object(self.committed):
+            owners.update(d)
+        acc = self.backend.export_accounts()
+        own = np.array([self.owner_of_ledger(l) == self.rank for l in acc["ledger"]], dtype=bool)
+        xs = self.backend.export_transfers()
+        keep = np.array([owners.get(_id(r["id_lo"], r["id_hi"]), -1) == self.rank for r in xs], dtype=bool)
+        return acc[own] if len(acc) else acc, xs[keep] if len(xs) else xs

@@ -159,7 +159,7 @@ def config4(transfer_count: int = 16_380_000, ledgers: int = 1000, accounts_per_
         starts = rng.choice(np.arange(0, transfer_count - 1, 2), size=n_pairs, replace=False)
         starts = starts[(starts % batch) != batch - 1]
         t0 = transfers[starts]
-        t0["flags"] |= TransferFlags.linked
+        t0["flags"] |= np.uint16(int(TransferFlags.linked))
         transfers[starts] = t0
         other = (tl[starts] % ledgers) + 1
         t1 = transfers[starts + 1]

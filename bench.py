@@ -70,7 +70,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", type=int, default=2, choices=(1, 2))
+    ap.add_argument("--config", type=int, default=2, choices=(1, 2, 3))
+    ap.add_argument("--force-general", action="store_true", help="disable the fast path (measure the fixed point)")
     ap.add_argument("--batches-per-step", type=int, default=200)
     ap.add_argument("--accounts", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -99,13 +100,18 @@ def main():
     if args.config == 2:
         acc_n = args.accounts or 1_000_000
         w = workload.config2(transfer_count=n_transfers, account_count=acc_n, seed=42 + rank)
+    elif args.config == 3:
+        acc_n = args.accounts or 10_000
+        w = workload.config3(batches=n_batches, account_count=acc_n, seed=42 + rank)
+        n_batches = len(w.transfer_counts)  # + the funding batches
     else:
         acc_n = args.accounts or 10_000
         w = workload.config1(transfer_count=n_transfers, account_count=acc_n, seed=42 + rank)
     log(f"[rank {rank}] generated {n_transfers} transfers / {acc_n} accounts in {time.time() - t_gen:.1f}s")
 
-    eng = Engine(device=local_rank, accounts_max=acc_n, transfers_max=n_transfers + 1024,
-                 history_max=1024, events_per_call_max=B * BATCH_MAX)
+    eng = Engine(device=local_rank, accounts_max=acc_n, transfers_max=int(w.transfer_counts.sum()) + 1024,
+                 history_max=int(w.transfer_counts.sum()) + 1024 if args.config == 3 else 1024,
+                 events_per_call_max=B * BATCH_MAX, force_general=args.force_general)
     ats, tts = w.timestamps()
     _, rc = eng.create_accounts_batches(ats, w.account_counts, w.accounts)
     assert int(rc.sum()) == 0, "account creation failed"
@@ -133,6 +139,7 @@ def main():
     phase = np.zeros(8)
     dev_ms = 0.0
     iters = []
+    sorts = []
     non_ok = 0
     t0 = time.perf_counter()
     for k in range(W, W + K):
@@ -141,6 +148,7 @@ def main():
         phase += np.array(st.phase_ms[:8])
         dev_ms += st.device_ms
         iters.append(st.iterations)
+        sorts.append(st.sorts)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -153,7 +161,7 @@ def main():
         nk = torch.tensor([non_ok], dtype=torch.int64, device=dev)
         dist.all_reduce(nk)
         non_ok = int(nk.item())
-    per_rank = K * B * BATCH_MAX
+    per_rank = int(counts[W * B:(W + K) * B].sum())
     total = per_rank * world
     value = total / elapsed
     ms_per_step = elapsed / K * 1e3
@@ -221,12 +229,14 @@ def main():
             "dtype": "u128",
             "data": "synthetic",
             "config": {"workload": f"config{args.config}: {acc_n} accounts, "
-                                   + ("Zipf(0.99) pairs on 1 ledger" if args.config == 2 else "uniform pairs")
+                                   + {1: "uniform pairs", 2: "Zipf(0.99) pairs on 1 ledger",
+                                      3: "flag-heavy mix (limits, two-phase, balancing, chains)"}[args.config]
                                    + f", {B} x 8190-transfer batches per step (streamed, HBM-resident)",
                        "batches_per_step": B, "transfers_per_step_per_gpu": B * BATCH_MAX,
                        "parallelism": f"ledger-shard x{world}"},
             "non_ok_results": non_ok,
             "fixed_point_passes": max(iters) if iters else 0,
+            "fixed_point_sorts": max(sorts) if sorts else 0,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

@@ -530,7 +530,12 @@ __global__ void tr_sides(TrArgs C, EvalState S, u32 invalid, u32* skey, u32* sva
             d = C.dslot[i];
             c = C.cslot[i];
         } else {
-            const u32 p = S.pref[i];
+            // An unresolved post/void fails and moves no balance, so any key serves:
+            // keep its candidate pending's accounts and the keys stay put from pass to
+            // pass (a moved key costs a full re-sort).
+            u32 p = S.pref[i];
+            if (p == NONE32) p = C.pend_last[i] != NONE32 ? C.pend_last[i]
+                                 : (C.pre_p[i] != NONE32 ? (PREF_ROW | C.pre_p[i]) : NONE32);
             if (p != NONE32) {
                 if (p & PREF_ROW) { d = C.pp_dslot[i]; c = C.pp_cslot[i]; }
                 else { d = C.dslot[p]; c = C.cslot[p]; }

@@ -166,3 +166,50 @@ def test_fast_path_with_failures():
     st = _parity(w, split=1)
     assert st.path == 1
     st = _parity(w, split=2)
+
+
+def _chainy_config1(seed, n=40_000, accounts=800):
+    """config 1 with linked chains of 2-6 events, some with a failing member (unknown
+    account, amount 0, a repeated id) and open chains at batch ends."""
+    from tigerbeetle_amd.types import TransferFlags
+    w = workload.config1(transfer_count=n, account_count=accounts, seed=seed)
+    rng = np.random.default_rng(seed)
+    t = w.transfers
+    i = 0
+    while i < n - 1:
+        if rng.random() < 0.15:
+            ln = int(rng.integers(2, 7))
+            for q in range(i, min(i + ln - 1, n - 1)):
+                t[q]["flags"] |= np.uint16(int(TransferFlags.linked))
+            if rng.random() < 0.2:
+                v = i + int(rng.integers(0, ln))
+                if v < n:
+                    kind = int(rng.integers(0, 3))
+                    if kind == 0:
+                        t[v]["debit_account_id_lo"] = accounts + 5
+                    elif kind == 1:
+                        t[v]["amount_lo"] = 0
+                    elif v > 0:
+                        t[v]["id_lo"] = t[v - 1]["id_lo"]
+            i += ln
+        else:
+            i += 1
+    ends = np.cumsum(w.transfer_counts) - 1
+    for e in ends[rng.random(len(ends)) < 0.3]:
+        t[e]["flags"] |= np.uint16(int(TransferFlags.linked))
+    return w
+
+
+def test_fast_path_linked_chains():
+    st = _parity(_chainy_config1(3))
+    assert st.path in (0, 1)
+
+
+def test_fast_path_linked_chains_batch_by_batch():
+    _parity(_chainy_config1(4, n=12_000, accounts=300), split=1)
+
+
+def test_config4_cross_ledger_pairs_on_fast_path():
+    w = workload.config4(transfer_count=60_000, ledgers=20, accounts_per_ledger=200, seed=9, cross_ledger_pairs=0.02)
+    st = _parity(w)
+    assert st.path == 1, "config 4 (valid linked pairs) should stay on the single-pass path"

@@ -131,4 +131,5 @@ enum {
     FL_SLOW = 1u << 8,        // fast path: some event needs the fixed point
     FL_ERROR = 1u << 9,       // device-side protocol error (bounded spin expired)
     FL_NONMONO = 1u << 10,    // fast path: ids of the call are not strictly increasing
+    FL_FCHAIN = 1u << 11,     // fast path: linked chains, resolved by fp_chains
 };

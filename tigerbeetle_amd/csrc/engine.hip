@@ -383,6 +383,10 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tb_create_
     F.keys = c->f_keys;
     F.rows = c->f_rows;
     F.tile_idr = c->f_tile_idr;
+    F.ctl = c->rt_ctl;
+    F.fres2 = c->mask;
+    F.dry = c->rt_dry ? 1u : 0u;
+    F.commit_ts = c->rt_dry ? c->rt_dry_ts : c->T.commit_ts;
     static const u32 ablate = [] {  // timing-only ablation (profiles/ablate.py); never set in production
         const char* e = getenv("TBGPU_ABLATE");
         return e ? (u32)strtoul(e, nullptr, 0) : 0u;
@@ -403,7 +407,7 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tb_create_
     const u32 flags = c->h_counters[CNT_FLAGS];
     if (flags & FL_ERROR) tbgpu_fatal("create_transfers", "fast path look-back did not complete", __FILE__, __LINE__);
     if (flags & FL_SLOW) {
-        fp_launch_undo(c->T, F, s);
+        if (!F.dry) fp_launch_undo(c->T, F, s);  // a dry run applied no delta
         return false;
     }
     if (c->h_counters[CNT_BAD]) {
@@ -414,7 +418,7 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tb_create_
         HIP_CHECK(hipStreamSynchronize(s));
     }
     memcpy(counts_host, c->h_counts, nb * sizeof(u32));
-    c->n_rows += c->h_counters[CNT_OK];
+    if (!F.dry) c->n_rows += c->h_counters[CNT_OK];
     c->stats.path = 1;
     c->stats.iterations = 1;
     return true;
@@ -437,9 +441,7 @@ static void run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
         std::fill(counts_host, counts_host + nb, 0u);
         return;
     }
-    // the fast path knows no chains, so calls carrying chain control or a dry run
-    // take the fixed point
-    const bool fast_ok = !(c->opt.flags & TBGPU_OPT_FORCE_GENERAL) && !c->rt_ctl && !c->rt_dry;
+    const bool fast_ok = !(c->opt.flags & TBGPU_OPT_FORCE_GENERAL);
     if (fast_ok && try_fast(c, ev, n, nb, results_dev, counts_host)) return;
     prof_mark(c, PH_CLASSIFY);
     HIP_CHECK(hipMemsetAsync(c->counters, 0, CNT_COUNT * sizeof(u32), s));

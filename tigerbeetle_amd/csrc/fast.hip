@@ -20,6 +20,8 @@
 //
 // fp_commit: classify + balance deltas (LDS-aggregated, u64 atomics with carry)
 //            + optimistic stored rows at row_base + event.
+// fp_chains: linked-chain members (deferred by fp_commit): chain bounds, first
+//            failure, final results, deltas of the chains that hold.
 // fp_index:  publish the accepted ids in the transfer-id index.
 // With failures (results other than ok, the rare case for this path) fp_mask +
 // scan3 + fp_fix place the rows at their ranks and write the sparse replies, then
@@ -37,6 +39,7 @@ constexpr int FP_THREADS = FP_TILE;        // one event per thread, one tile per
 constexpr int AGG_SLOTS = 4 * FP_THREADS;  // LDS aggregation table (2x the sides of a tile)
 constexpr u32 AGG_EMPTY = 0xFFFFFFFFu;
 constexpr u8 FRES_SLOW = 0xFE;
+constexpr u8 FRES_CHAIN = 0x80;  // | own result: a chain member awaiting fp_chains
 
 __device__ __forceinline__ u32 fp_batch_of(const u32* __restrict__ b_start, u32 nb, u32 i) {
     u32 lo = 0, hi = nb;
@@ -118,7 +121,7 @@ __device__ __forceinline__ u8 fp_classify_guarded(const Tables& T, const FastArg
 __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, const Transfer& t, u32 i, u64 ts,
                                           u32* dslot_out, u32* cslot_out) {
     const u16 f = t.flags;
-    if (f & (TF_LINKED | TF_BDR | TF_BCR | TF_POST | TF_VOID) || *T.big)
+    if (f & (TF_BDR | TF_BCR | TF_POST | TF_VOID) || *T.big)
         return fp_classify_guarded(T, F, t, i, ts, dslot_out, cslot_out);
     // speculative first-slot reads (hash tables at load <= 0.5: usually the hit).
     // The 32-byte account index entries carry ledger and flags, so the rows
@@ -172,7 +175,6 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
 __device__ __forceinline__ u8 fp_classify_guarded(const Tables& T, const FastArgs& F, const Transfer& t, u32 i,
                                                        u64 ts, u32* dslot_out, u32* cslot_out) {
     const u16 f = t.flags;
-    if (f & TF_LINKED) return FRES_SLOW;  // linked chain
     if (t.timestamp != 0) return TB_CREATE_TRANSFER_TIMESTAMP_MUST_BE_ZERO;
     if (f & 0xFFC0u) return TB_CREATE_TRANSFER_RESERVED_FLAG;
     if (t.id == 0) return TB_CREATE_TRANSFER_ID_MUST_NOT_BE_ZERO;
@@ -276,15 +278,47 @@ void fp_commit(Tables T, FastArgs F) {
     // (a wave spans 64 events, so usually zero or one batch boundary)
     const u32 i0 = __builtin_amdgcn_readfirstlane(tile * FP_THREADS + wave * 64);
     if (i0 < F.n) b = fp_batch_of(F.b_start, F.nb, i0);
+    Transfer t{};
+    u32 bs = 0, nbatch = 0;
     if (valid) {
         while (F.b_start[b + 1] <= i) b++;
-        const u32 bs = F.b_start[b], nbatch = F.b_start[b + 1] - bs;
+        bs = F.b_start[b];
+        nbatch = F.b_start[b + 1] - bs;
         ts = F.ev_ts ? F.ev_ts[i] : F.b_ts[b] - nbatch + (i - bs) + 1;
-        Transfer t = F.ev[i];
+        t = F.ev[i];
+    }
+    // Linked-chain membership (execute, src/state_machine.zig:1018-1035): linked
+    // here, or the batch's previous event is (the router may close a chain that
+    // continues on another shard: TBGPU_CTL_CHAIN_END).
+    const u8 myctl = (valid && F.ctl) ? F.ctl[i] : 0;
+    const bool lk = valid && (t.flags & TF_LINKED) && !(myctl & TBGPU_CTL_CHAIN_END);
+    bool plk = __shfl_up(lk ? 1 : 0, 1) != 0;
+    if (lane == 0 && valid && i > 0)
+        plk = (F.ev[i - 1].flags & TF_LINKED) && !(F.ctl && (F.ctl[i - 1] & TBGPU_CTL_CHAIN_END));
+    plk = plk && valid && i > bs;
+    const bool member = lk || plk;
+    if (__ballot(member) && lane == 0) atomicOr(&F.counters[CNT_FLAGS], (u32)FL_FCHAIN);
+    bool own_ok = false;
+    if (valid) {
         id = t.id;
         u32 ds = NONE32, cs = NONE32;
-        r = fp_classify(T, F, t, i, ts, &ds, &cs);
-        F.fres[i] = r;
+        if (lk && i - bs == nbatch - 1) r = TB_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN;  // checked first (:1024)
+        else if (myctl & TBGPU_CTL_SKIP) r = TB_CREATE_TRANSFER_LINKED_EVENT_FAILED;    // broken on another shard
+        else r = fp_classify(T, F, t, i, ts, &ds, &cs);
+        own_ok = r == TB_CREATE_TRANSFER_OK;
+        if (member && r != FRES_SLOW) {
+            // deferred to fp_chains: no balance delta, no count; the optimistic row
+            // and the id claim as for any accepted event
+            F.fres[i] = FRES_CHAIN | r;
+            if (own_ok) {
+                F.keys[i] = t.id;
+                t.timestamp = ts;
+                if (!(F.ablate & ABL_ROWS)) T.xrows[F.row_base + i] = t;
+            }
+            r = FRES_CHAIN;
+        } else {
+            F.fres[i] = r;
+        }
         if (r == TB_CREATE_TRANSFER_OK) {
             F.keys[i] = t.id;
             // tile-local aggregation first: a hot account costs one global atomic per tile
@@ -299,12 +333,12 @@ void fp_commit(Tables T, FastArgs F) {
             if (!(F.ablate & ABL_ROWS)) T.xrows[F.row_base + i] = t;
         } else if (r == FRES_SLOW) {
             atomicOr(&F.counters[CNT_FLAGS], (u32)FL_SLOW);
-        } else {
+        } else if (r != FRES_CHAIN) {
             atomicAdd(&F.batch_counts[b], 1u);
         }
     }
     const bool ok = valid && r == TB_CREATE_TRANSFER_OK;
-    const bool bad = valid && r != TB_CREATE_TRANSFER_OK;
+    const bool bad = valid && r != TB_CREATE_TRANSFER_OK && r != FRES_CHAIN;
 
     // Strictly increasing ids across the whole call cannot repeat: then fp_dupcheck
     // has nothing to do (sequential ids, the benchmark's default id order).
@@ -327,8 +361,9 @@ void fp_commit(Tables T, FastArgs F) {
     u64 mts = ok ? ts : 0;
     for (int off = 32; off > 0; off >>= 1) mts = max(mts, (u64)__shfl_xor((unsigned long long)mts, off));
     // componentwise id range of the tile's accepted ids (for the index key-range filter)
-    u64 mxl = ok ? (u64)id : 0, mxh = ok ? (u64)(id >> 64) : 0;
-    u64 mnl = ok ? (u64)id : ~0ull, mnh = ok ? (u64)(id >> 64) : ~0ull;
+    const bool rng = ok || own_ok;  // a chain member's id may still be stored
+    u64 mxl = rng ? (u64)id : 0, mxh = rng ? (u64)(id >> 64) : 0;
+    u64 mnl = rng ? (u64)id : ~0ull, mnh = rng ? (u64)(id >> 64) : ~0ull;
     for (int off = 32; off > 0; off >>= 1) {
         mxl = max(mxl, (u64)__shfl_xor((unsigned long long)mxl, off));
         mxh = max(mxh, (u64)__shfl_xor((unsigned long long)mxh, off));
@@ -361,7 +396,7 @@ void fp_commit(Tables T, FastArgs F) {
             }
             if (nok) {
                 atomicAdd(&F.counters[CNT_OK], nok);
-                atomicMax((unsigned long long*)T.commit_ts, (unsigned long long)maxts);
+                atomicMax((unsigned long long*)F.commit_ts, (unsigned long long)maxts);
             }
             if (nbad) atomicAdd(&F.counters[CNT_BAD], nbad);
         }
@@ -369,6 +404,7 @@ void fp_commit(Tables T, FastArgs F) {
     // flush the tile's partial sums: u128 += (carry:sum) with u64 atomics.  All of a
     // thread's low-word atomics are issued before any returns (memory-level
     // parallelism); the rare carries follow.
+    if (F.dry) return;  // a dry run moves no balance
     constexpr int PER = AGG_SLOTS / FP_THREADS;
     u64* wp[PER];
     u64 av[PER], old[PER];
@@ -410,7 +446,8 @@ __global__ void fp_dupcheck(Tables T, FastArgs F) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= F.n) return;
     F.gpos[i] = NONE32;
-    if (F.fres[i] != TB_CREATE_TRANSFER_OK) return;
+    const u8 r = F.fres[i];
+    if (r != TB_CREATE_TRANSFER_OK && r != (FRES_CHAIN | TB_CREATE_TRANSFER_OK)) return;
     if (gtab_claim_is_dup(F, F.keys[i], i)) atomicOr(&F.counters[CNT_FLAGS], (u32)FL_SLOW);
 }
 
@@ -426,6 +463,7 @@ __global__ void fp_index(Tables T, FastArgs F, bool fixed) {
         if (g != NONE32) F.gtab[g] = 0;
     }
     if (flags & (FL_SLOW | FL_ERROR)) return;
+    if (F.dry) return;
     if (!fixed && F.counters[CNT_BAD] != 0) return;
     if (blockIdx.x == 0 && threadIdx.x < 64) {
         // fold the tiles' id ranges into the index's key range (one wave)
@@ -453,6 +491,81 @@ __global__ void fp_index(Tables T, FastArgs F, bool fixed) {
     if (i >= F.n) return;
     if (F.fres[i] != TB_CREATE_TRANSFER_OK) return;
     xidx_insert(T, F.keys[i], fixed ? F.rows[i] : (u32)(F.row_base + i));
+}
+
+__device__ __forceinline__ bool fp_linked(const FastArgs& F, u32 j) {
+    return (F.ev[j].flags & TF_LINKED) && !(F.ctl && (F.ctl[j] & TBGPU_CTL_CHAIN_END));
+}
+
+__device__ __forceinline__ void add_u128_small(const Tables& T, u128* p, u64 a) {
+    u64* w = (u64*)p;
+    const u64 old = atomicAdd((unsigned long long*)&w[0], (unsigned long long)a);
+    if (old + a < old) {
+        const u64 hi = atomicAdd((unsigned long long*)&w[1], 1ull);
+        if (hi + 1 >= (1ull << 62)) atomicOr(T.big, 1u);
+    }
+}
+
+// Linked chains of eligible events (execute, src/state_machine.zig:1018-1083): a
+// chain holds iff no member fails; otherwise the first failing member keeps its
+// own result, every other member gets linked_event_failed (members after the
+// break are not evaluated; linked_event_chain_open is checked before the break),
+// and commit_timestamp advanced only by the accepted members before the break
+// (:1366, not undone by scope_close).  Each member walks its own (short) chain;
+// results go to fres2 so that no thread reads a finalized code.
+__global__ void fp_chains(Tables T, FastArgs F) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    const u32 flags = F.counters[CNT_FLAGS];
+    if (!(flags & FL_FCHAIN) || (flags & (FL_SLOW | FL_ERROR)) || i >= F.n) return;
+    const u8 fr = F.fres[i];
+    if (!(fr & FRES_CHAIN) || fr == FRES_SLOW) return;
+    const u8 own = fr & 0x7F;
+    const u32 b = fp_batch_of(F.b_start, F.nb, i);
+    const u32 bs = F.b_start[b], be = F.b_start[b + 1];
+    u32 s = i;
+    while (s > bs && fp_linked(F, s - 1)) s--;
+    u32 e = i;
+    while (e + 1 < be && fp_linked(F, e)) e++;
+    u32 j = NONE32;
+    for (u32 k = s; k <= e; k++)
+        if ((F.fres[k] & 0x7F) != TB_CREATE_TRANSFER_OK) { j = k; break; }
+    u8 fin;
+    if (j == NONE32) fin = TB_CREATE_TRANSFER_OK;
+    else if (own == TB_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN) fin = own;
+    else if (i == j) fin = own;
+    else fin = TB_CREATE_TRANSFER_LINKED_EVENT_FAILED;
+    F.fres2[i] = fin;
+    const u64 nbatch = be - bs;
+    const u64 ts = F.ev_ts ? F.ev_ts[i] : F.b_ts[b] - nbatch + (i - bs) + 1;
+    if (own == TB_CREATE_TRANSFER_OK && (j == NONE32 || i < j))
+        atomicMax((unsigned long long*)F.commit_ts, (unsigned long long)ts);
+    if (fin == TB_CREATE_TRANSFER_OK) {
+        atomicAdd(&F.counters[CNT_OK], 1u);
+        if (!F.dry) {
+            const Transfer& t = F.ev[i];
+            const u32 ds = acc_probe(T.aidx, T.aidx_mask, t.debit_account_id);
+            const u32 cs = acc_probe(T.aidx, T.aidx_mask, t.credit_account_id);
+            const u64 a = (u64)t.amount;
+            if (t.flags & TF_PENDING) {
+                add_u128_small(T, &T.acc[ds].debits_pending, a);
+                add_u128_small(T, &T.acc[cs].credits_pending, a);
+            } else {
+                add_u128_small(T, &T.acc[ds].debits_posted, a);
+                add_u128_small(T, &T.acc[cs].credits_posted, a);
+            }
+        }
+    } else {
+        atomicAdd(&F.counters[CNT_BAD], 1u);
+        atomicAdd(&F.batch_counts[b], 1u);
+    }
+}
+
+__global__ void fp_chains_fin(FastArgs F) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    const u32 flags = F.counters[CNT_FLAGS];
+    if (!(flags & FL_FCHAIN) || (flags & (FL_SLOW | FL_ERROR)) || i >= F.n) return;
+    const u8 fr = F.fres[i];
+    if ((fr & FRES_CHAIN) && fr != FRES_SLOW) F.fres[i] = F.fres2[i];
 }
 
 // With failures: mask for the rank scan (bit0 accepted, bit1 failed).
@@ -521,6 +634,8 @@ void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream) {
 
 void fp_launch_index(const Tables& T, const FastArgs& F, hipStream_t stream) {
     fp_dupcheck<<<GRID(F.n)>>>(T, F);
+    fp_chains<<<GRID(F.n)>>>(T, F);   // both stand down without FL_FCHAIN
+    fp_chains_fin<<<GRID(F.n)>>>(F);
     fp_index<<<GRID(F.n)>>>(T, F, false);
     HIP_CHECK(hipGetLastError());
 }
@@ -529,7 +644,7 @@ void fp_launch_fix(const Tables& T, const FastArgs& F, u8* mask, uint4* ranks, S
     fp_mask<<<GRID(F.n)>>>(F, mask);
     scan3_exclusive(mask, ranks, F.n, sc, stream);
     fp_fix<<<GRID(F.n)>>>(F, T, ranks);
-    fp_index<<<GRID(F.n)>>>(T, F, true);
+    if (!F.dry) fp_index<<<GRID(F.n)>>>(T, F, true);
     HIP_CHECK(hipGetLastError());
 }
 

@@ -276,6 +276,10 @@ enum {
     /* The chain broke on another shard before this event: not evaluated, result
      * linked_event_failed (execute's chain_broken arm, :1037-1040). */
     TBGPU_CTL_SKIP = 1u << 1,
+    /* The chain breaks on another shard after this event, the last local member:
+     * the local part is evaluated, then rolled back (scope_close(.discard),
+     * :1049-1058) and its members get linked_event_failed. */
+    TBGPU_CTL_DOOM = 1u << 2,
 };
 
 /* create_transfers over `batch_count` owner sub-batches.  `event_timestamps[i]`
@@ -290,6 +294,14 @@ uint64_t tbgpu_create_transfers_routed(tbgpu_ctx* ctx, uint32_t batch_count, con
                                        const uint8_t* ctl, int dry_run,
                                        tb_create_transfers_result_t* results, uint32_t* result_counts,
                                        uint64_t* commit_timestamp);
+
+/* Same with events, event timestamps, chain control (may be NULL) and the
+ * replies in device memory (HBM); replies concatenated per sub-batch as in
+ * tbgpu_create_transfers_batches_device.  `counts` / `result_counts` are host arrays. */
+uint64_t tbgpu_create_transfers_routed_device(tbgpu_ctx* ctx, uint32_t batch_count, const uint32_t* counts,
+                                              const void* events_device, const void* event_timestamps_device,
+                                              const void* ctl_device, int dry_run, void* results_device,
+                                              uint32_t* result_counts, uint64_t* commit_timestamp);
 
 /* Copy committed transfers of another shard into this ctx's transfer table and id
  * index, without balance or posted effects: the `exists` comparisons of

@@ -139,6 +139,19 @@ class Oracle:
                                             _ptr(rc), ctypes.byref(cts))
         return out, rc, cts.value
 
+    def create_transfers_routed_tensors(self, counts, events, event_ts, ctl, dry_run, results):
+        """The Engine method of the same name over CPU tensors (sharded-commit tests)."""
+        ev = events.numpy().view(TRANSFER_DTYPE)
+        out, rc, cts = self.create_transfers_routed(counts, ev, event_ts.numpy().view(np.uint64),
+                                                    None if ctl is None else ctl.numpy(), dry_run)
+        cat, off, k = [], 0, 0
+        for n, c in zip(counts, rc):
+            cat.append(out[off:off + int(c)])
+            off += int(n)
+        flat = np.concatenate(cat) if cat else np.zeros(0, RESULT_DTYPE)
+        results.numpy()[:8 * len(flat)] = flat.view(np.uint8)
+        return rc, cts
+
     def import_transfers(self, rows: np.ndarray) -> None:
         rows = np.ascontiguousarray(rows, dtype=TRANSFER_DTYPE)
         if len(rows):

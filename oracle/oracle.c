@@ -532,8 +532,9 @@ static uint32_t execute_ex(orc_t* o, uint64_t timestamp, const uint8_t* events, 
         /* AccountFlags.linked / TransferFlags.linked; a routed chain part ends where
          * the router closed it (the chain continues on another shard) */
         const int linked = (flags & 1) && !(ctl && (ctl[index] & TBGPU_CTL_CHAIN_END));
+        const int doom = ctl && (ctl[index] & TBGPU_CTL_DOOM);
         uint32_t result;
-        if (linked && chain < 0) { chain = index; assert(!chain_broken); scope_open(o); }
+        if ((linked || doom) && chain < 0) { chain = index; assert(!chain_broken); scope_open(o); }
         if (linked && index == n - 1) {
             result = TB_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN; /* == account code 2 */
         } else if (chain_broken || (ctl && (ctl[index] & TBGPU_CTL_SKIP))) {
@@ -544,6 +545,8 @@ static uint32_t execute_ex(orc_t* o, uint64_t timestamp, const uint8_t* events, 
             ts = ev_ts ? ev_ts[index] : timestamp - n + index + 1;
             memcpy(event + 120, &ts, 8);
             result = create(o, event);
+            /* the chain breaks on another shard right after this member */
+            if (doom && result == 0) result = TB_CREATE_TRANSFER_LINKED_EVENT_FAILED;
         }
         if (result != 0) {
             if (chain >= 0) {

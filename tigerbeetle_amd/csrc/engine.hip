@@ -522,7 +522,7 @@ static void run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
 static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t* timestamps, const uint32_t* counts,
                                   const Transfer* ev_src, bool src_device, tb_create_transfers_result_t* results,
                                   bool dst_device, uint32_t* result_counts, const uint64_t* ev_ts_host = nullptr,
-                                  const uint8_t* ctl_host = nullptr) {
+                                  const uint8_t* ctl_host = nullptr, bool routed_device = false) {
     HIP_CHECK(hipSetDevice(c->device));
     HIP_CHECK(hipEventRecord(c->ev0, c->stream));
     std::vector<u32> starts;
@@ -544,13 +544,19 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         }
         c->rt_ev_ts = nullptr;
         c->rt_ctl = nullptr;
-        if (ev_ts_host) {
-            HIP_CHECK(hipMemcpyAsync(c->rt_ts_buf, ev_ts_host + ev_off, (u64)n * 8, hipMemcpyHostToDevice, c->stream));
-            c->rt_ev_ts = c->rt_ts_buf;
-        }
-        if (ctl_host) {
-            HIP_CHECK(hipMemcpyAsync(c->rt_ctl_buf, ctl_host + ev_off, n, hipMemcpyHostToDevice, c->stream));
-            c->rt_ctl = c->rt_ctl_buf;
+        if (routed_device) {  // already in HBM
+            c->rt_ev_ts = ev_ts_host ? ev_ts_host + ev_off : nullptr;
+            c->rt_ctl = ctl_host ? ctl_host + ev_off : nullptr;
+        } else {
+            if (ev_ts_host) {
+                HIP_CHECK(hipMemcpyAsync(c->rt_ts_buf, ev_ts_host + ev_off, (u64)n * 8, hipMemcpyHostToDevice,
+                                         c->stream));
+                c->rt_ev_ts = c->rt_ts_buf;
+            }
+            if (ctl_host) {
+                HIP_CHECK(hipMemcpyAsync(c->rt_ctl_buf, ctl_host + ev_off, n, hipMemcpyHostToDevice, c->stream));
+                c->rt_ctl = c->rt_ctl_buf;
+            }
         }
         tb_create_transfers_result_t* rdev =
             dst_device ? results + total : (tb_create_transfers_result_t*)c->res_buf;
@@ -575,25 +581,45 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
     return total;
 }
 
+static uint64_t routed(tbgpu_ctx* c, uint32_t batch_count, const uint32_t* counts, const void* events,
+                       const uint64_t* event_timestamps, const uint8_t* ctl, int dry_run, void* results,
+                       uint32_t* result_counts, uint64_t* commit_timestamp, bool device);
+
 extern "C" uint64_t tbgpu_create_transfers_routed(tbgpu_ctx* c, uint32_t batch_count, const uint32_t* counts,
                                                   const tb_transfer_t* events, const uint64_t* event_timestamps,
                                                   const uint8_t* ctl, int dry_run,
                                                   tb_create_transfers_result_t* results, uint32_t* result_counts,
                                                   uint64_t* commit_timestamp) {
+    return routed(c, batch_count, counts, events, event_timestamps, ctl, dry_run, results, result_counts,
+                  commit_timestamp, false);
+}
+
+extern "C" uint64_t tbgpu_create_transfers_routed_device(tbgpu_ctx* c, uint32_t batch_count, const uint32_t* counts,
+                                                         const void* events_device,
+                                                         const void* event_timestamps_device, const void* ctl_device,
+                                                         int dry_run, void* results_device, uint32_t* result_counts,
+                                                         uint64_t* commit_timestamp) {
+    return routed(c, batch_count, counts, events_device, (const uint64_t*)event_timestamps_device,
+                  (const uint8_t*)ctl_device, dry_run, results_device, result_counts, commit_timestamp, true);
+}
+
+static uint64_t routed(tbgpu_ctx* c, uint32_t batch_count, const uint32_t* counts, const void* events,
+                       const uint64_t* event_timestamps, const uint8_t* ctl, int dry_run, void* results,
+                       uint32_t* result_counts, uint64_t* commit_timestamp, bool device) {
     HIP_CHECK(hipSetDevice(c->device));
     u64 n = 0;
     for (u32 b = 0; b < batch_count; b++) n += counts[b];
     if (dry_run && (n > c->nmax || batch_count > c->bmax - 2))
         tbgpu_fatal("create_transfers_routed", "a dry run must fit one call (events_per_call_max)", __FILE__, __LINE__);
-    // the batch timestamps only order the batches here: every event carries its own
+    // the batch timestamps are unused: every event carries its own
     std::vector<u64> bts(batch_count, 0);
-    for (u32 b = 0; b < batch_count; b++) bts[b] = counts[b] ? event_timestamps[0] : 0;
     c->rt_dry = dry_run != 0;
     if (c->rt_dry) {
         HIP_CHECK(hipMemcpyAsync(c->rt_dry_ts, c->T.commit_ts, sizeof(u64), hipMemcpyDeviceToDevice, c->stream));
     }
-    const u64 total = transfers_batches(c, batch_count, bts.data(), counts, (const Transfer*)events, false, results,
-                                        false, result_counts, event_timestamps, ctl);
+    const u64 total = transfers_batches(c, batch_count, bts.data(), counts, (const Transfer*)events, device,
+                                        (tb_create_transfers_result_t*)results, device, result_counts,
+                                        event_timestamps, ctl, device);
     c->rt_ev_ts = nullptr;
     c->rt_ctl = nullptr;
     u64 ts = 0;

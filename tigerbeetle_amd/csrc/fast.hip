@@ -296,7 +296,7 @@ void fp_commit(Tables T, FastArgs F) {
     if (lane == 0 && valid && i > 0)
         plk = (F.ev[i - 1].flags & TF_LINKED) && !(F.ctl && (F.ctl[i - 1] & TBGPU_CTL_CHAIN_END));
     plk = plk && valid && i > bs;
-    const bool member = lk || plk;
+    const bool member = lk || plk || (myctl & TBGPU_CTL_DOOM);
     if (__ballot(member) && lane == 0) atomicOr(&F.counters[CNT_FLAGS], (u32)FL_FCHAIN);
     bool own_ok = false;
     if (valid) {
@@ -529,6 +529,7 @@ __global__ void fp_chains(Tables T, FastArgs F) {
     u32 j = NONE32;
     for (u32 k = s; k <= e; k++)
         if ((F.fres[k] & 0x7F) != TB_CREATE_TRANSFER_OK) { j = k; break; }
+    if (j == NONE32 && F.ctl && (F.ctl[e] & TBGPU_CTL_DOOM)) j = e + 1;  // breaks on another shard
     u8 fin;
     if (j == NONE32) fin = TB_CREATE_TRANSFER_OK;
     else if (own == TB_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN) fin = own;

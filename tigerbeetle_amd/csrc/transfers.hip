@@ -516,7 +516,8 @@ __global__ void tr_finalize(TrArgs C, EvalState D) {
     if (i >= C.n) return;
     const u8 o = D.ok[i] & 1;
     const u32 cs = C.cs[i];
-    const bool persisted = cs == C.ce[i] || D.cfail[cs] == NONE32;
+    const bool doom = C.ctl && (C.ctl[C.ce[i]] & TBGPU_CTL_DOOM);  // broken on another shard
+    const bool persisted = (cs == C.ce[i] || D.cfail[cs] == NONE32) && !doom;
     D.ok[i] = o | ((o && persisted) ? 2 : 0);
 }
 
@@ -562,8 +563,10 @@ __global__ void tr_mask(Tables T, TrArgs C, EvalState S, u8* fres, u8* mask) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= C.n) return;
     const u32 cs = C.cs[i];
-    const bool inch = cs != C.ce[i];
-    const u32 cf = inch ? S.cfail[cs] : NONE32;
+    const bool doom = C.ctl && (C.ctl[C.ce[i]] & TBGPU_CTL_DOOM);
+    const bool inch = cs != C.ce[i] || doom;
+    u32 cf = inch ? S.cfail[cs] : NONE32;
+    if (cf == NONE32 && doom) cf = C.ce[i] + 1;  // the chain breaks after its last local member
     u8 r;
     if (C.sres[i] == TB_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN) r = TB_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN;
     else if (cf < i) r = TB_CREATE_TRANSFER_LINKED_EVENT_FAILED;

@@ -94,6 +94,9 @@ def lib():
     L.tbgpu_create_transfers_routed.restype = u64
     L.tbgpu_create_transfers_routed.argtypes = [vp, u32, vp, vp, vp, vp, ctypes.c_int, vp, vp,
                                                 ctypes.POINTER(ctypes.c_uint64)]
+    L.tbgpu_create_transfers_routed_device.restype = u64
+    L.tbgpu_create_transfers_routed_device.argtypes = [vp, u32, vp, vp, vp, vp, ctypes.c_int, vp, vp,
+                                                       ctypes.POINTER(ctypes.c_uint64)]
     L.tbgpu_import_transfers.restype = ctypes.c_int
     L.tbgpu_import_transfers.argtypes = [vp, vp, u32]
     L.tbgpu_advance_commit_timestamp.argtypes = [vp, u64]
@@ -184,6 +187,20 @@ class Engine:
                                               None if c is None else _ptr(c), int(bool(dry_run)), _ptr(out),
                                               _ptr(rc), ctypes.byref(cts))
         return out, rc, cts.value
+
+    def create_transfers_routed_tensors(self, counts, events, event_ts, ctl, dry_run, results):
+        """Routed sub-batches with every array a device tensor (torch, on this engine's
+        GPU): events uint8 [n*128], event_ts int64 [n], ctl uint8 [n] or None, results
+        a uint8 tensor of >= 8*n bytes that receives the concatenated sparse replies.
+        Returns (result_counts per sub-batch, commit_timestamp)."""
+        cs = np.ascontiguousarray(counts, dtype=np.uint32)
+        rc = np.zeros(len(cs), dtype=np.uint32)
+        cts = ctypes.c_uint64(0)
+        self._L.tbgpu_create_transfers_routed_device(
+            self._h, len(cs), _ptr(cs), ctypes.c_void_p(events.data_ptr()), ctypes.c_void_p(event_ts.data_ptr()),
+            None if ctl is None else ctypes.c_void_p(ctl.data_ptr()), int(bool(dry_run)),
+            ctypes.c_void_p(results.data_ptr()), _ptr(rc), ctypes.byref(cts))
+        return rc, cts.value
 
     def import_transfers(self, rows: np.ndarray) -> None:
         rows = np.ascontiguousarray(rows, dtype=TRANSFER_DTYPE)

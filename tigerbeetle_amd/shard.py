@@ -14,11 +14,15 @@ Per step (`create_transfers`):
 1. Timestamps.  The batch counts are all-gathered; batch g of the global order
    gets T_g = T_{g-1} + 1 + n_g (the harness rule, src/state_machine.zig:1973)
    and event i of it T_g - n_g + i + 1 (execute, :1031).
-2. Id directory round.  Transfer ids are hash-partitioned over ranks ("homes").
-   Each event sends its id (and, for post/void, its pending id) to its home,
-   which answers in global order: committed on shard O (EXISTS), first seen
-   earlier in this step (DUP, with that event's route) or new.  Pending ids
-   resolve the same way to the shard holding (or creating) the pending.
+2. Id directory.  The engines are the directory: a committed transfer is stored
+   on the owner of its ledger, so "is id X committed, and where" is a lookup in
+   every shard's id index (tbgpu_lookup_transfers).  The step's ids are
+   all-gathered and resolved in global order: committed on shard O (EXISTS),
+   first seen earlier in this step (DUP, with that event's route) or new.
+   Pending ids resolve the same way to the shard holding (or creating) the
+   pending.  (The device fast step below needs no directory at all when the
+   step's ids rise above every id seen before -- the benchmark's sequential ids,
+   and the key-range short-circuit of src/lsm/tree.zig:289-300.)
 3. Routing.  Regular transfers go to owner(t.ledger); a transfer whose id is
    committed on O goes to O (it can only fail there, with `exists*` or an
    earlier code, so no balance moves); post/void goes to the pending's shard,
@@ -33,7 +37,7 @@ Per step (`create_transfers`):
    chain of its own (TBGPU_CTL_CHAIN_END).  While any exist, rounds of dry runs
    find every part's first failure; the all-gathered minimum is the chain's
    break, after which members are skipped (TBGPU_CTL_SKIP) and parts that lie
-   wholly before it are doomed by a synthetic skipped member.  The rounds stop
+   wholly before it are rolled back (TBGPU_CTL_DOOM).  The rounds stop
    when no break moves (a Jacobi fixed point over the step, as in the engine's
    own general path), then the step commits for real.
 6. Hazards.  A duplicate id whose first occurrence (in another chain) routes
@@ -41,9 +45,8 @@ Per step (`create_transfers`):
    transfer created by a post/void in the same step, depends on an outcome on
    another shard: the step is split before the hazard's chain, the prefix
    commits, and the rest is routed again.
-7. Replies go back to the source ranks with a second all-to-all; committed
-   ids are registered with their homes; commit_timestamp is the max over
-   shards and is propagated to every engine.
+7. Replies go back to the source ranks with a second all-to-all;
+   commit_timestamp is the max over shards and is propagated to every engine.
 
 The backend of a rank is anything with the engine's commit API: the HIP
 engine (`tigerbeetle_amd.engine.Engine`) on GPUs; the CPU tests use the
@@ -60,6 +63,7 @@ from .types import ACCOUNT_DTYPE, RESULT_DTYPE, TRANSFER_DTYPE, TransferFlags
 
 CTL_CHAIN_END = 1  # include/tbgpu.h TBGPU_CTL_CHAIN_END
 CTL_SKIP = 2       # include/tbgpu.h TBGPU_CTL_SKIP
+CTL_DOOM = 4       # include/tbgpu.h TBGPU_CTL_DOOM
 LINKED_EVENT_FAILED = 1
 LINKED = int(TransferFlags.linked)
 POST_VOID = int(TransferFlags.post_pending_transfer | TransferFlags.void_pending_transfer)
@@ -73,13 +77,6 @@ NEW, EXISTS, DUP, PEND, PEND_NONE, PEND_HAZARD = range(6)
 
 def _id(lo, hi) -> int:
     return (int(hi) << 64) | int(lo)
-
-
-def _home(key: int, world: int) -> int:
-    z = (key ^ (key >> 64)) & 0xFFFFFFFFFFFFFFFF
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9 & 0xFFFFFFFFFFFFFFFF
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EB & 0xFFFFFFFFFFFFFFFF
-    return (z ^ (z >> 31)) % world
 
 
 class Comm:
@@ -139,7 +136,7 @@ class ShardedStateMachine:
         self.owner_of_ledger = owner_of_ledger or (lambda ledger: int(ledger) % self.world)
         self.prepare_timestamp = 0
         self.commit_timestamp = 0
-        self.committed = {}     # home part of the id directory: transfer id -> owning shard
+        self.max_id = 0         # every transfer id seen so far is <= this (the fast step's id filter)
         self.stats = {"steps": 0, "splits": 0, "dry_rounds": 0, "cross_chains": 0, "imports": 0}
 
     # ------------------------------------------------------------ accounts --
@@ -224,8 +221,10 @@ class ShardedStateMachine:
                 loc.append((g, i))
         ev = {k: my_events[k[0]][k[1]] for k in loc}
 
-        # ---- 2. id directory round
-        reqs = [[] for _ in range(W)]
+        # ---- 2. id directory round: every rank sees the step's ids in global order;
+        # the engines themselves are the directory of committed ids (a committed
+        # transfer lives on the owner of its ledger: routing below keeps that so)
+        mine = []
         for (g, i) in loc:
             t = ev[(g, i)]
             x = _id(t["id_lo"], t["id_hi"])
@@ -234,41 +233,35 @@ class ShardedStateMachine:
             if x == 0 or x == (1 << 128) - 1:
                 continue  # fails statically (:1250-1251): no directory entry
             hint = PV if pv else (self.owner_of_ledger(t["ledger"]) if int(t["ledger"]) else ANY)
-            reqs[_home(x, W)].append((g, i, 0, x, hint))
+            mine.append((g, i, 0, x, hint))
             if pv:
                 p = _id(t["pending_id_lo"], t["pending_id_hi"])
                 if p != 0 and p != (1 << 128) - 1 and p != x:
-                    reqs[_home(p, W)].append((g, i, 1, p, ANY))
-        got = self._exchange_objects(reqs)
-        # home: answer in global order (kind 0 before kind 1 of the same event)
-        recs = sorted(((g, i, k, key, hint, src) for src, lst in enumerate(got) for (g, i, k, key, hint) in lst),
-                      key=lambda r: (r[0], r[1], r[2]))
+                    mine.append((g, i, 1, p, ANY))
+        recs = sorted((r for lst in self.comm.all_gather_object(mine) for r in lst), key=lambda r: (r[0], r[1], r[2]))
+        committed = self._owners_of(sorted({r[3] for r in recs}))
         first = {}  # key -> (g, i, route hint) of its first occurrence this round
-        ans = [[] for _ in range(W)]
-        for (g, i, k, key, hint, src) in recs:
+        dir_id, dir_p = {}, {}
+        for (g, i, k, key, hint) in recs:
             if k == 0:
-                if key in self.committed:
-                    a = (EXISTS, self.committed[key], None)
+                if key in committed:
+                    a = (EXISTS, committed[key], None)
                 elif key in first:
                     fg, fi, fh = first[key]
                     a = (DUP, fh, (fg, fi))
                 else:
                     first[key] = (g, i, hint)
                     a = (NEW, None, None)
+                dir_id[(g, i)] = a
             else:
-                if key in self.committed:
-                    a = (PEND, self.committed[key], None)
+                if key in committed:
+                    a = (PEND, committed[key], None)
                 elif key in first and first[key][:2] < (g, i):
                     fg, fi, fh = first[key]
                     a = (PEND_HAZARD, None, (fg, fi)) if fh in (ANY, PV) else (PEND, fh, (fg, fi))
                 else:
                     a = (PEND_NONE, None, None)
-            ans[src].append((g, i, k, a))
-        back = self._exchange_objects(ans)
-        dir_id, dir_p = {}, {}
-        for lst in back:
-            for (g, i, k, a) in lst:
-                (dir_id if k == 0 else dir_p)[(g, i)] = a
+                dir_p[(g, i)] = a
 
         # ---- 3. routing of my events
         route, hazard = {}, None
@@ -409,23 +402,16 @@ class ShardedStateMachine:
                 raise RuntimeError("sharded commit: cross-shard chains did not converge")
             brk = nb
 
-        # ---- 7. replies to sources, committed ids to homes
+        # ---- 7. replies to sources
         rep = [[] for _ in range(W)]
-        homes = [[] for _ in range(W)]
-        failed = {(g, i) for (g, i, c), code in res if code != 0}
         for (g, i, c), code in res:
             if code != 0:
                 rep[glob[g][0]].append((g, i, code))
-        for (g, i, c, e) in mine:
-            if (g, i) not in failed:
-                x = _id(e["id_lo"], e["id_hi"])
-                homes[_home(x, W)].append((x, self.rank))
         for lst in self._exchange_objects(rep):
             for (g, i, code) in lst:
                 replies[g].append((i, code))
-        for lst in self._exchange_objects(homes):
-            for (x, o) in lst:
-                self.committed[x] = o
+        top = max([0] + [_id(e["id_lo"], e["id_hi"]) for (g, i, c, e) in mine])
+        self.max_id = max(self.max_id, self.comm.allreduce_max(top))
         if stop is None:
             return None
         return stop
@@ -473,6 +459,21 @@ class ShardedStateMachine:
         enc = [np.frombuffer(pickle.dumps(p), dtype=np.uint8) for p in parts]
         return [pickle.loads(x.tobytes()) for x in self.comm.alltoallv(enc)]
 
+    def _owners_of(self, keys):
+        """Collective.  {transfer id: owning shard} for the committed ids among `keys`
+        (the same list on every rank), looked up in every shard's engine.  Imported
+        copies answer like the original: the owner follows the row's ledger."""
+        found = {}
+        for k0 in range(0, len(keys), 4096):
+            part = keys[k0:k0 + 4096]
+            for r in self.backend.lookup_transfers(part):
+                found[_id(r["id_lo"], r["id_hi"])] = int(r["ledger"])
+        out = {}
+        for d in self.comm.all_gather_object(found):
+            for x, ledger in d.items():
+                out[x] = self.owner_of_ledger(ledger)
+        return out
+
     def _exchange_events(self, parts):
         enc = [np.ascontiguousarray(np.array(p, dtype=TRANSFER_DTYPE) if p else np.zeros(0, TRANSFER_DTYPE))
                .view(np.uint8).reshape(-1) for p in parts]
@@ -505,19 +506,15 @@ class ShardedStateMachine:
         """Owner sub-batches (one per source batch, global order) with chain control."""
         evs, ts, ctl, keys, counts = [], [], [], [], []
         cur_g, cnt = None, 0
-        by_chain = {}
+        last_local = {}
         for idx, (g, i, c, e) in enumerate(mine):
-            by_chain.setdefault(c, []).append(idx)
-        last_local = {c: lst[-1] for c, lst in by_chain.items()}
+            last_local[c] = idx
         for idx, (g, i, c, e) in enumerate(mine):
             if g != cur_g:
                 if cur_g is not None:
                     counts.append(cnt)
                 cur_g, cnt = g, 0
-            n_g = glob[g][2]
-            t_i = T[g] - n_g + i + 1
             b = 0
-            doom = False
             if c in span:
                 q = brk.get(c)
                 if q is not None and (g, i) > q:
@@ -525,23 +522,12 @@ class ShardedStateMachine:
                 if idx == last_local[c] and (g, i) != last_member[c]:
                     b |= CTL_CHAIN_END
                     if q is not None and (g, i) < q:
-                        doom = True   # the chain breaks after this part: roll it back
-            if doom:
-                evs.append(e)
-                ts.append(t_i)
-                ctl.append(0)   # stays linked: the synthetic member closes the part
-                keys.append((g, i, c))
-                evs.append(e)
-                ts.append(t_i)
-                ctl.append(CTL_SKIP | CTL_CHAIN_END)
-                keys.append(None)
-                cnt += 2
-            else:
-                evs.append(e)
-                ts.append(t_i)
-                ctl.append(b)
-                keys.append((g, i, c))
-                cnt += 1
+                        b |= CTL_DOOM   # the chain breaks after this part: roll it back
+            evs.append(e)
+            ts.append(T[g] - glob[g][2] + i + 1)
+            ctl.append(b)
+            keys.append((g, i, c))
+            cnt += 1
         if cur_g is not None:
             counts.append(cnt)
         return evs, ts, ctl, keys, counts
@@ -566,13 +552,10 @@ class ShardedStateMachine:
 
     # -------------------------------------------------------------- export --
     def export_state(self):
-        """Collective.  (accounts of the ledgers this shard owns, transfers committed
-        on this shard -- imported copies excluded): for parity checks."""
-        owners = {}
-        for d in self.comm.all_gather_object(self.committed):
-            owners.update(d)
+        """(accounts of the ledgers this shard owns, transfers committed on this shard --
+        imported copies excluded): for parity checks."""
         acc = self.backend.export_accounts()
         own = np.array([self.owner_of_ledger(l) == self.rank for l in acc["ledger"]], dtype=bool)
         xs = self.backend.export_transfers()
-        keep = np.array([owners.get(_id(r["id_lo"], r["id_hi"]), -1) == self.rank for r in xs], dtype=bool)
+        keep = np.array([self.owner_of_ledger(l) == self.rank for l in xs["ledger"]], dtype=bool)
         return acc[own] if len(acc) else acc, xs[keep] if len(xs) else xs

@@ -17,3 +17,12 @@ def test_gpu_sharded_flag_mix():
 def test_gpu_sharded_config4():
     stats = _check(("c4", 5, 2, 2, 2), 2, kind="gpu")
     assert stats["dry_rounds"] > 0
+
+
+@pytest.mark.gpu
+def test_gpu_device_step_config4():
+    """The device-resident routed step with the HIP engine behind every rank (the
+    engine's tbgpu_create_transfers_routed_device, fast path with chain control
+    and dry runs)."""
+    stats = _check(("c4", 17, 2, 3, 2), 2, kind="gpu", device_step=True)
+    assert stats["dry_rounds"] > 0 and stats["splits"] == 0

@@ -17,6 +17,7 @@ import numpy as np
 import pytest
 
 import oracle
+from tigerbeetle_amd.types import TRANSFER_DTYPE
 from tests.shard_workload import ShardWorkload, config4_small
 
 
@@ -36,7 +37,7 @@ def _backend(kind, w):
     return oracle.Oracle(len(w.accounts), 1 << 14)
 
 
-def _worker(rank, world, port, out_dir, spec, kind="oracle"):
+def _worker(rank, world, port, out_dir, spec, kind="oracle", device_step=False):
     import torch.distributed as dist
     from tigerbeetle_amd.shard import Comm, ShardedStateMachine
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -48,7 +49,17 @@ def _worker(rank, world, port, out_dir, spec, kind="oracle"):
         acc_replies = sm.create_accounts(w.account_batches if rank == 0 else [])
         replies = []
         for s in range(w.steps):
-            replies.append([r.tobytes() for r in sm.create_transfers(w.step_batches(s, rank))])
+            batches = w.step_batches(s, rank)
+            if device_step:
+                import torch
+                flat = np.concatenate(batches) if batches else np.zeros(0, dtype=TRANSFER_DTYPE)
+                # the router's collectives are gloo here, so its tensors stay on the CPU
+                # (a GPU backend stages them in HBM per call)
+                t = torch.from_numpy(flat.view(np.uint8).copy())
+                got = sm.create_transfers_device(t, [len(b) for b in batches])
+            else:
+                got = sm.create_transfers(batches)
+            replies.append([r.tobytes() for r in got])
         acc, xs = sm.export_state()
         with open(os.path.join(out_dir, f"r{rank}.pkl"), "wb") as f:
             pickle.dump({"replies": replies, "acc_replies": [a.tobytes() for a in acc_replies],
@@ -65,11 +76,11 @@ def _make(spec):
     return config4_small(seed, world, steps, B)
 
 
-def _check(spec, world, kind="oracle"):
+def _check(spec, world, kind="oracle", device_step=False):
     import torch.multiprocessing as mp
     from tigerbeetle_amd.types import ACCOUNT_DTYPE, RESULT_DTYPE, TRANSFER_DTYPE
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d, spec, kind), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), d, spec, kind, device_step), nprocs=world, join=True)
         outs = [pickle.load(open(os.path.join(d, f"r{r}.pkl"), "rb")) for r in range(world)]
     w = _make(spec)
     # the single state machine over the global order
@@ -111,3 +122,17 @@ def test_sharded_flag_mix_matches_single_state_machine(world):
 def test_sharded_config4_cross_ledger_pairs():
     stats = _check(("c4", 11, 2, 2, 2), 2)
     assert stats["dry_rounds"] > 0
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_device_step_config4(world):
+    """The device-resident step (monotone ids, no post/void: no directory, on-device
+    partition + all-to-all, dry rounds for the cross-ledger pairs)."""
+    stats = _check(("c4", 13 + world, world, 3, 2), world, device_step=True)
+    assert stats["dry_rounds"] > 0 and stats["splits"] == 0
+
+
+def test_device_step_falls_back_exactly():
+    """Non-monotone ids and post/void: the device step hands over to the exact router."""
+    stats = _check(("mix", 31, 2, 2, 2), 2, device_step=True)
+    assert stats["steps"] > 0

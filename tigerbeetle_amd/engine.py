@@ -121,6 +121,7 @@ class Engine:
         opt = Options(device=device, accounts_max=accounts_max, transfers_max=transfers_max,
                       history_max=history_max, events_per_call_max=events_per_call_max,
                       flags=OPT_FORCE_GENERAL if force_general else 0)
+        self.device = device
         h = ctypes.c_void_p()
         rc = self._L.tbgpu_init(ctypes.byref(h), ctypes.byref(opt))
         if rc != 0:
@@ -193,6 +194,12 @@ class Engine:
         GPU): events uint8 [n*128], event_ts int64 [n], ctl uint8 [n] or None, results
         a uint8 tensor of >= 8*n bytes that receives the concatenated sparse replies.
         Returns (result_counts per sub-batch, commit_timestamp)."""
+        host_results = None
+        if not events.is_cuda:  # CPU tensors (the gloo-routed tests): stage them in HBM
+            dev = f"cuda:{self.device}"
+            events, event_ts = events.to(dev), event_ts.to(dev)
+            ctl = None if ctl is None else ctl.to(dev)
+            host_results, results = results, results.to(dev)
         cs = np.ascontiguousarray(counts, dtype=np.uint32)
         rc = np.zeros(len(cs), dtype=np.uint32)
         cts = ctypes.c_uint64(0)
@@ -200,6 +207,8 @@ class Engine:
             self._h, len(cs), _ptr(cs), ctypes.c_void_p(events.data_ptr()), ctypes.c_void_p(event_ts.data_ptr()),
             None if ctl is None else ctypes.c_void_p(ctl.data_ptr()), int(bool(dry_run)),
             ctypes.c_void_p(results.data_ptr()), _ptr(rc), ctypes.byref(cts))
+        if host_results is not None:
+            host_results.copy_(results.cpu())
         return rc, cts.value
 
     def import_transfers(self, rows: np.ndarray) -> None:

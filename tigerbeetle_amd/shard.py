@@ -200,6 +200,200 @@ class ShardedStateMachine:
             out.append(res)
         return out
 
+    # ------------------------------------------------------ device step --
+    def create_transfers_device(self, events, counts):
+        """One routed step with the events already in device memory: `events` is a
+        uint8 tensor of n*128 bytes on this rank's device, `counts` its batch sizes.
+        Returns this rank's replies (one RESULT_DTYPE array per batch).
+
+        Fast when the step has no post/void and its ids rise strictly along the
+        global order above every id seen before (no directory lookup can hit);
+        routing, partition and exchange then stay on the device: owner = ledger
+        % world, a stable partition by owner, RCCL all-to-all of the events and of
+        24-byte side records {timestamp, (batch, index), chain}, the owner's
+        tbgpu_create_transfers_routed_device, and dry rounds only when chains span
+        shards.  Anything else goes through create_transfers (exact, host side)."""
+        torch = self.comm.torch
+        dev = self.comm.device
+        W, me = self.world, self.rank
+        n = int(sum(counts))
+        ev = events.view(torch.uint8).reshape(-1)[:n * 128]
+        w32 = ev.view(torch.int32).view(n, 32)
+        w64 = ev.view(torch.int64).view(n, 16)
+        flags = (w32[:, 29] >> 16) & 0xFFFF
+        id_lo, id_hi = w64[:, 0], w64[:, 1]
+        # eligibility, one small all-gather: [n, min id, max id, monotone, plain]
+        if n:
+            mono = bool((id_lo[1:] > id_lo[:-1]).all()) if n > 1 else True
+            plain = bool(((flags & POST_VOID) == 0).all() & (id_hi == 0).all() & (id_lo > 0).all())
+            st = [n, int(id_lo.min()), int(id_lo.max()), int(mono), int(plain)]
+        else:
+            st = [0, 0, 0, 1, 1]
+        stats = torch.tensor(st, dtype=torch.int64, device=dev)
+        allst = [torch.empty_like(stats) for _ in range(W)]
+        self.comm.dist.all_gather(allst, stats, group=self.comm.group)
+        allst = [x.cpu().tolist() for x in allst]
+        ok, prev = True, self.max_id
+        for (cnt, lo, hi, mono, plain) in allst:
+            if cnt == 0:
+                continue
+            ok &= bool(mono and plain and lo > prev)
+            prev = hi
+        if not ok:
+            host = ev.cpu().numpy().view(TRANSFER_DTYPE)
+            offs = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+            return self.create_transfers([host[offs[j]:offs[j + 1]] for j in range(len(counts))])
+        self.max_id = max(self.max_id, prev)
+
+        # global order and timestamps (host: one entry per batch)
+        counts_all = self.comm.all_gather_object(list(map(int, counts)))
+        glob = [(r, j, c) for r, cl in enumerate(counts_all) for j, c in enumerate(cl)]
+        T = []
+        for r, j, c in glob:
+            self.prepare_timestamp += 1 + c
+            T.append(self.prepare_timestamp)
+        g0 = sum(len(cl) for cl in counts_all[:me])
+        if n:
+            cnt_t = torch.tensor(list(counts), dtype=torch.int64, device=dev)
+            nb = len(counts)
+            bidx = torch.repeat_interleave(torch.arange(nb, device=dev), cnt_t)
+            bstart = torch.cumsum(cnt_t, 0) - cnt_t
+            pos = torch.arange(n, device=dev) - bstart[bidx]
+            g = bidx + g0
+            Tg = torch.tensor(T, dtype=torch.int64, device=dev)
+            ng = torch.tensor([c for (_, _, c) in glob], dtype=torch.int64, device=dev)
+            ts = Tg[g] - ng[g] + pos + 1
+            linked = (flags & LINKED) != 0
+            prev_l = torch.zeros_like(linked)
+            prev_l[1:] = linked[:-1]
+            prev_l &= pos > 0
+            ar = torch.arange(n, device=dev)
+            cstart = torch.cummax(torch.where(prev_l, torch.zeros_like(ar), ar), 0).values
+            last = ~linked | (pos == cnt_t[bidx] - 1)      # the chain's own last member
+            owner = ((w32[:, 28].to(torch.int64) & 0xFFFFFFFF) % W)
+            omin = torch.full((n,), W, dtype=torch.int64, device=dev).scatter_reduce(0, cstart, owner, "amin")
+            omax = torch.full((n,), -1, dtype=torch.int64, device=dev).scatter_reduce(0, cstart, owner, "amax")
+            span = omin[cstart] != omax[cstart]
+            side = torch.stack([ts, (g << 32) | pos, (g << 32) | (cstart - bstart[bidx]),
+                                span.to(torch.int64) | (last.to(torch.int64) << 1)], 1)
+            perm = torch.argsort(owner, stable=True)
+            send = torch.bincount(owner, minlength=W)
+            ev_s = ev.view(n, 128).index_select(0, perm)
+            side_s = side.index_select(0, perm)
+        else:
+            send = torch.zeros(W, dtype=torch.int64, device=dev)
+            ev_s = torch.zeros((0, 128), dtype=torch.uint8, device=dev)
+            side_s = torch.zeros((0, 4), dtype=torch.int64, device=dev)
+        recv = torch.empty_like(send)
+        self.comm.dist.all_to_all_single(recv, send, group=self.comm.group)
+        sl, rl = send.cpu().tolist(), recv.cpu().tolist()
+        m = int(sum(rl))
+        R = torch.empty((m, 128), dtype=torch.uint8, device=dev)
+        S = torch.empty((m, 4), dtype=torch.int64, device=dev)
+        self.comm.dist.all_to_all_single(R, ev_s, rl, sl, group=self.comm.group)
+        self.comm.dist.all_to_all_single(S, side_s, rl, sl, group=self.comm.group)
+
+        # owner side: sub-batches in global order, chain control
+        res_pairs = []
+        if m:
+            gk = S[:, 1] >> 32
+            _, sub_counts = torch.unique_consecutive(gk, return_counts=True)
+            sub_counts = sub_counts.cpu().tolist()
+            key = S[:, 2]
+            spanm = (S[:, 3] & 1) != 0
+            lastm = (S[:, 3] & 2) != 0
+            nxt = torch.ones(m, dtype=torch.bool, device=dev)
+            nxt[:-1] = key[1:] != key[:-1]                 # last local member of its chain
+            base = (spanm & nxt & ~lastm).to(torch.uint8) * CTL_CHAIN_END
+            n_span = int(spanm.sum())
+        else:
+            sub_counts, n_span = [], 0
+        any_span = self.comm.allreduce_max(n_span) > 0
+        results = torch.empty(max(m, 1) * 8, dtype=torch.uint8, device=dev)
+        ts_r = S[:, 0].contiguous() if m else torch.zeros(1, dtype=torch.int64, device=dev)
+        Rf = R.reshape(-1) if m else torch.zeros(128, dtype=torch.uint8, device=dev)
+        offs = np.concatenate([[0], np.cumsum(sub_counts)]).astype(np.int64)
+
+        def commit(ctl, dry):
+            if not m:
+                return np.zeros(0, dtype=RESULT_DTYPE), np.zeros(0, dtype=np.int64), 0
+            rc, cts = self.backend.create_transfers_routed_tensors(sub_counts, Rf, ts_r, ctl, dry, results)
+            tot = int(np.sum(rc))
+            out = results[:tot * 8].cpu().numpy().view(RESULT_DTYPE).copy() if tot else np.zeros(0, RESULT_DTYPE)
+            at = np.repeat(offs[:-1], rc.astype(np.int64)) + out["index"].astype(np.int64) if tot else \
+                np.zeros(0, np.int64)
+            return out, at, cts
+
+        if not any_span:
+            out, at, cts = commit(None, False)
+        else:
+            self.stats["dry_rounds"] += 1
+            si = torch.nonzero(spanm).flatten() if m else torch.zeros(0, dtype=torch.int64, device=dev)
+            span_idx = si.cpu().numpy()
+            span_key = key[si].cpu().numpy() if m else np.zeros(0, np.int64)
+            span_pos = S[si, 1].cpu().numpy() if m else np.zeros(0, np.int64)
+            span_base = base[si].cpu().numpy() if m else np.zeros(0, np.uint8)
+            span_last = (nxt[si] & ~lastm[si]).cpu().numpy() if m else np.zeros(0, bool)
+            brk = {}
+            for _ in range(MAX_ROUNDS):
+                c = span_base.copy()
+                for q, (k, p) in enumerate(zip(span_key, span_pos)):
+                    b = brk.get(int(k))
+                    if b is not None:
+                        if p > b:
+                            c[q] |= CTL_SKIP
+                        elif span_last[q] and p < b:
+                            c[q] |= CTL_DOOM
+                ctl = torch.zeros(max(m, 1), dtype=torch.uint8, device=dev)
+                if m and len(span_idx):
+                    ctl[si] = torch.from_numpy(c).to(dev)
+                out, at, cts = commit(ctl, True)
+                fails = {}
+                where = dict(zip(span_idx.tolist(), range(len(span_idx))))
+                for a, r in zip(at.tolist(), out["result"].tolist()):
+                    q = where.get(a)
+                    if q is not None and r not in (0, LINKED_EVENT_FAILED):
+                        k = int(span_key[q])
+                        fails[k] = min(fails.get(k, 1 << 62), int(span_pos[q]))
+                nb_ = {}
+                for d in self.comm.all_gather_object(fails):
+                    for k, p in d.items():
+                        nb_[k] = min(nb_.get(k, 1 << 62), p)
+                if nb_ == brk:
+                    out2, at2, cts = commit(ctl, False)
+                    assert out2.tobytes() == out.tobytes(), "sharded commit: dry run and commit disagree"
+                    out, at = out2, at2
+                    break
+                brk = nb_
+                self.stats["dry_rounds"] += 1
+            else:
+                raise RuntimeError("sharded commit: cross-shard chains did not converge")
+        # replies to their sources
+        if len(at):
+            pg = S[torch.from_numpy(at).to(dev), 1].cpu().numpy()
+        else:
+            pg = np.zeros(0, np.int64)
+        rep = [[] for _ in range(W)]
+        for pgv, r in zip(pg.tolist(), out["result"].tolist()):
+            gg = pgv >> 32
+            rep[glob[gg][0]].append((gg, pgv & 0xFFFFFFFF, r))
+        mine = {j: [] for j in range(len(counts))}
+        for lst in self._exchange_objects(rep):
+            for (gg, i, r) in lst:
+                mine[gg - g0].append((i, r))
+        ts_all = self.comm.allreduce_max(cts if m else self.backend.commit_timestamp())
+        self.backend.advance_commit_timestamp(ts_all)
+        self.commit_timestamp = ts_all
+        replies = []
+        for j in range(len(counts)):
+            a = np.array(sorted(mine[j]), dtype=np.uint32).reshape(-1, 2)
+            res = np.zeros(len(a), dtype=RESULT_DTYPE)
+            if len(a):
+                res["index"], res["result"] = a[:, 0], a[:, 1]
+            replies.append(res)
+        self.stats["steps"] += 1
+        return replies
+
     def _sync_commit_timestamp(self):
         ts = self.comm.allreduce_max(self.backend.commit_timestamp())
         self.backend.advance_commit_timestamp(ts)

@@ -82,6 +82,33 @@ typedef struct tb_account_history_t {
     uint8_t reserved[88];
 } tb_account_history_t;
 
+/* AccountFilter, src/tigerbeetle.zig:268-302 (64 B): the input of
+ * get_account_transfers / get_account_history. */
+typedef struct tb_account_filter_t {
+    tb_uint128_t account_id;
+    uint64_t timestamp_min;  /* inclusive; 0 = no lower bound */
+    uint64_t timestamp_max;  /* inclusive; 0 = no upper bound */
+    uint32_t limit;
+    uint32_t flags;          /* TB_ACCOUNT_FILTER_* */
+    uint8_t reserved[24];
+} tb_account_filter_t;
+/* AccountFilterFlags, src/tigerbeetle.zig:289-302 */
+enum {
+    TB_ACCOUNT_FILTER_DEBITS = 1 << 0,
+    TB_ACCOUNT_FILTER_CREDITS = 1 << 1,
+    TB_ACCOUNT_FILTER_REVERSED = 1 << 2,
+};
+
+/* AccountBalance, src/tigerbeetle.zig:65-78 (128 B): one get_account_history row. */
+typedef struct tb_account_balance_t {
+    tb_uint128_t debits_pending;
+    tb_uint128_t debits_posted;
+    tb_uint128_t credits_pending;
+    tb_uint128_t credits_posted;
+    uint64_t timestamp;
+    uint8_t reserved[56];
+} tb_account_balance_t;
+
 /* AccountFlags, src/tigerbeetle.zig:42-63 */
 enum {
     TB_ACCOUNT_LINKED = 1 << 0,
@@ -316,6 +343,44 @@ void tbgpu_advance_commit_timestamp(tbgpu_ctx* ctx, uint64_t timestamp);
  * found objects are written densely in request order; returns the count. */
 uint32_t tbgpu_lookup_accounts(tbgpu_ctx* ctx, const tb_uint128_t* ids, uint32_t count, tb_account_t* out);
 uint32_t tbgpu_lookup_transfers(tbgpu_ctx* ctx, const tb_uint128_t* ids, uint32_t count, tb_transfer_t* out);
+
+/* ------------------------------------------------------------------------ */
+/* Account queries                                     */
+/* ------------------------------------------------------------------------ */
+/* constants.batch_max.get_account_transfers / _history: message_body_size_max /
+ * 128 B (src/state_machine.zig:53-76). */
+#define TBGPU_QUERY_MAX 8190u
+
+/* StateMachine.compact (src/state_machine.zig:930-955): fold the transfers stored
+ * since the previous compaction into the account-transfers index (the
+ * debit_account_id / credit_account_id index trees of the transfers groove,
+ * :198-220).  Queries compact first, so calling it is optional; a replica calls it
+ * once per op, off the commit's critical path.  Returns the rows indexed. */
+uint64_t tbgpu_compact(tbgpu_ctx* ctx);
+
+/* execute_get_account_transfers with its prefetch scan (src/state_machine.zig:693-734,
+ * :822-885, :1128-1147): the stored transfers whose debit (flags.debits) or credit
+ * (flags.credits) account is filter->account_id, with timestamp_min <= timestamp <=
+ * timestamp_max (0 = unbounded), in timestamp order (descending with
+ * flags.reversed), at most min(limit, TBGPU_QUERY_MAX).  An invalid filter
+ * (:822-833) yields nothing.  Returns the count written to `out`. */
+uint32_t tbgpu_get_account_transfers(tbgpu_ctx* ctx, const tb_account_filter_t* filter, tb_transfer_t* out);
+
+/* execute_get_account_history (:736-808, :1149-1196): the same scan, each
+ * transfer's account-history row (the filter account's balances after it), for
+ * an account with flags.history.  A post/void transfer stores no history row
+ * (:1342-1364 is create_transfer only); the reference's lookup then asserts
+ * (src/lsm/scan_lookup.zig:179, :215) -- here the transfer is skipped. */
+uint32_t tbgpu_get_account_history(tbgpu_ctx* ctx, const tb_account_filter_t* filter, tb_account_balance_t* out);
+
+/* Many queries in one launch, everything in device memory: filter q's results
+ * are written at out_device + q * stride (128-B rows), at most
+ * min(limit, TBGPU_QUERY_MAX, stride); result_counts (host) receives the counts.
+ * Returns the total. */
+uint64_t tbgpu_get_account_transfers_device(tbgpu_ctx* ctx, uint32_t count, const void* filters_device,
+                                            uint32_t stride, void* out_device, uint32_t* result_counts);
+uint64_t tbgpu_get_account_history_device(tbgpu_ctx* ctx, uint32_t count, const void* filters_device,
+                                          uint32_t stride, void* out_device, uint32_t* result_counts);
 
 /* Test harness `setup` action (src/state_machine.zig:1892-1908): overwrite an
  * existing account's four balances.  Returns 0, or -1 if the account is missing. */

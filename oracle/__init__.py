@@ -10,8 +10,8 @@ import subprocess
 
 import numpy as np
 
-from tigerbeetle_amd.types import (ACCOUNT_DTYPE, HISTORY_DTYPE, RESULT_DTYPE, TRANSFER_DTYPE,
-                                   U64_MAX, u128_array)
+from tigerbeetle_amd.types import (ACCOUNT_DTYPE, BALANCE_DTYPE, FILTER_DTYPE, HISTORY_DTYPE, QUERY_MAX,
+                                   RESULT_DTYPE, TRANSFER_DTYPE, U64_MAX, u128_array)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "liboracle.so")
@@ -72,6 +72,9 @@ def lib():
         L.orc_import_transfers.restype = ctypes.c_int
         L.orc_import_transfers.argtypes = [vp, vp, u32]
         L.orc_advance_commit_timestamp.argtypes = [vp, u64]
+        for name in ("orc_get_account_transfers", "orc_get_account_history"):
+            getattr(L, name).restype = u32
+            getattr(L, name).argtypes = [vp, vp, vp]
         L.orc_sum_overflows_u64.restype = ctypes.c_int
         L.orc_sum_overflows_u64.argtypes = [u64, u64]
         L.orc_sum_overflows_u128.restype = ctypes.c_int
@@ -218,6 +221,21 @@ class Oracle:
 
     def get_posted(self, pending_id: int) -> int:
         return self._L.orc_get_posted(self._h, u128(pending_id))
+
+    def get_account_transfers(self, filt: np.ndarray) -> np.ndarray:
+        f = np.ascontiguousarray(filt, dtype=FILTER_DTYPE).reshape(1)
+        out = np.zeros(QUERY_MAX, dtype=TRANSFER_DTYPE)
+        n = self._L.orc_get_account_transfers(self._h, _ptr(f), _ptr(out))
+        return out[:n].copy()
+
+    def get_account_history(self, filt: np.ndarray) -> np.ndarray:
+        f = np.ascontiguousarray(filt, dtype=FILTER_DTYPE).reshape(1)
+        out = np.zeros(QUERY_MAX, dtype=BALANCE_DTYPE)
+        n = self._L.orc_get_account_history(self._h, _ptr(f), _ptr(out))
+        return out[:n].copy()
+
+    def compact(self) -> int:
+        return self.transfer_count()  # the oracle scans its rows directly
 
 
 def sum_overflows(bits: int, a: int, b: int) -> bool:

@@ -11,6 +11,7 @@
  *   get_transfer / get_posted        src/state_machine.zig:1563-1573
  *   sum_overflows                    src/state_machine.zig:1645-1650
  *   lookup_accounts / _transfers     src/state_machine.zig:1091-1126
+ *   get_account_transfers / _history src/state_machine.zig:693-885, :1128-1196
  *
  * State is three maps (accounts, transfers, posted) plus the account-history
  * log.  Linked-chain scopes (scope_open/scope_close, :972-1000) are an undo log
@@ -126,6 +127,7 @@ struct orc {
     map_t posted_map;   /* pending timestamp -> fulfillment */
     tb_account_history_t* history; uint64_t history_len, history_cap;
     uint64_t commit_timestamp;
+    uint64_t* imp; uint64_t imp_len, imp_cap;  /* rows imported from other shards, ascending */
     /* scope (at most one open at a time: chains do not nest) */
     int scope_open;
     undo_t* undo; uint64_t undo_len, undo_cap;
@@ -597,7 +599,7 @@ orc_t* orc_new(uint64_t accounts_hint, uint64_t transfers_hint) {
 void orc_free(orc_t* o) {
     if (!o) return;
     map_free(&o->account_map); map_free(&o->transfer_map); map_free(&o->posted_map);
-    free(o->accounts); free(o->transfers); free(o->history); free(o->undo);
+    free(o->accounts); free(o->transfers); free(o->history); free(o->undo); free(o->imp);
     free(o);
 }
 
@@ -730,6 +732,7 @@ static orc_t* orc_clone(const orc_t* o) {
     c->transfers = (tb_transfer_t*)dup_array(o->transfers, o->transfers_cap, sizeof(tb_transfer_t));
     c->history = (tb_account_history_t*)dup_array(o->history, o->history_cap, sizeof(tb_account_history_t));
     c->undo = (undo_t*)dup_array(o->undo, o->undo_cap, sizeof(undo_t));
+    c->imp = (uint64_t*)dup_array(o->imp, o->imp_cap, sizeof(uint64_t));
     return c;
 }
 
@@ -759,6 +762,8 @@ int orc_import_transfers(orc_t* o, const tb_transfer_t* rows, uint32_t count) {
                                             sizeof(tb_transfer_t));
         o->transfers[o->transfers_len] = rows[i];
         map_put_new(&o->transfer_map, G(rows[i].id), o->transfers_len);
+        o->imp = (uint64_t*)grow(o->imp, &o->imp_cap, o->imp_len + 1, sizeof(uint64_t));
+        o->imp[o->imp_len++] = o->transfers_len;  /* another shard's transfer: never queried here */
         o->transfers_len++;
     }
     return 0;
@@ -766,4 +771,96 @@ int orc_import_transfers(orc_t* o, const tb_transfer_t* rows, uint32_t count) {
 
 void orc_advance_commit_timestamp(orc_t* o, uint64_t timestamp) {
     if (timestamp > o->commit_timestamp) o->commit_timestamp = timestamp;
+}
+
+/* ------------------------------------------------------------- queries --- */
+
+#define QUERY_MAX 8190u /* constants.batch_max.get_account_transfers / _history (src/state_machine.zig:53-76) */
+
+/* get_scan_from_filter's validity test (src/state_machine.zig:822-833). */
+static int filter_valid(const tb_account_filter_t* f) {
+    const u128 id = G(f->account_id);
+    for (int k = 0; k < 24; k++)
+        if (f->reserved[k]) return 0;
+    return id != 0 && id != U128_MAX && f->timestamp_min != UINT64_MAX && f->timestamp_max != UINT64_MAX &&
+           (f->timestamp_max == 0 || f->timestamp_min <= f->timestamp_max) && f->limit != 0 &&
+           (f->flags & (TB_ACCOUNT_FILTER_DEBITS | TB_ACCOUNT_FILTER_CREDITS)) != 0 && (f->flags >> 3) == 0;
+}
+
+static int row_imported(const orc_t* o, uint64_t row) {
+    uint64_t lo = 0, hi = o->imp_len;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) / 2;
+        if (o->imp[mid] < row) lo = mid + 1; else hi = mid;
+    }
+    return lo < o->imp_len && o->imp[lo] == row;
+}
+
+/* The account-history row stored under `timestamp` (rows ascend in timestamp). */
+static const tb_account_history_t* history_at(const orc_t* o, uint64_t timestamp) {
+    uint64_t lo = 0, hi = o->history_len;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) / 2;
+        if (o->history[mid].timestamp < timestamp) lo = mid + 1; else hi = mid;
+    }
+    return lo < o->history_len && o->history[lo].timestamp == timestamp ? &o->history[lo] : NULL;
+}
+
+/* The scan behind both queries: the union of the debit_account_id and
+ * credit_account_id prefix scans (:850-884) over the stored transfers -- in
+ * timestamp order, which is their insertion order -- restricted to
+ * [timestamp_min, timestamp_max] (0 = TimestampRange.timestamp_min / _max,
+ * src/lsm/timestamp_range.zig:4-5), descending when reversed, and cut at
+ * min(limit, batch_max) objects (:710-713).  get_account_history then looks up
+ * the history row of each timestamp (:769-779); a post/void transfer has none
+ * (only create_transfer stores one, :1342-1364) and the reference's lookup would
+ * assert (src/lsm/scan_lookup.zig:179, :215): it is skipped here. */
+static uint32_t scan_account(orc_t* o, const tb_account_filter_t* f, int history, void* out) {
+    const u128 id = G(f->account_id);
+    const uint32_t limit = f->limit < QUERY_MAX ? f->limit : QUERY_MAX;
+    const uint64_t tlo = f->timestamp_min ? f->timestamp_min : 1;
+    const uint64_t thi = f->timestamp_max ? f->timestamp_max : UINT64_MAX - 1;
+    const int rev = (f->flags & TB_ACCOUNT_FILTER_REVERSED) != 0;
+    const int dr = (f->flags & TB_ACCOUNT_FILTER_DEBITS) != 0, cr = (f->flags & TB_ACCOUNT_FILTER_CREDITS) != 0;
+    uint32_t n = 0;
+    for (uint64_t k = 0; k < o->transfers_len && n < limit; k++) {
+        const uint64_t i = rev ? o->transfers_len - 1 - k : k;
+        const tb_transfer_t* t = &o->transfers[i];
+        if (t->timestamp < tlo || t->timestamp > thi) continue;
+        if (!((dr && G(t->debit_account_id) == id) || (cr && G(t->credit_account_id) == id))) continue;
+        if (row_imported(o, i)) continue;
+        if (!history) {
+            ((tb_transfer_t*)out)[n++] = *t;
+            continue;
+        }
+        const tb_account_history_t* h = history_at(o, t->timestamp);
+        if (!h) continue;
+        /* execute_get_account_history (:1171-1192) */
+        tb_account_balance_t b;
+        memset(&b, 0, sizeof b);
+        if (G(h->dr_account_id) == id) {
+            b.debits_pending = h->dr_debits_pending; b.debits_posted = h->dr_debits_posted;
+            b.credits_pending = h->dr_credits_pending; b.credits_posted = h->dr_credits_posted;
+        } else {
+            b.debits_pending = h->cr_debits_pending; b.debits_posted = h->cr_debits_posted;
+            b.credits_pending = h->cr_credits_pending; b.credits_posted = h->cr_credits_posted;
+        }
+        b.timestamp = h->timestamp;
+        ((tb_account_balance_t*)out)[n++] = b;
+    }
+    return n;
+}
+
+/* execute_get_account_transfers (src/state_machine.zig:693-734, :1128-1147) */
+uint32_t orc_get_account_transfers(orc_t* o, const tb_account_filter_t* f, tb_transfer_t* out) {
+    return filter_valid(f) ? scan_account(o, f, 0, out) : 0;
+}
+
+/* execute_get_account_history (src/state_machine.zig:736-808, :1149-1196): only for
+ * an existing account with flags.history (:759-761). */
+uint32_t orc_get_account_history(orc_t* o, const tb_account_filter_t* f, tb_account_balance_t* out) {
+    if (!filter_valid(f)) return 0;
+    const tb_account_t* a = get_account(o, G(f->account_id));
+    if (!a || !(a->flags & TB_ACCOUNT_HISTORY)) return 0;
+    return scan_account(o, f, 1, out);
 }

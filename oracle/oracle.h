@@ -56,6 +56,9 @@ uint32_t orc_lookup_transfers(orc_t* o, const tb_uint128_t* ids, uint32_t count,
 int orc_set_balances(orc_t* o, tb_uint128_t id, tb_uint128_t dp, tb_uint128_t dpo, tb_uint128_t cp,
                      tb_uint128_t cpo);
 
+uint32_t orc_get_account_transfers(orc_t* o, const tb_account_filter_t* f, tb_transfer_t* out);
+uint32_t orc_get_account_history(orc_t* o, const tb_account_filter_t* f, tb_account_balance_t* out);
+
 uint64_t orc_account_count(orc_t* o);
 uint64_t orc_transfer_count(orc_t* o);
 uint64_t orc_history_count(orc_t* o);

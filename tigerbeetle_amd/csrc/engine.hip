@@ -19,6 +19,7 @@
 #include "engine.h"
 #include "transfers.h"
 #include "fast.h"
+#include "query.h"
 
 [[noreturn]] void tbgpu_fatal(const char* what, const char* why, const char* file, int line) {
     fprintf(stderr, "tbgpu: fatal: %s: %s (%s:%d)\n", what, why, file, line);
@@ -101,6 +102,12 @@ struct tbgpu_ctx {
     const u64* rt_ev_ts = nullptr;
     const u8* rt_ctl = nullptr;
     bool rt_dry = false;
+    // account-transfers index (query.hip), allocated by the first compaction
+    u32 *q_key = nullptr, *q_val = nullptr, *q_tkey = nullptr, *q_tval = nullptr;
+    SortScratch q_ss{};
+    u64* q_runs_dev = nullptr;
+    std::vector<u64> q_runs{0};  // row boundaries of the index runs; back() = rows indexed
+    u8* ximp = nullptr;          // per stored row: 1 = imported from another shard
     hipEvent_t ev0, ev1;
     // phase profiler: consecutive marks on the ctx stream; segment k belongs to
     // the phase opened by mark k.
@@ -261,8 +268,10 @@ extern "C" void tbgpu_reset(tbgpu_ctx* c) {
     HIP_CHECK(hipMemsetAsync(c->T.idr, 0, 2 * sizeof(u64), c->stream));                  // max = 0
     HIP_CHECK(hipMemsetAsync(c->T.idr + 2, 0xFF, 2 * sizeof(u64), c->stream));           // min = ~0
     HIP_CHECK(hipMemsetAsync(c->T.big, 0, sizeof(u32), c->stream));
+    if (c->ximp) HIP_CHECK(hipMemsetAsync(c->ximp, 0, c->xrow_cap, c->stream));
     HIP_CHECK(hipStreamSynchronize(c->stream));
     c->n_accounts = c->n_rows = c->n_hist = 0;
+    c->q_runs.assign(1, 0);
 }
 
 extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
@@ -277,7 +286,8 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
                     c->sval_s, c->spos, c->bb, c->ss.keys_tmp, c->ss.vals_tmp, c->ss.hist, c->side_tiles,
                     c->sc.tile_sums, c->fres, c->mask, c->ranks, c->res_buf, c->counts, c->counters, c->status,
                     c->f_gtab, c->f_gpos, c->f_keys, c->f_rows,
-                    c->f_tile_idr, c->rt_ts_buf, c->rt_ctl_buf, c->rt_dry_ts};
+                    c->f_tile_idr, c->rt_ts_buf, c->rt_ctl_buf, c->rt_dry_ts, c->q_key, c->q_val, c->q_tkey,
+                    c->q_tval, c->q_ss.keys_tmp, c->q_ss.vals_tmp, c->q_ss.hist, c->q_runs_dev, c->ximp};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     for (EvalState& s : c->st) {
         void* q[] = {s.res, s.ok, s.pref, s.cfail, s.amt, s.pamt, s.dpend, s.dpost};
@@ -653,6 +663,11 @@ extern "C" int tbgpu_import_transfers(tbgpu_ctx* c, const tb_transfer_t* rows, u
         const u32 k = (u32)std::min<u64>(n - off, c->nmax);
         HIP_CHECK(hipMemcpyAsync(c->ev_buf, keep.data() + off, (u64)k * 128, hipMemcpyHostToDevice, c->stream));
         launch_import_transfers(c->T, (const Transfer*)c->ev_buf, k, c->n_rows, c->stream);
+        if (!c->ximp) {
+            c->ximp = dalloc<u8>(c->xrow_cap, &c->bytes);
+            HIP_CHECK(hipMemsetAsync(c->ximp, 0, c->xrow_cap, c->stream));
+        }
+        HIP_CHECK(hipMemsetAsync(c->ximp + c->n_rows, 1, k, c->stream));  // not this shard's: never queried
         HIP_CHECK(hipStreamSynchronize(c->stream));
         c->n_rows += k;
         off += k;
@@ -804,6 +819,104 @@ extern "C" uint32_t tbgpu_lookup_transfers(tbgpu_ctx* c, const tb_uint128_t* ids
     return lookup(c, ids, count, (Transfer*)out, [&](const u128* d, u32 k, Transfer* o, u8* f) {
         launch_lookup_transfers(c->T, d, k, o, f, c->stream);
     });
+}
+
+// ------------------------------------------- account-transfers index ------
+
+// Stable re-sort of the index entries [e0, e1) by account row: rows already in
+// order within an account stay in order (query.hip).
+static void q_sort(tbgpu_ctx* c, u64 e0, u64 e1) {
+    const u64 m = e1 - e0;
+    radix_sort_pairs(c->q_key + e0, c->q_val + e0, c->q_tkey + e0, c->q_tval + e0, m, log2u(c->accounts_max + 1),
+                     c->q_ss, c->stream);
+    HIP_CHECK(hipMemcpyAsync(c->q_key + e0, c->q_tkey + e0, m * 4, hipMemcpyDeviceToDevice, c->stream));
+    HIP_CHECK(hipMemcpyAsync(c->q_val + e0, c->q_tval + e0, m * 4, hipMemcpyDeviceToDevice, c->stream));
+}
+
+extern "C" uint64_t tbgpu_compact(tbgpu_ctx* c) {
+    HIP_CHECK(hipSetDevice(c->device));
+    const u64 r0 = c->q_runs.back(), r1 = c->n_rows;
+    if (r1 == r0) return r1;
+    if (!c->q_key) {
+        u64& B = c->bytes;
+        const u64 cap = 2 * c->xrow_cap;  // two entries per stored row
+        c->q_key = dalloc<u32>(cap, &B);
+        c->q_val = dalloc<u32>(cap, &B);
+        c->q_tkey = dalloc<u32>(cap, &B);
+        c->q_tval = dalloc<u32>(cap, &B);
+        c->q_ss.keys_tmp = dalloc<u32>(cap, &B);
+        c->q_ss.vals_tmp = dalloc<u32>(cap, &B);
+        c->q_ss.hist = dalloc<u32>(radix_sort_hist_words(cap), &B);
+        c->q_ss.capacity = cap;
+        c->q_runs_dev = dalloc<u64>(Q_RUNS_MAX + 1, &B);
+    }
+    q_launch_entries(c->T, r0, r1 - r0, c->ximp, (u32)c->accounts_max, c->q_key + 2 * r0, c->q_val + 2 * r0,
+                     c->stream);
+    q_sort(c, 2 * r0, 2 * r1);
+    c->q_runs.push_back(r1);
+    // binary-counter merging: the newest run absorbs its predecessor while it is at
+    // least half as large, so run sizes more than halve from one run to the next
+    while (c->q_runs.size() >= 3) {
+        const size_t k = c->q_runs.size() - 1;
+        const u64 older = c->q_runs[k - 1] - c->q_runs[k - 2], newer = c->q_runs[k] - c->q_runs[k - 1];
+        if (2 * newer < older) break;
+        q_sort(c, 2 * c->q_runs[k - 2], 2 * c->q_runs[k]);
+        c->q_runs.erase(c->q_runs.end() - 2);
+    }
+    if (c->q_runs.size() > Q_RUNS_MAX + 1) tbgpu_fatal("compact", "index runs exceed Q_RUNS_MAX", __FILE__, __LINE__);
+    HIP_CHECK(hipMemcpyAsync(c->q_runs_dev, c->q_runs.data(), c->q_runs.size() * sizeof(u64), hipMemcpyHostToDevice,
+                             c->stream));
+    HIP_CHECK(hipStreamSynchronize(c->stream));
+    return r1;
+}
+
+// `nq` filters in device memory; results at out + q * stride rows.
+static u64 run_queries(tbgpu_ctx* c, const tb_account_filter_t* filters, u32 nq, u32 stride, void* out, bool history,
+                       uint32_t* counts_host) {
+    tbgpu_compact(c);
+    QIndex X{c->q_key, c->q_val, c->q_runs_dev, (u32)(c->q_runs.size() - 1)};
+    u64 total = 0;
+    const u32 step = (u32)c->bmax;  // c->counts holds bmax words
+    for (u32 q0 = 0; q0 < nq; q0 += step) {
+        const u32 k = std::min(step, nq - q0);
+        QArgs A{filters + q0, k, stride, (u8*)out + (u64)q0 * stride * 128, c->counts, history ? 1u : 0u, c->n_hist};
+        q_launch_scan(c->T, X, A, c->stream);
+        HIP_CHECK(hipMemcpyAsync(counts_host + q0, c->counts, k * sizeof(u32), hipMemcpyDeviceToHost, c->stream));
+        HIP_CHECK(hipStreamSynchronize(c->stream));
+        for (u32 j = 0; j < k; j++) total += counts_host[q0 + j];
+    }
+    return total;
+}
+
+static uint32_t query_host(tbgpu_ctx* c, const tb_account_filter_t* filter, void* out, bool history) {
+    HIP_CHECK(hipSetDevice(c->device));
+    tb_account_filter_t* fd = (tb_account_filter_t*)c->res_buf;  // nmax * 8 B >= 64 B
+    HIP_CHECK(hipMemcpyAsync(fd, filter, sizeof *filter, hipMemcpyHostToDevice, c->stream));
+    uint32_t n = 0;
+    run_queries(c, fd, 1, TBGPU_QUERY_MAX, c->ev_buf, history, &n);  // ev_buf: nmax * 128 B >= 8190 rows
+    if (n) HIP_CHECK(hipMemcpy(out, c->ev_buf, (u64)n * 128, hipMemcpyDeviceToHost));
+    return n;
+}
+
+extern "C" uint32_t tbgpu_get_account_transfers(tbgpu_ctx* c, const tb_account_filter_t* filter, tb_transfer_t* out) {
+    return query_host(c, filter, out, false);
+}
+
+extern "C" uint32_t tbgpu_get_account_history(tbgpu_ctx* c, const tb_account_filter_t* filter,
+                                              tb_account_balance_t* out) {
+    return query_host(c, filter, out, true);
+}
+
+extern "C" uint64_t tbgpu_get_account_transfers_device(tbgpu_ctx* c, uint32_t count, const void* filters_device,
+                                                       uint32_t stride, void* out_device, uint32_t* result_counts) {
+    HIP_CHECK(hipSetDevice(c->device));
+    return run_queries(c, (const tb_account_filter_t*)filters_device, count, stride, out_device, false, result_counts);
+}
+
+extern "C" uint64_t tbgpu_get_account_history_device(tbgpu_ctx* c, uint32_t count, const void* filters_device,
+                                                     uint32_t stride, void* out_device, uint32_t* result_counts) {
+    HIP_CHECK(hipSetDevice(c->device));
+    return run_queries(c, (const tb_account_filter_t*)filters_device, count, stride, out_device, true, result_counts);
 }
 
 static u128 to128(tb_uint128_t x) { return ((u128)x.hi << 64) | x.lo; }

@@ -12,7 +12,8 @@ import re
 
 import numpy as np
 
-from .types import (ACCOUNT_DTYPE, HISTORY_DTYPE, RESULT_DTYPE, TRANSFER_DTYPE, U64_MAX, u128_array)
+from .types import (ACCOUNT_DTYPE, BALANCE_DTYPE, FILTER_DTYPE, HISTORY_DTYPE, QUERY_MAX, RESULT_DTYPE,
+                    TRANSFER_DTYPE, U64_MAX, u128_array)
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
@@ -60,6 +61,13 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} is missing: run `python -m tigerbeetle_amd.build` (no CPU fallback)")
+    try:
+        # torch ships its own HIP runtime: load it first so that libtbgpu.so binds to
+        # the same one (one runtime per process; torch cannot see the GPU if ours
+        # initialised first).  torch is plumbing here: device buffers, streams, RCCL.
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     vp, u32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
     L.tbgpu_init.restype = ctypes.c_int
@@ -100,6 +108,14 @@ def lib():
     L.tbgpu_import_transfers.restype = ctypes.c_int
     L.tbgpu_import_transfers.argtypes = [vp, vp, u32]
     L.tbgpu_advance_commit_timestamp.argtypes = [vp, u64]
+    L.tbgpu_compact.restype = u64
+    L.tbgpu_compact.argtypes = [vp]
+    for name in ("tbgpu_get_account_transfers", "tbgpu_get_account_history"):
+        getattr(L, name).restype = u32
+        getattr(L, name).argtypes = [vp, vp, vp]
+    for name in ("tbgpu_get_account_transfers_device", "tbgpu_get_account_history_device"):
+        getattr(L, name).restype = u64
+        getattr(L, name).argtypes = [vp, u32, vp, u32, vp, vp]
     L.tbgpu_last_error.restype = ctypes.c_int
     L.tbgpu_last_error.argtypes = [vp, ctypes.c_char_p, u32]
     _lib = L
@@ -241,6 +257,29 @@ class Engine:
         out = np.zeros(max(len(q), 1), dtype=TRANSFER_DTYPE)
         n = self._L.tbgpu_lookup_transfers(self._h, _ptr(q), len(q), _ptr(out))
         return out[:n].copy()
+
+    def compact(self) -> int:
+        """tbgpu_compact: index the rows stored since the last compaction."""
+        return self._L.tbgpu_compact(self._h)
+
+    def get_account_transfers(self, filt: np.ndarray) -> np.ndarray:
+        f = np.ascontiguousarray(filt, dtype=FILTER_DTYPE).reshape(1)
+        out = np.zeros(QUERY_MAX, dtype=TRANSFER_DTYPE)
+        n = self._L.tbgpu_get_account_transfers(self._h, _ptr(f), _ptr(out))
+        return out[:n].copy()
+
+    def get_account_history(self, filt: np.ndarray) -> np.ndarray:
+        f = np.ascontiguousarray(filt, dtype=FILTER_DTYPE).reshape(1)
+        out = np.zeros(QUERY_MAX, dtype=BALANCE_DTYPE)
+        n = self._L.tbgpu_get_account_history(self._h, _ptr(f), _ptr(out))
+        return out[:n].copy()
+
+    def query_device(self, filters_ptr: int, count: int, stride: int, out_ptr: int, history: bool = False):
+        """Batched queries with filters and results in device memory; returns (total, counts)."""
+        rc = np.zeros(max(count, 1), dtype=np.uint32)
+        fn = self._L.tbgpu_get_account_history_device if history else self._L.tbgpu_get_account_transfers_device
+        total = fn(self._h, count, ctypes.c_void_p(filters_ptr), stride, ctypes.c_void_p(out_ptr), _ptr(rc))
+        return total, rc[:count]
 
     def set_balances(self, id_, dp, dpo, cp, cpo) -> None:
         rc = self._L.tbgpu_test_set_balances(self._h, u128(id_), u128(dp), u128(dpo), u128(cp), u128(cpo))

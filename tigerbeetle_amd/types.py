@@ -42,11 +42,19 @@ HISTORY_DTYPE = np.dtype(
     + _u128("cr_credits_posted") + [("timestamp", "<u8"), ("reserved", "u1", (88,))]
 )
 U128_DTYPE = np.dtype([("lo", "<u8"), ("hi", "<u8")])
+# AccountFilter (src/tigerbeetle.zig:268-302) and AccountBalance (:65-78)
+FILTER_DTYPE = np.dtype(_u128("account_id") + [("timestamp_min", "<u8"), ("timestamp_max", "<u8"),
+                                               ("limit", "<u4"), ("flags", "<u4"), ("reserved", "u1", (24,))])
+BALANCE_DTYPE = np.dtype(_u128("debits_pending") + _u128("debits_posted") + _u128("credits_pending")
+                         + _u128("credits_posted") + [("timestamp", "<u8"), ("reserved", "u1", (56,))])
+QUERY_MAX = 8190  # constants.batch_max.get_account_transfers / _history (src/state_machine.zig:53-76)
 
 assert ACCOUNT_DTYPE.itemsize == 128
 assert TRANSFER_DTYPE.itemsize == 128
 assert RESULT_DTYPE.itemsize == 8
 assert HISTORY_DTYPE.itemsize == 256
+assert FILTER_DTYPE.itemsize == 64
+assert BALANCE_DTYPE.itemsize == 128
 
 ACCOUNT_U128_FIELDS = ("id", "debits_pending", "debits_posted", "credits_pending", "credits_posted",
                        "user_data_128")
@@ -70,6 +78,13 @@ class TransferFlags(enum.IntFlag):
     void_pending_transfer = 1 << 3
     balancing_debit = 1 << 4
     balancing_credit = 1 << 5
+
+
+class AccountFilterFlags(enum.IntFlag):
+    """src/tigerbeetle.zig:289-302"""
+    debits = 1 << 0
+    credits = 1 << 1
+    reversed = 1 << 2
 
 
 class CreateAccountResult(enum.IntEnum):
@@ -213,3 +228,15 @@ def transfer(**kw) -> np.ndarray:
         else:
             t[k] = v
     return t
+
+
+def account_filter(account_id: int, timestamp_min: int = 0, timestamp_max: int = 0, limit: int = QUERY_MAX,
+                   flags: int = 3) -> np.ndarray:
+    """One AccountFilter record (flags: AccountFilterFlags bits; 3 = debits | credits)."""
+    f = np.zeros(1, dtype=FILTER_DTYPE)
+    set_u128(f, "account_id", int(account_id))
+    f["timestamp_min"] = timestamp_min
+    f["timestamp_max"] = timestamp_max
+    f["limit"] = limit
+    f["flags"] = flags
+    return f

@@ -65,6 +65,49 @@ def pmc_traffic(kernel: str, events_per_launch: float):
     return None, None
 
 
+def query_phase(eng, w, acc_n, torch, dev, count=100, batch=1024):
+    """The reference benchmark's second phase (src/tigerbeetle/benchmark_load.zig:401-446):
+    `count` get_account_transfers queries, one at a time, for uniformly random accounts
+    with limit = 8190 and both sides, over everything committed above; latency per
+    query (host filter in, up to 1 MB of rows out).  Also: the compaction that indexes
+    the committed rows (StateMachine.compact's work here, off the commit path) and the
+    throughput of `batch` such queries in one device launch.  Reported beside the
+    metric, never as `value`."""
+    from tigerbeetle_amd.types import FILTER_DTYPE, QUERY_MAX, account_filter
+    rows = eng.transfer_count()
+    t0 = time.perf_counter()
+    eng.compact()
+    compact_s = time.perf_counter() - t0
+    rng = np.random.default_rng(7)
+    ids = w.accounts["id_lo"]
+    lat, got = [], 0
+    for _ in range(count):
+        f = account_filter(int(ids[int(rng.integers(0, acc_n))]), limit=QUERY_MAX)
+        t0 = time.perf_counter()
+        got += len(eng.get_account_transfers(f))
+        lat.append(time.perf_counter() - t0)
+    lat = np.array(lat) * 1e6
+    filters = np.concatenate([account_filter(int(ids[int(rng.integers(0, acc_n))]), limit=QUERY_MAX)
+                              for _ in range(batch)]).astype(FILTER_DTYPE)
+    fd = torch.from_numpy(filters.view(np.uint8).copy()).to(dev)
+    out = torch.empty(batch * QUERY_MAX * 128, dtype=torch.uint8, device=dev)
+    eng.query_device(fd.data_ptr(), batch, QUERY_MAX, out.data_ptr())  # warm
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    total, _ = eng.query_device(fd.data_ptr(), batch, QUERY_MAX, out.data_ptr())
+    batch_s = time.perf_counter() - t0
+    del out
+    return {"workload": f"benchmark_load.zig query phase: {count} get_account_transfers, random account of "
+                        f"{acc_n}, limit {QUERY_MAX}, debits|credits, over {rows} stored transfers",
+            "latency_us": {"p50": round(float(np.percentile(lat, 50)), 1),
+                           "p99": round(float(np.percentile(lat, 99)), 1), "max": round(float(lat.max()), 1)},
+            "rows_returned_per_query": round(got / count, 1),
+            "batched": {"queries": batch, "seconds": round(batch_s, 6), "queries_per_s": round(batch / batch_s, 1),
+                        "rows_per_s": round(total / batch_s, 1)},
+            "compact": {"rows": rows, "seconds": round(compact_s, 4),
+                        "ns_per_row": round(compact_s / max(rows, 1) * 1e9, 3)}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -76,6 +119,7 @@ def main():
     ap.add_argument("--accounts", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-queries", action="store_true", help="skip the query phase (after the timed region)")
     ap.add_argument("--verify", action="store_true", help="check every result is ok (config 1/2 never fail)")
     args = ap.parse_args()
 
@@ -195,6 +239,10 @@ def main():
         "device_ms_per_step": round(dev_ms / K, 4),
     }
 
+    queries = None
+    if rank == 0 and not args.no_queries:
+        queries = query_phase(eng, w, acc_n, torch, dev)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         import oracle  # the CPU baseline leg (test infrastructure, never the product path)
@@ -239,6 +287,7 @@ def main():
             "fixed_point_sorts": max(sorts) if sorts else 0,
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "queries": queries,
         }
         print(json.dumps(line), flush=True)
     eng.close()

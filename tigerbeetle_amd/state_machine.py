@@ -11,7 +11,7 @@ from __future__ import annotations
 import numpy as np
 
 from .engine import Engine
-from .types import ACCOUNT_DTYPE, RESULT_DTYPE, TRANSFER_DTYPE, U128_DTYPE, Operation
+from .types import ACCOUNT_DTYPE, FILTER_DTYPE, RESULT_DTYPE, TRANSFER_DTYPE, U128_DTYPE, Operation
 
 MESSAGE_BODY_SIZE_MAX = (1 << 20) - 256  # constants.message_body_size_max (src/constants.zig:204)
 
@@ -30,6 +30,12 @@ class StateMachine:
     def prepare(self, operation: Operation, input: bytes) -> None:
         if operation in (Operation.create_accounts, Operation.create_transfers):
             self.prepare_timestamp += len(input) // 128
+
+    # src/state_machine.zig:930-955: the LSM compaction beat; here the account-transfers
+    # index folds in the rows committed since the previous beat.
+    def compact(self, callback, op: int) -> None:
+        self.engine.compact()
+        callback(self)
 
     # src/state_machine.zig:514-576 — the HBM tables need no prefetch; the callback
     # still runs (the reference delivers it asynchronously via the grid's next tick).
@@ -54,11 +60,37 @@ class StateMachine:
             ids = np.frombuffer(input, dtype=U128_DTYPE)
             out = self.engine.lookup_transfers([(int(x["hi"]) << 64) | int(x["lo"]) for x in ids])
             out = out[:MESSAGE_BODY_SIZE_MAX // 128]
+        elif operation in (Operation.get_account_transfers, Operation.get_account_history):
+            # parse_filter_from_input (src/state_machine.zig:812-820): a body that is not
+            # exactly one AccountFilter reads as the zeroed (invalid) filter
+            f = np.frombuffer(input, dtype=FILTER_DTYPE) if len(input) == FILTER_DTYPE.itemsize \
+                else np.zeros(1, dtype=FILTER_DTYPE)
+            out = (self.engine.get_account_transfers(f) if operation == Operation.get_account_transfers
+                   else self.engine.get_account_history(f))
         else:
-            raise NotImplementedError(f"{operation.name} is not served by the GPU engine (SURVEY.md §8f)")
+            raise NotImplementedError(f"{operation.name} is not served by the GPU engine")
         self.commit_timestamp = max(self.commit_timestamp, self.engine.commit_timestamp())
         return out.tobytes()
 
     @staticmethod
     def results(reply: bytes) -> np.ndarray:
         return np.frombuffer(reply, dtype=RESULT_DTYPE)
+
+
+class Demuxer:
+    """DemuxerType (src/state_machine.zig:126-165): splits one create_* reply (sparse
+    results of several client requests batched together) back into per-request
+    replies, in place.  decode() ranges must be disjoint and increasing."""
+
+    def __init__(self, reply: np.ndarray):
+        self.results = reply.view(RESULT_DTYPE)
+
+    def decode(self, event_offset: int, event_count: int) -> np.ndarray:
+        n = 0
+        for r in self.results:
+            if r["index"] < event_offset or r["index"] >= event_offset + event_count:
+                break
+            r["index"] -= event_offset
+            n += 1
+        out, self.results = self.results[:n], self.results[n:]
+        return out

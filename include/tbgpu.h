@@ -400,6 +400,25 @@ uint64_t tbgpu_export_history(tbgpu_ctx* ctx, uint64_t first, uint64_t count, tb
 /* Posted groove (src/state_machine.zig:235-248): fulfillment of the pending transfer
  * with this id: -1 none/not found, 0 posted, 1 voided. */
 int tbgpu_get_posted(tbgpu_ctx* ctx, tb_uint128_t pending_id);
+/* ------------------------------------------------------------------------ */
+/* Persistence                                         */
+/* ------------------------------------------------------------------------ */
+/* StateMachine.checkpoint (src/state_machine.zig:957-970) / open (:486-500): the
+ * state the ctx owns -- accounts, stored transfers, the posted groove, account
+ * history, commit_timestamp -- as one self-describing image in a caller buffer
+ * (the replica hands it to its grid / superblock).  Layout: a 64-B header
+ * {magic "TBGPUCK1", version 1, counts, commit_timestamp, checksum of the rest},
+ * then Account[n_accounts], Transfer[n_rows], posted u8[n_rows], imported
+ * u8[n_rows], AccountHistoryGrooveValue[n_history].  The indexes are derived
+ * state, rebuilt on open. */
+uint64_t tbgpu_checkpoint_size(tbgpu_ctx* ctx);
+/* Returns the bytes written, or 0 when `capacity` is too small. */
+uint64_t tbgpu_checkpoint(tbgpu_ctx* ctx, void* out, uint64_t capacity);
+/* Replaces the ctx's state by the image's.  Returns 0, -22 (EINVAL) for a bad
+ * magic/version/size/checksum, -28 (ENOSPC) when the image exceeds the ctx's
+ * capacities. */
+int tbgpu_open(tbgpu_ctx* ctx, const void* image, uint64_t size);
+
 /* StateMachine.commit_timestamp (src/state_machine.zig:375). */
 uint64_t tbgpu_commit_timestamp(tbgpu_ctx* ctx);
 

@@ -255,9 +255,42 @@ __global__ void import_transfers(Tables T, const Transfer* rows, u32 n, u64 row_
     atomicMin((unsigned long long*)&T.idr[3], (unsigned long long)(u64)(t.id >> 64));
 }
 
+// tbgpu_open: the account index from the dense rows (ac_apply's insert).
+__global__ void k_rebuild_aidx(Tables T, u64 n) {
+    const u64 row = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= n) return;
+    const Account& a = T.acc[row];
+    u64 h = hash128(a.id) & T.aidx_mask;
+    while (atomicCAS(&T.aidx[h].row1, 0u, (u32)row + 1) != 0) h = (h + 1) & T.aidx_mask;
+    AccIdx& e = T.aidx[h];
+    e.id_lo = (u64)a.id;
+    e.id_hi = (u64)(a.id >> 64);
+    e.ledger = a.ledger;
+    e.flags = a.flags;
+    e.code = a.code;
+}
+
+// tbgpu_open: the fast path's overflow guard (fast.hip) from the restored balances.
+__global__ void k_scan_big(Tables T, u64 n) {
+    const u64 row = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= n) return;
+    const Account& a = T.acc[row];
+    const u64 lim = 1ull << 62;
+    if ((u64)(a.debits_pending >> 64) >= lim || (u64)(a.debits_posted >> 64) >= lim ||
+        (u64)(a.credits_pending >> 64) >= lim || (u64)(a.credits_posted >> 64) >= lim)
+        atomicOr(T.big, 1u);
+}
+
 }  // namespace
 
 #define GRID(n) (u32)(((n) + 255) / 256), 256, 0, stream
+
+void launch_rebuild_accounts(const Tables& T, u64 n, hipStream_t stream) {
+    if (!n) return;
+    k_rebuild_aidx<<<GRID(n)>>>(T, n);
+    k_scan_big<<<GRID(n)>>>(T, n);
+    HIP_CHECK(hipGetLastError());
+}
 
 void ac_launch_classify(const Tables& T, const AcArgs& C, hipStream_t stream) {
     ac_classify<<<GRID(C.n)>>>(T, C);

@@ -919,6 +919,103 @@ extern "C" uint64_t tbgpu_get_account_history_device(tbgpu_ctx* c, uint32_t coun
     return run_queries(c, (const tb_account_filter_t*)filters_device, count, stride, out_device, true, result_counts);
 }
 
+// ------------------------------------------------------- persistence ------
+
+namespace {
+constexpr u64 CK_MAGIC = 0x314B435550474254ull;  // "TBGPUCK1"
+struct CkHeader {
+    u64 magic;
+    u32 version, reserved;
+    u64 n_accounts, n_rows, n_hist, commit_ts, checksum;
+    u64 pad;
+};
+static_assert(sizeof(CkHeader) == 64, "checkpoint header");
+
+u64 ck_payload_bytes(u64 na, u64 nr, u64 nh) { return na * 128 + nr * 128 + 2 * nr + nh * 256; }
+
+// Checksum of the payload: four interleaved multiply-xor lanes over u64 words
+// (integrity against truncation and corruption, not an adversary).
+u64 ck_checksum(const u8* p, u64 n) {
+    u64 h[4] = {0x9E3779B97F4A7C15ull, 0xC2B2AE3D27D4EB4Full, 0x165667B19E3779F9ull, 0x27D4EB2F165667C5ull};
+    const u64 words = n / 8;
+    const u64* w = (const u64*)p;
+    for (u64 k = 0; k < words; k++) h[k & 3] = (h[k & 3] ^ w[k]) * 0x100000001B3ull;
+    u64 tail = 0;
+    memcpy(&tail, p + words * 8, n - words * 8);
+    return mix64(h[0] ^ mix64(h[1] ^ mix64(h[2] ^ mix64(h[3] ^ tail ^ n))));
+}
+}  // namespace
+
+extern "C" uint64_t tbgpu_checkpoint_size(tbgpu_ctx* c) {
+    return sizeof(CkHeader) + ck_payload_bytes(c->n_accounts, c->n_rows, c->n_hist);
+}
+
+extern "C" uint64_t tbgpu_checkpoint(tbgpu_ctx* c, void* out, uint64_t capacity) {
+    HIP_CHECK(hipSetDevice(c->device));
+    const u64 size = tbgpu_checkpoint_size(c);
+    if (capacity < size) return 0;
+    HIP_CHECK(hipStreamSynchronize(c->stream));
+    u8* p = (u8*)out + sizeof(CkHeader);
+    const u64 na = c->n_accounts, nr = c->n_rows, nh = c->n_hist;
+    if (na) HIP_CHECK(hipMemcpy(p, c->T.acc, na * 128, hipMemcpyDeviceToHost));
+    if (nr) HIP_CHECK(hipMemcpy(p + na * 128, c->T.xrows, nr * 128, hipMemcpyDeviceToHost));
+    if (nr) HIP_CHECK(hipMemcpy(p + na * 128 + nr * 128, c->T.xful, nr, hipMemcpyDeviceToHost));
+    u8* imp = p + na * 128 + nr * 129;
+    if (nr && c->ximp) HIP_CHECK(hipMemcpy(imp, c->ximp, nr, hipMemcpyDeviceToHost));
+    else memset(imp, 0, nr);
+    if (nh) HIP_CHECK(hipMemcpy(imp + nr, c->T.hrows, nh * 256, hipMemcpyDeviceToHost));
+    CkHeader h{};
+    h.magic = CK_MAGIC;
+    h.version = 1;
+    h.n_accounts = na;
+    h.n_rows = nr;
+    h.n_hist = nh;
+    h.commit_ts = tbgpu_commit_timestamp(c);
+    h.checksum = ck_checksum(p, size - sizeof(CkHeader));
+    memcpy(out, &h, sizeof h);
+    return size;
+}
+
+extern "C" int tbgpu_open(tbgpu_ctx* c, const void* image, uint64_t size) {
+    HIP_CHECK(hipSetDevice(c->device));
+    if (size < sizeof(CkHeader)) return -22;
+    CkHeader h;
+    memcpy(&h, image, sizeof h);
+    if (h.magic != CK_MAGIC || h.version != 1) return -22;
+    if (size != sizeof(CkHeader) + ck_payload_bytes(h.n_accounts, h.n_rows, h.n_hist)) return -22;
+    const u8* p = (const u8*)image + sizeof(CkHeader);
+    if (ck_checksum(p, size - sizeof(CkHeader)) != h.checksum) return -22;
+    if (h.n_accounts > c->accounts_max || h.n_rows > c->xrow_cap || h.n_hist > c->hist_cap) return -28;
+    tbgpu_reset(c);
+    const u64 na = h.n_accounts, nr = h.n_rows, nh = h.n_hist;
+    hipStream_t s = c->stream;
+    if (na) HIP_CHECK(hipMemcpy(c->T.acc, p, na * 128, hipMemcpyHostToDevice));
+    if (nr) HIP_CHECK(hipMemcpy(c->T.xrows, p + na * 128, nr * 128, hipMemcpyHostToDevice));
+    if (nr) HIP_CHECK(hipMemcpy(c->T.xful, p + na * 128 + nr * 128, nr, hipMemcpyHostToDevice));
+    const u8* imp = p + na * 128 + nr * 129;
+    bool any_imported = false;
+    for (u64 k = 0; k < nr && !any_imported; k++) any_imported = imp[k] != 0;
+    if (any_imported) {
+        if (!c->ximp) c->ximp = dalloc<u8>(c->xrow_cap, &c->bytes);
+        HIP_CHECK(hipMemset(c->ximp, 0, c->xrow_cap));
+        HIP_CHECK(hipMemcpy(c->ximp, imp, nr, hipMemcpyHostToDevice));
+    }
+    if (nh) HIP_CHECK(hipMemcpy(c->T.hrows, imp + nr, nh * 256, hipMemcpyHostToDevice));
+    // derived state: the account index, the transfer-id index and its key range,
+    // the overflow guard; the account-transfers index rebuilds on the next query
+    launch_rebuild_accounts(c->T, na, s);
+    for (u64 off = 0; off < nr; off += 1u << 30) {
+        const u32 k = (u32)std::min<u64>(nr - off, 1u << 30);
+        launch_import_transfers(c->T, c->T.xrows + off, k, off, s);  // rows in place: index + key range
+    }
+    HIP_CHECK(hipMemcpyAsync(c->T.commit_ts, &h.commit_ts, sizeof(u64), hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    c->n_accounts = na;
+    c->n_rows = nr;
+    c->n_hist = nh;
+    return 0;
+}
+
 static u128 to128(tb_uint128_t x) { return ((u128)x.hi << 64) | x.lo; }
 
 extern "C" int tbgpu_test_set_balances(tbgpu_ctx* c, tb_uint128_t id, tb_uint128_t dp, tb_uint128_t dpo,

@@ -88,3 +88,4 @@ void launch_lookup_transfers(const Tables& T, const u128* ids, u32 n, Transfer* 
 void launch_set_balances(const Tables& T, u128 id, Bal4 b, int* status, hipStream_t stream);
 void launch_import_transfers(const Tables& T, const Transfer* rows, u32 n, u64 row_base, hipStream_t stream);
 void launch_get_posted(const Tables& T, u128 id, int* status, hipStream_t stream);
+void launch_rebuild_accounts(const Tables& T, u64 n, hipStream_t stream);

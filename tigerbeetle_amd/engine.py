@@ -108,6 +108,12 @@ def lib():
     L.tbgpu_import_transfers.restype = ctypes.c_int
     L.tbgpu_import_transfers.argtypes = [vp, vp, u32]
     L.tbgpu_advance_commit_timestamp.argtypes = [vp, u64]
+    L.tbgpu_checkpoint_size.restype = u64
+    L.tbgpu_checkpoint_size.argtypes = [vp]
+    L.tbgpu_checkpoint.restype = u64
+    L.tbgpu_checkpoint.argtypes = [vp, vp, u64]
+    L.tbgpu_open.restype = ctypes.c_int
+    L.tbgpu_open.argtypes = [vp, vp, u64]
     L.tbgpu_compact.restype = u64
     L.tbgpu_compact.argtypes = [vp]
     for name in ("tbgpu_get_account_transfers", "tbgpu_get_account_history"):
@@ -257,6 +263,18 @@ class Engine:
         out = np.zeros(max(len(q), 1), dtype=TRANSFER_DTYPE)
         n = self._L.tbgpu_lookup_transfers(self._h, _ptr(q), len(q), _ptr(out))
         return out[:n].copy()
+
+    def checkpoint(self) -> np.ndarray:
+        """tbgpu_checkpoint: the durable image of the ctx's state (uint8 array)."""
+        out = np.zeros(self._L.tbgpu_checkpoint_size(self._h), dtype=np.uint8)
+        n = self._L.tbgpu_checkpoint(self._h, _ptr(out), len(out))
+        assert n == len(out)
+        return out
+
+    def open(self, image: np.ndarray) -> int:
+        """tbgpu_open: replace the state by a checkpoint image; 0 or a negative errno."""
+        image = np.ascontiguousarray(image, dtype=np.uint8)
+        return self._L.tbgpu_open(self._h, _ptr(image), len(image))
 
     def compact(self) -> int:
         """tbgpu_compact: index the rows stored since the last compaction."""

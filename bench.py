@@ -7,7 +7,8 @@ consecutive 8190-transfer batches, with the events already resident in HBM
 StateMachine.commit per batch (tests/test_gpu_parity.py).
 
 Default workload: BASELINE config 2 (configs[1]) — 1M accounts on one ledger,
-Zipf(0.99) debit/credit accounts, 8190-transfer batches.  With --gpus N > 1
+Zipf(0.99) debit/credit accounts, 1000 batches of 8190 transfers: one step is
+the whole config-2 run (8,190,000 transfers) in one streamed call.  With --gpus N > 1
 (torchrun, one process per GPU) every rank owns its own ledger shard (weak
 scaling, no data-path collective): the ledger partition of SURVEY.md §8e with
 the routing already applied.
@@ -111,11 +112,12 @@ def query_phase(eng, w, acc_n, torch, dev, count=100, batch=1024):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=2, choices=(1, 2, 3))
     ap.add_argument("--force-general", action="store_true", help="disable the fast path (measure the fixed point)")
-    ap.add_argument("--batches-per-step", type=int, default=200)
+    ap.add_argument("--batches-per-step", type=int, default=None,
+                    help="default 1000 (config 1/2: a whole BASELINE config-2 run per call), 60 for config 3")
     ap.add_argument("--accounts", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -137,6 +139,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
+    if args.batches_per_step is None:
+        args.batches_per_step = 60 if args.config == 3 else 1000
     B, K, W = args.batches_per_step, args.steps, args.warmup
     n_batches = (K + W) * B
     n_transfers = n_batches * BATCH_MAX

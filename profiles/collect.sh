@@ -5,7 +5,7 @@
 #   bash profiles/collect.sh OUTDIR [bench args...]
 set -e
 OUT=${1:-gpurun_out/pmc}; shift || true
-ARGS=${@:---steps 3 --warmup 1 --no-cpu}
+ARGS=${@:---steps 2 --warmup 1 --no-cpu --no-queries}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 B="python3 bench.py $ARGS"
@@ -14,4 +14,4 @@ timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d "$OUT/p1" -o p1 --output-forma
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d "$OUT/p2" -o p2 --output-format csv -- $B > "$OUT/p2.log" 2>&1
 timeout -s KILL 150 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$OUT/p3" -o p3 --output-format csv -- $B > "$OUT/p3.log" 2>&1
 timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM -d "$OUT/p4" -o p4 --output-format csv -- $B > "$OUT/p4.log" 2>&1
-python3 profiles/summarize.py "$OUT" ${EVENTS_PER_LAUNCH:-1638000} "$OUT/traffic.json"
+python3 profiles/summarize.py "$OUT" ${EVENTS_PER_LAUNCH:-8190000} "$OUT/traffic.json"

@@ -246,7 +246,7 @@ __device__ __forceinline__ void agg_add(u32* keys, u64* sums, u32* carries, u32 
 }
 
 #ifndef FP_WAVES_PER_EU
-#define FP_WAVES_PER_EU 7
+#define FP_WAVES_PER_EU 5  // 3..5 measured alike, 7..8 slower (profiles/micro/README.md)
 #endif
 // One tile of FP_THREADS events per workgroup.  Rows are stored optimistically at
 // row_base + event (every event accepted, the benchmark's case); failures are
@@ -465,23 +465,21 @@ __global__ void fp_index(Tables T, FastArgs F, bool fixed) {
     if (flags & (FL_SLOW | FL_ERROR)) return;
     if (F.dry) return;
     if (!fixed && F.counters[CNT_BAD] != 0) return;
-    if (blockIdx.x == 0 && threadIdx.x < 64) {
-        // fold the tiles' id ranges into the index's key range (one wave)
-        const u32 lane = threadIdx.x, ntiles = (F.n + FP_THREADS - 1) / FP_THREADS;
+    const u32 ntiles = (F.n + FP_THREADS - 1) / FP_THREADS;
+    if (threadIdx.x < 64 && blockIdx.x * 64 < ntiles) {
+        // fold the tiles' id ranges into the index's key range: one wave per 64
+        // tiles (a single wave over 16k tiles was a serial tail of this launch)
+        const u32 k = blockIdx.x * 64 + threadIdx.x;
         u64 r[4] = {0, 0, ~0ull, ~0ull};
-        for (u32 k = lane; k < ntiles; k += 64) {
-            r[0] = max(r[0], F.tile_idr[4 * k + 0]);
-            r[1] = max(r[1], F.tile_idr[4 * k + 1]);
-            r[2] = min(r[2], F.tile_idr[4 * k + 2]);
-            r[3] = min(r[3], F.tile_idr[4 * k + 3]);
-        }
+        if (k < ntiles)
+            for (int w = 0; w < 4; w++) r[w] = F.tile_idr[4 * k + w];
         for (int off = 32; off > 0; off >>= 1) {
             r[0] = max(r[0], (u64)__shfl_xor((unsigned long long)r[0], off));
             r[1] = max(r[1], (u64)__shfl_xor((unsigned long long)r[1], off));
             r[2] = min(r[2], (u64)__shfl_xor((unsigned long long)r[2], off));
             r[3] = min(r[3], (u64)__shfl_xor((unsigned long long)r[3], off));
         }
-        if (lane == 0) {
+        if (threadIdx.x == 0) {
             atomicMax((unsigned long long*)&T.idr[0], (unsigned long long)r[0]);
             atomicMax((unsigned long long*)&T.idr[1], (unsigned long long)r[1]);
             atomicMin((unsigned long long*)&T.idr[2], (unsigned long long)r[2]);

@@ -113,6 +113,21 @@ def test_fast_path_falls_back_exactly():
     _parity(w)
 
 
+def test_fallback_keeps_commit_timestamp():
+    """The last event of a call repeats an earlier id of the same call: the fast
+    attempt classified it ok against the pre-call state (and saw its timestamp), but
+    sequentially it is `exists`, so commit_timestamp stays at the previous event's
+    (src/state_machine.zig:1366 only advances on ok).  Also with a post as the last
+    event, whose id a plain transfer took earlier in the call."""
+    for seed in (1, 2):
+        w = workload.config1(transfer_count=9_000, account_count=200, seed=seed)
+        t = w.transfers.copy()
+        t[-1]["id_lo"] = t[-3]["id_lo"]  # exists_with_different_* at the very end
+        w.transfers = t
+        _parity(w)
+        _parity(w, split=1)
+
+
 def test_overflow_guard_routes_to_general():
     """Huge balances (high words >= 2^62) are never handled by the fast path."""
     from table import check

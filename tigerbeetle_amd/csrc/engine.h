@@ -117,6 +117,7 @@ enum {
     CNT_KEYS = 2,       // side keys changed since the last sort
     CNT_OK = 3,         // fast path: accepted events
     CNT_BAD = 4,        // fast path: events with a result other than ok
+    CNT_TS_SAVE = 12,   // fast path: commit_timestamp before the call (u64 in words 12-13)
     CNT_COUNT = 16,
 };
 enum {

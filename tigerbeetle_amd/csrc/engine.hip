@@ -417,7 +417,7 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tb_create_
     const u32 flags = c->h_counters[CNT_FLAGS];
     if (flags & FL_ERROR) tbgpu_fatal("create_transfers", "fast path look-back did not complete", __FILE__, __LINE__);
     if (flags & FL_SLOW) {
-        if (!F.dry) fp_launch_undo(c->T, F, s);  // a dry run applied no delta
+        fp_launch_undo(c->T, F, s);  // commit_timestamp back; the deltas (a dry run applied none)
         return false;
     }
     if (c->h_counters[CNT_BAD]) {

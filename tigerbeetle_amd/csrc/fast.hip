@@ -592,17 +592,24 @@ __global__ void fp_fix(FastArgs F, Tables T, const uint4* rk) {
     F.rows[i] = row;
 }
 
-// Per-call reset of the fast path's counters and reply counts.
+// Per-call reset of the fast path's counters and reply counts, and a copy of
+// commit_timestamp for the fallback: fp_commit raises it for every event it
+// classifies ok against the pre-call state, which the sequential result may not
+// (an id repeated later in the call answers `exists`).
 __global__ void fp_prep(FastArgs F) {
     const u32 k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < CNT_COUNT) F.counters[k] = 0;
+    if (k < CNT_TS_SAVE) F.counters[k] = 0;
+    if (k == 0) *(u64*)&F.counters[CNT_TS_SAVE] = *F.commit_ts;
     if (k < F.nb) F.batch_counts[k] = 0;
 }
 
-// Exact inverse of fp_commit's balance deltas, before the general path redoes the call.
+// Exact inverse of fp_commit's effects, before the general path redoes the call:
+// commit_timestamp back to its pre-call value, and the balance deltas (none in a
+// dry run).
 __global__ void fp_undo(Tables T, FastArgs F) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= F.n) return;
+    if (i == 0) *F.commit_ts = *(const u64*)&F.counters[CNT_TS_SAVE];
+    if (F.dry || i >= F.n) return;
     if (F.fres[i] != TB_CREATE_TRANSFER_OK) return;
     const Transfer& t = F.ev[i];
     const u32 ds = acc_probe(T.aidx, T.aidx_mask, t.debit_account_id);

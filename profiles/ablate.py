@@ -8,8 +8,9 @@ import os
 import subprocess
 import sys
 
-MASKS = {"full": 0, "no-balances": 2, "no-rows": 4, "no-balances+rows": 6}
-args = sys.argv[1:] or ["--steps", "5", "--warmup", "1", "--batches-per-step", "100", "--no-cpu"]
+MASKS = {"full": 0, "no-balances": 2, "no-rows": 4, "no-balances+rows": 6, "no-probes": 32,
+         "no-probes+balances+rows": 38, "no-event-load": 16, "no-event+probes+balances+rows": 54}
+args = sys.argv[1:] or ["--steps", "3", "--warmup", "1", "--no-cpu", "--no-queries"]
 for name, m in MASKS.items():
     env = dict(os.environ, TBGPU_ABLATE=str(m))
     r = subprocess.run([sys.executable, "bench.py", *args], env=env, capture_output=True, text=True)

@@ -228,3 +228,46 @@ def test_config4_cross_ledger_pairs_on_fast_path():
     w = workload.config4(transfer_count=60_000, ledgers=20, accounts_per_ledger=200, seed=9, cross_ledger_pairs=0.02)
     st = _parity(w)
     assert st.path == 1, "config 4 (valid linked pairs) should stay on the single-pass path"
+
+
+def test_dense_directory_boundaries():
+    """Account ids 1..accounts_max use the direct-mapped directory, others the hash
+    index: mix both in every batch, with ids on either side of the boundary, ids in
+    range that were never created, u128 ids, and limit/history flags read through
+    the directory."""
+    from tigerbeetle_amd.engine import Engine
+    from tigerbeetle_amd.types import AccountFlags
+    amax = 1000  # engine accounts_max: the directory covers ids 1..1000
+    rng = np.random.default_rng(5)
+    ids = [k for k in range(1, 600) if k % 7] + [998, 999, 1000, 1001, 1002, 5000] + \
+          [(1 << 64) + k for k in range(1, 50)] + [(k << 70) | 3 for k in range(1, 30)]
+    ids = ids[:amax]
+    acc = workload.make_accounts(np.zeros(len(ids), dtype=np.uint64), ledger=1)
+    for j, v in enumerate(ids):
+        acc[j]["id_lo"], acc[j]["id_hi"] = v & ((1 << 64) - 1), v >> 64
+    roll = rng.random(len(ids))
+    acc["flags"] = np.where(roll < 0.1, int(AccountFlags.debits_must_not_exceed_credits),
+                            np.where(roll < 0.15, int(AccountFlags.history), 0)).astype(np.uint16)
+    pool = ids + [7, 14, 700, 1003, (1 << 64) + 77]  # never created: in range and out of it
+    n = 12_000
+    t = np.zeros(n, dtype=workload.TRANSFER_DTYPE)
+    t["id_lo"] = np.arange(1, n + 1)
+    for i in range(n):
+        d, c = pool[int(rng.integers(0, len(pool)))], pool[int(rng.integers(0, len(pool)))]
+        t[i]["debit_account_id_lo"], t[i]["debit_account_id_hi"] = d & ((1 << 64) - 1), d >> 64
+        t[i]["credit_account_id_lo"], t[i]["credit_account_id_hi"] = c & ((1 << 64) - 1), c >> 64
+    t["amount_lo"] = rng.integers(1, 100, n)
+    t["ledger"] = 1
+    t["code"] = 1
+    w = workload.Workload("dense", acc, np.array([len(acc)], dtype=np.uint32), t,
+                          np.array([3000] * 4, dtype=np.uint32))
+    plain = w.transfers.copy()
+    for fg in (False, True):
+        _parity(w, accounts_max=amax, force_general=fg)
+        _parity(w, split=1, accounts_max=amax, force_general=fg)
+    # without flagged accounts every call stays on the fast path
+    w.accounts = acc.copy()
+    w.accounts["flags"] = 0
+    w.transfers = plain
+    st = _parity(w, accounts_max=amax)
+    assert st.path == 1

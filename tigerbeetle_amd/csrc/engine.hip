@@ -253,6 +253,8 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     c->T.commit_ts = dalloc<u64>(2, &B);
     c->T.idr = dalloc<u64>(4, &B);
     c->T.big = dalloc<u32>(4, &B);
+    c->T.dense_n = o.accounts_max < (1ull << 29) - 1 ? o.accounts_max : 0;  // row + 1 in 29 bits
+    c->T.dense = dalloc<u64>(c->T.dense_n, &B);
     alloc_scratch(c, o.events_per_call_max);
     tbgpu_reset(c);
     *out = c;
@@ -268,6 +270,7 @@ extern "C" void tbgpu_reset(tbgpu_ctx* c) {
     HIP_CHECK(hipMemsetAsync(c->T.idr, 0, 2 * sizeof(u64), c->stream));                  // max = 0
     HIP_CHECK(hipMemsetAsync(c->T.idr + 2, 0xFF, 2 * sizeof(u64), c->stream));           // min = ~0
     HIP_CHECK(hipMemsetAsync(c->T.big, 0, sizeof(u32), c->stream));
+    if (c->T.dense_n) HIP_CHECK(hipMemsetAsync(c->T.dense, 0, c->T.dense_n * sizeof(u64), c->stream));
     if (c->ximp) HIP_CHECK(hipMemsetAsync(c->ximp, 0, c->xrow_cap, c->stream));
     HIP_CHECK(hipStreamSynchronize(c->stream));
     c->n_accounts = c->n_rows = c->n_hist = 0;
@@ -279,7 +282,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     // Free every device allocation by walking the struct's pointers.
-    void* ptrs[] = {c->T.acc, c->T.aidx, c->T.xrows, c->T.xful, c->T.xidx, c->T.hrows, c->T.commit_ts, c->T.idr, c->T.big, c->ev_buf,
+    void* ptrs[] = {c->T.dense, c->T.acc, c->T.aidx, c->T.xrows, c->T.xful, c->T.xidx, c->T.hrows, c->T.commit_ts, c->T.idr, c->T.big, c->ev_buf,
                     c->b_start, c->b_ts, c->ts, c->cs, c->ce, c->sres, c->dslot, c->cslot, c->pre_e, c->pre_p,
                     c->pp_dslot, c->pp_cslot, c->gslot, c->pslot, c->prev_id, c->pend_last, c->prev_pend,
                     c->gclaim, c->gcnt_id, c->gcnt_pd, c->gmem, c->gbeg, c->gend, c->skey, c->sval, c->skey_s,

@@ -26,7 +26,7 @@ struct FastArgs {
     u32 dry;            // dry run: replies only, no state change
     u32 ablate;         // timing-only builds (TBGPU_ABLATE): skip parts of the work; results wrong
 };
-enum { ABL_DUP = 1, ABL_BALANCES = 2, ABL_ROWS = 4, ABL_LOOKBACK = 8, ABL_EVENT = 16 };
+enum { ABL_DUP = 1, ABL_BALANCES = 2, ABL_ROWS = 4, ABL_LOOKBACK = 8, ABL_EVENT = 16, ABL_PROBE = 32 };
 
 void fp_launch_prep(const FastArgs& F, hipStream_t stream);
 void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream);

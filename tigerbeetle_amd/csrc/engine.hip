@@ -172,7 +172,7 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->f_gpos = dalloc<u32>(n, &B);
     c->f_keys = dalloc<u128>(n, &B);
     c->f_rows = dalloc<u32>(n, &B);
-    c->f_tile_idr = dalloc<u64>(4 * (fp_tiles(nmax) + 1), &B);
+    c->f_tile_idr = dalloc<u64>(TILE_WORDS * (fp_tiles(nmax) + 1), &B);
     c->rt_ts_buf = dalloc<u64>(n, &B);
     c->rt_ctl_buf = dalloc<u8>(n, &B);
     c->rt_dry_ts = dalloc<u64>(1, &B);

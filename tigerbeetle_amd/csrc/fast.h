@@ -19,13 +19,15 @@ struct FastArgs {
     u64 row_base;
     u128* keys;         // accepted ids, for fp_index
     u32* rows;          // stored row per accepted event (written by fp_fix only)
-    u64* tile_idr;      // per tile: componentwise max lo, max hi, min lo, min hi of accepted ids
+    u64* tile_idr;      // per tile (TILE_WORDS): componentwise max lo, max hi, min lo, min hi of the
+                        // accepted ids; max accepted timestamp; accepted count
     const u8* ctl;      // [n] TBGPU_CTL_* bits (routed calls) or null
     u8* fres2;          // chain members' final results (fp_chains), scratch
     u64* commit_ts;     // commit_timestamp sink (T.commit_ts, or a scratch word when dry)
     u32 dry;            // dry run: replies only, no state change
     u32 ablate;         // timing-only builds (TBGPU_ABLATE): skip parts of the work; results wrong
 };
+constexpr u32 TILE_WORDS = 6;
 enum { ABL_DUP = 1, ABL_BALANCES = 2, ABL_ROWS = 4, ABL_LOOKBACK = 8, ABL_EVENT = 16, ABL_PROBE = 32 };
 
 void fp_launch_prep(const FastArgs& F, hipStream_t stream);

@@ -407,7 +407,7 @@ void fp_commit(Tables T, FastArgs F) {
         if (lane < 4) {
             u64 v = s_idr[0][lane];
             for (int w = 1; w < FP_THREADS / 64; w++) v = lane < 2 ? max(v, s_idr[w][lane]) : min(v, s_idr[w][lane]);
-            F.tile_idr[4 * tile + lane] = v;
+            F.tile_idr[TILE_WORDS * tile + lane] = v;
         }
         if (lane == 0) {
             u32 nok = 0, nbad = 0;
@@ -417,10 +417,10 @@ void fp_commit(Tables T, FastArgs F) {
                 nbad += s_cnt[w][1];
                 maxts = max(maxts, s_maxts[w]);
             }
-            if (nok) {
-                atomicAdd(&F.counters[CNT_OK], nok);
-                atomicMax((unsigned long long*)F.commit_ts, (unsigned long long)maxts);
-            }
+            // accepted count and commit timestamp: folded by fp_index (one atomic per
+            // tile on one address would serialize 16k tiles at the memory side)
+            F.tile_idr[TILE_WORDS * tile + 4] = maxts;
+            F.tile_idr[TILE_WORDS * tile + 5] = nok;
             if (nbad) atomicAdd(&F.counters[CNT_BAD], nbad);
         }
     }
@@ -485,17 +485,36 @@ __global__ void fp_index(Tables T, FastArgs F, bool fixed) {
         const u32 g = F.gpos[i];
         if (g != NONE32) F.gtab[g] = 0;
     }
+    const u32 ntiles = (F.n + FP_THREADS - 1) / FP_THREADS;
+    if (!fixed && threadIdx.x < 64 && blockIdx.x * 64 < ntiles) {
+        // the call's accepted count and commit timestamp from fp_commit's tiles
+        // (also for dry runs and calls with failures; fp_undo restores the timestamp
+        // when the call falls back)
+        const u32 k = blockIdx.x * 64 + threadIdx.x;
+        u64 mts = 0, nok = 0;
+        if (k < ntiles) {
+            mts = F.tile_idr[TILE_WORDS * k + 4];
+            nok = F.tile_idr[TILE_WORDS * k + 5];
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            mts = max(mts, (u64)__shfl_xor((unsigned long long)mts, off));
+            nok += (u64)__shfl_xor((unsigned long long)nok, off);
+        }
+        if (threadIdx.x == 0) {
+            if (nok) atomicAdd(&F.counters[CNT_OK], (u32)nok);
+            if (mts) atomicMax((unsigned long long*)F.commit_ts, (unsigned long long)mts);
+        }
+    }
     if (flags & (FL_SLOW | FL_ERROR)) return;
     if (F.dry) return;
     if (!fixed && F.counters[CNT_BAD] != 0) return;
-    const u32 ntiles = (F.n + FP_THREADS - 1) / FP_THREADS;
     if (threadIdx.x < 64 && blockIdx.x * 64 < ntiles) {
         // fold the tiles' id ranges into the index's key range: one wave per 64
         // tiles (a single wave over 16k tiles was a serial tail of this launch)
         const u32 k = blockIdx.x * 64 + threadIdx.x;
         u64 r[4] = {0, 0, ~0ull, ~0ull};
         if (k < ntiles)
-            for (int w = 0; w < 4; w++) r[w] = F.tile_idr[4 * k + w];
+            for (int w = 0; w < 4; w++) r[w] = F.tile_idr[TILE_WORDS * k + w];
         for (int off = 32; off > 0; off >>= 1) {
             r[0] = max(r[0], (u64)__shfl_xor((unsigned long long)r[0], off));
             r[1] = max(r[1], (u64)__shfl_xor((unsigned long long)r[1], off));

@@ -463,15 +463,23 @@ void fp_commit(Tables T, FastArgs F) {
 }
 
 // Only when the call's ids were not increasing: claim every accepted id once.
-__global__ void fp_dupcheck(Tables T, FastArgs F) {
-    // Every event records its claim (or NONE) so fp_index can clear the table.
-    if (!(F.counters[CNT_FLAGS] & FL_NONMONO)) return;
-    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= F.n) return;
+__device__ __forceinline__ void fp_dupcheck_one(const FastArgs& F, u32 i) {
     F.gpos[i] = NONE32;
     const u8 r = F.fres[i];
     if (r != TB_CREATE_TRANSFER_OK && r != (FRES_CHAIN | TB_CREATE_TRANSFER_OK)) return;
     if (gtab_claim_is_dup(F, F.keys[i], i)) atomicOr(&F.counters[CNT_FLAGS], (u32)FL_SLOW);
+}
+
+// The launches that usually stand down (no repeated-id check, no chains) run a
+// small grid-stride grid: a full grid of 32k workgroups that all return at once
+// still costs its dispatch.
+#define FOR_EACH_EVENT(i) \
+    for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < F.n; i += gridDim.x * blockDim.x)
+
+__global__ void fp_dupcheck(Tables T, FastArgs F) {
+    // Every event records its claim (or NONE) so fp_index can clear the table.
+    if (!(F.counters[CNT_FLAGS] & FL_NONMONO)) return;
+    FOR_EACH_EVENT(i) fp_dupcheck_one(F, i);
 }
 
 // Publish the accepted ids.  fixed = false: the launch right after fp_commit, which
@@ -553,10 +561,7 @@ __device__ __forceinline__ void add_u128_small(const Tables& T, u128* p, u64 a) 
 // and commit_timestamp advanced only by the accepted members before the break
 // (:1366, not undone by scope_close).  Each member walks its own (short) chain;
 // results go to fres2 so that no thread reads a finalized code.
-__global__ void fp_chains(Tables T, FastArgs F) {
-    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    const u32 flags = F.counters[CNT_FLAGS];
-    if (!(flags & FL_FCHAIN) || (flags & (FL_SLOW | FL_ERROR)) || i >= F.n) return;
+__device__ void fp_chains_one(const Tables& T, const FastArgs& F, u32 i) {
     const u8 fr = F.fres[i];
     if (!(fr & FRES_CHAIN) || fr == FRES_SLOW) return;
     const u8 own = fr & 0x7F;
@@ -601,12 +606,19 @@ __global__ void fp_chains(Tables T, FastArgs F) {
     }
 }
 
-__global__ void fp_chains_fin(FastArgs F) {
-    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void fp_chains(Tables T, FastArgs F) {
     const u32 flags = F.counters[CNT_FLAGS];
-    if (!(flags & FL_FCHAIN) || (flags & (FL_SLOW | FL_ERROR)) || i >= F.n) return;
-    const u8 fr = F.fres[i];
-    if ((fr & FRES_CHAIN) && fr != FRES_SLOW) F.fres[i] = F.fres2[i];
+    if (!(flags & FL_FCHAIN) || (flags & (FL_SLOW | FL_ERROR))) return;
+    FOR_EACH_EVENT(i) fp_chains_one(T, F, i);
+}
+
+__global__ void fp_chains_fin(FastArgs F) {
+    const u32 flags = F.counters[CNT_FLAGS];
+    if (!(flags & FL_FCHAIN) || (flags & (FL_SLOW | FL_ERROR))) return;
+    FOR_EACH_EVENT(i) {
+        const u8 fr = F.fres[i];
+        if ((fr & FRES_CHAIN) && fr != FRES_SLOW) F.fres[i] = F.fres2[i];
+    }
 }
 
 // With failures: mask for the rank scan (bit0 accepted, bit1 failed).
@@ -681,9 +693,10 @@ void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream) {
 }
 
 void fp_launch_index(const Tables& T, const FastArgs& F, hipStream_t stream) {
-    fp_dupcheck<<<GRID(F.n)>>>(T, F);
-    fp_chains<<<GRID(F.n)>>>(T, F);   // both stand down without FL_FCHAIN
-    fp_chains_fin<<<GRID(F.n)>>>(F);
+    const u32 sg = std::min<u32>((F.n + 255) / 256, 1024);  // grid-stride: usually stands down
+    fp_dupcheck<<<std::max(sg, 1u), 256, 0, stream>>>(T, F);
+    fp_chains<<<std::max(sg, 1u), 256, 0, stream>>>(T, F);   // both stand down without FL_FCHAIN
+    fp_chains_fin<<<std::max(sg, 1u), 256, 0, stream>>>(F);
     fp_index<<<GRID(F.n)>>>(T, F, false);
     HIP_CHECK(hipGetLastError());
 }

@@ -102,6 +102,7 @@ struct tbgpu_ctx {
     const u64* rt_ev_ts = nullptr;
     const u8* rt_ctl = nullptr;
     bool rt_dry = false;
+    u32 slow_chunks = 0;  // consecutive chunks that needed the fixed point
     // account-transfers index (query.hip), allocated by the first compaction
     u32 *q_key = nullptr, *q_val = nullptr, *q_tkey = nullptr, *q_tval = nullptr;
     SortScratch q_ss{};
@@ -315,10 +316,15 @@ static void read_counters(tbgpu_ctx* c) {
 }
 
 // Splits batches [b0, b_end) into chunks of whole batches of <= nmax events.
-static u32 chunk_end(const tbgpu_ctx* c, const uint32_t* counts, u32 b0, u32 nb) {
+// The fixed point's passes grow with the dependency depth of a call, which grows
+// with its batch count; calls that need it are cut into chunks of at most this
+// many batches (the streaming semantics are those of consecutive calls anyway).
+constexpr u32 GENERAL_CHUNK_BATCHES = 16;
+
+static u32 chunk_end(const tbgpu_ctx* c, const uint32_t* counts, u32 b0, u32 nb, u32 max_batches = ~0u) {
     u64 ev = 0;
     u32 b = b0;
-    while (b < nb && b - b0 < c->bmax - 2) {
+    while (b < nb && b - b0 < c->bmax - 2 && b - b0 < max_batches) {
         if (ev + counts[b] > c->nmax) break;
         ev += counts[b];
         b++;
@@ -438,8 +444,11 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tb_create_
 }
 
 // One chunk of create_transfers: events already at `ev` on the device.
-static void run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
-                                tb_create_transfers_result_t* results_dev, u32* counts_host) {
+// Returns false (nothing committed, every effect undone) when the fast path does
+// not apply and `split` asks the caller to redo these batches in smaller chunks.
+static bool run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
+                                tb_create_transfers_result_t* results_dev, u32* counts_host, bool try_fast_path,
+                                bool split) {
     hipStream_t s = c->stream;
     TrArgs C = make_tr_args(c, ev, n, nb);
     const u64 g = C.gmask + 1;
@@ -452,10 +461,17 @@ static void run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
     c->stats.path = 0;
     if (n == 0) {
         std::fill(counts_host, counts_host + nb, 0u);
-        return;
+        return true;
     }
-    const bool fast_ok = !(c->opt.flags & TBGPU_OPT_FORCE_GENERAL);
-    if (fast_ok && try_fast(c, ev, n, nb, results_dev, counts_host)) return;
+    const bool fast_ok = try_fast_path && !(c->opt.flags & TBGPU_OPT_FORCE_GENERAL);
+    if (fast_ok) {
+        if (try_fast(c, ev, n, nb, results_dev, counts_host)) {
+            c->slow_chunks = 0;
+            return true;
+        }
+        if (split) return false;
+    }
+    c->slow_chunks++;
     prof_mark(c, PH_CLASSIFY);
     HIP_CHECK(hipMemsetAsync(c->counters, 0, CNT_COUNT * sizeof(u32), s));
     HIP_CHECK(hipMemsetAsync(c->gclaim, 0, g * sizeof(u32), s));
@@ -527,9 +543,10 @@ static void run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
     prof_mark(c, PH_END);
     HIP_CHECK(hipMemcpyAsync(counts_host, c->counts, nb * sizeof(u32), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
-    if (c->rt_dry) return;
+    if (c->rt_dry) return true;
     c->n_rows += tot.x;
     c->n_hist += tot.z;
+    return true;
 }
 
 static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t* timestamps, const uint32_t* counts,
@@ -542,8 +559,13 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
     u64 total = 0, ev_off = 0, events = 0;
     u32 iters = 0;
     u64 sorts = 0;
+    u32 small_until = 0;  // batches before this one go in general-path-sized chunks
     for (u32 b0 = 0; b0 < nb_total;) {
-        const u32 b1 = chunk_end(c, counts, b0, nb_total);
+        // After a call needed the fixed point, the next ones probably do too: small
+        // chunks, and the fast attempt only every 8th (it undoes itself when it fails).
+        // A dry run must stay one call (its chunks cannot see each other's effects).
+        const bool small = !c->rt_dry && (b0 < small_until || c->slow_chunks > 0);
+        const u32 b1 = chunk_end(c, counts, b0, nb_total, small ? GENERAL_CHUNK_BATCHES : ~0u);
         const u32 nb = b1 - b0;
         prof_mark(c, PH_UPLOAD);
         upload_batches(c, timestamps + b0, counts + b0, nb, starts);
@@ -573,7 +595,13 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         }
         tb_create_transfers_result_t* rdev =
             dst_device ? results + total : (tb_create_transfers_result_t*)c->res_buf;
-        run_transfers_chunk(c, ev, n, nb, rdev, result_counts + b0);
+        const bool try_fast_path = c->slow_chunks % 8 == 0;
+        if (!run_transfers_chunk(c, ev, n, nb, rdev, result_counts + b0, try_fast_path,
+                                 /*split=*/!c->rt_dry && nb > GENERAL_CHUNK_BATCHES)) {
+            small_until = b1;  // redo these batches in small chunks, on the general path
+            c->slow_chunks = 1;
+            continue;
+        }
         if (!dst_device) copy_results_to_batches(c, nb, starts, result_counts + b0, (u8*)(results + ev_off));
         for (u32 b = 0; b < nb; b++) total += result_counts[b0 + b];
         iters = std::max(iters, c->stats.iterations);

@@ -114,7 +114,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", type=int, default=2, choices=(1, 2, 3))
+    ap.add_argument("--config", type=int, default=2, choices=(1, 2, 3, 4),
+                    help="4: 1000 ledgers x 10k accounts with 1%% cross-ledger linked pairs, on one GPU")
     ap.add_argument("--force-general", action="store_true", help="disable the fast path (measure the fixed point)")
     ap.add_argument("--batches-per-step", type=int, default=None,
                     help="default 1000 (config 1/2: a whole BASELINE config-2 run per call), 60 for config 3")
@@ -148,6 +149,10 @@ def main():
     if args.config == 2:
         acc_n = args.accounts or 1_000_000
         w = workload.config2(transfer_count=n_transfers, account_count=acc_n, seed=42 + rank)
+    elif args.config == 4:
+        acc_n = args.accounts or 10_000_000
+        w = workload.config4(transfer_count=n_transfers, ledgers=1000, accounts_per_ledger=acc_n // 1000,
+                             seed=42 + rank)
     elif args.config == 3:
         acc_n = args.accounts or 10_000
         w = workload.config3(batches=n_batches, account_count=acc_n, seed=42 + rank)
@@ -282,7 +287,9 @@ def main():
             "data": "synthetic",
             "config": {"workload": f"config{args.config}: {acc_n} accounts, "
                                    + {1: "uniform pairs", 2: "Zipf(0.99) pairs on 1 ledger",
-                                      3: "flag-heavy mix (limits, two-phase, balancing, chains)"}[args.config]
+                                      3: "flag-heavy mix (limits, two-phase, balancing, chains)",
+                                      4: "1000 ledgers, uniform pairs within a ledger, 1% cross-ledger "
+                                         "linked pairs (u128 account ids: the hash index)"}[args.config]
                                    + f", {B} x 8190-transfer batches per step (streamed, HBM-resident)",
                        "batches_per_step": B, "transfers_per_step_per_gpu": B * BATCH_MAX,
                        "parallelism": f"ledger-shard x{world}"},

@@ -561,7 +561,9 @@ __device__ __forceinline__ void add_u128_small(const Tables& T, u128* p, u64 a) 
 // and commit_timestamp advanced only by the accepted members before the break
 // (:1366, not undone by scope_close).  Each member walks its own (short) chain;
 // results go to fres2 so that no thread reads a finalized code.
-__device__ void fp_chains_one(const Tables& T, const FastArgs& F, u32 i) {
+// Counts and the timestamp go to the caller's per-thread sums (one atomic per
+// workgroup after the loop: per-member atomics on one address serialize).
+__device__ void fp_chains_one(const Tables& T, const FastArgs& F, u32 i, u32& n_ok, u32& n_bad, u64& mts) {
     const u8 fr = F.fres[i];
     if (!(fr & FRES_CHAIN) || fr == FRES_SLOW) return;
     const u8 own = fr & 0x7F;
@@ -583,10 +585,9 @@ __device__ void fp_chains_one(const Tables& T, const FastArgs& F, u32 i) {
     F.fres2[i] = fin;
     const u64 nbatch = be - bs;
     const u64 ts = F.ev_ts ? F.ev_ts[i] : F.b_ts[b] - nbatch + (i - bs) + 1;
-    if (own == TB_CREATE_TRANSFER_OK && (j == NONE32 || i < j))
-        atomicMax((unsigned long long*)F.commit_ts, (unsigned long long)ts);
+    if (own == TB_CREATE_TRANSFER_OK && (j == NONE32 || i < j)) mts = max(mts, ts);
     if (fin == TB_CREATE_TRANSFER_OK) {
-        atomicAdd(&F.counters[CNT_OK], 1u);
+        n_ok++;
         if (!F.dry) {
             const Transfer& t = F.ev[i];
             const u32 ds = acc_probe(T.aidx, T.aidx_mask, t.debit_account_id);
@@ -601,7 +602,7 @@ __device__ void fp_chains_one(const Tables& T, const FastArgs& F, u32 i) {
             }
         }
     } else {
-        atomicAdd(&F.counters[CNT_BAD], 1u);
+        n_bad++;
         atomicAdd(&F.batch_counts[b], 1u);
     }
 }
@@ -609,7 +610,29 @@ __device__ void fp_chains_one(const Tables& T, const FastArgs& F, u32 i) {
 __global__ void fp_chains(Tables T, FastArgs F) {
     const u32 flags = F.counters[CNT_FLAGS];
     if (!(flags & FL_FCHAIN) || (flags & (FL_SLOW | FL_ERROR))) return;
-    FOR_EACH_EVENT(i) fp_chains_one(T, F, i);
+    u32 n_ok = 0, n_bad = 0;
+    u64 mts = 0;
+    FOR_EACH_EVENT(i) fp_chains_one(T, F, i, n_ok, n_bad, mts);
+    __shared__ u32 s_ok, s_bad;
+    __shared__ u64 s_mts;
+    if (threadIdx.x == 0) { s_ok = 0; s_bad = 0; s_mts = 0; }
+    __syncthreads();
+    for (int off = 32; off > 0; off >>= 1) {
+        n_ok += __shfl_xor(n_ok, off);
+        n_bad += __shfl_xor(n_bad, off);
+        mts = max(mts, (u64)__shfl_xor((unsigned long long)mts, off));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (n_ok) atomicAdd(&s_ok, n_ok);
+        if (n_bad) atomicAdd(&s_bad, n_bad);
+        if (mts) atomicMax((unsigned long long*)&s_mts, (unsigned long long)mts);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (s_ok) atomicAdd(&F.counters[CNT_OK], s_ok);
+        if (s_bad) atomicAdd(&F.counters[CNT_BAD], s_bad);
+        if (s_mts) atomicMax((unsigned long long*)F.commit_ts, (unsigned long long)s_mts);
+    }
 }
 
 __global__ void fp_chains_fin(FastArgs F) {
@@ -693,7 +716,7 @@ void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream) {
 }
 
 void fp_launch_index(const Tables& T, const FastArgs& F, hipStream_t stream) {
-    const u32 sg = std::min<u32>((F.n + 255) / 256, 1024);  // grid-stride: usually stands down
+    const u32 sg = std::min<u32>((F.n + 255) / 256, 2048);  // grid-stride: usually stands down
     fp_dupcheck<<<std::max(sg, 1u), 256, 0, stream>>>(T, F);
     fp_chains<<<std::max(sg, 1u), 256, 0, stream>>>(T, F);   // both stand down without FL_FCHAIN
     fp_chains_fin<<<std::max(sg, 1u), 256, 0, stream>>>(F);

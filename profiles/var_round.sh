@@ -4,6 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 for v in "$@"; do
+  [ "$v" = -- ] && break
   [ "$v" = base ] && continue
   TBGPU_LIB=tigerbeetle_amd/build/var_$v/libtbgpu.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q \
     --timeout 120 --timeout-method thread -k "config1 or config2 or fast or random or config4" > gpurun_out/par_$v.log 2>&1 \

@@ -258,6 +258,25 @@ __device__ __forceinline__ void agg_add(u32* keys, u64* sums, u32* carries, u32 
     if (old + a < old) atomicAdd(&carries[h], 1u);
 }
 
+// Events are loaded with coalesced 16-byte loads and handed to their lanes through
+// LDS (0.95 vs 1.03 ms per 8.19M transfers for one 128-byte load per lane;
+// FP_LANE_EVENTS builds the latter).  Stored rows staged the same way, or stored
+// coalesced for every event right after the load, measured slower than the
+// lane-per-row stores (profiles/micro/README.md).
+#if !defined(FP_LANE_EVENTS)
+#define FP_LDS_EVENTS 1
+#endif
+// Per-wave LDS staging of 128-byte records: 32
+// records of 8 16-byte chunks, chunk c of record e at e*8 + (c ^ (e & 7)) so the
+// lane-per-record writes and reads spread over the banks.
+constexpr int STAGE_RECS = 32;
+__device__ __forceinline__ u32 stage_slot(u32 e, u32 c) { return e * 8 + (c ^ (e & 7)); }
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 #ifndef FP_WAVES_PER_EU
 #define FP_WAVES_PER_EU 5  // 3..5 measured alike, 7..8 slower (profiles/micro/README.md)
 #endif
@@ -272,6 +291,9 @@ void fp_commit(Tables T, FastArgs F) {
     __shared__ u32 s_keys[AGG_SLOTS];
     __shared__ u64 s_sums[AGG_SLOTS];
     __shared__ u32 s_carry[AGG_SLOTS];
+#if defined(FP_LDS_EVENTS)
+    __shared__ uint4 s_stage[FP_THREADS / 64][STAGE_RECS * 8];
+#endif
     const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (u32 h = tid; h < AGG_SLOTS; h += FP_THREADS) {
         s_keys[h] = AGG_EMPTY;
@@ -307,9 +329,41 @@ void fp_commit(Tables T, FastArgs F) {
             t.ledger = 1;
             t.code = 1;
         } else {
+#if !defined(FP_LDS_EVENTS)
             t = F.ev[i];
+#endif
         }
     }
+#if defined(FP_LDS_EVENTS)
+    // the wave's 64 events: coalesced 16-byte loads (lane k of load j holds chunk
+    // (j*64 + k) of the wave's span), then two 32-event halves through LDS
+    if (!(F.ablate & ABL_EVENT)) {
+        const u32 wbase = tile * FP_THREADS + wave * 64;
+        const uint4* src = (const uint4*)F.ev;
+        uint4 ch[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const u32 q = j * 64 + lane;
+            ch[j] = wbase + (q >> 3) < F.n ? src[(u64)wbase * 8 + q] : make_uint4(0, 0, 0, 0);
+        }
+        uint4* st = s_stage[wave];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+#pragma unroll
+            for (int j = 4 * h; j < 4 * h + 4; j++) {
+                const u32 q = j * 64 + lane, e = (q >> 3) - 32 * h;
+                st[stage_slot(e, q & 7)] = ch[j];
+            }
+            wave_lds_sync();
+            if ((lane >> 5) == (u32)h && valid) {
+                uint4* tv = (uint4*)&t;
+#pragma unroll
+                for (int c = 0; c < 8; c++) tv[c] = st[stage_slot(lane & 31, c)];
+            }
+            wave_lds_sync();
+        }
+    }
+#endif
     // Linked-chain membership (execute, src/state_machine.zig:1018-1035): linked
     // here, or the batch's previous event is (the router may close a chain that
     // continues on another shard: TBGPU_CTL_CHAIN_END).
@@ -322,6 +376,7 @@ void fp_commit(Tables T, FastArgs F) {
     const bool member = lk || plk || (myctl & TBGPU_CTL_DOOM);
     if (__ballot(member) && lane == 0) atomicOr(&F.counters[CNT_FLAGS], (u32)FL_FCHAIN);
     bool own_ok = false;
+#define STORE_ROW() do { if (!(F.ablate & ABL_ROWS)) T.xrows[F.row_base + i] = t; } while (0)
     if (valid) {
         id = t.id;
         u32 ds = NONE32, cs = NONE32;
@@ -336,7 +391,7 @@ void fp_commit(Tables T, FastArgs F) {
             if (own_ok) {
                 F.keys[i] = t.id;
                 t.timestamp = ts;
-                if (!(F.ablate & ABL_ROWS)) T.xrows[F.row_base + i] = t;
+                STORE_ROW();
             }
             r = FRES_CHAIN;
         } else {
@@ -353,13 +408,14 @@ void fp_commit(Tables T, FastArgs F) {
             }
             // optimistic stored row (every predecessor accepted); fp_fix re-places it otherwise
             t.timestamp = ts;
-            if (!(F.ablate & ABL_ROWS)) T.xrows[F.row_base + i] = t;
+            STORE_ROW();
         } else if (r == FRES_SLOW) {
             atomicOr(&F.counters[CNT_FLAGS], (u32)FL_SLOW);
         } else if (r != FRES_CHAIN) {
             atomicAdd(&F.batch_counts[b], 1u);
         }
     }
+#undef STORE_ROW
     const bool ok = valid && r == TB_CREATE_TRANSFER_OK;
     const bool bad = valid && r != TB_CREATE_TRANSFER_OK && r != FRES_CHAIN;
 

@@ -295,31 +295,69 @@ void fp_commit(Tables T, FastArgs F) {
     __shared__ uint4 s_stage[FP_THREADS / 64][STAGE_RECS * 8];
 #endif
     const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const u32 tile = blockIdx.x;
+    const u32 i = tile * FP_THREADS + tid;
+    const bool valid = i < F.n;
+    const u32 wbase = tile * FP_THREADS + wave * 64;
+#if defined(FP_LDS_EVENTS)
+    // The wave's 64 events as coalesced 16-byte loads (lane k of load j holds chunk
+    // (j*64 + k) of the wave's span), issued before the table init and the scalar
+    // batch lookup, which do not depend on them.  (Measured alike to issuing them
+    // after the lookup: 0.93-0.94 ms either way per 8.19M transfers.  Loading lane
+    // 0's predecessor event up here in every lane, so that no branch waits on it,
+    // was slower: 0.98 ms.)
+    // Chunks past the last event re-read the last chunk (unconditional loads: no
+    // branch between them); they only reach lanes without an event.
+    // (eight named registers: an array live across the loops below went to scratch)
+    uint4 c0{}, c1{}, c2{}, c3{}, c4{}, c5{}, c6{}, c7{};
+    if (!(F.ablate & ABL_EVENT) && F.n) {
+        const uint4* src = (const uint4*)F.ev;
+        const u64 last = (u64)F.n * 8 - 1, q0 = (u64)wbase * 8 + lane;
+        c0 = src[min(q0, last)];
+        c1 = src[min(q0 + 64, last)];
+        c2 = src[min(q0 + 128, last)];
+        c3 = src[min(q0 + 192, last)];
+        c4 = src[min(q0 + 256, last)];
+        c5 = src[min(q0 + 320, last)];
+        c6 = src[min(q0 + 384, last)];
+        c7 = src[min(q0 + 448, last)];
+    }
+#endif
     for (u32 h = tid; h < AGG_SLOTS; h += FP_THREADS) {
         s_keys[h] = AGG_EMPTY;
         s_sums[h] = 0;
         s_carry[h] = 0;
     }
     __syncthreads();
-    const u32 tile = blockIdx.x;
-    const u32 i = tile * FP_THREADS + tid;
-    const bool valid = i < F.n;
 
     u8 r = FRES_SLOW;
     u32 b = 0;
     u64 ts = 0;
     u128 id = 0;
-    // batch of the event: one uniform binary search per wave, then a short walk
-    // (a wave spans 64 events, so usually zero or one batch boundary)
-    const u32 i0 = __builtin_amdgcn_readfirstlane(tile * FP_THREADS + wave * 64);
-    if (i0 < F.n) b = fp_batch_of(F.b_start, F.nb, i0);
+    // batch of the event: one uniform (scalar) binary search per wave; a wave spans
+    // 64 events, so usually one batch, and the lanes past a boundary walk on
+    const u32 i0 = __builtin_amdgcn_readfirstlane(wbase);
     Transfer t{};
     u32 bs = 0, nbatch = 0;
+    if (i0 < F.n) {
+        const u32 b0 = fp_batch_of(F.b_start, F.nb, i0);
+        const u32 s0 = F.b_start[b0], e0 = F.b_start[b0 + 1];
+        const u64 t0 = F.ev_ts ? 0 : F.b_ts[b0];
+        if (valid) {
+            if (i < e0) {
+                b = b0;
+                bs = s0;
+                nbatch = e0 - s0;
+            } else {
+                b = b0 + 1;
+                while (F.b_start[b + 1] <= i) b++;
+                bs = F.b_start[b];
+                nbatch = F.b_start[b + 1] - bs;
+            }
+            ts = F.ev_ts ? F.ev_ts[i] : (b == b0 ? t0 : F.b_ts[b]) - nbatch + (i - bs) + 1;
+        }
+    }
     if (valid) {
-        while (F.b_start[b + 1] <= i) b++;
-        bs = F.b_start[b];
-        nbatch = F.b_start[b + 1] - bs;
-        ts = F.ev_ts ? F.ev_ts[i] : F.b_ts[b] - nbatch + (i - bs) + 1;
         if (F.ablate & ABL_EVENT) {  // timing only: a made-up plain event instead of the load
             t.id = (u128)i + 1 + F.row_base;
             t.debit_account_id = (i * 7919u) % 1000000u + 1;
@@ -335,25 +373,16 @@ void fp_commit(Tables T, FastArgs F) {
         }
     }
 #if defined(FP_LDS_EVENTS)
-    // the wave's 64 events: coalesced 16-byte loads (lane k of load j holds chunk
-    // (j*64 + k) of the wave's span), then two 32-event halves through LDS
+    // two 32-event halves through LDS, one record per lane
     if (!(F.ablate & ABL_EVENT)) {
-        const u32 wbase = tile * FP_THREADS + wave * 64;
-        const uint4* src = (const uint4*)F.ev;
-        uint4 ch[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const u32 q = j * 64 + lane;
-            ch[j] = wbase + (q >> 3) < F.n ? src[(u64)wbase * 8 + q] : make_uint4(0, 0, 0, 0);
-        }
         uint4* st = s_stage[wave];
 #pragma unroll
         for (int h = 0; h < 2; h++) {
-#pragma unroll
-            for (int j = 4 * h; j < 4 * h + 4; j++) {
-                const u32 q = j * 64 + lane, e = (q >> 3) - 32 * h;
-                st[stage_slot(e, q & 7)] = ch[j];
-            }
+            // chunk j*64 + lane of the wave's span: event (j*64 + lane) / 8 - 32h
+#define STAGE(j, c) st[stage_slot(((j) * 64 + lane) / 8 - 32 * h, lane & 7)] = (c)
+            if (h == 0) { STAGE(0, c0); STAGE(1, c1); STAGE(2, c2); STAGE(3, c3); }
+            else { STAGE(4, c4); STAGE(5, c5); STAGE(6, c6); STAGE(7, c7); }
+#undef STAGE
             wave_lds_sync();
             if ((lane >> 5) == (u32)h && valid) {
                 uint4* tv = (uint4*)&t;

@@ -31,6 +31,7 @@ sys.path.insert(0, ROOT)
 
 ALGO_BYTES_PER_TRANSFER = 680  # 128 ev + 128 row + 2x128 acct + 2x64 bal + 16 probe + 24 insert
 COMMIT_BYTES_PER_TRANSFER = 656  # the same minus the 24-B id insert (fp_index)
+PV_BYTES = 824                 # post/void: + the pending row read and the posted insert (§8d)
 HBM_PEAK_GBPS = 8000.0         # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
@@ -48,22 +49,35 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def pmc_traffic(kernel: str, events_per_launch: float):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
-    (profiles/rNN/traffic.json, written by profiles/collect.sh on the same bench command:
-    2 x FETCH_SIZE + WRITE_SIZE per dispatch, MI355X_MICROARCH.md's gfx950 correction),
-    scaled to this run's events per launch.  None when no summary matches."""
+def pmc_traffic(config: int, accounts: int, kernel=None):
+    """HBM bytes per launch from the newest committed rocprofv3 PMC summary of THIS
+    workload (profiles/rNN/traffic*.json, written by profiles/collect.sh +
+    summarize.py on the same bench command and tagged with its config and account
+    count): 2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md's gfx950 correction)
+    per dispatch of `kernel`, or, with kernel=None, summed over every commit kernel
+    of a profiled step (the general path's roofline unit).  (None, reason) when no
+    summary of this workload exists."""
     import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")), reverse=True):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic*.json")), reverse=True):
         try:
-            d = json.load(open(f))[kernel]
-        except (OSError, KeyError, ValueError):
+            d = json.load(open(f))
+            meta = d["_meta"]
+        except (OSError, KeyError, ValueError, TypeError):
             continue
-        per_ev = d["traffic_bytes"] / d["events_per_launch"]
-        return round(per_ev * events_per_launch), (
-            f"{os.path.relpath(f, ROOT)}: {per_ev:.1f} B/transfer (2xFETCH_SIZE+WRITE_SIZE, "
-            f"rocprofv3 --pmc passes of this bench) x {events_per_launch:.0f} transfers per launch")
-    return None, None
+        if meta.get("config") != config or meta.get("accounts") != accounts:
+            continue
+        rel = os.path.relpath(f, ROOT)
+        ev = meta["events_per_step"]
+        if kernel is None:
+            per = meta["commit_traffic_bytes"] / meta["steps"]
+            what = f"all commit kernels, {meta['steps']} profiled steps"
+        elif kernel in d:
+            per = d[kernel]["traffic_bytes"]
+            what = f"{kernel} per dispatch"
+        else:
+            continue
+        return round(per), f"{rel}: 2xFETCH_SIZE+WRITE_SIZE, {what} ({per / ev:.1f} B/transfer)"
+    return None, f"no rocprofv3 PMC summary of config {config} with {accounts} accounts under profiles/"
 
 
 def query_phase(eng, w, acc_n, torch, dev, count=100, batch=1024):
@@ -109,6 +123,47 @@ def query_phase(eng, w, acc_n, torch, dev, count=100, batch=1024):
                         "ns_per_row": round(compact_s / max(rows, 1) * 1e9, 3)}}
 
 
+def host_path(eng, w, tts, counts, b0, nbs, torch):
+    """The drop-in's own call rate (INTEGRATION.md's Zig shim): events in pinned host
+    memory, replies back in host memory, PCIe inside the timing.
+    - `single`: one tbgpu_create_transfers call per 8190-event batch, as the shim
+      issues it once per committed prepare (src/state_machine.zig:894-928,
+      src/vsr/replica.zig:3755-3762): per-call latency and the rate it implies;
+    - `streamed`: tbgpu_create_transfers_batches over many batches from host memory.
+    Reported beside the metric, never as `value` (which is HBM-resident)."""
+    from tigerbeetle_amd.types import TRANSFER_DTYPE
+    single, streamed = nbs
+    offs = np.concatenate([[0], np.cumsum(counts.astype(np.int64))])
+    o0, o1 = int(offs[b0]), int(offs[b0 + single + streamed])
+    pinned = torch.empty((o1 - o0) * 128, dtype=torch.uint8, pin_memory=True)
+    view = pinned.numpy().view(TRANSFER_DTYPE)
+    view[:] = w.transfers[o0:o1]
+    lat = []
+    ev_single = 0
+    for k in range(single):
+        b = b0 + k
+        ev = view[int(offs[b]) - o0:int(offs[b + 1]) - o0]
+        t0 = time.perf_counter()
+        eng.create_transfers(int(tts[b]), ev)
+        lat.append(time.perf_counter() - t0)
+        ev_single += len(ev)
+    lat = np.array(lat) * 1e6
+    s0 = b0 + single
+    ev = view[int(offs[s0]) - o0:]
+    t0 = time.perf_counter()
+    eng.create_transfers_batches(tts[s0:s0 + streamed], counts[s0:s0 + streamed], ev)
+    el = time.perf_counter() - t0
+    return {"single": {"calls": single, "events_per_call": int(ev_single // max(single, 1)),
+                       "latency_us": {"p50": round(float(np.percentile(lat, 50)), 1),
+                                      "p99": round(float(np.percentile(lat, 99)), 1),
+                                      "max": round(float(lat.max()), 1)},
+                       "transfers_per_s": round(ev_single / (lat.sum() * 1e-6), 1),
+                       "entry": "tbgpu_create_transfers (one batch per call, pinned host buffers)"},
+            "streamed": {"batches": streamed, "transfers": len(ev), "seconds": round(el, 6),
+                         "transfers_per_s": round(len(ev) / el, 1),
+                         "entry": "tbgpu_create_transfers_batches (host buffers, H2D inside the call)"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -123,6 +178,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-queries", action="store_true", help="skip the query phase (after the timed region)")
+    ap.add_argument("--no-host", action="store_true", help="skip the host-buffer (drop-in call) measurement")
+    ap.add_argument("--host-batches", type=int, default=None,
+                    help="batches for the host-buffer measurement (default 64 single calls + 256 streamed)")
     ap.add_argument("--verify", action="store_true", help="check every result is ok (config 1/2 never fail)")
     args = ap.parse_args()
 
@@ -143,7 +201,9 @@ def main():
     if args.batches_per_step is None:
         args.batches_per_step = 60 if args.config == 3 else 1000
     B, K, W = args.batches_per_step, args.steps, args.warmup
-    n_batches = (K + W) * B
+    host_nb = (0, 0) if (args.no_host or world > 1) else \
+        ((args.host_batches or 64, (args.host_batches or 64) * 4) if args.config != 3 else (16, 48))
+    n_batches = (K + W) * B + sum(host_nb)
     n_transfers = n_batches * BATCH_MAX
     t_gen = time.time()
     if args.config == 2:
@@ -193,6 +253,7 @@ def main():
     dev_ms = 0.0
     iters = []
     sorts = []
+    paths = []
     non_ok = 0
     t0 = time.perf_counter()
     for k in range(W, W + K):
@@ -202,6 +263,7 @@ def main():
         dev_ms += st.device_ms
         iters.append(st.iterations)
         sorts.append(st.sorts)
+        paths.append(st.path)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -219,17 +281,38 @@ def main():
     value = total / elapsed
     ms_per_step = elapsed / K * 1e3
 
-    # Roofline of the dominant kernel, fp_commit (the single-pass create_transfers,
-    # fast.hip): its algorithmic bytes per transfer are SURVEY.md §8d's 680 B minus the
-    # 24-B id-index insert done by fp_index.  Its duration is the "classify" phase:
-    # HIP events recorded on the engine's stream around each launch in the timed region.
+    # Roofline.  Fast path (configs 1, 2, 4): the dominant kernel is fp_commit (the
+    # single-pass create_transfers, fast.hip); its algorithmic bytes per transfer are
+    # SURVEY.md §8d's 680 B minus the 24-B id-index insert done by fp_index; its
+    # duration is the "classify" phase: HIP events recorded on the engine's stream
+    # around each launch in the timed region.  General path (config 3): no single
+    # kernel dominates (sort, scan, evaluate, classify, apply are each 10-30 %), so
+    # the roofline is that of the whole path per call: §8d's algorithmic bytes of the
+    # call's events (680 B per transfer, 824 B per post/void, +8 B per non-ok reply)
+    # over the call's device time (HIP events around the call on the engine stream).
     names = list(PHASES)
     dom = int(np.argmax(phase[:len(names)]))
     phase_ms_per_step = {names[i]: round(phase[i] / K, 4) for i in range(len(names))}
-    commit_ms = phase[names.index("classify")] / K
-    achieved = per_rank / K * COMMIT_BYTES_PER_TRANSFER / (commit_ms * 1e-3) / 1e9 if commit_ms > 0 else 0.0
-    traffic, traffic_src = pmc_traffic("fp_commit", per_rank / K)
     e2e_gbps = value / world * ALGO_BYTES_PER_TRANSFER / 1e9
+    timed = w.transfers[int(counts[:W * B].sum()):int(counts[:(W + K) * B].sum())]
+    n_pv = int(((timed["flags"] & 12) != 0).sum())
+    fast = max(paths) == 1 and min(paths) == 1
+    if fast:
+        commit_ms = phase[names.index("classify")] / K
+        achieved = per_rank / K * COMMIT_BYTES_PER_TRANSFER / (commit_ms * 1e-3) / 1e9 if commit_ms > 0 else 0.0
+        traffic, traffic_src = pmc_traffic(args.config, acc_n, kernel="fp_commit")
+        kernel = "fp_commit"
+        basis = (f"{COMMIT_BYTES_PER_TRANSFER} B/transfer x {B * BATCH_MAX} transfers per launch "
+                 f"/ fp_commit launch time ({commit_ms:.4f} ms, HIP events on the engine stream)")
+    else:
+        call_ms = dev_ms / K
+        algo = (per_rank - n_pv) * ALGO_BYTES_PER_TRANSFER + n_pv * PV_BYTES + 8 * non_ok // world
+        achieved = algo / K / (call_ms * 1e-3) / 1e9 if call_ms > 0 else 0.0
+        traffic, traffic_src = pmc_traffic(args.config, acc_n, kernel=None)
+        kernel = "general path (every kernel of the call)"
+        basis = (f"{ALGO_BYTES_PER_TRANSFER} B x {per_rank - n_pv} transfers + {PV_BYTES} B x {n_pv} posts/voids "
+                 f"+ 8 B x {non_ok // world} non-ok replies over {K} calls / call device time "
+                 f"({call_ms:.4f} ms, HIP events on the engine stream)")
     roofline = {
         "bound": "hbm",
         "achieved": round(achieved, 2),
@@ -238,9 +321,8 @@ def main():
         "frac": round(achieved / HBM_PEAK_GBPS, 5),
         "traffic": traffic,
         "traffic_source": traffic_src,
-        "kernel": "fp_commit",
-        "basis": f"{COMMIT_BYTES_PER_TRANSFER} B/transfer x {B * BATCH_MAX} transfers per launch "
-                 f"/ fp_commit launch time ({commit_ms:.4f} ms, HIP events on the engine stream)",
+        "kernel": kernel,
+        "basis": basis,
         "end_to_end": {"achieved": round(e2e_gbps, 2), "frac": round(e2e_gbps / HBM_PEAK_GBPS, 5),
                        "basis": f"{ALGO_BYTES_PER_TRANSFER} B/transfer x per-GPU committed transfers/s"},
         "dominant_phase": names[dom],
@@ -252,9 +334,18 @@ def main():
     if rank == 0 and not args.no_queries:
         queries = query_phase(eng, w, acc_n, torch, dev)
 
+    host = None
+    if rank == 0 and world == 1 and not args.no_host:
+        host = host_path(eng, w, tts, counts, (W + K) * B, host_nb, torch)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         import oracle  # the CPU baseline leg (test infrastructure, never the product path)
+        # TigerBeetle commits on one core (docs/deploy/hardware.md:98): pin the oracle
+        # to one host core (the third core the process may use)
+        allowed = sorted(os.sched_getaffinity(0))
+        core = allowed[min(2, len(allowed) - 1)]
+        os.sched_setaffinity(0, {core})
         orc = oracle.Oracle(acc_n, 4 << 20)
         orc.create_accounts_batches(ats, w.account_counts, w.accounts)
         done, spent, b = 0, 0.0, 0
@@ -266,10 +357,11 @@ def main():
             done += n
             spent += el
             b += k
+        os.sched_setaffinity(0, set(allowed))
         cpu = {"value": round(done / spent, 1), "unit": "transfers/s", "cores": 1, "kind": "port",
-               "sample": f"oracle/oracle.c commit loop (single thread), first {b} batches ({done} transfers) "
-                         f"of the same config-{args.config} stream after creating the {acc_n} accounts; "
-                         f"{spent:.1f}s of CPU work on {cpu_model()}"}
+               "sample": f"oracle/oracle.c commit loop (single thread pinned to host core {core}), first {b} "
+                         f"batches ({done} transfers) of the same config-{args.config} stream after creating "
+                         f"the {acc_n} accounts; {spent:.1f}s of CPU work on {cpu_model()}"}
 
     if rank == 0:
         line = {
@@ -294,10 +386,12 @@ def main():
                        "batches_per_step": B, "transfers_per_step_per_gpu": B * BATCH_MAX,
                        "parallelism": f"ledger-shard x{world}"},
             "non_ok_results": non_ok,
+            "non_ok_rate": round(non_ok / total, 5) if total else 0.0,
             "fixed_point_passes": max(iters) if iters else 0,
             "fixed_point_sorts": max(sorts) if sorts else 0,
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "host_path": host,
             "queries": queries,
         }
         print(json.dumps(line), flush=True)

@@ -28,15 +28,15 @@ extern "C" {
 
 /* u128 as two little-endian u64 words (the reference targets little-endian only,
  * src/tigerbeetle.zig:306-309). */
-typedef struct tb_uint128_t { uint64_t lo, hi; } tb_uint128_t;
+typedef struct tbgpu_uint128_t { uint64_t lo, hi; } tbgpu_uint128_t;
 
-typedef struct tb_account_t {
-    tb_uint128_t id;
-    tb_uint128_t debits_pending;
-    tb_uint128_t debits_posted;
-    tb_uint128_t credits_pending;
-    tb_uint128_t credits_posted;
-    tb_uint128_t user_data_128;
+typedef struct tbgpu_account_t {
+    tbgpu_uint128_t id;
+    tbgpu_uint128_t debits_pending;
+    tbgpu_uint128_t debits_posted;
+    tbgpu_uint128_t credits_pending;
+    tbgpu_uint128_t credits_posted;
+    tbgpu_uint128_t user_data_128;
     uint64_t user_data_64;
     uint32_t user_data_32;
     uint32_t reserved;
@@ -44,15 +44,15 @@ typedef struct tb_account_t {
     uint16_t code;
     uint16_t flags;
     uint64_t timestamp;
-} tb_account_t;
+} tbgpu_account_t;
 
-typedef struct tb_transfer_t {
-    tb_uint128_t id;
-    tb_uint128_t debit_account_id;
-    tb_uint128_t credit_account_id;
-    tb_uint128_t amount;
-    tb_uint128_t pending_id;
-    tb_uint128_t user_data_128;
+typedef struct tbgpu_transfer_t {
+    tbgpu_uint128_t id;
+    tbgpu_uint128_t debit_account_id;
+    tbgpu_uint128_t credit_account_id;
+    tbgpu_uint128_t amount;
+    tbgpu_uint128_t pending_id;
+    tbgpu_uint128_t user_data_128;
     uint64_t user_data_64;
     uint32_t user_data_32;
     uint32_t timeout;
@@ -60,156 +60,156 @@ typedef struct tb_transfer_t {
     uint16_t code;
     uint16_t flags;
     uint64_t timestamp;
-} tb_transfer_t;
+} tbgpu_transfer_t;
 
 /* {index, result}: sparse, only non-ok events, ascending index. */
-typedef struct tb_create_accounts_result_t { uint32_t index; uint32_t result; } tb_create_accounts_result_t;
-typedef struct tb_create_transfers_result_t { uint32_t index; uint32_t result; } tb_create_transfers_result_t;
+typedef struct tbgpu_create_accounts_result_t { uint32_t index; uint32_t result; } tbgpu_create_accounts_result_t;
+typedef struct tbgpu_create_transfers_result_t { uint32_t index; uint32_t result; } tbgpu_create_transfers_result_t;
 
 /* AccountHistoryGrooveValue, src/state_machine.zig:275-294 (256 B). */
-typedef struct tb_account_history_t {
-    tb_uint128_t dr_account_id;
-    tb_uint128_t dr_debits_pending;
-    tb_uint128_t dr_debits_posted;
-    tb_uint128_t dr_credits_pending;
-    tb_uint128_t dr_credits_posted;
-    tb_uint128_t cr_account_id;
-    tb_uint128_t cr_debits_pending;
-    tb_uint128_t cr_debits_posted;
-    tb_uint128_t cr_credits_pending;
-    tb_uint128_t cr_credits_posted;
+typedef struct tbgpu_account_history_t {
+    tbgpu_uint128_t dr_account_id;
+    tbgpu_uint128_t dr_debits_pending;
+    tbgpu_uint128_t dr_debits_posted;
+    tbgpu_uint128_t dr_credits_pending;
+    tbgpu_uint128_t dr_credits_posted;
+    tbgpu_uint128_t cr_account_id;
+    tbgpu_uint128_t cr_debits_pending;
+    tbgpu_uint128_t cr_debits_posted;
+    tbgpu_uint128_t cr_credits_pending;
+    tbgpu_uint128_t cr_credits_posted;
     uint64_t timestamp;
     uint8_t reserved[88];
-} tb_account_history_t;
+} tbgpu_account_history_t;
 
 /* AccountFilter, src/tigerbeetle.zig:268-302 (64 B): the input of
  * get_account_transfers / get_account_history. */
-typedef struct tb_account_filter_t {
-    tb_uint128_t account_id;
+typedef struct tbgpu_account_filter_t {
+    tbgpu_uint128_t account_id;
     uint64_t timestamp_min;  /* inclusive; 0 = no lower bound */
     uint64_t timestamp_max;  /* inclusive; 0 = no upper bound */
     uint32_t limit;
-    uint32_t flags;          /* TB_ACCOUNT_FILTER_* */
+    uint32_t flags;          /* TBGPU_ACCOUNT_FILTER_* */
     uint8_t reserved[24];
-} tb_account_filter_t;
+} tbgpu_account_filter_t;
 /* AccountFilterFlags, src/tigerbeetle.zig:289-302 */
 enum {
-    TB_ACCOUNT_FILTER_DEBITS = 1 << 0,
-    TB_ACCOUNT_FILTER_CREDITS = 1 << 1,
-    TB_ACCOUNT_FILTER_REVERSED = 1 << 2,
+    TBGPU_ACCOUNT_FILTER_DEBITS = 1 << 0,
+    TBGPU_ACCOUNT_FILTER_CREDITS = 1 << 1,
+    TBGPU_ACCOUNT_FILTER_REVERSED = 1 << 2,
 };
 
 /* AccountBalance, src/tigerbeetle.zig:65-78 (128 B): one get_account_history row. */
-typedef struct tb_account_balance_t {
-    tb_uint128_t debits_pending;
-    tb_uint128_t debits_posted;
-    tb_uint128_t credits_pending;
-    tb_uint128_t credits_posted;
+typedef struct tbgpu_account_balance_t {
+    tbgpu_uint128_t debits_pending;
+    tbgpu_uint128_t debits_posted;
+    tbgpu_uint128_t credits_pending;
+    tbgpu_uint128_t credits_posted;
     uint64_t timestamp;
     uint8_t reserved[56];
-} tb_account_balance_t;
+} tbgpu_account_balance_t;
 
 /* AccountFlags, src/tigerbeetle.zig:42-63 */
 enum {
-    TB_ACCOUNT_LINKED = 1 << 0,
-    TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS = 1 << 1,
-    TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS = 1 << 2,
-    TB_ACCOUNT_HISTORY = 1 << 3,
+    TBGPU_ACCOUNT_LINKED = 1 << 0,
+    TBGPU_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS = 1 << 1,
+    TBGPU_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS = 1 << 2,
+    TBGPU_ACCOUNT_HISTORY = 1 << 3,
 };
 /* TransferFlags, src/tigerbeetle.zig:107-120 */
 enum {
-    TB_TRANSFER_LINKED = 1 << 0,
-    TB_TRANSFER_PENDING = 1 << 1,
-    TB_TRANSFER_POST_PENDING_TRANSFER = 1 << 2,
-    TB_TRANSFER_VOID_PENDING_TRANSFER = 1 << 3,
-    TB_TRANSFER_BALANCING_DEBIT = 1 << 4,
-    TB_TRANSFER_BALANCING_CREDIT = 1 << 5,
+    TBGPU_TRANSFER_LINKED = 1 << 0,
+    TBGPU_TRANSFER_PENDING = 1 << 1,
+    TBGPU_TRANSFER_POST_PENDING_TRANSFER = 1 << 2,
+    TBGPU_TRANSFER_VOID_PENDING_TRANSFER = 1 << 3,
+    TBGPU_TRANSFER_BALANCING_DEBIT = 1 << 4,
+    TBGPU_TRANSFER_BALANCING_CREDIT = 1 << 5,
 };
 
 /* CreateAccountResult, src/tigerbeetle.zig:125-160 */
 enum {
-    TB_CREATE_ACCOUNT_OK = 0,
-    TB_CREATE_ACCOUNT_LINKED_EVENT_FAILED = 1,
-    TB_CREATE_ACCOUNT_LINKED_EVENT_CHAIN_OPEN = 2,
-    TB_CREATE_ACCOUNT_TIMESTAMP_MUST_BE_ZERO = 3,
-    TB_CREATE_ACCOUNT_RESERVED_FIELD = 4,
-    TB_CREATE_ACCOUNT_RESERVED_FLAG = 5,
-    TB_CREATE_ACCOUNT_ID_MUST_NOT_BE_ZERO = 6,
-    TB_CREATE_ACCOUNT_ID_MUST_NOT_BE_INT_MAX = 7,
-    TB_CREATE_ACCOUNT_FLAGS_ARE_MUTUALLY_EXCLUSIVE = 8,
-    TB_CREATE_ACCOUNT_DEBITS_PENDING_MUST_BE_ZERO = 9,
-    TB_CREATE_ACCOUNT_DEBITS_POSTED_MUST_BE_ZERO = 10,
-    TB_CREATE_ACCOUNT_CREDITS_PENDING_MUST_BE_ZERO = 11,
-    TB_CREATE_ACCOUNT_CREDITS_POSTED_MUST_BE_ZERO = 12,
-    TB_CREATE_ACCOUNT_LEDGER_MUST_NOT_BE_ZERO = 13,
-    TB_CREATE_ACCOUNT_CODE_MUST_NOT_BE_ZERO = 14,
-    TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_FLAGS = 15,
-    TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_USER_DATA_128 = 16,
-    TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_USER_DATA_64 = 17,
-    TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_USER_DATA_32 = 18,
-    TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_LEDGER = 19,
-    TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_CODE = 20,
-    TB_CREATE_ACCOUNT_EXISTS = 21,
+    TBGPU_CREATE_ACCOUNT_OK = 0,
+    TBGPU_CREATE_ACCOUNT_LINKED_EVENT_FAILED = 1,
+    TBGPU_CREATE_ACCOUNT_LINKED_EVENT_CHAIN_OPEN = 2,
+    TBGPU_CREATE_ACCOUNT_TIMESTAMP_MUST_BE_ZERO = 3,
+    TBGPU_CREATE_ACCOUNT_RESERVED_FIELD = 4,
+    TBGPU_CREATE_ACCOUNT_RESERVED_FLAG = 5,
+    TBGPU_CREATE_ACCOUNT_ID_MUST_NOT_BE_ZERO = 6,
+    TBGPU_CREATE_ACCOUNT_ID_MUST_NOT_BE_INT_MAX = 7,
+    TBGPU_CREATE_ACCOUNT_FLAGS_ARE_MUTUALLY_EXCLUSIVE = 8,
+    TBGPU_CREATE_ACCOUNT_DEBITS_PENDING_MUST_BE_ZERO = 9,
+    TBGPU_CREATE_ACCOUNT_DEBITS_POSTED_MUST_BE_ZERO = 10,
+    TBGPU_CREATE_ACCOUNT_CREDITS_PENDING_MUST_BE_ZERO = 11,
+    TBGPU_CREATE_ACCOUNT_CREDITS_POSTED_MUST_BE_ZERO = 12,
+    TBGPU_CREATE_ACCOUNT_LEDGER_MUST_NOT_BE_ZERO = 13,
+    TBGPU_CREATE_ACCOUNT_CODE_MUST_NOT_BE_ZERO = 14,
+    TBGPU_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_FLAGS = 15,
+    TBGPU_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_USER_DATA_128 = 16,
+    TBGPU_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_USER_DATA_64 = 17,
+    TBGPU_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_USER_DATA_32 = 18,
+    TBGPU_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_LEDGER = 19,
+    TBGPU_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_CODE = 20,
+    TBGPU_CREATE_ACCOUNT_EXISTS = 21,
 };
 
 /* CreateTransferResult, src/tigerbeetle.zig:165-245 */
 enum {
-    TB_CREATE_TRANSFER_OK = 0,
-    TB_CREATE_TRANSFER_LINKED_EVENT_FAILED = 1,
-    TB_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN = 2,
-    TB_CREATE_TRANSFER_TIMESTAMP_MUST_BE_ZERO = 3,
-    TB_CREATE_TRANSFER_RESERVED_FLAG = 4,
-    TB_CREATE_TRANSFER_ID_MUST_NOT_BE_ZERO = 5,
-    TB_CREATE_TRANSFER_ID_MUST_NOT_BE_INT_MAX = 6,
-    TB_CREATE_TRANSFER_FLAGS_ARE_MUTUALLY_EXCLUSIVE = 7,
-    TB_CREATE_TRANSFER_DEBIT_ACCOUNT_ID_MUST_NOT_BE_ZERO = 8,
-    TB_CREATE_TRANSFER_DEBIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX = 9,
-    TB_CREATE_TRANSFER_CREDIT_ACCOUNT_ID_MUST_NOT_BE_ZERO = 10,
-    TB_CREATE_TRANSFER_CREDIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX = 11,
-    TB_CREATE_TRANSFER_ACCOUNTS_MUST_BE_DIFFERENT = 12,
-    TB_CREATE_TRANSFER_PENDING_ID_MUST_BE_ZERO = 13,
-    TB_CREATE_TRANSFER_PENDING_ID_MUST_NOT_BE_ZERO = 14,
-    TB_CREATE_TRANSFER_PENDING_ID_MUST_NOT_BE_INT_MAX = 15,
-    TB_CREATE_TRANSFER_PENDING_ID_MUST_BE_DIFFERENT = 16,
-    TB_CREATE_TRANSFER_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER = 17,
-    TB_CREATE_TRANSFER_AMOUNT_MUST_NOT_BE_ZERO = 18,
-    TB_CREATE_TRANSFER_LEDGER_MUST_NOT_BE_ZERO = 19,
-    TB_CREATE_TRANSFER_CODE_MUST_NOT_BE_ZERO = 20,
-    TB_CREATE_TRANSFER_DEBIT_ACCOUNT_NOT_FOUND = 21,
-    TB_CREATE_TRANSFER_CREDIT_ACCOUNT_NOT_FOUND = 22,
-    TB_CREATE_TRANSFER_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER = 23,
-    TB_CREATE_TRANSFER_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS = 24,
-    TB_CREATE_TRANSFER_PENDING_TRANSFER_NOT_FOUND = 25,
-    TB_CREATE_TRANSFER_PENDING_TRANSFER_NOT_PENDING = 26,
-    TB_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_DEBIT_ACCOUNT_ID = 27,
-    TB_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_CREDIT_ACCOUNT_ID = 28,
-    TB_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_LEDGER = 29,
-    TB_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_CODE = 30,
-    TB_CREATE_TRANSFER_EXCEEDS_PENDING_TRANSFER_AMOUNT = 31,
-    TB_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_AMOUNT = 32,
-    TB_CREATE_TRANSFER_PENDING_TRANSFER_ALREADY_POSTED = 33,
-    TB_CREATE_TRANSFER_PENDING_TRANSFER_ALREADY_VOIDED = 34,
-    TB_CREATE_TRANSFER_PENDING_TRANSFER_EXPIRED = 35,
-    TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_FLAGS = 36,
-    TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_DEBIT_ACCOUNT_ID = 37,
-    TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_CREDIT_ACCOUNT_ID = 38,
-    TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_AMOUNT = 39,
-    TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_PENDING_ID = 40,
-    TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_128 = 41,
-    TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_64 = 42,
-    TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_32 = 43,
-    TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_TIMEOUT = 44,
-    TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_CODE = 45,
-    TB_CREATE_TRANSFER_EXISTS = 46,
-    TB_CREATE_TRANSFER_OVERFLOWS_DEBITS_PENDING = 47,
-    TB_CREATE_TRANSFER_OVERFLOWS_CREDITS_PENDING = 48,
-    TB_CREATE_TRANSFER_OVERFLOWS_DEBITS_POSTED = 49,
-    TB_CREATE_TRANSFER_OVERFLOWS_CREDITS_POSTED = 50,
-    TB_CREATE_TRANSFER_OVERFLOWS_DEBITS = 51,
-    TB_CREATE_TRANSFER_OVERFLOWS_CREDITS = 52,
-    TB_CREATE_TRANSFER_OVERFLOWS_TIMEOUT = 53,
-    TB_CREATE_TRANSFER_EXCEEDS_CREDITS = 54,
-    TB_CREATE_TRANSFER_EXCEEDS_DEBITS = 55,
+    TBGPU_CREATE_TRANSFER_OK = 0,
+    TBGPU_CREATE_TRANSFER_LINKED_EVENT_FAILED = 1,
+    TBGPU_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN = 2,
+    TBGPU_CREATE_TRANSFER_TIMESTAMP_MUST_BE_ZERO = 3,
+    TBGPU_CREATE_TRANSFER_RESERVED_FLAG = 4,
+    TBGPU_CREATE_TRANSFER_ID_MUST_NOT_BE_ZERO = 5,
+    TBGPU_CREATE_TRANSFER_ID_MUST_NOT_BE_INT_MAX = 6,
+    TBGPU_CREATE_TRANSFER_FLAGS_ARE_MUTUALLY_EXCLUSIVE = 7,
+    TBGPU_CREATE_TRANSFER_DEBIT_ACCOUNT_ID_MUST_NOT_BE_ZERO = 8,
+    TBGPU_CREATE_TRANSFER_DEBIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX = 9,
+    TBGPU_CREATE_TRANSFER_CREDIT_ACCOUNT_ID_MUST_NOT_BE_ZERO = 10,
+    TBGPU_CREATE_TRANSFER_CREDIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX = 11,
+    TBGPU_CREATE_TRANSFER_ACCOUNTS_MUST_BE_DIFFERENT = 12,
+    TBGPU_CREATE_TRANSFER_PENDING_ID_MUST_BE_ZERO = 13,
+    TBGPU_CREATE_TRANSFER_PENDING_ID_MUST_NOT_BE_ZERO = 14,
+    TBGPU_CREATE_TRANSFER_PENDING_ID_MUST_NOT_BE_INT_MAX = 15,
+    TBGPU_CREATE_TRANSFER_PENDING_ID_MUST_BE_DIFFERENT = 16,
+    TBGPU_CREATE_TRANSFER_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER = 17,
+    TBGPU_CREATE_TRANSFER_AMOUNT_MUST_NOT_BE_ZERO = 18,
+    TBGPU_CREATE_TRANSFER_LEDGER_MUST_NOT_BE_ZERO = 19,
+    TBGPU_CREATE_TRANSFER_CODE_MUST_NOT_BE_ZERO = 20,
+    TBGPU_CREATE_TRANSFER_DEBIT_ACCOUNT_NOT_FOUND = 21,
+    TBGPU_CREATE_TRANSFER_CREDIT_ACCOUNT_NOT_FOUND = 22,
+    TBGPU_CREATE_TRANSFER_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER = 23,
+    TBGPU_CREATE_TRANSFER_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS = 24,
+    TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_NOT_FOUND = 25,
+    TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_NOT_PENDING = 26,
+    TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_DEBIT_ACCOUNT_ID = 27,
+    TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_CREDIT_ACCOUNT_ID = 28,
+    TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_LEDGER = 29,
+    TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_CODE = 30,
+    TBGPU_CREATE_TRANSFER_EXCEEDS_PENDING_TRANSFER_AMOUNT = 31,
+    TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_AMOUNT = 32,
+    TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_ALREADY_POSTED = 33,
+    TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_ALREADY_VOIDED = 34,
+    TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_EXPIRED = 35,
+    TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_FLAGS = 36,
+    TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_DEBIT_ACCOUNT_ID = 37,
+    TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_CREDIT_ACCOUNT_ID = 38,
+    TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_AMOUNT = 39,
+    TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_PENDING_ID = 40,
+    TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_128 = 41,
+    TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_64 = 42,
+    TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_32 = 43,
+    TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_TIMEOUT = 44,
+    TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_CODE = 45,
+    TBGPU_CREATE_TRANSFER_EXISTS = 46,
+    TBGPU_CREATE_TRANSFER_OVERFLOWS_DEBITS_PENDING = 47,
+    TBGPU_CREATE_TRANSFER_OVERFLOWS_CREDITS_PENDING = 48,
+    TBGPU_CREATE_TRANSFER_OVERFLOWS_DEBITS_POSTED = 49,
+    TBGPU_CREATE_TRANSFER_OVERFLOWS_CREDITS_POSTED = 50,
+    TBGPU_CREATE_TRANSFER_OVERFLOWS_DEBITS = 51,
+    TBGPU_CREATE_TRANSFER_OVERFLOWS_CREDITS = 52,
+    TBGPU_CREATE_TRANSFER_OVERFLOWS_TIMEOUT = 53,
+    TBGPU_CREATE_TRANSFER_EXCEEDS_CREDITS = 54,
+    TBGPU_CREATE_TRANSFER_EXCEEDS_DEBITS = 55,
 };
 
 /* constants.batch_max.create_transfers with production constants:
@@ -251,13 +251,13 @@ void tbgpu_reset(tbgpu_ctx* ctx);
  * timestamp - n + index + 1). Returns the number of sparse results written
  * (reply bytes = 8 * count). Host buffers, 16-byte aligned, caller-owned. */
 uint32_t tbgpu_create_accounts(tbgpu_ctx* ctx, uint64_t timestamp,
-                               const tb_account_t* events, uint32_t count,
-                               tb_create_accounts_result_t* results);
+                               const tbgpu_account_t* events, uint32_t count,
+                               tbgpu_create_accounts_result_t* results);
 
 /* execute(.create_transfers) — src/state_machine.zig:1002-1088, :1239-1573. */
 uint32_t tbgpu_create_transfers(tbgpu_ctx* ctx, uint64_t timestamp,
-                                const tb_transfer_t* events, uint32_t count,
-                                tb_create_transfers_result_t* results);
+                                const tbgpu_transfer_t* events, uint32_t count,
+                                tbgpu_create_transfers_result_t* results);
 
 /* Streaming form: `batch_count` consecutive commits of create_transfers, with
  * identical results to calling tbgpu_create_transfers once per batch in order.
@@ -267,8 +267,8 @@ uint32_t tbgpu_create_transfers(tbgpu_ctx* ctx, uint64_t timestamp,
  * Returns the total number of results. */
 uint64_t tbgpu_create_transfers_batches(tbgpu_ctx* ctx, uint32_t batch_count,
                                         const uint64_t* timestamps, const uint32_t* counts,
-                                        const tb_transfer_t* events,
-                                        tb_create_transfers_result_t* results,
+                                        const tbgpu_transfer_t* events,
+                                        tbgpu_create_transfers_result_t* results,
                                         uint32_t* result_counts);
 
 /* Same with the events already resident in device memory (HBM) and the replies
@@ -284,8 +284,8 @@ uint64_t tbgpu_create_transfers_batches_device(tbgpu_ctx* ctx, uint32_t batch_co
 
 uint64_t tbgpu_create_accounts_batches(tbgpu_ctx* ctx, uint32_t batch_count,
                                        const uint64_t* timestamps, const uint32_t* counts,
-                                       const tb_account_t* events,
-                                       tb_create_accounts_result_t* results,
+                                       const tbgpu_account_t* events,
+                                       tbgpu_create_accounts_result_t* results,
                                        uint32_t* result_counts);
 
 /* ------------------------------------------------------------------------ */
@@ -317,9 +317,9 @@ enum {
  * timestamp after the call (or, dry, what it would be).  Replies as in
  * tbgpu_create_transfers_batches (host buffers). */
 uint64_t tbgpu_create_transfers_routed(tbgpu_ctx* ctx, uint32_t batch_count, const uint32_t* counts,
-                                       const tb_transfer_t* events, const uint64_t* event_timestamps,
+                                       const tbgpu_transfer_t* events, const uint64_t* event_timestamps,
                                        const uint8_t* ctl, int dry_run,
-                                       tb_create_transfers_result_t* results, uint32_t* result_counts,
+                                       tbgpu_create_transfers_result_t* results, uint32_t* result_counts,
                                        uint64_t* commit_timestamp);
 
 /* Same with events, event timestamps, chain control (may be NULL) and the
@@ -333,7 +333,7 @@ uint64_t tbgpu_create_transfers_routed_device(tbgpu_ctx* ctx, uint32_t batch_cou
 /* Copy committed transfers of another shard into this ctx's transfer table and id
  * index, without balance or posted effects: the `exists` comparisons of
  * :1370-1389 / :1500-1561 then see a colliding id committed elsewhere.  Returns 0. */
-int tbgpu_import_transfers(tbgpu_ctx* ctx, const tb_transfer_t* rows, uint32_t count);
+int tbgpu_import_transfers(tbgpu_ctx* ctx, const tbgpu_transfer_t* rows, uint32_t count);
 
 /* commit_timestamp = max(commit_timestamp, timestamp): the node-wide commit
  * timestamp is the max over shards (:1366 advances it per created transfer). */
@@ -341,8 +341,8 @@ void tbgpu_advance_commit_timestamp(tbgpu_ctx* ctx, uint64_t timestamp);
 
 /* execute_lookup_accounts / execute_lookup_transfers (src/state_machine.zig:1091-1126):
  * found objects are written densely in request order; returns the count. */
-uint32_t tbgpu_lookup_accounts(tbgpu_ctx* ctx, const tb_uint128_t* ids, uint32_t count, tb_account_t* out);
-uint32_t tbgpu_lookup_transfers(tbgpu_ctx* ctx, const tb_uint128_t* ids, uint32_t count, tb_transfer_t* out);
+uint32_t tbgpu_lookup_accounts(tbgpu_ctx* ctx, const tbgpu_uint128_t* ids, uint32_t count, tbgpu_account_t* out);
+uint32_t tbgpu_lookup_transfers(tbgpu_ctx* ctx, const tbgpu_uint128_t* ids, uint32_t count, tbgpu_transfer_t* out);
 
 /* ------------------------------------------------------------------------ */
 /* Account queries                                     */
@@ -364,14 +364,14 @@ uint64_t tbgpu_compact(tbgpu_ctx* ctx);
  * timestamp_max (0 = unbounded), in timestamp order (descending with
  * flags.reversed), at most min(limit, TBGPU_QUERY_MAX).  An invalid filter
  * (:822-833) yields nothing.  Returns the count written to `out`. */
-uint32_t tbgpu_get_account_transfers(tbgpu_ctx* ctx, const tb_account_filter_t* filter, tb_transfer_t* out);
+uint32_t tbgpu_get_account_transfers(tbgpu_ctx* ctx, const tbgpu_account_filter_t* filter, tbgpu_transfer_t* out);
 
 /* execute_get_account_history (:736-808, :1149-1196): the same scan, each
  * transfer's account-history row (the filter account's balances after it), for
  * an account with flags.history.  A post/void transfer stores no history row
  * (:1342-1364 is create_transfer only); the reference's lookup then asserts
  * (src/lsm/scan_lookup.zig:179, :215) -- here the transfer is skipped. */
-uint32_t tbgpu_get_account_history(tbgpu_ctx* ctx, const tb_account_filter_t* filter, tb_account_balance_t* out);
+uint32_t tbgpu_get_account_history(tbgpu_ctx* ctx, const tbgpu_account_filter_t* filter, tbgpu_account_balance_t* out);
 
 /* Many queries in one launch, everything in device memory: filter q's results
  * are written at out_device + q * stride (128-B rows), at most
@@ -384,22 +384,22 @@ uint64_t tbgpu_get_account_history_device(tbgpu_ctx* ctx, uint32_t count, const 
 
 /* Test harness `setup` action (src/state_machine.zig:1892-1908): overwrite an
  * existing account's four balances.  Returns 0, or -1 if the account is missing. */
-int tbgpu_test_set_balances(tbgpu_ctx* ctx, tb_uint128_t id,
-                            tb_uint128_t debits_pending, tb_uint128_t debits_posted,
-                            tb_uint128_t credits_pending, tb_uint128_t credits_posted);
+int tbgpu_test_set_balances(tbgpu_ctx* ctx, tbgpu_uint128_t id,
+                            tbgpu_uint128_t debits_pending, tbgpu_uint128_t debits_posted,
+                            tbgpu_uint128_t credits_pending, tbgpu_uint128_t credits_posted);
 
 /* State export for parity checks (not on the reference's hot path). */
 uint64_t tbgpu_account_count(tbgpu_ctx* ctx);
 uint64_t tbgpu_transfer_count(tbgpu_ctx* ctx);
 uint64_t tbgpu_history_count(tbgpu_ctx* ctx);
 /* Stored transfers in commit order (rows [first, first+count)). */
-uint64_t tbgpu_export_transfers(tbgpu_ctx* ctx, uint64_t first, uint64_t count, tb_transfer_t* out);
+uint64_t tbgpu_export_transfers(tbgpu_ctx* ctx, uint64_t first, uint64_t count, tbgpu_transfer_t* out);
 /* All accounts, in unspecified order. `capacity` bounds `out`. */
-uint64_t tbgpu_export_accounts(tbgpu_ctx* ctx, tb_account_t* out, uint64_t capacity);
-uint64_t tbgpu_export_history(tbgpu_ctx* ctx, uint64_t first, uint64_t count, tb_account_history_t* out);
+uint64_t tbgpu_export_accounts(tbgpu_ctx* ctx, tbgpu_account_t* out, uint64_t capacity);
+uint64_t tbgpu_export_history(tbgpu_ctx* ctx, uint64_t first, uint64_t count, tbgpu_account_history_t* out);
 /* Posted groove (src/state_machine.zig:235-248): fulfillment of the pending transfer
  * with this id: -1 none/not found, 0 posted, 1 voided. */
-int tbgpu_get_posted(tbgpu_ctx* ctx, tb_uint128_t pending_id);
+int tbgpu_get_posted(tbgpu_ctx* ctx, tbgpu_uint128_t pending_id);
 /* ------------------------------------------------------------------------ */
 /* Persistence                                         */
 /* ------------------------------------------------------------------------ */

@@ -48,5 +48,18 @@ if ev:
         fm, wm = sum(f) / len(f) * 1024, sum(w) / len(w) * 1024
         res[k] = {"fetch_bytes_raw": fm, "write_bytes": wm, "traffic_bytes": 2 * fm + wm,
                   "events_per_launch": ev}
+    # Whole-step traffic of the commit path (the general path's roofline unit): every
+    # commit kernel's dispatches summed, over the profiled calls (warmup + steps), the
+    # account setup (ac_*, k_*) and queries (q_*) excluded.
+    tot = 0.0
+    for k in sorted({k for k, _ in agg}):
+        if k.startswith(("__amd", "ac_", "k_", "q_")):
+            continue
+        f, w = agg.get((k, "FETCH_SIZE")), agg.get((k, "WRITE_SIZE"))
+        if f and w:
+            tot += 2 * sum(f) * 1024 + sum(w) * 1024 * len(f) / len(w)
+    res["_meta"] = {"config": int(os.environ.get("TB_CONFIG", "2")), "accounts": int(os.environ.get("TB_ACCOUNTS", "1000000")),
+                    "steps": int(os.environ.get("TB_CALLS", "3")), "events_per_step": ev,
+                    "commit_traffic_bytes": tot}
     if len(sys.argv) > 3:
         json.dump(res, open(sys.argv[3], "w"), indent=1)

@@ -25,7 +25,7 @@ def test_header_declares_the_reference_entry_points():
 def _offsets_from_header(struct):
     text = open(engine.HEADER).read()
     body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (struct, struct), text, re.S).group(1)
-    size = {"tb_uint128_t": 16, "uint64_t": 8, "uint32_t": 4, "uint16_t": 2}
+    size = {"tbgpu_uint128_t": 16, "uint64_t": 8, "uint32_t": 4, "uint16_t": 2}
     off, out = 0, {}
     for line in body.split(";"):
         m = re.match(r"\s*(\w+)\s+(\w+)", line)
@@ -40,13 +40,49 @@ def _offsets_from_header(struct):
 
 
 def test_struct_layouts_match_numpy_views():
-    for struct, dt in (("tb_account_t", ACCOUNT_DTYPE), ("tb_transfer_t", TRANSFER_DTYPE)):
+    for struct, dt in (("tbgpu_account_t", ACCOUNT_DTYPE), ("tbgpu_transfer_t", TRANSFER_DTYPE)):
         offs, size = _offsets_from_header(struct)
         assert size == dt.itemsize == 128
         for name, off in offs.items():
             key = name + "_lo" if name + "_lo" in dt.fields else name
             assert dt.fields[key][1] == off, (struct, name)
     assert HISTORY_DTYPE.itemsize == 256
+
+
+REF_CLIENT_HEADER = "/root/reference/src/clients/c/tb_client.h"
+
+
+def test_header_coexists_with_reference_client_header(tmp_path):
+    """include/tbgpu.h and the reference's tb_client.h compile in one C translation unit
+    (distinct type and enumerator names), with identical struct sizes and every result
+    code and flag of tbgpu.h equal to its tb_client.h counterpart.  Runs only where the
+    reference checkout is present (this container); nothing of it is copied."""
+    import os
+    import shutil
+    import subprocess
+
+    import pytest
+    if not os.path.exists(REF_CLIENT_HEADER) or not shutil.which("gcc"):
+        pytest.skip("reference client header or gcc not available")
+    ours = open(engine.HEADER).read()
+    names = sorted(set(re.findall(r"\bTBGPU_((?:CREATE_ACCOUNT|CREATE_TRANSFER|ACCOUNT|TRANSFER)_[A-Z0-9_]+)\s*=",
+                                  ours)))
+    assert len(names) > 90
+    src = [f'#include "{REF_CLIENT_HEADER}"', f'#include "{engine.HEADER}"']
+    for a, b in (("tb_account_t", "tbgpu_account_t"), ("tb_transfer_t", "tbgpu_transfer_t"),
+                 ("tb_create_transfers_result_t", "tbgpu_create_transfers_result_t"),
+                 ("tb_create_accounts_result_t", "tbgpu_create_accounts_result_t"),
+                 ("tb_account_filter_t", "tbgpu_account_filter_t"),
+                 ("tb_account_balance_t", "tbgpu_account_balance_t")):
+        src.append(f'_Static_assert(sizeof({a}) == sizeof({b}), "{a}");')
+    for n in names:
+        src.append(f'_Static_assert((int)TB_{n} == (int)TBGPU_{n}, "{n}");')
+    src.append("int main(void) { return 0; }")
+    c = tmp_path / "both.c"
+    c.write_text("\n".join(src) + "\n")
+    r = subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-c", str(c), "-o", str(tmp_path / "both.o")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
 
 
 def test_init_without_gpu_fails_loudly():

@@ -64,6 +64,15 @@ def test_config3_full_batches(force_general):
     _parity(workload.config3(batches=4, account_count=10_000, seed=3), force_general=force_general)
 
 
+def test_config3_stress_flag_mix(force_general):
+    _parity(workload.config3_stress(batches=6, batch=2000, account_count=2000), force_general=force_general)
+
+
+def test_config3_stress_batch_by_batch(force_general):
+    _parity(workload.config3_stress(batches=4, batch=1000, account_count=500, seed=7), split=1,
+            force_general=force_general)
+
+
 def test_posted_groove():
     w = workload.config3(batches=3, batch=1500, account_count=800, seed=11)
     orc = oracle.Oracle()
@@ -147,6 +156,39 @@ commit lookup_accounts
     gpu = _engine()
     try:
         check(gpu, text)
+    finally:
+        gpu.close()
+
+
+@pytest.mark.parametrize("order", ["increasing", "random"])
+def test_guarded_fast_path_many_calls(order):
+    """Once any balance's high word reaches 2^62 every event takes the guarded
+    classification.  Many consecutive calls must stay on the fast path (no claim of
+    the in-call duplicate table may leak from one call into the next) and match the
+    oracle, with ids in order and in random order."""
+    w = workload.config1(transfer_count=12 * 4000, account_count=300, seed=31, batch=4000)
+    extra = workload.make_accounts(np.array([10_000], dtype=np.uint64), ledger=2)  # never transferred
+    w.accounts = np.concatenate([w.accounts, extra])
+    w.account_counts = np.array([len(w.accounts)], dtype=np.uint32)
+    if order == "random":
+        t = w.transfers.copy()
+        t["id_lo"] = np.random.default_rng(2).permutation(t["id_lo"])
+        w.transfers = t
+    orc, gpu = oracle.Oracle(), _engine(events_per_call_max=1 << 14)
+    try:
+        ats, tts = w.timestamps()
+        for be in (orc, gpu):
+            be.create_accounts_batches(ats, w.account_counts, w.accounts)
+            be.set_balances(10_000, 0, 1 << 127, 0, 0)
+        off = 0
+        for b, c in enumerate(w.transfer_counts):
+            ev = w.transfers[off:off + int(c)]
+            g = gpu.create_transfers(int(tts[b]), ev)
+            o = orc.create_transfers(int(tts[b]), ev)
+            assert g.tobytes() == o.tobytes(), f"call {b}"
+            assert gpu.stats().path == 1, f"call {b} left the fast path"
+            off += int(c)
+        assert_state_equal(gpu, orc)
     finally:
         gpu.close()
 

@@ -53,19 +53,19 @@ __global__ void ac_classify(Tables T, AcArgs C) {
     u8 sres;
     u32 pre = NONE32, gslot = NONE32;
     // execute (:1018-1035) then create_account's static checks (:1201-1216)
-    if ((a.flags & AF_LINKED) && k == nbatch - 1) sres = TB_CREATE_ACCOUNT_LINKED_EVENT_CHAIN_OPEN;
-    else if (a.timestamp != 0) sres = TB_CREATE_ACCOUNT_TIMESTAMP_MUST_BE_ZERO;
-    else if (a.reserved != 0) sres = TB_CREATE_ACCOUNT_RESERVED_FIELD;
-    else if (a.flags & 0xFFF0u) sres = TB_CREATE_ACCOUNT_RESERVED_FLAG;
-    else if (a.id == 0) sres = TB_CREATE_ACCOUNT_ID_MUST_NOT_BE_ZERO;
-    else if (a.id == U128_MAX) sres = TB_CREATE_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
-    else if ((a.flags & AF_DNEC) && (a.flags & AF_CNED)) sres = TB_CREATE_ACCOUNT_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
-    else if (a.debits_pending != 0) sres = TB_CREATE_ACCOUNT_DEBITS_PENDING_MUST_BE_ZERO;
-    else if (a.debits_posted != 0) sres = TB_CREATE_ACCOUNT_DEBITS_POSTED_MUST_BE_ZERO;
-    else if (a.credits_pending != 0) sres = TB_CREATE_ACCOUNT_CREDITS_PENDING_MUST_BE_ZERO;
-    else if (a.credits_posted != 0) sres = TB_CREATE_ACCOUNT_CREDITS_POSTED_MUST_BE_ZERO;
-    else if (a.ledger == 0) sres = TB_CREATE_ACCOUNT_LEDGER_MUST_NOT_BE_ZERO;
-    else if (a.code == 0) sres = TB_CREATE_ACCOUNT_CODE_MUST_NOT_BE_ZERO;
+    if ((a.flags & AF_LINKED) && k == nbatch - 1) sres = TBGPU_CREATE_ACCOUNT_LINKED_EVENT_CHAIN_OPEN;
+    else if (a.timestamp != 0) sres = TBGPU_CREATE_ACCOUNT_TIMESTAMP_MUST_BE_ZERO;
+    else if (a.reserved != 0) sres = TBGPU_CREATE_ACCOUNT_RESERVED_FIELD;
+    else if (a.flags & 0xFFF0u) sres = TBGPU_CREATE_ACCOUNT_RESERVED_FLAG;
+    else if (a.id == 0) sres = TBGPU_CREATE_ACCOUNT_ID_MUST_NOT_BE_ZERO;
+    else if (a.id == U128_MAX) sres = TBGPU_CREATE_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
+    else if ((a.flags & AF_DNEC) && (a.flags & AF_CNED)) sres = TBGPU_CREATE_ACCOUNT_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+    else if (a.debits_pending != 0) sres = TBGPU_CREATE_ACCOUNT_DEBITS_PENDING_MUST_BE_ZERO;
+    else if (a.debits_posted != 0) sres = TBGPU_CREATE_ACCOUNT_DEBITS_POSTED_MUST_BE_ZERO;
+    else if (a.credits_pending != 0) sres = TBGPU_CREATE_ACCOUNT_CREDITS_PENDING_MUST_BE_ZERO;
+    else if (a.credits_posted != 0) sres = TBGPU_CREATE_ACCOUNT_CREDITS_POSTED_MUST_BE_ZERO;
+    else if (a.ledger == 0) sres = TBGPU_CREATE_ACCOUNT_LEDGER_MUST_NOT_BE_ZERO;
+    else if (a.code == 0) sres = TBGPU_CREATE_ACCOUNT_CODE_MUST_NOT_BE_ZERO;
     else {
         sres = SRES_DYN;
         pre = acc_probe(T.aidx, T.aidx_mask, a.id);
@@ -107,7 +107,7 @@ __global__ void ac_init(AcArgs C, u8* res, u8* ok, u32* cfail) {
     if (i >= C.n) return;
     const u8 sr = C.sres[i];
     u8 r = sr;
-    if (sr == SRES_DYN) r = C.pre[i] != NONE32 ? TB_CREATE_ACCOUNT_EXISTS : TB_CREATE_ACCOUNT_OK;
+    if (sr == SRES_DYN) r = C.pre[i] != NONE32 ? TBGPU_CREATE_ACCOUNT_EXISTS : TBGPU_CREATE_ACCOUNT_OK;
     res[i] = r;
     ok[i] = r == 0 ? 1 : 0;
     if (r != 0 && C.cs[i] != C.ce[i]) atomicMin(&cfail[C.cs[i]], i);
@@ -124,13 +124,13 @@ __global__ void ac_finalize(AcArgs C, u8* ok, const u32* cfail) {
 
 // create_account_exists (src/state_machine.zig:1227-1237)
 __device__ __forceinline__ u8 account_exists(const Account& a, const Account& e) {
-    if (a.flags != e.flags) return TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_FLAGS;
-    if (a.user_data_128 != e.user_data_128) return TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_USER_DATA_128;
-    if (a.user_data_64 != e.user_data_64) return TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_USER_DATA_64;
-    if (a.user_data_32 != e.user_data_32) return TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_USER_DATA_32;
-    if (a.ledger != e.ledger) return TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_LEDGER;
-    if (a.code != e.code) return TB_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_CODE;
-    return TB_CREATE_ACCOUNT_EXISTS;
+    if (a.flags != e.flags) return TBGPU_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_FLAGS;
+    if (a.user_data_128 != e.user_data_128) return TBGPU_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_USER_DATA_128;
+    if (a.user_data_64 != e.user_data_64) return TBGPU_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_USER_DATA_64;
+    if (a.user_data_32 != e.user_data_32) return TBGPU_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_USER_DATA_32;
+    if (a.ledger != e.ledger) return TBGPU_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_LEDGER;
+    if (a.code != e.code) return TBGPU_CREATE_ACCOUNT_EXISTS_WITH_DIFFERENT_CODE;
+    return TBGPU_CREATE_ACCOUNT_EXISTS;
 }
 
 __global__ void ac_evaluate(Tables T, AcArgs C, const u8* res_s, const u8* ok_s, u8* res_d, u8* ok_d, u32* cfail_d) {
@@ -148,7 +148,7 @@ __global__ void ac_evaluate(Tables T, AcArgs C, const u8* res_s, const u8* ok_s,
         }
         if (e != NONE32) r = account_exists(a, C.ev[e]);
         else if (C.pre[i] != NONE32) r = account_exists(a, T.acc[C.pre[i]]);
-        else r = TB_CREATE_ACCOUNT_OK;
+        else r = TBGPU_CREATE_ACCOUNT_OK;
     }
     res_d[i] = r;
     ok_d[i] = r == 0 ? 1 : 0;
@@ -162,11 +162,11 @@ __global__ void ac_mask(AcArgs C, const u8* res, const u8* ok, const u32* cfail,
     const u32 cs = C.cs[i];
     const u32 cf = cs != C.ce[i] ? cfail[cs] : NONE32;
     u8 r;
-    if (C.sres[i] == TB_CREATE_ACCOUNT_LINKED_EVENT_CHAIN_OPEN) r = TB_CREATE_ACCOUNT_LINKED_EVENT_CHAIN_OPEN;
-    else if (cf < i) r = TB_CREATE_ACCOUNT_LINKED_EVENT_FAILED;
+    if (C.sres[i] == TBGPU_CREATE_ACCOUNT_LINKED_EVENT_CHAIN_OPEN) r = TBGPU_CREATE_ACCOUNT_LINKED_EVENT_CHAIN_OPEN;
+    else if (cf < i) r = TBGPU_CREATE_ACCOUNT_LINKED_EVENT_FAILED;
     else if (res[i] != 0) r = res[i];
-    else if (cf != NONE32) r = TB_CREATE_ACCOUNT_LINKED_EVENT_FAILED;
-    else r = TB_CREATE_ACCOUNT_OK;
+    else if (cf != NONE32) r = TBGPU_CREATE_ACCOUNT_LINKED_EVENT_FAILED;
+    else r = TBGPU_CREATE_ACCOUNT_OK;
     fres[i] = r;
     mask[i] = ((ok[i] & 2) ? 1 : 0) | (r != 0 ? 2 : 0);
     if ((ok[i] & 1) && (cf == NONE32 || i < cf))  // commit_timestamp survives rollback (:1223)
@@ -174,7 +174,7 @@ __global__ void ac_mask(AcArgs C, const u8* res, const u8* ok, const u32* cfail,
 }
 
 __global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const uint4* rk, u64 row_base,
-                         tb_create_accounts_result_t* results) {
+                         tbgpu_create_accounts_result_t* results) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= C.n) return;
     const u8 r = fres[i];
@@ -318,7 +318,7 @@ void ac_launch_mask(const Tables& T, const AcArgs& C, const u8* res, const u8* o
     ac_mask<<<GRID(C.n)>>>(C, res, ok, cfail, fres, mask, T.commit_ts);
 }
 void ac_launch_apply(const Tables& T, const AcArgs& C, const u8* ok, const u8* fres, const uint4* rk, u64 row_base,
-                     tb_create_accounts_result_t* results, u32* counts, hipStream_t stream) {
+                     tbgpu_create_accounts_result_t* results, u32* counts, hipStream_t stream) {
     ac_apply<<<GRID(C.n)>>>(T, C, ok, fres, rk, row_base, results);
     ac_batch_counts<<<GRID(C.nb)>>>(C.b_start, C.nb, rk, counts);
 }

@@ -43,8 +43,8 @@ struct alignas(16) History {
 static_assert(sizeof(Account) == 128, "Account layout");
 static_assert(sizeof(Transfer) == 128, "Transfer layout");
 static_assert(sizeof(History) == 256, "History layout");
-static_assert(sizeof(Account) == sizeof(tb_account_t), "ABI");
-static_assert(sizeof(Transfer) == sizeof(tb_transfer_t), "ABI");
+static_assert(sizeof(Account) == sizeof(tbgpu_account_t), "ABI");
+static_assert(sizeof(Transfer) == sizeof(tbgpu_transfer_t), "ABI");
 
 // Four balances of an account (the scan state).
 struct Bal4 {

@@ -273,6 +273,7 @@ extern "C" void tbgpu_reset(tbgpu_ctx* c) {
     HIP_CHECK(hipMemsetAsync(c->T.big, 0, sizeof(u32), c->stream));
     if (c->T.dense_n) HIP_CHECK(hipMemsetAsync(c->T.dense, 0, c->T.dense_n * sizeof(u64), c->stream));
     if (c->ximp) HIP_CHECK(hipMemsetAsync(c->ximp, 0, c->xrow_cap, c->stream));
+    HIP_CHECK(hipMemsetAsync(c->f_gtab, 0, c->f_gcap * sizeof(u32), c->stream));  // fast path's claim table
     HIP_CHECK(hipStreamSynchronize(c->stream));
     c->n_accounts = c->n_rows = c->n_hist = 0;
     c->q_runs.assign(1, 0);
@@ -386,7 +387,7 @@ static TrArgs make_tr_args(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb) {
 
 // Single-pass attempt (fast.hip).  Returns false, with every balance delta
 // undone, when some event needs the fixed point.
-static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tb_create_transfers_result_t* results_dev,
+static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_create_transfers_result_t* results_dev,
                      u32* counts_host) {
     hipStream_t s = c->stream;
     FastArgs F{};
@@ -447,7 +448,7 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tb_create_
 // Returns false (nothing committed, every effect undone) when the fast path does
 // not apply and `split` asks the caller to redo these batches in smaller chunks.
 static bool run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
-                                tb_create_transfers_result_t* results_dev, u32* counts_host, bool try_fast_path,
+                                tbgpu_create_transfers_result_t* results_dev, u32* counts_host, bool try_fast_path,
                                 bool split) {
     hipStream_t s = c->stream;
     TrArgs C = make_tr_args(c, ev, n, nb);
@@ -550,7 +551,7 @@ static bool run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
 }
 
 static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t* timestamps, const uint32_t* counts,
-                                  const Transfer* ev_src, bool src_device, tb_create_transfers_result_t* results,
+                                  const Transfer* ev_src, bool src_device, tbgpu_create_transfers_result_t* results,
                                   bool dst_device, uint32_t* result_counts, const uint64_t* ev_ts_host = nullptr,
                                   const uint8_t* ctl_host = nullptr, bool routed_device = false) {
     HIP_CHECK(hipSetDevice(c->device));
@@ -593,8 +594,8 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
                 c->rt_ctl = c->rt_ctl_buf;
             }
         }
-        tb_create_transfers_result_t* rdev =
-            dst_device ? results + total : (tb_create_transfers_result_t*)c->res_buf;
+        tbgpu_create_transfers_result_t* rdev =
+            dst_device ? results + total : (tbgpu_create_transfers_result_t*)c->res_buf;
         const bool try_fast_path = c->slow_chunks % 8 == 0;
         if (!run_transfers_chunk(c, ev, n, nb, rdev, result_counts + b0, try_fast_path,
                                  /*split=*/!c->rt_dry && nb > GENERAL_CHUNK_BATCHES)) {
@@ -627,9 +628,9 @@ static uint64_t routed(tbgpu_ctx* c, uint32_t batch_count, const uint32_t* count
                        uint32_t* result_counts, uint64_t* commit_timestamp, bool device);
 
 extern "C" uint64_t tbgpu_create_transfers_routed(tbgpu_ctx* c, uint32_t batch_count, const uint32_t* counts,
-                                                  const tb_transfer_t* events, const uint64_t* event_timestamps,
+                                                  const tbgpu_transfer_t* events, const uint64_t* event_timestamps,
                                                   const uint8_t* ctl, int dry_run,
-                                                  tb_create_transfers_result_t* results, uint32_t* result_counts,
+                                                  tbgpu_create_transfers_result_t* results, uint32_t* result_counts,
                                                   uint64_t* commit_timestamp) {
     return routed(c, batch_count, counts, events, event_timestamps, ctl, dry_run, results, result_counts,
                   commit_timestamp, false);
@@ -659,7 +660,7 @@ static uint64_t routed(tbgpu_ctx* c, uint32_t batch_count, const uint32_t* count
         HIP_CHECK(hipMemcpyAsync(c->rt_dry_ts, c->T.commit_ts, sizeof(u64), hipMemcpyDeviceToDevice, c->stream));
     }
     const u64 total = transfers_batches(c, batch_count, bts.data(), counts, (const Transfer*)events, device,
-                                        (tb_create_transfers_result_t*)results, device, result_counts,
+                                        (tbgpu_create_transfers_result_t*)results, device, result_counts,
                                         event_timestamps, ctl, device);
     c->rt_ev_ts = nullptr;
     c->rt_ctl = nullptr;
@@ -670,21 +671,21 @@ static uint64_t routed(tbgpu_ctx* c, uint32_t batch_count, const uint32_t* count
     return total;
 }
 
-extern "C" int tbgpu_import_transfers(tbgpu_ctx* c, const tb_transfer_t* rows, uint32_t count) {
+extern "C" int tbgpu_import_transfers(tbgpu_ctx* c, const tbgpu_transfer_t* rows, uint32_t count) {
     HIP_CHECK(hipSetDevice(c->device));
     if (count == 0) return 0;
     // rows already held (committed here or imported before) are skipped: rows are
     // immutable, and the id index must hold each id once
-    std::vector<tb_uint128_t> ids(count);
+    std::vector<tbgpu_uint128_t> ids(count);
     for (u32 i = 0; i < count; i++) ids[i] = rows[i].id;
-    std::vector<tb_transfer_t> found(count);
+    std::vector<tbgpu_transfer_t> found(count);
     const u32 held = tbgpu_lookup_transfers(c, ids.data(), count, found.data());
-    std::vector<tb_transfer_t> keep;
+    std::vector<tbgpu_transfer_t> keep;
     keep.reserve(count);
     for (u32 i = 0, f = 0; i < count; i++) {
         if (f < held && found[f].id.lo == rows[i].id.lo && found[f].id.hi == rows[i].id.hi) { f++; continue; }
         bool dup = false;  // a repeated id within this call
-        for (const tb_transfer_t& k : keep) dup |= k.id.lo == rows[i].id.lo && k.id.hi == rows[i].id.hi;
+        for (const tbgpu_transfer_t& k : keep) dup |= k.id.lo == rows[i].id.lo && k.id.hi == rows[i].id.hi;
         if (!dup) keep.push_back(rows[i]);
     }
     const u64 n = keep.size();
@@ -713,16 +714,16 @@ extern "C" void tbgpu_advance_commit_timestamp(tbgpu_ctx* c, uint64_t timestamp)
     if (timestamp > v) HIP_CHECK(hipMemcpy(c->T.commit_ts, &timestamp, sizeof(u64), hipMemcpyHostToDevice));
 }
 
-extern "C" uint32_t tbgpu_create_transfers(tbgpu_ctx* c, uint64_t timestamp, const tb_transfer_t* events,
-                                           uint32_t count, tb_create_transfers_result_t* results) {
+extern "C" uint32_t tbgpu_create_transfers(tbgpu_ctx* c, uint64_t timestamp, const tbgpu_transfer_t* events,
+                                           uint32_t count, tbgpu_create_transfers_result_t* results) {
     uint32_t rc = 0;
     const uint64_t ts = timestamp;
     return (uint32_t)transfers_batches(c, 1, &ts, &count, (const Transfer*)events, false, results, false, &rc);
 }
 
 extern "C" uint64_t tbgpu_create_transfers_batches(tbgpu_ctx* c, uint32_t batch_count, const uint64_t* timestamps,
-                                                   const uint32_t* counts, const tb_transfer_t* events,
-                                                   tb_create_transfers_result_t* results, uint32_t* result_counts) {
+                                                   const uint32_t* counts, const tbgpu_transfer_t* events,
+                                                   tbgpu_create_transfers_result_t* results, uint32_t* result_counts) {
     return transfers_batches(c, batch_count, timestamps, counts, (const Transfer*)events, false, results, false,
                              result_counts);
 }
@@ -732,13 +733,13 @@ extern "C" uint64_t tbgpu_create_transfers_batches_device(tbgpu_ctx* c, uint32_t
                                                           const void* events_device, void* results_device,
                                                           uint32_t* result_counts) {
     return transfers_batches(c, batch_count, timestamps, counts, (const Transfer*)events_device, true,
-                             (tb_create_transfers_result_t*)results_device, true, result_counts);
+                             (tbgpu_create_transfers_result_t*)results_device, true, result_counts);
 }
 
 // ------------------------------------------------------- create_accounts --
 
 static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
-                               tb_create_accounts_result_t* results_dev, u32* counts_host) {
+                               tbgpu_create_accounts_result_t* results_dev, u32* counts_host) {
     hipStream_t s = c->stream;
     if (n == 0) {
         std::fill(counts_host, counts_host + nb, 0u);
@@ -786,8 +787,8 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
 }
 
 extern "C" uint64_t tbgpu_create_accounts_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t* timestamps,
-                                                  const uint32_t* counts, const tb_account_t* events,
-                                                  tb_create_accounts_result_t* results, uint32_t* result_counts) {
+                                                  const uint32_t* counts, const tbgpu_account_t* events,
+                                                  tbgpu_create_accounts_result_t* results, uint32_t* result_counts) {
     HIP_CHECK(hipSetDevice(c->device));
     std::vector<u32> starts;
     u64 total = 0, ev_off = 0;
@@ -797,7 +798,7 @@ extern "C" uint64_t tbgpu_create_accounts_batches(tbgpu_ctx* c, uint32_t nb_tota
         upload_batches(c, timestamps + b0, counts + b0, nb, starts);
         const u32 n = starts[nb];
         HIP_CHECK(hipMemcpyAsync(c->ev_buf, events + ev_off, (u64)n * 128, hipMemcpyHostToDevice, c->stream));
-        run_accounts_chunk(c, (const Account*)c->ev_buf, n, nb, (tb_create_accounts_result_t*)c->res_buf,
+        run_accounts_chunk(c, (const Account*)c->ev_buf, n, nb, (tbgpu_create_accounts_result_t*)c->res_buf,
                            result_counts + b0);
         copy_results_to_batches(c, nb, starts, result_counts + b0, (u8*)(results + ev_off));
         for (u32 b = 0; b < nb; b++) total += result_counts[b0 + b];
@@ -807,8 +808,8 @@ extern "C" uint64_t tbgpu_create_accounts_batches(tbgpu_ctx* c, uint32_t nb_tota
     return total;
 }
 
-extern "C" uint32_t tbgpu_create_accounts(tbgpu_ctx* c, uint64_t timestamp, const tb_account_t* events,
-                                          uint32_t count, tb_create_accounts_result_t* results) {
+extern "C" uint32_t tbgpu_create_accounts(tbgpu_ctx* c, uint64_t timestamp, const tbgpu_account_t* events,
+                                          uint32_t count, tbgpu_create_accounts_result_t* results) {
     uint32_t rc = 0;
     return (uint32_t)tbgpu_create_accounts_batches(c, 1, &timestamp, &count, events, results, &rc);
 }
@@ -816,7 +817,7 @@ extern "C" uint32_t tbgpu_create_accounts(tbgpu_ctx* c, uint64_t timestamp, cons
 // ------------------------------------------------------------- lookups ----
 
 template <typename Row, typename Launch>
-static uint32_t lookup(tbgpu_ctx* c, const tb_uint128_t* ids, uint32_t count, Row* out, Launch launch) {
+static uint32_t lookup(tbgpu_ctx* c, const tbgpu_uint128_t* ids, uint32_t count, Row* out, Launch launch) {
     HIP_CHECK(hipSetDevice(c->device));
     uint32_t found_total = 0;
     std::vector<Row> rows;
@@ -840,13 +841,13 @@ static uint32_t lookup(tbgpu_ctx* c, const tb_uint128_t* ids, uint32_t count, Ro
     return found_total;
 }
 
-extern "C" uint32_t tbgpu_lookup_accounts(tbgpu_ctx* c, const tb_uint128_t* ids, uint32_t count, tb_account_t* out) {
+extern "C" uint32_t tbgpu_lookup_accounts(tbgpu_ctx* c, const tbgpu_uint128_t* ids, uint32_t count, tbgpu_account_t* out) {
     return lookup(c, ids, count, (Account*)out, [&](const u128* d, u32 k, Account* o, u8* f) {
         launch_lookup_accounts(c->T, d, k, o, f, c->stream);
     });
 }
 
-extern "C" uint32_t tbgpu_lookup_transfers(tbgpu_ctx* c, const tb_uint128_t* ids, uint32_t count, tb_transfer_t* out) {
+extern "C" uint32_t tbgpu_lookup_transfers(tbgpu_ctx* c, const tbgpu_uint128_t* ids, uint32_t count, tbgpu_transfer_t* out) {
     return lookup(c, ids, count, (Transfer*)out, [&](const u128* d, u32 k, Transfer* o, u8* f) {
         launch_lookup_transfers(c->T, d, k, o, f, c->stream);
     });
@@ -902,7 +903,7 @@ extern "C" uint64_t tbgpu_compact(tbgpu_ctx* c) {
 }
 
 // `nq` filters in device memory; results at out + q * stride rows.
-static u64 run_queries(tbgpu_ctx* c, const tb_account_filter_t* filters, u32 nq, u32 stride, void* out, bool history,
+static u64 run_queries(tbgpu_ctx* c, const tbgpu_account_filter_t* filters, u32 nq, u32 stride, void* out, bool history,
                        uint32_t* counts_host) {
     tbgpu_compact(c);
     QIndex X{c->q_key, c->q_val, c->q_runs_dev, (u32)(c->q_runs.size() - 1)};
@@ -919,9 +920,9 @@ static u64 run_queries(tbgpu_ctx* c, const tb_account_filter_t* filters, u32 nq,
     return total;
 }
 
-static uint32_t query_host(tbgpu_ctx* c, const tb_account_filter_t* filter, void* out, bool history) {
+static uint32_t query_host(tbgpu_ctx* c, const tbgpu_account_filter_t* filter, void* out, bool history) {
     HIP_CHECK(hipSetDevice(c->device));
-    tb_account_filter_t* fd = (tb_account_filter_t*)c->res_buf;  // nmax * 8 B >= 64 B
+    tbgpu_account_filter_t* fd = (tbgpu_account_filter_t*)c->res_buf;  // nmax * 8 B >= 64 B
     HIP_CHECK(hipMemcpyAsync(fd, filter, sizeof *filter, hipMemcpyHostToDevice, c->stream));
     uint32_t n = 0;
     run_queries(c, fd, 1, TBGPU_QUERY_MAX, c->ev_buf, history, &n);  // ev_buf: nmax * 128 B >= 8190 rows
@@ -929,25 +930,25 @@ static uint32_t query_host(tbgpu_ctx* c, const tb_account_filter_t* filter, void
     return n;
 }
 
-extern "C" uint32_t tbgpu_get_account_transfers(tbgpu_ctx* c, const tb_account_filter_t* filter, tb_transfer_t* out) {
+extern "C" uint32_t tbgpu_get_account_transfers(tbgpu_ctx* c, const tbgpu_account_filter_t* filter, tbgpu_transfer_t* out) {
     return query_host(c, filter, out, false);
 }
 
-extern "C" uint32_t tbgpu_get_account_history(tbgpu_ctx* c, const tb_account_filter_t* filter,
-                                              tb_account_balance_t* out) {
+extern "C" uint32_t tbgpu_get_account_history(tbgpu_ctx* c, const tbgpu_account_filter_t* filter,
+                                              tbgpu_account_balance_t* out) {
     return query_host(c, filter, out, true);
 }
 
 extern "C" uint64_t tbgpu_get_account_transfers_device(tbgpu_ctx* c, uint32_t count, const void* filters_device,
                                                        uint32_t stride, void* out_device, uint32_t* result_counts) {
     HIP_CHECK(hipSetDevice(c->device));
-    return run_queries(c, (const tb_account_filter_t*)filters_device, count, stride, out_device, false, result_counts);
+    return run_queries(c, (const tbgpu_account_filter_t*)filters_device, count, stride, out_device, false, result_counts);
 }
 
 extern "C" uint64_t tbgpu_get_account_history_device(tbgpu_ctx* c, uint32_t count, const void* filters_device,
                                                      uint32_t stride, void* out_device, uint32_t* result_counts) {
     HIP_CHECK(hipSetDevice(c->device));
-    return run_queries(c, (const tb_account_filter_t*)filters_device, count, stride, out_device, true, result_counts);
+    return run_queries(c, (const tbgpu_account_filter_t*)filters_device, count, stride, out_device, true, result_counts);
 }
 
 // ------------------------------------------------------- persistence ------
@@ -1047,10 +1048,10 @@ extern "C" int tbgpu_open(tbgpu_ctx* c, const void* image, uint64_t size) {
     return 0;
 }
 
-static u128 to128(tb_uint128_t x) { return ((u128)x.hi << 64) | x.lo; }
+static u128 to128(tbgpu_uint128_t x) { return ((u128)x.hi << 64) | x.lo; }
 
-extern "C" int tbgpu_test_set_balances(tbgpu_ctx* c, tb_uint128_t id, tb_uint128_t dp, tb_uint128_t dpo,
-                                       tb_uint128_t cp, tb_uint128_t cpo) {
+extern "C" int tbgpu_test_set_balances(tbgpu_ctx* c, tbgpu_uint128_t id, tbgpu_uint128_t dp, tbgpu_uint128_t dpo,
+                                       tbgpu_uint128_t cp, tbgpu_uint128_t cpo) {
     HIP_CHECK(hipSetDevice(c->device));
     Bal4 b{to128(dp), to128(dpo), to128(cp), to128(cpo)};
     launch_set_balances(c->T, to128(id), b, c->status, c->stream);
@@ -1060,7 +1061,7 @@ extern "C" int tbgpu_test_set_balances(tbgpu_ctx* c, tb_uint128_t id, tb_uint128
     return st;
 }
 
-extern "C" int tbgpu_get_posted(tbgpu_ctx* c, tb_uint128_t pending_id) {
+extern "C" int tbgpu_get_posted(tbgpu_ctx* c, tbgpu_uint128_t pending_id) {
     HIP_CHECK(hipSetDevice(c->device));
     launch_get_posted(c->T, to128(pending_id), c->status, c->stream);
     int st = 0;
@@ -1073,7 +1074,7 @@ extern "C" uint64_t tbgpu_account_count(tbgpu_ctx* c) { return c->n_accounts; }
 extern "C" uint64_t tbgpu_transfer_count(tbgpu_ctx* c) { return c->n_rows; }
 extern "C" uint64_t tbgpu_history_count(tbgpu_ctx* c) { return c->n_hist; }
 
-extern "C" uint64_t tbgpu_export_transfers(tbgpu_ctx* c, uint64_t first, uint64_t count, tb_transfer_t* out) {
+extern "C" uint64_t tbgpu_export_transfers(tbgpu_ctx* c, uint64_t first, uint64_t count, tbgpu_transfer_t* out) {
     HIP_CHECK(hipSetDevice(c->device));
     if (first >= c->n_rows) return 0;
     count = std::min<u64>(count, c->n_rows - first);
@@ -1081,7 +1082,7 @@ extern "C" uint64_t tbgpu_export_transfers(tbgpu_ctx* c, uint64_t first, uint64_
     return count;
 }
 
-extern "C" uint64_t tbgpu_export_history(tbgpu_ctx* c, uint64_t first, uint64_t count, tb_account_history_t* out) {
+extern "C" uint64_t tbgpu_export_history(tbgpu_ctx* c, uint64_t first, uint64_t count, tbgpu_account_history_t* out) {
     HIP_CHECK(hipSetDevice(c->device));
     if (first >= c->n_hist) return 0;
     count = std::min<u64>(count, c->n_hist - first);
@@ -1089,7 +1090,7 @@ extern "C" uint64_t tbgpu_export_history(tbgpu_ctx* c, uint64_t first, uint64_t 
     return count;
 }
 
-extern "C" uint64_t tbgpu_export_accounts(tbgpu_ctx* c, tb_account_t* out, uint64_t capacity) {
+extern "C" uint64_t tbgpu_export_accounts(tbgpu_ctx* c, tbgpu_account_t* out, uint64_t capacity) {
     HIP_CHECK(hipSetDevice(c->device));
     const u64 n = std::min<u64>(capacity, c->n_accounts);  // dense rows, creation order
     if (n) HIP_CHECK(hipMemcpy(out, c->T.acc, n * sizeof(Account), hipMemcpyDeviceToHost));

@@ -15,7 +15,7 @@ struct FastArgs {
     u8* fres;           // per-event result (0 = accepted, deltas applied)
     u32* counters;
     u32* batch_counts;  // failures per batch
-    tb_create_transfers_result_t* results;  // replies, concatenated across batches
+    tbgpu_create_transfers_result_t* results;  // replies, concatenated across batches
     u64 row_base;
     u128* keys;         // accepted ids, for fp_index
     u32* rows;          // stored row per accepted event (written by fp_fix only)

@@ -79,16 +79,16 @@ __device__ __forceinline__ bool gtab_claim_is_dup(const FastArgs& F, u128 id, u3
 
 // create_transfer_exists (src/state_machine.zig:1370-1389)
 __device__ __forceinline__ u8 fp_exists(const Transfer& t, const Transfer& e) {
-    if (t.flags != e.flags) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_FLAGS;
-    if (t.debit_account_id != e.debit_account_id) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_DEBIT_ACCOUNT_ID;
-    if (t.credit_account_id != e.credit_account_id) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_CREDIT_ACCOUNT_ID;
-    if (t.amount != e.amount) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_AMOUNT;
-    if (t.user_data_128 != e.user_data_128) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_128;
-    if (t.user_data_64 != e.user_data_64) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_64;
-    if (t.user_data_32 != e.user_data_32) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_32;
-    if (t.timeout != e.timeout) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_TIMEOUT;
-    if (t.code != e.code) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_CODE;
-    return TB_CREATE_TRANSFER_EXISTS;
+    if (t.flags != e.flags) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_FLAGS;
+    if (t.debit_account_id != e.debit_account_id) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_DEBIT_ACCOUNT_ID;
+    if (t.credit_account_id != e.credit_account_id) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_CREDIT_ACCOUNT_ID;
+    if (t.amount != e.amount) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_AMOUNT;
+    if (t.user_data_128 != e.user_data_128) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_128;
+    if (t.user_data_64 != e.user_data_64) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_64;
+    if (t.user_data_32 != e.user_data_32) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_32;
+    if (t.timeout != e.timeout) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_TIMEOUT;
+    if (t.code != e.code) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_CODE;
+    return TBGPU_CREATE_TRANSFER_EXISTS;
 }
 
 // Continue an account index probe after a first-slot miss; returns the slot.
@@ -142,32 +142,32 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
     const bool maybe = xidx_maybe_present(T, t.id);
     const u64 hx = xidx_hash(t.id) & T.xidx_mask;
     const u32 x_r1 = maybe ? T.xidx[hx] : 0u;
-    if (t.timestamp != 0) return TB_CREATE_TRANSFER_TIMESTAMP_MUST_BE_ZERO;
-    if (f & 0xFFC0u) return TB_CREATE_TRANSFER_RESERVED_FLAG;
-    if (t.id == 0) return TB_CREATE_TRANSFER_ID_MUST_NOT_BE_ZERO;
-    if (t.id == U128_MAX) return TB_CREATE_TRANSFER_ID_MUST_NOT_BE_INT_MAX;
-    if (t.debit_account_id == 0) return TB_CREATE_TRANSFER_DEBIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
-    if (t.debit_account_id == U128_MAX) return TB_CREATE_TRANSFER_DEBIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
-    if (t.credit_account_id == 0) return TB_CREATE_TRANSFER_CREDIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
-    if (t.credit_account_id == U128_MAX) return TB_CREATE_TRANSFER_CREDIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
-    if (t.credit_account_id == t.debit_account_id) return TB_CREATE_TRANSFER_ACCOUNTS_MUST_BE_DIFFERENT;
-    if (t.pending_id != 0) return TB_CREATE_TRANSFER_PENDING_ID_MUST_BE_ZERO;
-    if (!(f & TF_PENDING) && t.timeout != 0) return TB_CREATE_TRANSFER_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
-    if (t.amount == 0) return TB_CREATE_TRANSFER_AMOUNT_MUST_NOT_BE_ZERO;
-    if (t.ledger == 0) return TB_CREATE_TRANSFER_LEDGER_MUST_NOT_BE_ZERO;
-    if (t.code == 0) return TB_CREATE_TRANSFER_CODE_MUST_NOT_BE_ZERO;
+    if (t.timestamp != 0) return TBGPU_CREATE_TRANSFER_TIMESTAMP_MUST_BE_ZERO;
+    if (f & 0xFFC0u) return TBGPU_CREATE_TRANSFER_RESERVED_FLAG;
+    if (t.id == 0) return TBGPU_CREATE_TRANSFER_ID_MUST_NOT_BE_ZERO;
+    if (t.id == U128_MAX) return TBGPU_CREATE_TRANSFER_ID_MUST_NOT_BE_INT_MAX;
+    if (t.debit_account_id == 0) return TBGPU_CREATE_TRANSFER_DEBIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
+    if (t.debit_account_id == U128_MAX) return TBGPU_CREATE_TRANSFER_DEBIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
+    if (t.credit_account_id == 0) return TBGPU_CREATE_TRANSFER_CREDIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
+    if (t.credit_account_id == U128_MAX) return TBGPU_CREATE_TRANSFER_CREDIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
+    if (t.credit_account_id == t.debit_account_id) return TBGPU_CREATE_TRANSFER_ACCOUNTS_MUST_BE_DIFFERENT;
+    if (t.pending_id != 0) return TBGPU_CREATE_TRANSFER_PENDING_ID_MUST_BE_ZERO;
+    if (!(f & TF_PENDING) && t.timeout != 0) return TBGPU_CREATE_TRANSFER_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
+    if (t.amount == 0) return TBGPU_CREATE_TRANSFER_AMOUNT_MUST_NOT_BE_ZERO;
+    if (t.ledger == 0) return TBGPU_CREATE_TRANSFER_LEDGER_MUST_NOT_BE_ZERO;
+    if (t.code == 0) return TBGPU_CREATE_TRANSFER_CODE_MUST_NOT_BE_ZERO;
     if (!(F.ablate & ABL_PROBE)) {
         if (dd) A = {(u64)t.debit_account_id, 0, (u32)(EA & 0x1FFFFFFFu), (u32)(EA >> 32), (u16)((EA >> 28) & 0xE), 0, 0};
         if (dc) B = {(u64)t.credit_account_id, 0, (u32)(EB & 0x1FFFFFFFu), (u32)(EB >> 32), (u16)((EB >> 28) & 0xE), 0, 0};
     }
     const u64 dlo = (u64)t.debit_account_id, dhi = (u64)(t.debit_account_id >> 64);
     if (A.row1 != 0 && (A.id_lo != dlo || A.id_hi != dhi)) A = T.aidx[aidx_probe_from(T, hd, t.debit_account_id)];
-    if (A.row1 == 0) return TB_CREATE_TRANSFER_DEBIT_ACCOUNT_NOT_FOUND;
+    if (A.row1 == 0) return TBGPU_CREATE_TRANSFER_DEBIT_ACCOUNT_NOT_FOUND;
     const u64 clo = (u64)t.credit_account_id, chi = (u64)(t.credit_account_id >> 64);
     if (B.row1 != 0 && (B.id_lo != clo || B.id_hi != chi)) B = T.aidx[aidx_probe_from(T, hc, t.credit_account_id)];
-    if (B.row1 == 0) return TB_CREATE_TRANSFER_CREDIT_ACCOUNT_NOT_FOUND;
-    if (A.ledger != B.ledger) return TB_CREATE_TRANSFER_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
-    if (t.ledger != A.ledger) return TB_CREATE_TRANSFER_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
+    if (B.row1 == 0) return TBGPU_CREATE_TRANSFER_CREDIT_ACCOUNT_NOT_FOUND;
+    if (A.ledger != B.ledger) return TBGPU_CREATE_TRANSFER_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
+    if (t.ledger != A.ledger) return TBGPU_CREATE_TRANSFER_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
     if ((A.flags | B.flags) & (AF_DNEC | AF_CNED | AF_HISTORY)) return FRES_SLOW;  // limits / history
     if (x_r1 != 0) {
         const u32 pre = T.xrows[x_r1 - 1].id == t.id ? x_r1 - 1 : xidx_probe_from(T, hx, t.id);
@@ -177,10 +177,10 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
     // an id repeated within the call is caught by fp_dupcheck (only when ids are not increasing)
     // u128 overflow is impossible: amount < 2^64, balances < 2^126 (T.big clear), < 2^32 events
     if ((u64)(t.amount >> 64) != 0) return FRES_SLOW;
-    if (sum_overflows64(ts, (u64)t.timeout * NS_PER_S)) return TB_CREATE_TRANSFER_OVERFLOWS_TIMEOUT;
+    if (sum_overflows64(ts, (u64)t.timeout * NS_PER_S)) return TBGPU_CREATE_TRANSFER_OVERFLOWS_TIMEOUT;
     *dslot_out = ds;
     *cslot_out = cs;
-    return TB_CREATE_TRANSFER_OK;
+    return TBGPU_CREATE_TRANSFER_OK;
 }
 
 // The static checks that precede what makes an event ineligible (their results
@@ -188,51 +188,51 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
 __device__ __forceinline__ u8 fp_classify_guarded(const Tables& T, const FastArgs& F, const Transfer& t, u32 i,
                                                        u64 ts, u32* dslot_out, u32* cslot_out) {
     const u16 f = t.flags;
-    if (t.timestamp != 0) return TB_CREATE_TRANSFER_TIMESTAMP_MUST_BE_ZERO;
-    if (f & 0xFFC0u) return TB_CREATE_TRANSFER_RESERVED_FLAG;
-    if (t.id == 0) return TB_CREATE_TRANSFER_ID_MUST_NOT_BE_ZERO;
-    if (t.id == U128_MAX) return TB_CREATE_TRANSFER_ID_MUST_NOT_BE_INT_MAX;
+    if (t.timestamp != 0) return TBGPU_CREATE_TRANSFER_TIMESTAMP_MUST_BE_ZERO;
+    if (f & 0xFFC0u) return TBGPU_CREATE_TRANSFER_RESERVED_FLAG;
+    if (t.id == 0) return TBGPU_CREATE_TRANSFER_ID_MUST_NOT_BE_ZERO;
+    if (t.id == U128_MAX) return TBGPU_CREATE_TRANSFER_ID_MUST_NOT_BE_INT_MAX;
     if (f & (TF_POST | TF_VOID)) {
-        if ((f & TF_POST) && (f & TF_VOID)) return TB_CREATE_TRANSFER_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
-        if (f & (TF_PENDING | TF_BDR | TF_BCR)) return TB_CREATE_TRANSFER_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
-        if (t.pending_id == 0) return TB_CREATE_TRANSFER_PENDING_ID_MUST_NOT_BE_ZERO;
-        if (t.pending_id == U128_MAX) return TB_CREATE_TRANSFER_PENDING_ID_MUST_NOT_BE_INT_MAX;
-        if (t.pending_id == t.id) return TB_CREATE_TRANSFER_PENDING_ID_MUST_BE_DIFFERENT;
-        if (t.timeout != 0) return TB_CREATE_TRANSFER_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
+        if ((f & TF_POST) && (f & TF_VOID)) return TBGPU_CREATE_TRANSFER_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+        if (f & (TF_PENDING | TF_BDR | TF_BCR)) return TBGPU_CREATE_TRANSFER_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+        if (t.pending_id == 0) return TBGPU_CREATE_TRANSFER_PENDING_ID_MUST_NOT_BE_ZERO;
+        if (t.pending_id == U128_MAX) return TBGPU_CREATE_TRANSFER_PENDING_ID_MUST_NOT_BE_INT_MAX;
+        if (t.pending_id == t.id) return TBGPU_CREATE_TRANSFER_PENDING_ID_MUST_BE_DIFFERENT;
+        if (t.timeout != 0) return TBGPU_CREATE_TRANSFER_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
         return FRES_SLOW;  // resolves a pending transfer
     }
-    if (t.debit_account_id == 0) return TB_CREATE_TRANSFER_DEBIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
-    if (t.debit_account_id == U128_MAX) return TB_CREATE_TRANSFER_DEBIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
-    if (t.credit_account_id == 0) return TB_CREATE_TRANSFER_CREDIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
-    if (t.credit_account_id == U128_MAX) return TB_CREATE_TRANSFER_CREDIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
-    if (t.credit_account_id == t.debit_account_id) return TB_CREATE_TRANSFER_ACCOUNTS_MUST_BE_DIFFERENT;
-    if (t.pending_id != 0) return TB_CREATE_TRANSFER_PENDING_ID_MUST_BE_ZERO;
-    if (!(f & TF_PENDING) && t.timeout != 0) return TB_CREATE_TRANSFER_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
-    if (!(f & (TF_BDR | TF_BCR)) && t.amount == 0) return TB_CREATE_TRANSFER_AMOUNT_MUST_NOT_BE_ZERO;
-    if (t.ledger == 0) return TB_CREATE_TRANSFER_LEDGER_MUST_NOT_BE_ZERO;
-    if (t.code == 0) return TB_CREATE_TRANSFER_CODE_MUST_NOT_BE_ZERO;
+    if (t.debit_account_id == 0) return TBGPU_CREATE_TRANSFER_DEBIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
+    if (t.debit_account_id == U128_MAX) return TBGPU_CREATE_TRANSFER_DEBIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
+    if (t.credit_account_id == 0) return TBGPU_CREATE_TRANSFER_CREDIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
+    if (t.credit_account_id == U128_MAX) return TBGPU_CREATE_TRANSFER_CREDIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
+    if (t.credit_account_id == t.debit_account_id) return TBGPU_CREATE_TRANSFER_ACCOUNTS_MUST_BE_DIFFERENT;
+    if (t.pending_id != 0) return TBGPU_CREATE_TRANSFER_PENDING_ID_MUST_BE_ZERO;
+    if (!(f & TF_PENDING) && t.timeout != 0) return TBGPU_CREATE_TRANSFER_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
+    if (!(f & (TF_BDR | TF_BCR)) && t.amount == 0) return TBGPU_CREATE_TRANSFER_AMOUNT_MUST_NOT_BE_ZERO;
+    if (t.ledger == 0) return TBGPU_CREATE_TRANSFER_LEDGER_MUST_NOT_BE_ZERO;
+    if (t.code == 0) return TBGPU_CREATE_TRANSFER_CODE_MUST_NOT_BE_ZERO;
     const u32 ds = acc_probe(T.aidx, T.aidx_mask, t.debit_account_id);
-    if (ds == NONE32) return TB_CREATE_TRANSFER_DEBIT_ACCOUNT_NOT_FOUND;
+    if (ds == NONE32) return TBGPU_CREATE_TRANSFER_DEBIT_ACCOUNT_NOT_FOUND;
     const u32 cs = acc_probe(T.aidx, T.aidx_mask, t.credit_account_id);
-    if (cs == NONE32) return TB_CREATE_TRANSFER_CREDIT_ACCOUNT_NOT_FOUND;
+    if (cs == NONE32) return TBGPU_CREATE_TRANSFER_CREDIT_ACCOUNT_NOT_FOUND;
     const Account& dr = T.acc[ds];
     const Account& cr = T.acc[cs];
-    if (dr.ledger != cr.ledger) return TB_CREATE_TRANSFER_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
-    if (t.ledger != dr.ledger) return TB_CREATE_TRANSFER_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
+    if (dr.ledger != cr.ledger) return TBGPU_CREATE_TRANSFER_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
+    if (t.ledger != dr.ledger) return TBGPU_CREATE_TRANSFER_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
     if (f & (TF_BDR | TF_BCR)) return FRES_SLOW;                                  // balancing
     if ((dr.flags | cr.flags) & (AF_DNEC | AF_CNED | AF_HISTORY)) return FRES_SLOW;  // limits / history
     const u32 pre = xidx_probe(T, t.id);
     if (pre != NONE32) return fp_exists(t, T.xrows[pre]);
-    if (gtab_claim_is_dup(F, t.id, i)) return FRES_SLOW;                           // id repeats in the call
+    // an id repeated within the call is caught by fp_dupcheck, as on the unguarded path
     // overflow impossible: amount < 2^64 and the touched balances' high words < 2^62
     const u64 lim = 1ull << 62;
     if ((u64)(t.amount >> 64) != 0) return FRES_SLOW;
     if ((u64)(dr.debits_pending >> 64) >= lim || (u64)(dr.debits_posted >> 64) >= lim) return FRES_SLOW;
     if ((u64)(cr.credits_pending >> 64) >= lim || (u64)(cr.credits_posted >> 64) >= lim) return FRES_SLOW;
-    if (sum_overflows64(ts, (u64)t.timeout * NS_PER_S)) return TB_CREATE_TRANSFER_OVERFLOWS_TIMEOUT;
+    if (sum_overflows64(ts, (u64)t.timeout * NS_PER_S)) return TBGPU_CREATE_TRANSFER_OVERFLOWS_TIMEOUT;
     *dslot_out = ds;
     *cslot_out = cs;
-    return TB_CREATE_TRANSFER_OK;
+    return TBGPU_CREATE_TRANSFER_OK;
 }
 
 // Balance field of an account row: 0 debits_pending, 1 debits_posted,
@@ -409,10 +409,10 @@ void fp_commit(Tables T, FastArgs F) {
     if (valid) {
         id = t.id;
         u32 ds = NONE32, cs = NONE32;
-        if (lk && i - bs == nbatch - 1) r = TB_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN;  // checked first (:1024)
-        else if (myctl & TBGPU_CTL_SKIP) r = TB_CREATE_TRANSFER_LINKED_EVENT_FAILED;    // broken on another shard
+        if (lk && i - bs == nbatch - 1) r = TBGPU_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN;  // checked first (:1024)
+        else if (myctl & TBGPU_CTL_SKIP) r = TBGPU_CREATE_TRANSFER_LINKED_EVENT_FAILED;    // broken on another shard
         else r = fp_classify(T, F, t, i, ts, &ds, &cs);
-        own_ok = r == TB_CREATE_TRANSFER_OK;
+        own_ok = r == TBGPU_CREATE_TRANSFER_OK;
         if (member && r != FRES_SLOW) {
             // deferred to fp_chains: no balance delta, no count; the optimistic row
             // and the id claim as for any accepted event
@@ -426,7 +426,7 @@ void fp_commit(Tables T, FastArgs F) {
         } else {
             F.fres[i] = r;
         }
-        if (r == TB_CREATE_TRANSFER_OK) {
+        if (r == TBGPU_CREATE_TRANSFER_OK) {
             F.keys[i] = t.id;
             // tile-local aggregation first: a hot account costs one global atomic per tile
             const u64 a = (u64)t.amount;
@@ -445,8 +445,8 @@ void fp_commit(Tables T, FastArgs F) {
         }
     }
 #undef STORE_ROW
-    const bool ok = valid && r == TB_CREATE_TRANSFER_OK;
-    const bool bad = valid && r != TB_CREATE_TRANSFER_OK && r != FRES_CHAIN;
+    const bool ok = valid && r == TBGPU_CREATE_TRANSFER_OK;
+    const bool bad = valid && r != TBGPU_CREATE_TRANSFER_OK && r != FRES_CHAIN;
 
     // Strictly increasing ids across the whole call cannot repeat: then fp_dupcheck
     // has nothing to do (sequential ids, the benchmark's default id order).
@@ -551,7 +551,7 @@ void fp_commit(Tables T, FastArgs F) {
 __device__ __forceinline__ void fp_dupcheck_one(const FastArgs& F, u32 i) {
     F.gpos[i] = NONE32;
     const u8 r = F.fres[i];
-    if (r != TB_CREATE_TRANSFER_OK && r != (FRES_CHAIN | TB_CREATE_TRANSFER_OK)) return;
+    if (r != TBGPU_CREATE_TRANSFER_OK && r != (FRES_CHAIN | TBGPU_CREATE_TRANSFER_OK)) return;
     if (gtab_claim_is_dup(F, F.keys[i], i)) atomicOr(&F.counters[CNT_FLAGS], (u32)FL_SLOW);
 }
 
@@ -622,7 +622,7 @@ __global__ void fp_index(Tables T, FastArgs F, bool fixed) {
         }
     }
     if (i >= F.n) return;
-    if (F.fres[i] != TB_CREATE_TRANSFER_OK) return;
+    if (F.fres[i] != TBGPU_CREATE_TRANSFER_OK) return;
     xidx_insert(T, F.keys[i], fixed ? F.rows[i] : (u32)(F.row_base + i));
 }
 
@@ -660,18 +660,18 @@ __device__ void fp_chains_one(const Tables& T, const FastArgs& F, u32 i, u32& n_
     while (e + 1 < be && fp_linked(F, e)) e++;
     u32 j = NONE32;
     for (u32 k = s; k <= e; k++)
-        if ((F.fres[k] & 0x7F) != TB_CREATE_TRANSFER_OK) { j = k; break; }
+        if ((F.fres[k] & 0x7F) != TBGPU_CREATE_TRANSFER_OK) { j = k; break; }
     if (j == NONE32 && F.ctl && (F.ctl[e] & TBGPU_CTL_DOOM)) j = e + 1;  // breaks on another shard
     u8 fin;
-    if (j == NONE32) fin = TB_CREATE_TRANSFER_OK;
-    else if (own == TB_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN) fin = own;
+    if (j == NONE32) fin = TBGPU_CREATE_TRANSFER_OK;
+    else if (own == TBGPU_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN) fin = own;
     else if (i == j) fin = own;
-    else fin = TB_CREATE_TRANSFER_LINKED_EVENT_FAILED;
+    else fin = TBGPU_CREATE_TRANSFER_LINKED_EVENT_FAILED;
     F.fres2[i] = fin;
     const u64 nbatch = be - bs;
     const u64 ts = F.ev_ts ? F.ev_ts[i] : F.b_ts[b] - nbatch + (i - bs) + 1;
-    if (own == TB_CREATE_TRANSFER_OK && (j == NONE32 || i < j)) mts = max(mts, ts);
-    if (fin == TB_CREATE_TRANSFER_OK) {
+    if (own == TBGPU_CREATE_TRANSFER_OK && (j == NONE32 || i < j)) mts = max(mts, ts);
+    if (fin == TBGPU_CREATE_TRANSFER_OK) {
         n_ok++;
         if (!F.dry) {
             const Transfer& t = F.ev[i];
@@ -732,7 +732,7 @@ __global__ void fp_chains_fin(FastArgs F) {
 // With failures: mask for the rank scan (bit0 accepted, bit1 failed).
 __global__ void fp_mask(FastArgs F, u8* mask) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < F.n) mask[i] = F.fres[i] == TB_CREATE_TRANSFER_OK ? 1 : 2;
+    if (i < F.n) mask[i] = F.fres[i] == TBGPU_CREATE_TRANSFER_OK ? 1 : 2;
 }
 
 // With failures: stored rows at their ranks (re-copied from the events, so the
@@ -743,7 +743,7 @@ __global__ void fp_fix(FastArgs F, Tables T, const uint4* rk) {
     const u32 b = fp_batch_of(F.b_start, F.nb, i);
     const u32 bs = F.b_start[b];
     const u8 r = F.fres[i];
-    if (r != TB_CREATE_TRANSFER_OK) {
+    if (r != TBGPU_CREATE_TRANSFER_OK) {
         F.results[rk[i].y] = {i - bs, (u32)r};  // concatenated replies
         return;
     }
@@ -772,7 +772,7 @@ __global__ void fp_undo(Tables T, FastArgs F) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) *F.commit_ts = *(const u64*)&F.counters[CNT_TS_SAVE];
     if (F.dry || i >= F.n) return;
-    if (F.fres[i] != TB_CREATE_TRANSFER_OK) return;
+    if (F.fres[i] != TBGPU_CREATE_TRANSFER_OK) return;
     const Transfer& t = F.ev[i];
     const u32 ds = acc_probe(T.aidx, T.aidx_mask, t.debit_account_id);
     const u32 cs = acc_probe(T.aidx, T.aidx_mask, t.credit_account_id);

@@ -13,10 +13,10 @@ struct QIndex {
 };
 
 struct QArgs {
-    const tb_account_filter_t* filters;  // [nq], device
+    const tbgpu_account_filter_t* filters;  // [nq], device
     u32 nq;
     u32 stride;    // output rows reserved per filter
-    void* out;     // Transfer[nq * stride] or tb_account_balance_t[nq * stride]
+    void* out;     // Transfer[nq * stride] or tbgpu_account_balance_t[nq * stride]
     u32* counts;   // [nq] rows written per filter
     u32 history;   // 0 get_account_transfers, 1 get_account_history
     u64 n_hist;

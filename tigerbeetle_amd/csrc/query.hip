@@ -81,13 +81,13 @@ __device__ __forceinline__ u32 hist_at(const Tables& T, u64 n_hist, u64 ts) {
 }
 
 // get_scan_from_filter's validity test (src/state_machine.zig:822-833).
-__device__ __forceinline__ bool filter_valid(const tb_account_filter_t& f) {
+__device__ __forceinline__ bool filter_valid(const tbgpu_account_filter_t& f) {
     const u128 id = ((u128)f.account_id.hi << 64) | f.account_id.lo;
     bool reserved_zero = true;
     for (int k = 0; k < 24; k++) reserved_zero &= f.reserved[k] == 0;
     return id != 0 && id != U128_MAX && f.timestamp_min != ~0ull && f.timestamp_max != ~0ull &&
            (f.timestamp_max == 0 || f.timestamp_min <= f.timestamp_max) && f.limit != 0 &&
-           (f.flags & (TB_ACCOUNT_FILTER_DEBITS | TB_ACCOUNT_FILTER_CREDITS)) != 0 && (f.flags >> 3) == 0 &&
+           (f.flags & (TBGPU_ACCOUNT_FILTER_DEBITS | TBGPU_ACCOUNT_FILTER_CREDITS)) != 0 && (f.flags >> 3) == 0 &&
            reserved_zero;
 }
 
@@ -98,7 +98,7 @@ __global__ __launch_bounds__(Q_THREADS) void q_scan(Tables T, QIndex X, QArgs A)
     __shared__ u64 s_lo, s_hi;
     const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const u32 q = blockIdx.x;
-    const tb_account_filter_t f = A.filters[q];
+    const tbgpu_account_filter_t f = A.filters[q];
     const u128 fid = ((u128)f.account_id.hi << 64) | f.account_id.lo;
     if (tid == 0) {
         u32 acc = filter_valid(f) ? acc_probe(T.aidx, T.aidx_mask, fid) : NONE32;
@@ -114,8 +114,8 @@ __global__ __launch_bounds__(Q_THREADS) void q_scan(Tables T, QIndex X, QArgs A)
         // TimestampRange with 0 = unbounded (src/lsm/timestamp_range.zig:4-5)
         const u64 tlo = f.timestamp_min == 0 ? 1ull : f.timestamp_min;
         const u64 thi = f.timestamp_max == 0 ? ~0ull - 1 : f.timestamp_max;
-        const bool rev = f.flags & TB_ACCOUNT_FILTER_REVERSED;
-        const bool want_dr = f.flags & TB_ACCOUNT_FILTER_DEBITS, want_cr = f.flags & TB_ACCOUNT_FILTER_CREDITS;
+        const bool rev = f.flags & TBGPU_ACCOUNT_FILTER_REVERSED;
+        const bool want_dr = f.flags & TBGPU_ACCOUNT_FILTER_DEBITS, want_cr = f.flags & TBGPU_ACCOUNT_FILTER_CREDITS;
         const u64 lt = __lanemask_lt();
         for (u32 kk = 0; kk < X.nruns; kk++) {
             if (s_n >= lim) break;  // uniform (written before a barrier)
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(Q_THREADS) void q_scan(Tables T, QIndex X, QArgs A)
             out[k] = ((const uint4*)&T.xrows[s_sel[k >> 3]])[k & 7];
     } else {
         // execute_get_account_history (:1171-1192): the filter account's side
-        tb_account_balance_t* out = (tb_account_balance_t*)A.out + (u64)q * A.stride;
+        tbgpu_account_balance_t* out = (tbgpu_account_balance_t*)A.out + (u64)q * A.stride;
         for (u32 k = tid; k < n; k += Q_THREADS) {
             const History& h = T.hrows[s_sel[k]];
             const bool dr = h.dr_account_id == fid;
@@ -183,8 +183,8 @@ __global__ __launch_bounds__(Q_THREADS) void q_scan(Tables T, QIndex X, QArgs A)
                                dr ? h.dr_debits_posted : h.cr_debits_posted,
                                dr ? h.dr_credits_pending : h.cr_credits_pending,
                                dr ? h.dr_credits_posted : h.cr_credits_posted};
-            tb_account_balance_t b{};
-            tb_uint128_t* w = &b.debits_pending;
+            tbgpu_account_balance_t b{};
+            tbgpu_uint128_t* w = &b.debits_pending;
             for (int x = 0; x < 4; x++) w[x] = {(u64)v[x], (u64)(v[x] >> 64)};
             b.timestamp = h.timestamp;
             out[k] = b;

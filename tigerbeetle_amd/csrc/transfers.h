@@ -50,7 +50,7 @@ void tr_launch_evaluate(const Tables& T, const TrArgs& C, const EvalState& S, co
 void tr_launch_mask(const Tables& T, const TrArgs& C, const EvalState& S, u8* fres, u8* mask, hipStream_t stream);
 void tr_launch_apply(const Tables& T, const TrArgs& C, const EvalState& S, const u8* fres, const uint4* rk,
                      const u32* spos, const Bal4* bb, u64 row_base, u64 hist_base,
-                     tb_create_transfers_result_t* results, u32* counts, hipStream_t stream);
+                     tbgpu_create_transfers_result_t* results, u32* counts, hipStream_t stream);
 
 // create_accounts (accounts.hip)
 struct AcArgs {
@@ -80,7 +80,7 @@ void ac_launch_evaluate(const Tables& T, const AcArgs& C, const u8* res_s, const
 void ac_launch_mask(const Tables& T, const AcArgs& C, const u8* res, const u8* ok, const u32* cfail, u8* fres,
                     u8* mask, hipStream_t stream);
 void ac_launch_apply(const Tables& T, const AcArgs& C, const u8* ok, const u8* fres, const uint4* rk, u64 row_base,
-                     tb_create_accounts_result_t* results, u32* counts, hipStream_t stream);
+                     tbgpu_create_accounts_result_t* results, u32* counts, hipStream_t stream);
 
 // lookups / maintenance (accounts.hip)
 void launch_lookup_accounts(const Tables& T, const u128* ids, u32 n, Account* out, u8* found, hipStream_t stream);

@@ -98,26 +98,26 @@ __global__ void tr_classify(Tables T, TrArgs C) {
     u8 sres;
     const u16 f = t.flags;
     if (linked(i) && k == nbatch - 1) {
-        sres = TB_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN;
+        sres = TBGPU_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN;
     } else if (C.ctl && (C.ctl[i] & TBGPU_CTL_SKIP)) {
-        sres = TB_CREATE_TRANSFER_LINKED_EVENT_FAILED;  // chain broken on another shard
+        sres = TBGPU_CREATE_TRANSFER_LINKED_EVENT_FAILED;  // chain broken on another shard
     } else if (t.timestamp != 0) {
-        sres = TB_CREATE_TRANSFER_TIMESTAMP_MUST_BE_ZERO;
+        sres = TBGPU_CREATE_TRANSFER_TIMESTAMP_MUST_BE_ZERO;
     } else if (f & 0xFFC0u) {
-        sres = TB_CREATE_TRANSFER_RESERVED_FLAG;
+        sres = TBGPU_CREATE_TRANSFER_RESERVED_FLAG;
     } else if (t.id == 0) {
-        sres = TB_CREATE_TRANSFER_ID_MUST_NOT_BE_ZERO;
+        sres = TBGPU_CREATE_TRANSFER_ID_MUST_NOT_BE_ZERO;
     } else if (t.id == U128_MAX) {
-        sres = TB_CREATE_TRANSFER_ID_MUST_NOT_BE_INT_MAX;
+        sres = TBGPU_CREATE_TRANSFER_ID_MUST_NOT_BE_INT_MAX;
     } else if (f & (TF_POST | TF_VOID)) {
-        if ((f & TF_POST) && (f & TF_VOID)) sres = TB_CREATE_TRANSFER_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
-        else if (f & TF_PENDING) sres = TB_CREATE_TRANSFER_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
-        else if (f & TF_BDR) sres = TB_CREATE_TRANSFER_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
-        else if (f & TF_BCR) sres = TB_CREATE_TRANSFER_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
-        else if (t.pending_id == 0) sres = TB_CREATE_TRANSFER_PENDING_ID_MUST_NOT_BE_ZERO;
-        else if (t.pending_id == U128_MAX) sres = TB_CREATE_TRANSFER_PENDING_ID_MUST_NOT_BE_INT_MAX;
-        else if (t.pending_id == t.id) sres = TB_CREATE_TRANSFER_PENDING_ID_MUST_BE_DIFFERENT;
-        else if (t.timeout != 0) sres = TB_CREATE_TRANSFER_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
+        if ((f & TF_POST) && (f & TF_VOID)) sres = TBGPU_CREATE_TRANSFER_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+        else if (f & TF_PENDING) sres = TBGPU_CREATE_TRANSFER_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+        else if (f & TF_BDR) sres = TBGPU_CREATE_TRANSFER_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+        else if (f & TF_BCR) sres = TBGPU_CREATE_TRANSFER_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+        else if (t.pending_id == 0) sres = TBGPU_CREATE_TRANSFER_PENDING_ID_MUST_NOT_BE_ZERO;
+        else if (t.pending_id == U128_MAX) sres = TBGPU_CREATE_TRANSFER_PENDING_ID_MUST_NOT_BE_INT_MAX;
+        else if (t.pending_id == t.id) sres = TBGPU_CREATE_TRANSFER_PENDING_ID_MUST_BE_DIFFERENT;
+        else if (t.timeout != 0) sres = TBGPU_CREATE_TRANSFER_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
         else {
             sres = SRES_DYN;
             fl |= FL_POSTVOID;
@@ -132,34 +132,34 @@ __global__ void tr_classify(Tables T, TrArgs C) {
             pslot = gtab_find_or_insert(C, t.pending_id, i, 1);
         }
     } else if (t.debit_account_id == 0) {
-        sres = TB_CREATE_TRANSFER_DEBIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
+        sres = TBGPU_CREATE_TRANSFER_DEBIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
     } else if (t.debit_account_id == U128_MAX) {
-        sres = TB_CREATE_TRANSFER_DEBIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
+        sres = TBGPU_CREATE_TRANSFER_DEBIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
     } else if (t.credit_account_id == 0) {
-        sres = TB_CREATE_TRANSFER_CREDIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
+        sres = TBGPU_CREATE_TRANSFER_CREDIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
     } else if (t.credit_account_id == U128_MAX) {
-        sres = TB_CREATE_TRANSFER_CREDIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
+        sres = TBGPU_CREATE_TRANSFER_CREDIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
     } else if (t.credit_account_id == t.debit_account_id) {
-        sres = TB_CREATE_TRANSFER_ACCOUNTS_MUST_BE_DIFFERENT;
+        sres = TBGPU_CREATE_TRANSFER_ACCOUNTS_MUST_BE_DIFFERENT;
     } else if (t.pending_id != 0) {
-        sres = TB_CREATE_TRANSFER_PENDING_ID_MUST_BE_ZERO;
+        sres = TBGPU_CREATE_TRANSFER_PENDING_ID_MUST_BE_ZERO;
     } else if (!(f & TF_PENDING) && t.timeout != 0) {
-        sres = TB_CREATE_TRANSFER_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
+        sres = TBGPU_CREATE_TRANSFER_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
     } else if (!(f & (TF_BDR | TF_BCR)) && t.amount == 0) {
-        sres = TB_CREATE_TRANSFER_AMOUNT_MUST_NOT_BE_ZERO;
+        sres = TBGPU_CREATE_TRANSFER_AMOUNT_MUST_NOT_BE_ZERO;
     } else if (t.ledger == 0) {
-        sres = TB_CREATE_TRANSFER_LEDGER_MUST_NOT_BE_ZERO;
+        sres = TBGPU_CREATE_TRANSFER_LEDGER_MUST_NOT_BE_ZERO;
     } else if (t.code == 0) {
-        sres = TB_CREATE_TRANSFER_CODE_MUST_NOT_BE_ZERO;
+        sres = TBGPU_CREATE_TRANSFER_CODE_MUST_NOT_BE_ZERO;
     } else if ((dslot = acc_probe(T.aidx, T.aidx_mask, t.debit_account_id)) == NONE32) {
-        sres = TB_CREATE_TRANSFER_DEBIT_ACCOUNT_NOT_FOUND;
+        sres = TBGPU_CREATE_TRANSFER_DEBIT_ACCOUNT_NOT_FOUND;
     } else if ((cslot = acc_probe(T.aidx, T.aidx_mask, t.credit_account_id)) == NONE32) {
-        sres = TB_CREATE_TRANSFER_CREDIT_ACCOUNT_NOT_FOUND;
+        sres = TBGPU_CREATE_TRANSFER_CREDIT_ACCOUNT_NOT_FOUND;
     } else {
         const Account& dr = T.acc[dslot];
         const Account& cr = T.acc[cslot];
-        if (dr.ledger != cr.ledger) sres = TB_CREATE_TRANSFER_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
-        else if (t.ledger != dr.ledger) sres = TB_CREATE_TRANSFER_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
+        if (dr.ledger != cr.ledger) sres = TBGPU_CREATE_TRANSFER_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
+        else if (t.ledger != dr.ledger) sres = TBGPU_CREATE_TRANSFER_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
         else {
             sres = SRES_DYN;
             pre_e = xidx_probe(T, t.id);
@@ -304,43 +304,43 @@ __device__ Transfer load_ref(const Tables& T, const TrArgs& C, const EvalState& 
 
 // create_transfer_exists (src/state_machine.zig:1370-1389)
 __device__ __forceinline__ u8 create_transfer_exists(const Transfer& t, const Transfer& e) {
-    if (t.flags != e.flags) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_FLAGS;
-    if (t.debit_account_id != e.debit_account_id) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_DEBIT_ACCOUNT_ID;
-    if (t.credit_account_id != e.credit_account_id) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_CREDIT_ACCOUNT_ID;
-    if (t.amount != e.amount) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_AMOUNT;
-    if (t.user_data_128 != e.user_data_128) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_128;
-    if (t.user_data_64 != e.user_data_64) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_64;
-    if (t.user_data_32 != e.user_data_32) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_32;
-    if (t.timeout != e.timeout) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_TIMEOUT;
-    if (t.code != e.code) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_CODE;
-    return TB_CREATE_TRANSFER_EXISTS;
+    if (t.flags != e.flags) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_FLAGS;
+    if (t.debit_account_id != e.debit_account_id) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_DEBIT_ACCOUNT_ID;
+    if (t.credit_account_id != e.credit_account_id) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_CREDIT_ACCOUNT_ID;
+    if (t.amount != e.amount) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_AMOUNT;
+    if (t.user_data_128 != e.user_data_128) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_128;
+    if (t.user_data_64 != e.user_data_64) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_64;
+    if (t.user_data_32 != e.user_data_32) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_32;
+    if (t.timeout != e.timeout) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_TIMEOUT;
+    if (t.code != e.code) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_CODE;
+    return TBGPU_CREATE_TRANSFER_EXISTS;
 }
 
 // post_or_void_pending_transfer_exists (src/state_machine.zig:1500-1561)
 __device__ __forceinline__ u8 post_or_void_exists(const Transfer& t, const Transfer& e, const Transfer& p) {
-    if (t.flags != e.flags) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_FLAGS;
+    if (t.flags != e.flags) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_FLAGS;
     if (t.amount == 0) {
-        if (e.amount != p.amount) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_AMOUNT;
+        if (e.amount != p.amount) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_AMOUNT;
     } else {
-        if (t.amount != e.amount) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_AMOUNT;
+        if (t.amount != e.amount) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_AMOUNT;
     }
-    if (t.pending_id != e.pending_id) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_PENDING_ID;
+    if (t.pending_id != e.pending_id) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_PENDING_ID;
     if (t.user_data_128 == 0) {
-        if (e.user_data_128 != p.user_data_128) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_128;
+        if (e.user_data_128 != p.user_data_128) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_128;
     } else {
-        if (t.user_data_128 != e.user_data_128) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_128;
+        if (t.user_data_128 != e.user_data_128) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_128;
     }
     if (t.user_data_64 == 0) {
-        if (e.user_data_64 != p.user_data_64) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_64;
+        if (e.user_data_64 != p.user_data_64) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_64;
     } else {
-        if (t.user_data_64 != e.user_data_64) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_64;
+        if (t.user_data_64 != e.user_data_64) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_64;
     }
     if (t.user_data_32 == 0) {
-        if (e.user_data_32 != p.user_data_32) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_32;
+        if (e.user_data_32 != p.user_data_32) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_32;
     } else {
-        if (t.user_data_32 != e.user_data_32) return TB_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_32;
+        if (t.user_data_32 != e.user_data_32) return TBGPU_CREATE_TRANSFER_EXISTS_WITH_DIFFERENT_USER_DATA_32;
     }
-    return TB_CREATE_TRANSFER_EXISTS;
+    return TBGPU_CREATE_TRANSFER_EXISTS;
 }
 
 // Balance-dependent tail of create_transfer (src/state_machine.zig:1286-1322).
@@ -353,27 +353,27 @@ __device__ __forceinline__ u8 eval_balances(const Transfer& t, const Bal4& dr, c
         const u128 dr_balance = dr.dpo + dr.dp;
         const u128 avail = dr.cpo > dr_balance ? dr.cpo - dr_balance : 0;  // -| saturating
         if (avail < amount) amount = avail;
-        if (amount == 0) return TB_CREATE_TRANSFER_EXCEEDS_CREDITS;
+        if (amount == 0) return TBGPU_CREATE_TRANSFER_EXCEEDS_CREDITS;
     }
     if (f & TF_BCR) {
         const u128 cr_balance = cr.cpo + cr.cp;
         const u128 avail = cr.dpo > cr_balance ? cr.dpo - cr_balance : 0;
         if (avail < amount) amount = avail;
-        if (amount == 0) return TB_CREATE_TRANSFER_EXCEEDS_DEBITS;
+        if (amount == 0) return TBGPU_CREATE_TRANSFER_EXCEEDS_DEBITS;
     }
     if (f & TF_PENDING) {
-        if (sum_overflows128(amount, dr.dp)) return TB_CREATE_TRANSFER_OVERFLOWS_DEBITS_PENDING;
-        if (sum_overflows128(amount, cr.cp)) return TB_CREATE_TRANSFER_OVERFLOWS_CREDITS_PENDING;
+        if (sum_overflows128(amount, dr.dp)) return TBGPU_CREATE_TRANSFER_OVERFLOWS_DEBITS_PENDING;
+        if (sum_overflows128(amount, cr.cp)) return TBGPU_CREATE_TRANSFER_OVERFLOWS_CREDITS_PENDING;
     }
-    if (sum_overflows128(amount, dr.dpo)) return TB_CREATE_TRANSFER_OVERFLOWS_DEBITS_POSTED;
-    if (sum_overflows128(amount, cr.cpo)) return TB_CREATE_TRANSFER_OVERFLOWS_CREDITS_POSTED;
-    if (sum_overflows128(amount, dr.dp + dr.dpo)) return TB_CREATE_TRANSFER_OVERFLOWS_DEBITS;
-    if (sum_overflows128(amount, cr.cp + cr.cpo)) return TB_CREATE_TRANSFER_OVERFLOWS_CREDITS;
-    if (sum_overflows64(t.timestamp, (u64)t.timeout * NS_PER_S)) return TB_CREATE_TRANSFER_OVERFLOWS_TIMEOUT;
-    if ((dr_flags & AF_DNEC) && dr.dp + dr.dpo + amount > dr.cpo) return TB_CREATE_TRANSFER_EXCEEDS_CREDITS;
-    if ((cr_flags & AF_CNED) && cr.cp + cr.cpo + amount > cr.dpo) return TB_CREATE_TRANSFER_EXCEEDS_DEBITS;
+    if (sum_overflows128(amount, dr.dpo)) return TBGPU_CREATE_TRANSFER_OVERFLOWS_DEBITS_POSTED;
+    if (sum_overflows128(amount, cr.cpo)) return TBGPU_CREATE_TRANSFER_OVERFLOWS_CREDITS_POSTED;
+    if (sum_overflows128(amount, dr.dp + dr.dpo)) return TBGPU_CREATE_TRANSFER_OVERFLOWS_DEBITS;
+    if (sum_overflows128(amount, cr.cp + cr.cpo)) return TBGPU_CREATE_TRANSFER_OVERFLOWS_CREDITS;
+    if (sum_overflows64(t.timestamp, (u64)t.timeout * NS_PER_S)) return TBGPU_CREATE_TRANSFER_OVERFLOWS_TIMEOUT;
+    if ((dr_flags & AF_DNEC) && dr.dp + dr.dpo + amount > dr.cpo) return TBGPU_CREATE_TRANSFER_EXCEEDS_CREDITS;
+    if ((cr_flags & AF_CNED) && cr.cp + cr.cpo + amount > cr.dpo) return TBGPU_CREATE_TRANSFER_EXCEEDS_DEBITS;
     *amount_out = amount;
-    return TB_CREATE_TRANSFER_OK;
+    return TBGPU_CREATE_TRANSFER_OK;
 }
 
 __device__ __forceinline__ bool visible(const TrArgs& C, const EvalState& S, u32 j, u32 csi) {
@@ -409,7 +409,7 @@ __global__ void tr_evaluate(Tables T, TrArgs C, EvalState S, EvalState D, const 
                 const u16 dfl = T.acc[C.dslot[i]].flags, cfl = T.acc[C.cslot[i]].flags;
                 u128 amount = 0;
                 res = eval_balances(t, bd, bc, dfl, cfl, &amount);
-                if (res == TB_CREATE_TRANSFER_OK) {
+                if (res == TBGPU_CREATE_TRANSFER_OK) {
                     amt = amount;
                     if (t.flags & TF_PENDING) dpe = amount; else dpo = amount;
                 }
@@ -423,20 +423,20 @@ __global__ void tr_evaluate(Tables T, TrArgs C, EvalState S, EvalState D, const 
             pref = p;
             const bool post = t.flags & TF_POST;
             if (p == NONE32) {
-                res = TB_CREATE_TRANSFER_PENDING_TRANSFER_NOT_FOUND;
+                res = TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_NOT_FOUND;
             } else {
                 const Transfer P = load_ref(T, C, S, p);
                 const u128 amount = t.amount > 0 ? t.amount : P.amount;
-                if (!(P.flags & TF_PENDING)) res = TB_CREATE_TRANSFER_PENDING_TRANSFER_NOT_PENDING;
+                if (!(P.flags & TF_PENDING)) res = TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_NOT_PENDING;
                 else if (t.debit_account_id > 0 && t.debit_account_id != P.debit_account_id)
-                    res = TB_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_DEBIT_ACCOUNT_ID;
+                    res = TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_DEBIT_ACCOUNT_ID;
                 else if (t.credit_account_id > 0 && t.credit_account_id != P.credit_account_id)
-                    res = TB_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_CREDIT_ACCOUNT_ID;
-                else if (t.ledger > 0 && t.ledger != P.ledger) res = TB_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_LEDGER;
-                else if (t.code > 0 && t.code != P.code) res = TB_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_CODE;
-                else if (amount > P.amount) res = TB_CREATE_TRANSFER_EXCEEDS_PENDING_TRANSFER_AMOUNT;
+                    res = TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_CREDIT_ACCOUNT_ID;
+                else if (t.ledger > 0 && t.ledger != P.ledger) res = TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_LEDGER;
+                else if (t.code > 0 && t.code != P.code) res = TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_CODE;
+                else if (amount > P.amount) res = TBGPU_CREATE_TRANSFER_EXCEEDS_PENDING_TRANSFER_AMOUNT;
                 else if ((t.flags & TF_VOID) && amount < P.amount)
-                    res = TB_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_AMOUNT;
+                    res = TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_HAS_DIFFERENT_AMOUNT;
                 else if (e != NONE32) res = post_or_void_exists(t, load_ref(T, C, S, e), P);
                 else {
                     // posted groove (src/state_machine.zig:1431-1436)
@@ -444,12 +444,12 @@ __global__ void tr_evaluate(Tables T, TrArgs C, EvalState S, EvalState D, const 
                     for (u32 j = C.prev_pend[i]; j != NONE32; j = C.prev_pend[j])
                         if (visible(C, S, j, csi)) { ful = (C.ev[j].flags & TF_POST) ? 1 : 2; break; }
                     if (ful == 0 && (p & PREF_ROW)) ful = T.xful[p & ~PREF_ROW];
-                    if (ful == 1) res = TB_CREATE_TRANSFER_PENDING_TRANSFER_ALREADY_POSTED;
-                    else if (ful == 2) res = TB_CREATE_TRANSFER_PENDING_TRANSFER_ALREADY_VOIDED;
+                    if (ful == 1) res = TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_ALREADY_POSTED;
+                    else if (ful == 2) res = TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_ALREADY_VOIDED;
                     else if (P.timeout > 0 && t.timestamp >= P.timestamp + (u64)P.timeout * NS_PER_S)
-                        res = TB_CREATE_TRANSFER_PENDING_TRANSFER_EXPIRED;
+                        res = TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_EXPIRED;
                     else {
-                        res = TB_CREATE_TRANSFER_OK;
+                        res = TBGPU_CREATE_TRANSFER_OK;
                         amt = amount;
                         pamt = P.amount;
                         dpe = (u128)0 - P.amount;
@@ -460,13 +460,13 @@ __global__ void tr_evaluate(Tables T, TrArgs C, EvalState S, EvalState D, const 
         }
     }
     D.res[i] = res;
-    D.ok[i] = res == TB_CREATE_TRANSFER_OK ? 1 : 0;
+    D.ok[i] = res == TBGPU_CREATE_TRANSFER_OK ? 1 : 0;
     D.amt[i] = amt;
     D.pamt[i] = pamt;
     D.pref[i] = pref;
     D.dpend[i] = dpe;
     D.dpost[i] = dpo;
-    if (res != TB_CREATE_TRANSFER_OK && csi != C.ce[i]) atomicMin(&D.cfail[csi], i);
+    if (res != TBGPU_CREATE_TRANSFER_OK && csi != C.ce[i]) atomicMin(&D.cfail[csi], i);
     const bool changed = res != S.res[i] || amt != S.amt[i] || pamt != S.pamt[i] || pref != S.pref[i];
     if (changed) atomicAdd(&C.counters[CNT_CHANGES], 1u);
 }
@@ -490,7 +490,7 @@ __global__ void tr_init(Tables T, TrArgs C, EvalState D) {
             const u32 j = C.pend_last[i];
             pref = j != NONE32 ? j : (C.pre_p[i] != NONE32 ? (PREF_ROW | C.pre_p[i]) : NONE32);
             if (pref == NONE32) {
-                res = TB_CREATE_TRANSFER_PENDING_TRANSFER_NOT_FOUND;
+                res = TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_NOT_FOUND;
             } else {
                 res = 0;
                 pamt = (pref & PREF_ROW) ? T.xrows[pref & ~PREF_ROW].amount : C.ev[pref].amount;
@@ -568,11 +568,11 @@ __global__ void tr_mask(Tables T, TrArgs C, EvalState S, u8* fres, u8* mask) {
     u32 cf = inch ? S.cfail[cs] : NONE32;
     if (cf == NONE32 && doom) cf = C.ce[i] + 1;  // the chain breaks after its last local member
     u8 r;
-    if (C.sres[i] == TB_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN) r = TB_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN;
-    else if (cf < i) r = TB_CREATE_TRANSFER_LINKED_EVENT_FAILED;
+    if (C.sres[i] == TBGPU_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN) r = TBGPU_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN;
+    else if (cf < i) r = TBGPU_CREATE_TRANSFER_LINKED_EVENT_FAILED;
     else if (S.res[i] != 0) r = S.res[i];
-    else if (cf != NONE32) r = TB_CREATE_TRANSFER_LINKED_EVENT_FAILED;
-    else r = TB_CREATE_TRANSFER_OK;
+    else if (cf != NONE32) r = TBGPU_CREATE_TRANSFER_LINKED_EVENT_FAILED;
+    else r = TBGPU_CREATE_TRANSFER_OK;
     const bool ok = S.ok[i] & 2;
     bool hist = false;
     if (ok && !(C.ev[i].flags & (TF_POST | TF_VOID)))
@@ -587,7 +587,7 @@ __global__ void tr_mask(Tables T, TrArgs C, EvalState S, u8* fres, u8* mask) {
 
 __global__ void tr_apply(Tables T, TrArgs C, EvalState S, const u8* __restrict__ fres, const uint4* __restrict__ rk,
                          const u32* __restrict__ spos, const Bal4* __restrict__ bb, u64 row_base, u64 hist_base,
-                         tb_create_transfers_result_t* __restrict__ results) {
+                         tbgpu_create_transfers_result_t* __restrict__ results) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= C.n) return;
     const u8 r = fres[i];
@@ -697,7 +697,7 @@ void tr_launch_mask(const Tables& T, const TrArgs& C, const EvalState& S, u8* fr
 }
 void tr_launch_apply(const Tables& T, const TrArgs& C, const EvalState& S, const u8* fres, const uint4* rk,
                      const u32* spos, const Bal4* bb, u64 row_base, u64 hist_base,
-                     tb_create_transfers_result_t* results, u32* counts, hipStream_t stream) {
+                     tbgpu_create_transfers_result_t* results, u32* counts, hipStream_t stream) {
     tr_apply<<<GRID(C.n)>>>(T, C, S, fres, rk, spos, bb, row_base, hist_base, results);
     if (!C.dry) tr_range<<<GRID(C.n)>>>(T, C, S);
     batch_counts<<<GRID(C.nb)>>>(C.b_start, C.nb, rk, counts);

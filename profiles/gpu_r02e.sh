@@ -1,0 +1,9 @@
+#!/bin/bash
+set -o pipefail
+O=gpurun_out/r02f; mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -s --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1; rc=$?; echo "tests rc=$rc"; tail -3 $O/gpu_tests.log
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 300 python -u bench.py --config 3 --no-queries --no-host --no-cpu > $O/bench_c3.json 2> $O/bench_c3.err; echo "c3 rc=$?"; cat $O/bench_c3.json
+TBGPU_TRACE_PASSES=1 timeout -k 10 300 python -u bench.py --config 3 --no-queries --no-host --no-cpu --steps 1 > $O/bench_c3t.json 2> $O/trace.err; echo "c3t rc=$?"
+timeout -s KILL 200 rocprofv3 --kernel-trace --stats -d $O/kt3 -o kt --output-format csv -- python3 bench.py --config 3 --steps 2 --warmup 1 --no-cpu --no-queries --no-host > $O/kt3.log 2>&1; echo "kt3 rc=$?"

@@ -14,8 +14,10 @@
 // deltas, segmented by (account, chain).  Both are one scan with a two-level
 // segmented operator; H is compiled out when the call has no chains.
 //
-// Traffic per side: 8 B key/value + ~33 B delta gather + 64 B init gather
-// (L2-local: consecutive sides share the account row) + 64 B output.
+// Traffic per side: the 4-B key, the side record (4-B event, 4-B chain, 1-B ok,
+// 32-B deltas, contiguous), a 4-B chain-failure gather for chain members, the 64-B
+// initial balances (L2-local: consecutive sides share the account row) and the
+// 64-B output.
 #include "common.h"
 #include "engine.h"
 
@@ -59,7 +61,9 @@ __device__ __forceinline__ SE identity() {
 }
 
 // Load sorted position q as a scan element.  Invalid (inert) sides sort last and
-// contribute nothing; they are marked as segment starts so they never leak.
+// contribute nothing; they are marked as segment starts so they never leak.  The
+// side records are in sorted order (written there by the evaluation): the scan
+// reads them contiguously, plus the chain's first failure for chain members.
 template <bool HAS_H>
 __device__ __forceinline__ SE load_elem(const SideScanArgs& A, u64 q, u32 invalid) {
     SE e;
@@ -69,23 +73,24 @@ __device__ __forceinline__ SE load_elem(const SideScanArgs& A, u64 q, u32 invali
         e.fl = 3;
         return e;
     }
-    const u32 sv = A.sval[q];
-    const u32 i = sv >> 1;
+    const u32 cs = A.sq_cs[q] & SQ_CS;
     bool f_start = true, h_start = true;
     if (q > 0) {
-        const u32 pkey = A.skey[q - 1];
-        f_start = pkey != key;
-        h_start = f_start || A.cs[A.sval[q - 1] >> 1] != A.cs[i];
+        f_start = A.skey[q - 1] != key;
+        h_start = f_start || (A.sq_cs[q - 1] & SQ_CS) != cs;
     }
     e.fl = (f_start ? 1u : 0u) | (h_start ? 2u : 0u);
-    const u8 ok = A.ok[i];
-    u128 dpe = A.dpend[i], dpo = A.dpost[i];
     zero(e.F);
     if (HAS_H) zero(e.H);
-    if (ok & 2) {
-        if (sv & 1) { e.F.cp = dpe; e.F.cpo = dpo; } else { e.F.dp = dpe; e.F.dpo = dpo; }
-    } else if (HAS_H && (ok & 1)) {
-        if (sv & 1) { e.H.cp = dpe; e.H.cpo = dpo; } else { e.H.dp = dpe; e.H.dpo = dpo; }
+    const bool eval_ok = A.sq_ok[q] & 1;
+    if (!eval_ok) return e;
+    const bool fin = side_final(A, q);
+    const u128 dpe = A.sq_dpend[q], dpo = A.sq_dpost[q];
+    const bool credit = A.sq_ev[q] >> 31;
+    if (fin) {
+        if (credit) { e.F.cp = dpe; e.F.cpo = dpo; } else { e.F.dp = dpe; e.F.dpo = dpo; }
+    } else if (HAS_H) {
+        if (credit) { e.H.cp = dpe; e.H.cpo = dpo; } else { e.H.dp = dpe; e.H.dpo = dpo; }
     }
     return e;
 }
@@ -112,6 +117,7 @@ __device__ SE block_excl(SE v, SE* sh, SE* total) {
 
 template <bool HAS_H>
 __global__ __launch_bounds__(BS_THREADS) void bs_reduce(SideScanArgs A, u64 m, u32 invalid, SE* __restrict__ tagg) {
+    if (!gate_open(A.gate)) return;
     __shared__ SE sh[BS_THREADS];
     const u64 base = (u64)blockIdx.x * BS_TILE + (u64)threadIdx.x * BS_IPT;
     SE acc = identity<HAS_H>();
@@ -123,7 +129,8 @@ __global__ __launch_bounds__(BS_THREADS) void bs_reduce(SideScanArgs A, u64 m, u
 }
 
 template <bool HAS_H>
-__global__ __launch_bounds__(BS_THREADS) void bs_tiles(SE* __restrict__ tagg, u64 ntiles) {
+__global__ __launch_bounds__(BS_THREADS) void bs_tiles(PassGate gate, SE* __restrict__ tagg, u64 ntiles) {
+    if (!gate_open(gate)) return;
     __shared__ SE sh[BS_THREADS];
     const u32 tid = threadIdx.x;
     const u64 chunk = (ntiles + BS_THREADS - 1) / BS_THREADS;
@@ -143,6 +150,12 @@ __global__ __launch_bounds__(BS_THREADS) void bs_tiles(SE* __restrict__ tagg, u6
 template <bool HAS_H>
 __global__ __launch_bounds__(BS_THREADS) void bs_down(SideScanArgs A, u64 m, u32 invalid, const SE* __restrict__ tagg,
                                                       const Account* __restrict__ acc, Bal4* __restrict__ bb) {
+    if (!gate_open(A.gate)) return;
+    // the next state's per-chain first failures start at "none" (its evaluation
+    // follows this scan and lowers them with atomicMin)
+    if (A.cfail_clear)
+        for (u64 k = (u64)blockIdx.x * BS_THREADS + threadIdx.x; k < A.n; k += (u64)gridDim.x * BS_THREADS)
+            A.cfail_clear[k] = NONE32;
     __shared__ SE sh[BS_THREADS];
     const u64 base = (u64)blockIdx.x * BS_TILE + (u64)threadIdx.x * BS_IPT;
     SE acc_t = identity<HAS_H>();
@@ -180,22 +193,19 @@ __global__ void bs_final(SideScanArgs A, u64 m, u32 invalid, const Bal4* __restr
     if (key >= invalid) return;
     if (q + 1 < m && A.skey[q + 1] == key) return;
     Bal4 tot = bb[q];
-    const u32 i = A.sval[q] >> 1;
+    const u32 cs = A.sq_cs[q] & SQ_CS;
     // remove the H contribution (same account, same chain, eval-ok & !final-ok)
     for (u64 p = q; p > 0;) {
         --p;
-        if (A.skey[p] != key) break;
-        const u32 j = A.sval[p] >> 1;
-        if (A.cs[j] != A.cs[i]) break;
-        const u8 ok = A.ok[j];
-        if ((ok & 1) && !(ok & 2)) {
-            if (A.sval[p] & 1) { tot.cp -= A.dpend[j]; tot.cpo -= A.dpost[j]; }
-            else { tot.dp -= A.dpend[j]; tot.dpo -= A.dpost[j]; }
+        if (A.skey[p] != key || (A.sq_cs[p] & SQ_CS) != cs) break;
+        if ((A.sq_ok[p] & 1) && !side_final(A, p)) {
+            if (A.sq_ev[p] >> 31) { tot.cp -= A.sq_dpend[p]; tot.cpo -= A.sq_dpost[p]; }
+            else { tot.dp -= A.sq_dpend[p]; tot.dpo -= A.sq_dpost[p]; }
         }
     }
-    if (A.ok[i] & 2) {
-        if (A.sval[q] & 1) { tot.cp += A.dpend[i]; tot.cpo += A.dpost[i]; }
-        else { tot.dp += A.dpend[i]; tot.dpo += A.dpost[i]; }
+    if (side_final(A, q)) {
+        if (A.sq_ev[q] >> 31) { tot.cp += A.sq_dpend[q]; tot.cpo += A.sq_dpost[q]; }
+        else { tot.dp += A.sq_dpend[q]; tot.dpo += A.sq_dpost[q]; }
     }
     Account& a = acc[key];
     a.debits_pending = tot.dp;
@@ -219,11 +229,11 @@ void side_scan(const SideScanArgs& A, u64 m, u32 invalid, bool has_chains, void*
     SE* tagg = (SE*)tile_scratch;
     if (has_chains) {
         bs_reduce<true><<<(u32)ntiles, BS_THREADS, 0, stream>>>(A, m, invalid, tagg);
-        bs_tiles<true><<<1, BS_THREADS, 0, stream>>>(tagg, ntiles);
+        bs_tiles<true><<<1, BS_THREADS, 0, stream>>>(A.gate, tagg, ntiles);
         bs_down<true><<<(u32)ntiles, BS_THREADS, 0, stream>>>(A, m, invalid, tagg, acc, bb);
     } else {
         bs_reduce<false><<<(u32)ntiles, BS_THREADS, 0, stream>>>(A, m, invalid, tagg);
-        bs_tiles<false><<<1, BS_THREADS, 0, stream>>>(tagg, ntiles);
+        bs_tiles<false><<<1, BS_THREADS, 0, stream>>>(A.gate, tagg, ntiles);
         bs_down<false><<<(u32)ntiles, BS_THREADS, 0, stream>>>(A, m, invalid, tagg, acc, bb);
     }
     HIP_CHECK(hipGetLastError());

@@ -105,8 +105,9 @@ struct SortScratch {
     u32* hist;      // 256 * max_blocks
     u64 capacity;   // max items
 };
+// With `pred`, every kernel of the sort returns at once unless *pred & pred_mask.
 void radix_sort_pairs(const u32* keys_in, const u32* vals_in, u32* keys_out, u32* vals_out, u64 n, int bits,
-                      SortScratch& s, hipStream_t stream);
+                      SortScratch& s, hipStream_t stream, const u32* pred = nullptr, u32 pred_mask = 0);
 u64 radix_sort_hist_words(u64 capacity);
 
 // Exclusive scan of three u32 counters packed per element from a u8 bitmask.

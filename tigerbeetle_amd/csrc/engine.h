@@ -44,7 +44,13 @@ struct Tables {
     // read from an 8 MB table instead of a 32-byte probe of a 64 MB one.
     u64* dense;
     u64 dense_n;
+    // Device-side append cursors, so that consecutive chunks and calls need no host
+    // round trip: [0] stored transfer rows, [1] account-history rows, [2] replies
+    // written so far in the current call (the streaming reply offset).
+    u64* base;
+    u64 xrow_cap, hist_cap;
 };
+enum { BASE_ROWS = 0, BASE_HIST = 1, BASE_REPLIES = 2 };
 
 __device__ __forceinline__ bool dense_has(const Tables& T, u128 id) {
     return (u64)(id >> 64) == 0 && (u64)id - 1 < T.dense_n;
@@ -61,7 +67,7 @@ __device__ __forceinline__ bool xidx_maybe_present(const Tables& T, u128 id) {
 // One double-buffered fixed-point state (see transfers.hip).
 struct EvalState {
     u8* res;     // own evaluation result (0 = ok)
-    u8* ok;      // bit0 eval-ok, bit1 final-ok (chain persisted)
+    u8* ok;      // 1 = eval-ok (final-ok, chain persisted, is derived: final_ok below)
     u32* pref;   // resolved pending transfer reference
     u32* cfail;  // per chain start: first failing member (NONE32 = none)
     u128* amt;   // effective amount (balancing clamp / post amount)
@@ -70,14 +76,73 @@ struct EvalState {
     u128* dpost; // side delta on the *_posted balance
 };
 
+// Pass gate of the fixed point: the kernels of pass p run while the previous
+// pass changed something (its change count != 0; forced to 1 for the first pass) and no
+// side key has moved (a post/void resolved to another pending: the host re-sorts).
+// Passes are enqueued in groups without host round trips; the kernels of the
+// passes after convergence return at once.
+struct PassGate {
+    const u32* chg;     // the previous pass's change count (a ring word)
+    const u32* resort;  // nonzero: a side key moved, the host re-sorts before going on
+    u32 p;              // this pass's number
+};
+__device__ __forceinline__ bool gate_open(const PassGate& g) { return *g.chg != 0 && *g.resort == 0; }
+
+// final-ok: eval-ok and the event's chain persisted (execute's scope_close(.persist),
+// src/state_machine.zig:1074-1082), and not doomed by a break on another shard.
+__device__ __forceinline__ bool chain_persisted(const u32* cs, const u32* ce, const u32* cfail, const u8* ctl, u32 j) {
+    const u32 s = cs[j], e = ce[j];
+    if (ctl && (ctl[e] & TBGPU_CTL_DOOM)) return false;
+    return s == e || cfail[s] == NONE32;
+}
+__device__ __forceinline__ bool final_ok(const u32* cs, const u32* ce, const u32* cfail, const u8* ctl, const u8* ok,
+                                         u32 j) {
+    return (ok[j] & 1) && chain_persisted(cs, ce, cfail, ctl, j);
+}
+
+// The account sides of a chunk's events, sorted by account row and, within an
+// account, by event (a stable sort of the event-ordered sides).  A transfer has a
+// debit and a credit side; a post/void has one pair per candidate pending (the
+// pending it resolved to last pass, a committed transfer with that id, the first
+// earlier events with that id: at most SIDE_CANDS), of which only the pair of the
+// pending it resolves to carries its effect, so a post/void whose resolution moves
+// needs no re-sort.  `sq_*` are in sorted order: the scan reads them contiguously.
+constexpr u32 SIDE_CANDS = 3;
+struct Sides {
+    u32 m;            // sides of the chunk
+    u32* soff;        // [n + 1] first side (unsorted id) of each event
+    u32* sev;         // [m] unsorted: event | side << 31 (0 debit, 1 credit)
+    u32* scand;       // [m] unsorted: the candidate pending of a post/void pair (pref encoding), else NONE32
+    u32* spos;        // [m] sorted position of unsorted side s
+    const u32* skey_s;  // [m] sorted keys (account row; >= invalid: no account)
+    u32* sq_ev;       // [m] sorted: event | side << 31
+    u32* sq_cs;       // [m] sorted: chain start | standalone << 31 | doomed << 30
+    u8* sq_ok;        // [m] sorted, per pass: the side's effect is evaluated-ok
+    u128* sq_dpend;   // [m] sorted, per pass: its delta on the *_pending balance
+    u128* sq_dpost;   // [m] sorted, per pass: its delta on the *_posted balance
+};
+constexpr u32 SQ_STANDALONE = 1u << 31, SQ_DOOM = 1u << 30, SQ_CS = (1u << 30) - 1;
+
 struct SideScanArgs {
     const u32* skey;  // sorted side keys (account row; >= invalid for inert)
-    const u32* sval;  // sorted side ids (2*event + 0 debit / 1 credit)
-    const u32* cs;    // chain start per event
-    const u8* ok;
-    const u128* dpend;
-    const u128* dpost;
+    const u32* sq_ev;
+    const u32* sq_cs;
+    const u8* sq_ok;
+    const u128* sq_dpend;
+    const u128* sq_dpost;
+    const u32* cfail; // per-chain first failure of the state scanned
+    u32* cfail_clear; // the next state's cfail, reset by the scan (NONE32), or null
+    u32 n;            // events (cfail_clear length)
+    PassGate gate;
 };
+
+// final-ok of a sorted side: evaluated-ok and its chain persisted
+__device__ __forceinline__ bool side_final(const SideScanArgs& A, u64 q) {
+    if (!(A.sq_ok[q] & 1)) return false;
+    const u32 c = A.sq_cs[q];
+    if (c & SQ_DOOM) return false;
+    return (c & SQ_STANDALONE) || A.cfail[c & SQ_CS] == NONE32;
+}
 
 u64 side_scan_tile_bytes(u64 capacity);
 void side_scan(const SideScanArgs& A, u64 m, u32 invalid, bool has_chains, void* tile_scratch, const Account* acc,
@@ -132,6 +197,8 @@ enum {
     CNT_KEYS = 2,       // side keys changed since the last sort
     CNT_OK = 3,         // fast path: accepted events
     CNT_BAD = 4,        // fast path: events with a result other than ok
+    CNT_RESORT = 5,     // general path: pass + 1 whose evaluation moved a side key (0 = none)
+    CNT_DBG = 6,        // diagnostics (words 6-11): changed events by kind, summed over a call's passes
     CNT_TS_SAVE = 12,   // fast path: commit_timestamp before the call (u64 in words 12-13)
     CNT_COUNT = 16,
 };

@@ -10,6 +10,7 @@
 //
 // See transfers.hip for why the fixed point reproduces execute() exactly.
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -51,6 +52,9 @@ T* dalloc(u64 count, u64* total) {
 
 }  // namespace
 
+constexpr u32 PC_RING = 1024;        // pass-counter ring (passes in flight << ring)
+constexpr u32 PASS_GROUP_MAX = 48;   // passes enqueued between two host round trips
+
 struct tbgpu_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -69,10 +73,16 @@ struct tbgpu_ctx {
     u64* ts = nullptr;
     u32 *cs = nullptr, *ce = nullptr;
     u8* sres = nullptr;
-    u32 *dslot, *cslot, *pre_e, *pre_p, *pp_dslot, *pp_cslot, *gslot, *pslot, *prev_id, *pend_last, *prev_pend;
+    u32 *dslot, *cslot, *pre_e, *pre_p, *pp_dslot, *pp_cslot, *gslot, *pslot, *prev_id, *pend_last, *pend_first,
+        *prev_pend;
     u32 *gclaim, *gcnt_id, *gcnt_pd, *gmem, *gbeg, *gend;
     EvalState st[2];
+    u64 scap = 0, side_m = 0;  // side capacity, sides of the last fixed point
     u32 *skey, *sval, *skey_s, *sval_s, *spos;
+    u32 *soff, *sev, *scand, *sq_ev, *sq_cs;
+    u8* sq_ok = nullptr;
+    u128 *sq_dpend = nullptr, *sq_dpost = nullptr;
+    u32 *gkey_s, *gsorted;  // the id-group sort's output (the members of each id group, by event)
     Bal4* bb = nullptr;
     SortScratch ss{};
     void* side_tiles = nullptr;
@@ -103,6 +113,16 @@ struct tbgpu_ctx {
     const u8* rt_ctl = nullptr;
     bool rt_dry = false;
     u32 slow_chunks = 0;  // consecutive chunks that needed the fixed point
+    u32 last_passes = 8;  // passes the last fixed point took (sizes the next pass group)
+    // fixed-point pass counters, a ring of PC_RING words each: changes per pass (the
+    // gate of the next pass) and the first changed event of each pass
+    u32* pc = nullptr;
+    u64* rg_part = nullptr;    // tr_range's per-block records
+    u32* h_pc = nullptr;       // pinned mirror of the change ring
+    u64* h_base = nullptr;     // pinned mirror of T.base
+    u32* h_rc = nullptr;       // pinned per-batch reply counts of the current call
+    u64 h_rc_cap = 0;
+    u64 rows_hi = 0;           // upper bound of T.base[BASE_ROWS] (n_rows + events enqueued since)
     // account-transfers index (query.hip), allocated by the first compaction
     u32 *q_key = nullptr, *q_val = nullptr, *q_tkey = nullptr, *q_tval = nullptr;
     SortScratch q_ss{};
@@ -124,7 +144,9 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->nmax = nmax;
     c->bmax = nmax + 2;
     c->gcap = pow2_at_least(4 * nmax);
-    const u64 n = nmax, m = 2 * nmax;
+    // sides: two per transfer; a post/void with several candidate pendings has more
+    // (engine.h Sides); beyond this capacity a call falls back to one pair each
+    const u64 n = nmax, m = 3 * nmax;
     c->ev_buf = dalloc<u8>(n * 128, &B);
     c->b_start = dalloc<u32>(c->bmax + 1, &B);
     c->b_ts = dalloc<u64>(c->bmax, &B);
@@ -133,7 +155,7 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->ce = dalloc<u32>(n, &B);
     c->sres = dalloc<u8>(n, &B);
     u32** u32s[] = {&c->dslot, &c->cslot, &c->pre_e, &c->pre_p, &c->pp_dslot, &c->pp_cslot,
-                    &c->gslot, &c->pslot, &c->prev_id, &c->pend_last, &c->prev_pend};
+                    &c->gslot, &c->pslot, &c->prev_id, &c->pend_last, &c->pend_first, &c->prev_pend};
     for (u32** p : u32s) *p = dalloc<u32>(n, &B);
     u32** g32s[] = {&c->gclaim, &c->gcnt_id, &c->gcnt_pd, &c->gmem, &c->gbeg, &c->gend};
     for (u32** p : g32s) *p = dalloc<u32>(c->gcap, &B);
@@ -147,11 +169,22 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
         s.dpend = dalloc<u128>(n, &B);
         s.dpost = dalloc<u128>(n, &B);
     }
+    c->scap = m;
     c->skey = dalloc<u32>(m, &B);
     c->sval = dalloc<u32>(m, &B);
     c->skey_s = dalloc<u32>(m, &B);
     c->sval_s = dalloc<u32>(m, &B);
     c->spos = dalloc<u32>(m, &B);
+    c->soff = dalloc<u32>(n + 1, &B);
+    c->sev = dalloc<u32>(m, &B);
+    c->scand = dalloc<u32>(m, &B);
+    c->sq_ev = dalloc<u32>(m, &B);
+    c->sq_cs = dalloc<u32>(m, &B);
+    c->sq_ok = dalloc<u8>(m, &B);
+    c->sq_dpend = dalloc<u128>(m, &B);
+    c->sq_dpost = dalloc<u128>(m, &B);
+    c->gkey_s = dalloc<u32>(n, &B);
+    c->gsorted = dalloc<u32>(n, &B);
     c->bb = dalloc<Bal4>(m, &B);
     c->ss.keys_tmp = dalloc<u32>(m, &B);
     c->ss.vals_tmp = dalloc<u32>(m, &B);
@@ -177,6 +210,10 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->rt_ts_buf = dalloc<u64>(n, &B);
     c->rt_ctl_buf = dalloc<u8>(n, &B);
     c->rt_dry_ts = dalloc<u64>(1, &B);
+    c->pc = dalloc<u32>(2 * PC_RING, &B);
+    c->rg_part = dalloc<u64>(tr_range_part_words(n), &B);
+    HIP_CHECK(hipHostMalloc((void**)&c->h_pc, 2 * PC_RING * sizeof(u32), hipHostMallocDefault));
+    HIP_CHECK(hipHostMalloc((void**)&c->h_base, 8 * sizeof(u64), hipHostMallocDefault));  // [4..5]: a uint4
     HIP_CHECK(hipHostMalloc((void**)&c->h_counters, CNT_COUNT * sizeof(u32), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc((void**)&c->h_counts, c->bmax * sizeof(u32), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc((void**)&c->h_stage_ts, c->bmax * sizeof(u64), hipHostMallocDefault));
@@ -254,6 +291,9 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     c->T.commit_ts = dalloc<u64>(2, &B);
     c->T.idr = dalloc<u64>(4, &B);
     c->T.big = dalloc<u32>(4, &B);
+    c->T.base = dalloc<u64>(4, &B);
+    c->T.xrow_cap = c->xrow_cap;
+    c->T.hist_cap = c->hist_cap;
     c->T.dense_n = o.accounts_max < (1ull << 29) - 1 ? o.accounts_max : 0;  // row + 1 in 29 bits
     c->T.dense = dalloc<u64>(c->T.dense_n, &B);
     alloc_scratch(c, o.events_per_call_max);
@@ -271,11 +311,13 @@ extern "C" void tbgpu_reset(tbgpu_ctx* c) {
     HIP_CHECK(hipMemsetAsync(c->T.idr, 0, 2 * sizeof(u64), c->stream));                  // max = 0
     HIP_CHECK(hipMemsetAsync(c->T.idr + 2, 0xFF, 2 * sizeof(u64), c->stream));           // min = ~0
     HIP_CHECK(hipMemsetAsync(c->T.big, 0, sizeof(u32), c->stream));
+    HIP_CHECK(hipMemsetAsync(c->T.base, 0, 4 * sizeof(u64), c->stream));
     if (c->T.dense_n) HIP_CHECK(hipMemsetAsync(c->T.dense, 0, c->T.dense_n * sizeof(u64), c->stream));
     if (c->ximp) HIP_CHECK(hipMemsetAsync(c->ximp, 0, c->xrow_cap, c->stream));
     HIP_CHECK(hipMemsetAsync(c->f_gtab, 0, c->f_gcap * sizeof(u32), c->stream));  // fast path's claim table
     HIP_CHECK(hipStreamSynchronize(c->stream));
     c->n_accounts = c->n_rows = c->n_hist = 0;
+    c->rows_hi = 0;
     c->q_runs.assign(1, 0);
 }
 
@@ -286,12 +328,14 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     // Free every device allocation by walking the struct's pointers.
     void* ptrs[] = {c->T.dense, c->T.acc, c->T.aidx, c->T.xrows, c->T.xful, c->T.xidx, c->T.hrows, c->T.commit_ts, c->T.idr, c->T.big, c->ev_buf,
                     c->b_start, c->b_ts, c->ts, c->cs, c->ce, c->sres, c->dslot, c->cslot, c->pre_e, c->pre_p,
-                    c->pp_dslot, c->pp_cslot, c->gslot, c->pslot, c->prev_id, c->pend_last, c->prev_pend,
+                    c->pp_dslot, c->pp_cslot, c->gslot, c->pslot, c->prev_id, c->pend_last, c->pend_first, c->prev_pend,
                     c->gclaim, c->gcnt_id, c->gcnt_pd, c->gmem, c->gbeg, c->gend, c->skey, c->sval, c->skey_s,
+                    c->soff, c->sev, c->scand, c->sq_ev, c->sq_cs, c->sq_ok, c->sq_dpend, c->sq_dpost, c->gkey_s,
+                    c->gsorted,
                     c->sval_s, c->spos, c->bb, c->ss.keys_tmp, c->ss.vals_tmp, c->ss.hist, c->side_tiles,
                     c->sc.tile_sums, c->fres, c->mask, c->ranks, c->res_buf, c->counts, c->counters, c->status,
                     c->f_gtab, c->f_gpos, c->f_keys, c->f_rows,
-                    c->f_tile_idr, c->rt_ts_buf, c->rt_ctl_buf, c->rt_dry_ts, c->q_key, c->q_val, c->q_tkey,
+                    c->f_tile_idr, c->rt_ts_buf, c->rt_ctl_buf, c->rt_dry_ts, c->pc, c->rg_part, c->T.base, c->q_key, c->q_val, c->q_tkey,
                     c->q_tval, c->q_ss.keys_tmp, c->q_ss.vals_tmp, c->q_ss.hist, c->q_runs_dev, c->ximp};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     for (EvalState& s : c->st) {
@@ -302,6 +346,9 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     if (c->h_counts) (void)hipHostFree(c->h_counts);
     if (c->h_stage_ts) (void)hipHostFree(c->h_stage_ts);
     if (c->h_stage_start) (void)hipHostFree(c->h_stage_start);
+    if (c->h_pc) (void)hipHostFree(c->h_pc);
+    if (c->h_base) (void)hipHostFree(c->h_base);
+    if (c->h_rc) (void)hipHostFree(c->h_rc);
     for (hipEvent_t e : c->prof_pool) (void)hipEventDestroy(e);
     (void)hipEventDestroy(c->ev0);
     (void)hipEventDestroy(c->ev1);
@@ -314,6 +361,29 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
 static void read_counters(tbgpu_ctx* c) {
     HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, CNT_COUNT * sizeof(u32), hipMemcpyDeviceToHost, c->stream));
     HIP_CHECK(hipStreamSynchronize(c->stream));
+}
+
+// Host copies of the device cursors (stored rows, history rows), exact for all work
+// enqueued so far.  One round trip.
+static void refresh_bases(tbgpu_ctx* c) {
+    HIP_CHECK(hipMemcpyAsync(c->h_base, c->T.base, 4 * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(hipStreamSynchronize(c->stream));
+    c->n_rows = c->h_base[BASE_ROWS];
+    c->n_hist = c->h_base[BASE_HIST];
+    c->rows_hi = c->n_rows;
+}
+
+static void set_base(tbgpu_ctx* c, int k, u64 v) {
+    c->h_base[3] = v;  // staged through pinned memory (async copy), then waited for
+    HIP_CHECK(hipMemcpyAsync(c->T.base + k, c->h_base + 3, sizeof(u64), hipMemcpyHostToDevice, c->stream));
+    HIP_CHECK(hipStreamSynchronize(c->stream));
+}
+
+static void ensure_h_rc(tbgpu_ctx* c, u64 nb) {
+    if (nb <= c->h_rc_cap) return;
+    if (c->h_rc) HIP_CHECK(hipHostFree(c->h_rc));
+    c->h_rc_cap = std::max<u64>(nb, 1024);
+    HIP_CHECK(hipHostMalloc((void**)&c->h_rc, c->h_rc_cap * sizeof(u32), hipHostMallocDefault));
 }
 
 // Splits batches [b0, b_end) into chunks of whole batches of <= nmax events.
@@ -348,15 +418,14 @@ static void upload_batches(tbgpu_ctx* c, const uint64_t* timestamps, const uint3
 }
 
 // Device replies are concatenated across the chunk's batches; the host C-ABI
-// places batch b's reply at the batch's event offset.
+// places batch b's reply at the batch's event offset.  (The chunk is complete.)
 static void copy_results_to_batches(tbgpu_ctx* c, u32 nb, const std::vector<u32>& starts, const u32* counts,
                                     u8* dst_chunk) {
     u64 total = 0;
     for (u32 b = 0; b < nb; b++) total += counts[b];
     if (total == 0) return;
     std::vector<u8> tmp(total * 8);
-    HIP_CHECK(hipMemcpyAsync(tmp.data(), c->res_buf, total * 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_CHECK(hipStreamSynchronize(c->stream));
+    HIP_CHECK(hipMemcpy(tmp.data(), c->res_buf, total * 8, hipMemcpyDeviceToHost));
     u64 off = 0;
     for (u32 b = 0; b < nb; b++) {
         memcpy(dst_chunk + (u64)starts[b] * 8, tmp.data() + off * 8, (u64)counts[b] * 8);
@@ -371,9 +440,12 @@ static TrArgs make_tr_args(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb) {
     C.ts = c->ts; C.cs = c->cs; C.ce = c->ce; C.sres = c->sres;
     C.dslot = c->dslot; C.cslot = c->cslot; C.pre_e = c->pre_e; C.pre_p = c->pre_p;
     C.pp_dslot = c->pp_dslot; C.pp_cslot = c->pp_cslot; C.gslot = c->gslot; C.pslot = c->pslot;
-    C.prev_id = c->prev_id; C.pend_last = c->pend_last; C.prev_pend = c->prev_pend;
+    C.prev_id = c->prev_id; C.pend_last = c->pend_last; C.pend_first = c->pend_first; C.prev_pend = c->prev_pend;
     C.gclaim = c->gclaim; C.gcnt_id = c->gcnt_id; C.gcnt_pd = c->gcnt_pd; C.gmem = c->gmem;
-    C.gbeg = c->gbeg; C.gend = c->gend; C.gmembers = c->sval_s;
+    C.gbeg = c->gbeg; C.gend = c->gend; C.gmembers = c->gsorted;
+    C.sd.soff = c->soff; C.sd.sev = c->sev; C.sd.scand = c->scand; C.sd.spos = c->spos; C.sd.skey_s = c->skey_s;
+    C.sd.sq_ev = c->sq_ev; C.sd.sq_cs = c->sq_cs; C.sd.sq_ok = c->sq_ok; C.sd.sq_dpend = c->sq_dpend;
+    C.sd.sq_dpost = c->sq_dpost;
     // group table sized for this call: >= 2x the keys (ids + pending ids <= 2n)
     const u64 g = std::min<u64>(c->gcap, pow2_at_least(4ull * std::max<u32>(n, 1)));
     C.gmask = g - 1;
@@ -382,14 +454,20 @@ static TrArgs make_tr_args(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb) {
     C.ctl = c->rt_ctl;
     C.dry = c->rt_dry ? 1u : 0u;
     C.commit_ts = c->rt_dry ? c->rt_dry_ts : c->T.commit_ts;
+    static const bool debug = getenv("TBGPU_TRACE_PASSES") != nullptr;  // diagnostics only
+    C.debug = debug ? 1u : 0u;
     return C;
 }
 
 // Single-pass attempt (fast.hip).  Returns false, with every balance delta
-// undone, when some event needs the fixed point.
-static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_create_transfers_result_t* results_dev,
-                     u32* counts_host) {
+// undone, when some event needs the fixed point.  Replies go after the device
+// reply cursor; `counts_dev` receives the per-batch reply counts.
+static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_create_transfers_result_t* results_dev) {
     hipStream_t s = c->stream;
+    if (c->rows_hi + n > c->xrow_cap) {
+        refresh_bases(c);  // the bound is loose: look at the exact count
+        if (c->n_rows + n > c->xrow_cap) return false;  // let the general path report capacity exactly
+    }
     FastArgs F{};
     F.ev = ev; F.n = n; F.nb = nb; F.b_start = c->b_start; F.b_ts = c->b_ts; F.ev_ts = c->rt_ev_ts;
     F.gtab = c->f_gtab;
@@ -399,7 +477,7 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_crea
     F.counters = c->counters;
     F.batch_counts = c->counts;
     F.results = results_dev;
-    F.row_base = c->n_rows;
+    F.row_base = c->rows_hi;
     F.keys = c->f_keys;
     F.rows = c->f_rows;
     F.tile_idr = c->f_tile_idr;
@@ -412,7 +490,6 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_crea
         return e ? (u32)strtoul(e, nullptr, 0) : 0u;
     }();
     F.ablate = ablate;
-    if (c->n_rows + n > c->xrow_cap) return false;  // let the general path report capacity exactly
     prof_mark(c, PH_PREP);
     fp_launch_prep(F, s);
     prof_mark(c, PH_CLASSIFY);
@@ -420,9 +497,8 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_crea
     prof_mark(c, PH_INDEX);
     fp_launch_index(c->T, F, s);
     prof_mark(c, PH_END);
-    // one round trip: the flags decide whether the reply counts are valid
+    // one round trip: the flags decide whether the attempt stands
     HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, CNT_COUNT * sizeof(u32), hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipMemcpyAsync(c->h_counts, c->counts, nb * sizeof(u32), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     const u32 flags = c->h_counters[CNT_FLAGS];
     if (flags & FL_ERROR) tbgpu_fatal("create_transfers", "fast path look-back did not complete", __FILE__, __LINE__);
@@ -435,118 +511,164 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_crea
         prof_mark(c, PH_APPLY);
         fp_launch_fix(c->T, F, c->mask, c->ranks, c->sc, s);
         prof_mark(c, PH_END);
-        HIP_CHECK(hipStreamSynchronize(s));
     }
-    memcpy(counts_host, c->h_counts, nb * sizeof(u32));
-    if (!F.dry) c->n_rows += c->h_counters[CNT_OK];
+    fp_launch_advance(c->T, F, s);
+    if (!F.dry) c->rows_hi += c->h_counters[CNT_OK];
     c->stats.path = 1;
     c->stats.iterations = 1;
     return true;
 }
 
-// One chunk of create_transfers: events already at `ev` on the device.
-// Returns false (nothing committed, every effect undone) when the fast path does
-// not apply and `split` asks the caller to redo these batches in smaller chunks.
-static bool run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
-                                tbgpu_create_transfers_result_t* results_dev, u32* counts_host, bool try_fast_path,
-                                bool split) {
+// The general path's fixed point over one chunk (transfers.hip): classify, group,
+// the optimistic initial state, then Jacobi passes enqueued in groups without a
+// host round trip inside a group (the kernels of the passes after convergence
+// return at once), until a pass changes nothing.  Returns the converged state.
+static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n) {
     hipStream_t s = c->stream;
-    TrArgs C = make_tr_args(c, ev, n, nb);
     const u64 g = C.gmask + 1;
     const u32 inv_acc = (u32)c->accounts_max;  // side keys are account rows
     const int bits_acc = log2u(c->accounts_max + 1);
     const u32 inv_g = (u32)g;
     const int bits_g = log2u(g + 1);
+
+    u32* chg = c->pc;
+    u32* front = c->pc + PC_RING;
+    prof_mark(c, PH_CLASSIFY);
+    tr_launch_prep(C, c->st[0].cfail, c->pc, PC_RING, s);
+    tr_launch_classify(c->T, C, s);
+    // grouping by id / pending id: each step runs only when classify found the need
+    tr_launch_group_sort(C, 0, inv_g, bits_g, c->skey, c->sval, c->gkey_s, c->gsorted, c->ss, s);
+    tr_launch_group2(C, s);
+    tr_launch_group_sort(C, 1, inv_g, bits_g, c->skey, c->sval, c->skey_s, c->sval_s, c->ss, s);
+    tr_launch_init(c->T, C, c->st[0], s);
+
+    // The sides of the events, sorted by account (one host round trip: their count).
+    u64 m = 0;
+    auto build_sides = [&](const EvalState& S) {
+        prof_mark(c, PH_SORT);
+        for (u32 kmax : {SIDE_CANDS, 1u}) {
+            tr_launch_side_count(C, S, kmax, c->mask, s);
+            scan3_exclusive(c->mask, c->ranks, n, c->sc, s);
+            uint4 tot;
+            HIP_CHECK(hipMemcpyAsync(c->h_base + 4, c->ranks + n, sizeof(uint4), hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+            memcpy(&tot, c->h_base + 4, sizeof tot);
+            m = 2ull * (tot.x + tot.y + tot.z);
+            if (m <= c->scap) {
+                tr_launch_side_build(C, S, kmax, c->ranks, inv_acc, c->skey, c->sval, s);
+                break;
+            }
+        }
+        if (m > c->scap) tbgpu_fatal("create_transfers", "side capacity", __FILE__, __LINE__);
+        radix_sort_pairs(c->skey, c->sval, c->skey_s, c->sval_s, m, bits_acc, c->ss, s);
+        tr_launch_side_pos(C, c->sval_s, m, s);
+        tr_launch_side_rec(C, S, s);
+        c->stats.sorts++;
+    };
+    build_sides(c->st[0]);
+
+    SideScanArgs SA{};
+    SA.skey = c->skey_s; SA.sq_ev = c->sq_ev; SA.sq_cs = c->sq_cs; SA.sq_ok = c->sq_ok;
+    SA.sq_dpend = c->sq_dpend; SA.sq_dpost = c->sq_dpost; SA.n = n;
+    const bool chains = true;  // whether the call has chains is on the device: scan with the chain part
+    u32 p = 0;                  // next pass to enqueue
+    u32 group = std::max<u32>(2, std::min<u32>(c->last_passes, PASS_GROUP_MAX));
+    u32 done_at = NONE32;
+    for (;;) {
+        if (p > n + 2 + PC_RING) tbgpu_fatal("create_transfers", "fixed point did not converge", __FILE__, __LINE__);
+        prof_mark(c, PH_EVAL);  // the passes: balance scan + evaluation
+        for (u32 q = p; q < p + group; q++) {
+            EvalState& S = c->st[q & 1];
+            EvalState& D = c->st[(q + 1) & 1];
+            PassGate G{chg + q % PC_RING, c->counters + CNT_RESORT, q};
+            SA.cfail = S.cfail;
+            SA.cfail_clear = D.cfail;
+            SA.gate = G;
+            side_scan(SA, m, inv_acc, chains, c->side_tiles, c->T.acc, c->bb, s);
+            tr_launch_evaluate(c->T, C, S, D, c->bb, G, chg + (q + 1) % PC_RING, front + (q + 1) % PC_RING,
+                               chg + (q + 2) % PC_RING, front + (q + 2) % PC_RING, s);
+        }
+        const u32 p0 = p;
+        p += group;
+        prof_mark(c, PH_END);
+        HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, CNT_COUNT * sizeof(u32), hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipMemcpyAsync(c->h_pc, chg, PC_RING * sizeof(u32), hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        if (c->h_counters[CNT_FLAGS] & FL_ERROR) tbgpu_fatal("create_transfers", "device error", __FILE__, __LINE__);
+        static const bool trace = getenv("TBGPU_TRACE_PASSES") != nullptr;  // diagnostics only
+        if (trace) {
+            for (u32 q = p0; q < p; q++)
+                fprintf(stderr, "tbgpu: n=%u pass %u changes %u\n", n, q, c->h_pc[(q + 1) % PC_RING]);
+            const u32* d = c->h_counters + CNT_DBG;
+            fprintf(stderr, "tbgpu: changed so far: regular %u balancing %u post/void %u; result changed %u, "
+                            "chain members %u, limit accounts %u; resort %u\n", d[0], d[1], d[2], d[3], d[4], d[5],
+                    c->h_counters[CNT_RESORT]);
+        }
+        const u32 resort = c->h_counters[CNT_RESORT];
+        if (resort) {
+            // eval r resolved a post/void to a pending outside its sides: rebuild the
+            // sides from its state (its resolution is then a candidate), go on at r + 1
+            const u32 r = resort - 1;
+            build_sides(c->st[(r + 1) & 1]);
+            HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)(c->counters + CNT_RESORT), 0, 1, s));
+            HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)(chg + (r + 1) % PC_RING), 1, 1, s));
+            p = r + 1;
+            continue;
+        }
+        for (u32 q = p0; q < p; q++)
+            if (c->h_pc[(q + 1) % PC_RING] == 0) { done_at = q; break; }
+        if (done_at != NONE32) break;
+        // the changes decay about geometrically: enqueue the passes that decay predicts
+        const double last = c->h_pc[p % PC_RING], prev = c->h_pc[(p - 1) % PC_RING];
+        const double r = prev > 0 ? std::min(0.9, std::max(0.05, last / prev)) : 0.5;
+        group = (u32)std::ceil(std::log(last + 1.0) / -std::log(r)) + 1;
+        group = std::max<u32>(2, std::min<u32>(group, PASS_GROUP_MAX));
+    }
+    c->stats.iterations = done_at + 1;
+    c->last_passes = done_at + 1;
+    c->side_m = m;
+    return &c->st[(done_at + 1) & 1];
+}
+
+// One chunk of create_transfers: events already at `ev` on the device.  Replies go
+// to `results_dev` after the device reply cursor, per-batch reply counts to c->counts.
+// Returns false (nothing committed, every effect undone) when the fast path does
+// not apply and `split` asks the caller to redo these batches in smaller chunks.
+static bool run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
+                                tbgpu_create_transfers_result_t* results_dev, bool try_fast_path, bool split) {
+    hipStream_t s = c->stream;
     c->stats.iterations = 0;
-    c->stats.sorts = 0;
     c->stats.path = 0;
     if (n == 0) {
-        std::fill(counts_host, counts_host + nb, 0u);
+        HIP_CHECK(hipMemsetAsync(c->counts, 0, nb * sizeof(u32), s));
         return true;
     }
     const bool fast_ok = try_fast_path && !(c->opt.flags & TBGPU_OPT_FORCE_GENERAL);
     if (fast_ok) {
-        if (try_fast(c, ev, n, nb, results_dev, counts_host)) {
+        if (try_fast(c, ev, n, nb, results_dev)) {
             c->slow_chunks = 0;
             return true;
         }
         if (split) return false;
     }
     c->slow_chunks++;
-    prof_mark(c, PH_CLASSIFY);
-    HIP_CHECK(hipMemsetAsync(c->counters, 0, CNT_COUNT * sizeof(u32), s));
-    HIP_CHECK(hipMemsetAsync(c->gclaim, 0, g * sizeof(u32), s));
-    HIP_CHECK(hipMemsetAsync(c->gcnt_id, 0, g * sizeof(u32), s));
-    HIP_CHECK(hipMemsetAsync(c->gcnt_pd, 0, g * sizeof(u32), s));
-    tr_launch_classify(c->T, C, s);
-    read_counters(c);
-    const u32 flags = c->h_counters[CNT_FLAGS];
-    if (flags & FL_MULTI_ID) {
-        tr_launch_group_sort(C, 0, inv_g, bits_g, c->skey, c->sval, c->skey_s, c->sval_s, c->ss, s);
-        c->stats.sorts++;
-    }
-    if (flags & FL_POSTVOID) tr_launch_group2(C, s);
-    if (flags & FL_MULTI_PEND) {
-        tr_launch_group_sort(C, 1, inv_g, bits_g, c->skey, c->sval, c->skey_s, c->sval_s, c->ss, s);
-        c->stats.sorts++;
-    }
-    const bool chains = flags & FL_CHAINS;
-    const bool keys_dynamic = flags & FL_POSTVOID;
+    TrArgs C = make_tr_args(c, ev, n, nb);
+    EvalState* A = fixed_point(c, C, n);
 
-    EvalState* A = &c->st[0];
-    EvalState* Bst = &c->st[1];
-    HIP_CHECK(hipMemsetAsync(A->cfail, 0xFF, n * sizeof(u32), s));
-    tr_launch_init(c->T, C, *A, s);
-
-    const u64 m = 2ull * n;
-    SideScanArgs SA{};
-    SA.skey = c->skey_s; SA.sval = c->sval_s; SA.cs = c->cs;
-    u32 it = 0;
-    for (;; it++) {
-        if (it > n + 2) tbgpu_fatal("create_transfers", "fixed point did not converge", __FILE__, __LINE__);
-        HIP_CHECK(hipMemsetAsync(c->counters + CNT_CHANGES, 0, 2 * sizeof(u32), s));
-        tr_launch_sides(C, *A, inv_acc, c->skey, c->sval, s);
-        bool sort = it == 0;
-        if (!sort && keys_dynamic) {
-            read_counters(c);
-            sort = c->h_counters[CNT_KEYS] != 0;
-        }
-        if (sort) {
-            prof_mark(c, PH_SORT);
-            radix_sort_pairs(c->skey, c->sval, c->skey_s, c->sval_s, m, bits_acc, c->ss, s);
-            tr_launch_side_pos(c->sval_s, m, c->spos, s);
-            c->stats.sorts++;
-        }
-        prof_mark(c, PH_SCAN);
-        SA.ok = A->ok; SA.dpend = A->dpend; SA.dpost = A->dpost;
-        side_scan(SA, m, inv_acc, chains, c->side_tiles, c->T.acc, c->bb, s);
-        prof_mark(c, PH_EVAL);
-        HIP_CHECK(hipMemsetAsync(Bst->cfail, 0xFF, n * sizeof(u32), s));
-        tr_launch_evaluate(c->T, C, *A, *Bst, c->spos, c->bb, s);
-        read_counters(c);
-        std::swap(A, Bst);
-        if (c->h_counters[CNT_CHANGES] == 0) break;
-    }
-    c->stats.iterations = it + 1;
-
-    // apply: ranks of stored rows / results / history rows
+    // apply: ranks of stored rows / results / history rows, at the device cursors
     prof_mark(c, PH_APPLY);
     tr_launch_mask(c->T, C, *A, c->fres, c->mask, s);
     scan3_exclusive(c->mask, c->ranks, n, c->sc, s);
-    uint4 tot;
-    HIP_CHECK(hipMemcpyAsync(&tot, c->ranks + n, sizeof(uint4), hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
-    if (c->n_rows + tot.x > c->xrow_cap) tbgpu_fatal("create_transfers", "transfers_max exceeded", __FILE__, __LINE__);
-    if (c->n_hist + tot.z > c->hist_cap) tbgpu_fatal("create_transfers", "history_max exceeded", __FILE__, __LINE__);
-    SA.ok = A->ok; SA.dpend = A->dpend; SA.dpost = A->dpost;
-    tr_launch_apply(c->T, C, *A, c->fres, c->ranks, c->spos, c->bb, c->n_rows, c->n_hist, results_dev, c->counts, s);
-    if (!c->rt_dry) side_final_balances(SA, m, inv_acc, c->bb, c->T.acc, c->T.big, s);
+    tr_launch_apply(c->T, C, *A, c->fres, c->ranks, c->bb, results_dev, c->counts, c->rg_part, s);
+    if (!c->rt_dry) {
+        SideScanArgs SA{};
+        SA.skey = c->skey_s; SA.sq_ev = c->sq_ev; SA.sq_cs = c->sq_cs; SA.sq_ok = c->sq_ok;
+        SA.sq_dpend = c->sq_dpend; SA.sq_dpost = c->sq_dpost; SA.cfail = A->cfail; SA.n = n;
+        side_final_balances(SA, c->side_m, (u32)c->accounts_max, c->bb, c->T.acc, c->T.big, s);
+    }
+    tr_launch_advance(c->T, C, c->ranks, c->rg_part, s);
     prof_mark(c, PH_END);
-    HIP_CHECK(hipMemcpyAsync(counts_host, c->counts, nb * sizeof(u32), hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
-    if (c->rt_dry) return true;
-    c->n_rows += tot.x;
-    c->n_hist += tot.z;
+    if (!c->rt_dry) c->rows_hi += n;
     return true;
 }
 
@@ -556,11 +678,14 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
                                   const uint8_t* ctl_host = nullptr, bool routed_device = false) {
     HIP_CHECK(hipSetDevice(c->device));
     HIP_CHECK(hipEventRecord(c->ev0, c->stream));
+    ensure_h_rc(c, nb_total);
     std::vector<u32> starts;
-    u64 total = 0, ev_off = 0, events = 0;
+    u64 ev_off = 0, events = 0;
     u32 iters = 0;
     u64 sorts = 0;
+    c->stats.sorts = 0;
     u32 small_until = 0;  // batches before this one go in general-path-sized chunks
+    set_base(c, BASE_REPLIES, 0);  // the call's replies start at the front of `results`
     for (u32 b0 = 0; b0 < nb_total;) {
         // After a call needed the fixed point, the next ones probably do too: small
         // chunks, and the fast attempt only every 8th (it undoes itself when it fails).
@@ -594,19 +719,25 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
                 c->rt_ctl = c->rt_ctl_buf;
             }
         }
-        tbgpu_create_transfers_result_t* rdev =
-            dst_device ? results + total : (tbgpu_create_transfers_result_t*)c->res_buf;
+        // device results: the call's buffer (cursor-relative); host results: staged in
+        // res_buf one chunk at a time
+        if (!dst_device) set_base(c, BASE_REPLIES, 0);
+        tbgpu_create_transfers_result_t* rdev = dst_device ? results : (tbgpu_create_transfers_result_t*)c->res_buf;
         const bool try_fast_path = c->slow_chunks % 8 == 0;
-        if (!run_transfers_chunk(c, ev, n, nb, rdev, result_counts + b0, try_fast_path,
+        if (!run_transfers_chunk(c, ev, n, nb, rdev, try_fast_path,
                                  /*split=*/!c->rt_dry && nb > GENERAL_CHUNK_BATCHES)) {
             small_until = b1;  // redo these batches in small chunks, on the general path
             c->slow_chunks = 1;
             continue;
         }
-        if (!dst_device) copy_results_to_batches(c, nb, starts, result_counts + b0, (u8*)(results + ev_off));
-        for (u32 b = 0; b < nb; b++) total += result_counts[b0 + b];
+        HIP_CHECK(hipMemcpyAsync(c->h_rc + b0, c->counts, nb * sizeof(u32), hipMemcpyDeviceToHost, c->stream));
+        if (!dst_device) {
+            HIP_CHECK(hipStreamSynchronize(c->stream));
+            copy_results_to_batches(c, nb, starts, c->h_rc + b0, (u8*)(results + ev_off));
+        }
         iters = std::max(iters, c->stats.iterations);
         sorts += c->stats.sorts;
+        c->stats.sorts = 0;
         ev_off += n;
         events += n;
         b0 = b1;
@@ -615,6 +746,10 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
     HIP_CHECK(hipEventSynchronize(c->ev1));
     float ms = 0;
     HIP_CHECK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    refresh_bases(c);
+    u64 total = 0;
+    for (u32 b = 0; b < nb_total; b++) total += c->h_rc[b];
+    memcpy(result_counts, c->h_rc, nb_total * sizeof(u32));
     prof_collect(c);
     c->stats.events = events;
     c->stats.iterations = iters;
@@ -689,6 +824,7 @@ extern "C" int tbgpu_import_transfers(tbgpu_ctx* c, const tbgpu_transfer_t* rows
         if (!dup) keep.push_back(rows[i]);
     }
     const u64 n = keep.size();
+    refresh_bases(c);
     if (c->n_rows + n > c->xrow_cap) tbgpu_fatal("import_transfers", "transfers_max exceeded", __FILE__, __LINE__);
     u64 off = 0;
     while (off < n) {
@@ -704,6 +840,8 @@ extern "C" int tbgpu_import_transfers(tbgpu_ctx* c, const tbgpu_transfer_t* rows
         c->n_rows += k;
         off += k;
     }
+    set_base(c, BASE_ROWS, c->n_rows);
+    c->rows_hi = c->n_rows;
     return 0;
 }
 
@@ -1045,6 +1183,9 @@ extern "C" int tbgpu_open(tbgpu_ctx* c, const void* image, uint64_t size) {
     c->n_accounts = na;
     c->n_rows = nr;
     c->n_hist = nh;
+    c->rows_hi = nr;
+    set_base(c, BASE_ROWS, nr);
+    set_base(c, BASE_HIST, nh);
     return 0;
 }
 

@@ -16,7 +16,7 @@ struct FastArgs {
     u32* counters;
     u32* batch_counts;  // failures per batch
     tbgpu_create_transfers_result_t* results;  // replies, concatenated across batches
-    u64 row_base;
+    u64 row_base;       // host copy of T.base[BASE_ROWS] (timing ablations only; kernels read T.base)
     u128* keys;         // accepted ids, for fp_index
     u32* rows;          // stored row per accepted event (written by fp_fix only)
     u64* tile_idr;      // per tile (TILE_WORDS): componentwise max lo, max hi, min lo, min hi of the
@@ -35,4 +35,5 @@ void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream);
 void fp_launch_index(const Tables& T, const FastArgs& F, hipStream_t stream);
 void fp_launch_fix(const Tables& T, const FastArgs& F, u8* mask, uint4* ranks, Scan3Scratch& sc, hipStream_t stream);
 void fp_launch_undo(const Tables& T, const FastArgs& F, hipStream_t stream);
+void fp_launch_advance(const Tables& T, const FastArgs& F, hipStream_t stream);
 u64 fp_tiles(u64 n);

@@ -299,6 +299,7 @@ void fp_commit(Tables T, FastArgs F) {
     const u32 i = tile * FP_THREADS + tid;
     const bool valid = i < F.n;
     const u32 wbase = tile * FP_THREADS + wave * 64;
+    const u64 row_base = T.base[BASE_ROWS];  // device cursor: no host round trip between calls
 #if defined(FP_LDS_EVENTS)
     // The wave's 64 events as coalesced 16-byte loads (lane k of load j holds chunk
     // (j*64 + k) of the wave's span), issued before the table init and the scalar
@@ -405,7 +406,7 @@ void fp_commit(Tables T, FastArgs F) {
     const bool member = lk || plk || (myctl & TBGPU_CTL_DOOM);
     if (__ballot(member) && lane == 0) atomicOr(&F.counters[CNT_FLAGS], (u32)FL_FCHAIN);
     bool own_ok = false;
-#define STORE_ROW() do { if (!(F.ablate & ABL_ROWS)) T.xrows[F.row_base + i] = t; } while (0)
+#define STORE_ROW() do { if (!(F.ablate & ABL_ROWS)) T.xrows[row_base + i] = t; } while (0)
     if (valid) {
         id = t.id;
         u32 ds = NONE32, cs = NONE32;
@@ -623,7 +624,7 @@ __global__ void fp_index(Tables T, FastArgs F, bool fixed) {
     }
     if (i >= F.n) return;
     if (F.fres[i] != TBGPU_CREATE_TRANSFER_OK) return;
-    xidx_insert(T, F.keys[i], fixed ? F.rows[i] : (u32)(F.row_base + i));
+    xidx_insert(T, F.keys[i], fixed ? F.rows[i] : (u32)(T.base[BASE_ROWS] + i));
 }
 
 __device__ __forceinline__ bool fp_linked(const FastArgs& F, u32 j) {
@@ -744,14 +745,21 @@ __global__ void fp_fix(FastArgs F, Tables T, const uint4* rk) {
     const u32 bs = F.b_start[b];
     const u8 r = F.fres[i];
     if (r != TBGPU_CREATE_TRANSFER_OK) {
-        F.results[rk[i].y] = {i - bs, (u32)r};  // concatenated replies
+        F.results[T.base[BASE_REPLIES] + rk[i].y] = {i - bs, (u32)r};  // concatenated replies
         return;
     }
-    const u32 row = (u32)(F.row_base + rk[i].x);
+    const u32 row = (u32)(T.base[BASE_ROWS] + rk[i].x);
     Transfer t = F.ev[i];
     t.timestamp = F.ev_ts ? F.ev_ts[i] : F.b_ts[b] - (F.b_start[b + 1] - bs) + (i - bs) + 1;
     T.xrows[row] = t;
     F.rows[i] = row;
+}
+
+// After an accepted attempt: advance the device cursors by its stored rows and replies.
+__global__ void fp_advance(Tables T, FastArgs F) {
+    if (threadIdx.x != 0) return;
+    T.base[BASE_REPLIES] += F.counters[CNT_BAD];
+    if (!F.dry) T.base[BASE_ROWS] += F.counters[CNT_OK];
 }
 
 // Per-call reset of the fast path's counters and reply counts, and a copy of
@@ -814,6 +822,11 @@ void fp_launch_fix(const Tables& T, const FastArgs& F, u8* mask, uint4* ranks, S
     scan3_exclusive(mask, ranks, F.n, sc, stream);
     fp_fix<<<GRID(F.n)>>>(F, T, ranks);
     if (!F.dry) fp_index<<<GRID(F.n)>>>(T, F, true);
+    HIP_CHECK(hipGetLastError());
+}
+
+void fp_launch_advance(const Tables& T, const FastArgs& F, hipStream_t stream) {
+    fp_advance<<<1, 64, 0, stream>>>(T, F);
     HIP_CHECK(hipGetLastError());
 }
 

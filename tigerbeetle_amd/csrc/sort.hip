@@ -14,8 +14,13 @@ constexpr int RS_IPT = 8;
 constexpr int RS_TILE = RS_THREADS * RS_IPT;  // 2048 items per workgroup
 constexpr int RS_WAVES = RS_THREADS / 64;
 
+// A sort may be predicated on a device word (pred & mask != 0), so that the host
+// enqueues it without knowing whether it is needed.
+__device__ __forceinline__ bool rs_off(const u32* pred, u32 mask) { return pred && !(*pred & mask); }
+
 __global__ __launch_bounds__(RS_THREADS) void rs_hist(const u32* __restrict__ keys, u64 n, int shift,
-                                                      u32* __restrict__ hist, u32 nblocks) {
+                                                      u32* __restrict__ hist, u32 nblocks, const u32* pred, u32 pmask) {
+    if (rs_off(pred, pmask)) return;
     __shared__ u32 cnt[256];
     const u32 tid = threadIdx.x;
     cnt[tid] = 0;
@@ -30,29 +35,39 @@ __global__ __launch_bounds__(RS_THREADS) void rs_hist(const u32* __restrict__ ke
     hist[(u64)tid * nblocks + blockIdx.x] = cnt[tid];
 }
 
-// Exclusive scan of `total` u32 words in place, one workgroup of 1024 threads.
-__global__ __launch_bounds__(1024) void rs_scan(u32* __restrict__ data, u64 total) {
-    __shared__ u32 sums[1024];
-    const u32 tid = threadIdx.x;
-    const u64 chunk = (total + 1023) / 1024;
-    const u64 lo = (u64)tid * chunk;
-    const u64 hi = lo + chunk < total ? lo + chunk : total;
-    u32 s = 0;
-    for (u64 i = lo; i < hi; i++) s += data[i];
-    sums[tid] = s;
-    __syncthreads();
-    // Hillis-Steele inclusive scan over 1024 partial sums
-    for (u32 off = 1; off < 1024; off <<= 1) {
-        u32 v = tid >= off ? sums[tid - off] : 0;
+// Exclusive scan of `total` u32 words in place (total is a multiple of 256), one
+// workgroup of 1024 threads sweeping tiles of 4096 words with coalesced 16-byte
+// loads: wave scans by shuffles, the 16 wave sums through LDS, a running carry.
+__global__ __launch_bounds__(1024) void rs_scan(u32* __restrict__ data, u64 total, const u32* pred, u32 pmask) {
+    if (rs_off(pred, pmask)) return;
+    __shared__ u32 wsum[16];
+    const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    u32 carry = 0;
+    for (u64 base = 0; base < total; base += 4096) {
+        const u64 k = base + (u64)tid * 4;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (k < total) v = *(const uint4*)(data + k);
+        const u32 s = v.x + v.y + v.z + v.w;
+        u32 x = s;  // inclusive scan over the wave
+        for (int off = 1; off < 64; off <<= 1) {
+            const u32 y = __shfl_up(x, off);
+            if (lane >= (u32)off) x += y;
+        }
+        if (lane == 63) wsum[wave] = x;
         __syncthreads();
-        sums[tid] += v;
+        if (wave == 0) {
+            u32 t = lane < 16 ? wsum[lane] : 0;
+            for (int off = 1; off < 16; off <<= 1) {
+                const u32 y = __shfl_up(t, off);
+                if (lane >= (u32)off) t += y;
+            }
+            if (lane < 16) wsum[lane] = t;  // inclusive prefix of the wave sums
+        }
         __syncthreads();
-    }
-    u32 run = tid ? sums[tid - 1] : 0;
-    for (u64 i = lo; i < hi; i++) {
-        u32 v = data[i];
-        data[i] = run;
-        run += v;
+        const u32 excl = carry + (wave ? wsum[wave - 1] : 0) + x - s;
+        if (k < total) *(uint4*)(data + k) = make_uint4(excl, excl + v.x, excl + v.x + v.y, excl + v.x + v.y + v.z);
+        carry += wsum[15];
+        __syncthreads();
     }
 }
 
@@ -62,7 +77,9 @@ __global__ __launch_bounds__(1024) void rs_scan(u32* __restrict__ data, u64 tota
 __global__ __launch_bounds__(RS_THREADS) void rs_scatter(const u32* __restrict__ keys_in,
                                                          const u32* __restrict__ vals_in, u32* __restrict__ keys_out,
                                                          u32* __restrict__ vals_out, u64 n, int shift,
-                                                         const u32* __restrict__ hist, u32 nblocks) {
+                                                         const u32* __restrict__ hist, u32 nblocks,
+                                                         const u32* pred, u32 pmask) {
+    if (rs_off(pred, pmask)) return;
     __shared__ u32 run_base[256];
     __shared__ u32 wcnt[RS_WAVES][256];
     const u32 tid = threadIdx.x;
@@ -201,7 +218,7 @@ __global__ __launch_bounds__(SC_THREADS) void sc_down(const u8* __restrict__ mas
 u64 radix_sort_hist_words(u64 capacity) { return 256ull * ((capacity + RS_TILE - 1) / RS_TILE + 1); }
 
 void radix_sort_pairs(const u32* keys_in, const u32* vals_in, u32* keys_out, u32* vals_out, u64 n, int bits,
-                      SortScratch& s, hipStream_t stream) {
+                      SortScratch& s, hipStream_t stream, const u32* pred, u32 pred_mask) {
     if (n == 0) return;
     if (n > s.capacity) tbgpu_fatal("radix_sort_pairs", "n exceeds scratch capacity", __FILE__, __LINE__);
     const u32 nblocks = (u32)((n + RS_TILE - 1) / RS_TILE);
@@ -213,9 +230,9 @@ void radix_sort_pairs(const u32* keys_in, const u32* vals_in, u32* keys_out, u32
         u32* kd = to_out ? keys_out : s.keys_tmp;
         u32* vd = to_out ? vals_out : s.vals_tmp;
         const int shift = 8 * p;
-        rs_hist<<<nblocks, RS_THREADS, 0, stream>>>(ks, n, shift, s.hist, nblocks);
-        rs_scan<<<1, 1024, 0, stream>>>(s.hist, 256ull * nblocks);
-        rs_scatter<<<nblocks, RS_THREADS, 0, stream>>>(ks, vs, kd, vd, n, shift, s.hist, nblocks);
+        rs_hist<<<nblocks, RS_THREADS, 0, stream>>>(ks, n, shift, s.hist, nblocks, pred, pred_mask);
+        rs_scan<<<1, 1024, 0, stream>>>(s.hist, 256ull * nblocks, pred, pred_mask);
+        rs_scatter<<<nblocks, RS_THREADS, 0, stream>>>(ks, vs, kd, vd, n, shift, s.hist, nblocks, pred, pred_mask);
         ks = kd;
         vs = vd;
     }

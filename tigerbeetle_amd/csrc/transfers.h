@@ -26,6 +26,7 @@ struct TrArgs {
     u32* pslot;
     u32* prev_id;         // previous dynamic event with the same id
     u32* pend_last;       // last earlier dynamic event whose id == pending_id
+    u32* pend_first;      // first such event (the one that can succeed: the later ones repeat its id)
     u32* prev_pend;       // previous dynamic post/void with the same pending_id
     u32* gclaim;          // group table: claim words, member counts, ranges
     u32* gcnt_id;
@@ -36,6 +37,8 @@ struct TrArgs {
     const u32* gmembers;  // id-sorted members (valid when FL_MULTI_ID)
     u64 gmask;
     u32* counters;
+    u32 debug;            // diagnostics: count changed events by kind (TBGPU_TRACE_PASSES)
+    Sides sd;             // the account sides of the call's events (engine.h)
 };
 
 void tr_launch_classify(const Tables& T, const TrArgs& C, hipStream_t stream);
@@ -43,14 +46,20 @@ void tr_launch_group_sort(const TrArgs& C, u32 kind, u32 invalid, int bits, u32*
                           u32* v_out, SortScratch& ss, hipStream_t stream);
 void tr_launch_group2(const TrArgs& C, hipStream_t stream);
 void tr_launch_init(const Tables& T, const TrArgs& C, const EvalState& D, hipStream_t stream);
-void tr_launch_sides(const TrArgs& C, const EvalState& S, u32 invalid, u32* skey, u32* sval, hipStream_t stream);
-void tr_launch_side_pos(const u32* sval_s, u64 m, u32* spos, hipStream_t stream);
-void tr_launch_evaluate(const Tables& T, const TrArgs& C, const EvalState& S, const EvalState& D, const u32* spos,
-                        const Bal4* bb, hipStream_t stream);
+void tr_launch_side_count(const TrArgs& C, const EvalState& S, u32 kmax, u8* mask, hipStream_t stream);
+void tr_launch_side_build(const TrArgs& C, const EvalState& S, u32 kmax, const uint4* pairs, u32 invalid, u32* skey,
+                          u32* sval, hipStream_t stream);
+void tr_launch_side_pos(const TrArgs& C, const u32* sval_s, u64 m, hipStream_t stream);
+void tr_launch_side_rec(const TrArgs& C, const EvalState& S, hipStream_t stream);
+void tr_launch_evaluate(const Tables& T, const TrArgs& C, const EvalState& S, const EvalState& D, const Bal4* bb,
+                        const PassGate& g, u32* chg, u32* front, u32* chg_next, u32* front_next, hipStream_t stream);
 void tr_launch_mask(const Tables& T, const TrArgs& C, const EvalState& S, u8* fres, u8* mask, hipStream_t stream);
 void tr_launch_apply(const Tables& T, const TrArgs& C, const EvalState& S, const u8* fres, const uint4* rk,
-                     const u32* spos, const Bal4* bb, u64 row_base, u64 hist_base,
-                     tbgpu_create_transfers_result_t* results, u32* counts, hipStream_t stream);
+                     const Bal4* bb, tbgpu_create_transfers_result_t* results, u32* counts, u64* part,
+                     hipStream_t stream);
+void tr_launch_advance(const Tables& T, const TrArgs& C, const uint4* rk, const u64* part, hipStream_t stream);
+u64 tr_range_part_words(u64 n);
+void tr_launch_prep(const TrArgs& C, u32* cfail0, u32* pc, u32 ring, hipStream_t stream);
 
 // create_accounts (accounts.hip)
 struct AcArgs {

@@ -17,6 +17,8 @@
 // what depends on it (its accounts' later sides, same-id / same-pending events,
 // its linked chain).  Several batches of one call are one concatenated event
 // stream (chains never cross a batch, :1029), each with its own timestamps.
+#include <algorithm>
+
 #include "common.h"
 #include "engine.h"
 #include "transfers.h"
@@ -31,6 +33,21 @@ __device__ __forceinline__ u32 batch_of(const u32* __restrict__ b_start, u32 nb,
         if (b_start[mid] <= i) lo = mid; else hi = mid;
     }
     return lo;
+}
+
+// Wave-level reductions: one global atomic per wave instead of one per event (a
+// flag word or counter hit by every event serializes at the memory side).
+__device__ __forceinline__ u32 wave_or(u32 v) {
+    for (int off = 32; off > 0; off >>= 1) v |= __shfl_xor(v, off);
+    return v;
+}
+__device__ __forceinline__ u32 wave_min(u32 v) {
+    for (int off = 32; off > 0; off >>= 1) v = min(v, (u32)__shfl_xor(v, off));
+    return v;
+}
+__device__ __forceinline__ u64 wave_max64(u64 v) {
+    for (int off = 32; off > 0; off >>= 1) v = max(v, (u64)__shfl_xor((unsigned long long)v, off));
+    return v;
 }
 
 // Find-or-insert of a transfer id into the per-call group table.  A slot is
@@ -70,9 +87,7 @@ __device__ __forceinline__ u32 gtab_find(const TrArgs& C, u128 key) {
 // src/state_machine.zig:1239-1281 and :1398-1412), the timestamp and chain
 // bookkeeping of execute (:1018-1035), and the probes that replace prefetch
 // (:598-655): debit/credit account slots, pre-existing id, pending transfer.
-__global__ void tr_classify(Tables T, TrArgs C) {
-    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= C.n) return;
+__device__ __forceinline__ u32 classify_one(const Tables& T, const TrArgs& C, u32 i) {
     const u32 b = batch_of(C.b_start, C.nb, i);
     const u32 bs = C.b_start[b], be = C.b_start[b + 1];
     const u32 nbatch = be - bs, k = i - bs;
@@ -182,29 +197,43 @@ __global__ void tr_classify(Tables T, TrArgs C) {
     C.pslot[i] = pslot;
     C.prev_id[i] = NONE32;
     C.pend_last[i] = NONE32;
+    C.pend_first[i] = NONE32;
     C.prev_pend[i] = NONE32;
     if (gslot != NONE32) atomicAdd(&C.gcnt_id[gslot], 1u);
     if (pslot != NONE32) atomicAdd(&C.gcnt_pd[pslot], 1u);
-    if (fl) atomicOr(&C.counters[CNT_FLAGS], fl);
+    return fl;
+}
+
+__global__ void tr_classify(Tables T, TrArgs C) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    const u32 fl = wave_or(i < C.n ? classify_one(T, C, i) : 0u);
+    if ((threadIdx.x & 63) == 0 && fl) atomicOr(&C.counters[CNT_FLAGS], fl);
 }
 
 // Single-member id groups record their member; multi-member groups need a sort.
 __global__ void tr_group1(TrArgs C) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= C.n) return;
-    const u32 g = C.gslot[i];
-    if (g == NONE32) return;
     u32 fl = 0;
-    if (C.gcnt_id[g] == 1) C.gmem[g] = i; else fl |= FL_MULTI_ID;
-    const u32 p = C.pslot[i];
-    if (p != NONE32 && C.gcnt_pd[p] >= 2) fl |= FL_MULTI_PEND;
-    if (fl) atomicOr(&C.counters[CNT_FLAGS], fl);
+    const u32 g = i < C.n ? C.gslot[i] : NONE32;
+    if (g != NONE32) {
+        if (C.gcnt_id[g] == 1) C.gmem[g] = i; else fl |= FL_MULTI_ID;
+        const u32 p = C.pslot[i];
+        if (p != NONE32 && C.gcnt_pd[p] >= 2) fl |= FL_MULTI_PEND;
+    }
+    fl = wave_or(fl);
+    if ((threadIdx.x & 63) == 0 && fl) atomicOr(&C.counters[CNT_FLAGS], fl);
 }
 
 // Sort keys for grouping: events by id slot (kind 0) or post/voids by pending slot (kind 1).
+// The group kernels run only when classify found what they are for (the flag
+// word is on the device: no host round trip decides it).
+__device__ __forceinline__ bool need(const TrArgs& C, u32 kind) {
+    return C.counters[CNT_FLAGS] & (kind == 0 ? FL_MULTI_ID : FL_MULTI_PEND);
+}
+
 __global__ void tr_group_keys(TrArgs C, u32 kind, u32 invalid, u32* keys, u32* vals) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= C.n) return;
+    if (i >= C.n || !need(C, kind)) return;
     const u32 g = kind == 0 ? C.gslot[i] : C.pslot[i];
     keys[i] = g == NONE32 ? invalid : g;
     vals[i] = i;
@@ -213,7 +242,7 @@ __global__ void tr_group_keys(TrArgs C, u32 kind, u32 invalid, u32* keys, u32* v
 // Walk the id-sorted members: previous same-id event, and the group's range.
 __global__ void tr_group_ranges(TrArgs C, u32 invalid, const u32* ks, const u32* vs) {
     const u32 q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= C.n) return;
+    if (q >= C.n || !need(C, 0)) return;
     const u32 key = ks[q];
     if (key >= invalid) return;
     const u32 i = vs[q];
@@ -226,7 +255,7 @@ __global__ void tr_group_ranges(TrArgs C, u32 invalid, const u32* ks, const u32*
 
 __global__ void tr_pend_ranges(TrArgs C, u32 invalid, const u32* ks, const u32* vs) {
     const u32 q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= C.n) return;
+    if (q >= C.n || !need(C, 1)) return;
     const u32 key = ks[q];
     if (key >= invalid) return;
     C.prev_pend[vs[q]] = (q == 0 || ks[q - 1] != key) ? NONE32 : vs[q - 1];
@@ -235,23 +264,27 @@ __global__ void tr_pend_ranges(TrArgs C, u32 invalid, const u32* ks, const u32* 
 // Last in-call event j < i whose id is i's pending_id.
 __global__ void tr_group2(TrArgs C) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= C.n) return;
+    if (i >= C.n || !(C.counters[CNT_FLAGS] & FL_POSTVOID)) return;
     const u32 p = C.pslot[i];
     if (p == NONE32) return;
     const u32 c = C.gcnt_id[p];
-    u32 last = NONE32;
+    u32 last = NONE32, first = NONE32;
     if (c == 1) {
         const u32 j = C.gmem[p];
-        if (j < i) last = j;
+        if (j < i) last = first = j;
     } else if (c > 1) {
         u32 lo = C.gbeg[p], hi = C.gend[p];  // members sorted by index
         while (lo < hi) {
             const u32 mid = (lo + hi) >> 1;
             if (C.gmembers[mid] < i) lo = mid + 1; else hi = mid;
         }
-        if (lo > C.gbeg[p]) last = C.gmembers[lo - 1];
+        if (lo > C.gbeg[p]) {
+            last = C.gmembers[lo - 1];
+            first = C.gmembers[C.gbeg[p]];
+        }
     }
     C.pend_last[i] = last;
+    C.pend_first[i] = first;
 }
 
 // ---------------------------------------------------------- evaluation ----
@@ -376,16 +409,27 @@ __device__ __forceinline__ u8 eval_balances(const Transfer& t, const Bal4& dr, c
     return TBGPU_CREATE_TRANSFER_OK;
 }
 
+// What event j's effects look like to a later event of chain csi (execute's scopes,
+// src/state_machine.zig:1018-1083): evaluated inside the same open chain, final
+// (chain persisted) outside it.
 __device__ __forceinline__ bool visible(const TrArgs& C, const EvalState& S, u32 j, u32 csi) {
-    const u8 o = S.ok[j];
-    return C.cs[j] == csi ? (o & 1) : (o & 2);
+    if (C.cs[j] == csi) return S.ok[j] & 1;
+    return final_ok(C.cs, C.ce, S.cfail, C.ctl, S.ok, j);
+}
+__device__ __forceinline__ bool fin_ok(const TrArgs& C, const EvalState& S, u32 j) {
+    return final_ok(C.cs, C.ce, S.cfail, C.ctl, S.ok, j);
 }
 
-// One Jacobi pass: read state S (pass k-1), write state D (pass k).
-__global__ void tr_evaluate(Tables T, TrArgs C, EvalState S, EvalState D, const u32* __restrict__ spos,
-                            const Bal4* __restrict__ bb) {
-    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= C.n) return;
+// One Jacobi pass: read state S (pass k-1), write state D (pass k).  `chg` counts the
+// events whose outcome changed (the next pass's gate), `front` is the first of them
+// (everything before it is final: each event depends only on earlier ones).  An
+// accepted post/void whose balance effect sits under the wrong side keys (its
+// pending resolved to an event with other accounts) asks the host to re-sort.
+__device__ __forceinline__ bool write_sides(const TrArgs& C, u32 i, bool pv, bool ok, u32 pref, u128 dpe, u128 dpo);
+
+__device__ __forceinline__ bool evaluate_one(const Tables& T, const TrArgs& C, const EvalState& S,
+                                             const EvalState& D, const Bal4* __restrict__ bb, const PassGate& g,
+                                             u32 i) {
     const u8 sr = C.sres[i];
     u8 res;
     u128 amt = 0, pamt = 0, dpe = 0, dpo = 0;
@@ -404,8 +448,9 @@ __global__ void tr_evaluate(Tables T, TrArgs C, EvalState S, EvalState D, const 
             if (e != NONE32) {
                 res = create_transfer_exists(t, load_ref(T, C, S, e));
             } else {
-                const Bal4 bd = bb[spos[2 * i]];
-                const Bal4 bc = bb[spos[2 * i + 1]];
+                const u32 s0 = C.sd.soff[i];
+                const Bal4 bd = bb[C.sd.spos[s0]];
+                const Bal4 bc = bb[C.sd.spos[s0 + 1]];
                 const u16 dfl = T.acc[C.dslot[i]].flags, cfl = T.acc[C.cslot[i]].flags;
                 u128 amount = 0;
                 res = eval_balances(t, bd, bc, dfl, cfl, &amount);
@@ -468,14 +513,60 @@ __global__ void tr_evaluate(Tables T, TrArgs C, EvalState S, EvalState D, const 
     D.dpost[i] = dpo;
     if (res != TBGPU_CREATE_TRANSFER_OK && csi != C.ce[i]) atomicMin(&D.cfail[csi], i);
     const bool changed = res != S.res[i] || amt != S.amt[i] || pamt != S.pamt[i] || pref != S.pref[i];
-    if (changed) atomicAdd(&C.counters[CNT_CHANGES], 1u);
+    if (C.debug && changed) {
+        const u16 f = C.ev[i].flags;
+        const u32 kind = (f & (TF_POST | TF_VOID)) ? 2 : (f & (TF_BDR | TF_BCR)) ? 1 : 0;
+        atomicAdd(&C.counters[CNT_DBG + kind], 1u);
+        if (res != S.res[i]) atomicAdd(&C.counters[CNT_DBG + 3], 1u);
+        if (csi != C.ce[i]) atomicAdd(&C.counters[CNT_DBG + 4], 1u);
+        if (sr == SRES_DYN && !(f & (TF_POST | TF_VOID)) && (T.acc[C.dslot[i]].flags | T.acc[C.cslot[i]].flags) & (AF_DNEC | AF_CNED))
+            atomicAdd(&C.counters[CNT_DBG + 5], 1u);
+    }
+    // the side records the next pass's balance scan reads (static failures keep the
+    // records tr_side_rec gave them)
+    if (sr == SRES_DYN && !write_sides(C, i, C.ev[i].flags & (TF_POST | TF_VOID), res == TBGPU_CREATE_TRANSFER_OK,
+                                       pref, dpe, dpo))
+        atomicMax(&C.counters[CNT_RESORT], g.p + 1);  // its pending is not among its sides: rebuild them
+    return changed;
 }
 
-// Optimistic starting point: every statically valid event succeeds.
+// `chg` and `front` are ring words: this pass's count and first changed event; the
+// pass clears the words the pass after it writes (the host clears nothing per pass).
+__global__ void tr_evaluate(Tables T, TrArgs C, EvalState S, EvalState D, const Bal4* __restrict__ bb, PassGate g,
+                            u32* chg, u32* front, u32* chg_next, u32* front_next) {
+    if (!gate_open(g)) return;
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {
+        *chg_next = 0;
+        *front_next = NONE32;
+    }
+    const bool changed = i < C.n && evaluate_one(T, C, S, D, bb, g, i);
+    const u64 m = __ballot(changed);
+    if (m) {
+        const u32 f = wave_min(changed ? i : NONE32);
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(chg, (u32)__popcll(m));
+            atomicMin(front, f);
+        }
+    }
+}
+
+// The pending an unresolved post/void most likely resolves to: a committed transfer
+// with that id, else the first earlier event with that id (a later one repeats
+// its id and fails with `exists` unless the first one fails).
+__device__ __forceinline__ u32 pending_guess(const TrArgs& C, u32 i) {
+    if (C.pre_p[i] != NONE32) return PREF_ROW | C.pre_p[i];
+    return C.pend_first[i];
+}
+
+// Starting point: every statically valid event succeeds, except that an id already
+// committed, or seen earlier in the call, answers `exists` (the first event with an
+// id is the one that succeeds), and a post/void resolves to its likeliest pending.
 __global__ void tr_init(Tables T, TrArgs C, EvalState D) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= C.n) return;
-    const u8 sr = C.sres[i];
+    u8 sr = C.sres[i];
+    if (sr == SRES_DYN && (C.prev_id[i] != NONE32 || C.pre_e[i] != NONE32)) sr = TBGPU_CREATE_TRANSFER_EXISTS;
     u8 res = sr;
     u128 amt = 0, pamt = 0, dpe = 0, dpo = 0;
     u32 pref = NONE32;
@@ -487,8 +578,7 @@ __global__ void tr_init(Tables T, TrArgs C, EvalState D) {
             if ((t.flags & (TF_BDR | TF_BCR)) && amt == 0) amt = (u128)0xFFFFFFFFFFFFFFFFull;
             if (t.flags & TF_PENDING) dpe = amt; else dpo = amt;
         } else {
-            const u32 j = C.pend_last[i];
-            pref = j != NONE32 ? j : (C.pre_p[i] != NONE32 ? (PREF_ROW | C.pre_p[i]) : NONE32);
+            pref = pending_guess(C, i);
             if (pref == NONE32) {
                 res = TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_NOT_FOUND;
             } else {
@@ -510,50 +600,133 @@ __global__ void tr_init(Tables T, TrArgs C, EvalState D) {
     if (res != 0 && C.cs[i] != C.ce[i]) atomicMin(&D.cfail[C.cs[i]], i);
 }
 
-// final-ok = eval-ok and the event's chain was persisted (scope_close(.persist)).
-__global__ void tr_finalize(TrArgs C, EvalState D) {
-    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= C.n) return;
-    const u8 o = D.ok[i] & 1;
-    const u32 cs = C.cs[i];
-    const bool doom = C.ctl && (C.ctl[C.ce[i]] & TBGPU_CTL_DOOM);  // broken on another shard
-    const bool persisted = (cs == C.ce[i] || D.cfail[cs] == NONE32) && !doom;
-    D.ok[i] = o | ((o && persisted) ? 2 : 0);
+// ------------------------------------------------------------------ sides ----
+// The candidate pendings of post/void i (pref encoding), at most kmax, distinct:
+// the one it resolved to in state S, a committed transfer with that id, then the
+// earlier events of the call with that id from the first (the first is the one
+// that succeeds unless it fails; a later one repeats its id).  The evaluation
+// resolves to the last visible such event, else the committed one
+// (src/state_machine.zig:1409-1428): when that is not among these, the host
+// rebuilds the sides with it (PassGate.resort).
+__device__ __forceinline__ u32 post_candidates(const TrArgs& C, const EvalState& S, u32 i, u32 kmax, u32* out) {
+    u32 k = 0;
+    auto add = [&](u32 v) {
+        if (v == NONE32 || k >= kmax) return;
+        for (u32 j = 0; j < k; j++)
+            if (out[j] == v) return;
+        out[k++] = v;
+    };
+    add(S.pref[i]);
+    if (C.pre_p[i] != NONE32) add(PREF_ROW | C.pre_p[i]);
+    const u32 p = C.pslot[i];
+    if (p != NONE32) {
+        const u32 cnt = C.gcnt_id[p];
+        if (cnt == 1) {
+            const u32 j = C.gmem[p];
+            if (j < i) add(j);
+        } else if (cnt > 1) {
+            for (u32 q = C.gbeg[p]; q < C.gend[p] && k < kmax; q++) {
+                const u32 j = C.gmembers[q];
+                if (j >= i) break;
+                add(j);
+            }
+        }
+    }
+    return k;
 }
 
-// Side keys: the debit and credit account slots each event may touch.
-__global__ void tr_sides(TrArgs C, EvalState S, u32 invalid, u32* skey, u32* sval) {
+__device__ __forceinline__ bool is_post_void(const TrArgs& C, u32 i) {
+    return C.sres[i] == SRES_DYN && (C.ev[i].flags & (TF_POST | TF_VOID));
+}
+
+// Side pairs per event, as a popcount mask for scan3: 1 -> 0b001, 2 -> 0b011, 3 -> 0b111.
+__global__ void tr_side_count(TrArgs C, EvalState S, u32 kmax, u8* mask) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= C.n) return;
+    u32 pairs = 1;
+    if (is_post_void(C, i)) {
+        u32 cand[SIDE_CANDS];
+        pairs = max(1u, post_candidates(C, S, i, kmax, cand));
+    }
+    mask[i] = (u8)((1u << pairs) - 1);
+}
+
+// The account slots of a candidate pending (a committed row's were probed by classify).
+__device__ __forceinline__ void cand_slots(const TrArgs& C, u32 i, u32 cand, u32* d, u32* c) {
+    if (cand == NONE32) { *d = *c = NONE32; return; }
+    if (cand & PREF_ROW) { *d = C.pp_dslot[i]; *c = C.pp_cslot[i]; return; }
+    *d = C.dslot[cand];
+    *c = C.cslot[cand];
+}
+
+__global__ void tr_side_build(TrArgs C, EvalState S, u32 kmax, const uint4* pairs, u32 invalid, u32* skey, u32* sval) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > C.n) return;
+    const uint4 pr = pairs[i];
+    const u32 s0 = 2 * (pr.x + pr.y + pr.z);
+    C.sd.soff[i] = s0;
+    if (i == C.n) return;
+    u32 cand[SIDE_CANDS];
+    u32 k = 1;
     u32 d = NONE32, c = NONE32;
+    cand[0] = NONE32;
     if (C.sres[i] == SRES_DYN) {
         if (!(C.ev[i].flags & (TF_POST | TF_VOID))) {
             d = C.dslot[i];
             c = C.cslot[i];
         } else {
-            // An unresolved post/void fails and moves no balance, so any key serves:
-            // keep its candidate pending's accounts and the keys stay put from pass to
-            // pass (a moved key costs a full re-sort).
-            u32 p = S.pref[i];
-            if (p == NONE32) p = C.pend_last[i] != NONE32 ? C.pend_last[i]
-                                 : (C.pre_p[i] != NONE32 ? (PREF_ROW | C.pre_p[i]) : NONE32);
-            if (p != NONE32) {
-                if (p & PREF_ROW) { d = C.pp_dslot[i]; c = C.pp_cslot[i]; }
-                else { d = C.dslot[p]; c = C.cslot[p]; }
-            }
+            k = max(1u, post_candidates(C, S, i, kmax, cand));
         }
     }
-    if (d == NONE32 || c == NONE32) d = c = invalid;
-    if (skey[2 * i] != d || skey[2 * i + 1] != c) atomicAdd(&C.counters[CNT_KEYS], 1u);
-    skey[2 * i] = d;
-    skey[2 * i + 1] = c;
-    sval[2 * i] = 2 * i;
-    sval[2 * i + 1] = 2 * i + 1;
+    for (u32 j = 0; j < k; j++) {
+        if (is_post_void(C, i)) cand_slots(C, i, cand[j], &d, &c);
+        if (d == NONE32 || c == NONE32) d = c = invalid;
+        const u32 s = s0 + 2 * j;
+        skey[s] = d;
+        skey[s + 1] = c;
+        sval[s] = s;
+        sval[s + 1] = s + 1;
+        C.sd.sev[s] = i;
+        C.sd.sev[s + 1] = i | (1u << 31);
+        C.sd.scand[s] = C.sd.scand[s + 1] = is_post_void(C, i) ? cand[j] : NONE32;
+    }
 }
 
-__global__ void tr_side_pos(const u32* sval_s, u64 m, u32* spos) {
+// Sorted positions and the static per-side information in sorted order.
+__global__ void tr_side_pos(TrArgs C, const u32* sval_s, u64 m) {
     const u64 q = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q < m) spos[sval_s[q]] = (u32)q;
+    if (q >= m) return;
+    const u32 s = sval_s[q];
+    C.sd.spos[s] = (u32)q;
+    const u32 ev = C.sd.sev[s];
+    C.sd.sq_ev[q] = ev;
+    const u32 i = ev & 0x7FFFFFFFu;
+    const u32 cs = C.cs[i], ce = C.ce[i];
+    const bool doom = C.ctl && (C.ctl[ce] & TBGPU_CTL_DOOM);
+    C.sd.sq_cs[q] = cs | (cs == ce ? SQ_STANDALONE : 0u) | (doom ? SQ_DOOM : 0u);
+}
+
+// Write event i's side records (sorted order) for its outcome: the debit and credit
+// sides of a transfer, or of the candidate pair of a post/void that it resolved to.
+// Returns false when an accepted post/void's pending is not among its candidates.
+__device__ __forceinline__ bool write_sides(const TrArgs& C, u32 i, bool pv, bool ok, u32 pref, u128 dpe, u128 dpo) {
+    const u32 s0 = C.sd.soff[i], s1 = C.sd.soff[i + 1];
+    bool found = !pv || !ok;
+    for (u32 s = s0; s < s1; s += 2) {
+        const bool act = ok && (!pv || C.sd.scand[s] == pref);
+        found |= pv && act;
+        const u32 q0 = C.sd.spos[s], q1 = C.sd.spos[s + 1];
+        C.sd.sq_ok[q0] = C.sd.sq_ok[q1] = act ? 1 : 0;
+        C.sd.sq_dpend[q0] = C.sd.sq_dpend[q1] = act ? dpe : 0;
+        C.sd.sq_dpost[q0] = C.sd.sq_dpost[q1] = act ? dpo : 0;
+    }
+    return found;
+}
+
+__global__ void tr_side_rec(TrArgs C, EvalState S) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= C.n) return;
+    write_sides(C, i, is_post_void(C, i), S.ok[i] & 1, S.pref[i], S.dpend[i], S.dpost[i]);
 }
 
 // ---------------------------------------------------------------- apply ----
@@ -573,32 +746,37 @@ __global__ void tr_mask(Tables T, TrArgs C, EvalState S, u8* fres, u8* mask) {
     else if (S.res[i] != 0) r = S.res[i];
     else if (cf != NONE32) r = TBGPU_CREATE_TRANSFER_LINKED_EVENT_FAILED;
     else r = TBGPU_CREATE_TRANSFER_OK;
-    const bool ok = S.ok[i] & 2;
+    const bool ok = fin_ok(C, S, i);
     bool hist = false;
     if (ok && !(C.ev[i].flags & (TF_POST | TF_VOID)))
         hist = (T.acc[C.dslot[i]].flags | T.acc[C.cslot[i]].flags) & AF_HISTORY;
     fres[i] = r;
     mask[i] = (ok ? 1 : 0) | (r != 0 ? 2 : 0) | (hist ? 4 : 0);
-    // commit_timestamp is a plain field, not undone by scope_close(.discard): every
-    // create_transfer that returned ok before its chain broke advanced it (:1366).
-    if ((S.ok[i] & 1) && (cf == NONE32 || i < cf))
-        atomicMax((unsigned long long*)C.commit_ts, (unsigned long long)C.ts[i]);
 }
 
+// Rows, replies and history rows go after the device-side cursors T.base (the
+// previous chunks' and calls' output), so chunks follow each other without a host
+// round trip.  A call that would overflow a table writes nothing and raises
+// FL_ERROR (the host aborts, as the reference asserts).
 __global__ void tr_apply(Tables T, TrArgs C, EvalState S, const u8* __restrict__ fres, const uint4* __restrict__ rk,
-                         const u32* __restrict__ spos, const Bal4* __restrict__ bb, u64 row_base, u64 hist_base,
-                         tbgpu_create_transfers_result_t* __restrict__ results) {
+                         const Bal4* __restrict__ bb, tbgpu_create_transfers_result_t* __restrict__ results) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= C.n) return;
+    const u64 row_base = T.base[BASE_ROWS], hist_base = T.base[BASE_HIST];
+    const uint4 tot = rk[C.n];
+    if (!C.dry && (row_base + tot.x > T.xrow_cap || hist_base + tot.z > T.hist_cap)) {
+        if (i == 0) atomicOr(&C.counters[CNT_FLAGS], (u32)FL_ERROR);
+        return;
+    }
     const u8 r = fres[i];
     const uint4 q = rk[i];
     if (r != 0) {
         // replies of consecutive batches are concatenated: global non-ok rank
         const u32 b = batch_of(C.b_start, C.nb, i);
-        results[q.y] = {i - C.b_start[b], (u32)r};
+        results[T.base[BASE_REPLIES] + q.y] = {i - C.b_start[b], (u32)r};
         return;
     }
-    if (C.dry || !(S.ok[i] & 2)) return;
+    if (C.dry || !fin_ok(C, S, i)) return;
     const Transfer t = C.ev[i];
     const u64 row = row_base + q.x;
     const Transfer s = load_ref(T, C, S, i);
@@ -613,7 +791,8 @@ __global__ void tr_apply(Tables T, TrArgs C, EvalState S, const u8* __restrict__
         const Account& cra = T.acc[C.cslot[i]];
         if ((dra.flags | cra.flags) & AF_HISTORY) {
             // balances after this transfer (src/state_machine.zig:1342-1364)
-            Bal4 d = bb[spos[2 * i]], c = bb[spos[2 * i + 1]];
+            const u32 s0 = C.sd.soff[i];
+            Bal4 d = bb[C.sd.spos[s0]], c = bb[C.sd.spos[s0 + 1]];
             d.dp += S.dpend[i]; d.dpo += S.dpost[i];
             c.cp += S.dpend[i]; c.cpo += S.dpost[i];
             History h;
@@ -634,24 +813,44 @@ __global__ void tr_apply(Tables T, TrArgs C, EvalState S, const u8* __restrict__
     }
 }
 
-// Widen the index's componentwise key range by the stored ids (one atomic per
-// wave and word; every lane of every wave takes part).
-__global__ void tr_range(Tables T, TrArgs C, EvalState S) {
-    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool ok = i < C.n && (S.ok[i] & 2);
+// Per 1024-event block: the componentwise key range of the stored ids (for the
+// index's range filter) and the largest timestamp that advances commit_timestamp.
+// commit_timestamp is a plain field, not undone by scope_close(.discard): every
+// create_transfer that returned ok before its chain broke advanced it (:1366).
+// tr_advance folds the blocks' records (no global atomics here: every block on
+// the same five words would serialize).
+constexpr int RG_THREADS = 1024;
+__global__ __launch_bounds__(RG_THREADS) void tr_range(Tables T, TrArgs C, EvalState S, u64* part) {
+    __shared__ u64 sh[RG_THREADS / 64][5];
+    const u32 i = blockIdx.x * RG_THREADS + threadIdx.x;
+    const bool valid = i < C.n;
+    const bool ok = valid && fin_ok(C, S, i);
+    u64 mts = 0;
+    if (valid && (S.ok[i] & 1)) {
+        const u32 cs = C.cs[i];
+        const bool doom = C.ctl && (C.ctl[C.ce[i]] & TBGPU_CTL_DOOM);
+        u32 cf = (cs != C.ce[i] || doom) ? S.cfail[cs] : NONE32;
+        if (cf == NONE32 && doom) cf = C.ce[i] + 1;
+        if (cf == NONE32 || i < cf) mts = C.ts[i];
+    }
     const u128 id = ok ? C.ev[i].id : 0;
-    u64 r[4] = {ok ? (u64)id : 0, ok ? (u64)(id >> 64) : 0, ok ? (u64)id : ~0ull, ok ? (u64)(id >> 64) : ~0ull};
+    u64 r[5] = {ok ? (u64)id : 0, ok ? (u64)(id >> 64) : 0, ok ? (u64)id : ~0ull, ok ? (u64)(id >> 64) : ~0ull, mts};
     for (int off = 32; off > 0; off >>= 1) {
         r[0] = max(r[0], (u64)__shfl_xor((unsigned long long)r[0], off));
         r[1] = max(r[1], (u64)__shfl_xor((unsigned long long)r[1], off));
         r[2] = min(r[2], (u64)__shfl_xor((unsigned long long)r[2], off));
         r[3] = min(r[3], (u64)__shfl_xor((unsigned long long)r[3], off));
+        r[4] = max(r[4], (u64)__shfl_xor((unsigned long long)r[4], off));
     }
-    if ((threadIdx.x & 63) == 0 && r[0] | r[1] | ~r[2] | ~r[3]) {
-        atomicMax((unsigned long long*)&T.idr[0], (unsigned long long)r[0]);
-        atomicMax((unsigned long long*)&T.idr[1], (unsigned long long)r[1]);
-        atomicMin((unsigned long long*)&T.idr[2], (unsigned long long)r[2]);
-        atomicMin((unsigned long long*)&T.idr[3], (unsigned long long)r[3]);
+    const u32 w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < 5; k++) sh[w][k] = r[k];
+    __syncthreads();
+    if (threadIdx.x < 5) {
+        const int k = threadIdx.x;
+        u64 v = sh[0][k];
+        for (int q = 1; q < RG_THREADS / 64; q++) v = (k == 2 || k == 3) ? min(v, sh[q][k]) : max(v, sh[q][k]);
+        part[(u64)blockIdx.x * 8 + k] = v;
     }
 }
 
@@ -660,10 +859,71 @@ __global__ void batch_counts(const u32* b_start, u32 nb, const uint4* rk, u32* c
     if (b < nb) counts[b] = rk[b_start[b + 1]].y - rk[b_start[b]].y;
 }
 
+// Fold tr_range's block records into the index key range and commit_timestamp, and
+// advance the device cursors by the chunk's stored rows, replies and history rows.
+__global__ __launch_bounds__(256) void tr_advance(Tables T, TrArgs C, const uint4* rk, const u64* part, u32 nparts) {
+    if (C.counters[CNT_FLAGS] & FL_ERROR) return;
+    u64 r[5] = {0, 0, ~0ull, ~0ull, 0};
+    for (u32 b = threadIdx.x; b < nparts; b += 256) {
+        r[0] = max(r[0], part[b * 8 + 0]);
+        r[1] = max(r[1], part[b * 8 + 1]);
+        r[2] = min(r[2], part[b * 8 + 2]);
+        r[3] = min(r[3], part[b * 8 + 3]);
+        r[4] = max(r[4], part[b * 8 + 4]);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        r[0] = max(r[0], (u64)__shfl_xor((unsigned long long)r[0], off));
+        r[1] = max(r[1], (u64)__shfl_xor((unsigned long long)r[1], off));
+        r[2] = min(r[2], (u64)__shfl_xor((unsigned long long)r[2], off));
+        r[3] = min(r[3], (u64)__shfl_xor((unsigned long long)r[3], off));
+        r[4] = max(r[4], (u64)__shfl_xor((unsigned long long)r[4], off));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (r[4]) atomicMax((unsigned long long*)C.commit_ts, (unsigned long long)r[4]);
+        if (!C.dry && (r[0] | r[1] | ~r[2] | ~r[3])) {
+            atomicMax((unsigned long long*)&T.idr[0], (unsigned long long)r[0]);
+            atomicMax((unsigned long long*)&T.idr[1], (unsigned long long)r[1]);
+            atomicMin((unsigned long long*)&T.idr[2], (unsigned long long)r[2]);
+            atomicMin((unsigned long long*)&T.idr[3], (unsigned long long)r[3]);
+        }
+    }
+    if (threadIdx.x != 0) return;
+    const uint4 tot = rk[C.n];
+    T.base[BASE_REPLIES] += tot.y;
+    if (C.dry) return;
+    T.base[BASE_ROWS] += tot.x;
+    T.base[BASE_HIST] += tot.z;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------ launchers ----
 #define GRID(n) (u32)(((n) + 255) / 256), 256, 0, stream
+
+// Per-chunk reset in one launch: counters, the group table, the initial state's
+// chain failures, the pass-counter ring (the first pass's gate open).
+__global__ void tr_prep(TrArgs C, u32* cfail0, u32* pc, u32 ring) {
+    const u64 g = C.gmask + 1;
+    const u64 tot = max(max(g, (u64)C.n), (u64)ring);
+    for (u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x; k < tot; k += (u64)gridDim.x * blockDim.x) {
+        if (k < g) {
+            C.gclaim[k] = 0;
+            C.gcnt_id[k] = 0;
+            C.gcnt_pd[k] = 0;
+        }
+        if (k < C.n) cfail0[k] = NONE32;
+        if (k < ring) {
+            pc[k] = k == 0 ? 1u : 0u;
+            pc[ring + k] = NONE32;
+        }
+        if (k < CNT_COUNT) C.counters[k] = 0;
+    }
+}
+
+void tr_launch_prep(const TrArgs& C, u32* cfail0, u32* pc, u32 ring, hipStream_t stream) {
+    const u64 tot = std::max<u64>(std::max<u64>(C.gmask + 1, C.n), ring);
+    tr_prep<<<(u32)std::min<u64>((tot + 255) / 256, 2048), 256, 0, stream>>>(C, cfail0, pc, ring);
+}
 
 void tr_launch_classify(const Tables& T, const TrArgs& C, hipStream_t stream) {
     tr_classify<<<GRID(C.n)>>>(T, C);
@@ -672,33 +932,43 @@ void tr_launch_classify(const Tables& T, const TrArgs& C, hipStream_t stream) {
 void tr_launch_group_sort(const TrArgs& C, u32 kind, u32 invalid, int bits, u32* k_in, u32* v_in, u32* k_out,
                           u32* v_out, SortScratch& ss, hipStream_t stream) {
     tr_group_keys<<<GRID(C.n)>>>(C, kind, invalid, k_in, v_in);
-    radix_sort_pairs(k_in, v_in, k_out, v_out, C.n, bits, ss, stream);
+    radix_sort_pairs(k_in, v_in, k_out, v_out, C.n, bits, ss, stream, C.counters + CNT_FLAGS,
+                     kind == 0 ? FL_MULTI_ID : FL_MULTI_PEND);
     if (kind == 0) tr_group_ranges<<<GRID(C.n)>>>(C, invalid, k_out, v_out);
     else tr_pend_ranges<<<GRID(C.n)>>>(C, invalid, k_out, v_out);
 }
 void tr_launch_group2(const TrArgs& C, hipStream_t stream) { tr_group2<<<GRID(C.n)>>>(C); }
 void tr_launch_init(const Tables& T, const TrArgs& C, const EvalState& D, hipStream_t stream) {
     tr_init<<<GRID(C.n)>>>(T, C, D);
-    tr_finalize<<<GRID(C.n)>>>(C, D);
 }
-void tr_launch_sides(const TrArgs& C, const EvalState& S, u32 invalid, u32* skey, u32* sval, hipStream_t stream) {
-    tr_sides<<<GRID(C.n)>>>(C, S, invalid, skey, sval);
+void tr_launch_side_count(const TrArgs& C, const EvalState& S, u32 kmax, u8* mask, hipStream_t stream) {
+    tr_side_count<<<GRID(C.n)>>>(C, S, kmax, mask);
 }
-void tr_launch_side_pos(const u32* sval_s, u64 m, u32* spos, hipStream_t stream) {
-    tr_side_pos<<<GRID(m)>>>(sval_s, m, spos);
+void tr_launch_side_build(const TrArgs& C, const EvalState& S, u32 kmax, const uint4* pairs, u32 invalid, u32* skey,
+                          u32* sval, hipStream_t stream) {
+    tr_side_build<<<GRID(C.n + 1)>>>(C, S, kmax, pairs, invalid, skey, sval);
 }
-void tr_launch_evaluate(const Tables& T, const TrArgs& C, const EvalState& S, const EvalState& D, const u32* spos,
-                        const Bal4* bb, hipStream_t stream) {
-    tr_evaluate<<<GRID(C.n)>>>(T, C, S, D, spos, bb);
-    tr_finalize<<<GRID(C.n)>>>(C, D);
+void tr_launch_side_pos(const TrArgs& C, const u32* sval_s, u64 m, hipStream_t stream) {
+    tr_side_pos<<<GRID(m)>>>(C, sval_s, m);
+}
+void tr_launch_side_rec(const TrArgs& C, const EvalState& S, hipStream_t stream) {
+    tr_side_rec<<<GRID(C.n)>>>(C, S);
+}
+void tr_launch_evaluate(const Tables& T, const TrArgs& C, const EvalState& S, const EvalState& D, const Bal4* bb,
+                        const PassGate& g, u32* chg, u32* front, u32* chg_next, u32* front_next, hipStream_t stream) {
+    tr_evaluate<<<GRID(C.n)>>>(T, C, S, D, bb, g, chg, front, chg_next, front_next);
 }
 void tr_launch_mask(const Tables& T, const TrArgs& C, const EvalState& S, u8* fres, u8* mask, hipStream_t stream) {
     tr_mask<<<GRID(C.n)>>>(T, C, S, fres, mask);
 }
 void tr_launch_apply(const Tables& T, const TrArgs& C, const EvalState& S, const u8* fres, const uint4* rk,
-                     const u32* spos, const Bal4* bb, u64 row_base, u64 hist_base,
-                     tbgpu_create_transfers_result_t* results, u32* counts, hipStream_t stream) {
-    tr_apply<<<GRID(C.n)>>>(T, C, S, fres, rk, spos, bb, row_base, hist_base, results);
-    if (!C.dry) tr_range<<<GRID(C.n)>>>(T, C, S);
+                     const Bal4* bb, tbgpu_create_transfers_result_t* results, u32* counts, u64* part,
+                     hipStream_t stream) {
+    tr_apply<<<GRID(C.n)>>>(T, C, S, fres, rk, bb, results);
+    tr_range<<<(C.n + RG_THREADS - 1) / RG_THREADS, RG_THREADS, 0, stream>>>(T, C, S, part);
     batch_counts<<<GRID(C.nb)>>>(C.b_start, C.nb, rk, counts);
 }
+void tr_launch_advance(const Tables& T, const TrArgs& C, const uint4* rk, const u64* part, hipStream_t stream) {
+    tr_advance<<<1, 256, 0, stream>>>(T, C, rk, part, (C.n + RG_THREADS - 1) / RG_THREADS);
+}
+u64 tr_range_part_words(u64 n) { return 8 * ((n + RG_THREADS - 1) / RG_THREADS + 1); }

@@ -218,7 +218,146 @@ __global__ void bs_final(SideScanArgs A, u64 m, u32 invalid, const Bal4* __restr
         atomicOr(big, 1u);
 }
 
+// --------------------------------------------------------- fused scan ----
+// One launch per pass: a workgroup of BF_THREADS sides (one per thread) finds the
+// balance carried into its tile from the previous tile alone -- the tail of the
+// account segment that crosses the boundary, which starts inside the previous tile
+// unless a segment is longer than BF_THREADS sides -- then scans its own tile.  No
+// tile aggregates, no second launch, no single-workgroup tile scan.  A segment
+// longer than the window raises halt[1] (the host redoes the pass with the
+// three-launch scan above).
+constexpr int BF_THREADS = 256;
+
+__device__ __forceinline__ u64 shup(u64 v, int off) { return (u64)__shfl_up((unsigned long long)v, off); }
+__device__ __forceinline__ u128 shup128(u128 v, int off) {
+    return ((u128)shup((u64)(v >> 64), off) << 64) | shup((u64)v, off);
+}
+__device__ __forceinline__ Bal4 shup_bal(const Bal4& b, int off) {
+    Bal4 r;
+    r.dp = shup128(b.dp, off);
+    r.dpo = shup128(b.dpo, off);
+    r.cp = shup128(b.cp, off);
+    r.cpo = shup128(b.cpo, off);
+    return r;
+}
+
+// Exclusive segmented scan of one element per thread over the workgroup: wave
+// scans by shuffles, the four wave totals through LDS.
+template <bool HAS_H>
+__device__ SE block_excl_waves(SE v, SE* wtot) {
+    const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int off = 1; off < 64; off <<= 1) {
+        SE o;
+        o.F = shup_bal(v.F, off);
+        if (HAS_H) o.H = shup_bal(v.H, off);
+        o.fl = __shfl_up(v.fl, off);
+        if (lane >= (u32)off) v = combine<HAS_H>(o, v);
+    }
+    // v is inclusive; exclusive by one more shift
+    SE ex;
+    ex.F = shup_bal(v.F, 1);
+    if (HAS_H) ex.H = shup_bal(v.H, 1);
+    ex.fl = __shfl_up(v.fl, 1);
+    if (lane == 0) ex = identity<HAS_H>();
+    if (lane == 63) wtot[w] = v;
+    __syncthreads();
+    SE pre = identity<HAS_H>();
+    for (u32 k = 0; k < w; k++) pre = combine<HAS_H>(pre, wtot[k]);
+    __syncthreads();
+    return combine<HAS_H>(pre, ex);
+}
+
+__device__ __forceinline__ u32 block_max(u32 v, u32* sh) {
+    for (int off = 32; off > 0; off >>= 1) v = max(v, (u32)__shfl_xor(v, off));
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    v = sh[0];
+    for (int k = 1; k < BF_THREADS / 64; k++) v = max(v, sh[k]);
+    __syncthreads();
+    return v;
+}
+
+__device__ __forceinline__ u128 wave_sum128(u128 v) {
+    u64 lo = (u64)v, hi = (u64)(v >> 64);
+    for (int off = 32; off > 0; off >>= 1) {
+        const u64 l2 = (u64)__shfl_xor((unsigned long long)lo, off), h2 = (u64)__shfl_xor((unsigned long long)hi, off);
+        const u64 s = lo + l2;
+        hi = hi + h2 + (s < lo ? 1 : 0);
+        lo = s;
+    }
+    return ((u128)hi << 64) | lo;
+}
+__device__ __forceinline__ Bal4 block_sum_bal(Bal4 b, Bal4* sh) {
+    b.dp = wave_sum128(b.dp);
+    b.dpo = wave_sum128(b.dpo);
+    b.cp = wave_sum128(b.cp);
+    b.cpo = wave_sum128(b.cpo);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = b;
+    __syncthreads();
+    Bal4 r = sh[0];
+    for (int k = 1; k < BF_THREADS / 64; k++) r = add(r, sh[k]);
+    __syncthreads();
+    return r;
+}
+
+template <bool HAS_H>
+__global__ __launch_bounds__(BF_THREADS) void bs_fused(SideScanArgs A, u64 m, u32 invalid, u32* long_flag,
+                                                       const Account* __restrict__ acc, Bal4* __restrict__ bb) {
+    if (!gate_open(A.gate)) return;
+    __shared__ SE wtot[BF_THREADS / 64];
+    __shared__ Bal4 bsum[BF_THREADS / 64];
+    __shared__ u32 umax[BF_THREADS / 64];
+    // the next state's per-chain first failures start at "none"
+    if (A.cfail_clear)
+        for (u64 k = (u64)blockIdx.x * BF_THREADS + threadIdx.x; k < A.n; k += (u64)gridDim.x * BF_THREADS)
+            A.cfail_clear[k] = NONE32;
+    const u64 q0 = (u64)blockIdx.x * BF_THREADS;
+    const u64 q = q0 + threadIdx.x;
+    // 1. the carry: the tail, in the previous tile, of the segment that crosses into this one
+    SE carry = identity<HAS_H>();
+    const u32 K = q0 > 0 ? A.skey[q0 - 1] : invalid;
+    if (K < invalid) {
+        const u64 p = q0 - BF_THREADS + threadIdx.x;  // q0 >= BF_THREADS here
+        SE e = load_elem<HAS_H>(A, p, invalid);
+        const bool mine = A.skey[p] == K;
+        const u32 fs = block_max(mine && (e.fl & 1) ? (u32)threadIdx.x + 1 : 0u, umax);
+        const u32 hs = block_max(mine && (e.fl & 2) ? (u32)threadIdx.x + 1 : 0u, umax);
+        if (fs == 0) {  // the segment started before the previous tile
+            if (threadIdx.x == 0) atomicMax(long_flag, A.gate.p + 1);
+            return;
+        }
+        Bal4 z;
+        zero(z);
+        carry.F = block_sum_bal(mine && threadIdx.x + 1 >= fs ? e.F : z, bsum);
+        if (HAS_H) carry.H = block_sum_bal(mine && threadIdx.x + 1 >= hs ? e.H : z, bsum);
+    }
+    // 2. this tile
+    SE e = q < m ? load_elem<HAS_H>(A, q, invalid) : identity<HAS_H>();
+    if (q >= m) e.fl = 3;
+    SE run = combine<HAS_H>(carry, block_excl_waves<HAS_H>(e, wtot));
+    if (q >= m) return;
+    const u32 key = A.skey[q];
+    if (key >= invalid) return;
+    const Account& a = acc[key];
+    Bal4 out;
+    out.dp = a.debits_pending;
+    out.dpo = a.debits_posted;
+    out.cp = a.credits_pending;
+    out.cpo = a.credits_posted;
+    if (!(e.fl & 1)) out = add(out, run.F);
+    if (HAS_H && !(e.fl & 2)) out = add(out, run.H);
+    bb[q] = out;
+}
+
 }  // namespace
+
+void side_scan_fused(const SideScanArgs& A, u64 m, u32 invalid, u32* long_flag, const Account* acc, Bal4* bb,
+                     hipStream_t stream) {
+    if (m == 0) return;
+    bs_fused<true><<<(u32)((m + BF_THREADS - 1) / BF_THREADS), BF_THREADS, 0, stream>>>(A, m, invalid, long_flag,
+                                                                                        acc, bb);
+    HIP_CHECK(hipGetLastError());
+}
 
 u64 side_scan_tile_bytes(u64 capacity) { return ((capacity + BS_TILE - 1) / BS_TILE + 1) * sizeof(SE); }
 

@@ -59,6 +59,11 @@ __device__ __forceinline__ u64 dense_entry(u32 row, u32 ledger, u16 flags) {
     return (u64)(row + 1) | ((u64)(flags & 0xEu) << 28) | ((u64)ledger << 32);
 }
 
+// Account lookup: the direct-mapped directory for ids 1..dense_n (8 bytes), the
+// hash index otherwise.  Returns the row (NONE32 when absent) with its ledger and
+// flags (limit / history bits), which are immutable after create_account.
+__device__ __forceinline__ u32 acc_find(const Tables& T, u128 id, u32* ledger, u16* flags);
+
 __device__ __forceinline__ bool xidx_maybe_present(const Tables& T, u128 id) {
     const u64 lo = (u64)id, hi = (u64)(id >> 64);
     return lo <= T.idr[0] && hi <= T.idr[1] && lo >= T.idr[2] && hi >= T.idr[3];
@@ -83,10 +88,11 @@ struct EvalState {
 // passes after convergence return at once.
 struct PassGate {
     const u32* chg;     // the previous pass's change count (a ring word)
-    const u32* resort;  // nonzero: a side key moved, the host re-sorts before going on
+    const u32* halt;    // [0] a post/void resolved outside its sides (rebuild them), [1] the fused
+                        // balance scan met an account segment longer than its window: nonzero halts
     u32 p;              // this pass's number
 };
-__device__ __forceinline__ bool gate_open(const PassGate& g) { return *g.chg != 0 && *g.resort == 0; }
+__device__ __forceinline__ bool gate_open(const PassGate& g) { return *g.chg != 0 && g.halt[0] == 0 && g.halt[1] == 0; }
 
 // final-ok: eval-ok and the event's chain persisted (execute's scope_close(.persist),
 // src/state_machine.zig:1074-1082), and not doomed by a break on another shard.
@@ -147,6 +153,10 @@ __device__ __forceinline__ bool side_final(const SideScanArgs& A, u64 q) {
 u64 side_scan_tile_bytes(u64 capacity);
 void side_scan(const SideScanArgs& A, u64 m, u32 invalid, bool has_chains, void* tile_scratch, const Account* acc,
                Bal4* bb, hipStream_t stream);
+// One-launch form (balances.hip bs_fused): raises *long_flag (= pass + 1) and leaves
+// the pass incomplete when an account segment is longer than its window.
+void side_scan_fused(const SideScanArgs& A, u64 m, u32 invalid, u32* long_flag, const Account* acc, Bal4* bb,
+                     hipStream_t stream);
 void side_final_balances(const SideScanArgs& A, u64 m, u32 invalid, const Bal4* bb, Account* acc, u32* big,
                          hipStream_t stream);
 
@@ -159,6 +169,28 @@ __device__ __forceinline__ u32 acc_probe(const AccIdx* __restrict__ aidx, u64 ma
         if (e.row1 == 0) return NONE32;
         if (e.id_lo == lo && e.id_hi == hi) return e.row1 - 1;
         h = (h + 1) & mask;
+    }
+}
+
+__device__ __forceinline__ u32 acc_find(const Tables& T, u128 id, u32* ledger, u16* flags) {
+    if (dense_has(T, id)) {
+        const u64 e = T.dense[(u64)id - 1];
+        if (e == 0) return NONE32;
+        *ledger = (u32)(e >> 32);
+        *flags = (u16)((e >> 28) & 0xE);
+        return (u32)(e & 0x1FFFFFFFu) - 1;
+    }
+    const u64 lo = (u64)id, hi = (u64)(id >> 64);
+    u64 h = hash128(lo, hi) & T.aidx_mask;
+    for (;;) {
+        const AccIdx& e = T.aidx[h];
+        if (e.row1 == 0) return NONE32;
+        if (e.id_lo == lo && e.id_hi == hi) {
+            *ledger = e.ledger;
+            *flags = e.flags;
+            return e.row1 - 1;
+        }
+        h = (h + 1) & T.aidx_mask;
     }
 }
 
@@ -175,6 +207,7 @@ __device__ __forceinline__ u64 xidx_hash(u128 id) {
 }
 
 __device__ __forceinline__ u32 xidx_probe(const Tables& T, u128 id) {
+    if (!xidx_maybe_present(T, id)) return NONE32;  // outside the stored ids' key range
     u64 h = xidx_hash(id) & T.xidx_mask;
     for (;;) {
         const u32 r1 = T.xidx[h];
@@ -197,10 +230,11 @@ enum {
     CNT_KEYS = 2,       // side keys changed since the last sort
     CNT_OK = 3,         // fast path: accepted events
     CNT_BAD = 4,        // fast path: events with a result other than ok
-    CNT_RESORT = 5,     // general path: pass + 1 whose evaluation moved a side key (0 = none)
-    CNT_DBG = 6,        // diagnostics (words 6-11): changed events by kind, summed over a call's passes
+    CNT_RESORT = 5,     // general path: pass + 1 whose evaluation resolved a post/void outside its sides
+    CNT_LONG = 6,       // general path: pass + 1 whose fused scan met a segment longer than its window
     CNT_TS_SAVE = 12,   // fast path: commit_timestamp before the call (u64 in words 12-13)
-    CNT_COUNT = 16,
+    CNT_DBG = 16,       // diagnostics (words 16-21): changed events by kind, summed over a call's passes
+    CNT_COUNT = 24,
 };
 enum {
     FL_CHAINS = 1u << 0,      // some event is in a linked chain

@@ -80,6 +80,7 @@ struct tbgpu_ctx {
     u64 scap = 0, side_m = 0;  // side capacity, sides of the last fixed point
     u32 *skey, *sval, *skey_s, *sval_s, *spos;
     u32 *soff, *sev, *scand, *sq_ev, *sq_cs;
+    EvCore* core = nullptr;
     u8* sq_ok = nullptr;
     u128 *sq_dpend = nullptr, *sq_dpost = nullptr;
     u32 *gkey_s, *gsorted;  // the id-group sort's output (the members of each id group, by event)
@@ -114,6 +115,7 @@ struct tbgpu_ctx {
     bool rt_dry = false;
     u32 slow_chunks = 0;  // consecutive chunks that needed the fixed point
     u32 last_passes = 8;  // passes the last fixed point took (sizes the next pass group)
+    bool long_segments = false;  // this call has an account segment too long for the fused scan
     // fixed-point pass counters, a ring of PC_RING words each: changes per pass (the
     // gate of the next pass) and the first changed event of each pass
     u32* pc = nullptr;
@@ -176,6 +178,7 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->sval_s = dalloc<u32>(m, &B);
     c->spos = dalloc<u32>(m, &B);
     c->soff = dalloc<u32>(n + 1, &B);
+    c->core = dalloc<EvCore>(n, &B);
     c->sev = dalloc<u32>(m, &B);
     c->scand = dalloc<u32>(m, &B);
     c->sq_ev = dalloc<u32>(m, &B);
@@ -330,7 +333,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
                     c->b_start, c->b_ts, c->ts, c->cs, c->ce, c->sres, c->dslot, c->cslot, c->pre_e, c->pre_p,
                     c->pp_dslot, c->pp_cslot, c->gslot, c->pslot, c->prev_id, c->pend_last, c->pend_first, c->prev_pend,
                     c->gclaim, c->gcnt_id, c->gcnt_pd, c->gmem, c->gbeg, c->gend, c->skey, c->sval, c->skey_s,
-                    c->soff, c->sev, c->scand, c->sq_ev, c->sq_cs, c->sq_ok, c->sq_dpend, c->sq_dpost, c->gkey_s,
+                    c->soff, c->core, c->sev, c->scand, c->sq_ev, c->sq_cs, c->sq_ok, c->sq_dpend, c->sq_dpost, c->gkey_s,
                     c->gsorted,
                     c->sval_s, c->spos, c->bb, c->ss.keys_tmp, c->ss.vals_tmp, c->ss.hist, c->side_tiles,
                     c->sc.tile_sums, c->fres, c->mask, c->ranks, c->res_buf, c->counts, c->counters, c->status,
@@ -437,7 +440,7 @@ static TrArgs make_tr_args(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb) {
     TrArgs C{};
     C.ev = ev; C.n = n; C.nb = nb;
     C.b_start = c->b_start; C.b_ts = c->b_ts;
-    C.ts = c->ts; C.cs = c->cs; C.ce = c->ce; C.sres = c->sres;
+    C.ts = c->ts; C.core = c->core; C.cs = c->cs; C.ce = c->ce; C.sres = c->sres;
     C.dslot = c->dslot; C.cslot = c->cslot; C.pre_e = c->pre_e; C.pre_p = c->pre_p;
     C.pp_dslot = c->pp_dslot; C.pp_cslot = c->pp_cslot; C.gslot = c->gslot; C.pslot = c->pslot;
     C.prev_id = c->prev_id; C.pend_last = c->pend_last; C.pend_first = c->pend_first; C.prev_pend = c->prev_pend;
@@ -584,7 +587,8 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n) {
             SA.cfail = S.cfail;
             SA.cfail_clear = D.cfail;
             SA.gate = G;
-            side_scan(SA, m, inv_acc, chains, c->side_tiles, c->T.acc, c->bb, s);
+            if (c->long_segments) side_scan(SA, m, inv_acc, chains, c->side_tiles, c->T.acc, c->bb, s);
+            else side_scan_fused(SA, m, inv_acc, c->counters + CNT_LONG, c->T.acc, c->bb, s);
             tr_launch_evaluate(c->T, C, S, D, c->bb, G, chg + (q + 1) % PC_RING, front + (q + 1) % PC_RING,
                                chg + (q + 2) % PC_RING, front + (q + 2) % PC_RING, s);
         }
@@ -603,6 +607,16 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n) {
             fprintf(stderr, "tbgpu: changed so far: regular %u balancing %u post/void %u; result changed %u, "
                             "chain members %u, limit accounts %u; resort %u\n", d[0], d[1], d[2], d[3], d[4], d[5],
                     c->h_counters[CNT_RESORT]);
+        }
+        const u32 lng = c->h_counters[CNT_LONG];
+        if (lng) {
+            // pass r's fused scan met an account segment longer than its window: redo
+            // it, and the rest of the call, with the three-launch scan
+            const u32 r = lng - 1;
+            c->long_segments = true;
+            HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)(c->counters + CNT_LONG), 0, 1, s));
+            p = r;
+            continue;
         }
         const u32 resort = c->h_counters[CNT_RESORT];
         if (resort) {
@@ -686,6 +700,7 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
     c->stats.sorts = 0;
     u32 small_until = 0;  // batches before this one go in general-path-sized chunks
     set_base(c, BASE_REPLIES, 0);  // the call's replies start at the front of `results`
+    c->long_segments = false;
     for (u32 b0 = 0; b0 < nb_total;) {
         // After a call needed the fixed point, the next ones probably do too: small
         // chunks, and the fast attempt only every 8th (it undoes itself when it fails).

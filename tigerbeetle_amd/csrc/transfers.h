@@ -2,6 +2,18 @@
 #pragma once
 #include "engine.h"
 
+// What the fixed point's evaluation reads of a transfer on every pass, compact
+// (the 128-byte event is read again only for an `exists` comparison or a post/void).
+struct alignas(16) EvCore {
+    u128 amount;
+    u64 ts;       // the event's timestamp
+    u32 timeout;
+    u16 flags;    // transfer flags
+    u8 aflags;    // debit account flags | credit account flags << 4 (limits, history)
+    u8 pad;
+};
+static_assert(sizeof(EvCore) == 32, "EvCore");
+
 struct TrArgs {
     const Transfer* ev;   // events of the call (all batches), in HBM
     u32 n;                // event count
@@ -13,6 +25,7 @@ struct TrArgs {
     u64* commit_ts;       // commit_timestamp sink (T.commit_ts, or a scratch word when dry)
     u32 dry;              // dry run: replies only, no state change
     u64* ts;              // assigned event timestamps
+    EvCore* core;         // compact per-event record (classify)
     u32* cs;              // linked-chain start (== index for standalone events)
     u32* ce;              // linked-chain end (inclusive)
     u8* sres;             // static result or SRES_DYN

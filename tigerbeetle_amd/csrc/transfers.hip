@@ -110,6 +110,8 @@ __device__ __forceinline__ u32 classify_one(const Tables& T, const TrArgs& C, u3
 
     u32 dslot = NONE32, cslot = NONE32, pre_e = NONE32, pre_p = NONE32, ppd = NONE32, ppc = NONE32;
     u32 gslot = NONE32, pslot = NONE32;
+    u32 dled = 0, cled = 0;
+    u16 dfl = 0, cfl = 0;
     u8 sres;
     const u16 f = t.flags;
     if (linked(i) && k == nbatch - 1) {
@@ -140,8 +142,10 @@ __device__ __forceinline__ u32 classify_one(const Tables& T, const TrArgs& C, u3
             pre_p = xidx_probe(T, t.pending_id);
             if (pre_p != NONE32) {
                 const Transfer& p = T.xrows[pre_p];
-                ppd = acc_probe(T.aidx, T.aidx_mask, p.debit_account_id);
-                ppc = acc_probe(T.aidx, T.aidx_mask, p.credit_account_id);
+                u32 lg;
+                u16 af;
+                ppd = acc_find(T, p.debit_account_id, &lg, &af);
+                ppc = acc_find(T, p.credit_account_id, &lg, &af);
             }
             gslot = gtab_find_or_insert(C, t.id, i, 0);
             pslot = gtab_find_or_insert(C, t.pending_id, i, 1);
@@ -166,26 +170,32 @@ __device__ __forceinline__ u32 classify_one(const Tables& T, const TrArgs& C, u3
         sres = TBGPU_CREATE_TRANSFER_LEDGER_MUST_NOT_BE_ZERO;
     } else if (t.code == 0) {
         sres = TBGPU_CREATE_TRANSFER_CODE_MUST_NOT_BE_ZERO;
-    } else if ((dslot = acc_probe(T.aidx, T.aidx_mask, t.debit_account_id)) == NONE32) {
+    } else if ((dslot = acc_find(T, t.debit_account_id, &dled, &dfl)) == NONE32) {
         sres = TBGPU_CREATE_TRANSFER_DEBIT_ACCOUNT_NOT_FOUND;
-    } else if ((cslot = acc_probe(T.aidx, T.aidx_mask, t.credit_account_id)) == NONE32) {
+    } else if ((cslot = acc_find(T, t.credit_account_id, &cled, &cfl)) == NONE32) {
         sres = TBGPU_CREATE_TRANSFER_CREDIT_ACCOUNT_NOT_FOUND;
     } else {
-        const Account& dr = T.acc[dslot];
-        const Account& cr = T.acc[cslot];
-        if (dr.ledger != cr.ledger) sres = TBGPU_CREATE_TRANSFER_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
-        else if (t.ledger != dr.ledger) sres = TBGPU_CREATE_TRANSFER_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
+        if (dled != cled) sres = TBGPU_CREATE_TRANSFER_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
+        else if (t.ledger != dled) sres = TBGPU_CREATE_TRANSFER_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
         else {
             sres = SRES_DYN;
             pre_e = xidx_probe(T, t.id);
             gslot = gtab_find_or_insert(C, t.id, i, 0);
             if (f & (TF_BDR | TF_BCR)) fl |= FL_BALANCING;
             if (f & TF_PENDING) fl |= FL_PENDING;
-            if ((dr.flags | cr.flags) & (AF_DNEC | AF_CNED)) fl |= FL_LIMITS;
-            if ((dr.flags | cr.flags) & AF_HISTORY) fl |= FL_HISTORY;
+            if ((dfl | cfl) & (AF_DNEC | AF_CNED)) fl |= FL_LIMITS;
+            if ((dfl | cfl) & AF_HISTORY) fl |= FL_HISTORY;
         }
     }
     if (sres != SRES_DYN) { dslot = NONE32; cslot = NONE32; }
+    EvCore core;
+    core.amount = t.amount;
+    core.ts = ts;
+    core.timeout = t.timeout;
+    core.flags = f;
+    core.aflags = (u8)((dfl & 0xF) | (cfl & 0xF) << 4);
+    core.pad = 0;
+    C.core[i] = core;
     C.sres[i] = sres;
     C.dslot[i] = dslot;
     C.cslot[i] = cslot;
@@ -377,9 +387,9 @@ __device__ __forceinline__ u8 post_or_void_exists(const Transfer& t, const Trans
 }
 
 // Balance-dependent tail of create_transfer (src/state_machine.zig:1286-1322).
-__device__ __forceinline__ u8 eval_balances(const Transfer& t, const Bal4& dr, const Bal4& cr, u16 dr_flags,
-                                            u16 cr_flags, u128* amount_out) {
+__device__ __forceinline__ u8 eval_balances(const EvCore& t, const Bal4& dr, const Bal4& cr, u128* amount_out) {
     const u16 f = t.flags;
+    const u16 dr_flags = t.aflags & 0xF, cr_flags = t.aflags >> 4;
     u128 amount = t.amount;
     if ((f & (TF_BDR | TF_BCR)) && amount == 0) amount = (u128)0xFFFFFFFFFFFFFFFFull;  // maxInt(u64)
     if (f & TF_BDR) {
@@ -402,7 +412,7 @@ __device__ __forceinline__ u8 eval_balances(const Transfer& t, const Bal4& dr, c
     if (sum_overflows128(amount, cr.cpo)) return TBGPU_CREATE_TRANSFER_OVERFLOWS_CREDITS_POSTED;
     if (sum_overflows128(amount, dr.dp + dr.dpo)) return TBGPU_CREATE_TRANSFER_OVERFLOWS_DEBITS;
     if (sum_overflows128(amount, cr.cp + cr.cpo)) return TBGPU_CREATE_TRANSFER_OVERFLOWS_CREDITS;
-    if (sum_overflows64(t.timestamp, (u64)t.timeout * NS_PER_S)) return TBGPU_CREATE_TRANSFER_OVERFLOWS_TIMEOUT;
+    if (sum_overflows64(t.ts, (u64)t.timeout * NS_PER_S)) return TBGPU_CREATE_TRANSFER_OVERFLOWS_TIMEOUT;
     if ((dr_flags & AF_DNEC) && dr.dp + dr.dpo + amount > dr.cpo) return TBGPU_CREATE_TRANSFER_EXCEEDS_CREDITS;
     if ((cr_flags & AF_CNED) && cr.cp + cr.cpo + amount > cr.dpo) return TBGPU_CREATE_TRANSFER_EXCEEDS_DEBITS;
     *amount_out = amount;
@@ -438,28 +448,30 @@ __device__ __forceinline__ bool evaluate_one(const Tables& T, const TrArgs& C, c
     if (sr != SRES_DYN) {
         res = sr;
     } else {
-        Transfer t = C.ev[i];
-        t.timestamp = C.ts[i];
+        const EvCore k = C.core[i];
         u32 e = NONE32;
         for (u32 j = C.prev_id[i]; j != NONE32; j = C.prev_id[j])
             if (visible(C, S, j, csi)) { e = j; break; }
         if (e == NONE32 && C.pre_e[i] != NONE32) e = PREF_ROW | C.pre_e[i];
-        if (!(t.flags & (TF_POST | TF_VOID))) {
+        if (!(k.flags & (TF_POST | TF_VOID))) {
             if (e != NONE32) {
+                Transfer t = C.ev[i];
+                t.timestamp = k.ts;
                 res = create_transfer_exists(t, load_ref(T, C, S, e));
             } else {
                 const u32 s0 = C.sd.soff[i];
                 const Bal4 bd = bb[C.sd.spos[s0]];
                 const Bal4 bc = bb[C.sd.spos[s0 + 1]];
-                const u16 dfl = T.acc[C.dslot[i]].flags, cfl = T.acc[C.cslot[i]].flags;
                 u128 amount = 0;
-                res = eval_balances(t, bd, bc, dfl, cfl, &amount);
+                res = eval_balances(k, bd, bc, &amount);
                 if (res == TBGPU_CREATE_TRANSFER_OK) {
                     amt = amount;
-                    if (t.flags & TF_PENDING) dpe = amount; else dpo = amount;
+                    if (k.flags & TF_PENDING) dpe = amount; else dpo = amount;
                 }
             }
         } else {
+            Transfer t = C.ev[i];
+            t.timestamp = k.ts;
             // post_or_void_pending_transfer (src/state_machine.zig:1391-1498)
             u32 p = NONE32;
             for (u32 j = C.pend_last[i]; j != NONE32; j = C.prev_id[j])
@@ -519,7 +531,7 @@ __device__ __forceinline__ bool evaluate_one(const Tables& T, const TrArgs& C, c
         atomicAdd(&C.counters[CNT_DBG + kind], 1u);
         if (res != S.res[i]) atomicAdd(&C.counters[CNT_DBG + 3], 1u);
         if (csi != C.ce[i]) atomicAdd(&C.counters[CNT_DBG + 4], 1u);
-        if (sr == SRES_DYN && !(f & (TF_POST | TF_VOID)) && (T.acc[C.dslot[i]].flags | T.acc[C.cslot[i]].flags) & (AF_DNEC | AF_CNED))
+        if (sr == SRES_DYN && !(f & (TF_POST | TF_VOID)) && (C.core[i].aflags & 0x66))
             atomicAdd(&C.counters[CNT_DBG + 5], 1u);
     }
     // the side records the next pass's balance scan reads (static failures keep the
@@ -748,8 +760,8 @@ __global__ void tr_mask(Tables T, TrArgs C, EvalState S, u8* fres, u8* mask) {
     else r = TBGPU_CREATE_TRANSFER_OK;
     const bool ok = fin_ok(C, S, i);
     bool hist = false;
-    if (ok && !(C.ev[i].flags & (TF_POST | TF_VOID)))
-        hist = (T.acc[C.dslot[i]].flags | T.acc[C.cslot[i]].flags) & AF_HISTORY;
+    if (ok && !(C.core[i].flags & (TF_POST | TF_VOID)))
+        hist = C.core[i].aflags & (AF_HISTORY | AF_HISTORY << 4);
     fres[i] = r;
     mask[i] = (ok ? 1 : 0) | (r != 0 ? 2 : 0) | (hist ? 4 : 0);
 }

@@ -167,10 +167,11 @@ def host_path(eng, w, tts, counts, b0, nbs, torch):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None, help="default 3 (config 5: 14, ~the whole shard)")
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", type=int, default=2, choices=(1, 2, 3, 4),
-                    help="4: 1000 ledgers x 10k accounts with 1%% cross-ledger linked pairs, on one GPU")
+    ap.add_argument("--config", type=int, default=2, choices=(1, 2, 3, 4, 5),
+                    help="4: 1000 ledgers x 10k accounts with 1%% cross-ledger linked pairs, on one GPU; "
+                         "5: 100M accounts, one 1/8 ledger shard of 1B transfers per GPU (generated in HBM)")
     ap.add_argument("--force-general", action="store_true", help="disable the fast path (measure the fixed point)")
     ap.add_argument("--batches-per-step", type=int, default=None,
                     help="default 1000 (config 1/2: a whole BASELINE config-2 run per call), 60 for config 3")
@@ -200,13 +201,20 @@ def main():
 
     if args.batches_per_step is None:
         args.batches_per_step = 60 if args.config == 3 else 1000
+    if args.steps is None:
+        args.steps = 14 if args.config == 5 else 3
     B, K, W = args.batches_per_step, args.steps, args.warmup
-    host_nb = (0, 0) if (args.no_host or world > 1) else \
+    host_nb = (0, 0) if (args.no_host or world > 1 or args.config == 5) else \
         ((args.host_batches or 64, (args.host_batches or 64) * 4) if args.config != 3 else (16, 48))
     n_batches = (K + W) * B + sum(host_nb)
     n_transfers = n_batches * BATCH_MAX
     t_gen = time.time()
-    if args.config == 2:
+    c5 = None
+    if args.config == 5:
+        c5 = workload.config5(shard=rank, shards=8)
+        acc_n = c5.accounts
+        w = None
+    elif args.config == 2:
         acc_n = args.accounts or 1_000_000
         w = workload.config2(transfer_count=n_transfers, account_count=acc_n, seed=42 + rank)
     elif args.config == 4:
@@ -222,18 +230,42 @@ def main():
         w = workload.config1(transfer_count=n_transfers, account_count=acc_n, seed=42 + rank)
     log(f"[rank {rank}] generated {n_transfers} transfers / {acc_n} accounts in {time.time() - t_gen:.1f}s")
 
-    eng = Engine(device=local_rank, accounts_max=acc_n, transfers_max=int(w.transfer_counts.sum()) + 1024,
-                 history_max=int(w.transfer_counts.sum()) + 1024 if args.config == 3 else 1024,
-                 events_per_call_max=B * BATCH_MAX, force_general=args.force_general)
-    ats, tts = w.timestamps()
-    _, rc = eng.create_accounts_batches(ats, w.account_counts, w.accounts)
-    assert int(rc.sum()) == 0, "account creation failed"
-
     dev = torch.device("cuda", local_rank)
-    ev_dev = torch.from_numpy(w.transfers.view(np.uint8)).to(dev)
+    if c5 is not None:
+        # config 5: the load is generated in HBM (workload.DeviceLoad, csrc/loadgen.hip)
+        from tigerbeetle_amd.engine import generate_accounts, generate_transfers
+        counts = c5.transfer_batches()[:n_batches]
+        n_batches = len(counts)
+        ats, tts = c5.timestamps()
+        eng = Engine(device=local_rank, accounts_max=acc_n, transfers_max=int(counts.sum()) + 1024, history_max=1024,
+                     events_per_call_max=B * BATCH_MAX, force_general=args.force_general)
+        ab = c5.account_batches()
+        buf = torch.empty(1221 * BATCH_MAX * 128, dtype=torch.uint8, device=dev)
+        res = torch.empty(1221 * BATCH_MAX * 8, dtype=torch.uint8, device=dev)
+        first = 1
+        for b0 in range(0, len(ab), 1221):
+            cnt = ab[b0:b0 + 1221]
+            generate_accounts(local_rank, first, int(cnt.sum()), c5.accounts_per_ledger, buf.data_ptr())
+            tot, _ = eng.create_accounts_batches_device(ats[b0:b0 + len(cnt)], cnt, buf.data_ptr(), res.data_ptr())
+            assert tot == 0, "account creation failed"
+            first += int(cnt.sum())
+        del buf, res
+        ev_dev = torch.empty(int(counts.sum()) * 128, dtype=torch.uint8, device=dev)
+        generate_transfers(local_rank, c5.first_transfer_id, int(counts.sum()), c5.seed, c5.ledger0, c5.ledgers,
+                           c5.accounts_per_ledger, ev_dev.data_ptr())
+        log(f"[rank {rank}] config 5: {acc_n} accounts created, {int(counts.sum())} transfers generated in HBM "
+            f"in {time.time() - t_gen:.1f}s")
+    else:
+        eng = Engine(device=local_rank, accounts_max=acc_n, transfers_max=int(w.transfer_counts.sum()) + 1024,
+                     history_max=int(w.transfer_counts.sum()) + 1024 if args.config == 3 else 1024,
+                     events_per_call_max=B * BATCH_MAX, force_general=args.force_general)
+        ats, tts = w.timestamps()
+        _, rc = eng.create_accounts_batches(ats, w.account_counts, w.accounts)
+        assert int(rc.sum()) == 0, "account creation failed"
+        ev_dev = torch.from_numpy(w.transfers.view(np.uint8)).to(dev)
+        counts = w.transfer_counts
     res_dev = torch.empty(B * BATCH_MAX * 8, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
-    counts = w.transfer_counts
     ev_base = ev_dev.data_ptr()
     res_ptr = res_dev.data_ptr()
 
@@ -294,8 +326,11 @@ def main():
     dom = int(np.argmax(phase[:len(names)]))
     phase_ms_per_step = {names[i]: round(phase[i] / K, 4) for i in range(len(names))}
     e2e_gbps = value / world * ALGO_BYTES_PER_TRANSFER / 1e9
-    timed = w.transfers[int(counts[:W * B].sum()):int(counts[:(W + K) * B].sum())]
-    n_pv = int(((timed["flags"] & 12) != 0).sum())
+    if w is not None:
+        timed = w.transfers[int(counts[:W * B].sum()):int(counts[:(W + K) * B].sum())]
+        n_pv = int(((timed["flags"] & 12) != 0).sum())
+    else:
+        n_pv = 0  # config 5: plain transfers
     fast = max(paths) == 1 and min(paths) == 1
     if fast:
         commit_ms = phase[names.index("classify")] / K
@@ -331,7 +366,7 @@ def main():
     }
 
     queries = None
-    if rank == 0 and not args.no_queries:
+    if rank == 0 and not args.no_queries and w is not None:
         queries = query_phase(eng, w, acc_n, torch, dev)
 
     host = None
@@ -346,14 +381,30 @@ def main():
         allowed = sorted(os.sched_getaffinity(0))
         core = allowed[min(2, len(allowed) - 1)]
         os.sched_setaffinity(0, {core})
-        orc = oracle.Oracle(acc_n, 4 << 20)
-        orc.create_accounts_batches(ats, w.account_counts, w.accounts)
+        if w is not None:
+            orc = oracle.Oracle(acc_n, 4 << 20)
+            orc.create_accounts_batches(ats, w.account_counts, w.accounts)
+            host_events = w.transfers
+        else:
+            # config 5: the leading 256 batches, with the accounts they touch (a 100M-account
+            # oracle would not fit the sample): their results do not depend on the others
+            from tigerbeetle_amd.types import ACCOUNT_DTYPE, TRANSFER_DTYPE
+            nh = int(counts[:256].sum())
+            host_events = ev_dev[:nh * 128].cpu().numpy().view(TRANSFER_DTYPE)
+            ids = np.unique(np.concatenate([host_events["debit_account_id_lo"], host_events["credit_account_id_lo"]]))
+            acc = np.zeros(len(ids), dtype=ACCOUNT_DTYPE)
+            acc["id_lo"] = ids
+            acc["ledger"] = ((ids - 1) // c5.accounts_per_ledger + 1).astype(np.uint32)
+            acc["code"] = 1
+            orc = oracle.Oracle(len(ids), nh)
+            orc.create_accounts_batches(np.array([ats[-1]], np.uint64), np.array([len(acc)], np.uint32), acc)
         done, spent, b = 0, 0.0, 0
-        while spent < args.cpu_seconds and b < len(counts):
-            k = min(16, len(counts) - b)
+        nb_host = len(counts) if w is not None else 256
+        while spent < args.cpu_seconds and b < nb_host:
+            k = min(16, nb_host - b)
             off = int(counts[:b].sum())
             n = int(counts[b:b + k].sum())
-            _, _, el = orc.create_transfers_batches(tts[b:b + k], counts[b:b + k], w.transfers[off:off + n])
+            _, _, el = orc.create_transfers_batches(tts[b:b + k], counts[b:b + k], host_events[off:off + n])
             done += n
             spent += el
             b += k
@@ -381,7 +432,9 @@ def main():
                                    + {1: "uniform pairs", 2: "Zipf(0.99) pairs on 1 ledger",
                                       3: "flag-heavy mix (limits, two-phase, balancing, chains)",
                                       4: "1000 ledgers, uniform pairs within a ledger, 1% cross-ledger "
-                                         "linked pairs (u128 account ids: the hash index)"}[args.config]
+                                         "linked pairs (u128 account ids: the hash index)",
+                                      5: "1000 ledgers, one 1/8 ledger shard of 1B transfers (the per-GPU shard), "
+                                         "uniform pairs within a ledger, generated in HBM"}[args.config]
                                    + f", {B} x 8190-transfer batches per step (streamed, HBM-resident)",
                        "batches_per_step": B, "transfers_per_step_per_gpu": B * BATCH_MAX,
                        "parallelism": f"ledger-shard x{world}"},

@@ -1,6 +1,6 @@
 #!/bin/bash
 set -o pipefail
-O=gpurun_out/r02h; mkdir -p $O
+O=gpurun_out/r02j; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -s --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1; rc=$?; echo "tests rc=$rc"; tail -3 $O/gpu_tests.log
 [ $rc -eq 0 ] || exit 1

@@ -219,14 +219,16 @@ __global__ void bs_final(SideScanArgs A, u64 m, u32 invalid, const Bal4* __restr
 }
 
 // --------------------------------------------------------- fused scan ----
-// One launch per pass: a workgroup of BF_THREADS sides (one per thread) finds the
-// balance carried into its tile from the previous tile alone -- the tail of the
-// account segment that crosses the boundary, which starts inside the previous tile
-// unless a segment is longer than BF_THREADS sides -- then scans its own tile.  No
-// tile aggregates, no second launch, no single-workgroup tile scan.  A segment
-// longer than the window raises halt[1] (the host redoes the pass with the
-// three-launch scan above).
+// One launch per pass.  Tiles are cut at account boundaries: tile t holds the
+// accounts whose first side lies in [t*BF_TILE, (t+1)*BF_TILE) (tstart[t], found
+// once per chunk by tr_side_pos), so no balance carries from one tile to the next
+// and a workgroup scans its tile alone: at most 2*BF_TILE sides while no account
+// has more than BF_TILE sides in the chunk.  An account with more (no account
+// starts in some window) raises halt[1]: the host redoes the pass with the
+// three-launch scan above.
 constexpr int BF_THREADS = 256;
+constexpr int BF_IPT = 2;                     // sides per thread
+constexpr int BF_TILE = BF_THREADS;           // nominal tile (sides): the 2x slack covers the last account
 
 __device__ __forceinline__ u64 shup(u64 v, int off) { return (u64)__shfl_up((unsigned long long)v, off); }
 __device__ __forceinline__ u128 shup128(u128 v, int off) {
@@ -241,123 +243,131 @@ __device__ __forceinline__ Bal4 shup_bal(const Bal4& b, int off) {
     return r;
 }
 
-// Exclusive segmented scan of one element per thread over the workgroup: wave
-// scans by shuffles, the four wave totals through LDS.
-template <bool HAS_H>
-__device__ SE block_excl_waves(SE v, SE* wtot) {
+// Exclusive segmented scan (F only) of one element per thread over the workgroup:
+// wave scans by shuffles, the four wave totals through LDS.
+struct SF {
+    Bal4 F;
+    u32 fl;
+};
+__device__ __forceinline__ SF combine_f(const SF& a, const SF& b) {
+    SF c;
+    c.F = (b.fl & 1) ? b.F : add(a.F, b.F);
+    c.fl = a.fl | b.fl;
+    return c;
+}
+__device__ SF block_excl_f(SF v, SF* wtot) {
     const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int off = 1; off < 64; off <<= 1) {
-        SE o;
+        SF o;
         o.F = shup_bal(v.F, off);
-        if (HAS_H) o.H = shup_bal(v.H, off);
         o.fl = __shfl_up(v.fl, off);
-        if (lane >= (u32)off) v = combine<HAS_H>(o, v);
+        if (lane >= (u32)off) v = combine_f(o, v);
     }
-    // v is inclusive; exclusive by one more shift
-    SE ex;
+    SF ex;
     ex.F = shup_bal(v.F, 1);
-    if (HAS_H) ex.H = shup_bal(v.H, 1);
     ex.fl = __shfl_up(v.fl, 1);
-    if (lane == 0) ex = identity<HAS_H>();
+    if (lane == 0) { zero(ex.F); ex.fl = 0; }
     if (lane == 63) wtot[w] = v;
     __syncthreads();
-    SE pre = identity<HAS_H>();
-    for (u32 k = 0; k < w; k++) pre = combine<HAS_H>(pre, wtot[k]);
-    __syncthreads();
-    return combine<HAS_H>(pre, ex);
+    SF pre;
+    zero(pre.F);
+    pre.fl = 0;
+    for (u32 k = 0; k < w; k++) pre = combine_f(pre, wtot[k]);
+    return combine_f(pre, ex);
 }
 
-__device__ __forceinline__ u32 block_max(u32 v, u32* sh) {
-    for (int off = 32; off > 0; off >>= 1) v = max(v, (u32)__shfl_xor(v, off));
-    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
-    __syncthreads();
-    v = sh[0];
-    for (int k = 1; k < BF_THREADS / 64; k++) v = max(v, sh[k]);
-    __syncthreads();
-    return v;
+// A sorted side's contributions: to F (final-ok), or to H (evaluated-ok in a chain
+// that does not persist: visible only to later members of its chain).
+__device__ __forceinline__ void side_contrib(const SideScanArgs& A, u64 q, Bal4* F, Bal4* H) {
+    zero(*F);
+    zero(*H);
+    if (!(A.sq_ok[q] & 1)) return;
+    const u128 dpe = A.sq_dpend[q], dpo = A.sq_dpost[q];
+    Bal4* t = side_final(A, q) ? F : H;
+    if (A.sq_ev[q] >> 31) { t->cp = dpe; t->cpo = dpo; } else { t->dp = dpe; t->dpo = dpo; }
 }
 
-__device__ __forceinline__ u128 wave_sum128(u128 v) {
-    u64 lo = (u64)v, hi = (u64)(v >> 64);
-    for (int off = 32; off > 0; off >>= 1) {
-        const u64 l2 = (u64)__shfl_xor((unsigned long long)lo, off), h2 = (u64)__shfl_xor((unsigned long long)hi, off);
-        const u64 s = lo + l2;
-        hi = hi + h2 + (s < lo ? 1 : 0);
-        lo = s;
-    }
-    return ((u128)hi << 64) | lo;
-}
-__device__ __forceinline__ Bal4 block_sum_bal(Bal4 b, Bal4* sh) {
-    b.dp = wave_sum128(b.dp);
-    b.dpo = wave_sum128(b.dpo);
-    b.cp = wave_sum128(b.cp);
-    b.cpo = wave_sum128(b.cpo);
-    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = b;
-    __syncthreads();
-    Bal4 r = sh[0];
-    for (int k = 1; k < BF_THREADS / 64; k++) r = add(r, sh[k]);
-    __syncthreads();
-    return r;
-}
-
-template <bool HAS_H>
-__global__ __launch_bounds__(BF_THREADS) void bs_fused(SideScanArgs A, u64 m, u32 invalid, u32* long_flag,
-                                                       const Account* __restrict__ acc, Bal4* __restrict__ bb) {
+// F is scanned (segmented by account); H, non-zero only behind earlier members of
+// the side's own chain on the same account -- the sides right before it in sorted
+// order -- is summed by walking back over that run, staged in LDS.
+__global__ __launch_bounds__(BF_THREADS) void bs_fused(SideScanArgs A, u64 m, u32 invalid, const u32* __restrict__ tstart,
+                                                       u32 ntiles, u32* long_flag, const Account* __restrict__ acc,
+                                                       Bal4* __restrict__ bb) {
     if (!gate_open(A.gate)) return;
-    __shared__ SE wtot[BF_THREADS / 64];
-    __shared__ Bal4 bsum[BF_THREADS / 64];
-    __shared__ u32 umax[BF_THREADS / 64];
+    __shared__ SF wtot[BF_THREADS / 64];
+    __shared__ u32 s_key[BF_THREADS * BF_IPT], s_cs[BF_THREADS * BF_IPT];
+    __shared__ Bal4 s_h[BF_THREADS * BF_IPT];
     // the next state's per-chain first failures start at "none"
     if (A.cfail_clear)
         for (u64 k = (u64)blockIdx.x * BF_THREADS + threadIdx.x; k < A.n; k += (u64)gridDim.x * BF_THREADS)
             A.cfail_clear[k] = NONE32;
-    const u64 q0 = (u64)blockIdx.x * BF_THREADS;
-    const u64 q = q0 + threadIdx.x;
-    // 1. the carry: the tail, in the previous tile, of the segment that crosses into this one
-    SE carry = identity<HAS_H>();
-    const u32 K = q0 > 0 ? A.skey[q0 - 1] : invalid;
-    if (K < invalid) {
-        const u64 p = q0 - BF_THREADS + threadIdx.x;  // q0 >= BF_THREADS here
-        SE e = load_elem<HAS_H>(A, p, invalid);
-        const bool mine = A.skey[p] == K;
-        const u32 fs = block_max(mine && (e.fl & 1) ? (u32)threadIdx.x + 1 : 0u, umax);
-        const u32 hs = block_max(mine && (e.fl & 2) ? (u32)threadIdx.x + 1 : 0u, umax);
-        if (fs == 0) {  // the segment started before the previous tile
-            if (threadIdx.x == 0) atomicMax(long_flag, A.gate.p + 1);
-            return;
-        }
-        Bal4 z;
-        zero(z);
-        carry.F = block_sum_bal(mine && threadIdx.x + 1 >= fs ? e.F : z, bsum);
-        if (HAS_H) carry.H = block_sum_bal(mine && threadIdx.x + 1 >= hs ? e.H : z, bsum);
+    const u32 t = blockIdx.x, tid = threadIdx.x;
+    const u32 a0 = tstart[t];
+    if (a0 == NONE32) return;  // no account starts in this window: the previous tile has its sides
+    u32 b0 = (u32)m;
+    for (u32 k = t + 1; k < ntiles; k++)
+        if (tstart[k] != NONE32) { b0 = tstart[k]; break; }
+    if (b0 - a0 > BF_THREADS * BF_IPT) {  // an account longer than a window
+        if (tid == 0) atomicMax(long_flag, A.gate.p + 1);
+        return;
     }
-    // 2. this tile
-    SE e = q < m ? load_elem<HAS_H>(A, q, invalid) : identity<HAS_H>();
-    if (q >= m) e.fl = 3;
-    SE run = combine<HAS_H>(carry, block_excl_waves<HAS_H>(e, wtot));
-    if (q >= m) return;
-    const u32 key = A.skey[q];
-    if (key >= invalid) return;
-    const Account& a = acc[key];
-    Bal4 out;
-    out.dp = a.debits_pending;
-    out.dpo = a.debits_posted;
-    out.cp = a.credits_pending;
-    out.cpo = a.credits_posted;
-    if (!(e.fl & 1)) out = add(out, run.F);
-    if (HAS_H && !(e.fl & 2)) out = add(out, run.H);
-    bb[q] = out;
+    // the thread's two sides (contiguous), loaded before any barrier
+    const u64 qa = (u64)a0 + BF_IPT * tid;
+    u32 key[BF_IPT], cs[BF_IPT];
+    Bal4 f[BF_IPT], h[BF_IPT];
+    SF e[BF_IPT];
+#pragma unroll
+    for (int k = 0; k < BF_IPT; k++) {
+        const u64 q = qa + k;
+        const bool v = q < b0;
+        key[k] = v ? A.skey[q] : invalid;
+        cs[k] = v ? (A.sq_cs[q] & SQ_CS) : NONE32;
+        zero(f[k]);
+        zero(h[k]);
+        e[k].fl = 1;
+        if (key[k] < invalid) {
+            side_contrib(A, q, &f[k], &h[k]);
+            e[k].fl = (q == a0 || A.skey[q - 1] != key[k]) ? 1u : 0u;
+        }
+        e[k].F = f[k];
+        s_key[BF_IPT * tid + k] = key[k];
+        s_cs[BF_IPT * tid + k] = cs[k];
+        s_h[BF_IPT * tid + k] = h[k];
+    }
+    const SF agg = combine_f(e[0], e[1]);
+    SF run = block_excl_f(agg, wtot);  // (its barrier publishes s_key / s_cs / s_h)
+#pragma unroll
+    for (int k = 0; k < BF_IPT; k++) {
+        const u64 q = qa + k;
+        if (key[k] < invalid) {
+            Bal4 H;
+            zero(H);
+            u32 j = BF_IPT * tid + k;
+            while (j > 0 && s_key[j - 1] == key[k] && s_cs[j - 1] == cs[k]) H = add(H, s_h[--j]);
+            const Account& ac = acc[key[k]];
+            Bal4 out;
+            out.dp = ac.debits_pending;
+            out.dpo = ac.debits_posted;
+            out.cp = ac.credits_pending;
+            out.cpo = ac.credits_posted;
+            if (!(e[k].fl & 1)) out = add(out, run.F);
+            bb[q] = add(out, H);
+        }
+        run = combine_f(run, e[k]);
+    }
 }
 
 }  // namespace
 
-void side_scan_fused(const SideScanArgs& A, u64 m, u32 invalid, u32* long_flag, const Account* acc, Bal4* bb,
-                     hipStream_t stream) {
+void side_scan_fused(const SideScanArgs& A, u64 m, u32 invalid, const u32* tstart, u32* long_flag,
+                     const Account* acc, Bal4* bb, hipStream_t stream) {
     if (m == 0) return;
-    bs_fused<true><<<(u32)((m + BF_THREADS - 1) / BF_THREADS), BF_THREADS, 0, stream>>>(A, m, invalid, long_flag,
-                                                                                        acc, bb);
+    const u32 ntiles = (u32)((m + BF_TILE - 1) / BF_TILE);
+    bs_fused<<<ntiles, BF_THREADS, 0, stream>>>(A, m, invalid, tstart, ntiles, long_flag, acc, bb);
     HIP_CHECK(hipGetLastError());
 }
+
+u32 side_scan_fused_tile() { return BF_TILE; }
 
 u64 side_scan_tile_bytes(u64 capacity) { return ((capacity + BS_TILE - 1) / BS_TILE + 1) * sizeof(SE); }
 

@@ -77,8 +77,6 @@ struct EvalState {
     u32* cfail;  // per chain start: first failing member (NONE32 = none)
     u128* amt;   // effective amount (balancing clamp / post amount)
     u128* pamt;  // pending transfer amount (post/void)
-    u128* dpend; // side delta on the *_pending balance (two's complement for void/post)
-    u128* dpost; // side delta on the *_posted balance
 };
 
 // Pass gate of the fixed point: the kernels of pass p run while the previous
@@ -126,6 +124,9 @@ struct Sides {
     u8* sq_ok;        // [m] sorted, per pass: the side's effect is evaluated-ok
     u128* sq_dpend;   // [m] sorted, per pass: its delta on the *_pending balance
     u128* sq_dpost;   // [m] sorted, per pass: its delta on the *_posted balance
+    u32* tstart;      // [m / tile + 1] first account start in each fused-scan window (NONE32: none)
+    u32 tile;         // the fused scan's window (sides)
+    u32 inert;        // the key of sides that touch no account (each stands alone)
 };
 constexpr u32 SQ_STANDALONE = 1u << 31, SQ_DOOM = 1u << 30, SQ_CS = (1u << 30) - 1;
 
@@ -155,8 +156,9 @@ void side_scan(const SideScanArgs& A, u64 m, u32 invalid, bool has_chains, void*
                Bal4* bb, hipStream_t stream);
 // One-launch form (balances.hip bs_fused): raises *long_flag (= pass + 1) and leaves
 // the pass incomplete when an account segment is longer than its window.
-void side_scan_fused(const SideScanArgs& A, u64 m, u32 invalid, u32* long_flag, const Account* acc, Bal4* bb,
-                     hipStream_t stream);
+void side_scan_fused(const SideScanArgs& A, u64 m, u32 invalid, const u32* tstart, u32* long_flag,
+                     const Account* acc, Bal4* bb, hipStream_t stream);
+u32 side_scan_fused_tile();
 void side_final_balances(const SideScanArgs& A, u64 m, u32 invalid, const Bal4* bb, Account* acc, u32* big,
                          hipStream_t stream);
 

@@ -81,6 +81,7 @@ struct tbgpu_ctx {
     u32 *skey, *sval, *skey_s, *sval_s, *spos;
     u32 *soff, *sev, *scand, *sq_ev, *sq_cs;
     EvCore* core = nullptr;
+    u32* tstart = nullptr;
     u8* sq_ok = nullptr;
     u128 *sq_dpend = nullptr, *sq_dpost = nullptr;
     u32 *gkey_s, *gsorted;  // the id-group sort's output (the members of each id group, by event)
@@ -168,8 +169,6 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
         s.cfail = dalloc<u32>(n, &B);
         s.amt = dalloc<u128>(n, &B);
         s.pamt = dalloc<u128>(n, &B);
-        s.dpend = dalloc<u128>(n, &B);
-        s.dpost = dalloc<u128>(n, &B);
     }
     c->scap = m;
     c->skey = dalloc<u32>(m, &B);
@@ -179,6 +178,7 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->spos = dalloc<u32>(m, &B);
     c->soff = dalloc<u32>(n + 1, &B);
     c->core = dalloc<EvCore>(n, &B);
+    c->tstart = dalloc<u32>(m / side_scan_fused_tile() + 2, &B);
     c->sev = dalloc<u32>(m, &B);
     c->scand = dalloc<u32>(m, &B);
     c->sq_ev = dalloc<u32>(m, &B);
@@ -333,7 +333,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
                     c->b_start, c->b_ts, c->ts, c->cs, c->ce, c->sres, c->dslot, c->cslot, c->pre_e, c->pre_p,
                     c->pp_dslot, c->pp_cslot, c->gslot, c->pslot, c->prev_id, c->pend_last, c->pend_first, c->prev_pend,
                     c->gclaim, c->gcnt_id, c->gcnt_pd, c->gmem, c->gbeg, c->gend, c->skey, c->sval, c->skey_s,
-                    c->soff, c->core, c->sev, c->scand, c->sq_ev, c->sq_cs, c->sq_ok, c->sq_dpend, c->sq_dpost, c->gkey_s,
+                    c->soff, c->core, c->tstart, c->sev, c->scand, c->sq_ev, c->sq_cs, c->sq_ok, c->sq_dpend, c->sq_dpost, c->gkey_s,
                     c->gsorted,
                     c->sval_s, c->spos, c->bb, c->ss.keys_tmp, c->ss.vals_tmp, c->ss.hist, c->side_tiles,
                     c->sc.tile_sums, c->fres, c->mask, c->ranks, c->res_buf, c->counts, c->counters, c->status,
@@ -342,7 +342,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
                     c->q_tval, c->q_ss.keys_tmp, c->q_ss.vals_tmp, c->q_ss.hist, c->q_runs_dev, c->ximp};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     for (EvalState& s : c->st) {
-        void* q[] = {s.res, s.ok, s.pref, s.cfail, s.amt, s.pamt, s.dpend, s.dpost};
+        void* q[] = {s.res, s.ok, s.pref, s.cfail, s.amt, s.pamt};
         for (void* p : q) if (p) (void)hipFree(p);
     }
     if (c->h_counters) (void)hipHostFree(c->h_counters);
@@ -393,7 +393,13 @@ static void ensure_h_rc(tbgpu_ctx* c, u64 nb) {
 // The fixed point's passes grow with the dependency depth of a call, which grows
 // with its batch count; calls that need it are cut into chunks of at most this
 // many batches (the streaming semantics are those of consecutive calls anyway).
-constexpr u32 GENERAL_CHUNK_BATCHES = 16;
+static u32 general_chunk_batches() {
+    static const u32 v = [] {  // TBGPU_CHUNK_BATCHES: experiments only
+        const char* e = getenv("TBGPU_CHUNK_BATCHES");
+        return e ? (u32)strtoul(e, nullptr, 0) : 16u;
+    }();
+    return v;
+}
 
 static u32 chunk_end(const tbgpu_ctx* c, const uint32_t* counts, u32 b0, u32 nb, u32 max_batches = ~0u) {
     u64 ev = 0;
@@ -449,6 +455,9 @@ static TrArgs make_tr_args(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb) {
     C.sd.soff = c->soff; C.sd.sev = c->sev; C.sd.scand = c->scand; C.sd.spos = c->spos; C.sd.skey_s = c->skey_s;
     C.sd.sq_ev = c->sq_ev; C.sd.sq_cs = c->sq_cs; C.sd.sq_ok = c->sq_ok; C.sd.sq_dpend = c->sq_dpend;
     C.sd.sq_dpost = c->sq_dpost;
+    C.sd.tstart = c->tstart;
+    C.sd.tile = side_scan_fused_tile();
+    C.sd.inert = (u32)c->accounts_max;
     // group table sized for this call: >= 2x the keys (ids + pending ids <= 2n)
     const u64 g = std::min<u64>(c->gcap, pow2_at_least(4ull * std::max<u32>(n, 1)));
     C.gmask = g - 1;
@@ -588,7 +597,7 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n) {
             SA.cfail_clear = D.cfail;
             SA.gate = G;
             if (c->long_segments) side_scan(SA, m, inv_acc, chains, c->side_tiles, c->T.acc, c->bb, s);
-            else side_scan_fused(SA, m, inv_acc, c->counters + CNT_LONG, c->T.acc, c->bb, s);
+            else side_scan_fused(SA, m, inv_acc, c->tstart, c->counters + CNT_LONG, c->T.acc, c->bb, s);
             tr_launch_evaluate(c->T, C, S, D, c->bb, G, chg + (q + 1) % PC_RING, front + (q + 1) % PC_RING,
                                chg + (q + 2) % PC_RING, front + (q + 2) % PC_RING, s);
         }
@@ -706,7 +715,7 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         // chunks, and the fast attempt only every 8th (it undoes itself when it fails).
         // A dry run must stay one call (its chunks cannot see each other's effects).
         const bool small = !c->rt_dry && (b0 < small_until || c->slow_chunks > 0);
-        const u32 b1 = chunk_end(c, counts, b0, nb_total, small ? GENERAL_CHUNK_BATCHES : ~0u);
+        const u32 b1 = chunk_end(c, counts, b0, nb_total, small ? general_chunk_batches() : ~0u);
         const u32 nb = b1 - b0;
         prof_mark(c, PH_UPLOAD);
         upload_batches(c, timestamps + b0, counts + b0, nb, starts);
@@ -740,7 +749,7 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         tbgpu_create_transfers_result_t* rdev = dst_device ? results : (tbgpu_create_transfers_result_t*)c->res_buf;
         const bool try_fast_path = c->slow_chunks % 8 == 0;
         if (!run_transfers_chunk(c, ev, n, nb, rdev, try_fast_path,
-                                 /*split=*/!c->rt_dry && nb > GENERAL_CHUNK_BATCHES)) {
+                                 /*split=*/!c->rt_dry && nb > general_chunk_batches())) {
             small_until = b1;  // redo these batches in small chunks, on the general path
             c->slow_chunks = 1;
             continue;
@@ -939,9 +948,9 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
     c->n_accounts += tot.x;
 }
 
-extern "C" uint64_t tbgpu_create_accounts_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t* timestamps,
-                                                  const uint32_t* counts, const tbgpu_account_t* events,
-                                                  tbgpu_create_accounts_result_t* results, uint32_t* result_counts) {
+static uint64_t accounts_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t* timestamps, const uint32_t* counts,
+                                 const Account* events, bool device, tbgpu_create_accounts_result_t* results,
+                                 uint32_t* result_counts) {
     HIP_CHECK(hipSetDevice(c->device));
     std::vector<u32> starts;
     u64 total = 0, ev_off = 0;
@@ -950,15 +959,40 @@ extern "C" uint64_t tbgpu_create_accounts_batches(tbgpu_ctx* c, uint32_t nb_tota
         const u32 nb = b1 - b0;
         upload_batches(c, timestamps + b0, counts + b0, nb, starts);
         const u32 n = starts[nb];
-        HIP_CHECK(hipMemcpyAsync(c->ev_buf, events + ev_off, (u64)n * 128, hipMemcpyHostToDevice, c->stream));
-        run_accounts_chunk(c, (const Account*)c->ev_buf, n, nb, (tbgpu_create_accounts_result_t*)c->res_buf,
-                           result_counts + b0);
-        copy_results_to_batches(c, nb, starts, result_counts + b0, (u8*)(results + ev_off));
-        for (u32 b = 0; b < nb; b++) total += result_counts[b0 + b];
+        const Account* ev = events + ev_off;
+        if (!device) {
+            HIP_CHECK(hipMemcpyAsync(c->ev_buf, ev, (u64)n * 128, hipMemcpyHostToDevice, c->stream));
+            ev = (const Account*)c->ev_buf;
+        }
+        run_accounts_chunk(c, ev, n, nb, (tbgpu_create_accounts_result_t*)c->res_buf, result_counts + b0);
+        u64 chunk_total = 0;
+        for (u32 b = 0; b < nb; b++) chunk_total += result_counts[b0 + b];
+        if (device) {  // replies concatenated in device memory, as for create_transfers
+            if (chunk_total)
+                HIP_CHECK(hipMemcpyAsync(results + total, c->res_buf, chunk_total * 8, hipMemcpyDeviceToDevice,
+                                         c->stream));
+        } else {
+            copy_results_to_batches(c, nb, starts, result_counts + b0, (u8*)(results + ev_off));
+        }
+        total += chunk_total;
         ev_off += n;
         b0 = b1;
     }
+    HIP_CHECK(hipStreamSynchronize(c->stream));
     return total;
+}
+
+extern "C" uint64_t tbgpu_create_accounts_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t* timestamps,
+                                                  const uint32_t* counts, const tbgpu_account_t* events,
+                                                  tbgpu_create_accounts_result_t* results, uint32_t* result_counts) {
+    return accounts_batches(c, nb_total, timestamps, counts, (const Account*)events, false, results, result_counts);
+}
+
+extern "C" uint64_t tbgpu_create_accounts_batches_device(tbgpu_ctx* c, uint32_t nb_total, const uint64_t* timestamps,
+                                                         const uint32_t* counts, const void* events_device,
+                                                         void* results_device, uint32_t* result_counts) {
+    return accounts_batches(c, nb_total, timestamps, counts, (const Account*)events_device, true,
+                            (tbgpu_create_accounts_result_t*)results_device, result_counts);
 }
 
 extern "C" uint32_t tbgpu_create_accounts(tbgpu_ctx* c, uint64_t timestamp, const tbgpu_account_t* events,

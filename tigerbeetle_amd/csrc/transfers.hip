@@ -521,8 +521,6 @@ __device__ __forceinline__ bool evaluate_one(const Tables& T, const TrArgs& C, c
     D.amt[i] = amt;
     D.pamt[i] = pamt;
     D.pref[i] = pref;
-    D.dpend[i] = dpe;
-    D.dpost[i] = dpo;
     if (res != TBGPU_CREATE_TRANSFER_OK && csi != C.ce[i]) atomicMin(&D.cfail[csi], i);
     const bool changed = res != S.res[i] || amt != S.amt[i] || pamt != S.pamt[i] || pref != S.pref[i];
     if (C.debug && changed) {
@@ -607,9 +605,25 @@ __global__ void tr_init(Tables T, TrArgs C, EvalState D) {
     D.amt[i] = amt;
     D.pamt[i] = pamt;
     D.pref[i] = pref;
-    D.dpend[i] = dpe;
-    D.dpost[i] = dpo;
     if (res != 0 && C.cs[i] != C.ce[i]) atomicMin(&D.cfail[C.cs[i]], i);
+}
+
+// An accepted event's balance deltas (pending, posted) from its state: a transfer
+// adds its amount to the pending or posted balances (src/state_machine.zig:1330-1340);
+// a post/void releases the pending amount and a post adds the posted amount
+// (:1470-1486).  Two's complement: a void or post is a subtraction.
+__device__ __forceinline__ void state_deltas(const TrArgs& C, const EvalState& S, u32 i, u128* dpe, u128* dpo) {
+    *dpe = *dpo = 0;
+    if (!(S.ok[i] & 1)) return;
+    const u16 f = C.core[i].flags;
+    if (f & (TF_POST | TF_VOID)) {
+        *dpe = (u128)0 - S.pamt[i];
+        *dpo = (f & TF_POST) ? S.amt[i] : 0;
+    } else if (f & TF_PENDING) {
+        *dpe = S.amt[i];
+    } else {
+        *dpo = S.amt[i];
+    }
 }
 
 // ------------------------------------------------------------------ sides ----
@@ -716,6 +730,9 @@ __global__ void tr_side_pos(TrArgs C, const u32* sval_s, u64 m) {
     const u32 cs = C.cs[i], ce = C.ce[i];
     const bool doom = C.ctl && (C.ctl[ce] & TBGPU_CTL_DOOM);
     C.sd.sq_cs[q] = cs | (cs == ce ? SQ_STANDALONE : 0u) | (doom ? SQ_DOOM : 0u);
+    // account starts, for the fused scan's windows (inert sides each stand alone)
+    const u32 key = C.sd.skey_s[q];
+    if (q == 0 || key != C.sd.skey_s[q - 1] || key == C.sd.inert) atomicMin(&C.sd.tstart[q / C.sd.tile], (u32)q);
 }
 
 // Write event i's side records (sorted order) for its outcome: the debit and credit
@@ -738,7 +755,9 @@ __device__ __forceinline__ bool write_sides(const TrArgs& C, u32 i, bool pv, boo
 __global__ void tr_side_rec(TrArgs C, EvalState S) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= C.n) return;
-    write_sides(C, i, is_post_void(C, i), S.ok[i] & 1, S.pref[i], S.dpend[i], S.dpost[i]);
+    u128 dpe, dpo;
+    state_deltas(C, S, i, &dpe, &dpo);
+    write_sides(C, i, is_post_void(C, i), S.ok[i] & 1, S.pref[i], dpe, dpo);
 }
 
 // ---------------------------------------------------------------- apply ----
@@ -805,8 +824,10 @@ __global__ void tr_apply(Tables T, TrArgs C, EvalState S, const u8* __restrict__
             // balances after this transfer (src/state_machine.zig:1342-1364)
             const u32 s0 = C.sd.soff[i];
             Bal4 d = bb[C.sd.spos[s0]], c = bb[C.sd.spos[s0 + 1]];
-            d.dp += S.dpend[i]; d.dpo += S.dpost[i];
-            c.cp += S.dpend[i]; c.cpo += S.dpost[i];
+            u128 dpe, dpo;
+            state_deltas(C, S, i, &dpe, &dpo);
+            d.dp += dpe; d.dpo += dpo;
+            c.cp += dpe; c.cpo += dpo;
             History h;
             memset(&h, 0, sizeof h);
             h.timestamp = s.timestamp;
@@ -961,6 +982,7 @@ void tr_launch_side_build(const TrArgs& C, const EvalState& S, u32 kmax, const u
     tr_side_build<<<GRID(C.n + 1)>>>(C, S, kmax, pairs, invalid, skey, sval);
 }
 void tr_launch_side_pos(const TrArgs& C, const u32* sval_s, u64 m, hipStream_t stream) {
+    HIP_CHECK(hipMemsetAsync(C.sd.tstart, 0xFF, ((m + C.sd.tile - 1) / C.sd.tile + 1) * sizeof(u32), stream));
     tr_side_pos<<<GRID(m)>>>(C, sval_s, m);
 }
 void tr_launch_side_rec(const TrArgs& C, const EvalState& S, hipStream_t stream) {

@@ -78,7 +78,7 @@ def lib():
         getattr(L, name).restype = u32
         getattr(L, name).argtypes = [vp, u64, vp, u32, vp]
     for name in ("tbgpu_create_transfers_batches", "tbgpu_create_accounts_batches",
-                 "tbgpu_create_transfers_batches_device"):
+                 "tbgpu_create_transfers_batches_device", "tbgpu_create_accounts_batches_device"):
         getattr(L, name).restype = u64
         getattr(L, name).argtypes = [vp, u32, vp, vp, vp, vp, vp]
     for name in ("tbgpu_lookup_accounts", "tbgpu_lookup_transfers"):
@@ -122,6 +122,10 @@ def lib():
     for name in ("tbgpu_get_account_transfers_device", "tbgpu_get_account_history_device"):
         getattr(L, name).restype = u64
         getattr(L, name).argtypes = [vp, u32, vp, u32, vp, vp]
+    L.tbgpu_bench_generate_accounts.restype = ctypes.c_int
+    L.tbgpu_bench_generate_accounts.argtypes = [ctypes.c_int, u64, u64, u32, vp]
+    L.tbgpu_bench_generate_transfers.restype = ctypes.c_int
+    L.tbgpu_bench_generate_transfers.argtypes = [ctypes.c_int, u64, u64, u64, u32, u32, u32, vp]
     L.tbgpu_last_error.restype = ctypes.c_int
     L.tbgpu_last_error.argtypes = [vp, ctypes.c_char_p, u32]
     _lib = L
@@ -241,6 +245,15 @@ class Engine:
     def advance_commit_timestamp(self, ts: int) -> None:
         self._L.tbgpu_advance_commit_timestamp(self._h, int(ts))
 
+    def create_accounts_batches_device(self, timestamps, counts, events_ptr: int, results_ptr: int):
+        ts = np.ascontiguousarray(timestamps, dtype=np.uint64)
+        cs = np.ascontiguousarray(counts, dtype=np.uint32)
+        rc = np.zeros(len(cs), dtype=np.uint32)
+        total = self._L.tbgpu_create_accounts_batches_device(self._h, len(cs), _ptr(ts), _ptr(cs),
+                                                             ctypes.c_void_p(events_ptr),
+                                                             ctypes.c_void_p(results_ptr), _ptr(rc))
+        return total, rc
+
     def create_accounts_batches(self, timestamps, counts, events):
         ts = np.ascontiguousarray(timestamps, dtype=np.uint64)
         cs = np.ascontiguousarray(counts, dtype=np.uint32)
@@ -344,3 +357,19 @@ class Engine:
         s = Stats()
         self._L.tbgpu_last_stats(self._h, ctypes.byref(s))
         return s
+
+
+def generate_accounts(device: int, first_id: int, count: int, accounts_per_ledger: int, out_ptr: int) -> None:
+    """The benchmark's accounts in device memory (tbgpu_bench_generate_accounts)."""
+    rc = lib().tbgpu_bench_generate_accounts(device, first_id, count, accounts_per_ledger, ctypes.c_void_p(out_ptr))
+    if rc != 0:
+        raise RuntimeError(f"tbgpu_bench_generate_accounts failed ({rc})")
+
+
+def generate_transfers(device: int, first_id: int, count: int, seed: int, ledger0: int, ledgers: int,
+                       accounts_per_ledger: int, out_ptr: int) -> None:
+    """The benchmark's transfers in device memory (tbgpu_bench_generate_transfers)."""
+    rc = lib().tbgpu_bench_generate_transfers(device, first_id, count, seed, ledger0, ledgers, accounts_per_ledger,
+                                              ctypes.c_void_p(out_ptr))
+    if rc != 0:
+        raise RuntimeError(f"tbgpu_bench_generate_transfers failed ({rc})")

@@ -10,6 +10,8 @@ config 3  flag-heavy mix: limit accounts, pending / post / void, balancing,
           linked chains, duplicate ids and invalid fields, periodic ticks.
 config 4  1000 ledgers x 10k accounts, uniform pairs within a ledger, 1%
           cross-ledger linked pairs (ledger-sharded across GPUs).
+config 5  100M accounts over 1000 ledgers, 1B transfers over 8 ledger shards,
+          generated in HBM (DeviceLoad: the load is too large for the host).
 
 The reference draws from Zig's std.rand; only the *distributions* are
 reproduced (numpy PCG64 streams, seed 42 by default).  Timestamps follow the
@@ -516,6 +518,50 @@ def config3_stress(batches: int = 200, batch: int = BATCH_MAX, account_count: in
     transfers = np.concatenate(out)
     return Workload("config3_stress", accounts, _batches(account_count), transfers,
                     np.array(counts, dtype=np.uint32), ticks)
+
+
+@dataclass
+class DeviceLoad:
+    """BASELINE config 5's load for one ledger shard, generated in HBM by the engine's
+    counter-based generator (engine.generate_accounts / generate_transfers,
+    csrc/loadgen.hip): record i depends only on (seed, first id + i).
+
+    100M accounts over 1000 ledgers (ids 1..100M, ledger (id - 1) / 100k + 1,
+    every shard holds them all: the replicated account directory of the sharded
+    design), 1B transfers split evenly over `shards` ledger shards: shard s draws
+    its transfers from ledgers [ledger0, ledger0 + ledgers), uniform distinct
+    debit / credit accounts within a ledger, amount floor(Exp(1) * 10000) + 1 --
+    the `tigerbeetle benchmark` distribution (src/tigerbeetle/benchmark_load.zig:
+    266-330) within each ledger."""
+    accounts: int
+    accounts_per_ledger: int
+    ledger0: int
+    ledgers: int
+    transfers: int
+    seed: int
+    first_transfer_id: int = 1
+
+    def account_batches(self, batch: int = BATCH_MAX) -> np.ndarray:
+        return _batches(self.accounts, batch)
+
+    def transfer_batches(self, batch: int = BATCH_MAX) -> np.ndarray:
+        return _batches(self.transfers, batch)
+
+    def timestamps(self, batch: int = BATCH_MAX):
+        """Commit timestamps of the account batches then the transfer batches (the
+        reference harness rule, as Workload.timestamps)."""
+        ac, tc = self.account_batches(batch).astype(np.uint64), self.transfer_batches(batch).astype(np.uint64)
+        acc_ts = np.cumsum(ac + np.uint64(1))
+        tr_ts = acc_ts[-1] + np.cumsum(tc + np.uint64(1))
+        return acc_ts, tr_ts
+
+
+def config5(shard: int = 0, shards: int = 8, accounts: int = 100_000_000, ledgers: int = 1000,
+            transfers_total: int = 1_000_000_000, seed: int = 42) -> DeviceLoad:
+    per = ledgers // shards
+    return DeviceLoad(accounts=accounts, accounts_per_ledger=accounts // ledgers, ledger0=shard * per + 1,
+                      ledgers=per, transfers=transfers_total // shards, seed=seed + shard,
+                      first_transfer_id=shard * (transfers_total // shards) + 1)
 
 
 def make(config: int, **kw) -> Workload:

@@ -370,7 +370,7 @@ def main():
         queries = query_phase(eng, w, acc_n, torch, dev)
 
     host = None
-    if rank == 0 and world == 1 and not args.no_host:
+    if rank == 0 and world == 1 and not args.no_host and w is not None and sum(host_nb):
         host = host_path(eng, w, tts, counts, (W + K) * B, host_nb, torch)
 
     cpu = None
@@ -386,10 +386,10 @@ def main():
             orc.create_accounts_batches(ats, w.account_counts, w.accounts)
             host_events = w.transfers
         else:
-            # config 5: the leading 256 batches, with the accounts they touch (a 100M-account
-            # oracle would not fit the sample): their results do not depend on the others
+            # config 5: the leading 1024 batches, with the accounts they touch (the sample
+            # need not create all 100M): their results do not depend on the others
             from tigerbeetle_amd.types import ACCOUNT_DTYPE, TRANSFER_DTYPE
-            nh = int(counts[:256].sum())
+            nh = int(counts[:1024].sum())
             host_events = ev_dev[:nh * 128].cpu().numpy().view(TRANSFER_DTYPE)
             ids = np.unique(np.concatenate([host_events["debit_account_id_lo"], host_events["credit_account_id_lo"]]))
             acc = np.zeros(len(ids), dtype=ACCOUNT_DTYPE)
@@ -399,7 +399,7 @@ def main():
             orc = oracle.Oracle(len(ids), nh)
             orc.create_accounts_batches(np.array([ats[-1]], np.uint64), np.array([len(acc)], np.uint32), acc)
         done, spent, b = 0, 0.0, 0
-        nb_host = len(counts) if w is not None else 256
+        nb_host = len(counts) if w is not None else 1024
         while spent < args.cpu_seconds and b < nb_host:
             k = min(16, nb_host - b)
             off = int(counts[:b].sum())

@@ -721,6 +721,15 @@ __global__ void tr_side_build(TrArgs C, EvalState S, u32 kmax, const uint4* pair
 // Sorted positions and the static per-side information in sorted order.
 __global__ void tr_side_pos(TrArgs C, const u32* sval_s, u64 m) {
     const u64 q = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    // account starts, for the fused scan's windows (inert sides each stand alone):
+    // the wave's first start, one atomic per wave (a tile spans whole waves)
+    u32 start = NONE32;
+    if (q < m) {
+        const u32 key = C.sd.skey_s[q];
+        if (q == 0 || key != C.sd.skey_s[q - 1] || key == C.sd.inert) start = (u32)q;
+    }
+    start = wave_min(start);
+    if (start != NONE32 && q == start) atomicMin(&C.sd.tstart[q / C.sd.tile], start);
     if (q >= m) return;
     const u32 s = sval_s[q];
     C.sd.spos[s] = (u32)q;
@@ -730,9 +739,6 @@ __global__ void tr_side_pos(TrArgs C, const u32* sval_s, u64 m) {
     const u32 cs = C.cs[i], ce = C.ce[i];
     const bool doom = C.ctl && (C.ctl[ce] & TBGPU_CTL_DOOM);
     C.sd.sq_cs[q] = cs | (cs == ce ? SQ_STANDALONE : 0u) | (doom ? SQ_DOOM : 0u);
-    // account starts, for the fused scan's windows (inert sides each stand alone)
-    const u32 key = C.sd.skey_s[q];
-    if (q == 0 || key != C.sd.skey_s[q - 1] || key == C.sd.inert) atomicMin(&C.sd.tstart[q / C.sd.tile], (u32)q);
 }
 
 // Write event i's side records (sorted order) for its outcome: the debit and credit

@@ -7,9 +7,13 @@ import os
 import sys
 
 out = sys.argv[1]
+avg_ns = {}
 for f in sorted(glob.glob(os.path.join(out, "kt", "**", "*kernel_stats.csv"), recursive=True)):
     print("== kernel stats", f)
-    for r in list(csv.DictReader(open(f)))[:12]:
+    rows = list(csv.DictReader(open(f)))
+    for r in rows:
+        avg_ns[r["Name"].replace("(anonymous namespace)::", "").split("(")[0][-40:]] = float(r["AverageNs"])
+    for r in rows[:12]:
         print(f"{r['Name'][:60]:60s} calls={r['Calls']:>5s} avg_us={float(r['AverageNs'])/1e3:9.2f} pct={float(r['Percentage']):6.2f}")
 agg = collections.defaultdict(list)
 for f in sorted(glob.glob(os.path.join(out, "p*", "**", "*counter_collection.csv"), recursive=True)):
@@ -21,6 +25,18 @@ for (k, c), v in sorted(agg.items()):
     if sum(v) == 0:
         continue
     print(f"{k:40s} {c:24s} n={len(v):4d} mean={sum(v)/len(v):.4g}")
+# LDS bank conflicts (extra cycles over all LDS cycles) and mean resident waves per
+# busy CU cycle, per kernel that ran the LDS / occupancy pass.
+for k in sorted({k for k, _ in agg}):
+    bc, ia = agg.get((k, "SQ_LDS_BANK_CONFLICT")), agg.get((k, "SQ_LDS_IDX_ACTIVE"))
+    wc = agg.get((k, "SQ_WAVE_CYCLES"))
+    if bc and ia and sum(ia):
+        print(f"{k:40s} lds_bank_conflict_frac={sum(bc)/sum(ia):.4f}")
+    if wc and k in avg_ns and avg_ns[k] > 0:
+        # SQ_WAVE_CYCLES counts quad-cycles (MI355X_MICROARCH.md): resident waves per CU
+        # = 4 x wave-cycles / (kernel duration x 2.4 GHz x 256 CUs), max 32 (8 per SIMD)
+        occ = 4 * sum(wc) / len(wc) / (avg_ns[k] * 1e-9 * 2.4e9 * 256)
+        print(f"{k:40s} mean_resident_waves_per_cu={occ:.1f} (of 32; {avg_ns[k] / 1e3:.1f} us/dispatch)")
 # Per-event HBM bytes of the fast-path kernels: FETCH_SIZE / WRITE_SIZE are in KiB;
 # on gfx950 FETCH_SIZE counts half the bytes of wide streaming reads
 # (MI355X_MICROARCH.md, HBM section), so both the raw and the x2 figure are shown.
@@ -53,7 +69,7 @@ if ev:
     # account setup (ac_*, k_*) and queries (q_*) excluded.
     tot = 0.0
     for k in sorted({k for k, _ in agg}):
-        if k.startswith(("__amd", "ac_", "k_", "q_")):
+        if k.startswith(("__amd", "ac_", "k_", "q_", "lg_")):
             continue
         f, w = agg.get((k, "FETCH_SIZE")), agg.get((k, "WRITE_SIZE"))
         if f and w:

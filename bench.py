@@ -164,14 +164,132 @@ def host_path(eng, w, tts, counts, b0, nbs, torch):
                          "entry": "tbgpu_create_transfers_batches (host buffers, H2D inside the call)"}}
 
 
+def routed_bench(args, rank, world, local_rank, torch, dist, backend="nccl"):
+    """N > 1, BASELINE config 4 through the ledger-sharded router (SURVEY.md §8e,
+    tigerbeetle_amd/shard.py): every rank receives its own client batches (1000
+    ledgers, uniform pairs within a ledger, 1% cross-ledger linked pairs), the step
+    scatters them to the owners of their ledgers (ledger % N) with RCCL all-to-all
+    over xGMI, every owner commits its sub-batches in global order
+    (tbgpu_create_transfers_routed_device), cross-shard pairs are settled by one
+    dry run of their members, and replies go back to the sources.  Accounts are
+    replicated (each rank creates all of them).  Transfer ids rise along the global
+    order (step, rank, index), the benchmark's sequential ids."""
+    from tigerbeetle_amd import workload
+    from tigerbeetle_amd.engine import Engine
+    from tigerbeetle_amd.shard import Comm, ShardedStateMachine
+    from tigerbeetle_amd.types import BATCH_MAX
+    B = args.batches_per_step
+    K, W = args.steps, args.warmup
+    per_step = B * BATCH_MAX
+    acc_n = args.accounts or 10_000_000
+    t_gen = time.time()
+    w = workload.config4(transfer_count=(K + W) * per_step, ledgers=1000, accounts_per_ledger=acc_n // 1000,
+                         seed=42 + rank)
+    j = np.arange(len(w.transfers), dtype=np.uint64)
+    w.transfers["id_lo"] = ((j // per_step) * world + rank) * per_step + (j % per_step) + 1
+    w.transfers["id_hi"] = 0
+    log(f"[rank {rank}] generated {len(w.transfers)} transfers / {acc_n} accounts in {time.time() - t_gen:.1f}s")
+    dev = torch.device("cuda", local_rank)
+    eng = Engine(device=local_rank, accounts_max=acc_n, transfers_max=int((K + W) * per_step * 1.25) + 4096,
+                 history_max=1024, events_per_call_max=int(per_step * 1.25) + BATCH_MAX)
+    ats, _ = w.timestamps()
+    _, rc = eng.create_accounts_batches(ats, w.account_counts, w.accounts)
+    assert int(rc.sum()) == 0, "account creation failed"
+    cdev = dev if backend == "nccl" else torch.device("cpu")  # where the router's tensors live
+    ssm = ShardedStateMachine(eng, Comm(rank, world, device=cdev))
+    ssm.adopt_accounts(w.accounts, int(ats[-1]))
+    ev_dev = torch.from_numpy(w.transfers.view(np.uint8)).to(cdev)
+    counts = w.transfer_counts
+    del w
+    torch.cuda.synchronize()
+
+    def step(k):
+        ev = ev_dev[k * per_step * 128:(k + 1) * per_step * 128]
+        reps = ssm.create_transfers_device(ev, list(map(int, counts[k * B:(k + 1) * B])))
+        return sum(len(r) for r in reps)
+
+    for k in range(W):
+        step(k)
+    torch.cuda.synchronize()
+    dist.barrier()
+    for key in ssm.timing:
+        ssm.timing[key] = 0.0
+    st0 = dict(ssm.stats)
+    ssm.timed = True
+    non_ok = 0
+    t0 = time.perf_counter()
+    for k in range(W, W + K):
+        non_ok += step(k)
+    torch.cuda.synchronize()
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ssm.timed = False
+    t = torch.tensor([elapsed, non_ok] + [ssm.timing[x] for x in sorted(ssm.timing)], dtype=torch.float64,
+                     device=cdev)
+    tmax = t.clone()
+    dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    tsum = t.clone()
+    dist.all_reduce(tsum)
+    elapsed = float(tmax[0])
+    non_ok = int(tsum[1])
+    total = per_step * K * world
+    value = total / elapsed
+    phases = {x: round(float(tmax[2 + i]) / K, 3) for i, x in enumerate(sorted(ssm.timing))}
+    if rank == 0:
+        e2e = value / world * ALGO_BYTES_PER_TRANSFER / 1e9
+        a2a_bytes = per_step * (128 + 32) * (world - 1) / world  # events + side records leaving each rank
+        line = {
+            "metric": "committed transfers/sec (whole node), 8190-transfer batches; % HBM roofline",
+            "value": round(value, 1),
+            "unit": "transfers/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": round(elapsed / K * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u128",
+            "data": "synthetic",
+            "config": {"workload": f"config4 routed: {acc_n} accounts (replicated), 1000 ledgers sharded by "
+                                   f"ledger % {world}, uniform pairs within a ledger, 1% cross-ledger linked "
+                                   f"pairs; per rank {B} x 8190-transfer client batches per step, scattered to "
+                                   f"their ledger owners by RCCL all-to-all and replied to by all-to-all",
+                       "batches_per_step": B, "transfers_per_step_per_gpu": per_step,
+                       "parallelism": f"ledger-shard x{world}, routed (tigerbeetle_amd/shard.py device step, "
+                                      f"{'RCCL' if backend == 'nccl' else backend} collectives)"},
+            "non_ok_results": non_ok,
+            "non_ok_rate": round(non_ok / total, 5),
+            "routed": {"phase_ms_per_step_max_over_ranks": phases,
+                       "alltoall_bytes_per_rank_per_step": int(a2a_bytes),
+                       "alltoall_GBps_per_rank": round(a2a_bytes / (phases["exchange_ms"] * 1e-3) / 1e9, 1)
+                       if phases["exchange_ms"] > 0 else None,
+                       "cross_shard_prerun_steps": ssm.stats["preruns"] - st0["preruns"],
+                       "dry_rounds": ssm.stats["dry_rounds"] - st0["dry_rounds"],
+                       "fallbacks": ssm.stats["device_fallbacks"] - st0["device_fallbacks"]},
+            "roofline": {"bound": "hbm", "achieved": round(e2e, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(e2e / HBM_PEAK_GBPS, 5), "traffic": None,
+                         "kernel": "whole routed step per GPU",
+                         "basis": f"{ALGO_BYTES_PER_TRANSFER} B/transfer x per-GPU committed transfers/s "
+                                  "(partition, all-to-all, commit and replies inside the time)"},
+            "cpu_baseline": None,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="default 3 (config 5: 14, ~the whole shard)")
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", type=int, default=2, choices=(1, 2, 3, 4, 5),
-                    help="4: 1000 ledgers x 10k accounts with 1%% cross-ledger linked pairs, on one GPU; "
-                         "5: 100M accounts, one 1/8 ledger shard of 1B transfers per GPU (generated in HBM)")
+    ap.add_argument("--config", type=int, default=None, choices=(1, 2, 3, 4, 5),
+                    help="default 2 on one GPU, 4 (routed) on several.  4: 1000 ledgers x 10k accounts with "
+                         "1%% cross-ledger linked pairs; 5: 100M accounts, one 1/8 ledger shard of 1B transfers "
+                         "per GPU (generated in HBM)")
+    ap.add_argument("--unrouted", action="store_true",
+                    help="N > 1: every rank commits its own pre-routed ledger shard (no all-to-all)")
     ap.add_argument("--force-general", action="store_true", help="disable the fast path (measure the fixed point)")
     ap.add_argument("--batches-per-step", type=int, default=None,
                     help="default 1000 (config 1/2: a whole BASELINE config-2 run per call), 60 for config 3")
@@ -188,6 +306,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("TB_DIST_BACKEND", "nccl") != "nccl":
+        import torch
+        local_rank %= max(torch.cuda.device_count(), 1)  # rehearsal: ranks may share a GPU
 
     import torch  # device memory + torch.distributed plumbing (loaded before libtbgpu: one HIP runtime)
     import torch.distributed as dist
@@ -196,8 +317,16 @@ def main():
     from tigerbeetle_amd.types import BATCH_MAX
 
     torch.cuda.set_device(local_rank)
+    backend = os.environ.get("TB_DIST_BACKEND", "nccl")  # gloo: a CPU-collective rehearsal on one GPU
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
+    if args.config is None:
+        args.config = 2 if world == 1 else 4
+    if world > 1 and args.config == 4 and not args.unrouted:
+        return routed_bench(args, rank, world, local_rank, torch, dist, backend)
 
     if args.batches_per_step is None:
         args.batches_per_step = 60 if args.config == 3 else 1000

@@ -139,3 +139,36 @@ def config4_small(seed: int, world: int, steps: int, batches_per_rank: int, batc
     sw.account_batches = [w.accounts[i:i + 4096] for i in range(0, len(w.accounts), 4096)]
     sw.batches = [w.transfers[i:i + batch] for i in range(0, total, batch)]
     return sw
+
+
+def config4_failing(seed: int, world: int, steps: int, batches_per_rank: int, batch: int = 256,
+                    limits: bool = False):
+    """config4_small whose cross-ledger pairs sometimes break: a member with code 0 or an
+    unknown debit account fails by itself (`limits` = False: every outcome is
+    independent of other transfers, the device step's one-dry-run case), or, with
+    `limits`, some accounts carry debits_must_not_exceed_credits with little credit,
+    so members fail on balances written by other transfers (the dry-round case)."""
+    from tigerbeetle_amd.types import AccountFlags, TransferFlags
+    sw = config4_small(seed, world, steps, batches_per_rank, batch=batch, cross=0.1)
+    rng = np.random.default_rng(seed + 1000)
+    if limits:
+        acc = sw.accounts.copy()
+        lim = rng.random(len(acc)) < 0.3
+        acc["flags"][lim] |= np.uint16(int(AccountFlags.debits_must_not_exceed_credits))
+        sw.accounts = acc
+        sw.account_batches = [acc[i:i + 4096] for i in range(0, len(acc), 4096)]
+    out = []
+    for b in sw.batches:
+        b = b.copy()
+        linked = (b["flags"] & int(TransferFlags.linked)) != 0
+        pairs = np.nonzero(linked)[0]
+        for j in pairs:
+            u = rng.random()
+            k = j + int(rng.integers(0, 2))
+            if u < 0.15:
+                b[k]["code"] = 0
+            elif u < 0.25:
+                b[k]["debit_account_id_hi"] = 7  # unknown account
+        out.append(b)
+    sw.batches = out
+    return sw

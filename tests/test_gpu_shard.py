@@ -25,4 +25,14 @@ def test_gpu_device_step_config4():
     engine's tbgpu_create_transfers_routed_device, fast path with chain control
     and dry runs)."""
     stats = _check(("c4", 17, 2, 3, 2), 2, kind="gpu", device_step=True)
-    assert stats["dry_rounds"] > 0 and stats["splits"] == 0
+    assert stats["preruns"] > 0 and stats["dry_rounds"] == 0 and stats["splits"] == 0
+
+
+@pytest.mark.gpu
+def test_gpu_device_step_breaking_chains():
+    """Cross-shard pairs that break: the one-dry-run settlement (static failures) and
+    dry rounds (balance-limited accounts) with the HIP engine behind every rank."""
+    stats = _check(("c4f", 19, 2, 3, 2), 2, kind="gpu", device_step=True)
+    assert stats["preruns"] > 0 and stats["dry_rounds"] == 0
+    stats = _check(("c4l", 23, 2, 3, 2), 2, kind="gpu", device_step=True)
+    assert stats["dry_rounds"] > 0

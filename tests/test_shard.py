@@ -18,7 +18,7 @@ import pytest
 
 import oracle
 from tigerbeetle_amd.types import TRANSFER_DTYPE
-from tests.shard_workload import ShardWorkload, config4_small
+from tests.shard_workload import ShardWorkload, config4_failing, config4_small
 
 
 def _free_port() -> int:
@@ -37,7 +37,7 @@ def _backend(kind, w):
     return oracle.Oracle(len(w.accounts), 1 << 14)
 
 
-def _worker(rank, world, port, out_dir, spec, kind="oracle", device_step=False):
+def _worker(rank, world, port, out_dir, spec, kind="oracle", device_step=False, max_rounds=None):
     import torch.distributed as dist
     from tigerbeetle_amd.shard import Comm, ShardedStateMachine
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -46,6 +46,8 @@ def _worker(rank, world, port, out_dir, spec, kind="oracle", device_step=False):
     try:
         w = _make(spec)
         sm = ShardedStateMachine(_backend(kind, w), Comm(rank, world))
+        if max_rounds is not None:
+            sm.max_rounds = max_rounds
         acc_replies = sm.create_accounts(w.account_batches if rank == 0 else [])
         replies = []
         for s in range(w.steps):
@@ -73,14 +75,17 @@ def _make(spec):
     kind, seed, world, steps, B = spec
     if kind == "mix":
         return ShardWorkload(seed, world, steps, B)
+    if kind in ("c4f", "c4l"):
+        return config4_failing(seed, world, steps, B, limits=kind == "c4l")
     return config4_small(seed, world, steps, B)
 
 
-def _check(spec, world, kind="oracle", device_step=False):
+def _check(spec, world, kind="oracle", device_step=False, max_rounds=None):
     import torch.multiprocessing as mp
     from tigerbeetle_amd.types import ACCOUNT_DTYPE, RESULT_DTYPE, TRANSFER_DTYPE
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d, spec, kind, device_step), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), d, spec, kind, device_step, max_rounds), nprocs=world,
+                 join=True)
         outs = [pickle.load(open(os.path.join(d, f"r{r}.pkl"), "rb")) for r in range(world)]
     w = _make(spec)
     # the single state machine over the global order
@@ -129,10 +134,39 @@ def test_device_step_config4(world):
     """The device-resident step (monotone ids, no post/void: no directory, on-device
     partition + all-to-all, dry rounds for the cross-ledger pairs)."""
     stats = _check(("c4", 13 + world, world, 3, 2), world, device_step=True)
-    assert stats["dry_rounds"] > 0 and stats["splits"] == 0
+    assert stats["preruns"] > 0 and stats["dry_rounds"] == 0 and stats["splits"] == 0
 
 
 def test_device_step_falls_back_exactly():
     """Non-monotone ids and post/void: the device step hands over to the exact router."""
     stats = _check(("mix", 31, 2, 2, 2), 2, device_step=True)
     assert stats["steps"] > 0
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_device_step_settles_plain_cross_shard_chains_with_one_dry_run(world):
+    """Cross-ledger pairs that break on static checks: one dry run of the spanning
+    members alone, then the commit (no dry rounds over the step)."""
+    stats = _check(("c4f", 41 + world, world, 3, 2), world, device_step=True)
+    assert stats["preruns"] > 0 and stats["dry_rounds"] == 0 and stats["device_fallbacks"] == 0
+
+
+def test_device_step_dry_rounds_with_limit_accounts():
+    """Spanning members on balance-limited accounts: dry rounds to the fixed point."""
+    stats = _check(("c4l", 51, 2, 3, 2), 2, device_step=True)
+    assert stats["dry_rounds"] > 0 and stats["preruns"] == 0
+
+
+def test_device_step_hands_over_after_max_rounds():
+    """No fixed point within max_rounds (forced to 1): the device step hands the
+    step, uncommitted, to the exact router and its serial fallback."""
+    stats = _check(("c4l", 53, 2, 3, 2), 2, device_step=True, max_rounds=1)
+    assert stats["device_fallbacks"] > 0 and stats["serial_fallbacks"] > 0
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_serial_fallback_one_cross_shard_chain_per_round(world):
+    """The exact router with max_rounds = 1: every step whose chains do not settle in
+    one dry round is committed one cross-shard chain at a time, still bit-exact."""
+    stats = _check(("mix", 61 + world, world, 2, 2), world, max_rounds=1)
+    assert stats["serial_fallbacks"] > 0

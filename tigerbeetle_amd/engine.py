@@ -221,7 +221,12 @@ class Engine:
         a uint8 tensor of >= 8*n bytes that receives the concatenated sparse replies.
         Returns (result_counts per sub-batch, commit_timestamp)."""
         host_results = None
-        if not events.is_cuda:  # CPU tensors (the gloo-routed tests): stage them in HBM
+        if events.is_cuda:
+            # the tensors were produced on torch's current stream; the engine runs on
+            # its own, so wait for them (the call itself returns after its stream drained)
+            import torch
+            torch.cuda.current_stream(events.device).synchronize()
+        else:  # CPU tensors (the gloo-routed tests): stage them in HBM
             dev = f"cuda:{self.device}"
             events, event_ts = events.to(dev), event_ts.to(dev)
             ctl = None if ctl is None else ctl.to(dev)

@@ -191,7 +191,8 @@ def routed_bench(args, rank, world, local_rank, torch, dist, backend="nccl"):
     log(f"[rank {rank}] generated {len(w.transfers)} transfers / {acc_n} accounts in {time.time() - t_gen:.1f}s")
     dev = torch.device("cuda", local_rank)
     eng = Engine(device=local_rank, accounts_max=acc_n, transfers_max=int((K + W) * per_step * 1.25) + 4096,
-                 history_max=1024, events_per_call_max=int(per_step * 1.25) + BATCH_MAX)
+                 history_max=1024, events_per_call_max=int(per_step * 1.25) + BATCH_MAX,
+                 dense_block_span=acc_n // 1000)
     ats, _ = w.timestamps()
     _, rc = eng.create_accounts_batches(ats, w.account_counts, w.accounts)
     assert int(rc.sum()) == 0, "account creation failed"
@@ -387,7 +388,9 @@ def main():
     else:
         eng = Engine(device=local_rank, accounts_max=acc_n, transfers_max=int(w.transfer_counts.sum()) + 1024,
                      history_max=int(w.transfer_counts.sum()) + 1024 if args.config == 3 else 1024,
-                     events_per_call_max=B * BATCH_MAX, force_general=args.force_general)
+                     events_per_call_max=B * BATCH_MAX, force_general=args.force_general,
+                     # config 4 numbers its accounts ledger << 32 | k: the blocked directory
+                     dense_block_span=acc_n // 1000 if args.config == 4 else 0)
         ats, tts = w.timestamps()
         _, rc = eng.create_accounts_batches(ats, w.account_counts, w.accounts)
         assert int(rc.sum()) == 0, "account creation failed"
@@ -561,7 +564,7 @@ def main():
                                    + {1: "uniform pairs", 2: "Zipf(0.99) pairs on 1 ledger",
                                       3: "flag-heavy mix (limits, two-phase, balancing, chains)",
                                       4: "1000 ledgers, uniform pairs within a ledger, 1% cross-ledger "
-                                         "linked pairs (u128 account ids: the hash index)",
+                                         "linked pairs (ids ledger << 32 | k: the blocked directory)",
                                       5: "1000 ledgers, one 1/8 ledger shard of 1B transfers (the per-GPU shard), "
                                          "uniform pairs within a ledger, generated in HBM"}[args.config]
                                    + f", {B} x 8190-transfer batches per step (streamed, HBM-resident)",

@@ -232,7 +232,8 @@ typedef struct tbgpu_options {
     uint64_t history_max;         /* account-history rows                            */
     uint64_t events_per_call_max; /* events one (multi-batch) call may carry        */
     uint32_t flags;               /* TBGPU_OPT_*                                    */
-    uint32_t reserved1;
+    uint32_t dense_block_span;    /* 0, or S: ids (b << 32) | k, b < accounts_max / S + 2,
+                                     1 <= k <= S, sit in the direct-mapped directory  */
 } tbgpu_options;
 
 enum {

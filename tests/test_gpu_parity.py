@@ -313,3 +313,37 @@ def test_dense_directory_boundaries():
     w.transfers = plain
     st = _parity(w, accounts_max=amax)
     assert st.path == 1
+
+
+def test_blocked_dense_directory(force_general):
+    """tbgpu_options.dense_block_span: ledger-major ids (ledger << 32 | k) in the
+    direct-mapped directory (config 4's numbering), with ids past the span, in block
+    0, beyond the last block and never created mixed in, plus limit flags read
+    through the directory; and the config-4 workload itself with the span set."""
+    from tigerbeetle_amd.types import AccountFlags
+    span, ledgers = 50, 8
+    rng = np.random.default_rng(17)
+    ids = [(l << 32) | k for l in range(1, ledgers + 1) for k in range(1, span + 1) if (l + k) % 5] + \
+          [(1 << 32) | (span + 1), (2 << 32) | (span + 7), 3, span, ((ledgers + 9) << 32) | 1, (1 << 64) | 5]
+    acc = workload.make_accounts(np.zeros(len(ids), dtype=np.uint64), ledger=1)
+    for j, v in enumerate(ids):
+        acc[j]["id_lo"], acc[j]["id_hi"] = v & ((1 << 64) - 1), v >> 64
+    acc["flags"] = np.where(rng.random(len(ids)) < 0.1, int(AccountFlags.debits_must_not_exceed_credits),
+                            0).astype(np.uint16)
+    pool = ids + [(1 << 32) | 5, (4 << 32), ((ledgers + 1) << 32) | 3, (2 << 32) | (span + 2)]  # never created
+    n = 9_000
+    t = np.zeros(n, dtype=workload.TRANSFER_DTYPE)
+    t["id_lo"] = np.arange(1, n + 1)
+    for i in range(n):
+        d, c = pool[int(rng.integers(0, len(pool)))], pool[int(rng.integers(0, len(pool)))]
+        t[i]["debit_account_id_lo"], t[i]["debit_account_id_hi"] = d & ((1 << 64) - 1), d >> 64
+        t[i]["credit_account_id_lo"], t[i]["credit_account_id_hi"] = c & ((1 << 64) - 1), c >> 64
+    t["amount_lo"] = rng.integers(1, 100, n)
+    t["ledger"] = 1
+    t["code"] = 1
+    w = workload.Workload("blocked", acc, np.array([len(acc)], dtype=np.uint32), t,
+                          np.array([3000] * 3, dtype=np.uint32))
+    _parity(w, accounts_max=ledgers * span, dense_block_span=span, force_general=force_general)
+    w4 = workload.config4(transfer_count=40_000, ledgers=20, accounts_per_ledger=200, seed=3, cross_ledger_pairs=0.02)
+    st = _parity(w4, accounts_max=20 * 200, dense_block_span=200, force_general=force_general)
+    assert force_general or st.path == 1

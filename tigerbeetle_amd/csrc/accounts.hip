@@ -199,7 +199,7 @@ __global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const
     e.ledger = a.ledger;
     e.flags = a.flags;
     e.code = a.code;
-    if (dense_has(T, a.id)) T.dense[(u64)a.id - 1] = dense_entry(row, a.ledger, a.flags);
+    if (dense_has(T, a.id)) T.dense[dense_slot(T, a.id)] = dense_entry(row, a.ledger, a.flags);
 }
 
 __global__ void ac_batch_counts(const u32* b_start, u32 nb, const uint4* rk, u32* counts) {
@@ -269,7 +269,7 @@ __global__ void k_rebuild_aidx(Tables T, u64 n) {
     e.ledger = a.ledger;
     e.flags = a.flags;
     e.code = a.code;
-    if (dense_has(T, a.id)) T.dense[(u64)a.id - 1] = dense_entry((u32)row, a.ledger, a.flags);
+    if (dense_has(T, a.id)) T.dense[dense_slot(T, a.id)] = dense_entry((u32)row, a.ledger, a.flags);
 }
 
 // tbgpu_open: the fast path's overflow guard (fast.hip) from the restored balances.

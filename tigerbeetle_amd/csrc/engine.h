@@ -36,14 +36,17 @@ struct Tables {
     // Set once any balance high word reaches 2^62: until then a call of < 2^32
     // events with amounts < 2^64 cannot overflow a u128 sum (fast.hip).
     u32* big;
-    // Direct-mapped account directory for the ids 1..dense_n: entry k describes
-    // id k + 1 as (row + 1) | (flags & 0xE) << 28 | ledger << 32, 0 = no such
-    // account.  Every account with such an id has its entry, so the directory is
-    // exact for them; other ids use `aidx`.  The reference benchmark numbers its
-    // accounts 1..N (src/tigerbeetle/benchmark_load.zig:134-138, :223): one 8-byte
-    // read from an 8 MB table instead of a 32-byte probe of a 64 MB one.
+    // Direct-mapped account directory.  Ids (b << 32) | k with b < dense_blocks and
+    // 1 <= k <= dense_span have entry b * dense_span + k - 1, describing the account
+    // as (row + 1) | (flags & 0xE) << 28 | ledger << 32, 0 = no such account.  Every
+    // account with such an id has its entry, so the directory is exact for them;
+    // other ids use `aidx`.  By default one block: ids 1..accounts_max, the reference
+    // benchmark's numbering (src/tigerbeetle/benchmark_load.zig:134-138, :223); with
+    // tbgpu_options.dense_block_span, ledger-major ids (ledger << 32 | k).  One
+    // 8-byte read instead of a 32-byte probe of a twice-as-large hash index.
     u64* dense;
-    u64 dense_n;
+    u64 dense_n;       // entries (dense_blocks * dense_span)
+    u64 dense_span, dense_blocks;
     // Device-side append cursors, so that consecutive chunks and calls need no host
     // round trip: [0] stored transfer rows, [1] account-history rows, [2] replies
     // written so far in the current call (the streaming reply offset).
@@ -53,7 +56,13 @@ struct Tables {
 enum { BASE_ROWS = 0, BASE_HIST = 1, BASE_REPLIES = 2 };
 
 __device__ __forceinline__ bool dense_has(const Tables& T, u128 id) {
-    return (u64)(id >> 64) == 0 && (u64)id - 1 < T.dense_n;
+    const u64 lo = (u64)id;
+    return (u64)(id >> 64) == 0 && (lo >> 32) < T.dense_blocks && (u64)(u32)lo - 1 < T.dense_span;
+}
+// the entry of an id for which dense_has holds
+__device__ __forceinline__ u64 dense_slot(const Tables& T, u128 id) {
+    const u64 lo = (u64)id;
+    return (lo >> 32) * T.dense_span + (u32)lo - 1;
 }
 __device__ __forceinline__ u64 dense_entry(u32 row, u32 ledger, u16 flags) {
     return (u64)(row + 1) | ((u64)(flags & 0xEu) << 28) | ((u64)ledger << 32);
@@ -176,7 +185,7 @@ __device__ __forceinline__ u32 acc_probe(const AccIdx* __restrict__ aidx, u64 ma
 
 __device__ __forceinline__ u32 acc_find(const Tables& T, u128 id, u32* ledger, u16* flags) {
     if (dense_has(T, id)) {
-        const u64 e = T.dense[(u64)id - 1];
+        const u64 e = T.dense[dense_slot(T, id)];
         if (e == 0) return NONE32;
         *ledger = (u32)(e >> 32);
         *flags = (u16)((e >> 28) & 0xE);

@@ -297,7 +297,15 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     c->T.base = dalloc<u64>(4, &B);
     c->T.xrow_cap = c->xrow_cap;
     c->T.hist_cap = c->hist_cap;
-    c->T.dense_n = o.accounts_max < (1ull << 29) - 1 ? o.accounts_max : 0;  // row + 1 in 29 bits
+    // row + 1 in 29 bits; ids below 2^32 in block 0, or dense_block_span-wide blocks
+    // for ledger-major ids, one spare block (ledgers are numbered from 1)
+    if (o.accounts_max > 0 && o.accounts_max < (1ull << 29) - 1) {
+        const u64 span = o.dense_block_span ? o.dense_block_span : std::max<u64>(o.accounts_max, 1);
+        c->T.dense_span = span;
+        c->T.dense_blocks = o.dense_block_span ? (o.accounts_max + span - 1) / span + 2 : 1;
+        c->T.dense_n = c->T.dense_span * c->T.dense_blocks;
+        if (!o.dense_block_span) c->T.dense_n = o.accounts_max;
+    }
     c->T.dense = dalloc<u64>(c->T.dense_n, &B);
     alloc_scratch(c, o.events_per_call_max);
     tbgpu_reset(c);

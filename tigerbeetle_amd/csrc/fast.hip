@@ -128,7 +128,7 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
     // themselves are only touched by the balance atomics.
     u64 hd = hash128(t.debit_account_id) & T.aidx_mask;
     u64 hc = hash128(t.credit_account_id) & T.aidx_mask;
-    // Ids 1..dense_n read the 8-byte directory entry, others the 32-byte index slot.
+    // Ids in the direct-mapped directory read its 8-byte entry, others the 32-byte index slot.
     AccIdx A, B;
     const bool dd = dense_has(T, t.debit_account_id), dc = dense_has(T, t.credit_account_id);
     u64 EA = 0, EB = 0;
@@ -136,8 +136,8 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
         A = {(u64)t.debit_account_id, (u64)(t.debit_account_id >> 64), (u32)(hd % 1000) + 1, t.ledger, 0, 1, 0};
         B = {(u64)t.credit_account_id, (u64)(t.credit_account_id >> 64), (u32)(hc % 1000) + 1, t.ledger, 0, 1, 0};
     } else {
-        if (dd) EA = T.dense[(u64)t.debit_account_id - 1]; else A = T.aidx[hd];
-        if (dc) EB = T.dense[(u64)t.credit_account_id - 1]; else B = T.aidx[hc];
+        if (dd) EA = T.dense[dense_slot(T, t.debit_account_id)]; else A = T.aidx[hd];
+        if (dc) EB = T.dense[dense_slot(T, t.credit_account_id)]; else B = T.aidx[hc];
     }
     const bool maybe = xidx_maybe_present(T, t.id);
     const u64 hx = xidx_hash(t.id) & T.xidx_mask;

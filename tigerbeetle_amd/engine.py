@@ -35,7 +35,7 @@ class Options(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("reserved0", ctypes.c_uint32), ("accounts_max", ctypes.c_uint64),
                 ("transfers_max", ctypes.c_uint64), ("history_max", ctypes.c_uint64),
                 ("events_per_call_max", ctypes.c_uint64), ("flags", ctypes.c_uint32),
-                ("reserved1", ctypes.c_uint32)]
+                ("dense_block_span", ctypes.c_uint32)]
 
 
 class Stats(ctypes.Structure):
@@ -142,11 +142,16 @@ class Engine:
     name = "gpu"
 
     def __init__(self, device: int = 0, accounts_max: int = 1 << 16, transfers_max: int = 1 << 20,
-                 history_max: int = 1 << 16, events_per_call_max: int = 1 << 17, force_general: bool = False):
+                 history_max: int = 1 << 16, events_per_call_max: int = 1 << 17, force_general: bool = False,
+                 dense_block_span: int = 0):
+        """dense_block_span = S > 0: account ids of the form (b << 32) | k with 1 <= k <= S
+        (e.g. ledger-major numbering) are looked up in the direct-mapped directory, one
+        8-byte read; other ids use the hash index.  0: the directory covers ids
+        1..accounts_max (the reference benchmark's numbering)."""
         self._L = lib()
         opt = Options(device=device, accounts_max=accounts_max, transfers_max=transfers_max,
                       history_max=history_max, events_per_call_max=events_per_call_max,
-                      flags=OPT_FORCE_GENERAL if force_general else 0)
+                      flags=OPT_FORCE_GENERAL if force_general else 0, dense_block_span=dense_block_span)
         self.device = device
         h = ctypes.c_void_p()
         rc = self._L.tbgpu_init(ctypes.byref(h), ctypes.byref(opt))

@@ -289,6 +289,8 @@ def main():
                     help="default 2 on one GPU, 4 (routed) on several.  4: 1000 ledgers x 10k accounts with "
                          "1%% cross-ledger linked pairs; 5: 100M accounts, one 1/8 ledger shard of 1B transfers "
                          "per GPU (generated in HBM)")
+    ap.add_argument("--routed", action="store_true",
+                    help="config 4 through the ledger router even on one GPU (a one-rank RCCL group)")
     ap.add_argument("--unrouted", action="store_true",
                     help="N > 1: every rank commits its own pre-routed ledger shard (no all-to-all)")
     ap.add_argument("--force-general", action="store_true", help="disable the fast path (measure the fixed point)")
@@ -319,14 +321,19 @@ def main():
 
     torch.cuda.set_device(local_rank)
     backend = os.environ.get("TB_DIST_BACKEND", "nccl")  # gloo: a CPU-collective rehearsal on one GPU
-    if world > 1:
+    if world == 1 and args.routed:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if world > 1 or args.routed:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         else:
             dist.init_process_group(backend)
     if args.config is None:
-        args.config = 2 if world == 1 else 4
-    if world > 1 and args.config == 4 and not args.unrouted:
+        args.config = 4 if (world > 1 or args.routed) else 2
+    if (world > 1 or args.routed) and args.config == 4 and not args.unrouted:
         return routed_bench(args, rank, world, local_rank, torch, dist, backend)
 
     if args.batches_per_step is None:

@@ -226,9 +226,10 @@ __global__ void bs_final(SideScanArgs A, u64 m, u32 invalid, const Bal4* __restr
 // has more than BF_TILE sides in the chunk.  An account with more (no account
 // starts in some window) raises halt[1]: the host redoes the pass with the
 // three-launch scan above.
-constexpr int BF_THREADS = 256;
-constexpr int BF_IPT = 2;                     // sides per thread
-constexpr int BF_TILE = BF_THREADS;           // nominal tile (sides): the 2x slack covers the last account
+constexpr int BF_THREADS = 512;
+constexpr int BF_IPT = 1;                     // sides per thread
+constexpr int BF_TILE = 256;                  // nominal tile (sides): the 2x slack covers the last account
+static_assert(BF_THREADS * BF_IPT == 2 * BF_TILE, "a workgroup scans two nominal tiles");
 
 __device__ __forceinline__ u64 shup(u64 v, int off) { return (u64)__shfl_up((unsigned long long)v, off); }
 __device__ __forceinline__ u128 shup128(u128 v, int off) {
@@ -314,27 +315,47 @@ __global__ __launch_bounds__(BF_THREADS) void bs_fused(SideScanArgs A, u64 m, u3
     // the thread's two sides (contiguous), loaded before any barrier
     const u64 qa = (u64)a0 + BF_IPT * tid;
     u32 key[BF_IPT], cs[BF_IPT];
-    Bal4 f[BF_IPT], h[BF_IPT];
+    Bal4 f[BF_IPT], h[BF_IPT], row[BF_IPT];
     SF e[BF_IPT];
 #pragma unroll
     for (int k = 0; k < BF_IPT; k++) {
         const u64 q = qa + k;
-        const bool v = q < b0;
-        key[k] = v ? A.skey[q] : invalid;
-        cs[k] = v ? (A.sq_cs[q] & SQ_CS) : NONE32;
+        key[k] = q < b0 ? A.skey[q] : invalid;
+    }
+#pragma unroll
+    for (int k = 0; k < BF_IPT; k++) {
+        // the account row (pre-chunk balances) is issued before the scan's barrier
+        zero(row[k]);
+        if (key[k] < invalid) {
+            const Account& ac = acc[key[k]];
+            row[k].dp = ac.debits_pending;
+            row[k].dpo = ac.debits_posted;
+            row[k].cp = ac.credits_pending;
+            row[k].cpo = ac.credits_posted;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < BF_IPT; k++) {
+        const u64 q = qa + k;
+        const u32 c = q < b0 ? A.sq_cs[q] : SQ_STANDALONE;
+        cs[k] = c & SQ_CS;
         zero(f[k]);
         zero(h[k]);
         e[k].fl = 1;
         if (key[k] < invalid) {
             side_contrib(A, q, &f[k], &h[k]);
-            e[k].fl = (q == a0 || A.skey[q - 1] != key[k]) ? 1u : 0u;
+            const u32 prev = k > 0 ? key[k - 1] : (q == a0 ? invalid : A.skey[q - 1]);
+            e[k].fl = prev != key[k] ? 1u : 0u;
         }
         e[k].F = f[k];
         s_key[BF_IPT * tid + k] = key[k];
-        s_cs[BF_IPT * tid + k] = cs[k];
-        s_h[BF_IPT * tid + k] = h[k];
+        // chain members only: the walk below reads s_h behind a side of its own chain
+        s_cs[BF_IPT * tid + k] = (c & SQ_STANDALONE) ? NONE32 : cs[k];
+        if (!(c & SQ_STANDALONE)) s_h[BF_IPT * tid + k] = h[k];
     }
-    const SF agg = combine_f(e[0], e[1]);
+    SF agg = e[0];
+#pragma unroll
+    for (int k = 1; k < BF_IPT; k++) agg = combine_f(agg, e[k]);
     SF run = block_excl_f(agg, wtot);  // (its barrier publishes s_key / s_cs / s_h)
 #pragma unroll
     for (int k = 0; k < BF_IPT; k++) {
@@ -343,13 +364,9 @@ __global__ __launch_bounds__(BF_THREADS) void bs_fused(SideScanArgs A, u64 m, u3
             Bal4 H;
             zero(H);
             u32 j = BF_IPT * tid + k;
-            while (j > 0 && s_key[j - 1] == key[k] && s_cs[j - 1] == cs[k]) H = add(H, s_h[--j]);
-            const Account& ac = acc[key[k]];
-            Bal4 out;
-            out.dp = ac.debits_pending;
-            out.dpo = ac.debits_posted;
-            out.cp = ac.credits_pending;
-            out.cpo = ac.credits_posted;
+            if (s_cs[j] != NONE32)
+                while (j > 0 && s_key[j - 1] == key[k] && s_cs[j - 1] == cs[k]) H = add(H, s_h[--j]);
+            Bal4 out = row[k];
             if (!(e[k].fl & 1)) out = add(out, run.F);
             bb[q] = add(out, H);
         }

@@ -134,6 +134,7 @@ struct Sides {
     u128* sq_dpend;   // [m] sorted, per pass: its delta on the *_pending balance
     u128* sq_dpost;   // [m] sorted, per pass: its delta on the *_posted balance
     u32* tstart;      // [m / tile + 1] first account start in each fused-scan window (NONE32: none)
+    uint2* epos;      // [n] sorted positions of each event's first side pair (debit, credit)
     u32 tile;         // the fused scan's window (sides)
     u32 inert;        // the key of sides that touch no account (each stands alone)
 };

@@ -82,6 +82,7 @@ struct tbgpu_ctx {
     u32 *soff, *sev, *scand, *sq_ev, *sq_cs;
     EvCore* core = nullptr;
     u32* tstart = nullptr;
+    uint2* epos = nullptr;
     u8* sq_ok = nullptr;
     u128 *sq_dpend = nullptr, *sq_dpost = nullptr;
     u32 *gkey_s, *gsorted;  // the id-group sort's output (the members of each id group, by event)
@@ -179,6 +180,7 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->soff = dalloc<u32>(n + 1, &B);
     c->core = dalloc<EvCore>(n, &B);
     c->tstart = dalloc<u32>(m / side_scan_fused_tile() + 2, &B);
+    c->epos = dalloc<uint2>(nmax + 1, &B);
     c->sev = dalloc<u32>(m, &B);
     c->scand = dalloc<u32>(m, &B);
     c->sq_ev = dalloc<u32>(m, &B);
@@ -341,7 +343,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
                     c->b_start, c->b_ts, c->ts, c->cs, c->ce, c->sres, c->dslot, c->cslot, c->pre_e, c->pre_p,
                     c->pp_dslot, c->pp_cslot, c->gslot, c->pslot, c->prev_id, c->pend_last, c->pend_first, c->prev_pend,
                     c->gclaim, c->gcnt_id, c->gcnt_pd, c->gmem, c->gbeg, c->gend, c->skey, c->sval, c->skey_s,
-                    c->soff, c->core, c->tstart, c->sev, c->scand, c->sq_ev, c->sq_cs, c->sq_ok, c->sq_dpend, c->sq_dpost, c->gkey_s,
+                    c->soff, c->core, c->tstart, c->epos, c->sev, c->scand, c->sq_ev, c->sq_cs, c->sq_ok, c->sq_dpend, c->sq_dpost, c->gkey_s,
                     c->gsorted,
                     c->sval_s, c->spos, c->bb, c->ss.keys_tmp, c->ss.vals_tmp, c->ss.hist, c->side_tiles,
                     c->sc.tile_sums, c->fres, c->mask, c->ranks, c->res_buf, c->counts, c->counters, c->status,
@@ -464,6 +466,7 @@ static TrArgs make_tr_args(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb) {
     C.sd.sq_ev = c->sq_ev; C.sd.sq_cs = c->sq_cs; C.sd.sq_ok = c->sq_ok; C.sd.sq_dpend = c->sq_dpend;
     C.sd.sq_dpost = c->sq_dpost;
     C.sd.tstart = c->tstart;
+    C.sd.epos = c->epos;
     C.sd.tile = side_scan_fused_tile();
     C.sd.inert = (u32)c->accounts_max;
     // group table sized for this call: >= 2x the keys (ids + pending ids <= 2n)

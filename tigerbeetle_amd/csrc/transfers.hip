@@ -440,28 +440,35 @@ __device__ __forceinline__ bool write_sides(const TrArgs& C, u32 i, bool pv, boo
 __device__ __forceinline__ bool evaluate_one(const Tables& T, const TrArgs& C, const EvalState& S,
                                              const EvalState& D, const Bal4* __restrict__ bb, const PassGate& g,
                                              u32 i) {
+    // Everything a regular transfer reads is issued up front, unconditionally (the
+    // indices are valid for every event; unused values are dropped): one memory
+    // round trip for the event's records, one for its two balances.
     const u8 sr = C.sres[i];
+    const u32 csi = C.cs[i];
+    const EvCore k = C.core[i];
+    const u32 pid = C.prev_id[i], pre_e = C.pre_e[i];
+    const uint2 ep = C.sd.epos[i];
+    const u8 s_res = S.res[i];
+    const u128 s_amt = S.amt[i], s_pamt = S.pamt[i];
+    const u32 s_pref = S.pref[i];
+    const Bal4 bd = bb[ep.x];
+    const Bal4 bc = bb[ep.y];
     u8 res;
     u128 amt = 0, pamt = 0, dpe = 0, dpo = 0;
     u32 pref = NONE32;
-    const u32 csi = C.cs[i];
     if (sr != SRES_DYN) {
         res = sr;
     } else {
-        const EvCore k = C.core[i];
         u32 e = NONE32;
-        for (u32 j = C.prev_id[i]; j != NONE32; j = C.prev_id[j])
+        for (u32 j = pid; j != NONE32; j = C.prev_id[j])
             if (visible(C, S, j, csi)) { e = j; break; }
-        if (e == NONE32 && C.pre_e[i] != NONE32) e = PREF_ROW | C.pre_e[i];
+        if (e == NONE32 && pre_e != NONE32) e = PREF_ROW | pre_e;
         if (!(k.flags & (TF_POST | TF_VOID))) {
             if (e != NONE32) {
                 Transfer t = C.ev[i];
                 t.timestamp = k.ts;
                 res = create_transfer_exists(t, load_ref(T, C, S, e));
             } else {
-                const u32 s0 = C.sd.soff[i];
-                const Bal4 bd = bb[C.sd.spos[s0]];
-                const Bal4 bc = bb[C.sd.spos[s0 + 1]];
                 u128 amount = 0;
                 res = eval_balances(k, bd, bc, &amount);
                 if (res == TBGPU_CREATE_TRANSFER_OK) {
@@ -522,12 +529,12 @@ __device__ __forceinline__ bool evaluate_one(const Tables& T, const TrArgs& C, c
     D.pamt[i] = pamt;
     D.pref[i] = pref;
     if (res != TBGPU_CREATE_TRANSFER_OK && csi != C.ce[i]) atomicMin(&D.cfail[csi], i);
-    const bool changed = res != S.res[i] || amt != S.amt[i] || pamt != S.pamt[i] || pref != S.pref[i];
+    const bool changed = res != s_res || amt != s_amt || pamt != s_pamt || pref != s_pref;
     if (C.debug && changed) {
         const u16 f = C.ev[i].flags;
         const u32 kind = (f & (TF_POST | TF_VOID)) ? 2 : (f & (TF_BDR | TF_BCR)) ? 1 : 0;
         atomicAdd(&C.counters[CNT_DBG + kind], 1u);
-        if (res != S.res[i]) atomicAdd(&C.counters[CNT_DBG + 3], 1u);
+        if (res != s_res) atomicAdd(&C.counters[CNT_DBG + 3], 1u);
         if (csi != C.ce[i]) atomicAdd(&C.counters[CNT_DBG + 4], 1u);
         if (sr == SRES_DYN && !(f & (TF_POST | TF_VOID)) && (C.core[i].aflags & 0x66))
             atomicAdd(&C.counters[CNT_DBG + 5], 1u);
@@ -736,6 +743,7 @@ __global__ void tr_side_pos(TrArgs C, const u32* sval_s, u64 m) {
     const u32 ev = C.sd.sev[s];
     C.sd.sq_ev[q] = ev;
     const u32 i = ev & 0x7FFFFFFFu;
+    if (s - C.sd.soff[i] < 2) ((u32*)&C.sd.epos[i])[ev >> 31] = (u32)q;
     const u32 cs = C.cs[i], ce = C.ce[i];
     const bool doom = C.ctl && (C.ctl[ce] & TBGPU_CTL_DOOM);
     C.sd.sq_cs[q] = cs | (cs == ce ? SQ_STANDALONE : 0u) | (doom ? SQ_DOOM : 0u);
@@ -745,6 +753,13 @@ __global__ void tr_side_pos(TrArgs C, const u32* sval_s, u64 m) {
 // sides of a transfer, or of the candidate pair of a post/void that it resolved to.
 // Returns false when an accepted post/void's pending is not among its candidates.
 __device__ __forceinline__ bool write_sides(const TrArgs& C, u32 i, bool pv, bool ok, u32 pref, u128 dpe, u128 dpo) {
+    if (!pv) {  // one side pair
+        const uint2 ep = C.sd.epos[i];
+        C.sd.sq_ok[ep.x] = C.sd.sq_ok[ep.y] = ok ? 1 : 0;
+        C.sd.sq_dpend[ep.x] = C.sd.sq_dpend[ep.y] = ok ? dpe : 0;
+        C.sd.sq_dpost[ep.x] = C.sd.sq_dpost[ep.y] = ok ? dpo : 0;
+        return true;
+    }
     const u32 s0 = C.sd.soff[i], s1 = C.sd.soff[i + 1];
     bool found = !pv || !ok;
     for (u32 s = s0; s < s1; s += 2) {

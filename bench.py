@@ -333,14 +333,14 @@ def main():
             dist.init_process_group(backend)
     if args.config is None:
         args.config = 4 if (world > 1 or args.routed) else 2
-    if (world > 1 or args.routed) and args.config == 4 and not args.unrouted:
-        return routed_bench(args, rank, world, local_rank, torch, dist, backend)
 
     if args.batches_per_step is None:
         args.batches_per_step = 60 if args.config == 3 else 1000
     if args.steps is None:
         args.steps = 14 if args.config == 5 else 3
     B, K, W = args.batches_per_step, args.steps, args.warmup
+    if (world > 1 or args.routed) and args.config == 4 and not args.unrouted:
+        return routed_bench(args, rank, world, local_rank, torch, dist, backend)
     host_nb = (0, 0) if (args.no_host or world > 1 or args.config == 5) else \
         ((args.host_batches or 64, (args.host_batches or 64) * 4) if args.config != 3 else (16, 48))
     n_batches = (K + W) * B + sum(host_nb)

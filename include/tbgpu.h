@@ -338,6 +338,25 @@ uint64_t tbgpu_create_transfers_routed_device(tbgpu_ctx* ctx, uint32_t batch_cou
                                               const void* ctl_device, int dry_run, void* results_device,
                                               uint32_t* result_counts, uint64_t* commit_timestamp);
 
+/* The send side of a routed step (tigerbeetle_amd/shard.py): this rank's client
+ * batches (`counts`, prepare timestamps `batch_timestamps`, global number of the
+ * first one `first_global_batch`), events in device memory, are written to
+ * `send_events_device` (n * 128 B) owner-major -- owner = ledger % world -- in event
+ * order within an owner, each with a 32-byte record in `send_sides_device` (n * 32 B):
+ * {event timestamp, global batch << 32 | index, global batch << 32 | index of its
+ * chain's first member, bit 0: the chain spans owners | bit 1: the event ends its
+ * chain}.  `send_counts[world]` (host) receives the events per owner.  world <= 256.
+ * Returns 0, or -22 for a bad argument.  Synchronous. */
+/* One pass over a routed step's local events (device memory) deciding whether the
+ * device path applies: out[0] min id (low word), out[1] max id (low word), out[2]
+ * bit 0: an id not above its predecessor, bit 1: an id with a high word or zero,
+ * bit 2: a post/void, bit 3: an amount of 2^64 or more; out[3], out[4]: the sum of
+ * the amounts (low, high word).  Returns 0.  Synchronous. */
+int tbgpu_route_stats(tbgpu_ctx* ctx, const void* events_device, uint64_t count, uint64_t* out);
+int tbgpu_route_scatter(tbgpu_ctx* ctx, uint32_t world, uint32_t batch_count, const uint32_t* counts,
+                        const uint64_t* batch_timestamps, uint64_t first_global_batch, const void* events_device,
+                        void* send_events_device, void* send_sides_device, uint64_t* send_counts);
+
 /* Copy committed transfers of another shard into this ctx's transfer table and id
  * index, without balance or posted effects: the `exists` comparisons of
  * :1370-1389 / :1500-1561 then see a colliding id committed elsewhere.  Returns 0. */

@@ -36,3 +36,71 @@ def test_gpu_device_step_breaking_chains():
     assert stats["preruns"] > 0 and stats["dry_rounds"] == 0
     stats = _check(("c4l", 23, 2, 3, 2), 2, kind="gpu", device_step=True)
     assert stats["dry_rounds"] > 0
+
+
+@pytest.mark.gpu
+def test_route_scatter_matches_torch_partition():
+    """tbgpu_route_scatter (csrc/route.hip) against the router's torch partition:
+    identical send buffers, side records and per-owner counts, with empty batches,
+    chains (some spanning owners, some open at a batch end) and 1..256 owners."""
+    import numpy as np
+    import torch
+
+    from tigerbeetle_amd.engine import Engine
+    from tigerbeetle_amd.shard import partition_torch
+    from tigerbeetle_amd.types import TRANSFER_DTYPE
+    rng = np.random.default_rng(3)
+    counts = [8190, 17, 0, 1000, 1, 0, 8190, 333]
+    n = sum(counts)
+    t = np.zeros(n, dtype=TRANSFER_DTYPE)
+    t["id_lo"] = np.arange(1, n + 1)
+    t["ledger"] = rng.integers(0, 5000, n)
+    t["flags"] = np.where(rng.random(n) < 0.3, 1, 0) | np.where(rng.random(n) < 0.1, 2, 0)
+    dev = torch.device("cuda", 0)
+    ev = torch.from_numpy(t.view(np.uint8).copy()).to(dev)
+    bts = np.cumsum(np.array(counts, dtype=np.uint64) + 1) + 1000
+    eng = Engine(device=0, accounts_max=16, transfers_max=16, events_per_call_max=1 << 12)
+    try:
+        for W in (1, 2, 3, 8, 256):
+            e_t, s_t, c_t = partition_torch(torch, ev, counts, bts, 5, W, dev)
+            e_n = torch.empty((n, 128), dtype=torch.uint8, device=dev)
+            s_n = torch.empty((n, 4), dtype=torch.int64, device=dev)
+            c_n = eng.route_scatter(W, counts, bts, 5, ev, e_n, s_n)
+            assert c_n.tolist() == c_t.cpu().tolist(), W
+            assert torch.equal(e_n, e_t), W
+            assert torch.equal(s_n, s_t), W
+    finally:
+        eng.close()
+
+
+@pytest.mark.gpu
+def test_route_stats_matches_numpy():
+    """tbgpu_route_stats (csrc/route.hip) against numpy over the same events."""
+    import numpy as np
+    import torch
+
+    from tigerbeetle_amd.engine import Engine
+    from tigerbeetle_amd.types import TRANSFER_DTYPE
+    rng = np.random.default_rng(11)
+    eng = Engine(device=0, accounts_max=16, transfers_max=16, events_per_call_max=1 << 12)
+    try:
+        for n, mono, pv, big in ((1, True, False, False), (1000, True, False, False), (77_777, True, False, True),
+                                 (50_001, False, True, False), (8190 * 3, True, False, False)):
+            t = np.zeros(n, dtype=TRANSFER_DTYPE)
+            ids = np.sort(rng.choice(1 << 40, size=n, replace=False)).astype(np.uint64) + 1
+            if not mono:
+                ids[n // 2], ids[n // 2 + 1] = ids[n // 2 + 1], ids[n // 2]
+            t["id_lo"] = ids
+            t["amount_lo"] = rng.integers(0, 1 << 63, n, dtype=np.uint64) * 2
+            if big:
+                t["amount_hi"][n // 3] = 1
+            if pv:
+                t["flags"][n - 1] = 4
+            ev = torch.from_numpy(t.view(np.uint8).copy()).to("cuda:0")
+            mn, mx, mo, ids_ok, has_pv, has_big, asum = eng.route_stats(ev, n)
+            assert (mn, mx) == (int(ids.min()), int(ids.max()))
+            assert mo == mono and ids_ok and has_pv == pv and has_big == big
+            want = sum(int(x) for x in t["amount_lo"]) + (sum(int(x) for x in t["amount_hi"]) << 64)
+            assert asum == want % (1 << 128)
+    finally:
+        eng.close()

@@ -112,6 +112,14 @@ struct tbgpu_ctx {
     u64* rt_ts_buf = nullptr;
     u8* rt_ctl_buf = nullptr;
     u64* rt_dry_ts = nullptr;
+    u64* rt_stats = nullptr;  // [5] tbgpu_route_stats
+    // the router's send-side scatter (route.hip), grown on demand
+    u64 ro_cap = 0, ro_bcap = 0;
+    uint2* ro_orank = nullptr;
+    u32* ro_blk = nullptr;
+    u32* ro_bstart = nullptr;
+    u64* ro_bts = nullptr;
+    u64* ro_counts = nullptr;
     const u64* rt_ev_ts = nullptr;
     const u8* rt_ctl = nullptr;
     bool rt_dry = false;
@@ -215,6 +223,7 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->rt_ts_buf = dalloc<u64>(n, &B);
     c->rt_ctl_buf = dalloc<u8>(n, &B);
     c->rt_dry_ts = dalloc<u64>(1, &B);
+    c->rt_stats = dalloc<u64>(8, &B);
     c->pc = dalloc<u32>(2 * PC_RING, &B);
     c->rg_part = dalloc<u64>(tr_range_part_words(n), &B);
     HIP_CHECK(hipHostMalloc((void**)&c->h_pc, 2 * PC_RING * sizeof(u32), hipHostMallocDefault));
@@ -339,6 +348,8 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     // Free every device allocation by walking the struct's pointers.
+    for (void* p : {(void*)c->ro_orank, (void*)c->ro_blk, (void*)c->ro_bstart, (void*)c->ro_bts, (void*)c->ro_counts})
+        if (p) (void)hipFree(p);
     void* ptrs[] = {c->T.dense, c->T.acc, c->T.aidx, c->T.xrows, c->T.xful, c->T.xidx, c->T.hrows, c->T.commit_ts, c->T.idr, c->T.big, c->ev_buf,
                     c->b_start, c->b_ts, c->ts, c->cs, c->ce, c->sres, c->dslot, c->cslot, c->pre_e, c->pre_p,
                     c->pp_dslot, c->pp_cslot, c->gslot, c->pslot, c->prev_id, c->pend_last, c->pend_first, c->prev_pend,
@@ -348,7 +359,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
                     c->sval_s, c->spos, c->bb, c->ss.keys_tmp, c->ss.vals_tmp, c->ss.hist, c->side_tiles,
                     c->sc.tile_sums, c->fres, c->mask, c->ranks, c->res_buf, c->counts, c->counters, c->status,
                     c->f_gtab, c->f_gpos, c->f_keys, c->f_rows,
-                    c->f_tile_idr, c->rt_ts_buf, c->rt_ctl_buf, c->rt_dry_ts, c->pc, c->rg_part, c->T.base, c->q_key, c->q_val, c->q_tkey,
+                    c->f_tile_idr, c->rt_ts_buf, c->rt_ctl_buf, c->rt_dry_ts, c->rt_stats, c->pc, c->rg_part, c->T.base, c->q_key, c->q_val, c->q_tkey,
                     c->q_tval, c->q_ss.keys_tmp, c->q_ss.vals_tmp, c->q_ss.hist, c->q_runs_dev, c->ximp};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     for (EvalState& s : c->st) {
@@ -877,6 +888,55 @@ extern "C" int tbgpu_import_transfers(tbgpu_ctx* c, const tbgpu_transfer_t* rows
     }
     set_base(c, BASE_ROWS, c->n_rows);
     c->rows_hi = c->n_rows;
+    return 0;
+}
+
+u64 route_block_count(u64 n);
+void route_stats(const Transfer* ev, u64 n, u64* out, hipStream_t stream);
+
+extern "C" int tbgpu_route_stats(tbgpu_ctx* c, const void* events_device, uint64_t count, uint64_t* out) {
+    HIP_CHECK(hipSetDevice(c->device));
+    route_stats((const Transfer*)events_device, count, c->rt_stats, c->stream);
+    HIP_CHECK(hipMemcpyAsync(out, c->rt_stats, 5 * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+void route_scatter(const Transfer* ev, u64 n, u32 world, u32 nb, const u32* b_start, const u64* b_ts, u64 g0,
+                   uint2* orank, u32* blk, u64* counts, Transfer* out_ev, u64* out_side, hipStream_t stream);
+
+extern "C" int tbgpu_route_scatter(tbgpu_ctx* c, uint32_t world, uint32_t batch_count, const uint32_t* counts,
+                                   const uint64_t* batch_timestamps, uint64_t first_global_batch,
+                                   const void* events_device, void* send_events_device, void* send_sides_device,
+                                   uint64_t* send_counts) {
+    HIP_CHECK(hipSetDevice(c->device));
+    if (world == 0 || world > 256) return -22;
+    std::vector<u32> starts(batch_count + 1, 0);
+    for (u32 b = 0; b < batch_count; b++) starts[b + 1] = starts[b] + counts[b];
+    const u64 n = starts[batch_count];
+    const u64 nblk = route_block_count(n);
+    if (n > c->ro_cap || world * std::max<u64>(nblk, 1) > c->ro_bcap || batch_count + 1 > c->ro_cap + 2) {
+        for (void* p : {(void*)c->ro_orank, (void*)c->ro_blk, (void*)c->ro_bstart, (void*)c->ro_bts, (void*)c->ro_counts})
+            if (p) HIP_CHECK(hipFree(p));
+        c->ro_cap = std::max<u64>(n, batch_count + 1);
+        c->ro_bcap = 256ull * std::max<u64>(route_block_count(c->ro_cap), 1);
+        HIP_CHECK(hipMalloc((void**)&c->ro_orank, c->ro_cap * sizeof(uint2)));
+        HIP_CHECK(hipMalloc((void**)&c->ro_blk, c->ro_bcap * sizeof(u32)));
+        HIP_CHECK(hipMalloc((void**)&c->ro_bstart, (c->ro_cap + 3) * sizeof(u32)));
+        HIP_CHECK(hipMalloc((void**)&c->ro_bts, (c->ro_cap + 3) * sizeof(u64)));
+        HIP_CHECK(hipMalloc((void**)&c->ro_counts, 256 * sizeof(u64)));
+    }
+    if (n == 0) {
+        for (u32 o = 0; o < world; o++) send_counts[o] = 0;
+        return 0;
+    }
+    HIP_CHECK(hipMemcpyAsync(c->ro_bstart, starts.data(), (batch_count + 1) * sizeof(u32), hipMemcpyHostToDevice,
+                             c->stream));
+    HIP_CHECK(hipMemcpyAsync(c->ro_bts, batch_timestamps, batch_count * sizeof(u64), hipMemcpyHostToDevice, c->stream));
+    route_scatter((const Transfer*)events_device, n, world, batch_count, c->ro_bstart, c->ro_bts, first_global_batch,
+                  c->ro_orank, c->ro_blk, c->ro_counts, (Transfer*)send_events_device, (u64*)send_sides_device,
+                  c->stream);
+    HIP_CHECK(hipMemcpyAsync(send_counts, c->ro_counts, world * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(hipStreamSynchronize(c->stream));
     return 0;
 }
 

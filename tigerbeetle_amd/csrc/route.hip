@@ -1,0 +1,257 @@
+// route.hip — the send side of a routed step (tigerbeetle_amd/shard.py).
+//
+// A rank's client batches go to the owners of their ledgers (owner = ledger %
+// world: a valid transfer has dr.ledger == cr.ledger == t.ledger,
+// src/state_machine.zig:1280-1281).  Before the all-to-all every event is placed in
+// an owner-major send buffer, in event order within an owner (each owner commits
+// its sub-batches in global order), beside a 32-byte side record carrying what
+// `execute` derives from the event's place in its batch (:1018-1035):
+//   [0] timestamp T - n + index + 1 of its batch,
+//   [1] global batch << 32 | index,
+//   [2] global batch << 32 | index of its chain's first member (the chain key),
+//   [3] bit 0: the chain has members on more than one owner, bit 1: the event ends
+//       its chain (not linked, or last of its batch).
+// Three launches: classify + stable rank within the workgroup, an exclusive scan of
+// the (owner, workgroup) counts, scatter.  Pure data movement: HBM-bound.
+#include "common.h"
+
+namespace {
+
+constexpr int RT_THREADS = 256;
+constexpr int RT_WAVES = RT_THREADS / 64;
+
+struct RouteArgs {
+    const Transfer* ev;
+    u64 n;
+    u32 world;
+    u32 nb;
+    const u32* b_start;   // [nb + 1] first event of each local batch
+    const u64* b_ts;      // [nb] prepare timestamp of each local batch
+    u64 g0;               // global number of the first local batch
+    uint2* orank;         // [n] owner, rank within (workgroup, owner)
+    u32* blk;             // [world * nblk] per-owner counts, then their exclusive scan
+    u32 nblk;
+    u64* counts;          // [world] events per owner
+    Transfer* out_ev;
+    u64* out_side;        // [n * 4]
+};
+
+__device__ __forceinline__ u32 rt_batch(const RouteArgs& A, u32 i) {
+    u32 lo = 0, hi = A.nb;  // last b with b_start[b] <= i
+    while (hi - lo > 1) {
+        const u32 mid = (lo + hi) / 2;
+        if (A.b_start[mid] <= i) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ u32 rt_owner(const RouteArgs& A, u64 i) { return A.ev[i].ledger % A.world; }
+
+__global__ __launch_bounds__(RT_THREADS) void rt_rank(RouteArgs A) {
+    __shared__ u32 s_cnt[RT_WAVES][256];
+    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (u32 o = tid; o < A.world; o += RT_THREADS)
+        for (int k = 0; k < RT_WAVES; k++) s_cnt[k][o] = 0;
+    __syncthreads();
+    const u64 i = (u64)blockIdx.x * RT_THREADS + tid;
+    const bool v = i < A.n;
+    const u32 own = v ? rt_owner(A, i) : NONE32;
+    // stable rank within the wave: one ballot per distinct owner present in the wave
+    u32 rank = 0;
+    u64 todo = __ballot(v);
+    while (todo) {
+        const u32 o = __shfl(own, __ffsll((unsigned long long)todo) - 1);
+        const u64 m = __ballot(own == o);
+        if (own == o) rank = __popcll(m & ((1ull << lane) - 1));
+        if (lane == 0) s_cnt[w][o] = __popcll(m);
+        todo &= ~m;
+    }
+    __syncthreads();
+    if (v) {
+        for (u32 k = 0; k < w; k++) rank += s_cnt[k][own];
+        A.orank[i] = make_uint2(own, rank);
+    }
+    for (u32 o = tid; o < A.world; o += RT_THREADS) {
+        u32 t = 0;
+        for (int k = 0; k < RT_WAVES; k++) t += s_cnt[k][o];
+        A.blk[(u64)o * A.nblk + blockIdx.x] = t;
+    }
+}
+
+// Exclusive scan of blk (owner-major) in one workgroup, and the per-owner totals.
+__global__ __launch_bounds__(1024) void rt_scan(RouteArgs A) {
+    __shared__ u64 s_part[1024];
+    const u64 total_n = (u64)A.world * A.nblk;
+    const u64 per = (total_n + 1023) / 1024;
+    const u64 b = threadIdx.x * per, e = min(total_n, b + per);
+    u64 sum = 0;
+    for (u64 k = b; k < e; k++) sum += A.blk[k];
+    s_part[threadIdx.x] = sum;
+    __syncthreads();
+    for (u32 off = 1; off < 1024; off <<= 1) {
+        const u64 x = threadIdx.x >= off ? s_part[threadIdx.x - off] : 0;
+        __syncthreads();
+        s_part[threadIdx.x] += x;
+        __syncthreads();
+    }
+    u64 run = s_part[threadIdx.x] - sum;  // exclusive
+    for (u64 k = b; k < e; k++) {
+        const u32 c = A.blk[k];
+        A.blk[k] = (u32)run;
+        run += c;
+    }
+    __syncthreads();
+    const u64 all = s_part[1023];
+    for (u32 o = threadIdx.x; o < A.world; o += 1024) {
+        const u64 s = A.blk[(u64)o * A.nblk];
+        const u64 t = o + 1 < A.world ? A.blk[(u64)(o + 1) * A.nblk] : all;
+        A.counts[o] = t - s;
+    }
+}
+
+__global__ __launch_bounds__(RT_THREADS) void rt_scatter(RouteArgs A) {
+    // the workgroup's first batch by one binary search; each event steps on from it
+    __shared__ u32 s_b0;
+    if (threadIdx.x == 0) s_b0 = rt_batch(A, (u32)((u64)blockIdx.x * RT_THREADS));
+    __syncthreads();
+    const u64 i = (u64)blockIdx.x * RT_THREADS + threadIdx.x;
+    const u32 lane = threadIdx.x & 63;
+    const u64 wbase = i - lane;
+    u64 dst = 0;
+    uint2 orr = make_uint2(0, 0);
+    if (i < A.n) {
+        orr = A.orank[i];
+        dst = (u64)A.blk[(u64)orr.x * A.nblk + blockIdx.x] + orr.y;
+    }
+    // the rows, eight lanes per row: each round moves eight whole rows (1 KiB) with
+    // one 16-byte access per lane, coalesced on both sides
+    const uint4* src = (const uint4*)A.ev;
+    uint4* out = (uint4*)A.out_ev;
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        const u32 k = (u32)r * 8 + (lane >> 3);
+        const u64 d = (u64)__shfl((unsigned long long)dst, (int)k);
+        if (wbase + k < A.n) out[d * 8 + (lane & 7)] = src[(wbase + k) * 8 + (lane & 7)];
+    }
+    if (i >= A.n) return;
+    // the side record: timestamp, position, chain key, span / end bits
+    u32 b = s_b0;
+    while (A.b_start[b + 1] <= (u32)i) b++;
+    const u32 bs = A.b_start[b], be = A.b_start[b + 1];
+    const u32 pos = (u32)i - bs, nbatch = be - bs;
+    const u64 g = A.g0 + b;
+    auto linked = [&](u32 j) { return (A.ev[j].flags & TF_LINKED) != 0; };
+    u32 s = (u32)i, e = (u32)i;
+    while (s > bs && linked(s - 1)) s--;
+    while (e + 1 < be && linked(e)) e++;
+    u32 omin = orr.x, omax = orr.x;
+    for (u32 j = s; j <= e; j++) {
+        const u32 o = rt_owner(A, j);
+        omin = min(omin, o);
+        omax = max(omax, o);
+    }
+    const bool last = !linked((u32)i) || pos == nbatch - 1;
+    ulonglong2* side = (ulonglong2*)&A.out_side[dst * 4];
+    side[0] = make_ulonglong2(A.b_ts[b] - nbatch + pos + 1, (g << 32) | pos);
+    side[1] = make_ulonglong2((g << 32) | (s - bs), (omin != omax ? 1ull : 0ull) | (last ? 2ull : 0ull));
+}
+
+// Eligibility of a step for the device path, in one pass over its events:
+// out[0] min id (low word), out[1] max id, out[2] bit 0: some id not above its
+// predecessor, bit 1: some id with a high word or zero, bit 2: a post/void,
+// bit 3: an amount with a high word; out[3..4] the sum of the amounts (u128).
+__global__ __launch_bounds__(RT_THREADS) void rt_stats(const Transfer* ev, u64 n, u64* out) {
+    // eight lanes per row, one 16-byte piece each (coalesced): piece 0 is the id,
+    // piece 3 the amount, piece 7 holds the flags
+    u64 mn = ~0ull, mx = 0, fl = 0, slo = 0, shi = 0;
+    const u32 lane = threadIdx.x & 63, piece = lane & 7;
+    const uint4* rows = (const uint4*)ev;
+    const u64 waves = (u64)gridDim.x * (RT_THREADS / 64);
+    constexpr int U = 4;  // rounds in flight per wave
+    for (u64 r0 = (u64)blockIdx.x * (RT_THREADS / 64) + (threadIdx.x >> 6); r0 * 8 < n; r0 += U * waves) {
+        uint4 v[U], pv[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const u64 i = (r0 + u * waves) * 8 + (lane >> 3);
+            v[u] = i < n ? rows[i * 8 + piece] : make_uint4(0, 0, 0, 0);
+            pv[u] = piece == 0 && i < n && i > 0 ? rows[(i - 1) * 8] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const u64 i = (r0 + u * waves) * 8 + (lane >> 3);
+            if (i >= n) continue;
+            const u64 lo = ((u64)v[u].y << 32) | v[u].x, hi = ((u64)v[u].w << 32) | v[u].z;
+            if (piece == 0) {
+                mn = min(mn, lo);
+                mx = max(mx, lo);
+                if (hi != 0 || lo == 0) fl |= 2;
+                const u64 plo = ((u64)pv[u].y << 32) | pv[u].x, phi = ((u64)pv[u].w << 32) | pv[u].z;
+                if (i > 0 && !(phi < hi || (phi == hi && plo < lo))) fl |= 1;
+            } else if (piece == 3) {
+                if (hi) fl |= 8;
+                slo += lo;
+                shi += hi + (slo < lo ? 1 : 0);
+            } else if (piece == 7) {
+                if ((v[u].y >> 16) & (TF_POST | TF_VOID)) fl |= 4;
+            }
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        mn = min(mn, (u64)__shfl_xor((unsigned long long)mn, off));
+        mx = max(mx, (u64)__shfl_xor((unsigned long long)mx, off));
+        fl |= (u64)__shfl_xor((unsigned long long)fl, off);
+        const u64 olo = (u64)__shfl_xor((unsigned long long)slo, off);
+        const u64 ohi = (u64)__shfl_xor((unsigned long long)shi, off);
+        const u64 t = slo + olo;
+        shi += ohi + (t < slo ? 1 : 0);
+        slo = t;
+    }
+    // the workgroup's result, then one set of atomics per workgroup (same-address
+    // atomics serialize: one set per wave cost more than the pass over the rows)
+    __shared__ u64 s_r[RT_THREADS / 64][5];
+    const u32 w = threadIdx.x >> 6;
+    if (lane == 0) {
+        s_r[w][0] = mn; s_r[w][1] = mx; s_r[w][2] = fl; s_r[w][3] = slo; s_r[w][4] = shi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < RT_THREADS / 64; k++) {
+            mn = min(mn, s_r[k][0]);
+            mx = max(mx, s_r[k][1]);
+            fl |= s_r[k][2];
+            const u64 t = slo + s_r[k][3];
+            shi += s_r[k][4] + (t < slo ? 1 : 0);
+            slo = t;
+        }
+        atomicMin((unsigned long long*)&out[0], (unsigned long long)mn);
+        atomicMax((unsigned long long*)&out[1], (unsigned long long)mx);
+        if (fl) atomicOr((unsigned long long*)&out[2], (unsigned long long)fl);
+        if (slo || shi) {
+            const u64 old = atomicAdd((unsigned long long*)&out[3], (unsigned long long)slo);
+            atomicAdd((unsigned long long*)&out[4], (unsigned long long)(shi + (old + slo < old ? 1 : 0)));
+        }
+    }
+}
+
+}  // namespace
+
+void route_stats(const Transfer* ev, u64 n, u64* out, hipStream_t stream) {
+    const u64 init[5] = {~0ull, 0, 0, 0, 0};
+    HIP_CHECK(hipMemcpyAsync(out, init, sizeof init, hipMemcpyHostToDevice, stream));
+    if (n) rt_stats<<<(u32)std::min<u64>((n + RT_THREADS / 8 - 1) / (RT_THREADS / 8), 1024), RT_THREADS, 0, stream>>>(ev, n, out);
+    HIP_CHECK(hipGetLastError());
+}
+
+u64 route_block_count(u64 n) { return (n + RT_THREADS - 1) / RT_THREADS; }
+
+void route_scatter(const Transfer* ev, u64 n, u32 world, u32 nb, const u32* b_start, const u64* b_ts, u64 g0,
+                   uint2* orank, u32* blk, u64* counts, Transfer* out_ev, u64* out_side, hipStream_t stream) {
+    RouteArgs A{};
+    A.ev = ev; A.n = n; A.world = world; A.nb = nb; A.b_start = b_start; A.b_ts = b_ts; A.g0 = g0;
+    A.orank = orank; A.blk = blk; A.nblk = (u32)route_block_count(n); A.counts = counts;
+    A.out_ev = out_ev; A.out_side = out_side;
+    if (n) rt_rank<<<A.nblk, RT_THREADS, 0, stream>>>(A);
+    rt_scan<<<1, 1024, 0, stream>>>(A);
+    if (n) rt_scatter<<<A.nblk, RT_THREADS, 0, stream>>>(A);
+    HIP_CHECK(hipGetLastError());
+}

@@ -105,6 +105,10 @@ def lib():
     L.tbgpu_create_transfers_routed_device.restype = u64
     L.tbgpu_create_transfers_routed_device.argtypes = [vp, u32, vp, vp, vp, vp, ctypes.c_int, vp, vp,
                                                        ctypes.POINTER(ctypes.c_uint64)]
+    L.tbgpu_route_scatter.restype = ctypes.c_int
+    L.tbgpu_route_scatter.argtypes = [vp, u32, u32, vp, vp, u64, vp, vp, vp, vp]
+    L.tbgpu_route_stats.restype = ctypes.c_int
+    L.tbgpu_route_stats.argtypes = [vp, vp, u64, vp]
     L.tbgpu_import_transfers.restype = ctypes.c_int
     L.tbgpu_import_transfers.argtypes = [vp, vp, u32]
     L.tbgpu_advance_commit_timestamp.argtypes = [vp, u64]
@@ -251,6 +255,34 @@ class Engine:
         rows = np.ascontiguousarray(rows, dtype=TRANSFER_DTYPE)
         if len(rows):
             self._L.tbgpu_import_transfers(self._h, _ptr(rows), len(rows))
+
+    def route_scatter(self, world: int, counts, batch_timestamps, first_global_batch: int, events, send_events,
+                      send_sides) -> np.ndarray:
+        """The send side of a routed step (tbgpu_route_scatter): `events` (uint8 device
+        tensor, n*128 B) to owner-major `send_events` (n*128 B) with 32-byte records in
+        `send_sides` (n*32 B).  Returns the events per owner."""
+        import torch
+        torch.cuda.current_stream(events.device).synchronize()
+        cs = np.ascontiguousarray(counts, dtype=np.uint32)
+        ts = np.ascontiguousarray(batch_timestamps, dtype=np.uint64)
+        out = np.zeros(world, dtype=np.uint64)
+        rc = self._L.tbgpu_route_scatter(self._h, world, len(cs), _ptr(cs), _ptr(ts), int(first_global_batch),
+                                         ctypes.c_void_p(events.data_ptr()), ctypes.c_void_p(send_events.data_ptr()),
+                                         ctypes.c_void_p(send_sides.data_ptr()), _ptr(out))
+        if rc != 0:
+            raise ValueError(f"tbgpu_route_scatter failed ({rc})")
+        return out
+
+    def route_stats(self, events, n: int):
+        """tbgpu_route_stats over n events of a uint8 device tensor: (min id, max id,
+        monotone, plain ids, any post/void, any amount >= 2^64, amount sum)."""
+        import torch
+        torch.cuda.current_stream(events.device).synchronize()
+        out = np.zeros(5, dtype=np.uint64)
+        self._L.tbgpu_route_stats(self._h, ctypes.c_void_p(events.data_ptr()), int(n), _ptr(out))
+        fl = int(out[2])
+        return (int(out[0]), int(out[1]), not (fl & 1), not (fl & 2), bool(fl & 4), bool(fl & 8),
+                int(out[3]) | (int(out[4]) << 64))
 
     def advance_commit_timestamp(self, ts: int) -> None:
         self._L.tbgpu_advance_commit_timestamp(self._h, int(ts))

@@ -143,7 +143,8 @@ class ShardedStateMachine:
         self.limit_ids: set[int] = set()  # ids of accounts created with a balance limit flag
         self.amount_bound = 0.0  # >= the sum of every transfer amount routed: bounds every balance
         self.timed = False       # accumulate per-phase wall times of the device step (with syncs)
-        self.timing = {"partition_ms": 0.0, "exchange_ms": 0.0, "commit_ms": 0.0, "replies_ms": 0.0}
+        self.timing = {"eligibility_ms": 0.0, "order_ms": 0.0, "partition_ms": 0.0, "exchange_ms": 0.0,
+                       "commit_ms": 0.0, "replies_ms": 0.0}
         self.stats = {"steps": 0, "splits": 0, "dry_rounds": 0, "cross_chains": 0, "imports": 0,
                       "preruns": 0, "serial_fallbacks": 0, "device_fallbacks": 0}
 
@@ -262,7 +263,13 @@ class ShardedStateMachine:
         flags = (w32[:, 29] >> 16) & 0xFFFF
         id_lo, id_hi = w64[:, 0], w64[:, 1]
         # eligibility, one small all-gather: [n, min id, max id, monotone, plain, amount bound in 2^32 units]
-        if n:
+        if n and ev.is_cuda and hasattr(self.backend, "route_stats"):
+            # one pass of the engine's kernel (csrc/route.hip) instead of the torch reductions
+            mn, mx, mono, ids_ok, pv, big, asum = self.backend.route_stats(ev, n)
+            ok_ids = ids_ok and mx < (1 << 63)  # the all-gather below carries int64
+            units = (1 << 62) if big else (asum >> 32) + 2
+            st = [n, mn if ok_ids else 0, mx if ok_ids else 0, int(mono), int(ok_ids and not pv), units]
+        elif n:
             mono = bool((id_lo[1:] > id_lo[:-1]).all()) if n > 1 else True
             plain = bool(((flags & POST_VOID) == 0).all() & (id_hi == 0).all() & (id_lo > 0).all())
             a = w64[:, 6].double()
@@ -286,6 +293,7 @@ class ShardedStateMachine:
         if not ok:
             host = ev.cpu().numpy().view(TRANSFER_DTYPE)
             return self.create_transfers([host[offs_h[j]:offs_h[j + 1]] for j in range(len(counts))])
+        clock("eligibility_ms")
         saved = (self.prepare_timestamp, self.max_id, self.amount_bound)
         self.max_id = max(self.max_id, prev)
         self.amount_bound += sum(float(x[5]) for x in allst) * 2.0**32
@@ -298,33 +306,16 @@ class ShardedStateMachine:
             self.prepare_timestamp += 1 + c
             T.append(self.prepare_timestamp)
         g0 = sum(len(cl) for cl in counts_all[:me])
-        if n:
-            cnt_t = torch.tensor(list(counts), dtype=torch.int64, device=dev)
-            nb = len(counts)
-            bidx = torch.repeat_interleave(torch.arange(nb, device=dev), cnt_t)
-            bstart = torch.cumsum(cnt_t, 0) - cnt_t
-            pos = torch.arange(n, device=dev) - bstart[bidx]
-            g = bidx + g0
-            Tg = torch.tensor(T, dtype=torch.int64, device=dev)
-            ng = torch.tensor([c for (_, _, c) in glob], dtype=torch.int64, device=dev)
-            ts = Tg[g] - ng[g] + pos + 1
-            linked = (flags & LINKED) != 0
-            prev_l = torch.zeros_like(linked)
-            prev_l[1:] = linked[:-1]
-            prev_l &= pos > 0
-            ar = torch.arange(n, device=dev)
-            cstart = torch.cummax(torch.where(prev_l, torch.zeros_like(ar), ar), 0).values
-            last = ~linked | (pos == cnt_t[bidx] - 1)      # the chain's own last member
-            owner = ((w32[:, 28].to(torch.int64) & 0xFFFFFFFF) % W)
-            omin = torch.full((n,), W, dtype=torch.int64, device=dev).scatter_reduce(0, cstart, owner, "amin")
-            omax = torch.full((n,), -1, dtype=torch.int64, device=dev).scatter_reduce(0, cstart, owner, "amax")
-            span = omin[cstart] != omax[cstart]
-            side = torch.stack([ts, (g << 32) | pos, (g << 32) | (cstart - bstart[bidx]),
-                                span.to(torch.int64) | (last.to(torch.int64) << 1)], 1)
-            perm = torch.argsort(owner, stable=True)
-            send = torch.bincount(owner, minlength=W)
-            ev_s = ev.view(n, 128).index_select(0, perm)
-            side_s = side.index_select(0, perm)
+        clock("order_ms")
+        native = n and ev.is_cuda and hasattr(self.backend, "route_scatter")
+        if native:
+            # the engine's scatter kernels (csrc/route.hip): same layout as below
+            ev_s = torch.empty((n, 128), dtype=torch.uint8, device=dev)
+            side_s = torch.empty((n, 4), dtype=torch.int64, device=dev)
+            sc = self.backend.route_scatter(W, list(map(int, counts)), T[g0:g0 + len(counts)], g0, ev, ev_s, side_s)
+            send = torch.from_numpy(sc.astype(np.int64)).to(dev)
+        elif n:
+            ev_s, side_s, send = partition_torch(torch, ev, counts, T[g0:g0 + len(counts)], g0, W, dev)
         else:
             send = torch.zeros(W, dtype=torch.int64, device=dev)
             ev_s = torch.zeros((0, 128), dtype=torch.uint8, device=dev)
@@ -905,3 +896,38 @@ class ShardedStateMachine:
         xs = self.backend.export_transfers()
         keep = np.array([self.owner_of_ledger(l) == self.rank for l in xs["ledger"]], dtype=bool)
         return acc[own] if len(acc) else acc, xs[keep] if len(xs) else xs
+
+
+def partition_torch(torch, ev, counts, batch_ts, g0: int, W: int, dev):
+    """The send side of a routed step with torch tensor ops (the CPU-collective tests'
+    path; on GPUs the engine's tbgpu_route_scatter computes the same thing): events
+    owner-major (owner = ledger % W), in event order within an owner, with their
+    32-byte side records {timestamp, g << 32 | index, g << 32 | chain start, span |
+    end << 1}.  Returns (events [n, 128], records [n, 4], per-owner counts)."""
+    n = int(sum(counts))
+    w32 = ev.view(torch.int32).view(n, 32)
+    flags = (w32[:, 29] >> 16) & 0xFFFF
+    cnt_t = torch.tensor(list(counts), dtype=torch.int64, device=dev)
+    nb = len(counts)
+    bidx = torch.repeat_interleave(torch.arange(nb, device=dev), cnt_t)
+    bstart = torch.cumsum(cnt_t, 0) - cnt_t
+    pos = torch.arange(n, device=dev) - bstart[bidx]
+    Tb = torch.tensor(list(map(int, batch_ts)), dtype=torch.int64, device=dev)
+    ts = Tb[bidx] - cnt_t[bidx] + pos + 1
+    g = bidx + g0
+    linked = (flags & LINKED) != 0
+    prev_l = torch.zeros_like(linked)
+    prev_l[1:] = linked[:-1]
+    prev_l &= pos > 0
+    ar = torch.arange(n, device=dev)
+    cstart = torch.cummax(torch.where(prev_l, torch.zeros_like(ar), ar), 0).values
+    last = ~linked | (pos == cnt_t[bidx] - 1)      # the chain's own last member
+    owner = ((w32[:, 28].to(torch.int64) & 0xFFFFFFFF) % W)
+    omin = torch.full((n,), W, dtype=torch.int64, device=dev).scatter_reduce(0, cstart, owner, "amin")
+    omax = torch.full((n,), -1, dtype=torch.int64, device=dev).scatter_reduce(0, cstart, owner, "amax")
+    span = omin[cstart] != omax[cstart]
+    side = torch.stack([ts, (g << 32) | pos, (g << 32) | (cstart - bstart[bidx]),
+                        span.to(torch.int64) | (last.to(torch.int64) << 1)], 1)
+    perm = torch.argsort(owner, stable=True)
+    send = torch.bincount(owner, minlength=W)
+    return ev.view(n, 128).index_select(0, perm), side.index_select(0, perm), send

@@ -280,6 +280,43 @@ def routed_bench(args, rank, world, local_rank, torch, dist, backend="nccl"):
     dist.destroy_process_group()
 
 
+def verify_stream(eng, w, ats, tts, counts, B, steps, replies, acc_n):
+    """The same stream through the CPU oracle (test infrastructure: the checker, never
+    the thing measured): every batch's replies of every step, then every account row
+    and every stored transfer row, bit for bit."""
+    import oracle
+    from tigerbeetle_amd.types import ACCOUNT_DTYPE, RESULT_DTYPE
+    nb = steps * B
+    n = int(counts[:nb].sum())
+    orc = oracle.Oracle(acc_n, n + 1024)
+    try:
+        orc.create_accounts_batches(ats, w.account_counts, w.accounts)
+        off = 0
+        mismatches = []
+        for k in range(steps):
+            b0 = k * B
+            m = int(counts[b0:b0 + B].sum())
+            o, orc_rc, _ = orc.create_transfers_batches(tts[b0:b0 + B], counts[b0:b0 + B], w.transfers[off:off + m])
+            g_rc, g_res = replies[k]
+            want = np.concatenate([o[int(s):int(s) + int(c)] for s, c in
+                                   zip(np.concatenate([[0], np.cumsum(counts[b0:b0 + B])[:-1]]), orc_rc)]) \
+                if int(orc_rc.sum()) else np.zeros(0, RESULT_DTYPE)
+            if not np.array_equal(g_rc, orc_rc) or g_res.tobytes() != want.tobytes():
+                mismatches.append(k)
+            off += m
+        key = lambda a: a[np.lexsort((a["id_lo"], a["id_hi"]))]
+        ga, oa = key(eng.export_accounts()), key(orc.export_accounts())
+        accounts_equal = ga.tobytes() == oa.tobytes()
+        transfers_equal = eng.export_transfers().tobytes() == orc.export_transfers().tobytes()
+        non_ok = sum(int(r[0].sum()) for r in replies)
+        return {"steps": steps, "batches": nb, "transfers": n, "non_ok_results": non_ok,
+                "replies_bit_exact": not mismatches, "mismatched_steps": mismatches[:8],
+                "accounts_bit_exact": accounts_equal, "stored_transfers_bit_exact": transfers_equal,
+                "checker": "oracle/oracle.c over the same batches in the same order"}
+    finally:
+        orc.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -303,7 +340,9 @@ def main():
     ap.add_argument("--no-host", action="store_true", help="skip the host-buffer (drop-in call) measurement")
     ap.add_argument("--host-batches", type=int, default=None,
                     help="batches for the host-buffer measurement (default 64 single calls + 256 streamed)")
-    ap.add_argument("--verify", action="store_true", help="check every result is ok (config 1/2 never fail)")
+    ap.add_argument("--verify", action="store_true",
+                    help="after the timed region, replay the same stream through the CPU oracle and compare "
+                         "every reply and the final state bit for bit (configs 1-4)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -408,10 +447,14 @@ def main():
     ev_base = ev_dev.data_ptr()
     res_ptr = res_dev.data_ptr()
 
+    replies = []  # --verify: every step's replies (copied after the step, outside nothing timed by HIP events)
+
     def step(k):
         b0 = k * B
         off = int(counts[:b0].sum()) * 128
         total, rcs = eng.create_transfers_batches_device(tts[b0:b0 + B], counts[b0:b0 + B], ev_base + off, res_ptr)
+        if args.verify:
+            replies.append((np.array(rcs, dtype=np.uint32).copy(), res_dev[:int(total) * 8].cpu().numpy().copy()))
         return int(total)
 
     for k in range(W):
@@ -504,6 +547,11 @@ def main():
         "device_ms_per_step": round(dev_ms / K, 4),
     }
 
+    verify = None
+    if args.verify and w is not None:
+        verify = verify_stream(eng, w, ats, tts, counts, B, W + K, replies, acc_n)
+        log(f"[rank {rank}] verify: {verify}")
+
     queries = None
     if rank == 0 and not args.no_queries and w is not None:
         queries = query_phase(eng, w, acc_n, torch, dev)
@@ -585,6 +633,7 @@ def main():
             "cpu_baseline": cpu,
             "host_path": host,
             "queries": queries,
+            "verify": verify,
         }
         print(json.dumps(line), flush=True)
     eng.close()

@@ -530,6 +530,9 @@ def main():
         basis = (f"{ALGO_BYTES_PER_TRANSFER} B x {per_rank - n_pv} transfers + {PV_BYTES} B x {n_pv} posts/voids "
                  f"+ 8 B x {non_ok // world} non-ok replies over {K} calls / call device time "
                  f"({call_ms:.4f} ms, HIP events on the engine stream)")
+    # the same launch time priced with the measured HBM bytes instead of the algorithmic ones
+    t_ms = commit_ms if fast else dev_ms / K
+    traffic_gbps = traffic / (t_ms * 1e-3) / 1e9 if traffic and t_ms > 0 else None
     roofline = {
         "bound": "hbm",
         "achieved": round(achieved, 2),
@@ -538,6 +541,8 @@ def main():
         "frac": round(achieved / HBM_PEAK_GBPS, 5),
         "traffic": traffic,
         "traffic_source": traffic_src,
+        "traffic_achieved": round(traffic_gbps, 2) if traffic_gbps else None,
+        "traffic_frac": round(traffic_gbps / HBM_PEAK_GBPS, 5) if traffic_gbps else None,
         "kernel": kernel,
         "basis": basis,
         "end_to_end": {"achieved": round(e2e_gbps, 2), "frac": round(e2e_gbps / HBM_PEAK_GBPS, 5),

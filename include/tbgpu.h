@@ -345,7 +345,9 @@ uint64_t tbgpu_create_transfers_routed_device(tbgpu_ctx* ctx, uint32_t batch_cou
  * order within an owner, each with a 32-byte record in `send_sides_device` (n * 32 B):
  * {event timestamp, global batch << 32 | index, global batch << 32 | index of its
  * chain's first member, bit 0: the chain spans owners | bit 1: the event ends its
- * chain}.  `send_counts[world]` (host) receives the events per owner.  world <= 256.
+ * chain}.  `send_counts[world]` (host) receives the events per owner; when not NULL,
+ * `send_batch_counts[world * batch_count]` the events per (owner, batch) and
+ * `send_span_counts[world]` the events per owner whose chain spans owners.  world <= 256.
  * Returns 0, or -22 for a bad argument.  Synchronous. */
 /* One pass over a routed step's local events (device memory) deciding whether the
  * device path applies: out[0] min id (low word), out[1] max id (low word), out[2]
@@ -355,7 +357,8 @@ uint64_t tbgpu_create_transfers_routed_device(tbgpu_ctx* ctx, uint32_t batch_cou
 int tbgpu_route_stats(tbgpu_ctx* ctx, const void* events_device, uint64_t count, uint64_t* out);
 int tbgpu_route_scatter(tbgpu_ctx* ctx, uint32_t world, uint32_t batch_count, const uint32_t* counts,
                         const uint64_t* batch_timestamps, uint64_t first_global_batch, const void* events_device,
-                        void* send_events_device, void* send_sides_device, uint64_t* send_counts);
+                        void* send_events_device, void* send_sides_device, uint64_t* send_counts,
+                        uint32_t* send_batch_counts, uint32_t* send_span_counts);
 
 /* Copy committed transfers of another shard into this ctx's transfer table and id
  * index, without balance or posted effects: the `exists` comparisons of

@@ -62,11 +62,13 @@ def test_route_scatter_matches_torch_partition():
     eng = Engine(device=0, accounts_max=16, transfers_max=16, events_per_call_max=1 << 12)
     try:
         for W in (1, 2, 3, 8, 256):
-            e_t, s_t, c_t = partition_torch(torch, ev, counts, bts, 5, W, dev)
+            e_t, s_t, c_t, b_t, p_t = partition_torch(torch, ev, counts, bts, 5, W, dev, detail=True)
             e_n = torch.empty((n, 128), dtype=torch.uint8, device=dev)
             s_n = torch.empty((n, 4), dtype=torch.int64, device=dev)
-            c_n = eng.route_scatter(W, counts, bts, 5, ev, e_n, s_n)
+            c_n, b_n, p_n = eng.route_scatter(W, counts, bts, 5, ev, e_n, s_n, detail=True)
             assert c_n.tolist() == c_t.cpu().tolist(), W
+            assert b_n.tolist() == b_t.cpu().tolist(), W
+            assert p_n.tolist() == p_t.cpu().tolist(), W
             assert torch.equal(e_n, e_t), W
             assert torch.equal(s_n, s_t), W
     finally:

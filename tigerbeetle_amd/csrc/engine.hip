@@ -120,6 +120,8 @@ struct tbgpu_ctx {
     u32* ro_bstart = nullptr;
     u64* ro_bts = nullptr;
     u64* ro_counts = nullptr;
+    u32* ro_bcount = nullptr;  // [256] spanning counts per owner, then [world * batches] per (owner, batch)
+    u64 ro_bc_cap = 0;
     const u64* rt_ev_ts = nullptr;
     const u8* rt_ctl = nullptr;
     bool rt_dry = false;
@@ -348,7 +350,8 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     // Free every device allocation by walking the struct's pointers.
-    for (void* p : {(void*)c->ro_orank, (void*)c->ro_blk, (void*)c->ro_bstart, (void*)c->ro_bts, (void*)c->ro_counts})
+    for (void* p : {(void*)c->ro_orank, (void*)c->ro_blk, (void*)c->ro_bstart, (void*)c->ro_bts, (void*)c->ro_counts,
+                    (void*)c->ro_bcount})
         if (p) (void)hipFree(p);
     void* ptrs[] = {c->T.dense, c->T.acc, c->T.aidx, c->T.xrows, c->T.xful, c->T.xidx, c->T.hrows, c->T.commit_ts, c->T.idr, c->T.big, c->ev_buf,
                     c->b_start, c->b_ts, c->ts, c->cs, c->ce, c->sres, c->dslot, c->cslot, c->pre_e, c->pre_p,
@@ -902,20 +905,23 @@ extern "C" int tbgpu_route_stats(tbgpu_ctx* c, const void* events_device, uint64
     return 0;
 }
 void route_scatter(const Transfer* ev, u64 n, u32 world, u32 nb, const u32* b_start, const u64* b_ts, u64 g0,
-                   uint2* orank, u32* blk, u64* counts, Transfer* out_ev, u64* out_side, hipStream_t stream);
+                   uint2* orank, u32* blk, u64* counts, Transfer* out_ev, u64* out_side, u32* bcount, u32* scount,
+                   hipStream_t stream);
 
 extern "C" int tbgpu_route_scatter(tbgpu_ctx* c, uint32_t world, uint32_t batch_count, const uint32_t* counts,
                                    const uint64_t* batch_timestamps, uint64_t first_global_batch,
                                    const void* events_device, void* send_events_device, void* send_sides_device,
-                                   uint64_t* send_counts) {
+                                   uint64_t* send_counts, uint32_t* send_batch_counts, uint32_t* send_span_counts) {
     HIP_CHECK(hipSetDevice(c->device));
     if (world == 0 || world > 256) return -22;
     std::vector<u32> starts(batch_count + 1, 0);
     for (u32 b = 0; b < batch_count; b++) starts[b + 1] = starts[b] + counts[b];
     const u64 n = starts[batch_count];
     const u64 nblk = route_block_count(n);
-    if (n > c->ro_cap || world * std::max<u64>(nblk, 1) > c->ro_bcap || batch_count + 1 > c->ro_cap + 2) {
-        for (void* p : {(void*)c->ro_orank, (void*)c->ro_blk, (void*)c->ro_bstart, (void*)c->ro_bts, (void*)c->ro_counts})
+    if (n > c->ro_cap || world * std::max<u64>(nblk, 1) > c->ro_bcap || batch_count + 1 > c->ro_cap + 2 ||
+        (u64)world * batch_count > c->ro_bc_cap) {
+        for (void* p : {(void*)c->ro_orank, (void*)c->ro_blk, (void*)c->ro_bstart, (void*)c->ro_bts, (void*)c->ro_counts,
+                        (void*)c->ro_bcount})
             if (p) HIP_CHECK(hipFree(p));
         c->ro_cap = std::max<u64>(n, batch_count + 1);
         c->ro_bcap = 256ull * std::max<u64>(route_block_count(c->ro_cap), 1);
@@ -924,9 +930,13 @@ extern "C" int tbgpu_route_scatter(tbgpu_ctx* c, uint32_t world, uint32_t batch_
         HIP_CHECK(hipMalloc((void**)&c->ro_bstart, (c->ro_cap + 3) * sizeof(u32)));
         HIP_CHECK(hipMalloc((void**)&c->ro_bts, (c->ro_cap + 3) * sizeof(u64)));
         HIP_CHECK(hipMalloc((void**)&c->ro_counts, 256 * sizeof(u64)));
+        c->ro_bc_cap = std::max<u64>((u64)world * batch_count, 256ull * 64);
+        HIP_CHECK(hipMalloc((void**)&c->ro_bcount, (c->ro_bc_cap + 256) * sizeof(u32)));
     }
     if (n == 0) {
         for (u32 o = 0; o < world; o++) send_counts[o] = 0;
+        if (send_batch_counts) memset(send_batch_counts, 0, (u64)world * batch_count * sizeof(u32));
+        if (send_span_counts) memset(send_span_counts, 0, world * sizeof(u32));
         return 0;
     }
     HIP_CHECK(hipMemcpyAsync(c->ro_bstart, starts.data(), (batch_count + 1) * sizeof(u32), hipMemcpyHostToDevice,
@@ -934,8 +944,13 @@ extern "C" int tbgpu_route_scatter(tbgpu_ctx* c, uint32_t world, uint32_t batch_
     HIP_CHECK(hipMemcpyAsync(c->ro_bts, batch_timestamps, batch_count * sizeof(u64), hipMemcpyHostToDevice, c->stream));
     route_scatter((const Transfer*)events_device, n, world, batch_count, c->ro_bstart, c->ro_bts, first_global_batch,
                   c->ro_orank, c->ro_blk, c->ro_counts, (Transfer*)send_events_device, (u64*)send_sides_device,
-                  c->stream);
+                  c->ro_bcount + 256, c->ro_bcount, c->stream);
     HIP_CHECK(hipMemcpyAsync(send_counts, c->ro_counts, world * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    if (send_batch_counts)
+        HIP_CHECK(hipMemcpyAsync(send_batch_counts, c->ro_bcount + 256, (u64)world * batch_count * sizeof(u32),
+                                 hipMemcpyDeviceToHost, c->stream));
+    if (send_span_counts)
+        HIP_CHECK(hipMemcpyAsync(send_span_counts, c->ro_bcount, world * sizeof(u32), hipMemcpyDeviceToHost, c->stream));
     HIP_CHECK(hipStreamSynchronize(c->stream));
     return 0;
 }

@@ -34,6 +34,8 @@ struct RouteArgs {
     u64* counts;          // [world] events per owner
     Transfer* out_ev;
     u64* out_side;        // [n * 4]
+    u32* bcount;          // [world * nb] events per (owner, local batch)
+    u32* scount;          // [world] events per owner whose chain spans owners
 };
 
 __device__ __forceinline__ u32 rt_batch(const RouteArgs& A, u32 i) {
@@ -151,6 +153,26 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scatter(RouteArgs A) {
         omax = max(omax, o);
     }
     const bool last = !linked((u32)i) || pos == nbatch - 1;
+    // per (owner, batch) and per-owner spanning counts: one atomic per distinct key per wave
+    {
+        const u32 key = orr.x * A.nb + b;
+        u64 todo = __ballot(true);
+        while (todo) {
+            const u32 k = __shfl(key, __ffsll((unsigned long long)todo) - 1);
+            const u64 mk = __ballot(key == k);
+            if (key == k && lane == (u32)__ffsll((unsigned long long)mk) - 1) atomicAdd(&A.bcount[k], (u32)__popcll(mk));
+            todo &= ~mk;
+        }
+        const bool sp = omin != omax;
+        todo = __ballot(sp);
+        while (todo) {
+            const u32 o = __shfl(orr.x, __ffsll((unsigned long long)todo) - 1);
+            const u64 mo = __ballot(sp && orr.x == o);
+            if (sp && orr.x == o && lane == (u32)__ffsll((unsigned long long)mo) - 1)
+                atomicAdd(&A.scount[o], (u32)__popcll(mo));
+            todo &= ~mo;
+        }
+    }
     ulonglong2* side = (ulonglong2*)&A.out_side[dst * 4];
     side[0] = make_ulonglong2(A.b_ts[b] - nbatch + pos + 1, (g << 32) | pos);
     side[1] = make_ulonglong2((g << 32) | (s - bs), (omin != omax ? 1ull : 0ull) | (last ? 2ull : 0ull));
@@ -245,8 +267,13 @@ void route_stats(const Transfer* ev, u64 n, u64* out, hipStream_t stream) {
 u64 route_block_count(u64 n) { return (n + RT_THREADS - 1) / RT_THREADS; }
 
 void route_scatter(const Transfer* ev, u64 n, u32 world, u32 nb, const u32* b_start, const u64* b_ts, u64 g0,
-                   uint2* orank, u32* blk, u64* counts, Transfer* out_ev, u64* out_side, hipStream_t stream) {
+                   uint2* orank, u32* blk, u64* counts, Transfer* out_ev, u64* out_side, u32* bcount, u32* scount,
+                   hipStream_t stream) {
     RouteArgs A{};
+    A.bcount = bcount;
+    A.scount = scount;
+    HIP_CHECK(hipMemsetAsync(bcount, 0, (u64)world * nb * sizeof(u32), stream));
+    HIP_CHECK(hipMemsetAsync(scount, 0, world * sizeof(u32), stream));
     A.ev = ev; A.n = n; A.world = world; A.nb = nb; A.b_start = b_start; A.b_ts = b_ts; A.g0 = g0;
     A.orank = orank; A.blk = blk; A.nblk = (u32)route_block_count(n); A.counts = counts;
     A.out_ev = out_ev; A.out_side = out_side;

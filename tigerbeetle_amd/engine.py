@@ -106,7 +106,7 @@ def lib():
     L.tbgpu_create_transfers_routed_device.argtypes = [vp, u32, vp, vp, vp, vp, ctypes.c_int, vp, vp,
                                                        ctypes.POINTER(ctypes.c_uint64)]
     L.tbgpu_route_scatter.restype = ctypes.c_int
-    L.tbgpu_route_scatter.argtypes = [vp, u32, u32, vp, vp, u64, vp, vp, vp, vp]
+    L.tbgpu_route_scatter.argtypes = [vp, u32, u32, vp, vp, u64, vp, vp, vp, vp, vp, vp]
     L.tbgpu_route_stats.restype = ctypes.c_int
     L.tbgpu_route_stats.argtypes = [vp, vp, u64, vp]
     L.tbgpu_import_transfers.restype = ctypes.c_int
@@ -257,21 +257,24 @@ class Engine:
             self._L.tbgpu_import_transfers(self._h, _ptr(rows), len(rows))
 
     def route_scatter(self, world: int, counts, batch_timestamps, first_global_batch: int, events, send_events,
-                      send_sides) -> np.ndarray:
+                      send_sides, detail: bool = False):
         """The send side of a routed step (tbgpu_route_scatter): `events` (uint8 device
         tensor, n*128 B) to owner-major `send_events` (n*128 B) with 32-byte records in
-        `send_sides` (n*32 B).  Returns the events per owner."""
+        `send_sides` (n*32 B).  Returns the events per owner; with `detail`, also the
+        events per (owner, batch) and the spanning events per owner."""
         import torch
         torch.cuda.current_stream(events.device).synchronize()
         cs = np.ascontiguousarray(counts, dtype=np.uint32)
         ts = np.ascontiguousarray(batch_timestamps, dtype=np.uint64)
         out = np.zeros(world, dtype=np.uint64)
+        bc = np.zeros((world, max(len(cs), 1)), dtype=np.uint32)
+        sp = np.zeros(world, dtype=np.uint32)
         rc = self._L.tbgpu_route_scatter(self._h, world, len(cs), _ptr(cs), _ptr(ts), int(first_global_batch),
                                          ctypes.c_void_p(events.data_ptr()), ctypes.c_void_p(send_events.data_ptr()),
-                                         ctypes.c_void_p(send_sides.data_ptr()), _ptr(out))
+                                         ctypes.c_void_p(send_sides.data_ptr()), _ptr(out), _ptr(bc), _ptr(sp))
         if rc != 0:
             raise ValueError(f"tbgpu_route_scatter failed ({rc})")
-        return out
+        return (out, bc[:, :len(cs)], sp) if detail else out
 
     def route_stats(self, events, n: int):
         """tbgpu_route_stats over n events of a uint8 device tensor: (min id, max id,

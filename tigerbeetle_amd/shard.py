@@ -70,6 +70,7 @@ POST_VOID = int(TransferFlags.post_pending_transfer | TransferFlags.void_pending
 ANY = -1           # route: state-independent failure, any shard computes it
 PV = -2            # directory hint of a post/void: its shard is that of its pending
 MAX_ROUNDS = 8     # dry rounds before the serial fallback (one cross-shard chain per round)
+NB_GATHER = 2048   # batch counts per rank carried by the device step's first all-gather
 LIMITS = 2 | 4     # AccountFlags debits_must_not_exceed_credits | credits_must_not_exceed_debits
 BALANCING = 8 | 16  # TransferFlags balancing_debit | balancing_credit
 
@@ -279,12 +280,16 @@ class ShardedStateMachine:
             st = [n, int(id_lo.min()), int(id_lo.max()), int(mono), int(plain), units]
         else:
             st = [0, 0, 0, 1, 1, 0]
+        # with the batch counts of the step (the global order), in the same all-gather
+        nb_here = len(counts)
+        st += [nb_here] + (list(map(int, counts)) if nb_here <= NB_GATHER else []) + \
+            [0] * (NB_GATHER - (nb_here if nb_here <= NB_GATHER else 0))
         stats = torch.tensor(st, dtype=torch.int64, device=dev)
         allst = [torch.empty_like(stats) for _ in range(W)]
         self.comm.dist.all_gather(allst, stats, group=self.comm.group)
-        allst = [x.cpu().tolist() for x in allst]
+        allst = torch.stack(allst).cpu().tolist()
         ok, prev = True, self.max_id
-        for (cnt, lo, hi, mono, plain, _) in allst:
+        for (cnt, lo, hi, mono, plain, _) in (x[:6] for x in allst):
             if cnt == 0:
                 continue
             ok &= bool(mono and plain and lo > prev)
@@ -299,7 +304,10 @@ class ShardedStateMachine:
         self.amount_bound += sum(float(x[5]) for x in allst) * 2.0**32
 
         # global order and timestamps (host: one entry per batch)
-        counts_all = self.comm.all_gather_object(list(map(int, counts)))
+        if all(x[6] <= NB_GATHER for x in allst):
+            counts_all = [x[7:7 + x[6]] for x in allst]
+        else:
+            counts_all = self.comm.all_gather_object(list(map(int, counts)))
         glob = [(r, j, c) for r, cl in enumerate(counts_all) for j, c in enumerate(cl)]
         T = []
         for r, j, c in glob:
@@ -308,22 +316,39 @@ class ShardedStateMachine:
         g0 = sum(len(cl) for cl in counts_all[:me])
         clock("order_ms")
         native = n and ev.is_cuda and hasattr(self.backend, "route_scatter")
+        nb_me = len(counts)
         if native:
-            # the engine's scatter kernels (csrc/route.hip): same layout as below
+            # the engine's scatter kernels (csrc/route.hip): same layout as partition_torch
             ev_s = torch.empty((n, 128), dtype=torch.uint8, device=dev)
             side_s = torch.empty((n, 4), dtype=torch.int64, device=dev)
-            sc = self.backend.route_scatter(W, list(map(int, counts)), T[g0:g0 + len(counts)], g0, ev, ev_s, side_s)
-            send = torch.from_numpy(sc.astype(np.int64)).to(dev)
+            sc, bc, spc = self.backend.route_scatter(W, list(map(int, counts)), T[g0:g0 + nb_me], g0, ev, ev_s,
+                                                     side_s, detail=True)
         elif n:
-            ev_s, side_s, send = partition_torch(torch, ev, counts, T[g0:g0 + len(counts)], g0, W, dev)
+            ev_s, side_s, send_t, bc_t, spc_t = partition_torch(torch, ev, counts, T[g0:g0 + nb_me], g0, W, dev,
+                                                                detail=True)
+            sc, bc, spc = send_t.cpu().numpy(), bc_t.cpu().numpy(), spc_t.cpu().numpy()
         else:
-            send = torch.zeros(W, dtype=torch.int64, device=dev)
+            sc, bc, spc = np.zeros(W, np.int64), np.zeros((W, 0), np.int64), np.zeros(W, np.int64)
             ev_s = torch.zeros((0, 128), dtype=torch.uint8, device=dev)
             side_s = torch.zeros((0, 4), dtype=torch.int64, device=dev)
         clock("partition_ms")
-        recv = torch.empty_like(send)
-        self.comm.dist.all_to_all_single(recv, send, group=self.comm.group)
-        sl, rl = send.cpu().tolist(), recv.cpu().tolist()
+        # per owner: [events, spanning events, all spanning events sent, events per batch...]
+        meta = np.concatenate([np.asarray(sc, np.int64)[:, None], np.asarray(spc, np.int64)[:, None],
+                               np.full((W, 1), int(np.sum(spc)), np.int64), np.asarray(bc, np.int64)], axis=1)
+        nbs = [len(cl) for cl in counts_all]
+        rmeta = torch.empty(sum(3 + k for k in nbs), dtype=torch.int64, device=dev)
+        self.comm.dist.all_to_all_single(rmeta, torch.from_numpy(meta.reshape(-1)).to(dev), [3 + k for k in nbs],
+                                         [3 + nb_me] * W, group=self.comm.group)
+        rmeta = rmeta.cpu().numpy()
+        sl, rl, sub_counts, n_span, span_sent = [int(x) for x in sc], [], [], 0, 0
+        off = 0
+        for k in nbs:
+            row = rmeta[off:off + 3 + k]
+            rl.append(int(row[0]))
+            n_span += int(row[1])
+            span_sent += int(row[2])
+            sub_counts += [int(c) for c in row[3:] if c]
+            off += 3 + k
         m = int(sum(rl))
         R = torch.empty((m, 128), dtype=torch.uint8, device=dev)
         S = torch.empty((m, 4), dtype=torch.int64, device=dev)
@@ -332,11 +357,10 @@ class ShardedStateMachine:
         del ev_s, side_s
         clock("exchange_ms")
 
-        # owner side: sub-batches in global order, chain control
-        if m:
+        # owner side: sub-batches in global order (from the senders' counts), chain control
+        si = torch.zeros(0, dtype=torch.int64, device=dev)
+        if n_span:
             gk = S[:, 1] >> 32
-            _, sub_counts = torch.unique_consecutive(gk, return_counts=True)
-            sub_counts = sub_counts.cpu().tolist()
             key = S[:, 2]
             spanm = (S[:, 3] & 1) != 0
             lastm = (S[:, 3] & 2) != 0
@@ -344,10 +368,7 @@ class ShardedStateMachine:
             nxt[:-1] = key[1:] != key[:-1]                 # last local member of its chain
             base = (spanm & nxt & ~lastm).to(torch.uint8) * CTL_CHAIN_END
             si = torch.nonzero(spanm).flatten()
-        else:
-            sub_counts = []
-            si = torch.zeros(0, dtype=torch.int64, device=dev)
-        n_span = int(si.numel())
+            assert int(si.numel()) == n_span, "spanning counts disagree with the received records"
         plain_local = True
         if n_span:
             Rs = R.index_select(0, si)
@@ -361,9 +382,11 @@ class ShardedStateMachine:
                     if any(((int(h) << 64) | int(lo_)) in self.limit_ids for lo_, h in zip(lo.tolist(), hi.tolist())):
                         plain_local = False
                         break
-        spans = self.comm.all_gather_object((n_span, plain_local))
-        any_span = any(x[0] for x in spans)
-        all_plain = all(x[1] for x in spans) and self.amount_bound < 2.0**125
+        # every rank knows whether anything spans (the senders' totals came with the counts)
+        any_span = span_sent > 0
+        all_plain = True
+        if any_span:
+            all_plain = all(self.comm.all_gather_object(plain_local)) and self.amount_bound < 2.0**125
         results = torch.empty(max(m, 1) * 8, dtype=torch.uint8, device=dev)
         ts_r = S[:, 0].contiguous() if m else torch.zeros(1, dtype=torch.int64, device=dev)
         Rf = R.reshape(-1) if m else torch.zeros(128, dtype=torch.uint8, device=dev)
@@ -463,28 +486,36 @@ class ShardedStateMachine:
         else:
             out, at, cts = commit(None, False)
         clock("commit_ms")
-        # replies to their sources
-        if len(at):
-            pg = S[torch.from_numpy(at).to(dev), 1].cpu().numpy()
-        else:
-            pg = np.zeros(0, np.int64)
-        rep = [[] for _ in range(W)]
-        for pgv, r in zip(pg.tolist(), out["result"].tolist()):
-            gg = pgv >> 32
-            rep[glob[gg][0]].append((gg, pgv & 0xFFFFFFFF, r))
+        # the node's commit timestamp and whether any owner has replies, in one all-gather
+        fin = torch.tensor([len(at), cts if m else self.backend.commit_timestamp()], dtype=torch.int64, device=dev)
+        allfin = [torch.empty_like(fin) for _ in range(W)]
+        self.comm.dist.all_gather(allfin, fin, group=self.comm.group)
+        allfin = torch.stack(allfin).cpu().tolist()
+        ts_all = max(x[1] for x in allfin)
         mine = {j: [] for j in range(len(counts))}
-        for lst in self._exchange_objects(rep):
-            for (gg, i, r) in lst:
-                mine[gg - g0].append((i, r))
-        ts_all = self.comm.allreduce_max(cts if m else self.backend.commit_timestamp())
+        if any(x[0] for x in allfin):
+            # replies to their sources
+            if len(at):
+                pg = S[torch.from_numpy(at).to(dev), 1].cpu().numpy()
+            else:
+                pg = np.zeros(0, np.int64)
+            rep = [[] for _ in range(W)]
+            for pgv, r in zip(pg.tolist(), out["result"].tolist()):
+                gg = pgv >> 32
+                rep[glob[gg][0]].append((gg, pgv & 0xFFFFFFFF, r))
+            for lst in self._exchange_objects(rep):
+                for (gg, i, r) in lst:
+                    mine[gg - g0].append((i, r))
         self.backend.advance_commit_timestamp(ts_all)
         self.commit_timestamp = ts_all
         replies = []
         for j in range(len(counts)):
+            if not mine[j]:
+                replies.append(np.zeros(0, dtype=RESULT_DTYPE))
+                continue
             a = np.array(sorted(mine[j]), dtype=np.uint32).reshape(-1, 2)
             res = np.zeros(len(a), dtype=RESULT_DTYPE)
-            if len(a):
-                res["index"], res["result"] = a[:, 0], a[:, 1]
+            res["index"], res["result"] = a[:, 0], a[:, 1]
             replies.append(res)
         self.stats["steps"] += 1
         clock("replies_ms")
@@ -898,7 +929,7 @@ class ShardedStateMachine:
         return acc[own] if len(acc) else acc, xs[keep] if len(xs) else xs
 
 
-def partition_torch(torch, ev, counts, batch_ts, g0: int, W: int, dev):
+def partition_torch(torch, ev, counts, batch_ts, g0: int, W: int, dev, detail: bool = False):
     """The send side of a routed step with torch tensor ops (the CPU-collective tests'
     path; on GPUs the engine's tbgpu_route_scatter computes the same thing): events
     owner-major (owner = ledger % W), in event order within an owner, with their
@@ -930,4 +961,9 @@ def partition_torch(torch, ev, counts, batch_ts, g0: int, W: int, dev):
                         span.to(torch.int64) | (last.to(torch.int64) << 1)], 1)
     perm = torch.argsort(owner, stable=True)
     send = torch.bincount(owner, minlength=W)
-    return ev.view(n, 128).index_select(0, perm), side.index_select(0, perm), send
+    out = (ev.view(n, 128).index_select(0, perm), side.index_select(0, perm), send)
+    if not detail:
+        return out
+    per_batch = torch.bincount(owner * nb + bidx, minlength=W * nb).view(W, nb)
+    spanning = torch.bincount(owner[span], minlength=W)
+    return out + (per_batch, spanning)

@@ -97,7 +97,7 @@ __device__ __forceinline__ SE load_elem(const SideScanArgs& A, u64 q, u32 invali
 
 // Exclusive segmented scan of one value per thread across the workgroup.
 template <bool HAS_H>
-__device__ SE block_excl(SE v, SE* sh, SE* total) {
+__device__ __forceinline__ SE block_excl(SE v, SE* sh, SE& total) {
     const u32 tid = threadIdx.x;
     sh[tid] = v;
     __syncthreads();
@@ -110,7 +110,7 @@ __device__ SE block_excl(SE v, SE* sh, SE* total) {
         __syncthreads();
     }
     SE excl = tid ? sh[tid - 1] : identity<HAS_H>();
-    *total = sh[BS_THREADS - 1];
+    total = sh[BS_THREADS - 1];
     __syncthreads();
     return excl;
 }
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(BS_THREADS) void bs_reduce(SideScanArgs A, u64 m, u
     for (int k = 0; k < BS_IPT; k++)
         if (base + k < m) acc = combine<HAS_H>(acc, load_elem<HAS_H>(A, base + k, invalid));
     SE total;
-    block_excl<HAS_H>(acc, sh, &total);
+    block_excl<HAS_H>(acc, sh, total);
     if (threadIdx.x == 0) tagg[blockIdx.x] = total;
 }
 
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(BS_THREADS) void bs_tiles(PassGate gate, SE* __rest
     SE acc = identity<HAS_H>();
     for (u64 t = lo; t < hi; t++) acc = combine<HAS_H>(acc, tagg[t]);
     SE total;
-    SE run = block_excl<HAS_H>(acc, sh, &total);
+    SE run = block_excl<HAS_H>(acc, sh, total);
     for (u64 t = lo; t < hi; t++) {
         SE v = tagg[t];
         tagg[t] = run;
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(BS_THREADS) void bs_down(SideScanArgs A, u64 m, u32
     for (int k = 0; k < BS_IPT; k++)
         if (base + k < m) acc_t = combine<HAS_H>(acc_t, load_elem<HAS_H>(A, base + k, invalid));
     SE total;
-    SE run = combine<HAS_H>(tagg[blockIdx.x], block_excl<HAS_H>(acc_t, sh, &total));
+    SE run = combine<HAS_H>(tagg[blockIdx.x], block_excl<HAS_H>(acc_t, sh, total));
     for (int k = 0; k < BS_IPT; k++) {
         const u64 q = base + k;
         if (q >= m) break;
@@ -256,7 +256,7 @@ __device__ __forceinline__ SF combine_f(const SF& a, const SF& b) {
     c.fl = a.fl | b.fl;
     return c;
 }
-__device__ SF block_excl_f(SF v, SF* wtot) {
+__device__ __forceinline__ SF block_excl_f(SF v, SF* wtot) {
     const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int off = 1; off < 64; off <<= 1) {
         SF o;
@@ -279,13 +279,16 @@ __device__ SF block_excl_f(SF v, SF* wtot) {
 
 // A sorted side's contributions: to F (final-ok), or to H (evaluated-ok in a chain
 // that does not persist: visible only to later members of its chain).
-__device__ __forceinline__ void side_contrib(const SideScanArgs& A, u64 q, Bal4* F, Bal4* H) {
-    zero(*F);
-    zero(*H);
+// (by value and selects, not a pointer to one of two locals: that put both in scratch)
+__device__ __forceinline__ void side_contrib(const SideScanArgs& A, u64 q, Bal4& F, Bal4& H) {
+    zero(F);
+    zero(H);
     if (!(A.sq_ok[q] & 1)) return;
     const u128 dpe = A.sq_dpend[q], dpo = A.sq_dpost[q];
-    Bal4* t = side_final(A, q) ? F : H;
-    if (A.sq_ev[q] >> 31) { t->cp = dpe; t->cpo = dpo; } else { t->dp = dpe; t->dpo = dpo; }
+    const bool fin = side_final(A, q), credit = A.sq_ev[q] >> 31;
+    const u128 pe = credit ? 0 : dpe, po = credit ? 0 : dpo, ce = credit ? dpe : 0, co = credit ? dpo : 0;
+    if (fin) { F.dp = pe; F.dpo = po; F.cp = ce; F.cpo = co; }
+    else { H.dp = pe; H.dpo = po; H.cp = ce; H.cpo = co; }
 }
 
 // F is scanned (segmented by account); H, non-zero only behind earlier members of
@@ -343,7 +346,7 @@ __global__ __launch_bounds__(BF_THREADS) void bs_fused(SideScanArgs A, u64 m, u3
         zero(h[k]);
         e[k].fl = 1;
         if (key[k] < invalid) {
-            side_contrib(A, q, &f[k], &h[k]);
+            side_contrib(A, q, f[k], h[k]);
             const u32 prev = k > 0 ? key[k - 1] : (q == a0 ? invalid : A.skey[q - 1]);
             e[k].fl = prev != key[k] ? 1u : 0u;
         }

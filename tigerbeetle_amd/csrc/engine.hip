@@ -128,8 +128,8 @@ struct tbgpu_ctx {
     u32 slow_chunks = 0;  // consecutive chunks that needed the fixed point
     u32 last_passes = 8;  // passes the last fixed point took (sizes the next pass group)
     bool long_segments = false;  // this call has an account segment too long for the fused scan
-    // fixed-point pass counters, a ring of PC_RING words each: changes per pass (the
-    // gate of the next pass) and the first changed event of each pass
+    // fixed-point pass counters, a ring of PC_RING words: changes per pass (the gate
+    // of the next pass); a second ring of PC_RING words is spare
     u32* pc = nullptr;
     u64* rg_part = nullptr;    // tr_range's per-block records
     u32* h_pc = nullptr;       // pinned mirror of the change ring
@@ -569,7 +569,6 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n) {
     const int bits_g = log2u(g + 1);
 
     u32* chg = c->pc;
-    u32* front = c->pc + PC_RING;
     prof_mark(c, PH_CLASSIFY);
     tr_launch_prep(C, c->st[0].cfail, c->pc, PC_RING, s);
     tr_launch_classify(c->T, C, s);
@@ -623,8 +622,7 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n) {
             SA.gate = G;
             if (c->long_segments) side_scan(SA, m, inv_acc, chains, c->side_tiles, c->T.acc, c->bb, s);
             else side_scan_fused(SA, m, inv_acc, c->tstart, c->counters + CNT_LONG, c->T.acc, c->bb, s);
-            tr_launch_evaluate(c->T, C, S, D, c->bb, G, chg + (q + 1) % PC_RING, front + (q + 1) % PC_RING,
-                               chg + (q + 2) % PC_RING, front + (q + 2) % PC_RING, s);
+            tr_launch_evaluate(c->T, C, S, D, c->bb, G, chg + (q + 1) % PC_RING, chg + (q + 2) % PC_RING, s);
         }
         const u32 p0 = p;
         p += group;

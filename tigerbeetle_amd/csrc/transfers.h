@@ -65,7 +65,7 @@ void tr_launch_side_build(const TrArgs& C, const EvalState& S, u32 kmax, const u
 void tr_launch_side_pos(const TrArgs& C, const u32* sval_s, u64 m, hipStream_t stream);
 void tr_launch_side_rec(const TrArgs& C, const EvalState& S, hipStream_t stream);
 void tr_launch_evaluate(const Tables& T, const TrArgs& C, const EvalState& S, const EvalState& D, const Bal4* bb,
-                        const PassGate& g, u32* chg, u32* front, u32* chg_next, u32* front_next, hipStream_t stream);
+                        const PassGate& g, u32* chg, u32* chg_next, hipStream_t stream);
 void tr_launch_mask(const Tables& T, const TrArgs& C, const EvalState& S, u8* fres, u8* mask, hipStream_t stream);
 void tr_launch_apply(const Tables& T, const TrArgs& C, const EvalState& S, const u8* fres, const uint4* rk,
                      const Bal4* bb, tbgpu_create_transfers_result_t* results, u32* counts, u64* part,

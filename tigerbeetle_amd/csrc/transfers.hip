@@ -41,6 +41,30 @@ __device__ __forceinline__ u32 wave_or(u32 v) {
     for (int off = 32; off > 0; off >>= 1) v |= __shfl_xor(v, off);
     return v;
 }
+// Workgroup reductions for flag words and counters: one atomic per workgroup, not
+// per wave (same-address atomics serialize at the memory side, ≈5-10 ns each: one per
+// wave of a 131k-event launch is 2k of them, longer than the launch's own work).
+// Every thread of the workgroup must call; the result is valid in thread 0.
+__device__ __forceinline__ u32 block_or(u32 v) {
+    __shared__ u32 s_red[16];
+    for (int off = 32; off > 0; off >>= 1) v |= __shfl_xor(v, off);
+    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    u32 r = 0;
+    if (threadIdx.x == 0)
+        for (u32 k = 0; k < (blockDim.x + 63) / 64; k++) r |= s_red[k];
+    return r;
+}
+__device__ __forceinline__ u32 block_sum(u32 v) {
+    __shared__ u32 s_sum[16];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = v;
+    __syncthreads();
+    u32 r = 0;
+    if (threadIdx.x == 0)
+        for (u32 k = 0; k < (blockDim.x + 63) / 64; k++) r += s_sum[k];
+    return r;
+}
 __device__ __forceinline__ u32 wave_min(u32 v) {
     for (int off = 32; off > 0; off >>= 1) v = min(v, (u32)__shfl_xor(v, off));
     return v;
@@ -216,8 +240,8 @@ __device__ __forceinline__ u32 classify_one(const Tables& T, const TrArgs& C, u3
 
 __global__ void tr_classify(Tables T, TrArgs C) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    const u32 fl = wave_or(i < C.n ? classify_one(T, C, i) : 0u);
-    if ((threadIdx.x & 63) == 0 && fl) atomicOr(&C.counters[CNT_FLAGS], fl);
+    const u32 fl = block_or(i < C.n ? classify_one(T, C, i) : 0u);
+    if (threadIdx.x == 0 && fl) atomicOr(&C.counters[CNT_FLAGS], fl);
 }
 
 // Single-member id groups record their member; multi-member groups need a sort.
@@ -230,8 +254,8 @@ __global__ void tr_group1(TrArgs C) {
         const u32 p = C.pslot[i];
         if (p != NONE32 && C.gcnt_pd[p] >= 2) fl |= FL_MULTI_PEND;
     }
-    fl = wave_or(fl);
-    if ((threadIdx.x & 63) == 0 && fl) atomicOr(&C.counters[CNT_FLAGS], fl);
+    fl = block_or(fl);
+    if (threadIdx.x == 0 && fl) atomicOr(&C.counters[CNT_FLAGS], fl);
 }
 
 // Sort keys for grouping: events by id slot (kind 0) or post/voids by pending slot (kind 1).
@@ -547,25 +571,16 @@ __device__ __forceinline__ bool evaluate_one(const Tables& T, const TrArgs& C, c
     return changed;
 }
 
-// `chg` and `front` are ring words: this pass's count and first changed event; the
-// pass clears the words the pass after it writes (the host clears nothing per pass).
+// `chg` is a ring word: this pass's count of changed events; the pass clears the
+// word the pass after it writes (the host clears nothing per pass).
 __global__ void tr_evaluate(Tables T, TrArgs C, EvalState S, EvalState D, const Bal4* __restrict__ bb, PassGate g,
-                            u32* chg, u32* front, u32* chg_next, u32* front_next) {
+                            u32* chg, u32* chg_next) {
     if (!gate_open(g)) return;
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) {
-        *chg_next = 0;
-        *front_next = NONE32;
-    }
+    if (i == 0) *chg_next = 0;
     const bool changed = i < C.n && evaluate_one(T, C, S, D, bb, g, i);
-    const u64 m = __ballot(changed);
-    if (m) {
-        const u32 f = wave_min(changed ? i : NONE32);
-        if ((threadIdx.x & 63) == 0) {
-            atomicAdd(chg, (u32)__popcll(m));
-            atomicMin(front, f);
-        }
-    }
+    const u32 c = block_sum(changed ? 1u : 0u);
+    if (threadIdx.x == 0 && c) atomicAdd(chg, c);
 }
 
 // The pending an unresolved post/void most likely resolves to: a committed transfer
@@ -1010,8 +1025,8 @@ void tr_launch_side_rec(const TrArgs& C, const EvalState& S, hipStream_t stream)
     tr_side_rec<<<GRID(C.n)>>>(C, S);
 }
 void tr_launch_evaluate(const Tables& T, const TrArgs& C, const EvalState& S, const EvalState& D, const Bal4* bb,
-                        const PassGate& g, u32* chg, u32* front, u32* chg_next, u32* front_next, hipStream_t stream) {
-    tr_evaluate<<<GRID(C.n)>>>(T, C, S, D, bb, g, chg, front, chg_next, front_next);
+                        const PassGate& g, u32* chg, u32* chg_next, hipStream_t stream) {
+    tr_evaluate<<<GRID(C.n)>>>(T, C, S, D, bb, g, chg, chg_next);
 }
 void tr_launch_mask(const Tables& T, const TrArgs& C, const EvalState& S, u8* fres, u8* mask, hipStream_t stream) {
     tr_mask<<<GRID(C.n)>>>(T, C, S, fres, mask);

@@ -124,10 +124,26 @@ __device__ __forceinline__ u32 classify_one(const Tables& T, const TrArgs& C, u3
     auto linked = [&](u32 j) {
         return (C.ev[j].flags & TF_LINKED) && !(C.ctl && (C.ctl[j] & TBGPU_CTL_CHAIN_END));
     };
-    u32 s = i;
-    while (s > bs && linked(s - 1)) s--;
-    u32 e = i;
-    while (e + 1 < be && linked(e)) e++;
+    // within the wave from one ballot of the lanes' own flags; only a chain that
+    // crosses the wave's edge walks on (lanes below an active lane are active)
+    const u32 lane = threadIdx.x & 63, w0 = i - lane;
+    const u64 lm = __ballot((t.flags & TF_LINKED) && !(C.ctl && (C.ctl[i] & TBGPU_CTL_CHAIN_END)));
+    const u64 below = ~lm & ((1ull << lane) - 1), above = ~lm & (~0ull << lane);
+    u32 s, e;
+    if (below) {
+        s = w0 + 64 - __clzll((long long)below);  // one past the last unlinked lane below
+    } else {
+        s = w0;
+        while (s > bs && linked(s - 1)) s--;
+    }
+    if (s < bs) s = bs;
+    if (above) {
+        e = w0 + __ffsll((unsigned long long)above) - 1;
+    } else {
+        e = w0 + 63;
+        while (e + 1 < be && linked(e)) e++;
+    }
+    if (e > be - 1) e = be - 1;
     C.cs[i] = s;
     C.ce[i] = e;
     u32 fl = (s != e) ? FL_CHAINS : 0u;
@@ -555,7 +571,7 @@ __device__ __forceinline__ bool evaluate_one(const Tables& T, const TrArgs& C, c
     if (res != TBGPU_CREATE_TRANSFER_OK && csi != C.ce[i]) atomicMin(&D.cfail[csi], i);
     const bool changed = res != s_res || amt != s_amt || pamt != s_pamt || pref != s_pref;
     if (C.debug && changed) {
-        const u16 f = C.ev[i].flags;
+        const u16 f = k.flags;
         const u32 kind = (f & (TF_POST | TF_VOID)) ? 2 : (f & (TF_BDR | TF_BCR)) ? 1 : 0;
         atomicAdd(&C.counters[CNT_DBG + kind], 1u);
         if (res != s_res) atomicAdd(&C.counters[CNT_DBG + 3], 1u);
@@ -565,7 +581,7 @@ __device__ __forceinline__ bool evaluate_one(const Tables& T, const TrArgs& C, c
     }
     // the side records the next pass's balance scan reads (static failures keep the
     // records tr_side_rec gave them)
-    if (sr == SRES_DYN && !write_sides(C, i, C.ev[i].flags & (TF_POST | TF_VOID), res == TBGPU_CREATE_TRANSFER_OK,
+    if (sr == SRES_DYN && !write_sides(C, i, k.flags & (TF_POST | TF_VOID), res == TBGPU_CREATE_TRANSFER_OK,
                                        pref, dpe, dpo))
         atomicMax(&C.counters[CNT_RESORT], g.p + 1);  // its pending is not among its sides: rebuild them
     return changed;
@@ -684,7 +700,7 @@ __device__ __forceinline__ u32 post_candidates(const TrArgs& C, const EvalState&
 }
 
 __device__ __forceinline__ bool is_post_void(const TrArgs& C, u32 i) {
-    return C.sres[i] == SRES_DYN && (C.ev[i].flags & (TF_POST | TF_VOID));
+    return C.sres[i] == SRES_DYN && (C.core[i].flags & (TF_POST | TF_VOID));
 }
 
 // Side pairs per event, as a popcount mask for scan3: 1 -> 0b001, 2 -> 0b011, 3 -> 0b111.
@@ -719,7 +735,7 @@ __global__ void tr_side_build(TrArgs C, EvalState S, u32 kmax, const uint4* pair
     u32 d = NONE32, c = NONE32;
     cand[0] = NONE32;
     if (C.sres[i] == SRES_DYN) {
-        if (!(C.ev[i].flags & (TF_POST | TF_VOID))) {
+        if (!(C.core[i].flags & (TF_POST | TF_VOID))) {
             d = C.dslot[i];
             c = C.cslot[i];
         } else {

@@ -244,6 +244,8 @@ enum {
     CNT_BAD = 4,        // fast path: events with a result other than ok
     CNT_RESORT = 5,     // general path: pass + 1 whose evaluation resolved a post/void outside its sides
     CNT_LONG = 6,       // general path: pass + 1 whose fused scan met a segment longer than its window
+    CNT_GCUR = 8,       // general path: id-group ranges reserved so far
+    CNT_PCUR = 9,       // general path: pending-group ranges reserved so far
     CNT_TS_SAVE = 12,   // fast path: commit_timestamp before the call (u64 in words 12-13)
     CNT_DBG = 16,       // diagnostics (words 16-21): changed events by kind, summed over a call's passes
     CNT_COUNT = 24,

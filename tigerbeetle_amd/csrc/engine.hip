@@ -75,7 +75,7 @@ struct tbgpu_ctx {
     u8* sres = nullptr;
     u32 *dslot, *cslot, *pre_e, *pre_p, *pp_dslot, *pp_cslot, *gslot, *pslot, *prev_id, *pend_last, *pend_first,
         *prev_pend;
-    u32 *gclaim, *gcnt_id, *gcnt_pd, *gmem, *gbeg, *gend;
+    u32 *gclaim, *gcnt_id, *gcnt_pd, *gmem, *gbeg, *gend, *gfill, *pfill, *pbeg;
     EvalState st[2];
     u64 scap = 0, side_m = 0;  // side capacity, sides of the last fixed point
     u32 *skey, *sval, *skey_s, *sval_s, *spos;
@@ -171,7 +171,8 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     u32** u32s[] = {&c->dslot, &c->cslot, &c->pre_e, &c->pre_p, &c->pp_dslot, &c->pp_cslot,
                     &c->gslot, &c->pslot, &c->prev_id, &c->pend_last, &c->pend_first, &c->prev_pend};
     for (u32** p : u32s) *p = dalloc<u32>(n, &B);
-    u32** g32s[] = {&c->gclaim, &c->gcnt_id, &c->gcnt_pd, &c->gmem, &c->gbeg, &c->gend};
+    u32** g32s[] = {&c->gclaim, &c->gcnt_id, &c->gcnt_pd, &c->gmem, &c->gbeg, &c->gend, &c->gfill, &c->pfill,
+                    &c->pbeg};
     for (u32** p : g32s) *p = dalloc<u32>(c->gcap, &B);
     for (EvalState& s : c->st) {
         s.res = dalloc<u8>(n, &B);
@@ -356,7 +357,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     void* ptrs[] = {c->T.dense, c->T.acc, c->T.aidx, c->T.xrows, c->T.xful, c->T.xidx, c->T.hrows, c->T.commit_ts, c->T.idr, c->T.big, c->ev_buf,
                     c->b_start, c->b_ts, c->ts, c->cs, c->ce, c->sres, c->dslot, c->cslot, c->pre_e, c->pre_p,
                     c->pp_dslot, c->pp_cslot, c->gslot, c->pslot, c->prev_id, c->pend_last, c->pend_first, c->prev_pend,
-                    c->gclaim, c->gcnt_id, c->gcnt_pd, c->gmem, c->gbeg, c->gend, c->skey, c->sval, c->skey_s,
+                    c->gclaim, c->gcnt_id, c->gcnt_pd, c->gmem, c->gbeg, c->gend, c->gfill, c->pfill, c->pbeg, c->skey, c->sval, c->skey_s,
                     c->soff, c->core, c->tstart, c->epos, c->sev, c->scand, c->sq_ev, c->sq_cs, c->sq_ok, c->sq_dpend, c->sq_dpost, c->gkey_s,
                     c->gsorted,
                     c->sval_s, c->spos, c->bb, c->ss.keys_tmp, c->ss.vals_tmp, c->ss.hist, c->side_tiles,
@@ -476,6 +477,9 @@ static TrArgs make_tr_args(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb) {
     C.prev_id = c->prev_id; C.pend_last = c->pend_last; C.pend_first = c->pend_first; C.prev_pend = c->prev_pend;
     C.gclaim = c->gclaim; C.gcnt_id = c->gcnt_id; C.gcnt_pd = c->gcnt_pd; C.gmem = c->gmem;
     C.gbeg = c->gbeg; C.gend = c->gend; C.gmembers = c->gsorted;
+    C.gfill = c->gfill; C.pfill = c->pfill; C.pbeg = c->pbeg;
+    C.glist = c->gkey_s;  // scratch (free before the sides are built)
+    C.plist = c->skey;
     C.sd.soff = c->soff; C.sd.sev = c->sev; C.sd.scand = c->scand; C.sd.spos = c->spos; C.sd.skey_s = c->skey_s;
     C.sd.sq_ev = c->sq_ev; C.sd.sq_cs = c->sq_cs; C.sd.sq_ok = c->sq_ok; C.sd.sq_dpend = c->sq_dpend;
     C.sd.sq_dpost = c->sq_dpost;
@@ -573,9 +577,9 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n) {
     tr_launch_prep(C, c->st[0].cfail, c->pc, PC_RING, s);
     tr_launch_classify(c->T, C, s);
     // grouping by id / pending id: each step runs only when classify found the need
-    tr_launch_group_sort(C, 0, inv_g, bits_g, c->skey, c->sval, c->gkey_s, c->gsorted, c->ss, s);
+    tr_launch_group(C, 0, s);
     tr_launch_group2(C, s);
-    tr_launch_group_sort(C, 1, inv_g, bits_g, c->skey, c->sval, c->skey_s, c->sval_s, c->ss, s);
+    tr_launch_group(C, 1, s);
     tr_launch_init(c->T, C, c->st[0], s);
 
     // The sides of the events, sorted by account (one host round trip: their count).

@@ -45,9 +45,14 @@ struct TrArgs {
     u32* gcnt_id;
     u32* gcnt_pd;
     u32* gmem;
-    u32* gbeg;
+    u32* gbeg;            // id groups of 2+ members: [gbeg, gend) of gmembers, ascending
     u32* gend;
-    const u32* gmembers;  // id-sorted members (valid when FL_MULTI_ID)
+    u32* gmembers;        // id-group members by index (valid when FL_MULTI_ID)
+    u32* gfill;           // per slot: members placed so far (id groups), then pending groups
+    u32* pfill;
+    u32* pbeg;            // pending groups of 2+ members: their range in plist
+    u32* glist;           // scratch: id-group members in arrival order
+    u32* plist;           // scratch: pending-group members in arrival order
     u64 gmask;
     u32* counters;
     u32 debug;            // diagnostics: count changed events by kind (TBGPU_TRACE_PASSES)
@@ -55,8 +60,9 @@ struct TrArgs {
 };
 
 void tr_launch_classify(const Tables& T, const TrArgs& C, hipStream_t stream);
-void tr_launch_group_sort(const TrArgs& C, u32 kind, u32 invalid, int bits, u32* k_in, u32* v_in, u32* k_out,
-                          u32* v_out, SortScratch& ss, hipStream_t stream);
+// Events sharing an id (kind 0: prev_id, ranges) or a pending id (kind 1: prev_pend),
+// without a sort: ranges reserved per group, members placed, then ranked in it.
+void tr_launch_group(const TrArgs& C, u32 kind, hipStream_t stream);
 void tr_launch_group2(const TrArgs& C, hipStream_t stream);
 void tr_launch_init(const Tables& T, const TrArgs& C, const EvalState& D, hipStream_t stream);
 void tr_launch_side_count(const TrArgs& C, const EvalState& S, u32 kmax, u8* mask, hipStream_t stream);

@@ -281,34 +281,70 @@ __device__ __forceinline__ bool need(const TrArgs& C, u32 kind) {
     return C.counters[CNT_FLAGS] & (kind == 0 ? FL_MULTI_ID : FL_MULTI_PEND);
 }
 
-__global__ void tr_group_keys(TrArgs C, u32 kind, u32 invalid, u32* keys, u32* vals) {
+// Groups of 2+ members, without sorting the call: (1) one member of each group
+// reserves the group's range (a per-wave prefix of the counts, one cursor atomic per
+// wave), (2) every member takes a place in its range, (3) every member counts the
+// members before it (its rank: the range ends up in event order) and finds its
+// predecessor.  Groups are small; a group of k members costs k^2 / 2 reads in (3).
+__device__ __forceinline__ void grp_fields(const TrArgs& C, u32 kind, u32 i, u32* slot, u32* cnt) {
+    *slot = kind == 0 ? C.gslot[i] : C.pslot[i];
+    *cnt = *slot == NONE32 ? 0u : (kind == 0 ? C.gcnt_id[*slot] : C.gcnt_pd[*slot]);
+}
+
+__global__ void tr_grp_reserve(TrArgs C, u32 kind) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (!need(C, kind)) return;
+    u32 slot = NONE32, cnt = 0;
+    if (i < C.n) grp_fields(C, kind, i, &slot, &cnt);
+    u32* beg = kind == 0 ? C.gbeg : C.pbeg;
+    const bool win = cnt >= 2 && atomicCAS(&beg[slot], NONE32, NONE32 - 1) == NONE32;
+    u32 mine = win ? cnt : 0u, pre = mine;
+    const u32 lane = threadIdx.x & 63;
+    for (int off = 1; off < 64; off <<= 1) {  // inclusive prefix over the wave
+        const u32 o = __shfl_up(pre, off);
+        if (lane >= (u32)off) pre += o;
+    }
+    const u32 tot = __shfl(pre, 63);
+    u32 base = 0;
+    if (lane == 63 && tot) base = atomicAdd(&C.counters[kind == 0 ? CNT_GCUR : CNT_PCUR], tot);
+    base = __shfl(base, 63);
+    if (win) beg[slot] = base + pre - mine;
+}
+
+__global__ void tr_grp_place(TrArgs C, u32 kind) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= C.n || !need(C, kind)) return;
-    const u32 g = kind == 0 ? C.gslot[i] : C.pslot[i];
-    keys[i] = g == NONE32 ? invalid : g;
-    vals[i] = i;
+    u32 slot, cnt;
+    grp_fields(C, kind, i, &slot, &cnt);
+    if (cnt < 2) return;
+    const u32 b = kind == 0 ? C.gbeg[slot] : C.pbeg[slot];
+    const u32 k = atomicAdd(kind == 0 ? &C.gfill[slot] : &C.pfill[slot], 1u);
+    (kind == 0 ? C.glist : C.plist)[b + k] = i;
 }
 
-// Walk the id-sorted members: previous same-id event, and the group's range.
-__global__ void tr_group_ranges(TrArgs C, u32 invalid, const u32* ks, const u32* vs) {
-    const u32 q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= C.n || !need(C, 0)) return;
-    const u32 key = ks[q];
-    if (key >= invalid) return;
-    const u32 i = vs[q];
-    const bool first = q == 0 || ks[q - 1] != key;
-    const bool last = q + 1 == C.n || ks[q + 1] != key;
-    C.prev_id[i] = first ? NONE32 : vs[q - 1];
-    if (first) C.gbeg[key] = q;
-    if (last) C.gend[key] = q + 1;
-}
-
-__global__ void tr_pend_ranges(TrArgs C, u32 invalid, const u32* ks, const u32* vs) {
-    const u32 q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= C.n || !need(C, 1)) return;
-    const u32 key = ks[q];
-    if (key >= invalid) return;
-    C.prev_pend[vs[q]] = (q == 0 || ks[q - 1] != key) ? NONE32 : vs[q - 1];
+__global__ void tr_grp_rank(TrArgs C, u32 kind) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= C.n || !need(C, kind)) return;
+    u32 slot, cnt;
+    grp_fields(C, kind, i, &slot, &cnt);
+    if (cnt < 2) return;
+    const u32 b = kind == 0 ? C.gbeg[slot] : C.pbeg[slot];
+    const u32* list = kind == 0 ? C.glist : C.plist;
+    u32 r = 0, prev = NONE32;
+    for (u32 j = b; j < b + cnt; j++) {
+        const u32 v = list[j];
+        if (v < i) {
+            r++;
+            prev = prev == NONE32 ? v : max(prev, v);
+        }
+    }
+    if (kind == 0) {
+        C.gmembers[b + r] = i;
+        C.prev_id[i] = prev;
+        if (r == 0) C.gend[slot] = b + cnt;
+    } else {
+        C.prev_pend[i] = prev;
+    }
 }
 
 // Last in-call event j < i whose id is i's pending_id.
@@ -995,6 +1031,10 @@ __global__ void tr_prep(TrArgs C, u32* cfail0, u32* pc, u32 ring) {
             C.gclaim[k] = 0;
             C.gcnt_id[k] = 0;
             C.gcnt_pd[k] = 0;
+            C.gbeg[k] = NONE32;
+            C.pbeg[k] = NONE32;
+            C.gfill[k] = 0;
+            C.pfill[k] = 0;
         }
         if (k < C.n) cfail0[k] = NONE32;
         if (k < ring) {
@@ -1014,13 +1054,10 @@ void tr_launch_classify(const Tables& T, const TrArgs& C, hipStream_t stream) {
     tr_classify<<<GRID(C.n)>>>(T, C);
     tr_group1<<<GRID(C.n)>>>(C);
 }
-void tr_launch_group_sort(const TrArgs& C, u32 kind, u32 invalid, int bits, u32* k_in, u32* v_in, u32* k_out,
-                          u32* v_out, SortScratch& ss, hipStream_t stream) {
-    tr_group_keys<<<GRID(C.n)>>>(C, kind, invalid, k_in, v_in);
-    radix_sort_pairs(k_in, v_in, k_out, v_out, C.n, bits, ss, stream, C.counters + CNT_FLAGS,
-                     kind == 0 ? FL_MULTI_ID : FL_MULTI_PEND);
-    if (kind == 0) tr_group_ranges<<<GRID(C.n)>>>(C, invalid, k_out, v_out);
-    else tr_pend_ranges<<<GRID(C.n)>>>(C, invalid, k_out, v_out);
+void tr_launch_group(const TrArgs& C, u32 kind, hipStream_t stream) {
+    tr_grp_reserve<<<GRID(C.n)>>>(C, kind);
+    tr_grp_place<<<GRID(C.n)>>>(C, kind);
+    tr_grp_rank<<<GRID(C.n)>>>(C, kind);
 }
 void tr_launch_group2(const TrArgs& C, hipStream_t stream) { tr_group2<<<GRID(C.n)>>>(C); }
 void tr_launch_init(const Tables& T, const TrArgs& C, const EvalState& D, hipStream_t stream) {

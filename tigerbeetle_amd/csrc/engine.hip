@@ -674,6 +674,33 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n) {
         group = (u32)std::ceil(std::log(last + 1.0) / -std::log(r)) + 1;
         group = std::max<u32>(2, std::min<u32>(group, PASS_GROUP_MAX));
     }
+    static const bool probe = getenv("TBGPU_EVAL_PROBE") != nullptr;  // timing diagnostics only
+    if (probe) {
+        // the converged state evaluated again into the other buffer (unused afterwards)
+        // under each probe mode: where a pass's evaluation time goes
+        EvalState& S = c->st[(done_at + 1) & 1];
+        EvalState& D = c->st[done_at & 1];
+        u32* one = c->pc + PC_RING;  // spare ring: an open gate
+        HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)one, 1, 1, s));
+        PassGate G{one, c->counters + CNT_RESORT, 0};
+        for (u32 mode : {0u, 1u, 2u, 3u}) {
+            TrArgs P = C;
+            P.probe = mode;
+            hipEvent_t e0, e1;
+            HIP_CHECK(hipEventCreate(&e0));
+            HIP_CHECK(hipEventCreate(&e1));
+            HIP_CHECK(hipEventRecord(e0, s));
+            for (int r = 0; r < 5; r++) tr_launch_evaluate(c->T, P, S, D, c->bb, G, one + 2, one + 3, s);
+            HIP_CHECK(hipEventRecord(e1, s));
+            HIP_CHECK(hipEventSynchronize(e1));
+            float ms = 0;
+            HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+            fprintf(stderr, "tbgpu: eval probe mode %u: %.2f us per launch (n=%u)\n", mode, ms * 1e3f / 5, n);
+            HIP_CHECK(hipEventDestroy(e0));
+            HIP_CHECK(hipEventDestroy(e1));
+        }
+        HIP_CHECK(hipMemsetAsync(c->counters + CNT_RESORT, 0, sizeof(u32), s));
+    }
     c->stats.iterations = done_at + 1;
     c->last_passes = done_at + 1;
     c->side_m = m;

@@ -56,6 +56,7 @@ struct TrArgs {
     u64 gmask;
     u32* counters;
     u32 debug;            // diagnostics: count changed events by kind (TBGPU_TRACE_PASSES)
+    u32 probe;            // timing probes only (TBGPU_EVAL_PROBE, after convergence): 1 skip post/void, 2 no side records
     Sides sd;             // the account sides of the call's events (engine.h)
 };
 

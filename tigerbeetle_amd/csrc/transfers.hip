@@ -522,6 +522,7 @@ __device__ __forceinline__ bool evaluate_one(const Tables& T, const TrArgs& C, c
     const u8 sr = C.sres[i];
     const u32 csi = C.cs[i];
     const EvCore k = C.core[i];
+    if ((C.probe & 1) && (k.flags & (TF_POST | TF_VOID))) return false;
     const u32 pid = C.prev_id[i], pre_e = C.pre_e[i];
     const uint2 ep = C.sd.epos[i];
     const u8 s_res = S.res[i];
@@ -615,9 +616,10 @@ __device__ __forceinline__ bool evaluate_one(const Tables& T, const TrArgs& C, c
         if (sr == SRES_DYN && !(f & (TF_POST | TF_VOID)) && (C.core[i].aflags & 0x66))
             atomicAdd(&C.counters[CNT_DBG + 5], 1u);
     }
-    // the side records the next pass's balance scan reads (static failures keep the
-    // records tr_side_rec gave them)
-    if (sr == SRES_DYN && !write_sides(C, i, k.flags & (TF_POST | TF_VOID), res == TBGPU_CREATE_TRANSFER_OK,
+    // the side records the next pass's balance scan reads: they hold the previous
+    // state's (written by the previous pass, or tr_side_rec after a sort), so only an
+    // event whose outcome changed rewrites them; static failures keep tr_side_rec's
+    if (sr == SRES_DYN && changed && !(C.probe & 2) && !write_sides(C, i, k.flags & (TF_POST | TF_VOID), res == TBGPU_CREATE_TRANSFER_OK,
                                        pref, dpe, dpo))
         atomicMax(&C.counters[CNT_RESORT], g.p + 1);  // its pending is not among its sides: rebuild them
     return changed;

@@ -421,7 +421,7 @@ static void ensure_h_rc(tbgpu_ctx* c, u64 nb) {
 static u32 general_chunk_batches() {
     static const u32 v = [] {  // TBGPU_CHUNK_BATCHES: experiments only
         const char* e = getenv("TBGPU_CHUNK_BATCHES");
-        return e ? (u32)strtoul(e, nullptr, 0) : 16u;
+        return e ? (u32)strtoul(e, nullptr, 0) : 20u;  // config 3 (r02): 8: 104, 12: 130, 16: 140, 20: 148, 24: 143, 30: 146, 40: 139 M/s
     }();
     return v;
 }

@@ -1,0 +1,81 @@
+"""The device-resident routed step with several ranks on one GPU and CUDA tensors:
+the path `bench.py --gpus N` takes over RCCL (the engine's tbgpu_route_stats /
+tbgpu_route_scatter, the all-to-all of events and side records, the owner commit,
+the one-dry-run settlement of cross-shard chains), with the collectives stood in by
+threads (tests/thread_dist.py) because one RCCL rank needs one GPU.  Checked against
+the single CPU state machine over the router's global order (tests/test_shard.py)."""
+import threading
+
+import numpy as np
+import pytest
+
+from tests.shard_workload import config4_failing, config4_small
+from tests.test_shard import verify
+from tests.thread_dist import ThreadDist, ThreadGroup
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(w, world):
+    import torch
+
+    from tigerbeetle_amd.engine import Engine
+    from tigerbeetle_amd.shard import Comm, ShardedStateMachine
+    from tigerbeetle_amd.types import TRANSFER_DTYPE
+    group = ThreadGroup(world)
+    outs, errors = [None] * world, []
+    dev = torch.device("cuda", 0)
+
+    def worker(rank):
+        eng = None
+        try:
+            eng = Engine(device=0, accounts_max=len(w.accounts) + 16, transfers_max=1 << 16, history_max=1 << 12,
+                         events_per_call_max=1 << 14)
+            comm = Comm(rank, world, device=dev)
+            comm.dist = ThreadDist(group, rank)
+            sm = ShardedStateMachine(eng, comm)
+            acc_replies = sm.create_accounts(w.account_batches if rank == 0 else [])
+            replies = []
+            for s in range(w.steps):
+                batches = w.step_batches(s, rank)
+                flat = np.concatenate(batches) if batches else np.zeros(0, dtype=TRANSFER_DTYPE)
+                ev = torch.from_numpy(flat.view(np.uint8).copy()).to(dev)
+                got = sm.create_transfers_device(ev, [len(b) for b in batches])
+                replies.append([r.tobytes() for r in got])
+            acc, xs = sm.export_state()
+            outs[rank] = {"replies": replies, "acc_replies": [a.tobytes() for a in acc_replies],
+                          "acc": acc.tobytes(), "xs": xs.tobytes(), "cts": sm.commit_timestamp,
+                          "stats": dict(sm.stats)}
+        except BaseException as e:  # noqa: BLE001 -- re-raised in the main thread
+            errors.append(e)
+            group.barrier.abort()
+        finally:
+            if eng is not None:
+                eng.close()
+
+    threads = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=240)
+    assert not any(t.is_alive() for t in threads), "a rank did not finish"
+    if errors:
+        raise errors[0]
+    return verify(w, outs, world)
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_routed_device_step_config4(world):
+    stats = _run(config4_small(71 + world, world, 3, 2), world)
+    assert stats["preruns"] > 0 and stats["dry_rounds"] == 0 and stats["device_fallbacks"] == 0
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_routed_device_step_breaking_chains(world):
+    stats = _run(config4_failing(81 + world, world, 3, 2), world)
+    assert stats["preruns"] > 0 and stats["dry_rounds"] == 0
+
+
+def test_routed_device_step_limit_accounts():
+    stats = _run(config4_failing(91, 3, 3, 2, limits=True), 3)
+    assert stats["dry_rounds"] > 0

@@ -82,12 +82,18 @@ def _make(spec):
 
 def _check(spec, world, kind="oracle", device_step=False, max_rounds=None):
     import torch.multiprocessing as mp
-    from tigerbeetle_amd.types import ACCOUNT_DTYPE, RESULT_DTYPE, TRANSFER_DTYPE
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(world, _free_port(), d, spec, kind, device_step, max_rounds), nprocs=world,
                  join=True)
         outs = [pickle.load(open(os.path.join(d, f"r{r}.pkl"), "rb")) for r in range(world)]
-    w = _make(spec)
+    return verify(_make(spec), outs, world)
+
+
+def verify(w, outs, world):
+    """The single state machine (one oracle) over the router's global order: every
+    reply of every rank, the accounts each shard owns, the transfers each stored and
+    the commit timestamp, bit for bit.  Returns rank 0's router stats."""
+    from tigerbeetle_amd.types import ACCOUNT_DTYPE, RESULT_DTYPE, TRANSFER_DTYPE
     # the single state machine over the global order
     o = oracle.Oracle(len(w.accounts), 1 << 14)
     ts = 0

@@ -554,19 +554,54 @@ __device__ __forceinline__ bool evaluate_one(const Tables& T, const TrArgs& C, c
                 }
             }
         } else {
+            // post_or_void_pending_transfer (src/state_machine.zig:1391-1498).  What the
+            // likely answers read is issued together: the last earlier event with the
+            // pending id (its visibility inputs and its row), the committed pending row,
+            // the previous post/void of the same pending -- then the chain words -- instead
+            // of a walk of dependent loads.  The walks below stay for the other cases.
             Transfer t = C.ev[i];
             t.timestamp = k.ts;
-            // post_or_void_pending_transfer (src/state_machine.zig:1391-1498)
+            const u32 pl = C.pend_last[i], pp = C.pre_p[i], pvp = C.prev_pend[i];
+            const bool pl_v = pl != NONE32, pp_v = pp != NONE32, pvp_v = pvp != NONE32;
+            const u32 pl_cs = pl_v ? C.cs[pl] : 0u, pl_ce = pl_v ? C.ce[pl] : 0u;
+            const u8 pl_ok = pl_v ? S.ok[pl] : 0;
+            const Transfer pl_row = pl_v ? C.ev[pl] : t;
+            const u128 pl_amt = pl_v ? S.amt[pl] : 0;
+            const u64 pl_ts = pl_v ? C.ts[pl] : 0;
+            const Transfer pp_row = pp_v ? T.xrows[pp] : t;
+            const u8 pp_ful = pp_v ? T.xful[pp] : 0;
+            const u32 pvp_cs = pvp_v ? C.cs[pvp] : 0u, pvp_ce = pvp_v ? C.ce[pvp] : 0u;
+            const u8 pvp_ok = pvp_v ? S.ok[pvp] : 0;
+            const u16 pvp_fl = pvp_v ? C.core[pvp].flags : 0;
+            auto vis = [&](u32 j, u32 js, u32 je, u8 ok) {  // visible() from loaded words
+                if (js == csi) return (ok & 1) != 0;
+                if (!(ok & 1)) return false;
+                if (C.ctl && (C.ctl[je] & TBGPU_CTL_DOOM)) return false;
+                return js == je || S.cfail[js] == NONE32;
+            };
             u32 p = NONE32;
-            for (u32 j = C.pend_last[i]; j != NONE32; j = C.prev_id[j])
-                if (visible(C, S, j, csi)) { p = j; break; }
-            if (p == NONE32 && C.pre_p[i] != NONE32) p = PREF_ROW | C.pre_p[i];
+            if (pl_v && vis(pl, pl_cs, pl_ce, pl_ok)) {
+                p = pl;
+            } else if (pl_v) {
+                for (u32 j = C.prev_id[pl]; j != NONE32; j = C.prev_id[j])
+                    if (visible(C, S, j, csi)) { p = j; break; }
+            }
+            if (p == NONE32 && pp_v) p = PREF_ROW | pp;
             pref = p;
             const bool post = t.flags & TF_POST;
             if (p == NONE32) {
                 res = TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_NOT_FOUND;
             } else {
-                const Transfer P = load_ref(T, C, S, p);
+                Transfer P;
+                if (p == pl && !(pl_row.flags & (TF_POST | TF_VOID))) {
+                    P = pl_row;  // stored_regular
+                    P.amount = pl_amt;
+                    P.timestamp = pl_ts;
+                } else if (p == (PREF_ROW | pp)) {
+                    P = pp_row;
+                } else {
+                    P = load_ref(T, C, S, p);
+                }
                 const u128 amount = t.amount > 0 ? t.amount : P.amount;
                 if (!(P.flags & TF_PENDING)) res = TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_NOT_PENDING;
                 else if (t.debit_account_id > 0 && t.debit_account_id != P.debit_account_id)
@@ -582,9 +617,13 @@ __device__ __forceinline__ bool evaluate_one(const Tables& T, const TrArgs& C, c
                 else {
                     // posted groove (src/state_machine.zig:1431-1436)
                     u32 ful = 0;
-                    for (u32 j = C.prev_pend[i]; j != NONE32; j = C.prev_pend[j])
-                        if (visible(C, S, j, csi)) { ful = (C.ev[j].flags & TF_POST) ? 1 : 2; break; }
-                    if (ful == 0 && (p & PREF_ROW)) ful = T.xful[p & ~PREF_ROW];
+                    if (pvp_v && vis(pvp, pvp_cs, pvp_ce, pvp_ok)) {
+                        ful = (pvp_fl & TF_POST) ? 1 : 2;
+                    } else if (pvp_v) {
+                        for (u32 j = C.prev_pend[pvp]; j != NONE32; j = C.prev_pend[j])
+                            if (visible(C, S, j, csi)) { ful = (C.core[j].flags & TF_POST) ? 1 : 2; break; }
+                    }
+                    if (ful == 0 && (p & PREF_ROW)) ful = (p == (PREF_ROW | pp)) ? pp_ful : T.xful[p & ~PREF_ROW];
                     if (ful == 1) res = TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_ALREADY_POSTED;
                     else if (ful == 2) res = TBGPU_CREATE_TRANSFER_PENDING_TRANSFER_ALREADY_VOIDED;
                     else if (P.timeout > 0 && t.timestamp >= P.timestamp + (u64)P.timeout * NS_PER_S)

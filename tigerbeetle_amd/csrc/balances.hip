@@ -256,14 +256,41 @@ __device__ __forceinline__ SF combine_f(const SF& a, const SF& b) {
     c.fl = a.fl | b.fl;
     return c;
 }
+// One DPP step of the wave's inclusive segmented scan: every lane combines the value
+// `ctrl` names (row_shr:n within a row of 16, or the row_bcast of a row's last lane
+// into the rows `row_mask` selects); a lane without a source gets zero: the identity.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ u32 dpp32(u32 x) {
+    return (u32)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROW_MASK, 0xf, true);
+}
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ u128 dpp128(u128 x) {
+    const u64 lo = (u64)x, hi = (u64)(x >> 64);
+    const u64 l = (u64)dpp32<CTRL, ROW_MASK>((u32)lo) | ((u64)dpp32<CTRL, ROW_MASK>((u32)(lo >> 32)) << 32);
+    const u64 h = (u64)dpp32<CTRL, ROW_MASK>((u32)hi) | ((u64)dpp32<CTRL, ROW_MASK>((u32)(hi >> 32)) << 32);
+    return ((u128)h << 64) | l;
+}
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ void dpp_step(SF& v) {
+    SF o;
+    o.F.dp = dpp128<CTRL, ROW_MASK>(v.F.dp);
+    o.F.dpo = dpp128<CTRL, ROW_MASK>(v.F.dpo);
+    o.F.cp = dpp128<CTRL, ROW_MASK>(v.F.cp);
+    o.F.cpo = dpp128<CTRL, ROW_MASK>(v.F.cpo);
+    o.fl = dpp32<CTRL, ROW_MASK>(v.fl);
+    v = combine_f(o, v);
+}
+
 __device__ __forceinline__ SF block_excl_f(SF v, SF* wtot) {
     const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int off = 1; off < 64; off <<= 1) {
-        SF o;
-        o.F = shup_bal(v.F, off);
-        o.fl = __shfl_up(v.fl, off);
-        if (lane >= (u32)off) v = combine_f(o, v);
-    }
+    // inclusive over the wave by DPP (no LDS round trips): within rows of 16, then
+    // row 0's last into row 1 and row 2's into row 3, then row 1's into rows 2 and 3
+    dpp_step<0x111, 0xf>(v);  // row_shr:1
+    dpp_step<0x112, 0xf>(v);  // row_shr:2
+    dpp_step<0x114, 0xf>(v);  // row_shr:4
+    dpp_step<0x118, 0xf>(v);  // row_shr:8
+    dpp_step<0x142, 0xa>(v);  // row_bcast:15
+    dpp_step<0x143, 0xc>(v);  // row_bcast:31
     SF ex;
     ex.F = shup_bal(v.F, 1);
     ex.fl = __shfl_up(v.fl, 1);
@@ -285,7 +312,7 @@ __device__ __forceinline__ void side_contrib(const SideScanArgs& A, u64 q, Bal4&
     zero(H);
     if (!(A.sq_ok[q] & 1)) return;
     const u128 dpe = A.sq_dpend[q], dpo = A.sq_dpost[q];
-    const bool fin = side_final(A, q), credit = A.sq_ev[q] >> 31;
+    const bool fin = (A.probe & 1) ? true : side_final(A, q), credit = A.sq_ev[q] >> 31;
     const u128 pe = credit ? 0 : dpe, po = credit ? 0 : dpo, ce = credit ? dpe : 0, co = credit ? dpo : 0;
     if (fin) { F.dp = pe; F.dpo = po; F.cp = ce; F.cpo = co; }
     else { H.dp = pe; H.dpo = po; H.cp = ce; H.cpo = co; }
@@ -329,7 +356,7 @@ __global__ __launch_bounds__(BF_THREADS) void bs_fused(SideScanArgs A, u64 m, u3
     for (int k = 0; k < BF_IPT; k++) {
         // the account row (pre-chunk balances) is issued before the scan's barrier
         zero(row[k]);
-        if (key[k] < invalid) {
+        if (key[k] < invalid && !(A.probe & 2)) {
             const Account& ac = acc[key[k]];
             row[k].dp = ac.debits_pending;
             row[k].dpo = ac.debits_posted;
@@ -359,7 +386,14 @@ __global__ __launch_bounds__(BF_THREADS) void bs_fused(SideScanArgs A, u64 m, u3
     SF agg = e[0];
 #pragma unroll
     for (int k = 1; k < BF_IPT; k++) agg = combine_f(agg, e[k]);
-    SF run = block_excl_f(agg, wtot);  // (its barrier publishes s_key / s_cs / s_h)
+    SF run;
+    if (A.probe & 4) {
+        zero(run.F);
+        run.fl = 0;
+        __syncthreads();
+    } else {
+        run = block_excl_f(agg, wtot);  // (its barrier publishes s_key / s_cs / s_h)
+    }
 #pragma unroll
     for (int k = 0; k < BF_IPT; k++) {
         const u64 q = qa + k;

@@ -151,6 +151,7 @@ struct SideScanArgs {
     u32* cfail_clear; // the next state's cfail, reset by the scan (NONE32), or null
     u32 n;            // events (cfail_clear length)
     PassGate gate;
+    u32 probe;        // timing probes only (TBGPU_EVAL_PROBE): 1 no chain words, 2 no account rows, 4 no block scan
 };
 
 // final-ok of a sorted side: evaluated-ok and its chain persisted

@@ -699,6 +699,27 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n) {
             HIP_CHECK(hipEventDestroy(e0));
             HIP_CHECK(hipEventDestroy(e1));
         }
+        for (u32 mode : {0u, 1u, 2u, 4u, 7u}) {
+            SideScanArgs P = SA;
+            P.probe = mode;
+            P.cfail = S.cfail;
+            P.cfail_clear = nullptr;
+            P.gate = G;
+            hipEvent_t e0, e1;
+            HIP_CHECK(hipEventCreate(&e0));
+            HIP_CHECK(hipEventCreate(&e1));
+            HIP_CHECK(hipEventRecord(e0, s));
+            for (int r = 0; r < 5; r++)
+                side_scan_fused(P, m, inv_acc, c->tstart, c->counters + CNT_LONG, c->T.acc, c->bb, s);
+            HIP_CHECK(hipEventRecord(e1, s));
+            HIP_CHECK(hipEventSynchronize(e1));
+            float ms = 0;
+            HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+            fprintf(stderr, "tbgpu: scan probe mode %u: %.2f us per launch (m=%llu)\n", mode, ms * 1e3f / 5,
+                    (unsigned long long)m);
+            HIP_CHECK(hipEventDestroy(e0));
+            HIP_CHECK(hipEventDestroy(e1));
+        }
         HIP_CHECK(hipMemsetAsync(c->counters + CNT_RESORT, 0, sizeof(u32), s));
     }
     c->stats.iterations = done_at + 1;

@@ -183,14 +183,15 @@ def routed_bench(args, rank, world, local_rank, torch, dist, backend="nccl"):
     per_step = B * BATCH_MAX
     acc_n = args.accounts or 10_000_000
     t_gen = time.time()
-    w = workload.config4(transfer_count=(K + W) * per_step, ledgers=1000, accounts_per_ledger=acc_n // 1000,
+    P = 1  # a step after the timed region, run with per-phase synchronization for the breakdown
+    w = workload.config4(transfer_count=(K + W + P) * per_step, ledgers=1000, accounts_per_ledger=acc_n // 1000,
                          seed=42 + rank)
     j = np.arange(len(w.transfers), dtype=np.uint64)
     w.transfers["id_lo"] = ((j // per_step) * world + rank) * per_step + (j % per_step) + 1
     w.transfers["id_hi"] = 0
     log(f"[rank {rank}] generated {len(w.transfers)} transfers / {acc_n} accounts in {time.time() - t_gen:.1f}s")
     dev = torch.device("cuda", local_rank)
-    eng = Engine(device=local_rank, accounts_max=acc_n, transfers_max=int((K + W) * per_step * 1.25) + 4096,
+    eng = Engine(device=local_rank, accounts_max=acc_n, transfers_max=int((K + W + P) * per_step * 1.25) + 4096,
                  history_max=1024, events_per_call_max=int(per_step * 1.25) + BATCH_MAX,
                  dense_block_span=acc_n // 1000)
     ats, _ = w.timestamps()
@@ -204,26 +205,33 @@ def routed_bench(args, rank, world, local_rank, torch, dist, backend="nccl"):
     del w
     torch.cuda.synchronize()
 
-    def step(k):
-        ev = ev_dev[k * per_step * 128:(k + 1) * per_step * 128]
-        reps = ssm.create_transfers_device(ev, list(map(int, counts[k * B:(k + 1) * B])))
-        return sum(len(r) for r in reps)
+    def step_args(k):
+        return ev_dev[k * per_step * 128:(k + 1) * per_step * 128], list(map(int, counts[k * B:(k + 1) * B]))
 
     for k in range(W):
-        step(k)
+        ssm.create_transfers_device(*step_args(k))
     torch.cuda.synchronize()
     dist.barrier()
-    for key in ssm.timing:
-        ssm.timing[key] = 0.0
     st0 = dict(ssm.stats)
-    ssm.timed = True
     non_ok = 0
+    # the timed steps; with --pipelined step k + 1 is routed (eligibility, scatter,
+    # all-to-all) while step k's owner commit runs (shard.py create_transfers_device_stream):
+    # on one GPU that measured slower (both halves are HBM-bound), so it is not the default
     t0 = time.perf_counter()
-    for k in range(W, W + K):
-        non_ok += step(k)
+    if args.pipelined:
+        for reps in ssm.create_transfers_device_stream(step_args(k) for k in range(W, W + K)):
+            non_ok += sum(len(r) for r in reps)
+    else:
+        for k in range(W, W + K):
+            non_ok += sum(len(r) for r in ssm.create_transfers_device(*step_args(k)))
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0
+    # one more step, unpipelined and synchronized per phase: where a step's time goes
+    for key in ssm.timing:
+        ssm.timing[key] = 0.0
+    ssm.timed = True
+    ssm.create_transfers_device(*step_args(W + K))
     ssm.timed = False
     t = torch.tensor([elapsed, non_ok] + [ssm.timing[x] for x in sorted(ssm.timing)], dtype=torch.float64,
                      device=cdev)
@@ -235,7 +243,7 @@ def routed_bench(args, rank, world, local_rank, torch, dist, backend="nccl"):
     non_ok = int(tsum[1])
     total = per_step * K * world
     value = total / elapsed
-    phases = {x: round(float(tmax[2 + i]) / K, 3) for i, x in enumerate(sorted(ssm.timing))}
+    phases = {x: round(float(tmax[2 + i]), 3) for i, x in enumerate(sorted(ssm.timing))}
     if rank == 0:
         e2e = value / world * ALGO_BYTES_PER_TRANSFER / 1e9
         a2a_bytes = per_step * (128 + 32) * (world - 1) / world  # events + side records leaving each rank
@@ -261,7 +269,8 @@ def routed_bench(args, rank, world, local_rank, torch, dist, backend="nccl"):
                                       f"{'RCCL' if backend == 'nccl' else backend} collectives)"},
             "non_ok_results": non_ok,
             "non_ok_rate": round(non_ok / total, 5),
-            "routed": {"phase_ms_per_step_max_over_ranks": phases,
+            "routed": {"pipelined": bool(args.pipelined),
+                       "phase_ms_one_unpipelined_step_max_over_ranks": phases,
                        "alltoall_bytes_per_rank_per_step": int(a2a_bytes),
                        "alltoall_GBps_per_rank": round(a2a_bytes / (phases["exchange_ms"] * 1e-3) / 1e9, 1)
                        if phases["exchange_ms"] > 0 else None,
@@ -328,6 +337,8 @@ def main():
                          "per GPU (generated in HBM)")
     ap.add_argument("--routed", action="store_true",
                     help="config 4 through the ledger router even on one GPU (a one-rank RCCL group)")
+    ap.add_argument("--pipelined", action="store_true",
+                    help="routed: route step k + 1 while step k commits (measured slower on one GPU, r02)")
     ap.add_argument("--unrouted", action="store_true",
                     help="N > 1: every rank commits its own pre-routed ledger shard (no all-to-all)")
     ap.add_argument("--force-general", action="store_true", help="disable the fast path (measure the fixed point)")

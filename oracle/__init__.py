@@ -142,7 +142,7 @@ class Oracle:
                                             _ptr(rc), ctypes.byref(cts))
         return out, rc, cts.value
 
-    def create_transfers_routed_tensors(self, counts, events, event_ts, ctl, dry_run, results):
+    def create_transfers_routed_tensors(self, counts, events, event_ts, ctl, dry_run, results, sync_inputs=True):
         """The Engine method of the same name over CPU tensors (sharded-commit tests)."""
         ev = events.numpy().view(TRANSFER_DTYPE)
         out, rc, cts = self.create_transfers_routed(counts, ev, event_ts.numpy().view(np.uint64),

@@ -16,7 +16,7 @@ from tests.thread_dist import ThreadDist, ThreadGroup
 pytestmark = pytest.mark.gpu
 
 
-def _run(w, world):
+def _run(w, world, pipelined=False):
     import torch
 
     from tigerbeetle_amd.engine import Engine
@@ -36,12 +36,18 @@ def _run(w, world):
             sm = ShardedStateMachine(eng, comm)
             acc_replies = sm.create_accounts(w.account_batches if rank == 0 else [])
             replies = []
+            steps = []
             for s in range(w.steps):
                 batches = w.step_batches(s, rank)
                 flat = np.concatenate(batches) if batches else np.zeros(0, dtype=TRANSFER_DTYPE)
-                ev = torch.from_numpy(flat.view(np.uint8).copy()).to(dev)
-                got = sm.create_transfers_device(ev, [len(b) for b in batches])
-                replies.append([r.tobytes() for r in got])
+                steps.append((torch.from_numpy(flat.view(np.uint8).copy()).to(dev), [len(b) for b in batches]))
+            if pipelined:
+                for got in sm.create_transfers_device_stream(steps):
+                    replies.append([r.tobytes() for r in got])
+            else:
+                for ev, cnt in steps:
+                    got = sm.create_transfers_device(ev, cnt)
+                    replies.append([r.tobytes() for r in got])
             acc, xs = sm.export_state()
             outs[rank] = {"replies": replies, "acc_replies": [a.tobytes() for a in acc_replies],
                           "acc": acc.tobytes(), "xs": xs.tobytes(), "cts": sm.commit_timestamp,
@@ -78,4 +84,14 @@ def test_routed_device_step_breaking_chains(world):
 
 def test_routed_device_step_limit_accounts():
     stats = _run(config4_failing(91, 3, 3, 2, limits=True), 3)
+    assert stats["dry_rounds"] > 0
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_routed_device_stream_pipelined(world):
+    """The pipelined form (bench.py's timed loop): step k + 1's stats, scatter and
+    all-to-all while step k's owner commit runs on a worker thread."""
+    stats = _run(config4_failing(111 + world, world, 4, 2), world, pipelined=True)
+    assert stats["preruns"] > 0
+    stats = _run(config4_failing(121 + world, world, 3, 2, limits=True), world, pipelined=True)
     assert stats["dry_rounds"] > 0

@@ -50,7 +50,17 @@ def _worker(rank, world, port, out_dir, spec, kind="oracle", device_step=False, 
             sm.max_rounds = max_rounds
         acc_replies = sm.create_accounts(w.account_batches if rank == 0 else [])
         replies = []
-        for s in range(w.steps):
+        if device_step == "stream":
+            # the pipelined form: step k + 1 routed while step k commits
+            import torch
+            steps = []
+            for s in range(w.steps):
+                batches = w.step_batches(s, rank)
+                flat = np.concatenate(batches) if batches else np.zeros(0, dtype=TRANSFER_DTYPE)
+                steps.append((torch.from_numpy(flat.view(np.uint8).copy()), [len(b) for b in batches]))
+            for got in sm.create_transfers_device_stream(steps):
+                replies.append([r.tobytes() for r in got])
+        for s in range(w.steps if device_step != "stream" else 0):
             batches = w.step_batches(s, rank)
             if device_step:
                 import torch
@@ -176,3 +186,10 @@ def test_serial_fallback_one_cross_shard_chain_per_round(world):
     one dry round is committed one cross-shard chain at a time, still bit-exact."""
     stats = _check(("mix", 61 + world, world, 2, 2), world, max_rounds=1)
     assert stats["serial_fallbacks"] > 0
+
+
+@pytest.mark.parametrize("kind", ["c4", "c4f", "c4l"])
+def test_device_step_pipelined(kind):
+    """create_transfers_device_stream: the next step routed while this one commits on a
+    worker thread; the same results as the single state machine."""
+    _check((kind, 101, 2, 3, 2), 2, device_step="stream")

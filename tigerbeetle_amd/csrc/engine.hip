@@ -113,6 +113,9 @@ struct tbgpu_ctx {
     u8* rt_ctl_buf = nullptr;
     u64* rt_dry_ts = nullptr;
     u64* rt_stats = nullptr;  // [5] tbgpu_route_stats
+    // the router's kernels run on their own stream: a routed step's scatter may
+    // overlap the previous step's commit (tigerbeetle_amd/shard.py pipelining)
+    hipStream_t route_stream = nullptr;
     // the router's send-side scatter (route.hip), grown on demand
     u64 ro_cap = 0, ro_bcap = 0;
     uint2* ro_orank = nullptr;
@@ -289,6 +292,7 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     c->device = o.device;
     HIP_CHECK(hipSetDevice(c->device));
     HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIP_CHECK(hipStreamCreateWithFlags(&c->route_stream, hipStreamNonBlocking));
     HIP_CHECK(hipEventCreate(&c->ev0));
     HIP_CHECK(hipEventCreate(&c->ev1));
     c->accounts_max = o.accounts_max;
@@ -381,6 +385,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     (void)hipEventDestroy(c->ev0);
     (void)hipEventDestroy(c->ev1);
     (void)hipStreamDestroy(c->stream);
+    (void)hipStreamDestroy(c->route_stream);
     delete c;
 }
 
@@ -949,9 +954,9 @@ void route_stats(const Transfer* ev, u64 n, u64* out, hipStream_t stream);
 
 extern "C" int tbgpu_route_stats(tbgpu_ctx* c, const void* events_device, uint64_t count, uint64_t* out) {
     HIP_CHECK(hipSetDevice(c->device));
-    route_stats((const Transfer*)events_device, count, c->rt_stats, c->stream);
-    HIP_CHECK(hipMemcpyAsync(out, c->rt_stats, 5 * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
-    HIP_CHECK(hipStreamSynchronize(c->stream));
+    route_stats((const Transfer*)events_device, count, c->rt_stats, c->route_stream);
+    HIP_CHECK(hipMemcpyAsync(out, c->rt_stats, 5 * sizeof(u64), hipMemcpyDeviceToHost, c->route_stream));
+    HIP_CHECK(hipStreamSynchronize(c->route_stream));
     return 0;
 }
 void route_scatter(const Transfer* ev, u64 n, u32 world, u32 nb, const u32* b_start, const u64* b_ts, u64 g0,
@@ -990,18 +995,18 @@ extern "C" int tbgpu_route_scatter(tbgpu_ctx* c, uint32_t world, uint32_t batch_
         return 0;
     }
     HIP_CHECK(hipMemcpyAsync(c->ro_bstart, starts.data(), (batch_count + 1) * sizeof(u32), hipMemcpyHostToDevice,
-                             c->stream));
-    HIP_CHECK(hipMemcpyAsync(c->ro_bts, batch_timestamps, batch_count * sizeof(u64), hipMemcpyHostToDevice, c->stream));
+                             c->route_stream));
+    HIP_CHECK(hipMemcpyAsync(c->ro_bts, batch_timestamps, batch_count * sizeof(u64), hipMemcpyHostToDevice, c->route_stream));
     route_scatter((const Transfer*)events_device, n, world, batch_count, c->ro_bstart, c->ro_bts, first_global_batch,
                   c->ro_orank, c->ro_blk, c->ro_counts, (Transfer*)send_events_device, (u64*)send_sides_device,
-                  c->ro_bcount + 256, c->ro_bcount, c->stream);
-    HIP_CHECK(hipMemcpyAsync(send_counts, c->ro_counts, world * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+                  c->ro_bcount + 256, c->ro_bcount, c->route_stream);
+    HIP_CHECK(hipMemcpyAsync(send_counts, c->ro_counts, world * sizeof(u64), hipMemcpyDeviceToHost, c->route_stream));
     if (send_batch_counts)
         HIP_CHECK(hipMemcpyAsync(send_batch_counts, c->ro_bcount + 256, (u64)world * batch_count * sizeof(u32),
-                                 hipMemcpyDeviceToHost, c->stream));
+                                 hipMemcpyDeviceToHost, c->route_stream));
     if (send_span_counts)
-        HIP_CHECK(hipMemcpyAsync(send_span_counts, c->ro_bcount, world * sizeof(u32), hipMemcpyDeviceToHost, c->stream));
-    HIP_CHECK(hipStreamSynchronize(c->stream));
+        HIP_CHECK(hipMemcpyAsync(send_span_counts, c->ro_bcount, world * sizeof(u32), hipMemcpyDeviceToHost, c->route_stream));
+    HIP_CHECK(hipStreamSynchronize(c->route_stream));
     return 0;
 }
 

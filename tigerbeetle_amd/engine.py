@@ -224,7 +224,7 @@ class Engine:
                                               _ptr(rc), ctypes.byref(cts))
         return out, rc, cts.value
 
-    def create_transfers_routed_tensors(self, counts, events, event_ts, ctl, dry_run, results):
+    def create_transfers_routed_tensors(self, counts, events, event_ts, ctl, dry_run, results, sync_inputs=True):
         """Routed sub-batches with every array a device tensor (torch, on this engine's
         GPU): events uint8 [n*128], event_ts int64 [n], ctl uint8 [n] or None, results
         a uint8 tensor of >= 8*n bytes that receives the concatenated sparse replies.
@@ -232,9 +232,11 @@ class Engine:
         host_results = None
         if events.is_cuda:
             # the tensors were produced on torch's current stream; the engine runs on
-            # its own, so wait for them (the call itself returns after its stream drained)
-            import torch
-            torch.cuda.current_stream(events.device).synchronize()
+            # its own, so wait for them (the call itself returns after its stream drained);
+            # a caller on another thread synchronizes before handing them over
+            if sync_inputs:
+                import torch
+                torch.cuda.current_stream(events.device).synchronize()
         else:  # CPU tensors (the gloo-routed tests): stage them in HBM
             dev = f"cuda:{self.device}"
             events, event_ts = events.to(dev), event_ts.to(dev)

@@ -56,6 +56,7 @@ oracle as the checker.
 from __future__ import annotations
 
 from dataclasses import dataclass
+from types import SimpleNamespace
 
 import numpy as np
 
@@ -252,6 +253,42 @@ class ShardedStateMachine:
         run to their fixed point, and past `max_rounds` the step goes to the exact
         router (create_transfers), which settles one cross-shard chain at a time.
         Anything else goes through create_transfers too."""
+        st = self.route_device(events, counts)
+        if st.fallback:
+            return self._host_step(st.ev, st.counts, st.offs_h)
+        self.commit_routed(st)
+        return self.finish_routed(st)
+
+    def create_transfers_device_stream(self, steps):
+        """create_transfers_device over consecutive steps ((events, counts) pairs),
+        pipelined: while step k's owner commit runs on a worker thread, step k + 1 is
+        routed (eligibility, scatter, all-to-all).  Yields each step's replies, equal to
+        create_transfers_device's (the results do not depend on the overlap)."""
+        it = iter(steps)
+        nxt = next(it, None)
+        st = self.route_device(*nxt) if nxt is not None else None
+        while st is not None:
+            if st.fallback:
+                yield self._host_step(st.ev, st.counts, st.offs_h)
+                nxt = next(it, None)
+                st = self.route_device(*nxt) if nxt is not None else None
+                continue
+            self.commit_routed(st, background=True)
+            nxt = next(it, None)
+            st2 = self.route_device(*nxt) if nxt is not None else None
+            yield self.finish_routed(st)
+            st = st2
+
+    def _host_step(self, ev, counts, offs_h):
+        host = ev.cpu().numpy().view(TRANSFER_DTYPE)
+        return self.create_transfers([host[offs_h[j]:offs_h[j + 1]] for j in range(len(counts))])
+
+    def route_device(self, events, counts):
+        """Phase 1 of a device step: eligibility, global order, scatter to the owners,
+        exchange, and what the owner side needs to settle cross-shard chains.  Returns
+        a step record; `fallback` set (and nothing changed) when the step must go
+        through the exact host router."""
+        clock = self._clock()
         import math
         torch = self.comm.torch
         dev = self.comm.device
@@ -296,8 +333,7 @@ class ShardedStateMachine:
             prev = hi
         offs_h = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
         if not ok:
-            host = ev.cpu().numpy().view(TRANSFER_DTYPE)
-            return self.create_transfers([host[offs_h[j]:offs_h[j + 1]] for j in range(len(counts))])
+            return SimpleNamespace(fallback=True, ev=ev, counts=counts, offs_h=offs_h)
         clock("eligibility_ms")
         saved = (self.prepare_timestamp, self.max_id, self.amount_bound)
         self.max_id = max(self.max_id, prev)
@@ -387,6 +423,23 @@ class ShardedStateMachine:
         all_plain = True
         if any_span:
             all_plain = all(self.comm.all_gather_object(plain_local)) and self.amount_bound < 2.0**125
+        return SimpleNamespace(**{k: v for k, v in locals().items() if k not in ("self", "clock")},
+                               fallback=False)
+
+    def commit_routed(self, st, background: bool = False):
+        """Phase 2: settle the step's cross-shard chains (collectives, on this thread),
+        then the owner commit -- on a worker thread when `background`, so that the next
+        step's routing (phase 1) overlaps it.  Sets st.out / st.at / st.cts (or, after a
+        device fallback, st.replies)."""
+        import threading
+        torch = self.comm.torch
+        clock = self._clock()
+        g = st.__dict__
+        dev, m, R, S, si, n_span = g["dev"], g["m"], g["R"], g["S"], g["si"], g["n_span"]
+        sub_counts, any_span, all_plain = g["sub_counts"], g["any_span"], g["all_plain"]
+        key, nxt, lastm, base, gk = (g.get(x) for x in ("key", "nxt", "lastm", "base", "gk"))
+        st.replies = None
+        st.thread = None
         results = torch.empty(max(m, 1) * 8, dtype=torch.uint8, device=dev)
         ts_r = S[:, 0].contiguous() if m else torch.zeros(1, dtype=torch.int64, device=dev)
         Rf = R.reshape(-1) if m else torch.zeros(128, dtype=torch.uint8, device=dev)
@@ -406,6 +459,9 @@ class ShardedStateMachine:
                 cx = None if ctl is None else ctl.index_select(0, sel)
                 ox = np.concatenate([[0], np.cumsum(cnts)]).astype(np.int64)
             rc, cts = self.backend.create_transfers_routed_tensors(cnts, rx, tx, cx, dry, results)
+            return decode(rc, cts, ox, sel)
+
+        def decode(rc, cts, ox, sel=None):
             tot = int(np.sum(rc))
             out = results[:tot * 8].cpu().numpy().view(RESULT_DTYPE).copy() if tot else np.zeros(0, RESULT_DTYPE)
             at = np.repeat(ox[:-1], rc.astype(np.int64)) + out["index"].astype(np.int64) if tot else \
@@ -461,8 +517,7 @@ class ShardedStateMachine:
                 # run of the cross-shard members alone finds every chain's break
                 self.stats["preruns"] += 1
                 d_out, d_at, _ = commit(control({}), True, sel=si)
-                brk = breaks(d_out, d_at)
-                out, at, cts = commit(control(brk), False)
+                final_ctl = control(breaks(d_out, d_at))
             else:
                 brk = {}
                 for _ in range(self.max_rounds):
@@ -473,19 +528,57 @@ class ShardedStateMachine:
                     if nb_ == brk:
                         out2, at2, cts = commit(ctl, False)
                         assert out2.tobytes() == out.tobytes(), "sharded commit: dry run and commit disagree"
-                        out, at = out2, at2
-                        break
+                        st.out, st.at, st.cts = out2, at2, cts
+                        clock("commit_ms")
+                        return st
                     brk = nb_
                 else:
                     # no fixed point within max_rounds: nothing was committed; the exact
                     # router settles the step one cross-shard chain at a time
                     self.stats["device_fallbacks"] += 1
-                    self.prepare_timestamp, self.max_id, self.amount_bound = saved
-                    host = ev.cpu().numpy().view(TRANSFER_DTYPE)
-                    return self.create_transfers([host[offs_h[j]:offs_h[j + 1]] for j in range(len(counts))])
+                    self.prepare_timestamp, self.max_id, self.amount_bound = g["saved"]
+                    st.replies = self._host_step(g["ev"], g["counts"], g["offs_h"])
+                    return st
         else:
-            out, at, cts = commit(None, False)
+            final_ctl = None
+        if background and m:
+            # the real commit on a worker thread; its results are read by finish_routed
+            if R.is_cuda:
+                torch.cuda.current_stream(R.device).synchronize()
+            box = {}
+
+            def run():
+                try:
+                    box["rc"] = self.backend.create_transfers_routed_tensors(
+                        sub_counts, Rf, ts_r, final_ctl, False, results, sync_inputs=False)
+                except BaseException as e:  # noqa: BLE001 -- re-raised by finish_routed
+                    box["error"] = e
+            st.thread = threading.Thread(target=run)
+            st.thread.start()
+            st.box, st.decode, st.offs = box, decode, offs
+            return st
+        out, at, cts = commit(final_ctl, False)
+        st.out, st.at, st.cts = out, at, cts
         clock("commit_ms")
+        return st
+
+    def finish_routed(self, st):
+        """Phase 3: the owner commit's results, the node's commit timestamp, replies back
+        to their sources.  Returns this rank's replies."""
+        torch = self.comm.torch
+        clock = self._clock()
+        if st.replies is not None:
+            return st.replies
+        if st.thread is not None:
+            st.thread.join()
+            if "error" in st.box:
+                raise st.box["error"]
+            rc, cts = st.box["rc"]
+            st.out, st.at, st.cts = st.decode(rc, cts, st.offs)
+            st.thread = None
+        g = st.__dict__
+        dev, W, m, S, glob, g0, counts = g["dev"], g["W"], g["m"], g["S"], g["glob"], g["g0"], g["counts"]
+        out, at, cts = st.out, st.at, st.cts
         # the node's commit timestamp and whether any owner has replies, in one all-gather
         fin = torch.tensor([len(at), cts if m else self.backend.commit_timestamp()], dtype=torch.int64, device=dev)
         allfin = [torch.empty_like(fin) for _ in range(W)]

@@ -98,6 +98,7 @@ struct tbgpu_ctx {
     int* status = nullptr;
     u32* h_counters = nullptr;  // pinned
     u32* h_counts = nullptr;    // pinned, bmax
+    u8* h_res = nullptr;        // pinned, nmax * 8: a chunk's replies for host-buffer calls
     u64* h_stage_ts = nullptr;  // pinned, bmax
     u32* h_stage_start = nullptr;  // pinned, bmax + 1
     // fast path (fast.hip)
@@ -235,6 +236,7 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     HIP_CHECK(hipHostMalloc((void**)&c->h_pc, 2 * PC_RING * sizeof(u32), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc((void**)&c->h_base, 8 * sizeof(u64), hipHostMallocDefault));  // [4..5]: a uint4
     HIP_CHECK(hipHostMalloc((void**)&c->h_counters, CNT_COUNT * sizeof(u32), hipHostMallocDefault));
+    HIP_CHECK(hipHostMalloc((void**)&c->h_res, c->nmax * 8 + 8, hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc((void**)&c->h_counts, c->bmax * sizeof(u32), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc((void**)&c->h_stage_ts, c->bmax * sizeof(u64), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc((void**)&c->h_stage_start, (c->bmax + 1) * sizeof(u32), hipHostMallocDefault));
@@ -381,6 +383,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     if (c->h_pc) (void)hipHostFree(c->h_pc);
     if (c->h_base) (void)hipHostFree(c->h_base);
     if (c->h_rc) (void)hipHostFree(c->h_rc);
+    if (c->h_res) (void)hipHostFree(c->h_res);
     for (hipEvent_t e : c->prof_pool) (void)hipEventDestroy(e);
     (void)hipEventDestroy(c->ev0);
     (void)hipEventDestroy(c->ev1);
@@ -407,6 +410,10 @@ static void refresh_bases(tbgpu_ctx* c) {
 }
 
 static void set_base(tbgpu_ctx* c, int k, u64 v) {
+    if (v == 0) {  // (the common reset: no staging, no round trip)
+        HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)(c->T.base + k), 0, 2, c->stream));
+        return;
+    }
     c->h_base[3] = v;  // staged through pinned memory (async copy), then waited for
     HIP_CHECK(hipMemcpyAsync(c->T.base + k, c->h_base + 3, sizeof(u64), hipMemcpyHostToDevice, c->stream));
     HIP_CHECK(hipStreamSynchronize(c->stream));
@@ -457,17 +464,17 @@ static void upload_batches(tbgpu_ctx* c, const uint64_t* timestamps, const uint3
 }
 
 // Device replies are concatenated across the chunk's batches; the host C-ABI
-// places batch b's reply at the batch's event offset.  (The chunk is complete.)
+// places batch b's reply at the batch's event offset.  The caller has copied them
+// back into the pinned staging buffer h_res (the chunk is complete).
 static void copy_results_to_batches(tbgpu_ctx* c, u32 nb, const std::vector<u32>& starts, const u32* counts,
                                     u8* dst_chunk) {
     u64 total = 0;
     for (u32 b = 0; b < nb; b++) total += counts[b];
     if (total == 0) return;
-    std::vector<u8> tmp(total * 8);
-    HIP_CHECK(hipMemcpy(tmp.data(), c->res_buf, total * 8, hipMemcpyDeviceToHost));
+    const u8* tmp = c->h_res;  // copied back with the chunk's counts
     u64 off = 0;
     for (u32 b = 0; b < nb; b++) {
-        memcpy(dst_chunk + (u64)starts[b] * 8, tmp.data() + off * 8, (u64)counts[b] * 8);
+        memcpy(dst_chunk + (u64)starts[b] * 8, tmp + off * 8, (u64)counts[b] * 8);
         off += counts[b];
     }
 }
@@ -836,6 +843,8 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         }
         HIP_CHECK(hipMemcpyAsync(c->h_rc + b0, c->counts, nb * sizeof(u32), hipMemcpyDeviceToHost, c->stream));
         if (!dst_device) {
+            // the chunk's replies (at most one per event) come back with its counts: one round trip
+            HIP_CHECK(hipMemcpyAsync(c->h_res, c->res_buf, (u64)n * 8, hipMemcpyDeviceToHost, c->stream));
             HIP_CHECK(hipStreamSynchronize(c->stream));
             copy_results_to_batches(c, nb, starts, c->h_rc + b0, (u8*)(results + ev_off));
         }
@@ -846,11 +855,15 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         events += n;
         b0 = b1;
     }
+    // the device cursors come back with the call's end (no extra round trip)
+    HIP_CHECK(hipMemcpyAsync(c->h_base, c->T.base, 4 * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
     HIP_CHECK(hipEventRecord(c->ev1, c->stream));
     HIP_CHECK(hipEventSynchronize(c->ev1));
     float ms = 0;
     HIP_CHECK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
-    refresh_bases(c);
+    c->n_rows = c->h_base[BASE_ROWS];
+    c->n_hist = c->h_base[BASE_HIST];
+    c->rows_hi = c->n_rows;
     u64 total = 0;
     for (u32 b = 0; b < nb_total; b++) total += c->h_rc[b];
     memcpy(result_counts, c->h_rc, nb_total * sizeof(u32));
@@ -1113,6 +1126,10 @@ static uint64_t accounts_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t
                 HIP_CHECK(hipMemcpyAsync(results + total, c->res_buf, chunk_total * 8, hipMemcpyDeviceToDevice,
                                          c->stream));
         } else {
+            if (chunk_total) {
+                HIP_CHECK(hipMemcpyAsync(c->h_res, c->res_buf, chunk_total * 8, hipMemcpyDeviceToHost, c->stream));
+                HIP_CHECK(hipStreamSynchronize(c->stream));
+            }
             copy_results_to_batches(c, nb, starts, result_counts + b0, (u8*)(results + ev_off));
         }
         total += chunk_total;

@@ -39,6 +39,28 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# stdout carries exactly one line, the result: whatever the libraries print there
+# (RCCL's version banner, gloo's connection notes) is sent to stderr instead
+_RESULT_FD = None
+
+
+def _claim_stdout():
+    global _RESULT_FD
+    if _RESULT_FD is None:
+        sys.stdout.flush()
+        _RESULT_FD = os.dup(1)
+        os.dup2(2, 1)
+
+
+def emit(line: dict):
+    data = (json.dumps(line) + "\n").encode()
+    if _RESULT_FD is None:
+        sys.stdout.write(data.decode())
+        sys.stdout.flush()
+    else:
+        os.write(_RESULT_FD, data)
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -284,7 +306,7 @@ def routed_bench(args, rank, world, local_rank, torch, dist, backend="nccl"):
                                   "(partition, all-to-all, commit and replies inside the time)"},
             "cpu_baseline": None,
         }
-        print(json.dumps(line), flush=True)
+        emit(line)
     eng.close()
     dist.destroy_process_group()
 
@@ -355,6 +377,7 @@ def main():
                     help="after the timed region, replay the same stream through the CPU oracle and compare "
                          "every reply and the final state bit for bit (configs 1-4)")
     args = ap.parse_args()
+    _claim_stdout()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -651,7 +674,7 @@ def main():
             "queries": queries,
             "verify": verify,
         }
-        print(json.dumps(line), flush=True)
+        emit(line)
     eng.close()
     if world > 1:
         dist.destroy_process_group()

@@ -338,27 +338,44 @@ uint64_t tbgpu_create_transfers_routed_device(tbgpu_ctx* ctx, uint32_t batch_cou
                                               const void* ctl_device, int dry_run, void* results_device,
                                               uint32_t* result_counts, uint64_t* commit_timestamp);
 
+/* The 8-byte record that travels with each routed event (tbgpu_route_scatter): */
+#define TBGPU_ROUTE_REC_POS 0x1FFFull        /* bits 0-12: the event's index in its batch */
+#define TBGPU_ROUTE_REC_SPAN (1ull << 13)    /* its linked chain has members on several owners */
+#define TBGPU_ROUTE_REC_LAST (1ull << 14)    /* it ends its chain (not linked, or last of its batch) */
+#define TBGPU_ROUTE_REC_CS_SHIFT 15          /* bits 15-27: index of its chain's first member */
+#define TBGPU_ROUTE_REC_CS_MASK 0x1FFFull
+#define TBGPU_ROUTE_REC_BATCH_SHIFT 32       /* bits 32-63: global batch number */
+
 /* The send side of a routed step (tigerbeetle_amd/shard.py): this rank's client
- * batches (`counts`, prepare timestamps `batch_timestamps`, global number of the
- * first one `first_global_batch`), events in device memory, are written to
- * `send_events_device` (n * 128 B) owner-major -- owner = ledger % world -- in event
- * order within an owner, each with a 32-byte record in `send_sides_device` (n * 32 B):
- * {event timestamp, global batch << 32 | index, global batch << 32 | index of its
- * chain's first member, bit 0: the chain spans owners | bit 1: the event ends its
- * chain}.  `send_counts[world]` (host) receives the events per owner; when not NULL,
- * `send_batch_counts[world * batch_count]` the events per (owner, batch) and
- * `send_span_counts[world]` the events per owner whose chain spans owners.  world <= 256.
- * Returns 0, or -22 for a bad argument.  Synchronous. */
+ * batches (`counts`, each <= 8192 events, prepare timestamps `batch_timestamps`,
+ * global number of the first one `first_global_batch`), events in device memory,
+ * are written to `send_events_device` (n * 128 B) owner-major -- owner = ledger %
+ * world -- in event order within an owner, each with an 8-byte record
+ * (TBGPU_ROUTE_REC_*) in `send_records_device` (n * 8 B).  `send_counts[world]`
+ * (host) receives the events per owner; when not NULL, `send_batch_counts[world *
+ * batch_count]` the events per (owner, batch) and `send_span_counts[world]` the
+ * events per owner whose chain spans owners.  world <= 256.  Returns 0, or -22 for
+ * a bad argument.  Synchronous. */
 /* One pass over a routed step's local events (device memory) deciding whether the
  * device path applies: out[0] min id (low word), out[1] max id (low word), out[2]
  * bit 0: an id not above its predecessor, bit 1: an id with a high word or zero,
  * bit 2: a post/void, bit 3: an amount of 2^64 or more; out[3], out[4]: the sum of
  * the amounts (low, high word).  Returns 0.  Synchronous. */
 int tbgpu_route_stats(tbgpu_ctx* ctx, const void* events_device, uint64_t count, uint64_t* out);
+/* tbgpu_route_stats and the first pass of tbgpu_route_scatter (each event's owner
+ * and rank) in one pass over the events; a tbgpu_route_scatter of the same events
+ * and world that follows skips that pass.  Returns 0, or -22.  Synchronous. */
+int tbgpu_route_prepare(tbgpu_ctx* ctx, uint32_t world, const void* events_device, uint64_t count, uint64_t* out);
 int tbgpu_route_scatter(tbgpu_ctx* ctx, uint32_t world, uint32_t batch_count, const uint32_t* counts,
                         const uint64_t* batch_timestamps, uint64_t first_global_batch, const void* events_device,
-                        void* send_events_device, void* send_sides_device, uint64_t* send_counts,
+                        void* send_events_device, void* send_records_device, uint64_t* send_counts,
                         uint32_t* send_batch_counts, uint32_t* send_span_counts);
+/* The owner side: event timestamps from received records, timestamps[i] =
+ * ts_base[batch of record i] + index + 1 with ts_base[g] = T_g - n_g of global batch
+ * g (src/vsr/replica.zig:5148-5157; `batches` entries, device memory).  Returns 0,
+ * or -22 when a record names a batch >= batches.  Synchronous. */
+int tbgpu_route_unpack(tbgpu_ctx* ctx, const void* records_device, uint64_t count, const void* ts_base_device,
+                       uint64_t batches, void* timestamps_device);
 
 /* Copy committed transfers of another shard into this ctx's transfer table and id
  * index, without balance or posted effects: the `exists` comparisons of

@@ -63,14 +63,26 @@ def test_route_scatter_matches_torch_partition():
     try:
         for W in (1, 2, 3, 8, 256):
             e_t, s_t, c_t, b_t, p_t = partition_torch(torch, ev, counts, bts, 5, W, dev, detail=True)
-            e_n = torch.empty((n, 128), dtype=torch.uint8, device=dev)
-            s_n = torch.empty((n, 4), dtype=torch.int64, device=dev)
-            c_n, b_n, p_n = eng.route_scatter(W, counts, bts, 5, ev, e_n, s_n, detail=True)
-            assert c_n.tolist() == c_t.cpu().tolist(), W
-            assert b_n.tolist() == b_t.cpu().tolist(), W
-            assert p_n.tolist() == p_t.cpu().tolist(), W
-            assert torch.equal(e_n, e_t), W
-            assert torch.equal(s_n, s_t), W
+            # the scatter on its own, and after tbgpu_route_prepare ranked the events
+            for prepared in (False, True):
+                if prepared:
+                    eng.route_stats(ev, n, world=W)
+                e_n = torch.empty((n, 128), dtype=torch.uint8, device=dev)
+                s_n = torch.empty(n, dtype=torch.int64, device=dev)
+                c_n, b_n, p_n = eng.route_scatter(W, counts, bts, 5, ev, e_n, s_n, detail=True)
+                assert c_n.tolist() == c_t.cpu().tolist(), (W, prepared)
+                assert b_n.tolist() == b_t.cpu().tolist(), (W, prepared)
+                assert p_n.tolist() == p_t.cpu().tolist(), (W, prepared)
+                assert torch.equal(e_n, e_t), (W, prepared)
+                assert torch.equal(s_n, s_t), (W, prepared)
+        # the owner side: timestamps from the records (global batches 5.. of this rank)
+        e_t, s_t, _ = partition_torch(torch, ev, counts, bts, 5, 3, dev)
+        tsb = torch.tensor([0] * 5 + [int(b) - c for b, c in zip(bts, counts)], dtype=torch.int64, device=dev)
+        ts_n = torch.empty(n, dtype=torch.int64, device=dev)
+        eng.route_unpack(s_t, tsb, ts_n)
+        assert torch.equal(ts_n, tsb[s_t >> 32] + (s_t & 0x1FFF) + 1)
+        with pytest.raises(ValueError):
+            eng.route_unpack(s_t, tsb[:7], ts_n)  # a record of batch 12 > the table
     finally:
         eng.close()
 
@@ -99,10 +111,11 @@ def test_route_stats_matches_numpy():
             if pv:
                 t["flags"][n - 1] = 4
             ev = torch.from_numpy(t.view(np.uint8).copy()).to("cuda:0")
-            mn, mx, mo, ids_ok, has_pv, has_big, asum = eng.route_stats(ev, n)
-            assert (mn, mx) == (int(ids.min()), int(ids.max()))
-            assert mo == mono and ids_ok and has_pv == pv and has_big == big
             want = sum(int(x) for x in t["amount_lo"]) + (sum(int(x) for x in t["amount_hi"]) << 64)
-            assert asum == want % (1 << 128)
+            for world in (0, 1, 5):  # tbgpu_route_stats, and tbgpu_route_prepare's fused pass
+                mn, mx, mo, ids_ok, has_pv, has_big, asum = eng.route_stats(ev, n, world=world)
+                assert (mn, mx) == (int(ids.min()), int(ids.max())), world
+                assert mo == mono and ids_ok and has_pv == pv and has_big == big, world
+                assert asum == want % (1 << 128), world
     finally:
         eng.close()

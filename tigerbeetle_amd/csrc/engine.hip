@@ -126,6 +126,12 @@ struct tbgpu_ctx {
     u64* ro_counts = nullptr;
     u32* ro_bcount = nullptr;  // [256] spanning counts per owner, then [world * batches] per (owner, batch)
     u64 ro_bc_cap = 0;
+    u64* ro_spart = nullptr;  // rt_rank's per-workgroup eligibility records
+    struct {
+        const void* events;
+        u64 n;
+        u32 world;
+    } ro_ranked{};  // what tbgpu_route_prepare ranked last (tbgpu_route_scatter skips that pass)
     const u64* rt_ev_ts = nullptr;
     const u8* rt_ctl = nullptr;
     bool rt_dry = false;
@@ -358,7 +364,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     // Free every device allocation by walking the struct's pointers.
     for (void* p : {(void*)c->ro_orank, (void*)c->ro_blk, (void*)c->ro_bstart, (void*)c->ro_bts, (void*)c->ro_counts,
-                    (void*)c->ro_bcount})
+                    (void*)c->ro_bcount, (void*)c->ro_spart})
         if (p) (void)hipFree(p);
     void* ptrs[] = {c->T.dense, c->T.acc, c->T.aidx, c->T.xrows, c->T.xful, c->T.xidx, c->T.hrows, c->T.commit_ts, c->T.idr, c->T.big, c->ev_buf,
                     c->b_start, c->b_ts, c->ts, c->cs, c->ce, c->sres, c->dslot, c->cslot, c->pre_e, c->pre_p,
@@ -974,33 +980,62 @@ extern "C" int tbgpu_route_stats(tbgpu_ctx* c, const void* events_device, uint64
 }
 void route_scatter(const Transfer* ev, u64 n, u32 world, u32 nb, const u32* b_start, const u64* b_ts, u64 g0,
                    uint2* orank, u32* blk, u64* counts, Transfer* out_ev, u64* out_side, u32* bcount, u32* scount,
-                   hipStream_t stream);
+                   bool ranked, hipStream_t stream);
+void route_rank(const Transfer* ev, u64 n, u32 world, uint2* orank, u32* blk, u64* part, u64* stats,
+                hipStream_t stream);
+void route_unpack(const u64* rec, u64 n, const u64* ts_base, u64 batches, u64* ts, u32* error, hipStream_t stream);
 
-extern "C" int tbgpu_route_scatter(tbgpu_ctx* c, uint32_t world, uint32_t batch_count, const uint32_t* counts,
-                                   const uint64_t* batch_timestamps, uint64_t first_global_batch,
-                                   const void* events_device, void* send_events_device, void* send_sides_device,
-                                   uint64_t* send_counts, uint32_t* send_batch_counts, uint32_t* send_span_counts) {
-    HIP_CHECK(hipSetDevice(c->device));
-    if (world == 0 || world > 256) return -22;
-    std::vector<u32> starts(batch_count + 1, 0);
-    for (u32 b = 0; b < batch_count; b++) starts[b + 1] = starts[b] + counts[b];
-    const u64 n = starts[batch_count];
+static void route_capacity(tbgpu_ctx* c, u32 world, u32 batch_count, u64 n) {
     const u64 nblk = route_block_count(n);
     if (n > c->ro_cap || world * std::max<u64>(nblk, 1) > c->ro_bcap || batch_count + 1 > c->ro_cap + 2 ||
         (u64)world * batch_count > c->ro_bc_cap) {
+        HIP_CHECK(hipStreamSynchronize(c->route_stream));
         for (void* p : {(void*)c->ro_orank, (void*)c->ro_blk, (void*)c->ro_bstart, (void*)c->ro_bts, (void*)c->ro_counts,
-                        (void*)c->ro_bcount})
+                        (void*)c->ro_bcount, (void*)c->ro_spart})
             if (p) HIP_CHECK(hipFree(p));
-        c->ro_cap = std::max<u64>(n, batch_count + 1);
+        c->ro_cap = std::max<u64>(std::max<u64>(n, batch_count + 1), c->ro_cap);
+        HIP_CHECK(hipMalloc((void**)&c->ro_spart, 5 * (route_block_count(c->ro_cap) + 1) * sizeof(u64)));
         c->ro_bcap = 256ull * std::max<u64>(route_block_count(c->ro_cap), 1);
         HIP_CHECK(hipMalloc((void**)&c->ro_orank, c->ro_cap * sizeof(uint2)));
         HIP_CHECK(hipMalloc((void**)&c->ro_blk, c->ro_bcap * sizeof(u32)));
         HIP_CHECK(hipMalloc((void**)&c->ro_bstart, (c->ro_cap + 3) * sizeof(u32)));
         HIP_CHECK(hipMalloc((void**)&c->ro_bts, (c->ro_cap + 3) * sizeof(u64)));
         HIP_CHECK(hipMalloc((void**)&c->ro_counts, 256 * sizeof(u64)));
-        c->ro_bc_cap = std::max<u64>((u64)world * batch_count, 256ull * 64);
+        c->ro_bc_cap = std::max<u64>((u64)world * std::max<u32>(batch_count, 1), 256ull * 64);
         HIP_CHECK(hipMalloc((void**)&c->ro_bcount, (c->ro_bc_cap + 256) * sizeof(u32)));
+        c->ro_ranked = {};
     }
+}
+
+extern "C" int tbgpu_route_prepare(tbgpu_ctx* c, uint32_t world, const void* events_device, uint64_t count,
+                                   uint64_t* out) {
+    HIP_CHECK(hipSetDevice(c->device));
+    if (world == 0 || world > 256) return -22;
+    route_capacity(c, world, 0, count);
+    route_rank((const Transfer*)events_device, count, world, c->ro_orank, c->ro_blk, c->ro_spart, c->rt_stats,
+               c->route_stream);
+    HIP_CHECK(hipMemcpyAsync(out, c->rt_stats, 5 * sizeof(u64), hipMemcpyDeviceToHost, c->route_stream));
+    HIP_CHECK(hipStreamSynchronize(c->route_stream));
+    c->ro_ranked = {events_device, count, world};
+    return 0;
+}
+
+extern "C" int tbgpu_route_scatter(tbgpu_ctx* c, uint32_t world, uint32_t batch_count, const uint32_t* counts,
+                                   const uint64_t* batch_timestamps, uint64_t first_global_batch,
+                                   const void* events_device, void* send_events_device, void* send_records_device,
+                                   uint64_t* send_counts, uint32_t* send_batch_counts, uint32_t* send_span_counts) {
+    HIP_CHECK(hipSetDevice(c->device));
+    if (world == 0 || world > 256) return -22;
+    std::vector<u32> starts(batch_count + 1, 0);
+    for (u32 b = 0; b < batch_count; b++) {
+        if (counts[b] > TBGPU_ROUTE_REC_POS + 1) return -22;  // an index must fit its record field
+        starts[b + 1] = starts[b] + counts[b];
+    }
+    const u64 n = starts[batch_count];
+    route_capacity(c, world, batch_count, n);
+    // tbgpu_route_prepare ranked these very events for this world: skip that pass
+    const bool ranked = c->ro_ranked.events == events_device && c->ro_ranked.n == n && c->ro_ranked.world == world;
+    c->ro_ranked = {};
     if (n == 0) {
         for (u32 o = 0; o < world; o++) send_counts[o] = 0;
         if (send_batch_counts) memset(send_batch_counts, 0, (u64)world * batch_count * sizeof(u32));
@@ -1011,8 +1046,8 @@ extern "C" int tbgpu_route_scatter(tbgpu_ctx* c, uint32_t world, uint32_t batch_
                              c->route_stream));
     HIP_CHECK(hipMemcpyAsync(c->ro_bts, batch_timestamps, batch_count * sizeof(u64), hipMemcpyHostToDevice, c->route_stream));
     route_scatter((const Transfer*)events_device, n, world, batch_count, c->ro_bstart, c->ro_bts, first_global_batch,
-                  c->ro_orank, c->ro_blk, c->ro_counts, (Transfer*)send_events_device, (u64*)send_sides_device,
-                  c->ro_bcount + 256, c->ro_bcount, c->route_stream);
+                  c->ro_orank, c->ro_blk, c->ro_counts, (Transfer*)send_events_device, (u64*)send_records_device,
+                  c->ro_bcount + 256, c->ro_bcount, ranked, c->route_stream);
     HIP_CHECK(hipMemcpyAsync(send_counts, c->ro_counts, world * sizeof(u64), hipMemcpyDeviceToHost, c->route_stream));
     if (send_batch_counts)
         HIP_CHECK(hipMemcpyAsync(send_batch_counts, c->ro_bcount + 256, (u64)world * batch_count * sizeof(u32),
@@ -1021,6 +1056,19 @@ extern "C" int tbgpu_route_scatter(tbgpu_ctx* c, uint32_t world, uint32_t batch_
         HIP_CHECK(hipMemcpyAsync(send_span_counts, c->ro_bcount, world * sizeof(u32), hipMemcpyDeviceToHost, c->route_stream));
     HIP_CHECK(hipStreamSynchronize(c->route_stream));
     return 0;
+}
+
+extern "C" int tbgpu_route_unpack(tbgpu_ctx* c, const void* records_device, uint64_t count,
+                                  const void* batch_ts_base_device, uint64_t batches, void* timestamps_device) {
+    HIP_CHECK(hipSetDevice(c->device));
+    u32* err = (u32*)(c->rt_stats + 6);
+    HIP_CHECK(hipMemsetAsync(err, 0, sizeof(u32), c->route_stream));
+    route_unpack((const u64*)records_device, count, (const u64*)batch_ts_base_device, batches, (u64*)timestamps_device,
+                 err, c->route_stream);
+    u32 e = 0;
+    HIP_CHECK(hipMemcpyAsync(&e, err, sizeof(u32), hipMemcpyDeviceToHost, c->route_stream));
+    HIP_CHECK(hipStreamSynchronize(c->route_stream));
+    return e ? -22 : 0;
 }
 
 extern "C" void tbgpu_advance_commit_timestamp(tbgpu_ctx* c, uint64_t timestamp) {

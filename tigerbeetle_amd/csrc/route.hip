@@ -4,15 +4,17 @@
 // world: a valid transfer has dr.ledger == cr.ledger == t.ledger,
 // src/state_machine.zig:1280-1281).  Before the all-to-all every event is placed in
 // an owner-major send buffer, in event order within an owner (each owner commits
-// its sub-batches in global order), beside a 32-byte side record carrying what
-// `execute` derives from the event's place in its batch (:1018-1035):
-//   [0] timestamp T - n + index + 1 of its batch,
-//   [1] global batch << 32 | index,
-//   [2] global batch << 32 | index of its chain's first member (the chain key),
-//   [3] bit 0: the chain has members on more than one owner, bit 1: the event ends
-//       its chain (not linked, or last of its batch).
-// Three launches: classify + stable rank within the workgroup, an exclusive scan of
-// the (owner, workgroup) counts, scatter.  Pure data movement: HBM-bound.
+// its sub-batches in global order), beside an 8-byte side record carrying what
+// `execute` derives from the event's place in its batch (:1018-1035), packed as
+// include/tbgpu.h TBGPU_ROUTE_REC_* describes:
+//   global batch << 32 | chain start (index of the chain's first member) << 15 |
+//   ends its chain << 14 | chain spans owners << 13 | index in its batch.
+// The owner derives the timestamp T - n + index + 1 from the batch's (T, n), which
+// every rank knows (tbgpu_route_unpack), so the all-to-all moves 136 bytes per
+// event, not 160.
+// Launches: classify + stable rank within the workgroup (with the step's
+// eligibility figures in the same pass over the events), an exclusive scan of the
+// (owner, workgroup) counts, scatter.  Pure data movement: HBM-bound.
 #include "common.h"
 
 namespace {
@@ -36,7 +38,12 @@ struct RouteArgs {
     u64* out_side;        // [n * 4]
     u32* bcount;          // [world * nb] events per (owner, local batch)
     u32* scount;          // [world] events per owner whose chain spans owners
+    u64* stats;           // rt_rank: the eligibility figures of rt_stats (out[0..4]), or null
 };
+
+constexpr u64 REC_POS = TBGPU_ROUTE_REC_POS, REC_SPAN = TBGPU_ROUTE_REC_SPAN, REC_LAST = TBGPU_ROUTE_REC_LAST;
+constexpr int REC_CS_SHIFT = TBGPU_ROUTE_REC_CS_SHIFT;
+static_assert(TBGPU_ROUTE_REC_BATCH_SHIFT == 32, "record layout");
 
 __device__ __forceinline__ u32 rt_batch(const RouteArgs& A, u32 i) {
     u32 lo = 0, hi = A.nb;  // last b with b_start[b] <= i
@@ -49,15 +56,68 @@ __device__ __forceinline__ u32 rt_batch(const RouteArgs& A, u32 i) {
 
 __device__ __forceinline__ u32 rt_owner(const RouteArgs& A, u64 i) { return A.ev[i].ledger % A.world; }
 
+__device__ void rt_stats_block(u64 mn, u64 mx, u64 fl, u64 slo, u64 shi, u64* out, u64* part);
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __global__ __launch_bounds__(RT_THREADS) void rt_rank(RouteArgs A) {
     __shared__ u32 s_cnt[RT_WAVES][256];
+    // the wave's 64 events' id, amount and ledger|code|flags words, loaded eight lanes
+    // per row (coalesced: lane-per-row loads of 128-byte-strided rows ran 5x slower)
+    __shared__ uint4 s_pc[RT_WAVES][64][3];
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const u64 i = (u64)blockIdx.x * RT_THREADS + tid;
+    const u64 wbase = i - lane;
+    const bool v = i < A.n;
+    {
+        const uint4* rows = (const uint4*)A.ev;
+        const u32 piece = lane & 7;
+        const int slot = piece == 0 ? 0 : piece == 3 ? 1 : piece == 7 ? 2 : -1;
+        const int sl = A.stats ? slot : (piece == 7 ? 2 : -1);  // without the figures: the ledger word
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            const u32 k = (u32)r * 8 + (lane >> 3);
+            if (sl >= 0 && wbase + k < A.n) s_pc[w][k][sl] = rows[(wbase + k) * 8 + piece];
+        }
+    }
+    uint4 pidv = make_uint4(0, 0, 0, 0);
+    if (A.stats && lane == 0 && v && i > 0) pidv = *(const uint4*)&A.ev[i - 1].id;
     for (u32 o = tid; o < A.world; o += RT_THREADS)
         for (int k = 0; k < RT_WAVES; k++) s_cnt[k][o] = 0;
+    wave_lds_sync();
+    const uint4 lw = s_pc[w][lane][2];
+    const u64 lcf = v ? ((u64)lw.y << 32 | lw.x) : 0;  // bytes 112..119: ledger, code, flags
+    uint4 idv = make_uint4(0, 0, 0, 0), amv = idv;
+    if (A.stats && v) {
+        idv = s_pc[w][lane][0];
+        amv = s_pc[w][lane][1];
+    }
     __syncthreads();
-    const u64 i = (u64)blockIdx.x * RT_THREADS + tid;
-    const bool v = i < A.n;
-    const u32 own = v ? rt_owner(A, i) : NONE32;
+    const u32 own = v ? (u32)lcf % A.world : NONE32;
+    if (A.stats) {
+        const u64 lo = ((u64)idv.y << 32) | idv.x, hi = ((u64)idv.w << 32) | idv.z;
+        u64 plo = (u64)__shfl_up((unsigned long long)lo, 1), phi = (u64)__shfl_up((unsigned long long)hi, 1);
+        if (lane == 0) {
+            plo = ((u64)pidv.y << 32) | pidv.x;
+            phi = ((u64)pidv.w << 32) | pidv.z;
+        }
+        u64 mn = ~0ull, mx = 0, fl = 0, slo = 0, shi = 0;
+        if (v) {
+            mn = mx = lo;
+            if (hi != 0 || lo == 0) fl |= 2;
+            if (i > 0 && !(phi < hi || (phi == hi && plo < lo))) fl |= 1;
+            const u64 alo = ((u64)amv.y << 32) | amv.x, ahi = ((u64)amv.w << 32) | amv.z;
+            if (ahi) fl |= 8;
+            slo = alo;
+            shi = ahi;
+            if ((lcf >> 48) & (TF_POST | TF_VOID)) fl |= 4;
+        }
+        rt_stats_block(mn, mx, fl, slo, shi, nullptr, A.stats);  // per-workgroup records: rt_stats_fold
+    }
     // stable rank within the wave: one ballot per distinct owner present in the wave
     u32 rank = 0;
     u64 todo = __ballot(v);
@@ -80,34 +140,50 @@ __global__ __launch_bounds__(RT_THREADS) void rt_rank(RouteArgs A) {
     }
 }
 
-// Exclusive scan of blk (owner-major) in one workgroup, and the per-owner totals.
+// Exclusive scan of blk (owner-major) in one workgroup, and the per-owner totals:
+// tiles of 4096 words, four consecutive words per thread (coalesced), wave scans by
+// shuffles, the sixteen wave sums through LDS, a running carry.
 __global__ __launch_bounds__(1024) void rt_scan(RouteArgs A) {
-    __shared__ u64 s_part[1024];
+    __shared__ u32 wsum[16];
     const u64 total_n = (u64)A.world * A.nblk;
-    const u64 per = (total_n + 1023) / 1024;
-    const u64 b = threadIdx.x * per, e = min(total_n, b + per);
-    u64 sum = 0;
-    for (u64 k = b; k < e; k++) sum += A.blk[k];
-    s_part[threadIdx.x] = sum;
-    __syncthreads();
-    for (u32 off = 1; off < 1024; off <<= 1) {
-        const u64 x = threadIdx.x >= off ? s_part[threadIdx.x - off] : 0;
+    const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    u64 carry = 0;
+    for (u64 base = 0; base < total_n; base += 4096) {
+        const u64 k = base + (u64)tid * 4;
+        u32 v[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) v[j] = k + j < total_n ? A.blk[k + j] : 0u;
+        const u32 s = v[0] + v[1] + v[2] + v[3];
+        u32 x = s;  // inclusive over the wave
+        for (int off = 1; off < 64; off <<= 1) {
+            const u32 y = __shfl_up(x, off);
+            if (lane >= (u32)off) x += y;
+        }
+        if (lane == 63) wsum[wave] = x;
         __syncthreads();
-        s_part[threadIdx.x] += x;
+        if (wave == 0) {
+            u32 t = lane < 16 ? wsum[lane] : 0;
+            for (int off = 1; off < 16; off <<= 1) {
+                const u32 y = __shfl_up(t, off);
+                if (lane >= (u32)off) t += y;
+            }
+            if (lane < 16) wsum[lane] = t;
+        }
+        __syncthreads();
+        u32 run = (u32)carry + (wave ? wsum[wave - 1] : 0) + x - s;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (k + j < total_n) A.blk[k + j] = run;
+            run += v[j];
+        }
+        carry += wsum[15];
         __syncthreads();
     }
-    u64 run = s_part[threadIdx.x] - sum;  // exclusive
-    for (u64 k = b; k < e; k++) {
-        const u32 c = A.blk[k];
-        A.blk[k] = (u32)run;
-        run += c;
-    }
     __syncthreads();
-    const u64 all = s_part[1023];
-    for (u32 o = threadIdx.x; o < A.world; o += 1024) {
-        const u64 s = A.blk[(u64)o * A.nblk];
-        const u64 t = o + 1 < A.world ? A.blk[(u64)(o + 1) * A.nblk] : all;
-        A.counts[o] = t - s;
+    for (u32 o = tid; o < A.world; o += 1024) {
+        const u64 s0 = A.blk[(u64)o * A.nblk];
+        const u64 t = o + 1 < A.world ? A.blk[(u64)(o + 1) * A.nblk] : carry;
+        A.counts[o] = t - s0;
     }
 }
 
@@ -173,9 +249,23 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scatter(RouteArgs A) {
             todo &= ~mo;
         }
     }
-    ulonglong2* side = (ulonglong2*)&A.out_side[dst * 4];
-    side[0] = make_ulonglong2(A.b_ts[b] - nbatch + pos + 1, (g << 32) | pos);
-    side[1] = make_ulonglong2((g << 32) | (s - bs), (omin != omax ? 1ull : 0ull) | (last ? 2ull : 0ull));
+    A.out_side[dst] = (g << 32) | ((u64)(s - bs) << REC_CS_SHIFT) | (last ? REC_LAST : 0) |
+                      (omin != omax ? REC_SPAN : 0) | pos;
+}
+
+// Timestamps of received events from their side records: batch g's events get
+// ts_base[g] + index + 1, where ts_base[g] = T_g - n_g (src/vsr/replica.zig:5148-5157).
+__global__ __launch_bounds__(RT_THREADS) void rt_unpack(const u64* __restrict__ rec, u64 n,
+                                                        const u64* __restrict__ ts_base, u64 batches,
+                                                        u64* __restrict__ ts, u32* error) {
+    const u64 i = (u64)blockIdx.x * RT_THREADS + threadIdx.x;
+    if (i >= n) return;
+    const u64 r = rec[i], g = r >> 32;
+    if (g >= batches) {
+        atomicOr(error, 1u);
+        return;
+    }
+    ts[i] = ts_base[g] + (r & REC_POS) + 1;
 }
 
 // Eligibility of a step for the device path, in one pass over its events:
@@ -218,6 +308,16 @@ __global__ __launch_bounds__(RT_THREADS) void rt_stats(const Transfer* ev, u64 n
             }
         }
     }
+    rt_stats_block(mn, mx, fl, slo, shi, out, nullptr);
+}
+
+// The workgroup's eligibility figures, then one set of atomics per workgroup
+// (same-address atomics serialize: one set per wave cost more than the pass over
+// the rows), or, with `part`, the workgroup's record part[5 * block] for
+// rt_stats_fold (a grid of one workgroup per 256 events: 32k sets of atomics on five
+// words took 1.5 ms).  Every thread of the workgroup calls.
+__device__ void rt_stats_block(u64 mn, u64 mx, u64 fl, u64 slo, u64 shi, u64* out, u64* part) {
+    const u32 lane = threadIdx.x & 63;
     for (int off = 32; off > 0; off >>= 1) {
         mn = min(mn, (u64)__shfl_xor((unsigned long long)mn, off));
         mx = max(mx, (u64)__shfl_xor((unsigned long long)mx, off));
@@ -228,8 +328,6 @@ __global__ __launch_bounds__(RT_THREADS) void rt_stats(const Transfer* ev, u64 n
         shi += ohi + (t < slo ? 1 : 0);
         slo = t;
     }
-    // the workgroup's result, then one set of atomics per workgroup (same-address
-    // atomics serialize: one set per wave cost more than the pass over the rows)
     __shared__ u64 s_r[RT_THREADS / 64][5];
     const u32 w = threadIdx.x >> 6;
     if (lane == 0) {
@@ -245,6 +343,11 @@ __global__ __launch_bounds__(RT_THREADS) void rt_stats(const Transfer* ev, u64 n
             shi += s_r[k][4] + (t < slo ? 1 : 0);
             slo = t;
         }
+        if (part) {
+            u64* r = part + 5ull * blockIdx.x;
+            r[0] = mn; r[1] = mx; r[2] = fl; r[3] = slo; r[4] = shi;
+            return;
+        }
         atomicMin((unsigned long long*)&out[0], (unsigned long long)mn);
         atomicMax((unsigned long long*)&out[1], (unsigned long long)mx);
         if (fl) atomicOr((unsigned long long*)&out[2], (unsigned long long)fl);
@@ -253,6 +356,22 @@ __global__ __launch_bounds__(RT_THREADS) void rt_stats(const Transfer* ev, u64 n
             atomicAdd((unsigned long long*)&out[4], (unsigned long long)(shi + (old + slo < old ? 1 : 0)));
         }
     }
+}
+
+// The workgroup records of rt_rank into out[0..4]: one workgroup per 64 records,
+// each folding its records and adding them to out with one set of atomics.
+__global__ __launch_bounds__(RT_THREADS) void rt_stats_fold(const u64* __restrict__ part, u32 nblk, u64* out) {
+    u64 mn = ~0ull, mx = 0, fl = 0, slo = 0, shi = 0;
+    for (u32 b = blockIdx.x * 64 + threadIdx.x; threadIdx.x < 64 && b < nblk; b += (u32)gridDim.x * 64) {
+        const u64* r = part + 5ull * b;
+        mn = min(mn, r[0]);
+        mx = max(mx, r[1]);
+        fl |= r[2];
+        const u64 t = slo + r[3];
+        shi += r[4] + (t < slo ? 1 : 0);
+        slo = t;
+    }
+    rt_stats_block(mn, mx, fl, slo, shi, out, nullptr);
 }
 
 }  // namespace
@@ -266,9 +385,33 @@ void route_stats(const Transfer* ev, u64 n, u64* out, hipStream_t stream) {
 
 u64 route_block_count(u64 n) { return (n + RT_THREADS - 1) / RT_THREADS; }
 
+// rt_rank alone, with the eligibility figures (stats: 5 words, initialized here):
+// the first half of a routed step's send side; route_scatter(..., ranked = true)
+// completes it.
+// part: 5 words per workgroup (route_block_count(n) of them)
+void route_rank(const Transfer* ev, u64 n, u32 world, uint2* orank, u32* blk, u64* part, u64* stats,
+                hipStream_t stream) {
+    const u64 init[5] = {~0ull, 0, 0, 0, 0};
+    HIP_CHECK(hipMemcpyAsync(stats, init, sizeof init, hipMemcpyHostToDevice, stream));
+    RouteArgs A{};
+    A.ev = ev; A.n = n; A.world = world; A.orank = orank; A.blk = blk; A.nblk = (u32)route_block_count(n);
+    A.stats = part;
+    if (n) {
+        rt_rank<<<A.nblk, RT_THREADS, 0, stream>>>(A);
+        rt_stats_fold<<<std::min<u32>((A.nblk + 63) / 64, 256), RT_THREADS, 0, stream>>>(part, A.nblk, stats);
+    }
+    HIP_CHECK(hipGetLastError());
+}
+
+void route_unpack(const u64* rec, u64 n, const u64* ts_base, u64 batches, u64* ts, u32* error, hipStream_t stream) {
+    if (n) rt_unpack<<<(u32)((n + RT_THREADS - 1) / RT_THREADS), RT_THREADS, 0, stream>>>(rec, n, ts_base, batches,
+                                                                                          ts, error);
+    HIP_CHECK(hipGetLastError());
+}
+
 void route_scatter(const Transfer* ev, u64 n, u32 world, u32 nb, const u32* b_start, const u64* b_ts, u64 g0,
                    uint2* orank, u32* blk, u64* counts, Transfer* out_ev, u64* out_side, u32* bcount, u32* scount,
-                   hipStream_t stream) {
+                   bool ranked, hipStream_t stream) {
     RouteArgs A{};
     A.bcount = bcount;
     A.scount = scount;
@@ -277,7 +420,7 @@ void route_scatter(const Transfer* ev, u64 n, u32 world, u32 nb, const u32* b_st
     A.ev = ev; A.n = n; A.world = world; A.nb = nb; A.b_start = b_start; A.b_ts = b_ts; A.g0 = g0;
     A.orank = orank; A.blk = blk; A.nblk = (u32)route_block_count(n); A.counts = counts;
     A.out_ev = out_ev; A.out_side = out_side;
-    if (n) rt_rank<<<A.nblk, RT_THREADS, 0, stream>>>(A);
+    if (n && !ranked) rt_rank<<<A.nblk, RT_THREADS, 0, stream>>>(A);
     rt_scan<<<1, 1024, 0, stream>>>(A);
     if (n) rt_scatter<<<A.nblk, RT_THREADS, 0, stream>>>(A);
     HIP_CHECK(hipGetLastError());

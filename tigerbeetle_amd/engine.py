@@ -109,6 +109,10 @@ def lib():
     L.tbgpu_route_scatter.argtypes = [vp, u32, u32, vp, vp, u64, vp, vp, vp, vp, vp, vp]
     L.tbgpu_route_stats.restype = ctypes.c_int
     L.tbgpu_route_stats.argtypes = [vp, vp, u64, vp]
+    L.tbgpu_route_prepare.restype = ctypes.c_int
+    L.tbgpu_route_prepare.argtypes = [vp, u32, vp, u64, vp]
+    L.tbgpu_route_unpack.restype = ctypes.c_int
+    L.tbgpu_route_unpack.argtypes = [vp, vp, u64, vp, u64, vp]
     L.tbgpu_import_transfers.restype = ctypes.c_int
     L.tbgpu_import_transfers.argtypes = [vp, vp, u32]
     L.tbgpu_advance_commit_timestamp.argtypes = [vp, u64]
@@ -259,11 +263,12 @@ class Engine:
             self._L.tbgpu_import_transfers(self._h, _ptr(rows), len(rows))
 
     def route_scatter(self, world: int, counts, batch_timestamps, first_global_batch: int, events, send_events,
-                      send_sides, detail: bool = False):
+                      send_records, detail: bool = False):
         """The send side of a routed step (tbgpu_route_scatter): `events` (uint8 device
-        tensor, n*128 B) to owner-major `send_events` (n*128 B) with 32-byte records in
-        `send_sides` (n*32 B).  Returns the events per owner; with `detail`, also the
-        events per (owner, batch) and the spanning events per owner."""
+        tensor, n*128 B) to owner-major `send_events` (n*128 B) with 8-byte records
+        (TBGPU_ROUTE_REC_*, shard.py REC_*) in `send_records` (n int64).  Returns the
+        events per owner; with `detail`, also the events per (owner, batch) and the
+        spanning events per owner."""
         import torch
         torch.cuda.current_stream(events.device).synchronize()
         cs = np.ascontiguousarray(counts, dtype=np.uint32)
@@ -273,21 +278,39 @@ class Engine:
         sp = np.zeros(world, dtype=np.uint32)
         rc = self._L.tbgpu_route_scatter(self._h, world, len(cs), _ptr(cs), _ptr(ts), int(first_global_batch),
                                          ctypes.c_void_p(events.data_ptr()), ctypes.c_void_p(send_events.data_ptr()),
-                                         ctypes.c_void_p(send_sides.data_ptr()), _ptr(out), _ptr(bc), _ptr(sp))
+                                         ctypes.c_void_p(send_records.data_ptr()), _ptr(out), _ptr(bc), _ptr(sp))
         if rc != 0:
             raise ValueError(f"tbgpu_route_scatter failed ({rc})")
         return (out, bc[:, :len(cs)], sp) if detail else out
 
-    def route_stats(self, events, n: int):
+    def route_stats(self, events, n: int, world: int = 0):
         """tbgpu_route_stats over n events of a uint8 device tensor: (min id, max id,
-        monotone, plain ids, any post/void, any amount >= 2^64, amount sum)."""
+        monotone, plain ids, any post/void, any amount >= 2^64, amount sum).  With
+        `world`, tbgpu_route_prepare: the same figures from the pass that also ranks the
+        events for a route_scatter of them to `world` owners (which then skips it)."""
         import torch
         torch.cuda.current_stream(events.device).synchronize()
         out = np.zeros(5, dtype=np.uint64)
-        self._L.tbgpu_route_stats(self._h, ctypes.c_void_p(events.data_ptr()), int(n), _ptr(out))
+        if world:
+            rc = self._L.tbgpu_route_prepare(self._h, int(world), ctypes.c_void_p(events.data_ptr()), int(n), _ptr(out))
+            if rc != 0:
+                raise ValueError(f"tbgpu_route_prepare failed ({rc})")
+        else:
+            self._L.tbgpu_route_stats(self._h, ctypes.c_void_p(events.data_ptr()), int(n), _ptr(out))
         fl = int(out[2])
         return (int(out[0]), int(out[1]), not (fl & 1), not (fl & 2), bool(fl & 4), bool(fl & 8),
                 int(out[3]) | (int(out[4]) << 64))
+
+    def route_unpack(self, records, ts_base, timestamps) -> None:
+        """tbgpu_route_unpack: event timestamps (int64 device tensor) from received
+        records and the per-global-batch T - n table `ts_base` (int64 device tensor)."""
+        import torch
+        torch.cuda.current_stream(records.device).synchronize()
+        rc = self._L.tbgpu_route_unpack(self._h, ctypes.c_void_p(records.data_ptr()), int(records.numel()),
+                                        ctypes.c_void_p(ts_base.data_ptr()), int(ts_base.numel()),
+                                        ctypes.c_void_p(timestamps.data_ptr()))
+        if rc != 0:
+            raise ValueError("tbgpu_route_unpack: a record names an unknown batch")
 
     def advance_commit_timestamp(self, ts: int) -> None:
         self._L.tbgpu_advance_commit_timestamp(self._h, int(ts))

@@ -74,6 +74,23 @@ MAX_ROUNDS = 8     # dry rounds before the serial fallback (one cross-shard chai
 NB_GATHER = 2048   # batch counts per rank carried by the device step's first all-gather
 LIMITS = 2 | 4     # AccountFlags debits_must_not_exceed_credits | credits_must_not_exceed_debits
 BALANCING = 8 | 16  # TransferFlags balancing_debit | balancing_credit
+# The 8-byte record of a routed event (include/tbgpu.h TBGPU_ROUTE_REC_*):
+# global batch << 32 | chain start << 15 | ends its chain << 14 | chain spans owners << 13 | index
+REC_POS = 0x1FFF
+REC_SPAN = 1 << 13
+REC_LAST = 1 << 14
+REC_CS_SHIFT = 15
+REC_CS_MASK = 0x1FFF
+
+
+def rec_position(rec):
+    """global batch << 32 | index in the batch (the event's place in the global order)"""
+    return ((rec >> 32) << 32) | (rec & REC_POS)
+
+
+def rec_chain_key(rec):
+    """global batch << 32 | index of the chain's first member"""
+    return ((rec >> 32) << 32) | ((rec >> REC_CS_SHIFT) & REC_CS_MASK)
 
 # directory replies
 NEW, EXISTS, DUP, PEND, PEND_NONE, PEND_HAZARD = range(6)
@@ -298,17 +315,19 @@ class ShardedStateMachine:
         ev = events.view(torch.uint8).reshape(-1)[:n * 128]
         w32 = ev.view(torch.int32).view(n, 32)
         w64 = ev.view(torch.int64).view(n, 16)
-        flags = (w32[:, 29] >> 16) & 0xFFFF
         id_lo, id_hi = w64[:, 0], w64[:, 1]
         # eligibility, one small all-gather: [n, min id, max id, monotone, plain, amount bound in 2^32 units]
+        native = n and ev.is_cuda and hasattr(self.backend, "route_scatter")
         if n and ev.is_cuda and hasattr(self.backend, "route_stats"):
-            # one pass of the engine's kernel (csrc/route.hip) instead of the torch reductions
-            mn, mx, mono, ids_ok, pv, big, asum = self.backend.route_stats(ev, n)
+            # one pass of the engine's kernel (csrc/route.hip) instead of the torch reductions;
+            # the same pass ranks the events for the scatter below
+            mn, mx, mono, ids_ok, pv, big, asum = self.backend.route_stats(ev, n, world=W if native else 0)
             ok_ids = ids_ok and mx < (1 << 63)  # the all-gather below carries int64
             units = (1 << 62) if big else (asum >> 32) + 2
             st = [n, mn if ok_ids else 0, mx if ok_ids else 0, int(mono), int(ok_ids and not pv), units]
         elif n:
             mono = bool((id_lo[1:] > id_lo[:-1]).all()) if n > 1 else True
+            flags = (w32[:, 29] >> 16) & 0xFFFF
             plain = bool(((flags & POST_VOID) == 0).all() & (id_hi == 0).all() & (id_lo > 0).all())
             a = w64[:, 6].double()
             a = torch.where(a < 0, a + 2.0**64, a)
@@ -351,12 +370,11 @@ class ShardedStateMachine:
             T.append(self.prepare_timestamp)
         g0 = sum(len(cl) for cl in counts_all[:me])
         clock("order_ms")
-        native = n and ev.is_cuda and hasattr(self.backend, "route_scatter")
         nb_me = len(counts)
         if native:
             # the engine's scatter kernels (csrc/route.hip): same layout as partition_torch
             ev_s = torch.empty((n, 128), dtype=torch.uint8, device=dev)
-            side_s = torch.empty((n, 4), dtype=torch.int64, device=dev)
+            side_s = torch.empty(n, dtype=torch.int64, device=dev)
             sc, bc, spc = self.backend.route_scatter(W, list(map(int, counts)), T[g0:g0 + nb_me], g0, ev, ev_s,
                                                      side_s, detail=True)
         elif n:
@@ -366,16 +384,19 @@ class ShardedStateMachine:
         else:
             sc, bc, spc = np.zeros(W, np.int64), np.zeros((W, 0), np.int64), np.zeros(W, np.int64)
             ev_s = torch.zeros((0, 128), dtype=torch.uint8, device=dev)
-            side_s = torch.zeros((0, 4), dtype=torch.int64, device=dev)
+            side_s = torch.zeros(0, dtype=torch.int64, device=dev)
         clock("partition_ms")
         # per owner: [events, spanning events, all spanning events sent, events per batch...]
         meta = np.concatenate([np.asarray(sc, np.int64)[:, None], np.asarray(spc, np.int64)[:, None],
                                np.full((W, 1), int(np.sum(spc)), np.int64), np.asarray(bc, np.int64)], axis=1)
         nbs = [len(cl) for cl in counts_all]
-        rmeta = torch.empty(sum(3 + k for k in nbs), dtype=torch.int64, device=dev)
-        self.comm.dist.all_to_all_single(rmeta, torch.from_numpy(meta.reshape(-1)).to(dev), [3 + k for k in nbs],
-                                         [3 + nb_me] * W, group=self.comm.group)
-        rmeta = rmeta.cpu().numpy()
+        if W > 1:
+            rmeta = torch.empty(sum(3 + k for k in nbs), dtype=torch.int64, device=dev)
+            self.comm.dist.all_to_all_single(rmeta, torch.from_numpy(meta.reshape(-1)).to(dev), [3 + k for k in nbs],
+                                             [3 + nb_me] * W, group=self.comm.group)
+            rmeta = rmeta.cpu().numpy()
+        else:
+            rmeta = meta.reshape(-1)
         sl, rl, sub_counts, n_span, span_sent = [int(x) for x in sc], [], [], 0, 0
         off = 0
         for k in nbs:
@@ -386,20 +407,25 @@ class ShardedStateMachine:
             sub_counts += [int(c) for c in row[3:] if c]
             off += 3 + k
         m = int(sum(rl))
-        R = torch.empty((m, 128), dtype=torch.uint8, device=dev)
-        S = torch.empty((m, 4), dtype=torch.int64, device=dev)
-        self.comm.dist.all_to_all_single(R, ev_s, rl, sl, group=self.comm.group)
-        self.comm.dist.all_to_all_single(S, side_s, rl, sl, group=self.comm.group)
+        if W > 1:
+            R = torch.empty((m, 128), dtype=torch.uint8, device=dev)
+            S = torch.empty(m, dtype=torch.int64, device=dev)
+            self.comm.dist.all_to_all_single(R, ev_s, rl, sl, group=self.comm.group)
+            self.comm.dist.all_to_all_single(S, side_s, rl, sl, group=self.comm.group)
+        else:  # one owner: the send buffers are what it receives
+            R, S = ev_s, side_s
         del ev_s, side_s
+        # the received events' timestamps: T - n + index + 1 of their global batch
+        tsb = torch.tensor([T[k] - glob[k][2] for k in range(len(glob))], dtype=torch.int64, device=dev)
         clock("exchange_ms")
 
         # owner side: sub-batches in global order (from the senders' counts), chain control
         si = torch.zeros(0, dtype=torch.int64, device=dev)
         if n_span:
-            gk = S[:, 1] >> 32
-            key = S[:, 2]
-            spanm = (S[:, 3] & 1) != 0
-            lastm = (S[:, 3] & 2) != 0
+            gk = S >> 32
+            key = rec_chain_key(S)
+            spanm = (S & REC_SPAN) != 0
+            lastm = (S & REC_LAST) != 0
             nxt = torch.ones(m, dtype=torch.bool, device=dev)
             nxt[:-1] = key[1:] != key[:-1]                 # last local member of its chain
             base = (spanm & nxt & ~lastm).to(torch.uint8) * CTL_CHAIN_END
@@ -441,7 +467,13 @@ class ShardedStateMachine:
         st.replies = None
         st.thread = None
         results = torch.empty(max(m, 1) * 8, dtype=torch.uint8, device=dev)
-        ts_r = S[:, 0].contiguous() if m else torch.zeros(1, dtype=torch.int64, device=dev)
+        if not m:
+            ts_r = torch.zeros(1, dtype=torch.int64, device=dev)
+        elif S.is_cuda and hasattr(self.backend, "route_unpack"):
+            ts_r = torch.empty(m, dtype=torch.int64, device=dev)
+            self.backend.route_unpack(S, g["tsb"], ts_r)
+        else:
+            ts_r = g["tsb"][S >> 32] + (S & REC_POS) + 1
         Rf = R.reshape(-1) if m else torch.zeros(128, dtype=torch.uint8, device=dev)
         offs = np.concatenate([[0], np.cumsum(sub_counts)]).astype(np.int64)
         si_np = si.cpu().numpy()
@@ -472,7 +504,7 @@ class ShardedStateMachine:
 
         if any_span:
             span_key = key.index_select(0, si).cpu().numpy() if n_span else np.zeros(0, np.int64)
-            span_pos = S[si, 1].cpu().numpy() if n_span else np.zeros(0, np.int64)
+            span_pos = rec_position(S[si]).cpu().numpy() if n_span else np.zeros(0, np.int64)
             span_base = base.index_select(0, si).cpu().numpy() if n_span else np.zeros(0, np.uint8)
             span_last = (nxt[si] & ~lastm[si]).cpu().numpy() if n_span else np.zeros(0, bool)
             where = np.full(max(m, 1), -1, dtype=np.int64)
@@ -589,7 +621,7 @@ class ShardedStateMachine:
         if any(x[0] for x in allfin):
             # replies to their sources
             if len(at):
-                pg = S[torch.from_numpy(at).to(dev), 1].cpu().numpy()
+                pg = rec_position(S[torch.from_numpy(at).to(dev)]).cpu().numpy()
             else:
                 pg = np.zeros(0, np.int64)
             rep = [[] for _ in range(W)]
@@ -1026,8 +1058,11 @@ def partition_torch(torch, ev, counts, batch_ts, g0: int, W: int, dev, detail: b
     """The send side of a routed step with torch tensor ops (the CPU-collective tests'
     path; on GPUs the engine's tbgpu_route_scatter computes the same thing): events
     owner-major (owner = ledger % W), in event order within an owner, with their
-    32-byte side records {timestamp, g << 32 | index, g << 32 | chain start, span |
-    end << 1}.  Returns (events [n, 128], records [n, 4], per-owner counts)."""
+    8-byte records (REC_*: g << 32 | chain start << 15 | end << 14 | span << 13 |
+    index).  `batch_ts` is no longer part of the record (the owner derives the
+    timestamps).  Returns (events [n, 128], records [n], per-owner counts)."""
+    if any(int(c) > REC_POS + 1 for c in counts):
+        raise ValueError("a routed batch holds at most 8192 events")
     n = int(sum(counts))
     w32 = ev.view(torch.int32).view(n, 32)
     flags = (w32[:, 29] >> 16) & 0xFFFF
@@ -1036,8 +1071,6 @@ def partition_torch(torch, ev, counts, batch_ts, g0: int, W: int, dev, detail: b
     bidx = torch.repeat_interleave(torch.arange(nb, device=dev), cnt_t)
     bstart = torch.cumsum(cnt_t, 0) - cnt_t
     pos = torch.arange(n, device=dev) - bstart[bidx]
-    Tb = torch.tensor(list(map(int, batch_ts)), dtype=torch.int64, device=dev)
-    ts = Tb[bidx] - cnt_t[bidx] + pos + 1
     g = bidx + g0
     linked = (flags & LINKED) != 0
     prev_l = torch.zeros_like(linked)
@@ -1050,8 +1083,8 @@ def partition_torch(torch, ev, counts, batch_ts, g0: int, W: int, dev, detail: b
     omin = torch.full((n,), W, dtype=torch.int64, device=dev).scatter_reduce(0, cstart, owner, "amin")
     omax = torch.full((n,), -1, dtype=torch.int64, device=dev).scatter_reduce(0, cstart, owner, "amax")
     span = omin[cstart] != omax[cstart]
-    side = torch.stack([ts, (g << 32) | pos, (g << 32) | (cstart - bstart[bidx]),
-                        span.to(torch.int64) | (last.to(torch.int64) << 1)], 1)
+    side = (g << 32) | ((cstart - bstart[bidx]) << REC_CS_SHIFT) | (last.to(torch.int64) << 14) | \
+        (span.to(torch.int64) << 13) | pos
     perm = torch.argsort(owner, stable=True)
     send = torch.bincount(owner, minlength=W)
     out = (ev.view(n, 128).index_select(0, perm), side.index_select(0, perm), send)

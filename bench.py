@@ -268,7 +268,7 @@ def routed_bench(args, rank, world, local_rank, torch, dist, backend="nccl"):
     phases = {x: round(float(tmax[2 + i]), 3) for i, x in enumerate(sorted(ssm.timing))}
     if rank == 0:
         e2e = value / world * ALGO_BYTES_PER_TRANSFER / 1e9
-        a2a_bytes = per_step * (128 + 32) * (world - 1) / world  # events + side records leaving each rank
+        a2a_bytes = per_step * (128 + 8) * (world - 1) / world  # events + 8-byte records leaving each rank
         line = {
             "metric": "committed transfers/sec (whole node), 8190-transfer batches; % HBM roofline",
             "value": round(value, 1),

@@ -261,7 +261,7 @@ class ShardedStateMachine:
         global order above every id seen before (no directory lookup can hit);
         routing, partition and exchange then stay on the device: owner = ledger
         % world, a stable partition by owner, RCCL all-to-all of the events and of
-        32-byte side records {timestamp, (batch, index), chain, span bits}, and the
+        8-byte records {(batch, index), chain start, span / end bits} (REC_*), and the
         owner's tbgpu_create_transfers_routed_device.  Chains that span shards are
         settled before the commit: when every member is a plain transfer between
         accounts without balance limits (its outcome then depends on no other
@@ -340,10 +340,13 @@ class ShardedStateMachine:
         nb_here = len(counts)
         st += [nb_here] + (list(map(int, counts)) if nb_here <= NB_GATHER else []) + \
             [0] * (NB_GATHER - (nb_here if nb_here <= NB_GATHER else 0))
-        stats = torch.tensor(st, dtype=torch.int64, device=dev)
-        allst = [torch.empty_like(stats) for _ in range(W)]
-        self.comm.dist.all_gather(allst, stats, group=self.comm.group)
-        allst = torch.stack(allst).cpu().tolist()
+        if W > 1:
+            stats = torch.tensor(st, dtype=torch.int64, device=dev)
+            allst = [torch.empty_like(stats) for _ in range(W)]
+            self.comm.dist.all_gather(allst, stats, group=self.comm.group)
+            allst = torch.stack(allst).cpu().tolist()
+        else:  # one rank: nothing to gather
+            allst = [st]
         ok, prev = True, self.max_id
         for (cnt, lo, hi, mono, plain, _) in (x[:6] for x in allst):
             if cnt == 0:
@@ -612,10 +615,14 @@ class ShardedStateMachine:
         dev, W, m, S, glob, g0, counts = g["dev"], g["W"], g["m"], g["S"], g["glob"], g["g0"], g["counts"]
         out, at, cts = st.out, st.at, st.cts
         # the node's commit timestamp and whether any owner has replies, in one all-gather
-        fin = torch.tensor([len(at), cts if m else self.backend.commit_timestamp()], dtype=torch.int64, device=dev)
-        allfin = [torch.empty_like(fin) for _ in range(W)]
-        self.comm.dist.all_gather(allfin, fin, group=self.comm.group)
-        allfin = torch.stack(allfin).cpu().tolist()
+        fin = [len(at), int(cts) if m else self.backend.commit_timestamp()]
+        if W > 1:
+            fin = torch.tensor(fin, dtype=torch.int64, device=dev)
+            allfin = [torch.empty_like(fin) for _ in range(W)]
+            self.comm.dist.all_gather(allfin, fin, group=self.comm.group)
+            allfin = torch.stack(allfin).cpu().tolist()
+        else:
+            allfin = [fin]
         ts_all = max(x[1] for x in allfin)
         mine = {j: [] for j in range(len(counts))}
         if any(x[0] for x in allfin):

@@ -88,6 +88,63 @@ def test_route_scatter_matches_torch_partition():
 
 
 @pytest.mark.gpu
+def test_route_packed_wire_format_round_trip():
+    """tbgpu_route_scatter_packed + tbgpu_route_unpack_packed (the all-to-all's wire
+    format: the step's nonzero 8-byte words, then the record) give back exactly the
+    torch partition's rows, records and timestamps, for masks from the events' own
+    nonzero words (tbgpu_route_stats) to all 16; a mask missing a nonzero word fails."""
+    import numpy as np
+    import torch
+
+    from tigerbeetle_amd.engine import Engine
+    from tigerbeetle_amd.shard import partition_torch
+    from tigerbeetle_amd.types import TRANSFER_DTYPE
+    rng = np.random.default_rng(5)
+    counts = [8190, 17, 0, 1000, 1, 0, 8190, 333, 4095]
+    n = sum(counts)
+    t = np.zeros(n, dtype=TRANSFER_DTYPE)
+    t["id_lo"] = np.arange(1, n + 1)
+    t["debit_account_id_lo"] = rng.integers(1, 1 << 40, n)
+    t["credit_account_id_lo"] = rng.integers(1, 1 << 40, n)
+    t["amount_lo"] = rng.integers(1, 1 << 20, n)
+    t["user_data_64"] = rng.integers(0, 1 << 63, n)
+    t["ledger"] = rng.integers(0, 5000, n)
+    t["code"] = 1
+    t["flags"] = np.where(rng.random(n) < 0.3, 1, 0) | np.where(rng.random(n) < 0.1, 2, 0)
+    t["timeout"][::97] = 3  # a word that is nonzero in few events
+    dev = torch.device("cuda", 0)
+    ev = torch.from_numpy(t.view(np.uint8).copy()).to(dev)
+    bts = np.cumsum(np.array(counts, dtype=np.uint64) + 1) + 1000
+    tsb = torch.tensor([0] * 5 + [int(b) - c for b, c in zip(bts, counts)], dtype=torch.int64, device=dev)
+    w64 = t.view(np.uint64).reshape(n, 16)
+    want_mask = sum(1 << w for w in range(16) if w64[:, w].any())
+    eng = Engine(device=0, accounts_max=16, transfers_max=16, events_per_call_max=1 << 12)
+    try:
+        *_, got_mask = eng.route_stats(ev, n, world=3, word_mask=True)
+        assert got_mask == want_mask
+        for W in (1, 3, 8):
+            e_t, s_t, c_t, b_t, p_t = partition_torch(torch, ev, counts, bts, 5, W, dev, detail=True)
+            for mask in (want_mask, want_mask | 0x8001, 0xFFFF):
+                k = bin(mask).count("1") + 1
+                send = torch.empty((n, k), dtype=torch.int64, device=dev)
+                c_n, b_n, p_n = eng.route_scatter_packed(W, counts, 5, ev, mask, send)
+                assert c_n.tolist() == c_t.cpu().tolist() and b_n.tolist() == b_t.cpu().tolist()
+                assert p_n.tolist() == p_t.cpu().tolist()
+                e_n = torch.empty((n, 128), dtype=torch.uint8, device=dev)
+                s_n = torch.empty(n, dtype=torch.int64, device=dev)
+                ts_n = torch.empty(n, dtype=torch.int64, device=dev)
+                eng.route_unpack_packed(send, mask, tsb, e_n, s_n, ts_n)
+                assert torch.equal(e_n, e_t), (W, mask)
+                assert torch.equal(s_n, s_t), (W, mask)
+                assert torch.equal(ts_n, tsb[s_t >> 32] + (s_t & 0x1FFF) + 1), (W, mask)
+        with pytest.raises(ValueError):
+            send = torch.empty((n, 16), dtype=torch.int64, device=dev)
+            eng.route_scatter_packed(3, counts, 5, ev, want_mask & ~(1 << 13), send)  # drops the timeouts
+    finally:
+        eng.close()
+
+
+@pytest.mark.gpu
 def test_route_stats_matches_numpy():
     """tbgpu_route_stats (csrc/route.hip) against numpy over the same events."""
     import numpy as np

@@ -980,7 +980,9 @@ extern "C" int tbgpu_route_stats(tbgpu_ctx* c, const void* events_device, uint64
 }
 void route_scatter(const Transfer* ev, u64 n, u32 world, u32 nb, const u32* b_start, const u64* b_ts, u64 g0,
                    uint2* orank, u32* blk, u64* counts, Transfer* out_ev, u64* out_side, u32* bcount, u32* scount,
-                   bool ranked, hipStream_t stream);
+                   u32 pack_mask, u64* out_packed, u32* error, bool ranked, hipStream_t stream);
+void route_unpack_rows(const u64* packed, u64 m, u32 mask, const u64* ts_base, u64 batches, Transfer* rows, u64* rec,
+                       u64* ts, u32* error, hipStream_t stream);
 void route_rank(const Transfer* ev, u64 n, u32 world, uint2* orank, u32* blk, u64* part, u64* stats,
                 hipStream_t stream);
 void route_unpack(const u64* rec, u64 n, const u64* ts_base, u64 batches, u64* ts, u32* error, hipStream_t stream);
@@ -1020,10 +1022,10 @@ extern "C" int tbgpu_route_prepare(tbgpu_ctx* c, uint32_t world, const void* eve
     return 0;
 }
 
-extern "C" int tbgpu_route_scatter(tbgpu_ctx* c, uint32_t world, uint32_t batch_count, const uint32_t* counts,
-                                   const uint64_t* batch_timestamps, uint64_t first_global_batch,
-                                   const void* events_device, void* send_events_device, void* send_records_device,
-                                   uint64_t* send_counts, uint32_t* send_batch_counts, uint32_t* send_span_counts) {
+static int route_scatter_any(tbgpu_ctx* c, uint32_t world, uint32_t batch_count, const uint32_t* counts,
+                             uint64_t first_global_batch, const void* events_device, void* send_events_device,
+                             void* send_records_device, uint32_t word_mask, void* send_packed_device,
+                             uint64_t* send_counts, uint32_t* send_batch_counts, uint32_t* send_span_counts) {
     HIP_CHECK(hipSetDevice(c->device));
     if (world == 0 || world > 256) return -22;
     std::vector<u32> starts(batch_count + 1, 0);
@@ -1042,20 +1044,56 @@ extern "C" int tbgpu_route_scatter(tbgpu_ctx* c, uint32_t world, uint32_t batch_
         if (send_span_counts) memset(send_span_counts, 0, world * sizeof(u32));
         return 0;
     }
+    u32* err = (u32*)(c->rt_stats + 7);
+    HIP_CHECK(hipMemsetAsync(err, 0, sizeof(u32), c->route_stream));
     HIP_CHECK(hipMemcpyAsync(c->ro_bstart, starts.data(), (batch_count + 1) * sizeof(u32), hipMemcpyHostToDevice,
                              c->route_stream));
-    HIP_CHECK(hipMemcpyAsync(c->ro_bts, batch_timestamps, batch_count * sizeof(u64), hipMemcpyHostToDevice, c->route_stream));
-    route_scatter((const Transfer*)events_device, n, world, batch_count, c->ro_bstart, c->ro_bts, first_global_batch,
+    route_scatter((const Transfer*)events_device, n, world, batch_count, c->ro_bstart, nullptr, first_global_batch,
                   c->ro_orank, c->ro_blk, c->ro_counts, (Transfer*)send_events_device, (u64*)send_records_device,
-                  c->ro_bcount + 256, c->ro_bcount, ranked, c->route_stream);
+                  c->ro_bcount + 256, c->ro_bcount, word_mask, (u64*)send_packed_device, err, ranked, c->route_stream);
     HIP_CHECK(hipMemcpyAsync(send_counts, c->ro_counts, world * sizeof(u64), hipMemcpyDeviceToHost, c->route_stream));
     if (send_batch_counts)
         HIP_CHECK(hipMemcpyAsync(send_batch_counts, c->ro_bcount + 256, (u64)world * batch_count * sizeof(u32),
                                  hipMemcpyDeviceToHost, c->route_stream));
     if (send_span_counts)
         HIP_CHECK(hipMemcpyAsync(send_span_counts, c->ro_bcount, world * sizeof(u32), hipMemcpyDeviceToHost, c->route_stream));
+    u32 e = 0;
+    HIP_CHECK(hipMemcpyAsync(&e, err, sizeof(u32), hipMemcpyDeviceToHost, c->route_stream));
     HIP_CHECK(hipStreamSynchronize(c->route_stream));
-    return 0;
+    return e ? -22 : 0;
+}
+
+extern "C" int tbgpu_route_scatter(tbgpu_ctx* c, uint32_t world, uint32_t batch_count, const uint32_t* counts,
+                                   const uint64_t* batch_timestamps, uint64_t first_global_batch,
+                                   const void* events_device, void* send_events_device, void* send_records_device,
+                                   uint64_t* send_counts, uint32_t* send_batch_counts, uint32_t* send_span_counts) {
+    (void)batch_timestamps;  // the owner derives the timestamps (tbgpu_route_unpack)
+    return route_scatter_any(c, world, batch_count, counts, first_global_batch, events_device, send_events_device,
+                             send_records_device, 0, nullptr, send_counts, send_batch_counts, send_span_counts);
+}
+
+extern "C" int tbgpu_route_scatter_packed(tbgpu_ctx* c, uint32_t world, uint32_t batch_count, const uint32_t* counts,
+                                          uint64_t first_global_batch, const void* events_device, uint32_t word_mask,
+                                          void* send_device, uint64_t* send_counts, uint32_t* send_batch_counts,
+                                          uint32_t* send_span_counts) {
+    if (word_mask == 0 || word_mask > 0xFFFFu) return -22;
+    return route_scatter_any(c, world, batch_count, counts, first_global_batch, events_device, nullptr, nullptr,
+                             word_mask, send_device, send_counts, send_batch_counts, send_span_counts);
+}
+
+extern "C" int tbgpu_route_unpack_packed(tbgpu_ctx* c, const void* packed_device, uint64_t count, uint32_t word_mask,
+                                         const void* batch_ts_base_device, uint64_t batches, void* events_device,
+                                         void* records_device, void* timestamps_device) {
+    HIP_CHECK(hipSetDevice(c->device));
+    if (word_mask == 0 || word_mask > 0xFFFFu) return -22;
+    u32* err = (u32*)(c->rt_stats + 6);
+    HIP_CHECK(hipMemsetAsync(err, 0, sizeof(u32), c->route_stream));
+    route_unpack_rows((const u64*)packed_device, count, word_mask, (const u64*)batch_ts_base_device, batches,
+                      (Transfer*)events_device, (u64*)records_device, (u64*)timestamps_device, err, c->route_stream);
+    u32 e = 0;
+    HIP_CHECK(hipMemcpyAsync(&e, err, sizeof(u32), hipMemcpyDeviceToHost, c->route_stream));
+    HIP_CHECK(hipStreamSynchronize(c->route_stream));
+    return e ? -22 : 0;
 }
 
 extern "C" int tbgpu_route_unpack(tbgpu_ctx* c, const void* records_device, uint64_t count,
@@ -1071,11 +1109,15 @@ extern "C" int tbgpu_route_unpack(tbgpu_ctx* c, const void* records_device, uint
     return e ? -22 : 0;
 }
 
+// max into the device scalar, ordered on the engine's stream (no host round trip)
+__global__ void k_advance_commit_ts(u64* ts, u64 v) {
+    if (threadIdx.x == 0 && *ts < v) *ts = v;
+}
+
 extern "C" void tbgpu_advance_commit_timestamp(tbgpu_ctx* c, uint64_t timestamp) {
     HIP_CHECK(hipSetDevice(c->device));
-    u64 v = 0;
-    HIP_CHECK(hipMemcpy(&v, c->T.commit_ts, sizeof(u64), hipMemcpyDeviceToHost));
-    if (timestamp > v) HIP_CHECK(hipMemcpy(c->T.commit_ts, &timestamp, sizeof(u64), hipMemcpyHostToDevice));
+    k_advance_commit_ts<<<1, 64, 0, c->stream>>>(c->T.commit_ts, timestamp);
+    HIP_CHECK(hipGetLastError());
 }
 
 extern "C" uint32_t tbgpu_create_transfers(tbgpu_ctx* c, uint64_t timestamp, const tbgpu_transfer_t* events,
@@ -1495,8 +1537,9 @@ extern "C" uint64_t tbgpu_export_accounts(tbgpu_ctx* c, tbgpu_account_t* out, ui
 
 extern "C" uint64_t tbgpu_commit_timestamp(tbgpu_ctx* c) {
     HIP_CHECK(hipSetDevice(c->device));
-    u64 v = 0;
-    HIP_CHECK(hipMemcpy(&v, c->T.commit_ts, sizeof(u64), hipMemcpyDeviceToHost));
+    u64 v = 0;  // behind whatever the engine's stream still has queued (tbgpu_advance_commit_timestamp)
+    HIP_CHECK(hipMemcpyAsync(&v, c->T.commit_ts, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(hipStreamSynchronize(c->stream));
     return v;
 }
 

@@ -39,6 +39,12 @@ struct RouteArgs {
     u32* bcount;          // [world * nb] events per (owner, local batch)
     u32* scount;          // [world] events per owner whose chain spans owners
     u64* stats;           // rt_rank: the eligibility figures of rt_stats (out[0..4]), or null
+    // packed wire format (pack_mask != 0): per event the 8-byte words of `pack_mask`
+    // in word order, then the record, in out_packed; a nonzero word outside the mask
+    // sets *error (the step must not lose data)
+    u32 pack_mask;
+    u64* out_packed;
+    u32* error;
 };
 
 constexpr u64 REC_POS = TBGPU_ROUTE_REC_POS, REC_SPAN = TBGPU_ROUTE_REC_SPAN, REC_LAST = TBGPU_ROUTE_REC_LAST;
@@ -73,16 +79,28 @@ __global__ __launch_bounds__(RT_THREADS) void rt_rank(RouteArgs A) {
     const u64 i = (u64)blockIdx.x * RT_THREADS + tid;
     const u64 wbase = i - lane;
     const bool v = i < A.n;
+    // with the figures, every piece is read: the step's nonzero 8-byte words (the
+    // packed wire format's mask) come from the same pass
+    u32 nzw = 0;
     {
         const uint4* rows = (const uint4*)A.ev;
         const u32 piece = lane & 7;
         const int slot = piece == 0 ? 0 : piece == 3 ? 1 : piece == 7 ? 2 : -1;
         const int sl = A.stats ? slot : (piece == 7 ? 2 : -1);  // without the figures: the ledger word
+        uint4 x[8];
 #pragma unroll
         for (int r = 0; r < 8; r++) {
             const u32 k = (u32)r * 8 + (lane >> 3);
-            if (sl >= 0 && wbase + k < A.n) s_pc[w][k][sl] = rows[(wbase + k) * 8 + piece];
+            x[r] = make_uint4(0, 0, 0, 0);
+            if ((A.stats || sl >= 0) && wbase + k < A.n) x[r] = rows[(wbase + k) * 8 + piece];
         }
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            const u32 k = (u32)r * 8 + (lane >> 3);
+            if (sl >= 0 && wbase + k < A.n) s_pc[w][k][sl] = x[r];
+            nzw |= ((x[r].x | x[r].y) ? 1u : 0u) | ((x[r].z | x[r].w) ? 2u : 0u);
+        }
+        nzw <<= 2 * piece;
     }
     uint4 pidv = make_uint4(0, 0, 0, 0);
     if (A.stats && lane == 0 && v && i > 0) pidv = *(const uint4*)&A.ev[i - 1].id;
@@ -105,7 +123,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_rank(RouteArgs A) {
             plo = ((u64)pidv.y << 32) | pidv.x;
             phi = ((u64)pidv.w << 32) | pidv.z;
         }
-        u64 mn = ~0ull, mx = 0, fl = 0, slo = 0, shi = 0;
+        u64 mn = ~0ull, mx = 0, fl = (u64)nzw << 16, slo = 0, shi = 0;
         if (v) {
             mn = mx = lo;
             if (hi != 0 || lo == 0) fl |= 2;
@@ -187,59 +205,93 @@ __global__ __launch_bounds__(1024) void rt_scan(RouteArgs A) {
     }
 }
 
+// The scatter.  The workgroup's 256 rows are staged in LDS by coalesced 16-byte loads
+// (eight lanes per row); every event then reads its own and its chain's flags and
+// owners from there (a chain reaching past the workgroup reads the rows it needs
+// from memory: lane-per-row loads of 128-byte-strided rows ran 5x slower than the
+// staged ones), and the rows leave LDS for their owners' runs: whole rows, 16 bytes
+// per lane, or packed (the 8-byte words of pack_mask, then the record), 8 bytes per
+// lane over consecutive words.
 __global__ __launch_bounds__(RT_THREADS) void rt_scatter(RouteArgs A) {
-    // the workgroup's first batch by one binary search; each event steps on from it
+    __shared__ uint4 s_rows[RT_THREADS][8];  // 32 KiB
+    __shared__ u32 s_om[RT_THREADS];         // owner << 1 | linked
+    __shared__ u32 s_dst[RT_THREADS];
+    __shared__ u64 s_rec[RT_THREADS];
     __shared__ u32 s_b0;
-    if (threadIdx.x == 0) s_b0 = rt_batch(A, (u32)((u64)blockIdx.x * RT_THREADS));
-    __syncthreads();
-    const u64 i = (u64)blockIdx.x * RT_THREADS + threadIdx.x;
-    const u32 lane = threadIdx.x & 63;
+    __shared__ u8 s_sel[16];                 // the packed row's word k is row word s_sel[k]
+    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const u32 blk0 = blockIdx.x * RT_THREADS;
+    const u64 i = (u64)blk0 + tid;
     const u64 wbase = i - lane;
-    u64 dst = 0;
-    uint2 orr = make_uint2(0, 0);
-    if (i < A.n) {
-        orr = A.orank[i];
-        dst = (u64)A.blk[(u64)orr.x * A.nblk + blockIdx.x] + orr.y;
+    if (tid == 0) {
+        // the workgroup's first batch by one binary search; each event steps on from it
+        s_b0 = rt_batch(A, blk0);
+        u32 k = 0;
+        for (u32 wd = 0; wd < 16; wd++)
+            if (A.pack_mask >> wd & 1) s_sel[k++] = (u8)wd;
     }
-    // the rows, eight lanes per row: each round moves eight whole rows (1 KiB) with
-    // one 16-byte access per lane, coalesced on both sides
-    const uint4* src = (const uint4*)A.ev;
-    uint4* out = (uint4*)A.out_ev;
-#pragma unroll
-    for (int r = 0; r < 8; r++) {
-        const u32 k = (u32)r * 8 + (lane >> 3);
-        const u64 d = (u64)__shfl((unsigned long long)dst, (int)k);
-        if (wbase + k < A.n) out[d * 8 + (lane & 7)] = src[(wbase + k) * 8 + (lane & 7)];
-    }
-    if (i >= A.n) return;
-    // the side record: timestamp, position, chain key, span / end bits
-    u32 b = s_b0;
-    while (A.b_start[b + 1] <= (u32)i) b++;
-    const u32 bs = A.b_start[b], be = A.b_start[b + 1];
-    const u32 pos = (u32)i - bs, nbatch = be - bs;
-    const u64 g = A.g0 + b;
-    auto linked = [&](u32 j) { return (A.ev[j].flags & TF_LINKED) != 0; };
-    u32 s = (u32)i, e = (u32)i;
-    while (s > bs && linked(s - 1)) s--;
-    while (e + 1 < be && linked(e)) e++;
-    u32 omin = orr.x, omax = orr.x;
-    for (u32 j = s; j <= e; j++) {
-        const u32 o = rt_owner(A, j);
-        omin = min(omin, o);
-        omax = max(omax, o);
-    }
-    const bool last = !linked((u32)i) || pos == nbatch - 1;
-    // per (owner, batch) and per-owner spanning counts: one atomic per distinct key per wave
     {
+        const uint4* src = (const uint4*)A.ev;
+        const u32 piece = lane & 7;
+        uint4 x[8];
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            const u32 k = (u32)r * 8 + (lane >> 3);
+            x[r] = wbase + k < A.n ? src[(wbase + k) * 8 + piece] : make_uint4(0, 0, 0, 0);
+        }
+        u32 lost = 0;  // nonzero words the packed format would drop
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            const u32 k = (u32)r * 8 + (lane >> 3);
+            s_rows[w * 64 + k][piece] = x[r];
+            lost |= ((x[r].x | x[r].y) ? 1u : 0u) | ((x[r].z | x[r].w) ? 2u : 0u);
+        }
+        if (A.pack_mask && ((lost << 2 * piece) & ~A.pack_mask)) atomicOr(A.error, 1u);
+    }
+    uint2 orr = make_uint2(0, 0);
+    const bool v = i < A.n;
+    if (v) orr = A.orank[i];
+    __syncthreads();
+    {
+        const uint4 p7 = s_rows[tid][7];  // bytes 112..127: ledger, code, flags, timestamp
+        s_om[tid] = (p7.x % A.world) << 1 | ((p7.y >> 16) & TF_LINKED);
+    }
+    __syncthreads();
+    if (v) {
+        const u32 dst = A.blk[(u64)orr.x * A.nblk + blockIdx.x] + orr.y;
+        s_dst[tid] = dst;
+        // the record: position, chain start, span / end bits, global batch
+        u32 b = s_b0;
+        while (A.b_start[b + 1] <= (u32)i) b++;
+        const u32 bs = A.b_start[b], be = A.b_start[b + 1];
+        const u32 pos = (u32)i - bs, nbatch = be - bs;
+        const u64 g = A.g0 + b;
+        auto om = [&](u32 j) -> u32 {
+            const u32 t = j - blk0;
+            return t < RT_THREADS ? s_om[t] : (rt_owner(A, j) << 1 | (A.ev[j].flags & TF_LINKED));
+        };
+        u32 s = (u32)i, e = (u32)i;
+        while (s > bs && (om(s - 1) & 1)) s--;
+        while (e + 1 < be && (om(e) & 1)) e++;
+        u32 omin = orr.x, omax = orr.x;
+        for (u32 j = s; j <= e; j++) {
+            const u32 o = om(j) >> 1;
+            omin = min(omin, o);
+            omax = max(omax, o);
+        }
+        const bool last = !(s_om[tid] & 1) || pos == nbatch - 1;
+        const bool sp = omin != omax;
+        s_rec[tid] = (g << 32) | ((u64)(s - bs) << REC_CS_SHIFT) | (last ? REC_LAST : 0) | (sp ? REC_SPAN : 0) | pos;
+        // per (owner, batch) and per-owner spanning counts: one atomic per distinct key per wave
         const u32 key = orr.x * A.nb + b;
-        u64 todo = __ballot(true);
+        const u64 live = __ballot(true);
+        u64 todo = live;
         while (todo) {
             const u32 k = __shfl(key, __ffsll((unsigned long long)todo) - 1);
             const u64 mk = __ballot(key == k);
             if (key == k && lane == (u32)__ffsll((unsigned long long)mk) - 1) atomicAdd(&A.bcount[k], (u32)__popcll(mk));
             todo &= ~mk;
         }
-        const bool sp = omin != omax;
         todo = __ballot(sp);
         while (todo) {
             const u32 o = __shfl(orr.x, __ffsll((unsigned long long)todo) - 1);
@@ -249,8 +301,71 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scatter(RouteArgs A) {
             todo &= ~mo;
         }
     }
-    A.out_side[dst] = (g << 32) | ((u64)(s - bs) << REC_CS_SHIFT) | (last ? REC_LAST : 0) |
-                      (omin != omax ? REC_SPAN : 0) | pos;
+    __syncthreads();
+    const u32 nv = (u32)min<u64>(64, A.n > wbase ? A.n - wbase : 0);  // the wave's rows
+    if (!A.pack_mask) {
+        uint4* out = (uint4*)A.out_ev;
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            const u32 k = (u32)r * 8 + (lane >> 3);
+            if (k < nv) out[(u64)s_dst[w * 64 + k] * 8 + (lane & 7)] = s_rows[w * 64 + k][lane & 7];
+        }
+        if (v) A.out_side[s_dst[tid]] = s_rec[tid];
+        return;
+    }
+    const u32 K = (u32)__popc(A.pack_mask) + 1;  // words per packed row
+    for (u32 f = lane; f < nv * K; f += 64) {
+        const u32 rr = f / K, wd = f - rr * K, row = w * 64 + rr;
+        const u64 val = wd + 1 < K ? ((const u64*)&s_rows[row][0])[s_sel[wd]] : s_rec[row];
+        A.out_packed[(u64)s_dst[row] * K + wd] = val;
+    }
+}
+
+// The owner side of the packed format: rows of K = popcount(mask) + 1 words back to
+// whole 128-byte rows (the words outside the mask are zero), the records, and each
+// event's timestamp ts_base[g] + index + 1 (src/vsr/replica.zig:5148-5157).
+__global__ __launch_bounds__(RT_THREADS) void rt_unpack_rows(const u64* __restrict__ packed, u64 m, u32 mask,
+                                                             const u64* __restrict__ ts_base, u64 batches,
+                                                             Transfer* __restrict__ rows, u64* __restrict__ rec,
+                                                             u64* __restrict__ ts, u32* error) {
+    __shared__ uint4 s_rows[RT_THREADS][8];
+    __shared__ u8 s_sel[16];
+    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const u64 i = (u64)blockIdx.x * RT_THREADS + tid;
+    const u64 wbase = i - lane;
+    const u32 K = (u32)__popc(mask) + 1;
+    if (tid == 0) {
+        u32 k = 0;
+        for (u32 wd = 0; wd < 16; wd++)
+            if (mask >> wd & 1) s_sel[k++] = (u8)wd;
+    }
+#pragma unroll
+    for (int p = 0; p < 8; p++) s_rows[tid][p] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    const u32 nv = (u32)min<u64>(64, m > wbase ? m - wbase : 0);
+    for (u32 f = lane; f < nv * K; f += 64) {
+        const u32 rr = f / K, wd = f - rr * K;
+        const u64 val = packed[wbase * K + f];
+        if (wd + 1 < K) {
+            ((u64*)&s_rows[w * 64 + rr][0])[s_sel[wd]] = val;
+        } else {
+            const u64 j = wbase + rr, g = val >> 32;
+            rec[j] = val;
+            if (g >= batches) {
+                atomicOr(error, 1u);
+                ts[j] = 0;
+            } else {
+                ts[j] = ts_base[g] + (val & REC_POS) + 1;
+            }
+        }
+    }
+    __syncthreads();
+    uint4* out = (uint4*)rows;
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        const u32 k = (u32)r * 8 + (lane >> 3);
+        if (k < nv) out[(wbase + k) * 8 + (lane & 7)] = s_rows[w * 64 + k][lane & 7];
+    }
 }
 
 // Timestamps of received events from their side records: batch g's events get
@@ -306,6 +421,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_stats(const Transfer* ev, u64 n
             } else if (piece == 7) {
                 if ((v[u].y >> 16) & (TF_POST | TF_VOID)) fl |= 4;
             }
+            fl |= (u64)(((v[u].x | v[u].y) ? 1u : 0u) | ((v[u].z | v[u].w) ? 2u : 0u)) << (16 + 2 * piece);
         }
     }
     rt_stats_block(mn, mx, fl, slo, shi, out, nullptr);
@@ -411,8 +527,11 @@ void route_unpack(const u64* rec, u64 n, const u64* ts_base, u64 batches, u64* t
 
 void route_scatter(const Transfer* ev, u64 n, u32 world, u32 nb, const u32* b_start, const u64* b_ts, u64 g0,
                    uint2* orank, u32* blk, u64* counts, Transfer* out_ev, u64* out_side, u32* bcount, u32* scount,
-                   bool ranked, hipStream_t stream) {
+                   u32 pack_mask, u64* out_packed, u32* error, bool ranked, hipStream_t stream) {
     RouteArgs A{};
+    A.pack_mask = pack_mask & 0xFFFFu;
+    A.out_packed = out_packed;
+    A.error = error;
     A.bcount = bcount;
     A.scount = scount;
     HIP_CHECK(hipMemsetAsync(bcount, 0, (u64)world * nb * sizeof(u32), stream));
@@ -423,5 +542,13 @@ void route_scatter(const Transfer* ev, u64 n, u32 world, u32 nb, const u32* b_st
     if (n && !ranked) rt_rank<<<A.nblk, RT_THREADS, 0, stream>>>(A);
     rt_scan<<<1, 1024, 0, stream>>>(A);
     if (n) rt_scatter<<<A.nblk, RT_THREADS, 0, stream>>>(A);
+    HIP_CHECK(hipGetLastError());
+}
+
+void route_unpack_rows(const u64* packed, u64 m, u32 mask, const u64* ts_base, u64 batches, Transfer* rows, u64* rec,
+                       u64* ts, u32* error, hipStream_t stream) {
+    if (m) rt_unpack_rows<<<(u32)((m + RT_THREADS - 1) / RT_THREADS), RT_THREADS, 0, stream>>>(packed, m, mask & 0xFFFFu,
+                                                                                              ts_base, batches, rows,
+                                                                                              rec, ts, error);
     HIP_CHECK(hipGetLastError());
 }

@@ -100,6 +100,10 @@ def _id(lo, hi) -> int:
     return (int(hi) << 64) | int(lo)
 
 
+_NO_REPLIES = np.zeros(0, dtype=RESULT_DTYPE)  # a batch without replies (shared, read-only)
+_NO_REPLIES.setflags(write=False)
+
+
 class Comm:
     """The collectives the router needs, over a torch.distributed group (gloo on
     CPU, nccl = RCCL on GPU: tensors then live on the rank's device)."""
@@ -318,10 +322,14 @@ class ShardedStateMachine:
         id_lo, id_hi = w64[:, 0], w64[:, 1]
         # eligibility, one small all-gather: [n, min id, max id, monotone, plain, amount bound in 2^32 units]
         native = n and ev.is_cuda and hasattr(self.backend, "route_scatter")
+        # this rank can send and receive the packed wire format (csrc/route.hip)
+        can_pack = W > 1 and ev.is_cuda and hasattr(self.backend, "route_scatter_packed")
+        wmask = 0xFFFF
         if n and ev.is_cuda and hasattr(self.backend, "route_stats"):
             # one pass of the engine's kernel (csrc/route.hip) instead of the torch reductions;
-            # the same pass ranks the events for the scatter below
-            mn, mx, mono, ids_ok, pv, big, asum = self.backend.route_stats(ev, n, world=W if native else 0)
+            # the same pass ranks the events for the scatter below and finds their nonzero words
+            mn, mx, mono, ids_ok, pv, big, asum, wmask = self.backend.route_stats(ev, n, world=W if native else 0,
+                                                                                 word_mask=True)
             ok_ids = ids_ok and mx < (1 << 63)  # the all-gather below carries int64
             units = (1 << 62) if big else (asum >> 32) + 2
             st = [n, mn if ok_ids else 0, mx if ok_ids else 0, int(mono), int(ok_ids and not pv), units]
@@ -336,7 +344,9 @@ class ShardedStateMachine:
             st = [n, int(id_lo.min()), int(id_lo.max()), int(mono), int(plain), units]
         else:
             st = [0, 0, 0, 1, 1, 0]
-        # with the batch counts of the step (the global order), in the same all-gather
+        # the packed format's words and capability, then the batch counts of the step
+        # (the global order), in the same all-gather
+        st += [(wmask if n else 0) | (int(can_pack) << 16)]
         nb_here = len(counts)
         st += [nb_here] + (list(map(int, counts)) if nb_here <= NB_GATHER else []) + \
             [0] * (NB_GATHER - (nb_here if nb_here <= NB_GATHER else 0))
@@ -362,8 +372,15 @@ class ShardedStateMachine:
         self.amount_bound += sum(float(x[5]) for x in allst) * 2.0**32
 
         # global order and timestamps (host: one entry per batch)
-        if all(x[6] <= NB_GATHER for x in allst):
-            counts_all = [x[7:7 + x[6]] for x in allst]
+        # every rank packs when every rank can: the union of the nonzero words travels
+        packed = W > 1 and all(x[6] >> 16 for x in allst)
+        pmask = 0
+        for x in allst:
+            pmask |= x[6] & 0xFFFF
+        pmask = pmask or 1
+        K = bin(pmask).count("1") + 1  # int64 words per packed row: the masked words, the record
+        if all(x[7] <= NB_GATHER for x in allst):
+            counts_all = [x[8:8 + x[7]] for x in allst]
         else:
             counts_all = self.comm.all_gather_object(list(map(int, counts)))
         glob = [(r, j, c) for r, cl in enumerate(counts_all) for j, c in enumerate(cl)]
@@ -374,7 +391,16 @@ class ShardedStateMachine:
         g0 = sum(len(cl) for cl in counts_all[:me])
         clock("order_ms")
         nb_me = len(counts)
-        if native:
+        send = None
+        if packed:
+            # the engine's scatter straight into the packed wire format (csrc/route.hip)
+            send = torch.empty((n, K), dtype=torch.int64, device=dev)
+            if n:
+                sc, bc, spc = self.backend.route_scatter_packed(W, list(map(int, counts)), g0, ev, pmask, send)
+            else:
+                sc, bc, spc = np.zeros(W, np.int64), np.zeros((W, 0), np.int64), np.zeros(W, np.int64)
+            ev_s = side_s = None
+        elif native:
             # the engine's scatter kernels (csrc/route.hip): same layout as partition_torch
             ev_s = torch.empty((n, 128), dtype=torch.uint8, device=dev)
             side_s = torch.empty(n, dtype=torch.int64, device=dev)
@@ -410,7 +436,20 @@ class ShardedStateMachine:
             sub_counts += [int(c) for c in row[3:] if c]
             off += 3 + k
         m = int(sum(rl))
-        if W > 1:
+        # the received events' timestamps: T - n + index + 1 of their global batch
+        tsb = torch.tensor([T[k] - glob[k][2] for k in range(len(glob))], dtype=torch.int64, device=dev)
+        ts_r = None
+        if packed:
+            recv = torch.empty((m, K), dtype=torch.int64, device=dev)
+            self.comm.dist.all_to_all_single(recv, send, rl, sl, group=self.comm.group)
+            del send
+            R = torch.empty((m, 128), dtype=torch.uint8, device=dev)
+            S = torch.empty(m, dtype=torch.int64, device=dev)
+            ts_r = torch.empty(m, dtype=torch.int64, device=dev)
+            if m:
+                self.backend.route_unpack_packed(recv, pmask, tsb, R, S, ts_r)
+            del recv
+        elif W > 1:
             R = torch.empty((m, 128), dtype=torch.uint8, device=dev)
             S = torch.empty(m, dtype=torch.int64, device=dev)
             self.comm.dist.all_to_all_single(R, ev_s, rl, sl, group=self.comm.group)
@@ -418,8 +457,6 @@ class ShardedStateMachine:
         else:  # one owner: the send buffers are what it receives
             R, S = ev_s, side_s
         del ev_s, side_s
-        # the received events' timestamps: T - n + index + 1 of their global batch
-        tsb = torch.tensor([T[k] - glob[k][2] for k in range(len(glob))], dtype=torch.int64, device=dev)
         clock("exchange_ms")
 
         # owner side: sub-batches in global order (from the senders' counts), chain control
@@ -472,6 +509,8 @@ class ShardedStateMachine:
         results = torch.empty(max(m, 1) * 8, dtype=torch.uint8, device=dev)
         if not m:
             ts_r = torch.zeros(1, dtype=torch.int64, device=dev)
+        elif g.get("ts_r") is not None:  # unpacked with the events (packed wire format)
+            ts_r = g["ts_r"]
         elif S.is_cuda and hasattr(self.backend, "route_unpack"):
             ts_r = torch.empty(m, dtype=torch.int64, device=dev)
             self.backend.route_unpack(S, g["tsb"], ts_r)
@@ -616,6 +655,7 @@ class ShardedStateMachine:
         out, at, cts = st.out, st.at, st.cts
         # the node's commit timestamp and whether any owner has replies, in one all-gather
         fin = [len(at), int(cts) if m else self.backend.commit_timestamp()]
+        fin_own = fin[1]
         if W > 1:
             fin = torch.tensor(fin, dtype=torch.int64, device=dev)
             allfin = [torch.empty_like(fin) for _ in range(W)]
@@ -624,7 +664,7 @@ class ShardedStateMachine:
         else:
             allfin = [fin]
         ts_all = max(x[1] for x in allfin)
-        mine = {j: [] for j in range(len(counts))}
+        mine = {}
         if any(x[0] for x in allfin):
             # replies to their sources
             if len(at):
@@ -637,13 +677,14 @@ class ShardedStateMachine:
                 rep[glob[gg][0]].append((gg, pgv & 0xFFFFFFFF, r))
             for lst in self._exchange_objects(rep):
                 for (gg, i, r) in lst:
-                    mine[gg - g0].append((i, r))
-        self.backend.advance_commit_timestamp(ts_all)
+                    mine.setdefault(gg - g0, []).append((i, r))
+        if ts_all > fin_own:
+            self.backend.advance_commit_timestamp(ts_all)
         self.commit_timestamp = ts_all
         replies = []
         for j in range(len(counts)):
-            if not mine[j]:
-                replies.append(np.zeros(0, dtype=RESULT_DTYPE))
+            if j not in mine:
+                replies.append(_NO_REPLIES)
                 continue
             a = np.array(sorted(mine[j]), dtype=np.uint32).reshape(-1, 2)
             res = np.zeros(len(a), dtype=RESULT_DTYPE)

@@ -9,9 +9,12 @@ StateMachine.commit per batch (tests/test_gpu_parity.py).
 Default workload: BASELINE config 2 (configs[1]) — 1M accounts on one ledger,
 Zipf(0.99) debit/credit accounts, 1000 batches of 8190 transfers: one step is
 the whole config-2 run (8,190,000 transfers) in one streamed call.  With --gpus N > 1
-(torchrun, one process per GPU) every rank owns its own ledger shard (weak
-scaling, no data-path collective): the ledger partition of SURVEY.md §8e with
-the routing already applied.
+(torchrun, one process per GPU) the step is BASELINE config 4 through the ledger
+router (tigerbeetle_amd/shard.py): every rank's client batches are
+scattered to the owners of their ledgers by RCCL all-to-all, committed there and
+answered by a second all-to-all (weak scaling: 1000 x 8190 transfers per rank per
+step); `--routed` runs the same on a one-rank group, `--unrouted` gives every rank
+its own pre-routed ledger shard instead.
 
 Prints ONE JSON line on rank 0.
 """
@@ -236,9 +239,8 @@ def routed_bench(args, rank, world, local_rank, torch, dist, backend="nccl"):
     dist.barrier()
     st0 = dict(ssm.stats)
     non_ok = 0
-    # the timed steps; with --pipelined step k + 1 is routed (eligibility, scatter,
-    # all-to-all) while step k's owner commit runs (shard.py create_transfers_device_stream):
-    # on one GPU that measured slower (both halves are HBM-bound), so it is not the default
+    # the timed steps; pipelined (the default on N > 1), step k + 1's all-to-all (xGMI)
+    # runs while step k's owner commit (HBM) runs (shard.py create_transfers_device_stream)
     t0 = time.perf_counter()
     if args.pipelined:
         for reps in ssm.create_transfers_device_stream(step_args(k) for k in range(W, W + K)):
@@ -268,7 +270,7 @@ def routed_bench(args, rank, world, local_rank, torch, dist, backend="nccl"):
     phases = {x: round(float(tmax[2 + i]), 3) for i, x in enumerate(sorted(ssm.timing))}
     if rank == 0:
         e2e = value / world * ALGO_BYTES_PER_TRANSFER / 1e9
-        a2a_bytes = per_step * (128 + 8) * (world - 1) / world  # events + 8-byte records leaving each rank
+        a2a_bytes = per_step * ssm.wire_bytes_per_event * (world - 1) / world  # leaving each rank per step
         line = {
             "metric": "committed transfers/sec (whole node), 8190-transfer batches; % HBM roofline",
             "value": round(value, 1),
@@ -292,6 +294,7 @@ def routed_bench(args, rank, world, local_rank, torch, dist, backend="nccl"):
             "non_ok_results": non_ok,
             "non_ok_rate": round(non_ok / total, 5),
             "routed": {"pipelined": bool(args.pipelined),
+                       "wire_bytes_per_event": ssm.wire_bytes_per_event,
                        "phase_ms_one_unpipelined_step_max_over_ranks": phases,
                        "alltoall_bytes_per_rank_per_step": int(a2a_bytes),
                        "alltoall_GBps_per_rank": round(a2a_bytes / (phases["exchange_ms"] * 1e-3) / 1e9, 1)
@@ -359,8 +362,10 @@ def main():
                          "per GPU (generated in HBM)")
     ap.add_argument("--routed", action="store_true",
                     help="config 4 through the ledger router even on one GPU (a one-rank RCCL group)")
-    ap.add_argument("--pipelined", action="store_true",
-                    help="routed: route step k + 1 while step k commits (measured slower on one GPU, r02)")
+    ap.add_argument("--pipelined", dest="pipelined", action="store_true", default=None,
+                    help="routed: step k + 1's all-to-all runs while step k commits (the default on N > 1 GPUs; "
+                         "a one-rank group has nothing to exchange)")
+    ap.add_argument("--no-pipelined", dest="pipelined", action="store_false")
     ap.add_argument("--unrouted", action="store_true",
                     help="N > 1: every rank commits its own pre-routed ledger shard (no all-to-all)")
     ap.add_argument("--force-general", action="store_true", help="disable the fast path (measure the fixed point)")
@@ -406,6 +411,8 @@ def main():
             dist.init_process_group(backend)
     if args.config is None:
         args.config = 4 if (world > 1 or args.routed) else 2
+    if args.pipelined is None:
+        args.pipelined = world > 1
 
     if args.batches_per_step is None:
         args.batches_per_step = 60 if args.config == 3 else 1000

@@ -359,8 +359,8 @@ uint64_t tbgpu_create_transfers_routed_device(tbgpu_ctx* ctx, uint32_t batch_cou
 /* One pass over a routed step's local events (device memory) deciding whether the
  * device path applies: out[0] min id (low word), out[1] max id (low word), out[2]
  * bit 0: an id not above its predecessor, bit 1: an id with a high word or zero,
- * bit 2: a post/void, bit 3: an amount of 2^64 or more, bits 16-31: bit 16 + w set
- * when 8-byte word w (0-15) of some event is nonzero (the packed wire format's
+ * bit 2: a post/void, bit 3: an amount of 2^64 or more, bits 16-47: bit 16 + w set
+ * when 4-byte word w (0-31) of some event is nonzero (the packed wire format's
  * mask, tbgpu_route_scatter_packed); out[3], out[4]: the sum of the amounts (low,
  * high word).  Returns 0.  Synchronous. */
 int tbgpu_route_stats(tbgpu_ctx* ctx, const void* events_device, uint64_t count, uint64_t* out);
@@ -372,11 +372,12 @@ int tbgpu_route_scatter(tbgpu_ctx* ctx, uint32_t world, uint32_t batch_count, co
                         const uint64_t* batch_timestamps, uint64_t first_global_batch, const void* events_device,
                         void* send_events_device, void* send_records_device, uint64_t* send_counts,
                         uint32_t* send_batch_counts, uint32_t* send_span_counts);
-/* tbgpu_route_scatter in the packed wire format: per event, the 8-byte words w of
- * the event with bit w of `word_mask` set (in word order), then its record
- * (TBGPU_ROUTE_REC_*): popcount(word_mask) + 1 words, owner-major in
+/* tbgpu_route_scatter in the packed wire format: per event, the 4-byte words w of
+ * the event with bit w of `word_mask` set (in word order), then the low word of its
+ * record (TBGPU_ROUTE_REC_*; the owner knows each row's batch from the per-(owner,
+ * batch) counts): popcount(word_mask) + 1 words of 4 bytes, owner-major in
  * `send_device`.  The mask is normally the union over the ranks of
- * tbgpu_route_stats' nonzero-word bits (config 4's events: 9 of 16 words, so 80
+ * tbgpu_route_stats' nonzero-word bits (config 4's events: 15 of 32 words, so 64
  * bytes on the wire instead of 136); an event with a nonzero word outside it
  * returns -22 (nothing is lost silently).  Synchronous. */
 int tbgpu_route_scatter_packed(tbgpu_ctx* ctx, uint32_t world, uint32_t batch_count, const uint32_t* counts,
@@ -385,12 +386,16 @@ int tbgpu_route_scatter_packed(tbgpu_ctx* ctx, uint32_t world, uint32_t batch_co
                                uint32_t* send_span_counts);
 /* The owner side of the packed format: `count` received rows of
  * popcount(word_mask) + 1 words back to whole 128-byte events (words outside the
- * mask zero) in `events_device`, their records in `records_device` (count * 8 B)
- * and their timestamps as tbgpu_route_unpack computes them.  Returns 0, or -22 when
- * a record names a batch >= batches.  Synchronous. */
+ * mask zero) in `events_device`, their whole records in `records_device` (count * 8
+ * B) and their timestamps as tbgpu_route_unpack computes them.  The rows are the
+ * owner's sub-batches in global order: sub-batch k starts at row
+ * `sub_offsets_device[k]` (uint32, sub_batch_count + 1 entries, the last = count)
+ * and belongs to global batch `sub_batches_device[k]` (uint32).  Returns 0, or -22
+ * when a batch is >= batches.  Synchronous. */
 int tbgpu_route_unpack_packed(tbgpu_ctx* ctx, const void* packed_device, uint64_t count, uint32_t word_mask,
-                              const void* ts_base_device, uint64_t batches, void* events_device,
-                              void* records_device, void* timestamps_device);
+                              uint32_t sub_batch_count, const void* sub_offsets_device,
+                              const void* sub_batches_device, const void* ts_base_device, uint64_t batches,
+                              void* events_device, void* records_device, void* timestamps_device);
 /* The owner side: event timestamps from received records, timestamps[i] =
  * ts_base[batch of record i] + index + 1 with ts_base[g] = T_g - n_g of global batch
  * g (src/vsr/replica.zig:5148-5157; `batches` entries, device memory).  Returns 0,

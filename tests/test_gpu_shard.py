@@ -90,9 +90,9 @@ def test_route_scatter_matches_torch_partition():
 @pytest.mark.gpu
 def test_route_packed_wire_format_round_trip():
     """tbgpu_route_scatter_packed + tbgpu_route_unpack_packed (the all-to-all's wire
-    format: the step's nonzero 8-byte words, then the record) give back exactly the
+    format: the step's nonzero 4-byte words, then the record's low word) give back exactly the
     torch partition's rows, records and timestamps, for masks from the events' own
-    nonzero words (tbgpu_route_stats) to all 16; a mask missing a nonzero word fails."""
+    nonzero words (tbgpu_route_stats) to all 32; a mask missing a nonzero word fails."""
     import numpy as np
     import torch
 
@@ -116,30 +116,36 @@ def test_route_packed_wire_format_round_trip():
     ev = torch.from_numpy(t.view(np.uint8).copy()).to(dev)
     bts = np.cumsum(np.array(counts, dtype=np.uint64) + 1) + 1000
     tsb = torch.tensor([0] * 5 + [int(b) - c for b, c in zip(bts, counts)], dtype=torch.int64, device=dev)
-    w64 = t.view(np.uint64).reshape(n, 16)
-    want_mask = sum(1 << w for w in range(16) if w64[:, w].any())
+    w32 = t.view(np.uint32).reshape(n, 32)
+    want_mask = sum(1 << w for w in range(32) if w32[:, w].any())
     eng = Engine(device=0, accounts_max=16, transfers_max=16, events_per_call_max=1 << 12)
     try:
         *_, got_mask = eng.route_stats(ev, n, world=3, word_mask=True)
         assert got_mask == want_mask
         for W in (1, 3, 8):
             e_t, s_t, c_t, b_t, p_t = partition_torch(torch, ev, counts, bts, 5, W, dev, detail=True)
-            for mask in (want_mask, want_mask | 0x8001, 0xFFFF):
+            # the whole send buffer as one owner's input: sub-batches owner-major, then by batch
+            bcn = b_t.cpu().numpy()
+            sub_c = [int(bcn[o, b]) for o in range(W) for b in range(len(counts)) if bcn[o, b]]
+            sub_g = [5 + b for o in range(W) for b in range(len(counts)) if bcn[o, b]]
+            sub_off = torch.tensor(np.concatenate([[0], np.cumsum(sub_c)]), dtype=torch.int32, device=dev)
+            sub_gt = torch.tensor(sub_g, dtype=torch.int32, device=dev)
+            for mask in (want_mask, want_mask | 0x80000001, 0xFFFFFFFF):
                 k = bin(mask).count("1") + 1
-                send = torch.empty((n, k), dtype=torch.int64, device=dev)
+                send = torch.empty((n, k), dtype=torch.int32, device=dev)
                 c_n, b_n, p_n = eng.route_scatter_packed(W, counts, 5, ev, mask, send)
                 assert c_n.tolist() == c_t.cpu().tolist() and b_n.tolist() == b_t.cpu().tolist()
                 assert p_n.tolist() == p_t.cpu().tolist()
                 e_n = torch.empty((n, 128), dtype=torch.uint8, device=dev)
                 s_n = torch.empty(n, dtype=torch.int64, device=dev)
                 ts_n = torch.empty(n, dtype=torch.int64, device=dev)
-                eng.route_unpack_packed(send, mask, tsb, e_n, s_n, ts_n)
+                eng.route_unpack_packed(send, mask, sub_off, sub_gt, tsb, e_n, s_n, ts_n)
                 assert torch.equal(e_n, e_t), (W, mask)
                 assert torch.equal(s_n, s_t), (W, mask)
                 assert torch.equal(ts_n, tsb[s_t >> 32] + (s_t & 0x1FFF) + 1), (W, mask)
         with pytest.raises(ValueError):
-            send = torch.empty((n, 16), dtype=torch.int64, device=dev)
-            eng.route_scatter_packed(3, counts, 5, ev, want_mask & ~(1 << 13), send)  # drops the timeouts
+            send = torch.empty((n, 32), dtype=torch.int32, device=dev)
+            eng.route_scatter_packed(3, counts, 5, ev, want_mask & ~(1 << 27), send)  # drops the timeouts
     finally:
         eng.close()
 

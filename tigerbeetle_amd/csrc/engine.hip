@@ -980,9 +980,10 @@ extern "C" int tbgpu_route_stats(tbgpu_ctx* c, const void* events_device, uint64
 }
 void route_scatter(const Transfer* ev, u64 n, u32 world, u32 nb, const u32* b_start, const u64* b_ts, u64 g0,
                    uint2* orank, u32* blk, u64* counts, Transfer* out_ev, u64* out_side, u32* bcount, u32* scount,
-                   u32 pack_mask, u64* out_packed, u32* error, bool ranked, hipStream_t stream);
-void route_unpack_rows(const u64* packed, u64 m, u32 mask, const u64* ts_base, u64 batches, Transfer* rows, u64* rec,
-                       u64* ts, u32* error, hipStream_t stream);
+                   u32 pack_mask, u32* out_packed, u32* error, bool ranked, hipStream_t stream);
+void route_unpack_rows(const u32* packed, u64 m, u32 mask, const u32* sub_off, const u32* sub_g, u32 nsub,
+                       const u64* ts_base, u64 batches, Transfer* rows, u64* rec, u64* ts, u32* error,
+                       hipStream_t stream);
 void route_rank(const Transfer* ev, u64 n, u32 world, uint2* orank, u32* blk, u64* part, u64* stats,
                 hipStream_t stream);
 void route_unpack(const u64* rec, u64 n, const u64* ts_base, u64 batches, u64* ts, u32* error, hipStream_t stream);
@@ -1050,7 +1051,7 @@ static int route_scatter_any(tbgpu_ctx* c, uint32_t world, uint32_t batch_count,
                              c->route_stream));
     route_scatter((const Transfer*)events_device, n, world, batch_count, c->ro_bstart, nullptr, first_global_batch,
                   c->ro_orank, c->ro_blk, c->ro_counts, (Transfer*)send_events_device, (u64*)send_records_device,
-                  c->ro_bcount + 256, c->ro_bcount, word_mask, (u64*)send_packed_device, err, ranked, c->route_stream);
+                  c->ro_bcount + 256, c->ro_bcount, word_mask, (u32*)send_packed_device, err, ranked, c->route_stream);
     HIP_CHECK(hipMemcpyAsync(send_counts, c->ro_counts, world * sizeof(u64), hipMemcpyDeviceToHost, c->route_stream));
     if (send_batch_counts)
         HIP_CHECK(hipMemcpyAsync(send_batch_counts, c->ro_bcount + 256, (u64)world * batch_count * sizeof(u32),
@@ -1076,19 +1077,22 @@ extern "C" int tbgpu_route_scatter_packed(tbgpu_ctx* c, uint32_t world, uint32_t
                                           uint64_t first_global_batch, const void* events_device, uint32_t word_mask,
                                           void* send_device, uint64_t* send_counts, uint32_t* send_batch_counts,
                                           uint32_t* send_span_counts) {
-    if (word_mask == 0 || word_mask > 0xFFFFu) return -22;
+    if (word_mask == 0) return -22;
     return route_scatter_any(c, world, batch_count, counts, first_global_batch, events_device, nullptr, nullptr,
                              word_mask, send_device, send_counts, send_batch_counts, send_span_counts);
 }
 
 extern "C" int tbgpu_route_unpack_packed(tbgpu_ctx* c, const void* packed_device, uint64_t count, uint32_t word_mask,
-                                         const void* batch_ts_base_device, uint64_t batches, void* events_device,
-                                         void* records_device, void* timestamps_device) {
+                                         uint32_t sub_batch_count, const void* sub_offsets_device,
+                                         const void* sub_batches_device, const void* batch_ts_base_device,
+                                         uint64_t batches, void* events_device, void* records_device,
+                                         void* timestamps_device) {
     HIP_CHECK(hipSetDevice(c->device));
-    if (word_mask == 0 || word_mask > 0xFFFFu) return -22;
+    if (word_mask == 0 || (count && sub_batch_count == 0)) return -22;
     u32* err = (u32*)(c->rt_stats + 6);
     HIP_CHECK(hipMemsetAsync(err, 0, sizeof(u32), c->route_stream));
-    route_unpack_rows((const u64*)packed_device, count, word_mask, (const u64*)batch_ts_base_device, batches,
+    route_unpack_rows((const u32*)packed_device, count, word_mask, (const u32*)sub_offsets_device,
+                      (const u32*)sub_batches_device, sub_batch_count, (const u64*)batch_ts_base_device, batches,
                       (Transfer*)events_device, (u64*)records_device, (u64*)timestamps_device, err, c->route_stream);
     u32 e = 0;
     HIP_CHECK(hipMemcpyAsync(&e, err, sizeof(u32), hipMemcpyDeviceToHost, c->route_stream));

@@ -39,11 +39,11 @@ struct RouteArgs {
     u32* bcount;          // [world * nb] events per (owner, local batch)
     u32* scount;          // [world] events per owner whose chain spans owners
     u64* stats;           // rt_rank: the eligibility figures of rt_stats (out[0..4]), or null
-    // packed wire format (pack_mask != 0): per event the 8-byte words of `pack_mask`
-    // in word order, then the record, in out_packed; a nonzero word outside the mask
-    // sets *error (the step must not lose data)
+    // packed wire format (pack_mask != 0): per event the 4-byte words of `pack_mask`
+    // in word order, then the record's low word (the owner knows the batch), in
+    // out_packed; a nonzero word outside the mask sets *error (nothing is lost silently)
     u32 pack_mask;
-    u64* out_packed;
+    u32* out_packed;
     u32* error;
 };
 
@@ -79,7 +79,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_rank(RouteArgs A) {
     const u64 i = (u64)blockIdx.x * RT_THREADS + tid;
     const u64 wbase = i - lane;
     const bool v = i < A.n;
-    // with the figures, every piece is read: the step's nonzero 8-byte words (the
+    // with the figures, every piece is read: the step's nonzero 4-byte words (the
     // packed wire format's mask) come from the same pass
     u32 nzw = 0;
     {
@@ -98,9 +98,9 @@ __global__ __launch_bounds__(RT_THREADS) void rt_rank(RouteArgs A) {
         for (int r = 0; r < 8; r++) {
             const u32 k = (u32)r * 8 + (lane >> 3);
             if (sl >= 0 && wbase + k < A.n) s_pc[w][k][sl] = x[r];
-            nzw |= ((x[r].x | x[r].y) ? 1u : 0u) | ((x[r].z | x[r].w) ? 2u : 0u);
+            nzw |= (x[r].x ? 1u : 0u) | (x[r].y ? 2u : 0u) | (x[r].z ? 4u : 0u) | (x[r].w ? 8u : 0u);
         }
-        nzw <<= 2 * piece;
+        nzw <<= 4 * piece;
     }
     uint4 pidv = make_uint4(0, 0, 0, 0);
     if (A.stats && lane == 0 && v && i > 0) pidv = *(const uint4*)&A.ev[i - 1].id;
@@ -218,7 +218,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scatter(RouteArgs A) {
     __shared__ u32 s_dst[RT_THREADS];
     __shared__ u64 s_rec[RT_THREADS];
     __shared__ u32 s_b0;
-    __shared__ u8 s_sel[16];                 // the packed row's word k is row word s_sel[k]
+    __shared__ u8 s_sel[32];                 // the packed row's word k is row word s_sel[k]
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const u32 blk0 = blockIdx.x * RT_THREADS;
     const u64 i = (u64)blk0 + tid;
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scatter(RouteArgs A) {
         // the workgroup's first batch by one binary search; each event steps on from it
         s_b0 = rt_batch(A, blk0);
         u32 k = 0;
-        for (u32 wd = 0; wd < 16; wd++)
+        for (u32 wd = 0; wd < 32; wd++)
             if (A.pack_mask >> wd & 1) s_sel[k++] = (u8)wd;
     }
     {
@@ -244,9 +244,9 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scatter(RouteArgs A) {
         for (int r = 0; r < 8; r++) {
             const u32 k = (u32)r * 8 + (lane >> 3);
             s_rows[w * 64 + k][piece] = x[r];
-            lost |= ((x[r].x | x[r].y) ? 1u : 0u) | ((x[r].z | x[r].w) ? 2u : 0u);
+            lost |= (x[r].x ? 1u : 0u) | (x[r].y ? 2u : 0u) | (x[r].z ? 4u : 0u) | (x[r].w ? 8u : 0u);
         }
-        if (A.pack_mask && ((lost << 2 * piece) & ~A.pack_mask)) atomicOr(A.error, 1u);
+        if (A.pack_mask && ((lost << 4 * piece) & ~A.pack_mask)) atomicOr(A.error, 1u);
     }
     uint2 orr = make_uint2(0, 0);
     const bool v = i < A.n;
@@ -316,27 +316,31 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scatter(RouteArgs A) {
     const u32 K = (u32)__popc(A.pack_mask) + 1;  // words per packed row
     for (u32 f = lane; f < nv * K; f += 64) {
         const u32 rr = f / K, wd = f - rr * K, row = w * 64 + rr;
-        const u64 val = wd + 1 < K ? ((const u64*)&s_rows[row][0])[s_sel[wd]] : s_rec[row];
+        const u32 val = wd + 1 < K ? ((const u32*)&s_rows[row][0])[s_sel[wd]] : (u32)s_rec[row];
         A.out_packed[(u64)s_dst[row] * K + wd] = val;
     }
 }
 
 // The owner side of the packed format: rows of K = popcount(mask) + 1 words back to
-// whole 128-byte rows (the words outside the mask are zero), the records, and each
-// event's timestamp ts_base[g] + index + 1 (src/vsr/replica.zig:5148-5157).
-__global__ __launch_bounds__(RT_THREADS) void rt_unpack_rows(const u64* __restrict__ packed, u64 m, u32 mask,
+// whole 128-byte rows (the words outside the mask are zero), the records (global
+// batch from the sub-batch the row falls in: the owner's sub-batches are in global
+// order, `sub_off[k]` the first row of sub-batch k, `sub_g[k]` its global batch), and
+// each event's timestamp ts_base[g] + index + 1 (src/vsr/replica.zig:5148-5157).
+__global__ __launch_bounds__(RT_THREADS) void rt_unpack_rows(const u32* __restrict__ packed, u64 m, u32 mask,
+                                                             const u32* __restrict__ sub_off,
+                                                             const u32* __restrict__ sub_g, u32 nsub,
                                                              const u64* __restrict__ ts_base, u64 batches,
                                                              Transfer* __restrict__ rows, u64* __restrict__ rec,
                                                              u64* __restrict__ ts, u32* error) {
     __shared__ uint4 s_rows[RT_THREADS][8];
-    __shared__ u8 s_sel[16];
+    __shared__ u8 s_sel[32];
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const u64 i = (u64)blockIdx.x * RT_THREADS + tid;
     const u64 wbase = i - lane;
     const u32 K = (u32)__popc(mask) + 1;
     if (tid == 0) {
         u32 k = 0;
-        for (u32 wd = 0; wd < 16; wd++)
+        for (u32 wd = 0; wd < 32; wd++)
             if (mask >> wd & 1) s_sel[k++] = (u8)wd;
     }
 #pragma unroll
@@ -345,13 +349,19 @@ __global__ __launch_bounds__(RT_THREADS) void rt_unpack_rows(const u64* __restri
     const u32 nv = (u32)min<u64>(64, m > wbase ? m - wbase : 0);
     for (u32 f = lane; f < nv * K; f += 64) {
         const u32 rr = f / K, wd = f - rr * K;
-        const u64 val = packed[wbase * K + f];
+        const u32 val = packed[wbase * K + f];
         if (wd + 1 < K) {
-            ((u64*)&s_rows[w * 64 + rr][0])[s_sel[wd]] = val;
+            ((u32*)&s_rows[w * 64 + rr][0])[s_sel[wd]] = val;
         } else {
-            const u64 j = wbase + rr, g = val >> 32;
-            rec[j] = val;
-            if (g >= batches) {
+            const u32 j = (u32)(wbase + rr);
+            u32 lo = 0, hi = nsub;  // the last sub-batch starting at or before row j
+            while (hi - lo > 1) {
+                const u32 mid = (lo + hi) / 2;
+                if (sub_off[mid] <= j) lo = mid; else hi = mid;
+            }
+            const u64 g = sub_g[lo];
+            rec[j] = (g << 32) | val;
+            if (g >= batches || nsub == 0 || j >= sub_off[nsub]) {
                 atomicOr(error, 1u);
                 ts[j] = 0;
             } else {
@@ -421,7 +431,8 @@ __global__ __launch_bounds__(RT_THREADS) void rt_stats(const Transfer* ev, u64 n
             } else if (piece == 7) {
                 if ((v[u].y >> 16) & (TF_POST | TF_VOID)) fl |= 4;
             }
-            fl |= (u64)(((v[u].x | v[u].y) ? 1u : 0u) | ((v[u].z | v[u].w) ? 2u : 0u)) << (16 + 2 * piece);
+            fl |= (u64)((v[u].x ? 1u : 0u) | (v[u].y ? 2u : 0u) | (v[u].z ? 4u : 0u) | (v[u].w ? 8u : 0u))
+                  << (16 + 4 * piece);
         }
     }
     rt_stats_block(mn, mx, fl, slo, shi, out, nullptr);
@@ -527,9 +538,9 @@ void route_unpack(const u64* rec, u64 n, const u64* ts_base, u64 batches, u64* t
 
 void route_scatter(const Transfer* ev, u64 n, u32 world, u32 nb, const u32* b_start, const u64* b_ts, u64 g0,
                    uint2* orank, u32* blk, u64* counts, Transfer* out_ev, u64* out_side, u32* bcount, u32* scount,
-                   u32 pack_mask, u64* out_packed, u32* error, bool ranked, hipStream_t stream) {
+                   u32 pack_mask, u32* out_packed, u32* error, bool ranked, hipStream_t stream) {
     RouteArgs A{};
-    A.pack_mask = pack_mask & 0xFFFFu;
+    A.pack_mask = pack_mask;
     A.out_packed = out_packed;
     A.error = error;
     A.bcount = bcount;
@@ -545,10 +556,10 @@ void route_scatter(const Transfer* ev, u64 n, u32 world, u32 nb, const u32* b_st
     HIP_CHECK(hipGetLastError());
 }
 
-void route_unpack_rows(const u64* packed, u64 m, u32 mask, const u64* ts_base, u64 batches, Transfer* rows, u64* rec,
-                       u64* ts, u32* error, hipStream_t stream) {
-    if (m) rt_unpack_rows<<<(u32)((m + RT_THREADS - 1) / RT_THREADS), RT_THREADS, 0, stream>>>(packed, m, mask & 0xFFFFu,
-                                                                                              ts_base, batches, rows,
-                                                                                              rec, ts, error);
+void route_unpack_rows(const u32* packed, u64 m, u32 mask, const u32* sub_off, const u32* sub_g, u32 nsub,
+                       const u64* ts_base, u64 batches, Transfer* rows, u64* rec, u64* ts, u32* error,
+                       hipStream_t stream) {
+    if (m) rt_unpack_rows<<<(u32)((m + RT_THREADS - 1) / RT_THREADS), RT_THREADS, 0, stream>>>(
+        packed, m, mask, sub_off, sub_g, nsub, ts_base, batches, rows, rec, ts, error);
     HIP_CHECK(hipGetLastError());
 }

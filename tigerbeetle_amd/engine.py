@@ -114,7 +114,7 @@ def lib():
     L.tbgpu_route_scatter_packed.restype = ctypes.c_int
     L.tbgpu_route_scatter_packed.argtypes = [vp, u32, u32, vp, u64, vp, u32, vp, vp, vp, vp]
     L.tbgpu_route_unpack_packed.restype = ctypes.c_int
-    L.tbgpu_route_unpack_packed.argtypes = [vp, vp, u64, u32, vp, u64, vp, vp, vp]
+    L.tbgpu_route_unpack_packed.argtypes = [vp, vp, u64, u32, u32, vp, vp, vp, u64, vp, vp, vp]
     L.tbgpu_route_unpack.restype = ctypes.c_int
     L.tbgpu_route_unpack.argtypes = [vp, vp, u64, vp, u64, vp]
     L.tbgpu_import_transfers.restype = ctypes.c_int
@@ -289,9 +289,9 @@ class Engine:
 
     def route_scatter_packed(self, world: int, counts, first_global_batch: int, events, word_mask: int, send):
         """tbgpu_route_scatter_packed: `events` (uint8 device tensor, n*128 B) to the
-        owner-major packed rows of `send` (int64 device tensor [n, popcount(mask) + 1]:
-        the event's words of `word_mask`, then its record).  Returns (events per
-        owner, events per (owner, batch), spanning events per owner)."""
+        owner-major packed rows of `send` (int32 device tensor [n, popcount(mask) + 1]:
+        the event's 4-byte words of `word_mask`, then its record's low word).  Returns
+        (events per owner, events per (owner, batch), spanning events per owner)."""
         import torch
         torch.cuda.current_stream(events.device).synchronize()
         cs = np.ascontiguousarray(counts, dtype=np.uint32)
@@ -305,13 +305,19 @@ class Engine:
             raise ValueError(f"tbgpu_route_scatter_packed failed ({rc}): an event word outside mask {word_mask:#x}?")
         return out, bc[:, :len(cs)], sp
 
-    def route_unpack_packed(self, packed, word_mask: int, ts_base, events, records, timestamps) -> None:
-        """tbgpu_route_unpack_packed: received packed rows (int64 device tensor [m, K])
-        back to events (uint8 [m*128]), records and timestamps (int64 [m])."""
+    def route_unpack_packed(self, packed, word_mask: int, sub_offsets, sub_batches, ts_base, events, records,
+                            timestamps) -> None:
+        """tbgpu_route_unpack_packed: received packed rows (int32 device tensor [m, K]) of
+        the sub-batches starting at rows `sub_offsets` (int32 device tensor, + the end)
+        of global batches `sub_batches` back to events (uint8 [m*128]), records and
+        timestamps (int64 [m])."""
         import torch
         torch.cuda.current_stream(packed.device).synchronize()
         rc = self._L.tbgpu_route_unpack_packed(self._h, ctypes.c_void_p(packed.data_ptr()), int(packed.shape[0]),
-                                               int(word_mask), ctypes.c_void_p(ts_base.data_ptr()),
+                                               int(word_mask), int(sub_batches.numel()),
+                                               ctypes.c_void_p(sub_offsets.data_ptr()),
+                                               ctypes.c_void_p(sub_batches.data_ptr()),
+                                               ctypes.c_void_p(ts_base.data_ptr()),
                                                int(ts_base.numel()), ctypes.c_void_p(events.data_ptr()),
                                                ctypes.c_void_p(records.data_ptr()),
                                                ctypes.c_void_p(timestamps.data_ptr()))
@@ -323,7 +329,7 @@ class Engine:
         monotone, plain ids, any post/void, any amount >= 2^64, amount sum).  With
         `world`, tbgpu_route_prepare: the same figures from the pass that also ranks the
         events for a route_scatter of them to `world` owners (which then skips it).
-        With `word_mask`, also the mask of the 8-byte words nonzero in some event."""
+        With `word_mask`, also the mask of the 4-byte words nonzero in some event."""
         import torch
         torch.cuda.current_stream(events.device).synchronize()
         out = np.zeros(5, dtype=np.uint64)
@@ -336,7 +342,7 @@ class Engine:
         fl = int(out[2])
         r = (int(out[0]), int(out[1]), not (fl & 1), not (fl & 2), bool(fl & 4), bool(fl & 8),
              int(out[3]) | (int(out[4]) << 64))
-        return r + ((fl >> 16) & 0xFFFF,) if word_mask else r
+        return r + ((fl >> 16) & 0xFFFFFFFF,) if word_mask else r
 
     def route_unpack(self, records, ts_base, timestamps) -> None:
         """tbgpu_route_unpack: event timestamps (int64 device tensor) from received

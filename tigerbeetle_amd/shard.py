@@ -166,6 +166,8 @@ class ShardedStateMachine:
         self.limit_ids: set[int] = set()  # ids of accounts created with a balance limit flag
         self.amount_bound = 0.0  # >= the sum of every transfer amount routed: bounds every balance
         self.timed = False       # accumulate per-phase wall times of the device step (with syncs)
+        self.wire_bytes_per_event = 0  # the last device step's all-to-all bytes per event
+        self._worker = None       # the pipelined stream's commit thread
         self.timing = {"eligibility_ms": 0.0, "order_ms": 0.0, "partition_ms": 0.0, "exchange_ms": 0.0,
                        "commit_ms": 0.0, "replies_ms": 0.0}
         self.stats = {"steps": 0, "splits": 0, "dry_rounds": 0, "cross_chains": 0, "imports": 0,
@@ -277,26 +279,34 @@ class ShardedStateMachine:
         st = self.route_device(events, counts)
         if st.fallback:
             return self._host_step(st.ev, st.counts, st.offs_h)
+        self.exchange_device(st)
         self.commit_routed(st)
         return self.finish_routed(st)
 
     def create_transfers_device_stream(self, steps):
         """create_transfers_device over consecutive steps ((events, counts) pairs),
-        pipelined: while step k's owner commit runs on a worker thread, step k + 1 is
-        routed (eligibility, scatter, all-to-all).  Yields each step's replies, equal to
+        pipelined: step k + 1 is routed (eligibility, scatter: HBM-bound) before step
+        k's owner commit starts, and its all-to-all (xGMI-bound) runs while that commit
+        runs on a worker thread.  Yields each step's replies, equal to
         create_transfers_device's (the results do not depend on the overlap)."""
         it = iter(steps)
         nxt = next(it, None)
         st = self.route_device(*nxt) if nxt is not None else None
+        if st is not None and not st.fallback:
+            self.exchange_device(st)
         while st is not None:
             if st.fallback:
                 yield self._host_step(st.ev, st.counts, st.offs_h)
                 nxt = next(it, None)
                 st = self.route_device(*nxt) if nxt is not None else None
+                if st is not None and not st.fallback:
+                    self.exchange_device(st)
                 continue
-            self.commit_routed(st, background=True)
             nxt = next(it, None)
             st2 = self.route_device(*nxt) if nxt is not None else None
+            self.commit_routed(st, background=True)
+            if st2 is not None and not st2.fallback:
+                self.exchange_device(st2)
             yield self.finish_routed(st)
             st = st2
 
@@ -324,7 +334,7 @@ class ShardedStateMachine:
         native = n and ev.is_cuda and hasattr(self.backend, "route_scatter")
         # this rank can send and receive the packed wire format (csrc/route.hip)
         can_pack = W > 1 and ev.is_cuda and hasattr(self.backend, "route_scatter_packed")
-        wmask = 0xFFFF
+        wmask = 0xFFFFFFFF
         if n and ev.is_cuda and hasattr(self.backend, "route_stats"):
             # one pass of the engine's kernel (csrc/route.hip) instead of the torch reductions;
             # the same pass ranks the events for the scatter below and finds their nonzero words
@@ -346,7 +356,7 @@ class ShardedStateMachine:
             st = [0, 0, 0, 1, 1, 0]
         # the packed format's words and capability, then the batch counts of the step
         # (the global order), in the same all-gather
-        st += [(wmask if n else 0) | (int(can_pack) << 16)]
+        st += [(wmask if n else 0) | (int(can_pack) << 32)]
         nb_here = len(counts)
         st += [nb_here] + (list(map(int, counts)) if nb_here <= NB_GATHER else []) + \
             [0] * (NB_GATHER - (nb_here if nb_here <= NB_GATHER else 0))
@@ -373,12 +383,12 @@ class ShardedStateMachine:
 
         # global order and timestamps (host: one entry per batch)
         # every rank packs when every rank can: the union of the nonzero words travels
-        packed = W > 1 and all(x[6] >> 16 for x in allst)
+        packed = W > 1 and all(x[6] >> 32 for x in allst)
         pmask = 0
         for x in allst:
-            pmask |= x[6] & 0xFFFF
+            pmask |= x[6] & 0xFFFFFFFF
         pmask = pmask or 1
-        K = bin(pmask).count("1") + 1  # int64 words per packed row: the masked words, the record
+        K = bin(pmask).count("1") + 1  # 4-byte words per packed row: the masked words, the record
         if all(x[7] <= NB_GATHER for x in allst):
             counts_all = [x[8:8 + x[7]] for x in allst]
         else:
@@ -394,7 +404,7 @@ class ShardedStateMachine:
         send = None
         if packed:
             # the engine's scatter straight into the packed wire format (csrc/route.hip)
-            send = torch.empty((n, K), dtype=torch.int64, device=dev)
+            send = torch.empty((n, K), dtype=torch.int32, device=dev)
             if n:
                 sc, bc, spc = self.backend.route_scatter_packed(W, list(map(int, counts)), g0, ev, pmask, send)
             else:
@@ -426,28 +436,52 @@ class ShardedStateMachine:
             rmeta = rmeta.cpu().numpy()
         else:
             rmeta = meta.reshape(-1)
-        sl, rl, sub_counts, n_span, span_sent = [int(x) for x in sc], [], [], 0, 0
-        off = 0
+        sl, rl, sub_counts, sub_g, n_span, span_sent = [int(x) for x in sc], [], [], [], 0, 0
+        off = gb = 0
         for k in nbs:
             row = rmeta[off:off + 3 + k]
             rl.append(int(row[0]))
             n_span += int(row[1])
             span_sent += int(row[2])
-            sub_counts += [int(c) for c in row[3:] if c]
+            nz = np.nonzero(row[3:])[0]
+            sub_counts += row[3:][nz].tolist()
+            sub_g += (nz + gb).tolist()
             off += 3 + k
+            gb += k
         m = int(sum(rl))
+        clock("exchange_ms")
+        # phase 1b (exchange_device) moves the events: the all-to-all over xGMI, which a
+        # pipelined stream overlaps with the previous step's owner commit
+        return SimpleNamespace(**{k: v for k, v in locals().items() if k not in ("self", "clock")},
+                               fallback=False)
+
+    def exchange_device(self, st):
+        """Phase 1b of a device step: the all-to-all of the events (packed wire format
+        when every rank runs the engine's kernels), the owner-side unpack (rows,
+        records, timestamps), and what the owner needs to settle cross-shard chains."""
+        torch = self.comm.torch
+        clock = self._clock()
+        g = st.__dict__
+        dev, W, m, T, glob, packed, K, pmask = (g[x] for x in ("dev", "W", "m", "T", "glob", "packed", "K", "pmask"))
+        rl, sl, sub_counts, sub_g, n_span, span_sent = (g[x] for x in ("rl", "sl", "sub_counts", "sub_g", "n_span",
+                                                                       "span_sent"))
+        send, ev_s, side_s = g.pop("send"), g.pop("ev_s"), g.pop("side_s")
+        self.wire_bytes_per_event = 4 * K if packed else 128 + 8  # what the all-to-all moves per event
         # the received events' timestamps: T - n + index + 1 of their global batch
         tsb = torch.tensor([T[k] - glob[k][2] for k in range(len(glob))], dtype=torch.int64, device=dev)
         ts_r = None
         if packed:
-            recv = torch.empty((m, K), dtype=torch.int64, device=dev)
+            recv = torch.empty((m, K), dtype=torch.int32, device=dev)
             self.comm.dist.all_to_all_single(recv, send, rl, sl, group=self.comm.group)
-            del send
+            send = None
             R = torch.empty((m, 128), dtype=torch.uint8, device=dev)
             S = torch.empty(m, dtype=torch.int64, device=dev)
             ts_r = torch.empty(m, dtype=torch.int64, device=dev)
             if m:
-                self.backend.route_unpack_packed(recv, pmask, tsb, R, S, ts_r)
+                # each row's global batch: the owner's sub-batches arrive in global order
+                sub = torch.tensor(np.concatenate([[0], np.cumsum(sub_counts), sub_g]).astype(np.int32), device=dev)
+                ns = len(sub_counts)
+                self.backend.route_unpack_packed(recv, pmask, sub[:ns + 1], sub[ns + 1:], tsb, R, S, ts_r)
             del recv
         elif W > 1:
             R = torch.empty((m, 128), dtype=torch.uint8, device=dev)
@@ -456,7 +490,7 @@ class ShardedStateMachine:
             self.comm.dist.all_to_all_single(S, side_s, rl, sl, group=self.comm.group)
         else:  # one owner: the send buffers are what it receives
             R, S = ev_s, side_s
-        del ev_s, side_s
+        ev_s = side_s = None
         clock("exchange_ms")
 
         # owner side: sub-batches in global order (from the senders' counts), chain control
@@ -489,15 +523,14 @@ class ShardedStateMachine:
         all_plain = True
         if any_span:
             all_plain = all(self.comm.all_gather_object(plain_local)) and self.amount_bound < 2.0**125
-        return SimpleNamespace(**{k: v for k, v in locals().items() if k not in ("self", "clock")},
-                               fallback=False)
+        g.update({k: v for k, v in locals().items() if k not in ("self", "clock", "g", "st", "torch")})
+        return st
 
     def commit_routed(self, st, background: bool = False):
         """Phase 2: settle the step's cross-shard chains (collectives, on this thread),
         then the owner commit -- on a worker thread when `background`, so that the next
         step's routing (phase 1) overlaps it.  Sets st.out / st.at / st.cts (or, after a
         device fallback, st.replies)."""
-        import threading
         torch = self.comm.torch
         clock = self._clock()
         g = st.__dict__
@@ -627,8 +660,12 @@ class ShardedStateMachine:
                         sub_counts, Rf, ts_r, final_ctl, False, results, sync_inputs=False)
                 except BaseException as e:  # noqa: BLE001 -- re-raised by finish_routed
                     box["error"] = e
-            st.thread = threading.Thread(target=run)
-            st.thread.start()
+            # one long-lived worker: a fresh OS thread per step paid the HIP runtime's
+            # per-thread setup on every commit
+            if self._worker is None:
+                from concurrent.futures import ThreadPoolExecutor
+                self._worker = ThreadPoolExecutor(max_workers=1, thread_name_prefix="tb-commit")
+            st.thread = self._worker.submit(run)
             st.box, st.decode, st.offs = box, decode, offs
             return st
         out, at, cts = commit(final_ctl, False)
@@ -644,7 +681,7 @@ class ShardedStateMachine:
         if st.replies is not None:
             return st.replies
         if st.thread is not None:
-            st.thread.join()
+            st.thread.result()
             if "error" in st.box:
                 raise st.box["error"]
             rc, cts = st.box["rc"]

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 import oracle
-from parity import assert_results_equal, assert_state_equal, run_workload
+from parity import assert_results_equal, assert_state_equal, per_batch_results, run_workload
 from tigerbeetle_amd import workload
 
 pytestmark = pytest.mark.gpu
@@ -347,3 +347,76 @@ def test_blocked_dense_directory(force_general):
     w4 = workload.config4(transfer_count=40_000, ledgers=20, accounts_per_ledger=200, seed=3, cross_ledger_pairs=0.02)
     st = _parity(w4, accounts_max=20 * 200, dense_block_span=200, force_general=force_general)
     assert force_general or st.path == 1
+
+
+def test_sorted_run_id_index():
+    """The id index's sorted run (engine.h xrun): monotone fast calls extend it
+    without hashing; then ids replayed from it answer `exists` (binary search),
+    posts and voids find pendings that live only in the run, a non-monotone call and
+    a call after a frozen run hash their ids, lookups see both, and a checkpoint
+    restores everything into the hash index -- all bit-exact vs the oracle."""
+    from tigerbeetle_amd.types import TRANSFER_DTYPE, TransferFlags
+    rng = np.random.default_rng(17)
+    w = workload.config1(transfer_count=8 * 8190, account_count=500, seed=3)
+    t = w.transfers
+    t["flags"][::5] = int(TransferFlags.pending)  # pendings that only the run will hold
+    ats, tts = w.timestamps()
+    calls = []
+    # 1-2: monotone plain calls (the run starts, then grows)
+    calls.append(t[:2 * 8190].copy())
+    calls.append(t[2 * 8190:4 * 8190].copy())
+    # 3: replays of run ids (exists / exists_with_different_*) next to new ids
+    c3 = t[4 * 8190:5 * 8190].copy()
+    rep = rng.choice(4 * 8190, 600, replace=False)
+    c3[:600] = t[rep]
+    c3["amount_lo"][:300] += 1
+    calls.append(c3)
+    # 4: posts and voids of pendings committed in the run (the general path)
+    pend = np.nonzero(t["flags"][:4 * 8190] == int(TransferFlags.pending))[0][:4000]
+    c4 = np.zeros(len(pend), dtype=TRANSFER_DTYPE)
+    c4["id_lo"] = 10_000_000 + np.arange(len(pend))
+    c4["pending_id_lo"] = t["id_lo"][pend]
+    c4["flags"] = np.where(np.arange(len(pend)) % 2 == 0, int(TransferFlags.post_pending_transfer),
+                           int(TransferFlags.void_pending_transfer))
+    calls.append(c4)
+    # 5: monotone again (the run is frozen: hashed); 6: non-monotone ids
+    calls.append(t[5 * 8190:6 * 8190].copy())
+    c6 = t[6 * 8190:8 * 8190].copy()
+    rng.shuffle(c6)
+    calls.append(c6)
+    orc = oracle.Oracle(len(w.accounts), 1 << 20)
+    gpu = _engine()
+    try:
+        for be in (orc, gpu):
+            be.create_accounts_batches(ats, w.account_counts, w.accounts)
+        ts = int(ats[-1])
+        for k, ev in enumerate(calls):
+            counts = np.full(len(ev) // 8190, 8190, dtype=np.uint32)
+            if len(ev) % 8190:
+                counts = np.append(counts, len(ev) % 8190).astype(np.uint32)
+            bts = ts + np.cumsum(counts.astype(np.uint64) + 1)
+            ts = int(bts[-1])
+            go, gr, _ = gpu.create_transfers_batches(bts, counts, ev)
+            oo, orr, _ = orc.create_transfers_batches(bts, counts, ev)
+            assert np.array_equal(gr, orr), k
+            assert_results_equal(per_batch_results(go, counts, gr), per_batch_results(oo, counts, orr), f"call {k}")
+            if k == 2:
+                assert int(gr.sum()) >= 600  # every replayed id answered from the run
+        assert_state_equal(gpu, orc)
+        ids = t["id_lo"][::7].tolist() + c4["id_lo"][::5].tolist() + [0, 99_999_999]
+        assert gpu.lookup_transfers(ids).tobytes() == orc.lookup_transfers(ids).tobytes()
+        image = gpu.checkpoint()
+        gpu2 = _engine()
+        try:
+            assert gpu2.open(image) == 0
+            assert gpu2.lookup_transfers(ids).tobytes() == orc.lookup_transfers(ids).tobytes()
+            again = t[:8190].copy()  # all exist, now through the rebuilt hash index
+            bts = np.array([ts + 8191], dtype=np.uint64)
+            go, gr, _ = gpu2.create_transfers_batches(bts, np.array([8190], np.uint32), again)
+            oo, orr, _ = orc.create_transfers_batches(bts, np.array([8190], np.uint32), again)
+            assert np.array_equal(gr, orr) and int(gr[0]) == 8190
+            assert go[:8190].tobytes() == oo[:8190].tobytes()
+        finally:
+            gpu2.close()
+    finally:
+        gpu.close()

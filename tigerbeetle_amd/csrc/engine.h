@@ -52,6 +52,13 @@ struct Tables {
     // written so far in the current call (the streaming reply offset).
     u64* base;
     u64 xrow_cap, hist_cap;
+    // The sorted run of the transfer-id index: rows [xrun[0], xrun[1]) of xrows were
+    // committed by calls whose ids rose strictly, each above the last id of the run,
+    // and are not in `xidx`: their ids are sorted by row, so a lookup is a binary
+    // search over the rows (an LSM table, src/lsm/tree.zig; the benchmark's
+    // sequential ids never touch the hash index).  xrun[2..3] the first id (lo, hi),
+    // xrun[4..5] the last; empty when xrun[0] == xrun[1].
+    u64* xrun;
 };
 enum { BASE_ROWS = 0, BASE_HIST = 1, BASE_REPLIES = 2 };
 
@@ -219,15 +226,35 @@ __device__ __forceinline__ u64 xidx_hash(u128 id) {
     return (hash128(lo >> 4, hi) << 4) | (lo & 15);
 }
 
-__device__ __forceinline__ u32 xidx_probe(const Tables& T, u128 id) {
-    if (!xidx_maybe_present(T, id)) return NONE32;  // outside the stored ids' key range
-    u64 h = xidx_hash(id) & T.xidx_mask;
-    for (;;) {
-        const u32 r1 = T.xidx[h];
-        if (r1 == 0) return NONE32;
-        if (T.xrows[r1 - 1].id == id) return r1 - 1;
-        h = (h + XIDX_STEP) & T.xidx_mask;
+__device__ __forceinline__ bool xrun_maybe(const Tables& T, u128 id) {
+    const u64* r = T.xrun;
+    if (r[0] == r[1]) return false;
+    return id >= (((u128)r[3] << 64) | r[2]) && id <= (((u128)r[5] << 64) | r[4]);
+}
+
+// the row of `id` in the sorted run, or NONE32
+__device__ __forceinline__ u32 xrun_find(const Tables& T, u128 id) {
+    u64 lo = T.xrun[0], hi = T.xrun[1];
+    while (lo < hi) {
+        const u64 mid = (lo + hi) / 2;
+        const u128 k = T.xrows[mid].id;
+        if (k == id) return (u32)mid;
+        if (k < id) lo = mid + 1; else hi = mid;
     }
+    return NONE32;
+}
+
+__device__ __forceinline__ u32 xidx_probe(const Tables& T, u128 id) {
+    if (xidx_maybe_present(T, id)) {  // else outside the hashed ids' key range
+        u64 h = xidx_hash(id) & T.xidx_mask;
+        for (;;) {
+            const u32 r1 = T.xidx[h];
+            if (r1 == 0) break;
+            if (T.xrows[r1 - 1].id == id) return r1 - 1;
+            h = (h + XIDX_STEP) & T.xidx_mask;
+        }
+    }
+    return xrun_maybe(T, id) ? xrun_find(T, id) : NONE32;
 }
 
 // Inserts never compare keys: a call inserts ids that are absent and distinct.
@@ -245,6 +272,7 @@ enum {
     CNT_BAD = 4,        // fast path: events with a result other than ok
     CNT_RESORT = 5,     // general path: pass + 1 whose evaluation resolved a post/void outside its sides
     CNT_LONG = 6,       // general path: pass + 1 whose fused scan met a segment longer than its window
+    CNT_RUN = 7,        // fast path: this call's rows extend the sorted run (fp_run), not the hash index
     CNT_GCUR = 8,       // general path: id-group ranges reserved so far
     CNT_PCUR = 9,       // general path: pending-group ranges reserved so far
     CNT_TS_SAVE = 12,   // fast path: commit_timestamp before the call (u64 in words 12-13)

@@ -319,6 +319,7 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     c->T.hrows = dalloc<History>(c->hist_cap, &B);
     c->T.commit_ts = dalloc<u64>(2, &B);
     c->T.idr = dalloc<u64>(4, &B);
+    c->T.xrun = dalloc<u64>(8, &B);
     c->T.big = dalloc<u32>(4, &B);
     c->T.base = dalloc<u64>(4, &B);
     c->T.xrow_cap = c->xrow_cap;
@@ -347,6 +348,7 @@ extern "C" void tbgpu_reset(tbgpu_ctx* c) {
     HIP_CHECK(hipMemsetAsync(c->T.commit_ts, 0, 2 * sizeof(u64), c->stream));
     HIP_CHECK(hipMemsetAsync(c->T.idr, 0, 2 * sizeof(u64), c->stream));                  // max = 0
     HIP_CHECK(hipMemsetAsync(c->T.idr + 2, 0xFF, 2 * sizeof(u64), c->stream));           // min = ~0
+    HIP_CHECK(hipMemsetAsync(c->T.xrun, 0, 8 * sizeof(u64), c->stream));                 // empty run
     HIP_CHECK(hipMemsetAsync(c->T.big, 0, sizeof(u32), c->stream));
     HIP_CHECK(hipMemsetAsync(c->T.base, 0, 4 * sizeof(u64), c->stream));
     if (c->T.dense_n) HIP_CHECK(hipMemsetAsync(c->T.dense, 0, c->T.dense_n * sizeof(u64), c->stream));
@@ -366,7 +368,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     for (void* p : {(void*)c->ro_orank, (void*)c->ro_blk, (void*)c->ro_bstart, (void*)c->ro_bts, (void*)c->ro_counts,
                     (void*)c->ro_bcount, (void*)c->ro_spart})
         if (p) (void)hipFree(p);
-    void* ptrs[] = {c->T.dense, c->T.acc, c->T.aidx, c->T.xrows, c->T.xful, c->T.xidx, c->T.hrows, c->T.commit_ts, c->T.idr, c->T.big, c->ev_buf,
+    void* ptrs[] = {c->T.dense, c->T.acc, c->T.aidx, c->T.xrows, c->T.xful, c->T.xidx, c->T.hrows, c->T.commit_ts, c->T.idr, c->T.xrun, c->T.big, c->ev_buf,
                     c->b_start, c->b_ts, c->ts, c->cs, c->ce, c->sres, c->dslot, c->cslot, c->pre_e, c->pre_p,
                     c->pp_dslot, c->pp_cslot, c->gslot, c->pslot, c->prev_id, c->pend_last, c->pend_first, c->prev_pend,
                     c->gclaim, c->gcnt_id, c->gcnt_pd, c->gmem, c->gbeg, c->gend, c->gfill, c->pfill, c->pbeg, c->skey, c->sval, c->skey_s,

@@ -173,6 +173,10 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
         const u32 pre = T.xrows[x_r1 - 1].id == t.id ? x_r1 - 1 : xidx_probe_from(T, hx, t.id);
         if (pre != NONE32) return fp_exists(t, T.xrows[pre]);
     }
+    if (xrun_maybe(T, t.id)) {  // the sorted run (an id replayed from an earlier call)
+        const u32 pre = xrun_find(T, t.id);
+        if (pre != NONE32) return fp_exists(t, T.xrows[pre]);
+    }
     const u32 ds = A.row1 - 1, cs = B.row1 - 1;
     // an id repeated within the call is caught by fp_dupcheck (only when ids are not increasing)
     // u128 overflow is impossible: amount < 2^64, balances < 2^126 (T.big clear), < 2^32 events
@@ -568,6 +572,34 @@ __global__ void fp_dupcheck(Tables T, FastArgs F) {
     FOR_EACH_EVENT(i) fp_dupcheck_one(F, i);
 }
 
+// Whether this call's rows extend the sorted run of the id index (engine.h xrun):
+// every event accepted, ids strictly increasing, the first above the run's last id
+// and the rows right after the run's.  Then the run takes them (CNT_RUN) and
+// fp_index inserts nothing; otherwise fp_index hashes them as before.  One thread.
+__global__ void fp_run(Tables T, FastArgs F) {
+    if (threadIdx.x != 0) return;
+    const u32 flags = F.counters[CNT_FLAGS];
+    u32 take = 0;
+    if (!F.dry && F.n && !(flags & (FL_SLOW | FL_ERROR | FL_NONMONO)) && F.counters[CNT_BAD] == 0) {
+        u64* r = T.xrun;
+        const u64 row0 = T.base[BASE_ROWS];
+        const u128 first = F.ev[0].id, last = F.ev[F.n - 1].id;
+        const bool empty = r[0] == r[1];
+        if (empty || (r[1] == row0 && first > (((u128)r[5] << 64) | r[4]))) {
+            if (empty) {
+                r[0] = row0;
+                r[2] = (u64)first;
+                r[3] = (u64)(first >> 64);
+            }
+            r[1] = row0 + F.n;
+            r[4] = (u64)last;
+            r[5] = (u64)(last >> 64);
+            take = 1;
+        }
+    }
+    F.counters[CNT_RUN] = take;
+}
+
 // Publish the accepted ids.  fixed = false: the launch right after fp_commit, which
 // stands down when the call had failures (rows not final yet) and always clears the
 // duplicate claims; fixed = true: after fp_fix, rows from F.rows.
@@ -602,6 +634,7 @@ __global__ void fp_index(Tables T, FastArgs F, bool fixed) {
     if (flags & (FL_SLOW | FL_ERROR)) return;
     if (F.dry) return;
     if (!fixed && F.counters[CNT_BAD] != 0) return;
+    if (!fixed && F.counters[CNT_RUN]) return;  // the rows extend the sorted run
     if (threadIdx.x < 64 && blockIdx.x * 64 < ntiles) {
         // fold the tiles' id ranges into the index's key range: one wave per 64
         // tiles (a single wave over 16k tiles was a serial tail of this launch)
@@ -813,6 +846,7 @@ void fp_launch_index(const Tables& T, const FastArgs& F, hipStream_t stream) {
     fp_dupcheck<<<std::max(sg, 1u), 256, 0, stream>>>(T, F);
     fp_chains<<<std::max(sg, 1u), 256, 0, stream>>>(T, F);   // both stand down without FL_FCHAIN
     fp_chains_fin<<<std::max(sg, 1u), 256, 0, stream>>>(F);
+    fp_run<<<1, 64, 0, stream>>>(T, F);
     fp_index<<<GRID(F.n)>>>(T, F, false);
     HIP_CHECK(hipGetLastError());
 }

@@ -219,7 +219,7 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->side_tiles = dalloc<u8>(side_scan_tile_bytes(m), &B);
     c->sc.tile_sums = dalloc<uint4>(scan3_tile_words(n), &B);
     c->sc.capacity = n;
-    c->fres = dalloc<u8>(n, &B);
+    c->fres = dalloc<u8>(n + 16, &B);  // + a 16-byte load's tail (fp_chains reads 16 results per lane)
     c->mask = dalloc<u8>(n, &B);
     c->ranks = dalloc<uint4>(n + 1, &B);
     c->res_buf = dalloc<u8>(n * 8, &B);

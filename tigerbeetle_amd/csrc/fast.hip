@@ -270,10 +270,16 @@ __device__ __forceinline__ void agg_add(u32* keys, u64* sums, u32* carries, u32 
 #if !defined(FP_LANE_EVENTS)
 #define FP_LDS_EVENTS 1
 #endif
-// Per-wave LDS staging of 128-byte records: 32
-// records of 8 16-byte chunks, chunk c of record e at e*8 + (c ^ (e & 7)) so the
-// lane-per-record writes and reads spread over the banks.
-constexpr int STAGE_RECS = 32;
+// Per-wave LDS staging of 128-byte records: STAGE_RECS records of 8 16-byte chunks,
+// chunk c of record e at e*8 + (c ^ (e & 7)) so the lane-per-record writes and reads
+// spread over the banks.  16 records (four rounds per wave) keep the workgroup's LDS
+// at 49 KB, so three workgroups (24 waves) fit a CU; 32 records (two rounds, 66 KB)
+// left room for two.
+#ifndef FP_STAGE_RECS
+#define FP_STAGE_RECS 16
+#endif
+constexpr int STAGE_RECS = FP_STAGE_RECS;
+static_assert(STAGE_RECS == 16 || STAGE_RECS == 32, "staging rounds");
 __device__ __forceinline__ u32 stage_slot(u32 e, u32 c) { return e * 8 + (c ^ (e & 7)); }
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -378,21 +384,29 @@ void fp_commit(Tables T, FastArgs F) {
         }
     }
 #if defined(FP_LDS_EVENTS)
-    // two 32-event halves through LDS, one record per lane
+    // the wave's events through LDS in rounds of STAGE_RECS, one record per lane
     if (!(F.ablate & ABL_EVENT)) {
         uint4* st = s_stage[wave];
+        constexpr int ROUNDS = 64 / STAGE_RECS;
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
-            // chunk j*64 + lane of the wave's span: event (j*64 + lane) / 8 - 32h
-#define STAGE(j, c) st[stage_slot(((j) * 64 + lane) / 8 - 32 * h, lane & 7)] = (c)
-            if (h == 0) { STAGE(0, c0); STAGE(1, c1); STAGE(2, c2); STAGE(3, c3); }
-            else { STAGE(4, c4); STAGE(5, c5); STAGE(6, c6); STAGE(7, c7); }
+        for (int h = 0; h < ROUNDS; h++) {
+            // chunk j*64 + lane of the wave's span: event (j*64 + lane) / 8 - STAGE_RECS*h
+#define STAGE(j, c) st[stage_slot(((j) * 64 + lane) / 8 - STAGE_RECS * h, lane & 7)] = (c)
+            if (ROUNDS == 2) {
+                if (h == 0) { STAGE(0, c0); STAGE(1, c1); STAGE(2, c2); STAGE(3, c3); }
+                else { STAGE(4, c4); STAGE(5, c5); STAGE(6, c6); STAGE(7, c7); }
+            } else {
+                if (h == 0) { STAGE(0, c0); STAGE(1, c1); }
+                else if (h == 1) { STAGE(2, c2); STAGE(3, c3); }
+                else if (h == 2) { STAGE(4, c4); STAGE(5, c5); }
+                else { STAGE(6, c6); STAGE(7, c7); }
+            }
 #undef STAGE
             wave_lds_sync();
-            if ((lane >> 5) == (u32)h && valid) {
+            if (lane / STAGE_RECS == (u32)h && valid) {
                 uint4* tv = (uint4*)&t;
 #pragma unroll
-                for (int c = 0; c < 8; c++) tv[c] = st[stage_slot(lane & 31, c)];
+                for (int c = 0; c < 8; c++) tv[c] = st[stage_slot(lane % STAGE_RECS, c)];
             }
             wave_lds_sync();
         }
@@ -709,8 +723,10 @@ __device__ void fp_chains_one(const Tables& T, const FastArgs& F, u32 i, u32& n_
         n_ok++;
         if (!F.dry) {
             const Transfer& t = F.ev[i];
-            const u32 ds = acc_probe(T.aidx, T.aidx_mask, t.debit_account_id);
-            const u32 cs = acc_probe(T.aidx, T.aidx_mask, t.credit_account_id);
+            u32 led;
+            u16 afl;
+            const u32 ds = acc_find(T, t.debit_account_id, &led, &afl);
+            const u32 cs = acc_find(T, t.credit_account_id, &led, &afl);
             const u64 a = (u64)t.amount;
             if (t.flags & TF_PENDING) {
                 add_u128_small(T, &T.acc[ds].debits_pending, a);
@@ -726,12 +742,39 @@ __device__ void fp_chains_one(const Tables& T, const FastArgs& F, u32 i, u32& n_
     }
 }
 
-__global__ void fp_chains(Tables T, FastArgs F) {
+// Chain members are few (config 4: 1 %) and each costs a chain of dependent loads,
+// so a wave first gathers the members among its grid-stride events into LDS (16
+// result bytes per lane in one load), then its lanes take one member each: the
+// members of ~1k events wait on memory together instead of one grid-stride step
+// after the other (177 -> ~30 us per 8.19M events on config 4).
+constexpr u32 CH_LIST = 1024;  // a wave's 64 lanes x 16 events: every member of one step
+__global__ __launch_bounds__(256) void fp_chains(Tables T, FastArgs F) {
     const u32 flags = F.counters[CNT_FLAGS];
     if (!(flags & FL_FCHAIN) || (flags & (FL_SLOW | FL_ERROR))) return;
     u32 n_ok = 0, n_bad = 0;
     u64 mts = 0;
-    FOR_EACH_EVENT(i) fp_chains_one(T, F, i, n_ok, n_bad, mts);
+    __shared__ u32 s_list[4][CH_LIST];
+    __shared__ u32 s_cnt[4];
+    const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const u32 nq = (F.n + 15) / 16, stride = gridDim.x * blockDim.x;
+    for (u32 qb = blockIdx.x * blockDim.x + w * 64; qb < nq; qb += stride) {
+        if (lane == 0) s_cnt[w] = 0;
+        wave_lds_sync();
+        const u32 q = qb + lane;
+        if (q < nq) {
+            const uint4 v = ((const uint4*)F.fres)[q];
+            const u8* fb = (const u8*)&v;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const u32 i = q * 16 + k;
+                if (i < F.n && (fb[k] & FRES_CHAIN) && fb[k] != FRES_SLOW) s_list[w][atomicAdd(&s_cnt[w], 1u)] = i;
+            }
+        }
+        wave_lds_sync();
+        const u32 cnt = s_cnt[w];
+        for (u32 k = lane; k < cnt; k += 64) fp_chains_one(T, F, s_list[w][k], n_ok, n_bad, mts);
+        wave_lds_sync();
+    }
     __shared__ u32 s_ok, s_bad;
     __shared__ u64 s_mts;
     if (threadIdx.x == 0) { s_ok = 0; s_bad = 0; s_mts = 0; }
@@ -757,9 +800,15 @@ __global__ void fp_chains(Tables T, FastArgs F) {
 __global__ void fp_chains_fin(FastArgs F) {
     const u32 flags = F.counters[CNT_FLAGS];
     if (!(flags & FL_FCHAIN) || (flags & (FL_SLOW | FL_ERROR))) return;
-    FOR_EACH_EVENT(i) {
-        const u8 fr = F.fres[i];
-        if ((fr & FRES_CHAIN) && fr != FRES_SLOW) F.fres[i] = F.fres2[i];
+    const u32 nq = (F.n + 15) / 16;  // 16 result bytes per lane per load
+    for (u32 q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
+        const uint4 v = ((const uint4*)F.fres)[q];
+        const u8* fb = (const u8*)&v;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const u32 i = q * 16 + k;
+            if (i < F.n && (fb[k] & FRES_CHAIN) && fb[k] != FRES_SLOW) F.fres[i] = F.fres2[i];
+        }
     }
 }
 

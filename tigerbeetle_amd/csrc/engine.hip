@@ -41,6 +41,9 @@ int log2u(u64 x) {
     return b;
 }
 
+// u32 words before the batch timestamps in the batch block: bmax + 1 starts, 8-byte aligned
+inline u64 batch_ts_offset(u64 bmax) { return (bmax + 2) & ~1ull; }
+
 template <typename T>
 T* dalloc(u64 count, u64* total) {
     void* p = nullptr;
@@ -54,6 +57,8 @@ T* dalloc(u64 count, u64* total) {
 
 constexpr u32 PC_RING = 1024;        // pass-counter ring (passes in flight << ring)
 constexpr u32 PASS_GROUP_MAX = 48;   // passes enqueued between two host round trips
+constexpr u32 PC_OFF = 32;           // the pass-change ring's offset behind the counter words
+static_assert(PC_OFF >= CNT_COUNT, "counter words overlap the pass-change ring");
 
 struct tbgpu_ctx {
     int device = 0;
@@ -172,8 +177,9 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     // (engine.h Sides); beyond this capacity a call falls back to one pair each
     const u64 n = nmax, m = 3 * nmax;
     c->ev_buf = dalloc<u8>(n * 128, &B);
-    c->b_start = dalloc<u32>(c->bmax + 1, &B);
-    c->b_ts = dalloc<u64>(c->bmax, &B);
+    // batch starts then batch timestamps in one block, staged by one copy per chunk
+    c->b_start = dalloc<u32>(batch_ts_offset(c->bmax) + 2 * c->bmax, &B);
+    c->b_ts = (u64*)(c->b_start + batch_ts_offset(c->bmax));
     c->ts = dalloc<u64>(n, &B);
     c->cs = dalloc<u32>(n, &B);
     c->ce = dalloc<u32>(n, &B);
@@ -224,7 +230,8 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->ranks = dalloc<uint4>(n + 1, &B);
     c->res_buf = dalloc<u8>(n * 8, &B);
     c->counts = dalloc<u32>(c->bmax, &B);
-    c->counters = dalloc<u32>(CNT_COUNT, &B);
+    // the counters, then the pass-change ring: one copy brings both back per pass group
+    c->counters = dalloc<u32>(PC_OFF + 2 * PC_RING, &B);
     c->status = dalloc<int>(4, &B);
     c->f_gcap = pow2_at_least(2 * nmax);
     c->f_gtab = dalloc<u32>(c->f_gcap, &B);
@@ -237,15 +244,17 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->rt_ctl_buf = dalloc<u8>(n, &B);
     c->rt_dry_ts = dalloc<u64>(1, &B);
     c->rt_stats = dalloc<u64>(8, &B);
-    c->pc = dalloc<u32>(2 * PC_RING, &B);
+    c->pc = c->counters + PC_OFF;
     c->rg_part = dalloc<u64>(tr_range_part_words(n), &B);
-    HIP_CHECK(hipHostMalloc((void**)&c->h_pc, 2 * PC_RING * sizeof(u32), hipHostMallocDefault));
+
     HIP_CHECK(hipHostMalloc((void**)&c->h_base, 8 * sizeof(u64), hipHostMallocDefault));  // [4..5]: a uint4
-    HIP_CHECK(hipHostMalloc((void**)&c->h_counters, CNT_COUNT * sizeof(u32), hipHostMallocDefault));
+    HIP_CHECK(hipHostMalloc((void**)&c->h_counters, (PC_OFF + 2 * PC_RING) * sizeof(u32), hipHostMallocDefault));
+    c->h_pc = c->h_counters + PC_OFF;
     HIP_CHECK(hipHostMalloc((void**)&c->h_res, c->nmax * 8 + 8, hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc((void**)&c->h_counts, c->bmax * sizeof(u32), hipHostMallocDefault));
-    HIP_CHECK(hipHostMalloc((void**)&c->h_stage_ts, c->bmax * sizeof(u64), hipHostMallocDefault));
-    HIP_CHECK(hipHostMalloc((void**)&c->h_stage_start, (c->bmax + 1) * sizeof(u32), hipHostMallocDefault));
+    HIP_CHECK(hipHostMalloc((void**)&c->h_stage_start, (batch_ts_offset(c->bmax) + 2 * c->bmax) * sizeof(u32),
+                            hipHostMallocDefault));
+    c->h_stage_ts = (u64*)(c->h_stage_start + batch_ts_offset(c->bmax));
 }
 
 enum { PH_UPLOAD = 0, PH_CLASSIFY = 1, PH_SORT = 2, PH_SCAN = 3, PH_EVAL = 4, PH_APPLY = 5, PH_INDEX = 6, PH_PREP = 7, PH_END = -1 };
@@ -369,7 +378,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
                     (void*)c->ro_bcount, (void*)c->ro_spart})
         if (p) (void)hipFree(p);
     void* ptrs[] = {c->T.dense, c->T.acc, c->T.aidx, c->T.xrows, c->T.xful, c->T.xidx, c->T.hrows, c->T.commit_ts, c->T.idr, c->T.xrun, c->T.big, c->ev_buf,
-                    c->b_start, c->b_ts, c->ts, c->cs, c->ce, c->sres, c->dslot, c->cslot, c->pre_e, c->pre_p,
+                    c->b_start, c->ts, c->cs, c->ce, c->sres, c->dslot, c->cslot, c->pre_e, c->pre_p,
                     c->pp_dslot, c->pp_cslot, c->gslot, c->pslot, c->prev_id, c->pend_last, c->pend_first, c->prev_pend,
                     c->gclaim, c->gcnt_id, c->gcnt_pd, c->gmem, c->gbeg, c->gend, c->gfill, c->pfill, c->pbeg, c->skey, c->sval, c->skey_s,
                     c->soff, c->core, c->tstart, c->epos, c->sev, c->scand, c->sq_ev, c->sq_cs, c->sq_ok, c->sq_dpend, c->sq_dpost, c->gkey_s,
@@ -377,7 +386,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
                     c->sval_s, c->spos, c->bb, c->ss.keys_tmp, c->ss.vals_tmp, c->ss.hist, c->side_tiles,
                     c->sc.tile_sums, c->fres, c->mask, c->ranks, c->res_buf, c->counts, c->counters, c->status,
                     c->f_gtab, c->f_gpos, c->f_keys, c->f_rows,
-                    c->f_tile_idr, c->rt_ts_buf, c->rt_ctl_buf, c->rt_dry_ts, c->rt_stats, c->pc, c->rg_part, c->T.base, c->q_key, c->q_val, c->q_tkey,
+                    c->f_tile_idr, c->rt_ts_buf, c->rt_ctl_buf, c->rt_dry_ts, c->rt_stats, c->rg_part, c->T.base, c->q_key, c->q_val, c->q_tkey,
                     c->q_tval, c->q_ss.keys_tmp, c->q_ss.vals_tmp, c->q_ss.hist, c->q_runs_dev, c->ximp};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     for (EvalState& s : c->st) {
@@ -386,9 +395,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     }
     if (c->h_counters) (void)hipHostFree(c->h_counters);
     if (c->h_counts) (void)hipHostFree(c->h_counts);
-    if (c->h_stage_ts) (void)hipHostFree(c->h_stage_ts);
     if (c->h_stage_start) (void)hipHostFree(c->h_stage_start);
-    if (c->h_pc) (void)hipHostFree(c->h_pc);
     if (c->h_base) (void)hipHostFree(c->h_base);
     if (c->h_rc) (void)hipHostFree(c->h_rc);
     if (c->h_res) (void)hipHostFree(c->h_res);
@@ -467,8 +474,9 @@ static void upload_batches(tbgpu_ctx* c, const uint64_t* timestamps, const uint3
     // call synchronizes before the staging buffer is reused)
     memcpy(c->h_stage_ts, timestamps, nb * sizeof(u64));
     memcpy(c->h_stage_start, starts.data(), (nb + 1) * sizeof(u32));
-    HIP_CHECK(hipMemcpyAsync(c->b_start, c->h_stage_start, (nb + 1) * sizeof(u32), hipMemcpyHostToDevice, c->stream));
-    HIP_CHECK(hipMemcpyAsync(c->b_ts, c->h_stage_ts, nb * sizeof(u64), hipMemcpyHostToDevice, c->stream));
+    // one copy: the starts, the unused rest of their region, the timestamps
+    HIP_CHECK(hipMemcpyAsync(c->b_start, c->h_stage_start, batch_ts_offset(c->bmax) * sizeof(u32) + nb * sizeof(u64),
+                             hipMemcpyHostToDevice, c->stream));
 }
 
 // Device replies are concatenated across the chunk's batches; the host C-ABI
@@ -651,8 +659,8 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n) {
         const u32 p0 = p;
         p += group;
         prof_mark(c, PH_END);
-        HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, CNT_COUNT * sizeof(u32), hipMemcpyDeviceToHost, s));
-        HIP_CHECK(hipMemcpyAsync(c->h_pc, chg, PC_RING * sizeof(u32), hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, (PC_OFF + PC_RING) * sizeof(u32), hipMemcpyDeviceToHost,
+                                 s));
         HIP_CHECK(hipStreamSynchronize(s));
         if (c->h_counters[CNT_FLAGS] & FL_ERROR) tbgpu_fatal("create_transfers", "device error", __FILE__, __LINE__);
         static const bool trace = getenv("TBGPU_TRACE_PASSES") != nullptr;  // diagnostics only

@@ -44,6 +44,37 @@ int log2u(u64 x) {
 // u32 words before the batch timestamps in the batch block: bmax + 1 starts, 8-byte aligned
 inline u64 batch_ts_offset(u64 bmax) { return (bmax + 2) & ~1ull; }
 
+// Waits on the engine's streams: blocking, or with TBGPU_POLL_SYNC=1 by polling
+// (hipStreamQuery / hipEventQuery in a loop).  Polling was measured alike on config
+// 3 (152 M/s either way) and slower on the routed step (gpurun_out/r02c13), so the
+// blocking wait is the default.
+inline bool blocking_sync() {
+    static const bool b = getenv("TBGPU_POLL_SYNC") == nullptr;
+    return b;
+}
+inline void wait_stream(hipStream_t s) {
+    if (blocking_sync()) {
+        HIP_CHECK(hipStreamSynchronize(s));
+        return;
+    }
+    for (;;) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e == hipSuccess) return;
+        if (e != hipErrorNotReady) HIP_CHECK(e);
+    }
+}
+inline void wait_event(hipEvent_t ev) {
+    if (blocking_sync()) {
+        HIP_CHECK(hipEventSynchronize(ev));
+        return;
+    }
+    for (;;) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e == hipSuccess) return;
+        if (e != hipErrorNotReady) HIP_CHECK(e);
+    }
+}
+
 template <typename T>
 T* dalloc(u64 count, u64* total) {
     void* p = nullptr;
@@ -363,7 +394,7 @@ extern "C" void tbgpu_reset(tbgpu_ctx* c) {
     if (c->T.dense_n) HIP_CHECK(hipMemsetAsync(c->T.dense, 0, c->T.dense_n * sizeof(u64), c->stream));
     if (c->ximp) HIP_CHECK(hipMemsetAsync(c->ximp, 0, c->xrow_cap, c->stream));
     HIP_CHECK(hipMemsetAsync(c->f_gtab, 0, c->f_gcap * sizeof(u32), c->stream));  // fast path's claim table
-    HIP_CHECK(hipStreamSynchronize(c->stream));
+    wait_stream(c->stream);
     c->n_accounts = c->n_rows = c->n_hist = 0;
     c->rows_hi = 0;
     c->q_runs.assign(1, 0);
@@ -411,14 +442,14 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
 
 static void read_counters(tbgpu_ctx* c) {
     HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, CNT_COUNT * sizeof(u32), hipMemcpyDeviceToHost, c->stream));
-    HIP_CHECK(hipStreamSynchronize(c->stream));
+    wait_stream(c->stream);
 }
 
 // Host copies of the device cursors (stored rows, history rows), exact for all work
 // enqueued so far.  One round trip.
 static void refresh_bases(tbgpu_ctx* c) {
     HIP_CHECK(hipMemcpyAsync(c->h_base, c->T.base, 4 * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
-    HIP_CHECK(hipStreamSynchronize(c->stream));
+    wait_stream(c->stream);
     c->n_rows = c->h_base[BASE_ROWS];
     c->n_hist = c->h_base[BASE_HIST];
     c->rows_hi = c->n_rows;
@@ -431,7 +462,7 @@ static void set_base(tbgpu_ctx* c, int k, u64 v) {
     }
     c->h_base[3] = v;  // staged through pinned memory (async copy), then waited for
     HIP_CHECK(hipMemcpyAsync(c->T.base + k, c->h_base + 3, sizeof(u64), hipMemcpyHostToDevice, c->stream));
-    HIP_CHECK(hipStreamSynchronize(c->stream));
+    wait_stream(c->stream);
 }
 
 static void ensure_h_rc(tbgpu_ctx* c, u64 nb) {
@@ -568,7 +599,7 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_crea
     prof_mark(c, PH_END);
     // one round trip: the flags decide whether the attempt stands
     HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, CNT_COUNT * sizeof(u32), hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+    wait_stream(s);
     const u32 flags = c->h_counters[CNT_FLAGS];
     if (flags & FL_ERROR) tbgpu_fatal("create_transfers", "fast path look-back did not complete", __FILE__, __LINE__);
     if (flags & FL_SLOW) {
@@ -619,7 +650,7 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n) {
             scan3_exclusive(c->mask, c->ranks, n, c->sc, s);
             uint4 tot;
             HIP_CHECK(hipMemcpyAsync(c->h_base + 4, c->ranks + n, sizeof(uint4), hipMemcpyDeviceToHost, s));
-            HIP_CHECK(hipStreamSynchronize(s));
+            wait_stream(s);
             memcpy(&tot, c->h_base + 4, sizeof tot);
             m = 2ull * (tot.x + tot.y + tot.z);
             if (m <= c->scap) {
@@ -661,7 +692,7 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n) {
         prof_mark(c, PH_END);
         HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, (PC_OFF + PC_RING) * sizeof(u32), hipMemcpyDeviceToHost,
                                  s));
-        HIP_CHECK(hipStreamSynchronize(s));
+        wait_stream(s);
         if (c->h_counters[CNT_FLAGS] & FL_ERROR) tbgpu_fatal("create_transfers", "device error", __FILE__, __LINE__);
         static const bool trace = getenv("TBGPU_TRACE_PASSES") != nullptr;  // diagnostics only
         if (trace) {
@@ -861,7 +892,7 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         if (!dst_device) {
             // the chunk's replies (at most one per event) come back with its counts: one round trip
             HIP_CHECK(hipMemcpyAsync(c->h_res, c->res_buf, (u64)n * 8, hipMemcpyDeviceToHost, c->stream));
-            HIP_CHECK(hipStreamSynchronize(c->stream));
+            wait_stream(c->stream);
             copy_results_to_batches(c, nb, starts, c->h_rc + b0, (u8*)(results + ev_off));
         }
         iters = std::max(iters, c->stats.iterations);
@@ -874,7 +905,7 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
     // the device cursors come back with the call's end (no extra round trip)
     HIP_CHECK(hipMemcpyAsync(c->h_base, c->T.base, 4 * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
     HIP_CHECK(hipEventRecord(c->ev1, c->stream));
-    HIP_CHECK(hipEventSynchronize(c->ev1));
+    wait_event(c->ev1);
     float ms = 0;
     HIP_CHECK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     c->n_rows = c->h_base[BASE_ROWS];
@@ -969,7 +1000,7 @@ extern "C" int tbgpu_import_transfers(tbgpu_ctx* c, const tbgpu_transfer_t* rows
             HIP_CHECK(hipMemsetAsync(c->ximp, 0, c->xrow_cap, c->stream));
         }
         HIP_CHECK(hipMemsetAsync(c->ximp + c->n_rows, 1, k, c->stream));  // not this shard's: never queried
-        HIP_CHECK(hipStreamSynchronize(c->stream));
+        wait_stream(c->stream);
         c->n_rows += k;
         off += k;
     }
@@ -985,7 +1016,7 @@ extern "C" int tbgpu_route_stats(tbgpu_ctx* c, const void* events_device, uint64
     HIP_CHECK(hipSetDevice(c->device));
     route_stats((const Transfer*)events_device, count, c->rt_stats, c->route_stream);
     HIP_CHECK(hipMemcpyAsync(out, c->rt_stats, 5 * sizeof(u64), hipMemcpyDeviceToHost, c->route_stream));
-    HIP_CHECK(hipStreamSynchronize(c->route_stream));
+    wait_stream(c->route_stream);
     return 0;
 }
 void route_scatter(const Transfer* ev, u64 n, u32 world, u32 nb, const u32* b_start, const u64* b_ts, u64 g0,
@@ -1002,7 +1033,7 @@ static void route_capacity(tbgpu_ctx* c, u32 world, u32 batch_count, u64 n) {
     const u64 nblk = route_block_count(n);
     if (n > c->ro_cap || world * std::max<u64>(nblk, 1) > c->ro_bcap || batch_count + 1 > c->ro_cap + 2 ||
         (u64)world * batch_count > c->ro_bc_cap) {
-        HIP_CHECK(hipStreamSynchronize(c->route_stream));
+        wait_stream(c->route_stream);
         for (void* p : {(void*)c->ro_orank, (void*)c->ro_blk, (void*)c->ro_bstart, (void*)c->ro_bts, (void*)c->ro_counts,
                         (void*)c->ro_bcount, (void*)c->ro_spart})
             if (p) HIP_CHECK(hipFree(p));
@@ -1028,7 +1059,7 @@ extern "C" int tbgpu_route_prepare(tbgpu_ctx* c, uint32_t world, const void* eve
     route_rank((const Transfer*)events_device, count, world, c->ro_orank, c->ro_blk, c->ro_spart, c->rt_stats,
                c->route_stream);
     HIP_CHECK(hipMemcpyAsync(out, c->rt_stats, 5 * sizeof(u64), hipMemcpyDeviceToHost, c->route_stream));
-    HIP_CHECK(hipStreamSynchronize(c->route_stream));
+    wait_stream(c->route_stream);
     c->ro_ranked = {events_device, count, world};
     return 0;
 }
@@ -1070,7 +1101,7 @@ static int route_scatter_any(tbgpu_ctx* c, uint32_t world, uint32_t batch_count,
         HIP_CHECK(hipMemcpyAsync(send_span_counts, c->ro_bcount, world * sizeof(u32), hipMemcpyDeviceToHost, c->route_stream));
     u32 e = 0;
     HIP_CHECK(hipMemcpyAsync(&e, err, sizeof(u32), hipMemcpyDeviceToHost, c->route_stream));
-    HIP_CHECK(hipStreamSynchronize(c->route_stream));
+    wait_stream(c->route_stream);
     return e ? -22 : 0;
 }
 
@@ -1106,7 +1137,7 @@ extern "C" int tbgpu_route_unpack_packed(tbgpu_ctx* c, const void* packed_device
                       (Transfer*)events_device, (u64*)records_device, (u64*)timestamps_device, err, c->route_stream);
     u32 e = 0;
     HIP_CHECK(hipMemcpyAsync(&e, err, sizeof(u32), hipMemcpyDeviceToHost, c->route_stream));
-    HIP_CHECK(hipStreamSynchronize(c->route_stream));
+    wait_stream(c->route_stream);
     return e ? -22 : 0;
 }
 
@@ -1119,7 +1150,7 @@ extern "C" int tbgpu_route_unpack(tbgpu_ctx* c, const void* records_device, uint
                  err, c->route_stream);
     u32 e = 0;
     HIP_CHECK(hipMemcpyAsync(&e, err, sizeof(u32), hipMemcpyDeviceToHost, c->route_stream));
-    HIP_CHECK(hipStreamSynchronize(c->route_stream));
+    wait_stream(c->route_stream);
     return e ? -22 : 0;
 }
 
@@ -1198,11 +1229,11 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
     scan3_exclusive(c->mask, c->ranks, n, c->sc, s);
     uint4 tot;
     HIP_CHECK(hipMemcpyAsync(&tot, c->ranks + n, sizeof(uint4), hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+    wait_stream(s);
     if (c->n_accounts + tot.x > c->accounts_max) tbgpu_fatal("create_accounts", "accounts_max exceeded", __FILE__, __LINE__);
     ac_launch_apply(c->T, C, A->ok, c->fres, c->ranks, c->n_accounts, results_dev, c->counts, s);
     HIP_CHECK(hipMemcpyAsync(counts_host, c->counts, nb * sizeof(u32), hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+    wait_stream(s);
     c->n_accounts += tot.x;
 }
 
@@ -1232,7 +1263,7 @@ static uint64_t accounts_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t
         } else {
             if (chunk_total) {
                 HIP_CHECK(hipMemcpyAsync(c->h_res, c->res_buf, chunk_total * 8, hipMemcpyDeviceToHost, c->stream));
-                HIP_CHECK(hipStreamSynchronize(c->stream));
+                wait_stream(c->stream);
             }
             copy_results_to_batches(c, nb, starts, result_counts + b0, (u8*)(results + ev_off));
         }
@@ -1240,7 +1271,7 @@ static uint64_t accounts_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t
         ev_off += n;
         b0 = b1;
     }
-    HIP_CHECK(hipStreamSynchronize(c->stream));
+    wait_stream(c->stream);
     return total;
 }
 
@@ -1283,7 +1314,7 @@ static uint32_t lookup(tbgpu_ctx* c, const tbgpu_uint128_t* ids, uint32_t count,
         found.resize(k);
         HIP_CHECK(hipMemcpyAsync(rows.data(), d_out, (u64)k * sizeof(Row), hipMemcpyDeviceToHost, c->stream));
         HIP_CHECK(hipMemcpyAsync(found.data(), d_found, k, hipMemcpyDeviceToHost, c->stream));
-        HIP_CHECK(hipStreamSynchronize(c->stream));
+        wait_stream(c->stream);
         for (u32 i = 0; i < k; i++)
             if (found[i]) memcpy(&out[found_total++], &rows[i], sizeof(Row));
     }
@@ -1347,7 +1378,7 @@ extern "C" uint64_t tbgpu_compact(tbgpu_ctx* c) {
     if (c->q_runs.size() > Q_RUNS_MAX + 1) tbgpu_fatal("compact", "index runs exceed Q_RUNS_MAX", __FILE__, __LINE__);
     HIP_CHECK(hipMemcpyAsync(c->q_runs_dev, c->q_runs.data(), c->q_runs.size() * sizeof(u64), hipMemcpyHostToDevice,
                              c->stream));
-    HIP_CHECK(hipStreamSynchronize(c->stream));
+    wait_stream(c->stream);
     return r1;
 }
 
@@ -1363,7 +1394,7 @@ static u64 run_queries(tbgpu_ctx* c, const tbgpu_account_filter_t* filters, u32 
         QArgs A{filters + q0, k, stride, (u8*)out + (u64)q0 * stride * 128, c->counts, history ? 1u : 0u, c->n_hist};
         q_launch_scan(c->T, X, A, c->stream);
         HIP_CHECK(hipMemcpyAsync(counts_host + q0, c->counts, k * sizeof(u32), hipMemcpyDeviceToHost, c->stream));
-        HIP_CHECK(hipStreamSynchronize(c->stream));
+        wait_stream(c->stream);
         for (u32 j = 0; j < k; j++) total += counts_host[q0 + j];
     }
     return total;
@@ -1435,7 +1466,7 @@ extern "C" uint64_t tbgpu_checkpoint(tbgpu_ctx* c, void* out, uint64_t capacity)
     HIP_CHECK(hipSetDevice(c->device));
     const u64 size = tbgpu_checkpoint_size(c);
     if (capacity < size) return 0;
-    HIP_CHECK(hipStreamSynchronize(c->stream));
+    wait_stream(c->stream);
     u8* p = (u8*)out + sizeof(CkHeader);
     const u64 na = c->n_accounts, nr = c->n_rows, nh = c->n_hist;
     if (na) HIP_CHECK(hipMemcpy(p, c->T.acc, na * 128, hipMemcpyDeviceToHost));
@@ -1490,7 +1521,7 @@ extern "C" int tbgpu_open(tbgpu_ctx* c, const void* image, uint64_t size) {
         launch_import_transfers(c->T, c->T.xrows + off, k, off, s);  // rows in place: index + key range
     }
     HIP_CHECK(hipMemcpyAsync(c->T.commit_ts, &h.commit_ts, sizeof(u64), hipMemcpyHostToDevice, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+    wait_stream(s);
     c->n_accounts = na;
     c->n_rows = nr;
     c->n_hist = nh;
@@ -1509,7 +1540,7 @@ extern "C" int tbgpu_test_set_balances(tbgpu_ctx* c, tbgpu_uint128_t id, tbgpu_u
     launch_set_balances(c->T, to128(id), b, c->status, c->stream);
     int st = 0;
     HIP_CHECK(hipMemcpyAsync(&st, c->status, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIP_CHECK(hipStreamSynchronize(c->stream));
+    wait_stream(c->stream);
     return st;
 }
 
@@ -1518,7 +1549,7 @@ extern "C" int tbgpu_get_posted(tbgpu_ctx* c, tbgpu_uint128_t pending_id) {
     launch_get_posted(c->T, to128(pending_id), c->status, c->stream);
     int st = 0;
     HIP_CHECK(hipMemcpyAsync(&st, c->status, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIP_CHECK(hipStreamSynchronize(c->stream));
+    wait_stream(c->stream);
     return st;
 }
 
@@ -1553,7 +1584,7 @@ extern "C" uint64_t tbgpu_commit_timestamp(tbgpu_ctx* c) {
     HIP_CHECK(hipSetDevice(c->device));
     u64 v = 0;  // behind whatever the engine's stream still has queued (tbgpu_advance_commit_timestamp)
     HIP_CHECK(hipMemcpyAsync(&v, c->T.commit_ts, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
-    HIP_CHECK(hipStreamSynchronize(c->stream));
+    wait_stream(c->stream);
     return v;
 }
 

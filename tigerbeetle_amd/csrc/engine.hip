@@ -41,7 +41,7 @@ int log2u(u64 x) {
     return b;
 }
 
-// u32 words before the batch timestamps in the batch block: bmax + 1 starts, 8-byte aligned
+// u32 words before the batch timestamps in a chunk's batch block: nb + 1 starts, 8-byte aligned
 inline u64 batch_ts_offset(u64 bmax) { return (bmax + 2) & ~1ull; }
 
 // Waits on the engine's streams: blocking, or with TBGPU_POLL_SYNC=1 by polling
@@ -503,11 +503,15 @@ static void upload_batches(tbgpu_ctx* c, const uint64_t* timestamps, const uint3
     for (u32 b = 0; b < nb; b++) starts[b + 1] = starts[b] + counts[b];
     // staged through pinned memory so the copies are truly asynchronous (every
     // call synchronizes before the staging buffer is reused)
+    // one copy of this chunk's block: its nb + 1 starts, then (8-byte aligned) its nb
+    // timestamps; b_ts points into the block for this chunk
+    const u64 off = batch_ts_offset(nb);
+    c->h_stage_ts = (u64*)(c->h_stage_start + off);
+    c->b_ts = (u64*)(c->b_start + off);
     memcpy(c->h_stage_ts, timestamps, nb * sizeof(u64));
     memcpy(c->h_stage_start, starts.data(), (nb + 1) * sizeof(u32));
-    // one copy: the starts, the unused rest of their region, the timestamps
-    HIP_CHECK(hipMemcpyAsync(c->b_start, c->h_stage_start, batch_ts_offset(c->bmax) * sizeof(u32) + nb * sizeof(u64),
-                             hipMemcpyHostToDevice, c->stream));
+    HIP_CHECK(hipMemcpyAsync(c->b_start, c->h_stage_start, off * sizeof(u32) + nb * sizeof(u64), hipMemcpyHostToDevice,
+                             c->stream));
 }
 
 // Device replies are concatenated across the chunk's batches; the host C-ABI

@@ -358,17 +358,20 @@ class ShardedStateMachine:
         # (the global order), in the same all-gather
         st += [(wmask if n else 0) | (int(can_pack) << 32)]
         nb_here = len(counts)
-        st += [nb_here] + (list(map(int, counts)) if nb_here <= NB_GATHER else []) + \
-            [0] * (NB_GATHER - (nb_here if nb_here <= NB_GATHER else 0))
+        sta = np.zeros(8 + NB_GATHER, dtype=np.int64)
+        sta[:7] = st
+        sta[7] = nb_here
+        if nb_here <= NB_GATHER:
+            sta[8:8 + nb_here] = np.asarray(counts, dtype=np.int64)
         if W > 1:
-            stats = torch.tensor(st, dtype=torch.int64, device=dev)
+            stats = torch.from_numpy(sta).to(dev)
             allst = [torch.empty_like(stats) for _ in range(W)]
             self.comm.dist.all_gather(allst, stats, group=self.comm.group)
-            allst = torch.stack(allst).cpu().tolist()
+            allst = torch.stack(allst).cpu().numpy()
         else:  # one rank: nothing to gather
-            allst = [st]
+            allst = sta[None, :]
         ok, prev = True, self.max_id
-        for (cnt, lo, hi, mono, plain, _) in (x[:6] for x in allst):
+        for (cnt, lo, hi, mono, plain, _) in (x[:6].tolist() for x in allst):
             if cnt == 0:
                 continue
             ok &= bool(mono and plain and lo > prev)
@@ -383,22 +386,26 @@ class ShardedStateMachine:
 
         # global order and timestamps (host: one entry per batch)
         # every rank packs when every rank can: the union of the nonzero words travels
-        packed = W > 1 and all(x[6] >> 32 for x in allst)
+        packed = W > 1 and all(int(x[6]) >> 32 for x in allst)
         pmask = 0
         for x in allst:
-            pmask |= x[6] & 0xFFFFFFFF
+            pmask |= int(x[6]) & 0xFFFFFFFF
         pmask = pmask or 1
         K = bin(pmask).count("1") + 1  # 4-byte words per packed row: the masked words, the record
-        if all(x[7] <= NB_GATHER for x in allst):
-            counts_all = [x[8:8 + x[7]] for x in allst]
+        if all(int(x[7]) <= NB_GATHER for x in allst):
+            counts_all = [x[8:8 + int(x[7])] for x in allst]
         else:
             counts_all = self.comm.all_gather_object(list(map(int, counts)))
-        glob = [(r, j, c) for r, cl in enumerate(counts_all) for j, c in enumerate(cl)]
-        T = []
-        for r, j, c in glob:
-            self.prepare_timestamp += 1 + c
-            T.append(self.prepare_timestamp)
-        g0 = sum(len(cl) for cl in counts_all[:me])
+        # the global order as arrays (one entry per batch of every rank: 8000 at N = 8,
+        # so no per-batch Python): each batch's size, source rank and prepare timestamp
+        nbs = [len(cl) for cl in counts_all]
+        gcount = np.concatenate([np.asarray(cl, np.int64) for cl in counts_all]) if sum(nbs) else \
+            np.zeros(0, np.int64)
+        grank = np.repeat(np.arange(W, dtype=np.int64), nbs)
+        T = self.prepare_timestamp + np.cumsum(gcount + 1)
+        if len(T):
+            self.prepare_timestamp = int(T[-1])
+        g0 = sum(nbs[:me])
         clock("order_ms")
         nb_me = len(counts)
         send = None
@@ -428,7 +435,6 @@ class ShardedStateMachine:
         # per owner: [events, spanning events, all spanning events sent, events per batch...]
         meta = np.concatenate([np.asarray(sc, np.int64)[:, None], np.asarray(spc, np.int64)[:, None],
                                np.full((W, 1), int(np.sum(spc)), np.int64), np.asarray(bc, np.int64)], axis=1)
-        nbs = [len(cl) for cl in counts_all]
         if W > 1:
             rmeta = torch.empty(sum(3 + k for k in nbs), dtype=torch.int64, device=dev)
             self.comm.dist.all_to_all_single(rmeta, torch.from_numpy(meta.reshape(-1)).to(dev), [3 + k for k in nbs],
@@ -462,13 +468,14 @@ class ShardedStateMachine:
         torch = self.comm.torch
         clock = self._clock()
         g = st.__dict__
-        dev, W, m, T, glob, packed, K, pmask = (g[x] for x in ("dev", "W", "m", "T", "glob", "packed", "K", "pmask"))
+        dev, W, m, T, gcount, packed, K, pmask = (g[x] for x in ("dev", "W", "m", "T", "gcount", "packed", "K",
+                                                                 "pmask"))
         rl, sl, sub_counts, sub_g, n_span, span_sent = (g[x] for x in ("rl", "sl", "sub_counts", "sub_g", "n_span",
                                                                        "span_sent"))
         send, ev_s, side_s = g.pop("send"), g.pop("ev_s"), g.pop("side_s")
         self.wire_bytes_per_event = 4 * K if packed else 128 + 8  # what the all-to-all moves per event
         # the received events' timestamps: T - n + index + 1 of their global batch
-        tsb = torch.tensor([T[k] - glob[k][2] for k in range(len(glob))], dtype=torch.int64, device=dev)
+        tsb = torch.from_numpy(T - gcount).to(dev)
         ts_r = None
         if packed:
             recv = torch.empty((m, K), dtype=torch.int32, device=dev)
@@ -688,7 +695,7 @@ class ShardedStateMachine:
             st.out, st.at, st.cts = st.decode(rc, cts, st.offs)
             st.thread = None
         g = st.__dict__
-        dev, W, m, S, glob, g0, counts = g["dev"], g["W"], g["m"], g["S"], g["glob"], g["g0"], g["counts"]
+        dev, W, m, S, grank, g0, counts = g["dev"], g["W"], g["m"], g["S"], g["grank"], g["g0"], g["counts"]
         out, at, cts = st.out, st.at, st.cts
         # the node's commit timestamp and whether any owner has replies, in one all-gather
         fin = [len(at), int(cts) if m else self.backend.commit_timestamp()]
@@ -711,7 +718,7 @@ class ShardedStateMachine:
             rep = [[] for _ in range(W)]
             for pgv, r in zip(pg.tolist(), out["result"].tolist()):
                 gg = pgv >> 32
-                rep[glob[gg][0]].append((gg, pgv & 0xFFFFFFFF, r))
+                rep[int(grank[gg])].append((gg, pgv & 0xFFFFFFFF, r))
             for lst in self._exchange_objects(rep):
                 for (gg, i, r) in lst:
                     mine.setdefault(gg - g0, []).append((i, r))

@@ -51,7 +51,7 @@ def _run(w, world, pipelined=False):
             acc, xs = sm.export_state()
             outs[rank] = {"replies": replies, "acc_replies": [a.tobytes() for a in acc_replies],
                           "acc": acc.tobytes(), "xs": xs.tobytes(), "cts": sm.commit_timestamp,
-                          "stats": dict(sm.stats)}
+                          "stats": dict(sm.stats), "wire": sm.wire_bytes_per_event}
         except BaseException as e:  # noqa: BLE001 -- re-raised in the main thread
             errors.append(e)
             group.barrier.abort()
@@ -67,10 +67,12 @@ def _run(w, world, pipelined=False):
     assert not any(t.is_alive() for t in threads), "a rank did not finish"
     if errors:
         raise errors[0]
+    # more than one rank: the events travelled in the packed wire format (<= 33 words of 4 B)
+    assert all(o["wire"] <= 4 * 33 for o in outs), [o["wire"] for o in outs]
     return verify(w, outs, world)
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_routed_device_step_config4(world):
     stats = _run(config4_small(71 + world, world, 3, 2), world)
     assert stats["preruns"] > 0 and stats["dry_rounds"] == 0 and stats["device_fallbacks"] == 0
@@ -87,7 +89,7 @@ def test_routed_device_step_limit_accounts():
     assert stats["dry_rounds"] > 0
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_routed_device_stream_pipelined(world):
     """The pipelined form (bench.py's timed loop): step k + 1's stats, scatter and
     all-to-all while step k's owner commit runs on a worker thread."""

@@ -4,7 +4,7 @@
 # two-rank routed rehearsal (gloo collectives, both ranks on the one GPU), kernel
 # traces and PMC passes of configs 2 and 4
 set -o pipefail
-O=gpurun_out/r02c_final; mkdir -p $O
+O=gpurun_out/r02c_final2; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/gpu_tests.txt 2>&1; rc=$?; echo "tests rc=$rc"; tail -1 $O/gpu_tests.txt
 [ $rc -eq 0 ] || exit 1
@@ -18,6 +18,7 @@ timeout -k 10 400 python3 -u bench.py --routed --steps 6 --no-cpu > $O/bench_rou
 timeout -k 10 400 python3 -u bench.py --routed --pipelined --steps 6 --no-cpu > $O/bench_routed_1rank_pipelined.json 2> $O/bench_routed_1rank_pipelined.err; echo "routed pipelined rc=$? $(grep -o '"value": [0-9.]*' $O/bench_routed_1rank_pipelined.json)"
 TB_DIST_BACKEND=gloo timeout -k 10 500 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --steps 2 --warmup 1 --batches-per-step 100 > $O/bench_routed_gloo2.json 2> $O/bench_routed_gloo2.err; echo "gloo2 rc=$? $(grep -o '"value": [0-9.]*' $O/bench_routed_gloo2.json)"
 TB_CONFIG=2 TB_ACCOUNTS=1000000 TB_CALLS=3 bash profiles/collect.sh $O/c2 --config 2 --steps 2 --warmup 1 --no-cpu --no-queries --no-host && python3 profiles/summarize.py $O/c2 8190000 > $O/c2/summary.txt && echo c2 pmc ok
+TB_CONFIG=3 TB_ACCOUNTS=10000 TB_CALLS=3 EVENTS_PER_LAUNCH=491400 bash profiles/collect.sh $O/c3 --config 3 --steps 2 --warmup 1 --no-cpu --no-queries --no-host && python3 profiles/summarize.py $O/c3 491400 > $O/c3/summary.txt && echo c3 pmc ok
 TB_CONFIG=4 TB_ACCOUNTS=10000000 TB_CALLS=3 bash profiles/collect.sh $O/c4 --config 4 --steps 2 --warmup 1 --no-cpu --no-queries --no-host && python3 profiles/summarize.py $O/c4 8190000 > $O/c4/summary.txt && echo c4 pmc ok
 timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d $O/kt_routed -o kt --output-format csv -- python3 bench.py --routed --steps 2 --no-cpu > $O/kt_routed.log 2>&1 && echo routed kt ok
 timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d $O/kt_c3 -o kt --output-format csv -- python3 bench.py --config 3 --steps 2 --warmup 1 --no-cpu --no-queries --no-host > $O/kt_c3.log 2>&1 && echo c3 kt ok

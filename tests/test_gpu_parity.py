@@ -420,3 +420,80 @@ def test_sorted_run_id_index():
             gpu2.close()
     finally:
         gpu.close()
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_sorted_run_random_call_mix(seed):
+    """Random sequences of calls against the oracle, each call one of: fresh rising ids
+    (the run grows), rising ids with failures (exists / invalid fields: hashed), a
+    shuffled call (non-monotone: hashed), replays of earlier ids, posts and voids of
+    earlier pendings (general path), linked pairs (fp_chains): the sorted run and the
+    hash index together must answer every `exists`, every pending lookup and every
+    lookup exactly as the oracle's single map does."""
+    from tigerbeetle_amd.types import TRANSFER_DTYPE, TransferFlags
+    rng = np.random.default_rng(100 + seed)
+    acc_n = 300
+    w = workload.config1(transfer_count=1, account_count=acc_n, seed=seed)
+    ats, _ = w.timestamps()
+    orc = oracle.Oracle(acc_n, 1 << 20)
+    gpu = _engine()
+    next_id = 1
+    committed = []  # ids and flags of events sent so far
+    try:
+        for be in (orc, gpu):
+            be.create_accounts_batches(ats, w.account_counts, w.accounts)
+        ts = int(ats[-1])
+        for k in range(24):
+            kind = rng.choice(["fresh", "fresh", "fail", "shuffle", "replay", "postvoid", "linked"])
+            n = int(rng.integers(1, 3 * 8190))
+            ev = np.zeros(n, dtype=TRANSFER_DTYPE)
+            ev["id_lo"] = np.arange(next_id, next_id + n)
+            next_id += n + int(rng.integers(0, 3))
+            d = rng.integers(1, acc_n + 1, n)
+            c = rng.integers(1, acc_n, n)
+            c = np.where(c >= d, c + 1, c)
+            ev["debit_account_id_lo"], ev["credit_account_id_lo"] = d, c
+            ev["amount_lo"] = rng.integers(1, 1000, n)
+            ev["ledger"], ev["code"] = 2, 1
+            ev["flags"] = np.where(rng.random(n) < 0.2, int(TransferFlags.pending), 0)
+            if kind == "fail":
+                bad = rng.random(n) < 0.05
+                ev["code"][bad] = 0
+            elif kind == "shuffle":
+                rng.shuffle(ev)
+            elif kind == "replay" and committed:
+                old = np.concatenate(committed)
+                pick = old[rng.integers(0, len(old), min(n, 2000))]
+                ev[:len(pick)] = pick
+                ev["amount_lo"][:len(pick) // 2] += 1
+            elif kind == "postvoid" and committed:
+                old = np.concatenate(committed)
+                pend = old[old["flags"] == int(TransferFlags.pending)]
+                if len(pend):
+                    m = min(n, len(pend))
+                    sel = pend[rng.choice(len(pend), m, replace=False)]
+                    ev = ev[:m]
+                    ev["pending_id_lo"] = sel["id_lo"]
+                    ev["debit_account_id_lo"] = 0
+                    ev["credit_account_id_lo"] = 0
+                    ev["amount_lo"] = 0
+                    ev["ledger"], ev["code"] = 0, 0
+                    ev["flags"] = np.where(rng.random(m) < 0.5, int(TransferFlags.post_pending_transfer),
+                                           int(TransferFlags.void_pending_transfer))
+            elif kind == "linked":
+                ev["flags"][0:n - 1:2] |= int(TransferFlags.linked)
+            counts = np.full(len(ev) // 8190, 8190, dtype=np.uint32)
+            if len(ev) % 8190:
+                counts = np.append(counts, len(ev) % 8190).astype(np.uint32)
+            bts = ts + np.cumsum(counts.astype(np.uint64) + 1)
+            ts = int(bts[-1])
+            go, gr, _ = gpu.create_transfers_batches(bts, counts, ev)
+            oo, orr, _ = orc.create_transfers_batches(bts, counts, ev)
+            assert np.array_equal(gr, orr), (k, kind)
+            assert_results_equal(per_batch_results(go, counts, gr), per_batch_results(oo, counts, orr), f"{k} {kind}")
+            committed.append(ev.copy())
+        assert_state_equal(gpu, orc)
+        ids = np.concatenate(committed)["id_lo"][::11].tolist() + [0, next_id + 5]
+        assert gpu.lookup_transfers(ids).tobytes() == orc.lookup_transfers(ids).tobytes()
+    finally:
+        gpu.close()

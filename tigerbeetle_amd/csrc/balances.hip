@@ -187,6 +187,11 @@ __global__ __launch_bounds__(BS_THREADS) void bs_down(SideScanArgs A, u64 m, u32
 // final balances: before(q) minus the in-chain H part, plus its own final delta.
 __global__ void bs_final(SideScanArgs A, u64 m, u32 invalid, const Bal4* __restrict__ bb, Account* __restrict__ acc,
                          u32* big) {
+    if (A.epi) {
+        const u32 e = *A.epi;
+        if (e == 0) return;
+        if (e == 2) A.cfail = A.cfail_alt;
+    }
     const u64 q = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= m) return;
     const u32 key = A.skey[q];

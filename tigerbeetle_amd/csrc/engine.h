@@ -159,6 +159,8 @@ struct SideScanArgs {
     u32 n;            // events (cfail_clear length)
     PassGate gate;
     u32 probe;        // timing probes only (TBGPU_EVAL_PROBE): 1 no chain words, 2 no account rows, 4 no block scan
+    const u32* epi;   // bs_final's gate (TrArgs::epi), or null; 2: use cfail_alt
+    const u32* cfail_alt;
 };
 
 // final-ok of a sorted side: evaluated-ok and its chain persisted

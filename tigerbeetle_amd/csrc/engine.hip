@@ -90,6 +90,8 @@ constexpr u32 PC_RING = 1024;        // pass-counter ring (passes in flight << r
 constexpr u32 PASS_GROUP_MAX = 48;   // passes enqueued between two host round trips
 constexpr u32 PC_OFF = 32;           // the pass-change ring's offset behind the counter words
 static_assert(PC_OFF >= CNT_COUNT, "counter words overlap the pass-change ring");
+constexpr u32 EPI_WORD = 28;         // the apply kernels' gate (TrArgs::epi), between the counters and the ring
+static_assert(EPI_WORD >= CNT_COUNT && EPI_WORD < PC_OFF, "gate word placement");
 
 struct tbgpu_ctx {
     int device = 0;
@@ -626,8 +628,12 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_crea
 // The general path's fixed point over one chunk (transfers.hip): classify, group,
 // the optimistic initial state, then Jacobi passes enqueued in groups without a
 // host round trip inside a group (the kernels of the passes after convergence
-// return at once), until a pass changes nothing.  Returns the converged state.
-static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n) {
+// return at once), until a pass changes nothing.  Behind every group the host also
+// enqueues the gate word and `epilogue(m)` (the apply kernels, gated on it), so when
+// the group converges they run right behind it instead of after the round trip.
+// Returns the converged state.
+template <typename Epi>
+static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilogue) {
     hipStream_t s = c->stream;
     const u64 g = C.gmask + 1;
     const u32 inv_acc = (u32)c->accounts_max;  // side keys are account rows
@@ -693,6 +699,8 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n) {
         }
         const u32 p0 = p;
         p += group;
+        tr_launch_converged(chg, PC_RING, p0, p, c->counters, c->counters + EPI_WORD, s);
+        epilogue(m);
         prof_mark(c, PH_END);
         HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, (PC_OFF + PC_RING) * sizeof(u32), hipMemcpyDeviceToHost,
                                  s));
@@ -814,21 +822,27 @@ static bool run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
     }
     c->slow_chunks++;
     TrArgs C = make_tr_args(c, ev, n, nb);
-    EvalState* A = fixed_point(c, C, n);
-
-    // apply: ranks of stored rows / results / history rows, at the device cursors
-    prof_mark(c, PH_APPLY);
-    tr_launch_mask(c->T, C, *A, c->fres, c->mask, s);
-    scan3_exclusive(c->mask, c->ranks, n, c->sc, s);
-    tr_launch_apply(c->T, C, *A, c->fres, c->ranks, c->bb, results_dev, c->counts, c->rg_part, s);
-    if (!c->rt_dry) {
-        SideScanArgs SA{};
-        SA.skey = c->skey_s; SA.sq_ev = c->sq_ev; SA.sq_cs = c->sq_cs; SA.sq_ok = c->sq_ok;
-        SA.sq_dpend = c->sq_dpend; SA.sq_dpost = c->sq_dpost; SA.cfail = A->cfail; SA.n = n;
-        side_final_balances(SA, c->side_m, (u32)c->accounts_max, c->bb, c->T.acc, c->T.big, s);
-    }
-    tr_launch_advance(c->T, C, c->ranks, c->rg_part, s);
-    prof_mark(c, PH_END);
+    C.epi = c->counters + EPI_WORD;  // the apply kernels run only behind a converged pass group
+    C.epi_alt = c->st[1];
+    // apply: ranks of stored rows / results / history rows, at the device cursors,
+    // from the converged state (st[0], or st[1] by the gate word)
+    auto epilogue = [&](u64 m) {
+        prof_mark(c, PH_APPLY);
+        tr_launch_mask(c->T, C, c->st[0], c->fres, c->mask, s);
+        scan3_exclusive(c->mask, c->ranks, n, c->sc, s);
+        tr_launch_apply(c->T, C, c->st[0], c->fres, c->ranks, c->bb, results_dev, c->counts, c->rg_part, s);
+        if (!c->rt_dry) {
+            SideScanArgs SA{};
+            SA.skey = c->skey_s; SA.sq_ev = c->sq_ev; SA.sq_cs = c->sq_cs; SA.sq_ok = c->sq_ok;
+            SA.sq_dpend = c->sq_dpend; SA.sq_dpost = c->sq_dpost; SA.n = n;
+            SA.cfail = c->st[0].cfail;
+            SA.cfail_alt = c->st[1].cfail;
+            SA.epi = C.epi;
+            side_final_balances(SA, m, (u32)c->accounts_max, c->bb, c->T.acc, c->T.big, s);
+        }
+        tr_launch_advance(c->T, C, c->ranks, c->rg_part, s);
+    };
+    fixed_point(c, C, n, epilogue);
     if (!c->rt_dry) c->rows_hi += n;
     return true;
 }

@@ -58,7 +58,18 @@ struct TrArgs {
     u32 debug;            // diagnostics: count changed events by kind (TBGPU_TRACE_PASSES)
     u32 probe;            // timing probes only (TBGPU_EVAL_PROBE, after convergence): 1 skip post/void, 2 no side records
     Sides sd;             // the account sides of the call's events (engine.h)
+    // The apply kernels' gate (tr_launch_converged): they run only when *epi != 0, so the
+    // host enqueues them behind a pass group before it knows whether the group converged
+    // (null: ungated).  *epi == 1: the converged state is the kernel's EvalState argument
+    // (st[0]), 2: epi_alt (st[1]).
+    const u32* epi;
+    EvalState epi_alt;
 };
+// epi = 1 + ((q + 1) & 1) for the first pass q of p0 .. p1 - 1 that changed nothing
+// (its result state is st[(q + 1) & 1]), when no pass halted (a re-sort or a long
+// account segment); 0 otherwise.  One thread.
+void tr_launch_converged(const u32* ring, u32 ring_len, u32 p0, u32 p1, const u32* counters, u32* epi,
+                         hipStream_t stream);
 
 void tr_launch_classify(const Tables& T, const TrArgs& C, hipStream_t stream);
 // Events sharing an id (kind 0: prev_id, ranges) or a pending id (kind 1: prev_pend),

@@ -892,7 +892,17 @@ __global__ void tr_side_rec(TrArgs C, EvalState S) {
 // ---------------------------------------------------------------- apply ----
 
 // Final result per event, as execute emits it (src/state_machine.zig:1051-1072).
+__device__ __forceinline__ bool epi_closed(const TrArgs& C) { return C.epi && *C.epi == 0; }
+// the gated kernels' converged state: the argument, or epi_alt
+__device__ __forceinline__ bool epi_state(const TrArgs& C, EvalState& S) {
+    if (!C.epi) return true;
+    const u32 e = *C.epi;
+    if (e == 2) S = C.epi_alt;
+    return e != 0;
+}
+
 __global__ void tr_mask(Tables T, TrArgs C, EvalState S, u8* fres, u8* mask) {
+    if (!epi_state(C, S)) return;
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= C.n) return;
     const u32 cs = C.cs[i];
@@ -920,6 +930,7 @@ __global__ void tr_mask(Tables T, TrArgs C, EvalState S, u8* fres, u8* mask) {
 // FL_ERROR (the host aborts, as the reference asserts).
 __global__ void tr_apply(Tables T, TrArgs C, EvalState S, const u8* __restrict__ fres, const uint4* __restrict__ rk,
                          const Bal4* __restrict__ bb, tbgpu_create_transfers_result_t* __restrict__ results) {
+    if (!epi_state(C, S)) return;
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= C.n) return;
     const u64 row_base = T.base[BASE_ROWS], hist_base = T.base[BASE_HIST];
@@ -983,6 +994,7 @@ __global__ void tr_apply(Tables T, TrArgs C, EvalState S, const u8* __restrict__
 // the same five words would serialize).
 constexpr int RG_THREADS = 1024;
 __global__ __launch_bounds__(RG_THREADS) void tr_range(Tables T, TrArgs C, EvalState S, u64* part) {
+    if (!epi_state(C, S)) return;
     __shared__ u64 sh[RG_THREADS / 64][5];
     const u32 i = blockIdx.x * RG_THREADS + threadIdx.x;
     const bool valid = i < C.n;
@@ -1016,7 +1028,8 @@ __global__ __launch_bounds__(RG_THREADS) void tr_range(Tables T, TrArgs C, EvalS
     }
 }
 
-__global__ void batch_counts(const u32* b_start, u32 nb, const uint4* rk, u32* counts) {
+__global__ void batch_counts(const u32* b_start, u32 nb, const uint4* rk, u32* counts, const u32* epi) {
+    if (epi && *epi == 0) return;
     const u32 b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b < nb) counts[b] = rk[b_start[b + 1]].y - rk[b_start[b]].y;
 }
@@ -1024,6 +1037,7 @@ __global__ void batch_counts(const u32* b_start, u32 nb, const uint4* rk, u32* c
 // Fold tr_range's block records into the index key range and commit_timestamp, and
 // advance the device cursors by the chunk's stored rows, replies and history rows.
 __global__ __launch_bounds__(256) void tr_advance(Tables T, TrArgs C, const uint4* rk, const u64* part, u32 nparts) {
+    if (epi_closed(C)) return;
     if (C.counters[CNT_FLAGS] & FL_ERROR) return;
     u64 r[5] = {0, 0, ~0ull, ~0ull, 0};
     for (u32 b = threadIdx.x; b < nparts; b += 256) {
@@ -1130,9 +1144,29 @@ void tr_launch_apply(const Tables& T, const TrArgs& C, const EvalState& S, const
                      hipStream_t stream) {
     tr_apply<<<GRID(C.n)>>>(T, C, S, fres, rk, bb, results);
     tr_range<<<(C.n + RG_THREADS - 1) / RG_THREADS, RG_THREADS, 0, stream>>>(T, C, S, part);
-    batch_counts<<<GRID(C.nb)>>>(C.b_start, C.nb, rk, counts);
+    batch_counts<<<GRID(C.nb)>>>(C.b_start, C.nb, rk, counts, C.epi);
 }
 void tr_launch_advance(const Tables& T, const TrArgs& C, const uint4* rk, const u64* part, hipStream_t stream) {
     tr_advance<<<1, 256, 0, stream>>>(T, C, rk, part, (C.n + RG_THREADS - 1) / RG_THREADS);
 }
 u64 tr_range_part_words(u64 n) { return 8 * ((n + RG_THREADS - 1) / RG_THREADS + 1); }
+
+namespace {
+__global__ void tr_converged(const u32* ring, u32 ring_len, u32 p0, u32 p1, const u32* counters, u32* epi) {
+    if (threadIdx.x != 0) return;
+    u32 e = 0;
+    if (counters[CNT_RESORT] == 0 && counters[CNT_LONG] == 0)
+        for (u32 q = p0; q < p1; q++)
+            if (ring[(q + 1) % ring_len] == 0) {
+                e = 1 + ((q + 1) & 1);
+                break;
+            }
+    *epi = e;
+}
+}  // namespace
+
+void tr_launch_converged(const u32* ring, u32 ring_len, u32 p0, u32 p1, const u32* counters, u32* epi,
+                         hipStream_t stream) {
+    tr_converged<<<1, 64, 0, stream>>>(ring, ring_len, p0, p1, counters, epi);
+    HIP_CHECK(hipGetLastError());
+}

@@ -115,5 +115,8 @@ struct Scan3Scratch {
     uint4* tile_sums;
     u64 capacity;
 };
-void scan3_exclusive(const u8* mask, uint4* out, u64 n, Scan3Scratch& s, hipStream_t stream);
+// gate (optional): the kernels return at once while *gate == 0 (enqueued before the
+// host knows whether the scan is needed)
+void scan3_exclusive(const u8* mask, uint4* out, u64 n, Scan3Scratch& s, hipStream_t stream,
+                     const u32* gate = nullptr);
 u64 scan3_tile_words(u64 capacity);

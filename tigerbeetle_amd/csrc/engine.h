@@ -276,6 +276,7 @@ enum {
     CNT_LONG = 6,       // general path: pass + 1 whose fused scan met a segment longer than its window
     CNT_RUN = 7,        // fast path: this call's rows extend the sorted run (fp_run), not the hash index
     CNT_NOKEYS = 10,    // fast path: fp_commit wrote no id keys (the run will likely take the rows)
+    CNT_FIX = 11,       // fast path: the call stands with failures: fp_fix re-places rows, writes replies (fp_run)
     CNT_GCUR = 8,       // general path: id-group ranges reserved so far
     CNT_PCUR = 9,       // general path: pending-group ranges reserved so far
     CNT_TS_SAVE = 12,   // fast path: commit_timestamp before the call (u64 in words 12-13)

@@ -174,6 +174,10 @@ struct tbgpu_ctx {
     const u8* rt_ctl = nullptr;
     bool rt_dry = false;
     u32 slow_chunks = 0;  // consecutive chunks that needed the fixed point
+    // a fast attempt enqueued without its round trip (try_fast spec): settled at the
+    // call's next wait (spec_settle), undone there if it fell back
+    bool spec_pending = false;
+    FastArgs spec_F{};
     u32 last_passes = 8;  // passes the last fixed point took (sizes the next pass group)
     bool long_segments = false;  // this call has an account segment too long for the fused scan
     // fixed-point pass counters, a ring of PC_RING words: changes per pass (the gate
@@ -568,7 +572,8 @@ static TrArgs make_tr_args(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb) {
 // Single-pass attempt (fast.hip).  Returns false, with every balance delta
 // undone, when some event needs the fixed point.  Replies go after the device
 // reply cursor; `counts_dev` receives the per-batch reply counts.
-static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_create_transfers_result_t* results_dev) {
+static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_create_transfers_result_t* results_dev,
+                     bool spec) {
     hipStream_t s = c->stream;
     if (c->rows_hi + n > c->xrow_cap) {
         refresh_bases(c);  // the bound is loose: look at the exact count
@@ -602,6 +607,22 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_crea
     fp_launch_commit(c->T, F, s);
     prof_mark(c, PH_INDEX);
     fp_launch_index(c->T, F, s);
+    if (spec) {
+        // the whole call is this one chunk: the fix (replies and rows at their ranks
+        // when there are failures) and the cursor advance are enqueued at once, gated
+        // on the device's flags, and the flags come back with the call's own final
+        // copies; spec_settle undoes the attempt if it fell back
+        prof_mark(c, PH_APPLY);
+        fp_launch_fix(c->T, F, c->mask, c->ranks, c->sc, s);
+        fp_launch_advance(c->T, F, s);
+        prof_mark(c, PH_END);
+        HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, CNT_COUNT * sizeof(u32), hipMemcpyDeviceToHost, s));
+        c->spec_F = F;
+        c->spec_pending = true;
+        c->stats.path = 1;
+        c->stats.iterations = 1;
+        return true;
+    }
     prof_mark(c, PH_END);
     // one round trip: the flags decide whether the attempt stands
     HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, CNT_COUNT * sizeof(u32), hipMemcpyDeviceToHost, s));
@@ -804,7 +825,8 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
 // Returns false (nothing committed, every effect undone) when the fast path does
 // not apply and `split` asks the caller to redo these batches in smaller chunks.
 static bool run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
-                                tbgpu_create_transfers_result_t* results_dev, bool try_fast_path, bool split) {
+                                tbgpu_create_transfers_result_t* results_dev, bool try_fast_path, bool split,
+                                bool spec = false) {
     hipStream_t s = c->stream;
     c->stats.iterations = 0;
     c->stats.path = 0;
@@ -814,7 +836,7 @@ static bool run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
     }
     const bool fast_ok = try_fast_path && !(c->opt.flags & TBGPU_OPT_FORCE_GENERAL);
     if (fast_ok) {
-        if (try_fast(c, ev, n, nb, results_dev)) {
+        if (try_fast(c, ev, n, nb, results_dev, spec)) {
             c->slow_chunks = 0;
             return true;
         }
@@ -845,6 +867,25 @@ static bool run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
     fixed_point(c, C, n, epilogue);
     if (!c->rt_dry) c->rows_hi += n;
     return true;
+}
+
+// TBGPU_NO_SPEC=1: every fast attempt waits for its own verdict (A/B timing)
+static bool spec_disabled() {
+    static const bool d = getenv("TBGPU_NO_SPEC") != nullptr;
+    return d;
+}
+
+// After the wait that follows a speculative fast attempt: true when it stood; false
+// when it fell back, with its effects undone (the caller redoes the call).
+static bool spec_settle(tbgpu_ctx* c) {
+    if (!c->spec_pending) return true;
+    c->spec_pending = false;
+    const u32 flags = c->h_counters[CNT_FLAGS];
+    if (flags & FL_ERROR) tbgpu_fatal("create_transfers", "fast path look-back did not complete", __FILE__, __LINE__);
+    if (!(flags & FL_SLOW)) return true;
+    fp_launch_undo(c->T, c->spec_F, c->stream);  // commit_timestamp back; the deltas
+    c->slow_chunks = 1;                          // the redo goes to the fixed point
+    return false;
 }
 
 static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t* timestamps, const uint32_t* counts,
@@ -900,8 +941,12 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         if (!dst_device) set_base(c, BASE_REPLIES, 0);
         tbgpu_create_transfers_result_t* rdev = dst_device ? results : (tbgpu_create_transfers_result_t*)c->res_buf;
         const bool try_fast_path = c->slow_chunks % 8 == 0;
+        // a call that is one chunk makes its fast attempt without the round trip that
+        // decides whether it stands: that answer comes with the call's final wait
+        const bool spec = try_fast_path && !c->rt_dry && b0 == 0 && b1 == nb_total &&
+                          !(c->opt.flags & TBGPU_OPT_FORCE_GENERAL) && !spec_disabled();
         if (!run_transfers_chunk(c, ev, n, nb, rdev, try_fast_path,
-                                 /*split=*/!c->rt_dry && nb > general_chunk_batches())) {
+                                 /*split=*/!c->rt_dry && nb > general_chunk_batches(), spec)) {
             small_until = b1;  // redo these batches in small chunks, on the general path
             c->slow_chunks = 1;
             continue;
@@ -911,6 +956,9 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
             // the chunk's replies (at most one per event) come back with its counts: one round trip
             HIP_CHECK(hipMemcpyAsync(c->h_res, c->res_buf, (u64)n * 8, hipMemcpyDeviceToHost, c->stream));
             wait_stream(c->stream);
+            if (!spec_settle(c))  // the speculative fast attempt fell back: redo the call
+                return transfers_batches(c, nb_total, timestamps, counts, ev_src, src_device, results, dst_device,
+                                         result_counts, ev_ts_host, ctl_host, routed_device);
             copy_results_to_batches(c, nb, starts, c->h_rc + b0, (u8*)(results + ev_off));
         }
         iters = std::max(iters, c->stats.iterations);
@@ -924,6 +972,9 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
     HIP_CHECK(hipMemcpyAsync(c->h_base, c->T.base, 4 * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
     HIP_CHECK(hipEventRecord(c->ev1, c->stream));
     wait_event(c->ev1);
+    if (!spec_settle(c))  // the speculative fast attempt fell back: redo the call
+        return transfers_batches(c, nb_total, timestamps, counts, ev_src, src_device, results, dst_device,
+                                 result_counts, ev_ts_host, ctl_host, routed_device);
     float ms = 0;
     HIP_CHECK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     c->n_rows = c->h_base[BASE_ROWS];

@@ -630,12 +630,16 @@ __global__ void fp_run(Tables T, FastArgs F) {
         }
     }
     F.counters[CNT_RUN] = take;
+    // whether the call stands with failures (the fix launches run; all of them are
+    // enqueued without waiting for this answer)
+    F.counters[CNT_FIX] = (F.counters[CNT_BAD] != 0 && !(flags & (FL_SLOW | FL_ERROR))) ? 1u : 0u;
 }
 
 // Publish the accepted ids.  fixed = false: the launch right after fp_commit, which
 // stands down when the call had failures (rows not final yet) and always clears the
 // duplicate claims; fixed = true: after fp_fix, rows from F.rows.
 __global__ void fp_index(Tables T, FastArgs F, bool fixed) {
+    if (fixed && !F.counters[CNT_FIX]) return;  // enqueued behind the fix, which may not have run
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     const u32 flags = F.counters[CNT_FLAGS];
     if (!fixed && (flags & FL_NONMONO) && i < F.n) {
@@ -832,6 +836,7 @@ __global__ void fp_chains_fin(FastArgs F) {
 
 // With failures: mask for the rank scan (bit0 accepted, bit1 failed).
 __global__ void fp_mask(FastArgs F, u8* mask) {
+    if (!F.counters[CNT_FIX]) return;
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < F.n) mask[i] = F.fres[i] == TBGPU_CREATE_TRANSFER_OK ? 1 : 2;
 }
@@ -839,6 +844,7 @@ __global__ void fp_mask(FastArgs F, u8* mask) {
 // With failures: stored rows at their ranks (re-copied from the events, so the
 // order of the writes does not matter) and the sparse replies.
 __global__ void fp_fix(FastArgs F, Tables T, const uint4* rk) {
+    if (!F.counters[CNT_FIX]) return;
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= F.n) return;
     const u32 b = fp_batch_of(F.b_start, F.nb, i);
@@ -858,6 +864,7 @@ __global__ void fp_fix(FastArgs F, Tables T, const uint4* rk) {
 // After an accepted attempt: advance the device cursors by its stored rows and replies.
 __global__ void fp_advance(Tables T, FastArgs F) {
     if (threadIdx.x != 0) return;
+    if (F.counters[CNT_FLAGS] & (FL_SLOW | FL_ERROR)) return;  // the call falls back (fp_undo)
     T.base[BASE_REPLIES] += F.counters[CNT_BAD];
     if (!F.dry) T.base[BASE_ROWS] += F.counters[CNT_OK];
 }
@@ -920,7 +927,7 @@ void fp_launch_index(const Tables& T, const FastArgs& F, hipStream_t stream) {
 
 void fp_launch_fix(const Tables& T, const FastArgs& F, u8* mask, uint4* ranks, Scan3Scratch& sc, hipStream_t stream) {
     fp_mask<<<GRID(F.n)>>>(F, mask);
-    scan3_exclusive(mask, ranks, F.n, sc, stream);
+    scan3_exclusive(mask, ranks, F.n, sc, stream, F.counters + CNT_FIX);
     fp_fix<<<GRID(F.n)>>>(F, T, ranks);
     if (!F.dry) fp_index<<<GRID(F.n)>>>(T, F, true);
     HIP_CHECK(hipGetLastError());

@@ -157,7 +157,8 @@ __device__ uint4 block_excl_scan4(uint4 v, uint4* sh, uint4* total) {
 }
 
 __global__ __launch_bounds__(SC_THREADS) void sc_reduce(const u8* __restrict__ mask, u64 n,
-                                                        uint4* __restrict__ tile_sums) {
+                                                        uint4* __restrict__ tile_sums, const u32* gate) {
+    if (gate && *gate == 0) return;
     __shared__ uint4 sh[SC_THREADS];
     const u64 base = (u64)blockIdx.x * SC_TILE + (u64)threadIdx.x * SC_IPT;
     uint4 s = make_uint4(0, 0, 0, 0);
@@ -168,7 +169,8 @@ __global__ __launch_bounds__(SC_THREADS) void sc_reduce(const u8* __restrict__ m
     if (threadIdx.x == 0) tile_sums[blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(1024) void sc_tiles(uint4* __restrict__ tile_sums, u64 ntiles) {
+__global__ __launch_bounds__(1024) void sc_tiles(uint4* __restrict__ tile_sums, u64 ntiles, const u32* gate) {
+    if (gate && *gate == 0) return;
     __shared__ uint4 sums[1024];
     const u32 tid = threadIdx.x;
     const u64 chunk = (ntiles + 1023) / 1024;
@@ -194,7 +196,9 @@ __global__ __launch_bounds__(1024) void sc_tiles(uint4* __restrict__ tile_sums, 
 }
 
 __global__ __launch_bounds__(SC_THREADS) void sc_down(const u8* __restrict__ mask, u64 n,
-                                                      const uint4* __restrict__ tile_sums, uint4* __restrict__ out) {
+                                                      const uint4* __restrict__ tile_sums, uint4* __restrict__ out,
+                                                      const u32* gate) {
+    if (gate && *gate == 0) return;
     __shared__ uint4 sh[SC_THREADS];
     const u64 base = (u64)blockIdx.x * SC_TILE + (u64)threadIdx.x * SC_IPT;
     uint4 v[SC_IPT];
@@ -242,14 +246,14 @@ void radix_sort_pairs(const u32* keys_in, const u32* vals_in, u32* keys_out, u32
 u64 scan3_tile_words(u64 capacity) { return (capacity + SC_TILE - 1) / SC_TILE + 2; }
 
 // out[i] = exclusive prefix of (bit0, bit1, bit2) of mask[0..i); out[n] = totals.
-void scan3_exclusive(const u8* mask, uint4* out, u64 n, Scan3Scratch& s, hipStream_t stream) {
+void scan3_exclusive(const u8* mask, uint4* out, u64 n, Scan3Scratch& s, hipStream_t stream, const u32* gate) {
     if (n == 0) {
         HIP_CHECK(hipMemsetAsync(out, 0, sizeof(uint4), stream));
         return;
     }
     const u64 ntiles = (n + SC_TILE - 1) / SC_TILE;
-    sc_reduce<<<(u32)ntiles, SC_THREADS, 0, stream>>>(mask, n, s.tile_sums);
-    sc_tiles<<<1, 1024, 0, stream>>>(s.tile_sums, ntiles);
-    sc_down<<<(u32)ntiles, SC_THREADS, 0, stream>>>(mask, n, s.tile_sums, out);
+    sc_reduce<<<(u32)ntiles, SC_THREADS, 0, stream>>>(mask, n, s.tile_sums, gate);
+    sc_tiles<<<1, 1024, 0, stream>>>(s.tile_sums, ntiles, gate);
+    sc_down<<<(u32)ntiles, SC_THREADS, 0, stream>>>(mask, n, s.tile_sums, out, gate);
     HIP_CHECK(hipGetLastError());
 }

@@ -160,7 +160,6 @@ struct tbgpu_ctx {
     uint2* ro_orank = nullptr;
     u32* ro_blk = nullptr;
     u32* ro_bstart = nullptr;
-    u64* ro_bts = nullptr;
     u64* ro_counts = nullptr;
     u32* ro_bcount = nullptr;  // [256] spanning counts per owner, then [world * batches] per (owner, batch)
     u64 ro_bc_cap = 0;
@@ -411,7 +410,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     // Free every device allocation by walking the struct's pointers.
-    for (void* p : {(void*)c->ro_orank, (void*)c->ro_blk, (void*)c->ro_bstart, (void*)c->ro_bts, (void*)c->ro_counts,
+    for (void* p : {(void*)c->ro_orank, (void*)c->ro_blk, (void*)c->ro_bstart, (void*)c->ro_counts,
                     (void*)c->ro_bcount, (void*)c->ro_spart})
         if (p) (void)hipFree(p);
     void* ptrs[] = {c->T.dense, c->T.acc, c->T.aidx, c->T.xrows, c->T.xful, c->T.xidx, c->T.hrows, c->T.commit_ts, c->T.idr, c->T.xrun, c->T.big, c->ev_buf,
@@ -1088,7 +1087,7 @@ extern "C" int tbgpu_route_stats(tbgpu_ctx* c, const void* events_device, uint64
     wait_stream(c->route_stream);
     return 0;
 }
-void route_scatter(const Transfer* ev, u64 n, u32 world, u32 nb, const u32* b_start, const u64* b_ts, u64 g0,
+void route_scatter(const Transfer* ev, u64 n, u32 world, u32 nb, const u32* b_start, u64 g0,
                    uint2* orank, u32* blk, u64* counts, Transfer* out_ev, u64* out_side, u32* bcount, u32* scount,
                    u32 pack_mask, u32* out_packed, u32* error, bool ranked, hipStream_t stream);
 void route_unpack_rows(const u32* packed, u64 m, u32 mask, const u32* sub_off, const u32* sub_g, u32 nsub,
@@ -1103,7 +1102,7 @@ static void route_capacity(tbgpu_ctx* c, u32 world, u32 batch_count, u64 n) {
     if (n > c->ro_cap || world * std::max<u64>(nblk, 1) > c->ro_bcap || batch_count + 1 > c->ro_cap + 2 ||
         (u64)world * batch_count > c->ro_bc_cap) {
         wait_stream(c->route_stream);
-        for (void* p : {(void*)c->ro_orank, (void*)c->ro_blk, (void*)c->ro_bstart, (void*)c->ro_bts, (void*)c->ro_counts,
+        for (void* p : {(void*)c->ro_orank, (void*)c->ro_blk, (void*)c->ro_bstart, (void*)c->ro_counts,
                         (void*)c->ro_bcount, (void*)c->ro_spart})
             if (p) HIP_CHECK(hipFree(p));
         c->ro_cap = std::max<u64>(std::max<u64>(n, batch_count + 1), c->ro_cap);
@@ -1112,7 +1111,6 @@ static void route_capacity(tbgpu_ctx* c, u32 world, u32 batch_count, u64 n) {
         HIP_CHECK(hipMalloc((void**)&c->ro_orank, c->ro_cap * sizeof(uint2)));
         HIP_CHECK(hipMalloc((void**)&c->ro_blk, c->ro_bcap * sizeof(u32)));
         HIP_CHECK(hipMalloc((void**)&c->ro_bstart, (c->ro_cap + 3) * sizeof(u32)));
-        HIP_CHECK(hipMalloc((void**)&c->ro_bts, (c->ro_cap + 3) * sizeof(u64)));
         HIP_CHECK(hipMalloc((void**)&c->ro_counts, 256 * sizeof(u64)));
         c->ro_bc_cap = std::max<u64>((u64)world * std::max<u32>(batch_count, 1), 256ull * 64);
         HIP_CHECK(hipMalloc((void**)&c->ro_bcount, (c->ro_bc_cap + 256) * sizeof(u32)));
@@ -1159,7 +1157,7 @@ static int route_scatter_any(tbgpu_ctx* c, uint32_t world, uint32_t batch_count,
     HIP_CHECK(hipMemsetAsync(err, 0, sizeof(u32), c->route_stream));
     HIP_CHECK(hipMemcpyAsync(c->ro_bstart, starts.data(), (batch_count + 1) * sizeof(u32), hipMemcpyHostToDevice,
                              c->route_stream));
-    route_scatter((const Transfer*)events_device, n, world, batch_count, c->ro_bstart, nullptr, first_global_batch,
+    route_scatter((const Transfer*)events_device, n, world, batch_count, c->ro_bstart, first_global_batch,
                   c->ro_orank, c->ro_blk, c->ro_counts, (Transfer*)send_events_device, (u64*)send_records_device,
                   c->ro_bcount + 256, c->ro_bcount, word_mask, (u32*)send_packed_device, err, ranked, c->route_stream);
     HIP_CHECK(hipMemcpyAsync(send_counts, c->ro_counts, world * sizeof(u64), hipMemcpyDeviceToHost, c->route_stream));

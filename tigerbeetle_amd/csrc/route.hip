@@ -10,11 +10,15 @@
 //   global batch << 32 | chain start (index of the chain's first member) << 15 |
 //   ends its chain << 14 | chain spans owners << 13 | index in its batch.
 // The owner derives the timestamp T - n + index + 1 from the batch's (T, n), which
-// every rank knows (tbgpu_route_unpack), so the all-to-all moves 136 bytes per
-// event, not 160.
+// every rank knows (tbgpu_route_unpack).  On several ranks the all-to-all moves the
+// packed wire format: only the 4-byte words that are nonzero in some event of the
+// step (the union mask the first pass finds), then the record's low word (the owner
+// knows each row's batch from the per-(owner, batch) counts): 64 bytes per config-4
+// event instead of 128 + 8 (rt_scatter's packed mode, rt_unpack_rows).
 // Launches: classify + stable rank within the workgroup (with the step's
-// eligibility figures in the same pass over the events), an exclusive scan of the
-// (owner, workgroup) counts, scatter.  Pure data movement: HBM-bound.
+// eligibility figures and nonzero-word mask in the same pass over the events), an
+// exclusive scan of the (owner, workgroup) counts, scatter.  Pure data movement:
+// HBM-bound.
 #include "common.h"
 
 namespace {
@@ -28,7 +32,6 @@ struct RouteArgs {
     u32 world;
     u32 nb;
     const u32* b_start;   // [nb + 1] first event of each local batch
-    const u64* b_ts;      // [nb] prepare timestamp of each local batch
     u64 g0;               // global number of the first local batch
     uint2* orank;         // [n] owner, rank within (workgroup, owner)
     u32* blk;             // [world * nblk] per-owner counts, then their exclusive scan
@@ -536,7 +539,7 @@ void route_unpack(const u64* rec, u64 n, const u64* ts_base, u64 batches, u64* t
     HIP_CHECK(hipGetLastError());
 }
 
-void route_scatter(const Transfer* ev, u64 n, u32 world, u32 nb, const u32* b_start, const u64* b_ts, u64 g0,
+void route_scatter(const Transfer* ev, u64 n, u32 world, u32 nb, const u32* b_start, u64 g0,
                    uint2* orank, u32* blk, u64* counts, Transfer* out_ev, u64* out_side, u32* bcount, u32* scount,
                    u32 pack_mask, u32* out_packed, u32* error, bool ranked, hipStream_t stream) {
     RouteArgs A{};
@@ -547,7 +550,7 @@ void route_scatter(const Transfer* ev, u64 n, u32 world, u32 nb, const u32* b_st
     A.scount = scount;
     HIP_CHECK(hipMemsetAsync(bcount, 0, (u64)world * nb * sizeof(u32), stream));
     HIP_CHECK(hipMemsetAsync(scount, 0, world * sizeof(u32), stream));
-    A.ev = ev; A.n = n; A.world = world; A.nb = nb; A.b_start = b_start; A.b_ts = b_ts; A.g0 = g0;
+    A.ev = ev; A.n = n; A.world = world; A.nb = nb; A.b_start = b_start; A.g0 = g0;
     A.orank = orank; A.blk = blk; A.nblk = (u32)route_block_count(n); A.counts = counts;
     A.out_ev = out_ev; A.out_side = out_side;
     if (n && !ranked) rt_rank<<<A.nblk, RT_THREADS, 0, stream>>>(A);

@@ -638,8 +638,36 @@ __global__ void fp_run(Tables T, FastArgs F) {
 // Publish the accepted ids.  fixed = false: the launch right after fp_commit, which
 // stands down when the call had failures (rows not final yet) and always clears the
 // duplicate claims; fixed = true: after fp_fix, rows from F.rows.
+// One wave: tiles k0 .. k0 + 63's componentwise id ranges into T.idr.
+__device__ __forceinline__ void fp_fold_idr(const Tables& T, const FastArgs& F, u32 k0, u32 ntiles) {
+    if (k0 >= ntiles) return;
+    const u32 k = k0 + (threadIdx.x & 63);
+    u64 r[4] = {0, 0, ~0ull, ~0ull};
+    if (k < ntiles)
+        for (int w = 0; w < 4; w++) r[w] = F.tile_idr[TILE_WORDS * k + w];
+    for (int off = 32; off > 0; off >>= 1) {
+        r[0] = max(r[0], (u64)__shfl_xor((unsigned long long)r[0], off));
+        r[1] = max(r[1], (u64)__shfl_xor((unsigned long long)r[1], off));
+        r[2] = min(r[2], (u64)__shfl_xor((unsigned long long)r[2], off));
+        r[3] = min(r[3], (u64)__shfl_xor((unsigned long long)r[3], off));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax((unsigned long long*)&T.idr[0], (unsigned long long)r[0]);
+        atomicMax((unsigned long long*)&T.idr[1], (unsigned long long)r[1]);
+        atomicMin((unsigned long long*)&T.idr[2], (unsigned long long)r[2]);
+        atomicMin((unsigned long long*)&T.idr[3], (unsigned long long)r[3]);
+    }
+}
+
 __global__ void fp_index(Tables T, FastArgs F, bool fixed) {
-    if (fixed && !F.counters[CNT_FIX]) return;  // enqueued behind the fix, which may not have run
+    if (fixed) {  // after fp_fix: the accepted ids at their final rows (grid-stride; gated like the fix)
+        if (!F.counters[CNT_FIX] || F.dry) return;
+        const u32 ntiles = (F.n + FP_THREADS - 1) / FP_THREADS;
+        if (threadIdx.x < 64)
+            for (u32 k0 = blockIdx.x * 64; k0 < ntiles; k0 += gridDim.x * 64) fp_fold_idr(T, F, k0, ntiles);
+        FOR_EACH_EVENT(j) if (F.fres[j] == TBGPU_CREATE_TRANSFER_OK) xidx_insert(T, fp_key(F, j), F.rows[j]);
+        return;
+    }
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     const u32 flags = F.counters[CNT_FLAGS];
     if (!fixed && (flags & FL_NONMONO) && i < F.n) {
@@ -671,29 +699,12 @@ __global__ void fp_index(Tables T, FastArgs F, bool fixed) {
     if (F.dry) return;
     if (!fixed && F.counters[CNT_BAD] != 0) return;
     if (!fixed && F.counters[CNT_RUN]) return;  // the rows extend the sorted run
-    if (threadIdx.x < 64 && blockIdx.x * 64 < ntiles) {
-        // fold the tiles' id ranges into the index's key range: one wave per 64
-        // tiles (a single wave over 16k tiles was a serial tail of this launch)
-        const u32 k = blockIdx.x * 64 + threadIdx.x;
-        u64 r[4] = {0, 0, ~0ull, ~0ull};
-        if (k < ntiles)
-            for (int w = 0; w < 4; w++) r[w] = F.tile_idr[TILE_WORDS * k + w];
-        for (int off = 32; off > 0; off >>= 1) {
-            r[0] = max(r[0], (u64)__shfl_xor((unsigned long long)r[0], off));
-            r[1] = max(r[1], (u64)__shfl_xor((unsigned long long)r[1], off));
-            r[2] = min(r[2], (u64)__shfl_xor((unsigned long long)r[2], off));
-            r[3] = min(r[3], (u64)__shfl_xor((unsigned long long)r[3], off));
-        }
-        if (threadIdx.x == 0) {
-            atomicMax((unsigned long long*)&T.idr[0], (unsigned long long)r[0]);
-            atomicMax((unsigned long long*)&T.idr[1], (unsigned long long)r[1]);
-            atomicMin((unsigned long long*)&T.idr[2], (unsigned long long)r[2]);
-            atomicMin((unsigned long long*)&T.idr[3], (unsigned long long)r[3]);
-        }
-    }
+    // fold the tiles' id ranges into the index's key range: one wave per 64 tiles (a
+    // single wave over 16k tiles was a serial tail of this launch)
+    if (threadIdx.x < 64) fp_fold_idr(T, F, blockIdx.x * 64, ntiles);
     if (i >= F.n) return;
     if (F.fres[i] != TBGPU_CREATE_TRANSFER_OK) return;
-    xidx_insert(T, fp_key(F, i), fixed ? F.rows[i] : (u32)(T.base[BASE_ROWS] + i));
+    xidx_insert(T, fp_key(F, i), (u32)(T.base[BASE_ROWS] + i));
 }
 
 __device__ __forceinline__ bool fp_linked(const FastArgs& F, u32 j) {
@@ -835,18 +846,17 @@ __global__ void fp_chains_fin(FastArgs F) {
 }
 
 // With failures: mask for the rank scan (bit0 accepted, bit1 failed).
+// The fix launches are enqueued whether or not the call has failures (CNT_FIX decides
+// on the device), so they run small grid-stride grids: a full grid that stands down
+// still costs its dispatch.
 __global__ void fp_mask(FastArgs F, u8* mask) {
     if (!F.counters[CNT_FIX]) return;
-    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < F.n) mask[i] = F.fres[i] == TBGPU_CREATE_TRANSFER_OK ? 1 : 2;
+    FOR_EACH_EVENT(i) mask[i] = F.fres[i] == TBGPU_CREATE_TRANSFER_OK ? 1 : 2;
 }
 
 // With failures: stored rows at their ranks (re-copied from the events, so the
 // order of the writes does not matter) and the sparse replies.
-__global__ void fp_fix(FastArgs F, Tables T, const uint4* rk) {
-    if (!F.counters[CNT_FIX]) return;
-    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= F.n) return;
+__device__ __forceinline__ void fp_fix_one(const FastArgs& F, const Tables& T, const uint4* rk, u32 i) {
     const u32 b = fp_batch_of(F.b_start, F.nb, i);
     const u32 bs = F.b_start[b];
     const u8 r = F.fres[i];
@@ -859,6 +869,11 @@ __global__ void fp_fix(FastArgs F, Tables T, const uint4* rk) {
     t.timestamp = F.ev_ts ? F.ev_ts[i] : F.b_ts[b] - (F.b_start[b + 1] - bs) + (i - bs) + 1;
     T.xrows[row] = t;
     F.rows[i] = row;
+}
+
+__global__ void fp_fix(FastArgs F, Tables T, const uint4* rk) {
+    if (!F.counters[CNT_FIX]) return;
+    FOR_EACH_EVENT(i) fp_fix_one(F, T, rk, i);
 }
 
 // After an accepted attempt: advance the device cursors by its stored rows and replies.
@@ -926,10 +941,11 @@ void fp_launch_index(const Tables& T, const FastArgs& F, hipStream_t stream) {
 }
 
 void fp_launch_fix(const Tables& T, const FastArgs& F, u8* mask, uint4* ranks, Scan3Scratch& sc, hipStream_t stream) {
-    fp_mask<<<GRID(F.n)>>>(F, mask);
+    const u32 sg = std::max<u32>(std::min<u32>((F.n + 255) / 256, 2048), 1);
+    fp_mask<<<sg, 256, 0, stream>>>(F, mask);
     scan3_exclusive(mask, ranks, F.n, sc, stream, F.counters + CNT_FIX);
-    fp_fix<<<GRID(F.n)>>>(F, T, ranks);
-    if (!F.dry) fp_index<<<GRID(F.n)>>>(T, F, true);
+    fp_fix<<<sg, 256, 0, stream>>>(F, T, ranks);
+    if (!F.dry) fp_index<<<sg, 256, 0, stream>>>(T, F, true);
     HIP_CHECK(hipGetLastError());
 }
 

@@ -570,6 +570,11 @@ void fp_commit(Tables T, FastArgs F) {
         if (wp[k]) __hip_atomic_fetch_add((unsigned long long*)&wp[k][0], (unsigned long long)av[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
 #endif
+#if defined(FP_SKIP_HOT)  // timing-only variant (profiles/variants.py): no flush for the hottest rows; results wrong
+#pragma unroll
+    for (int k = 0; k < PER; k++)
+        if (wp[k] && (s_keys[tid + k * FP_THREADS] >> 2) < FP_SKIP_HOT) wp[k] = nullptr;
+#endif
 #pragma unroll
     for (int k = 0; k < PER; k++)
         old[k] = wp[k] ? atomicAdd((unsigned long long*)&wp[k][0], (unsigned long long)av[k]) : 0;

@@ -88,6 +88,7 @@ T* dalloc(u64 count, u64* total) {
 
 constexpr u32 PC_RING = 1024;        // pass-counter ring (passes in flight << ring)
 constexpr u32 PASS_GROUP_MAX = 48;   // passes enqueued between two host round trips
+constexpr u32 RPT_BASE = CNT_COUNT, RPT_COUNTS = CNT_COUNT + 8;  // k_report's layout (words)
 constexpr u32 PC_OFF = 32;           // the pass-change ring's offset behind the counter words
 static_assert(PC_OFF >= CNT_COUNT, "counter words overlap the pass-change ring");
 constexpr u32 EPI_WORD = 28;         // the apply kernels' gate (TrArgs::epi), between the counters and the ring
@@ -186,6 +187,10 @@ struct tbgpu_ctx {
     u32* h_pc = nullptr;       // pinned mirror of the change ring
     u64* h_base = nullptr;     // pinned mirror of T.base
     u32* h_rc = nullptr;       // pinned per-batch reply counts of the current call
+    // the end of a call in one copy (k_report): counter words, T.base, the last chunk's
+    // reply counts
+    u32* report = nullptr;
+    u32* h_report = nullptr;  // pinned
     u64 h_rc_cap = 0;
     u64 rows_hi = 0;           // upper bound of T.base[BASE_ROWS] (n_rows + events enqueued since)
     // account-transfers index (query.hip), allocated by the first compaction
@@ -281,11 +286,13 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->rt_dry_ts = dalloc<u64>(1, &B);
     c->rt_stats = dalloc<u64>(8, &B);
     c->pc = c->counters + PC_OFF;
+    c->report = dalloc<u32>(RPT_COUNTS + c->bmax, &B);
     c->rg_part = dalloc<u64>(tr_range_part_words(n), &B);
 
     HIP_CHECK(hipHostMalloc((void**)&c->h_base, 8 * sizeof(u64), hipHostMallocDefault));  // [4..5]: a uint4
     HIP_CHECK(hipHostMalloc((void**)&c->h_counters, (PC_OFF + 2 * PC_RING) * sizeof(u32), hipHostMallocDefault));
     c->h_pc = c->h_counters + PC_OFF;
+    HIP_CHECK(hipHostMalloc((void**)&c->h_report, (RPT_COUNTS + c->bmax) * sizeof(u32), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc((void**)&c->h_res, c->nmax * 8 + 8, hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc((void**)&c->h_counts, c->bmax * sizeof(u32), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc((void**)&c->h_stage_start, (batch_ts_offset(c->bmax) + 2 * c->bmax) * sizeof(u32),
@@ -430,6 +437,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
         for (void* p : q) if (p) (void)hipFree(p);
     }
     if (c->h_counters) (void)hipHostFree(c->h_counters);
+    if (c->h_report) (void)hipHostFree(c->h_report);
     if (c->h_counts) (void)hipHostFree(c->h_counts);
     if (c->h_stage_start) (void)hipHostFree(c->h_stage_start);
     if (c->h_base) (void)hipHostFree(c->h_base);
@@ -444,6 +452,16 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
 }
 
 // ------------------------------------------------------------ helpers -----
+
+// The end of a call: counter words, the device cursors and the last chunk's reply
+// counts gathered into one buffer, so that one copy brings them back (three small
+// copies were three blit dispatches).
+__global__ void k_report(const u32* counters, const u64* base, const u32* counts, u32 nb, u32* out) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < RPT_BASE) out[i] = counters[i];
+    else if (i < RPT_COUNTS) out[i] = ((const u32*)base)[i - RPT_BASE];
+    else if (i < RPT_COUNTS + nb) out[i] = counts[i - RPT_COUNTS];
+}
 
 static void read_counters(tbgpu_ctx* c) {
     HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, CNT_COUNT * sizeof(u32), hipMemcpyDeviceToHost, c->stream));
@@ -605,6 +623,30 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_crea
     prof_mark(c, PH_CLASSIFY);
     fp_launch_commit(c->T, F, s);
     prof_mark(c, PH_INDEX);
+    static const bool no_tail = getenv("TBGPU_NO_TAIL") != nullptr;  // A/B timing of the launch sequence
+    if (n <= FP_TAIL_MAX && !no_tail) {
+        // a small call: index, fix and advance in one workgroup, gated on the device's
+        // flags like the speculative launches below
+        fp_launch_tail(c->T, F, s);
+        prof_mark(c, PH_END);
+        c->stats.path = 1;
+        c->stats.iterations = 1;
+        if (spec) {  // the flags come back with the call's k_report
+            c->spec_F = F;
+            c->spec_pending = true;
+            return true;
+        }
+        HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, CNT_COUNT * sizeof(u32), hipMemcpyDeviceToHost, s));
+        wait_stream(s);
+        const u32 flags = c->h_counters[CNT_FLAGS];
+        if (flags & FL_ERROR) tbgpu_fatal("create_transfers", "fast path look-back did not complete", __FILE__, __LINE__);
+        if (flags & FL_SLOW) {
+            fp_launch_undo(c->T, F, s);
+            return false;
+        }
+        if (!F.dry) c->rows_hi += c->h_counters[CNT_OK];
+        return true;
+    }
     fp_launch_index(c->T, F, s);
     if (spec) {
         // the whole call is this one chunk: the fix (replies and rows at their ranks
@@ -615,8 +657,7 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_crea
         fp_launch_fix(c->T, F, c->mask, c->ranks, c->sc, s);
         fp_launch_advance(c->T, F, s);
         prof_mark(c, PH_END);
-        HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, CNT_COUNT * sizeof(u32), hipMemcpyDeviceToHost, s));
-        c->spec_F = F;
+        c->spec_F = F;  // the flags come back with the call's k_report
         c->spec_pending = true;
         c->stats.path = 1;
         c->stats.iterations = 1;
@@ -899,6 +940,7 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
     u32 iters = 0;
     u64 sorts = 0;
     c->stats.sorts = 0;
+    bool ended = false;   // the last chunk brought the call's end back (k_report)
     u32 small_until = 0;  // batches before this one go in general-path-sized chunks
     set_base(c, BASE_REPLIES, 0);  // the call's replies start at the front of `results`
     c->long_segments = false;
@@ -937,7 +979,7 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         }
         // device results: the call's buffer (cursor-relative); host results: staged in
         // res_buf one chunk at a time
-        if (!dst_device) set_base(c, BASE_REPLIES, 0);
+        if (!dst_device && ev_off != 0) set_base(c, BASE_REPLIES, 0);  // (reset above for the first chunk)
         tbgpu_create_transfers_result_t* rdev = dst_device ? results : (tbgpu_create_transfers_result_t*)c->res_buf;
         const bool try_fast_path = c->slow_chunks % 8 == 0;
         // a call that is one chunk makes its fast attempt without the round trip that
@@ -950,15 +992,35 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
             c->slow_chunks = 1;
             continue;
         }
-        HIP_CHECK(hipMemcpyAsync(c->h_rc + b0, c->counts, nb * sizeof(u32), hipMemcpyDeviceToHost, c->stream));
-        if (!dst_device) {
-            // the chunk's replies (at most one per event) come back with its counts: one round trip
-            HIP_CHECK(hipMemcpyAsync(c->h_res, c->res_buf, (u64)n * 8, hipMemcpyDeviceToHost, c->stream));
-            wait_stream(c->stream);
+        if (b1 == nb_total) {
+            // the call's end: counters, cursors and reply counts in one copy, with the
+            // replies, and one wait
+            k_report<<<(RPT_COUNTS + nb + 255) / 256, 256, 0, c->stream>>>(c->counters, c->T.base, c->counts, nb,
+                                                                           c->report);
+            HIP_CHECK(hipGetLastError());
+            HIP_CHECK(hipMemcpyAsync(c->h_report, c->report, (RPT_COUNTS + nb) * sizeof(u32), hipMemcpyDeviceToHost,
+                                     c->stream));
+            if (!dst_device)
+                HIP_CHECK(hipMemcpyAsync(c->h_res, c->res_buf, (u64)n * 8, hipMemcpyDeviceToHost, c->stream));
+            HIP_CHECK(hipEventRecord(c->ev1, c->stream));
+            wait_event(c->ev1);
+            memcpy(c->h_counters, c->h_report, CNT_COUNT * sizeof(u32));
+            memcpy(c->h_base, c->h_report + RPT_BASE, 4 * sizeof(u64));
+            memcpy(c->h_rc + b0, c->h_report + RPT_COUNTS, nb * sizeof(u32));
             if (!spec_settle(c))  // the speculative fast attempt fell back: redo the call
                 return transfers_batches(c, nb_total, timestamps, counts, ev_src, src_device, results, dst_device,
                                          result_counts, ev_ts_host, ctl_host, routed_device);
-            copy_results_to_batches(c, nb, starts, c->h_rc + b0, (u8*)(results + ev_off));
+            if (!dst_device) copy_results_to_batches(c, nb, starts, c->h_rc + b0, (u8*)(results + ev_off));
+            ended = true;
+        } else {
+            HIP_CHECK(hipMemcpyAsync(c->h_rc + b0, c->counts, nb * sizeof(u32), hipMemcpyDeviceToHost, c->stream));
+            if (!dst_device) {
+                // the chunk's replies (at most one per event) come back with its counts: one
+                // round trip (no speculative attempt here: that is a one-chunk call)
+                HIP_CHECK(hipMemcpyAsync(c->h_res, c->res_buf, (u64)n * 8, hipMemcpyDeviceToHost, c->stream));
+                wait_stream(c->stream);
+                copy_results_to_batches(c, nb, starts, c->h_rc + b0, (u8*)(results + ev_off));
+            }
         }
         iters = std::max(iters, c->stats.iterations);
         sorts += c->stats.sorts;
@@ -967,10 +1029,11 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         events += n;
         b0 = b1;
     }
-    // the device cursors come back with the call's end (no extra round trip)
-    HIP_CHECK(hipMemcpyAsync(c->h_base, c->T.base, 4 * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
-    HIP_CHECK(hipEventRecord(c->ev1, c->stream));
-    wait_event(c->ev1);
+    if (!ended) {  // no batches
+        HIP_CHECK(hipMemcpyAsync(c->h_base, c->T.base, 4 * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+        HIP_CHECK(hipEventRecord(c->ev1, c->stream));
+        wait_event(c->ev1);
+    }
     if (!spec_settle(c))  // the speculative fast attempt fell back: redo the call
         return transfers_batches(c, nb_total, timestamps, counts, ev_src, src_device, results, dst_device,
                                  result_counts, ev_ts_host, ctl_host, routed_device);

@@ -28,6 +28,9 @@ struct FastArgs {
     u32 ablate;         // timing-only builds (TBGPU_ABLATE): skip parts of the work; results wrong
 };
 constexpr u32 TILE_WORDS = 6;
+// calls of at most FP_TAIL_MAX events run fp_launch_tail (one workgroup) instead of
+// fp_launch_index + fp_launch_fix + fp_launch_advance
+constexpr u32 FP_TAIL_THREADS = 1024, FP_TAIL_MAX = 16384;
 enum { ABL_DUP = 1, ABL_BALANCES = 2, ABL_ROWS = 4, ABL_LOOKBACK = 8, ABL_EVENT = 16, ABL_PROBE = 32 };
 
 void fp_launch_prep(const FastArgs& F, hipStream_t stream);
@@ -35,5 +38,6 @@ void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream);
 void fp_launch_index(const Tables& T, const FastArgs& F, hipStream_t stream);
 void fp_launch_fix(const Tables& T, const FastArgs& F, u8* mask, uint4* ranks, Scan3Scratch& sc, hipStream_t stream);
 void fp_launch_undo(const Tables& T, const FastArgs& F, hipStream_t stream);
+void fp_launch_tail(const Tables& T, const FastArgs& F, hipStream_t stream);
 void fp_launch_advance(const Tables& T, const FastArgs& F, hipStream_t stream);
 u64 fp_tiles(u64 n);

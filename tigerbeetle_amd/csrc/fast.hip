@@ -613,11 +613,9 @@ __global__ void fp_dupcheck(Tables T, FastArgs F) {
 // every event accepted, ids strictly increasing, the first above the run's last id
 // and the rows right after the run's.  Then the run takes them (CNT_RUN) and
 // fp_index inserts nothing; otherwise fp_index hashes them as before.  One thread.
-__global__ void fp_run(Tables T, FastArgs F) {
-    if (threadIdx.x != 0) return;
-    const u32 flags = F.counters[CNT_FLAGS];
+__device__ void fp_run_one(const Tables& T, const FastArgs& F, u32 flags, u32 bad) {
     u32 take = 0;
-    if (!F.dry && F.n && !(flags & (FL_SLOW | FL_ERROR | FL_NONMONO)) && F.counters[CNT_BAD] == 0) {
+    if (!F.dry && F.n && !(flags & (FL_SLOW | FL_ERROR | FL_NONMONO)) && bad == 0) {
         u64* r = T.xrun;
         const u64 row0 = T.base[BASE_ROWS];
         const u128 first = F.ev[0].id, last = F.ev[F.n - 1].id;
@@ -637,7 +635,11 @@ __global__ void fp_run(Tables T, FastArgs F) {
     F.counters[CNT_RUN] = take;
     // whether the call stands with failures (the fix launches run; all of them are
     // enqueued without waiting for this answer)
-    F.counters[CNT_FIX] = (F.counters[CNT_BAD] != 0 && !(flags & (FL_SLOW | FL_ERROR))) ? 1u : 0u;
+    F.counters[CNT_FIX] = (bad != 0 && !(flags & (FL_SLOW | FL_ERROR))) ? 1u : 0u;
+}
+
+__global__ void fp_run(Tables T, FastArgs F) {
+    if (threadIdx.x == 0) fp_run_one(T, F, F.counters[CNT_FLAGS], F.counters[CNT_BAD]);
 }
 
 // Publish the accepted ids.  fixed = false: the launch right after fp_commit, which
@@ -861,15 +863,15 @@ __global__ void fp_mask(FastArgs F, u8* mask) {
 
 // With failures: stored rows at their ranks (re-copied from the events, so the
 // order of the writes does not matter) and the sparse replies.
-__device__ __forceinline__ void fp_fix_one(const FastArgs& F, const Tables& T, const uint4* rk, u32 i) {
+__device__ __forceinline__ void fp_fix_one(const FastArgs& F, const Tables& T, u32 i, u32 rank_ok, u32 rank_bad) {
     const u32 b = fp_batch_of(F.b_start, F.nb, i);
     const u32 bs = F.b_start[b];
     const u8 r = F.fres[i];
     if (r != TBGPU_CREATE_TRANSFER_OK) {
-        F.results[T.base[BASE_REPLIES] + rk[i].y] = {i - bs, (u32)r};  // concatenated replies
+        F.results[T.base[BASE_REPLIES] + rank_bad] = {i - bs, (u32)r};  // concatenated replies
         return;
     }
-    const u32 row = (u32)(T.base[BASE_ROWS] + rk[i].x);
+    const u32 row = (u32)(T.base[BASE_ROWS] + rank_ok);
     Transfer t = F.ev[i];
     t.timestamp = F.ev_ts ? F.ev_ts[i] : F.b_ts[b] - (F.b_start[b + 1] - bs) + (i - bs) + 1;
     T.xrows[row] = t;
@@ -878,7 +880,7 @@ __device__ __forceinline__ void fp_fix_one(const FastArgs& F, const Tables& T, c
 
 __global__ void fp_fix(FastArgs F, Tables T, const uint4* rk) {
     if (!F.counters[CNT_FIX]) return;
-    FOR_EACH_EVENT(i) fp_fix_one(F, T, rk, i);
+    FOR_EACH_EVENT(i) fp_fix_one(F, T, i, rk[i].x, rk[i].y);
 }
 
 // After an accepted attempt: advance the device cursors by its stored rows and replies.
@@ -898,6 +900,129 @@ __global__ void fp_prep(FastArgs F) {
     if (k < CNT_TS_SAVE) F.counters[k] = 0;
     if (k == 0) *(u64*)&F.counters[CNT_TS_SAVE] = *F.commit_ts;
     if (k < F.nb) F.batch_counts[k] = 0;
+}
+
+// Small calls (n <= FP_TAIL_MAX, e.g. one drop-in batch of 8190): everything after
+// fp_commit in ONE workgroup, the launches of fp_launch_index, fp_launch_fix and
+// fp_launch_advance run as phases separated by barriers.  A batch of 8190 events
+// is ~2 us of work per phase, but each of those ~12 launches cost its dispatch and
+// host enqueue (the single-call timeline in profiles/README.md); this keeps the
+// small call at 3 launches.  Same results as the launch sequence, phase by phase.
+// Counters written by atomics in this launch are read with agent-scope loads (not
+// through the CU's L1) and broadcast through LDS so that every branch is uniform.
+__device__ __forceinline__ u32 fp_cnt(const FastArgs& F, int k) {
+    return __hip_atomic_load(&F.counters[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(FP_TAIL_THREADS) void fp_tail(Tables T, FastArgs F) {
+    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6, n = F.n;
+    const u32 ntiles = (n + FP_THREADS - 1) / FP_THREADS;
+    __shared__ u32 s_flags, s_bad, s_run, s_ok;
+    __shared__ u32 s_wsum[FP_TAIL_THREADS / 64];
+    if (tid == 0) s_flags = fp_cnt(F, CNT_FLAGS);
+    __syncthreads();
+    // fp_dupcheck
+    if (s_flags & FL_NONMONO)
+        for (u32 i = tid; i < n; i += FP_TAIL_THREADS) fp_dupcheck_one(F, i);
+    __syncthreads();
+    if (tid == 0) s_flags = fp_cnt(F, CNT_FLAGS);
+    __syncthreads();
+    const u32 flags = s_flags;
+    // fp_chains, fp_chains_fin
+    const bool chains = (flags & FL_FCHAIN) && !(flags & (FL_SLOW | FL_ERROR));
+    if (chains) {
+        u32 n_ok = 0, n_bad = 0;
+        u64 mts = 0;
+        for (u32 i = tid; i < n; i += FP_TAIL_THREADS) fp_chains_one(T, F, i, n_ok, n_bad, mts);
+        for (int off = 32; off > 0; off >>= 1) {
+            n_ok += __shfl_xor(n_ok, off);
+            n_bad += __shfl_xor(n_bad, off);
+            mts = max(mts, (u64)__shfl_xor((unsigned long long)mts, off));
+        }
+        if (lane == 0) {
+            if (n_ok) atomicAdd(&F.counters[CNT_OK], n_ok);
+            if (n_bad) atomicAdd(&F.counters[CNT_BAD], n_bad);
+            if (mts) atomicMax((unsigned long long*)F.commit_ts, (unsigned long long)mts);
+        }
+        __syncthreads();
+        for (u32 i = tid; i < n; i += FP_TAIL_THREADS) {
+            const u8 r = F.fres[i];
+            if ((r & FRES_CHAIN) && r != FRES_SLOW) F.fres[i] = F.fres2[i];
+        }
+    }
+    __syncthreads();
+    // fp_run
+    if (tid == 0) {
+        s_bad = fp_cnt(F, CNT_BAD);
+        fp_run_one(T, F, flags, s_bad);
+        s_run = F.counters[CNT_RUN];
+    }
+    __syncthreads();
+    const u32 bad = s_bad;
+    // fp_index (first launch): clear the claims, the tiles' accepted count and
+    // timestamp, then the ids when the call stands without failures
+    if (flags & FL_NONMONO)
+        for (u32 i = tid; i < n; i += FP_TAIL_THREADS) {
+            const u32 g = F.gpos[i];
+            if (g != NONE32) F.gtab[g] = 0;
+        }
+    if (w == 0) {
+        u64 mts = 0, nok = 0;
+        for (u32 k = lane; k < ntiles; k += 64) {
+            mts = max(mts, F.tile_idr[TILE_WORDS * k + 4]);
+            nok += F.tile_idr[TILE_WORDS * k + 5];
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            mts = max(mts, (u64)__shfl_xor((unsigned long long)mts, off));
+            nok += (u64)__shfl_xor((unsigned long long)nok, off);
+        }
+        if (lane == 0) {
+            if (nok) atomicAdd(&F.counters[CNT_OK], (u32)nok);
+            if (mts) atomicMax((unsigned long long*)F.commit_ts, (unsigned long long)mts);
+        }
+    }
+    const bool stands = !(flags & (FL_SLOW | FL_ERROR));
+    if (stands && !F.dry && bad == 0 && !s_run) {
+        if (w == 0)
+            for (u32 k0 = 0; k0 < ntiles; k0 += 64) fp_fold_idr(T, F, k0, ntiles);
+        const u64 row0 = T.base[BASE_ROWS];
+        for (u32 i = tid; i < n; i += FP_TAIL_THREADS)
+            if (F.fres[i] == TBGPU_CREATE_TRANSFER_OK) xidx_insert(T, fp_key(F, i), (u32)(row0 + i));
+    }
+    // fp_mask, scan3, fp_fix, fp_index (fixed): each thread takes a contiguous range,
+    // so its ranks are the workgroup's exclusive prefix plus a running count
+    if (stands && bad != 0) {
+        const u32 per = (n + FP_TAIL_THREADS - 1) / FP_TAIL_THREADS;
+        const u32 i0 = min(n, tid * per), i1 = min(n, i0 + per);
+        u32 v = 0;  // accepted | failed << 16 (n <= FP_TAIL_MAX < 65536)
+        for (u32 i = i0; i < i1; i++) v += F.fres[i] == TBGPU_CREATE_TRANSFER_OK ? 1u : 1u << 16;
+        u32 inc = v;
+        for (int off = 1; off < 64; off <<= 1) {
+            const u32 t = __shfl_up(inc, off);
+            if (lane >= (u32)off) inc += t;
+        }
+        if (lane == 63) s_wsum[w] = inc;
+        __syncthreads();
+        u32 ex = inc - v;
+        for (u32 k = 0; k < w; k++) ex += s_wsum[k];
+        u32 ra = ex & 0xFFFF, rf = ex >> 16;
+        for (u32 i = i0; i < i1; i++) {
+            if (F.fres[i] == TBGPU_CREATE_TRANSFER_OK) fp_fix_one(F, T, i, ra++, rf);
+            else fp_fix_one(F, T, i, ra, rf++);
+        }
+        if (!F.dry) {
+            if (w == 0)
+                for (u32 k0 = 0; k0 < ntiles; k0 += 64) fp_fold_idr(T, F, k0, ntiles);
+            for (u32 i = i0; i < i1; i++)
+                if (F.fres[i] == TBGPU_CREATE_TRANSFER_OK) xidx_insert(T, fp_key(F, i), F.rows[i]);
+        }
+    }
+    __syncthreads();
+    // fp_advance
+    if (tid == 0 && stands) {
+        T.base[BASE_REPLIES] += fp_cnt(F, CNT_BAD);
+        if (!F.dry) T.base[BASE_ROWS] += fp_cnt(F, CNT_OK);
+    }
 }
 
 // Exact inverse of fp_commit's effects, before the general path redoes the call:
@@ -951,6 +1076,11 @@ void fp_launch_fix(const Tables& T, const FastArgs& F, u8* mask, uint4* ranks, S
     scan3_exclusive(mask, ranks, F.n, sc, stream, F.counters + CNT_FIX);
     fp_fix<<<sg, 256, 0, stream>>>(F, T, ranks);
     if (!F.dry) fp_index<<<sg, 256, 0, stream>>>(T, F, true);
+    HIP_CHECK(hipGetLastError());
+}
+
+void fp_launch_tail(const Tables& T, const FastArgs& F, hipStream_t stream) {
+    fp_tail<<<1, FP_TAIL_THREADS, 0, stream>>>(T, F);
     HIP_CHECK(hipGetLastError());
 }
 

@@ -4,11 +4,12 @@
 # two-rank routed rehearsal (gloo collectives, both ranks on the one GPU), kernel
 # traces and PMC passes of configs 2 and 4
 set -o pipefail
-O=gpurun_out/r02c_final4; mkdir -p $O
+O=gpurun_out/r02c_final5; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/gpu_tests.txt 2>&1; rc=$?; echo "tests rc=$rc"; tail -1 $O/gpu_tests.txt
 [ $rc -eq 0 ] || exit 1
 timeout -k 10 300 python -u __graft_entry__.py smoke > $O/smoke.txt 2>&1; echo "smoke rc=$?"; tail -1 $O/smoke.txt
+timeout -k 10 200 python3 -u profiles/single_call.py 256 > $O/single_call.txt 2>&1; echo "single rc=$?"; tail -1 $O/single_call.txt
 timeout -k 10 900 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err; echo "bench rc=$? $(grep -o '"value": [0-9.]*' $O/bench.json | head -1) $(grep -o '"frac": [0-9.]*' $O/bench.json | head -1)"
 timeout -k 10 300 python3 -u bench.py --config 1 --no-queries > $O/bench_config1.json 2> $O/bench_config1.err; echo "c1 rc=$? $(grep -o '"value": [0-9.]*' $O/bench_config1.json | head -1)"
 timeout -k 10 300 python3 -u bench.py --config 3 --no-queries --verify > $O/bench_config3.json 2> $O/bench_config3.err; echo "c3 rc=$? $(grep -o '"value": [0-9.]*' $O/bench_config3.json | head -1)"

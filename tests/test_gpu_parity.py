@@ -497,3 +497,60 @@ def test_sorted_run_random_call_mix(seed):
         assert gpu.lookup_transfers(ids).tobytes() == orc.lookup_transfers(ids).tobytes()
     finally:
         gpu.close()
+
+
+@pytest.mark.parametrize("n", [1, 2, 511, 513, 8190, 16383, 16384, 16385])
+def test_small_call_tail_boundary(n):
+    """Calls on both sides of FP_TAIL_MAX (16384 events, fast.h): at most that many run
+    everything after fp_commit in one workgroup (fp_tail), more run the launch
+    sequence.  Each size goes through the kinds fp_tail has phases for: all accepted
+    with rising ids (the sorted run takes the rows), failures (fix ranks and replies),
+    linked chains with a failing member (fp_chains), shuffled ids (dupcheck, hash
+    index) and an id repeated within the call (the fallback to the general path)."""
+    from tigerbeetle_amd.types import TRANSFER_DTYPE, TransferFlags
+    rng = np.random.default_rng(n)
+    acc_n = 200
+    w = workload.config1(transfer_count=1, account_count=acc_n, seed=5)
+    ats, _ = w.timestamps()
+    orc = oracle.Oracle(acc_n, 1 << 20)
+    gpu = _engine()
+    next_id = 1
+    try:
+        for be in (orc, gpu):
+            be.create_accounts_batches(ats, w.account_counts, w.accounts)
+        ts = int(ats[-1])
+        for k, kind in enumerate(("fresh", "fail", "linked", "shuffle", "repeat", "fresh")):
+            ev = np.zeros(n, dtype=TRANSFER_DTYPE)
+            ev["id_lo"] = np.arange(next_id, next_id + n)
+            next_id += n + 1
+            d = rng.integers(1, acc_n + 1, n)
+            c = rng.integers(1, acc_n, n)
+            ev["debit_account_id_lo"], ev["credit_account_id_lo"] = d, np.where(c >= d, c + 1, c)
+            ev["amount_lo"] = rng.integers(1, 1000, n)
+            ev["ledger"], ev["code"] = 2, 1
+            if kind in ("fail", "linked"):
+                ev["code"][rng.random(n) < 0.03] = 0
+            if kind == "linked":
+                ev["flags"][0:n - 1:3] |= int(TransferFlags.linked)
+                ev["flags"][1:n - 1:3] |= int(TransferFlags.linked)
+            if kind == "shuffle":
+                rng.shuffle(ev)
+            if kind == "repeat" and n > 1:
+                ev["id_lo"][-1] = ev["id_lo"][0]
+            counts = np.full(n // 8190, 8190, dtype=np.uint32)
+            if n % 8190:
+                counts = np.append(counts, n % 8190).astype(np.uint32)
+            bts = ts + np.cumsum(counts.astype(np.uint64) + 1)
+            ts = int(bts[-1])
+            go, gr, _ = gpu.create_transfers_batches(bts, counts, ev)
+            oo, orr, _ = orc.create_transfers_batches(bts, counts, ev)
+            assert np.array_equal(gr, orr), kind
+            assert_results_equal(per_batch_results(go, counts, gr), per_batch_results(oo, counts, orr), f"{n} {kind}")
+            if k < 4 and kind != "linked":
+                assert gpu.stats().path == 1, kind  # the fast path stood (before any fallback)
+        assert_state_equal(gpu, orc)
+        assert gpu.commit_timestamp() == orc.commit_timestamp()
+        ids = list(range(1, next_id, max(1, n // 50))) + [next_id + 3]
+        assert gpu.lookup_transfers(ids).tobytes() == orc.lookup_transfers(ids).tobytes()
+    finally:
+        gpu.close()

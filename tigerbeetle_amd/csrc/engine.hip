@@ -189,8 +189,9 @@ struct tbgpu_ctx {
     u32* h_rc = nullptr;       // pinned per-batch reply counts of the current call
     // the end of a call in one copy (k_report): counter words, T.base, the last chunk's
     // reply counts
-    u32* report = nullptr;
     u32* h_report = nullptr;  // pinned
+    u32* h_report_dev = nullptr;  // its device address, and h_res's
+    u64* h_res_dev = nullptr;
     u64 h_rc_cap = 0;
     u64 rows_hi = 0;           // upper bound of T.base[BASE_ROWS] (n_rows + events enqueued since)
     // account-transfers index (query.hip), allocated by the first compaction
@@ -286,7 +287,6 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->rt_dry_ts = dalloc<u64>(1, &B);
     c->rt_stats = dalloc<u64>(8, &B);
     c->pc = c->counters + PC_OFF;
-    c->report = dalloc<u32>(RPT_COUNTS + c->bmax, &B);
     c->rg_part = dalloc<u64>(tr_range_part_words(n), &B);
 
     HIP_CHECK(hipHostMalloc((void**)&c->h_base, 8 * sizeof(u64), hipHostMallocDefault));  // [4..5]: a uint4
@@ -294,6 +294,8 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->h_pc = c->h_counters + PC_OFF;
     HIP_CHECK(hipHostMalloc((void**)&c->h_report, (RPT_COUNTS + c->bmax) * sizeof(u32), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc((void**)&c->h_res, c->nmax * 8 + 8, hipHostMallocDefault));
+    HIP_CHECK(hipHostGetDevicePointer((void**)&c->h_res_dev, c->h_res, 0));
+    HIP_CHECK(hipHostGetDevicePointer((void**)&c->h_report_dev, c->h_report, 0));
     HIP_CHECK(hipHostMalloc((void**)&c->h_counts, c->bmax * sizeof(u32), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc((void**)&c->h_stage_start, (batch_ts_offset(c->bmax) + 2 * c->bmax) * sizeof(u32),
                             hipHostMallocDefault));
@@ -454,13 +456,21 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
 // ------------------------------------------------------------ helpers -----
 
 // The end of a call: counter words, the device cursors and the last chunk's reply
-// counts gathered into one buffer, so that one copy brings them back (three small
-// copies were three blit dispatches).
-__global__ void k_report(const u32* counters, const u64* base, const u32* counts, u32 nb, u32* out) {
+// counts (and, for host-buffer calls, its replies) stored straight into pinned host
+// memory, so that no copy follows the call's last kernel (three small copies and the
+// replies' copy were four dispatches, each an engine hand-off of ~10 us).  Vector
+// stores over PCIe, made visible to the host before the launch completes.
+__global__ void k_report(const u32* counters, const u64* base, const u32* counts, u32 nb, u32* out,
+                         const u64* replies, u64* out_replies) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < RPT_BASE) out[i] = counters[i];
     else if (i < RPT_COUNTS) out[i] = ((const u32*)base)[i - RPT_BASE];
     else if (i < RPT_COUNTS + nb) out[i] = counts[i - RPT_COUNTS];
+    if (out_replies) {
+        const u64 total = base[BASE_REPLIES];
+        for (u64 j = i; j < total; j += (u64)gridDim.x * blockDim.x) out_replies[j] = replies[j];
+    }
+    __threadfence_system();
 }
 
 static void read_counters(tbgpu_ctx* c) {
@@ -995,13 +1005,10 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         if (b1 == nb_total) {
             // the call's end: counters, cursors and reply counts in one copy, with the
             // replies, and one wait
-            k_report<<<(RPT_COUNTS + nb + 255) / 256, 256, 0, c->stream>>>(c->counters, c->T.base, c->counts, nb,
-                                                                           c->report);
+            const u32 rb = std::max<u32>((RPT_COUNTS + nb + 255) / 256, dst_device ? 1u : std::min<u32>(n / 256, 1024));
+            k_report<<<rb, 256, 0, c->stream>>>(c->counters, c->T.base, c->counts, nb, c->h_report_dev,
+                                                (const u64*)c->res_buf, dst_device ? nullptr : c->h_res_dev);
             HIP_CHECK(hipGetLastError());
-            HIP_CHECK(hipMemcpyAsync(c->h_report, c->report, (RPT_COUNTS + nb) * sizeof(u32), hipMemcpyDeviceToHost,
-                                     c->stream));
-            if (!dst_device)
-                HIP_CHECK(hipMemcpyAsync(c->h_res, c->res_buf, (u64)n * 8, hipMemcpyDeviceToHost, c->stream));
             HIP_CHECK(hipEventRecord(c->ev1, c->stream));
             wait_event(c->ev1);
             memcpy(c->h_counters, c->h_report, CNT_COUNT * sizeof(u32));

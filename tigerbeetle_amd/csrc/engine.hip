@@ -952,7 +952,6 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
     c->stats.sorts = 0;
     bool ended = false;   // the last chunk brought the call's end back (k_report)
     u32 small_until = 0;  // batches before this one go in general-path-sized chunks
-    set_base(c, BASE_REPLIES, 0);  // the call's replies start at the front of `results`
     c->long_segments = false;
     for (u32 b0 = 0; b0 < nb_total;) {
         // After a call needed the fixed point, the next ones probably do too: small
@@ -962,15 +961,21 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         const u32 b1 = chunk_end(c, counts, b0, nb_total, small ? general_chunk_batches() : ~0u);
         const u32 nb = b1 - b0;
         prof_mark(c, PH_UPLOAD);
-        upload_batches(c, timestamps + b0, counts + b0, nb, starts);
-        const u32 n = starts[nb];
+        u32 n = 0;
+        for (u32 b = b0; b < b1; b++) n += counts[b];
         const Transfer* ev;
         if (src_device) {
             ev = ev_src + ev_off;
         } else {
+            // the events' copy (a DMA engine) first, then the small uploads and resets on
+            // the compute queue: one engine hand-off before the chunk's kernels, not two
             HIP_CHECK(hipMemcpyAsync(c->ev_buf, ev_src + ev_off, (u64)n * 128, hipMemcpyHostToDevice, c->stream));
             ev = (const Transfer*)c->ev_buf;
         }
+        upload_batches(c, timestamps + b0, counts + b0, nb, starts);
+        // the replies start at the front of `results` (device results: the call's first
+        // chunk; host results: every chunk, staged in res_buf)
+        if (ev_off == 0 || !dst_device) set_base(c, BASE_REPLIES, 0);
         c->rt_ev_ts = nullptr;
         c->rt_ctl = nullptr;
         if (routed_device) {  // already in HBM
@@ -989,7 +994,6 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         }
         // device results: the call's buffer (cursor-relative); host results: staged in
         // res_buf one chunk at a time
-        if (!dst_device && ev_off != 0) set_base(c, BASE_REPLIES, 0);  // (reset above for the first chunk)
         tbgpu_create_transfers_result_t* rdev = dst_device ? results : (tbgpu_create_transfers_result_t*)c->res_buf;
         const bool try_fast_path = c->slow_chunks % 8 == 0;
         // a call that is one chunk makes its fast attempt without the round trip that

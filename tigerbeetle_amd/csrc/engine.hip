@@ -140,6 +140,7 @@ struct tbgpu_ctx {
     u8* h_res = nullptr;        // pinned, nmax * 8: a chunk's replies for host-buffer calls
     u64* h_stage_ts = nullptr;  // pinned, bmax
     u32* h_stage_start = nullptr;  // pinned, bmax + 1
+    u32* h_stage_dev = nullptr;    // its device address (k_upload_block reads it)
     // fast path (fast.hip)
     u32* f_gtab = nullptr;
     u32* f_gpos = nullptr;
@@ -300,6 +301,7 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     HIP_CHECK(hipHostMalloc((void**)&c->h_stage_start, (batch_ts_offset(c->bmax) + 2 * c->bmax) * sizeof(u32),
                             hipHostMallocDefault));
     c->h_stage_ts = (u64*)(c->h_stage_start + batch_ts_offset(c->bmax));
+    HIP_CHECK(hipHostGetDevicePointer((void**)&c->h_stage_dev, c->h_stage_start, 0));
 }
 
 enum { PH_UPLOAD = 0, PH_CLASSIFY = 1, PH_SORT = 2, PH_SCAN = 3, PH_EVAL = 4, PH_APPLY = 5, PH_INDEX = 6, PH_PREP = 7, PH_END = -1 };
@@ -529,8 +531,17 @@ static u32 chunk_end(const tbgpu_ctx* c, const uint32_t* counts, u32 b0, u32 nb,
     return b;
 }
 
+// A chunk's batch block (starts, then timestamps) read by one kernel straight from
+// the pinned staging buffer, with the reply cursor's reset when asked: one dispatch
+// where a small copy (itself a blit dispatch) and a fill were two.
+__global__ void k_upload_block(const u32* host_block, u32 words, u32* block, u64* base, u32 reset_replies) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < words) block[i] = host_block[i];
+    if (i == 0 && reset_replies) base[BASE_REPLIES] = 0;
+}
+
 static void upload_batches(tbgpu_ctx* c, const uint64_t* timestamps, const uint32_t* counts, u32 nb,
-                           std::vector<u32>& starts) {
+                           std::vector<u32>& starts, bool reset_replies = false) {
     starts.resize(nb + 1);
     starts[0] = 0;
     for (u32 b = 0; b < nb; b++) starts[b + 1] = starts[b] + counts[b];
@@ -543,8 +554,10 @@ static void upload_batches(tbgpu_ctx* c, const uint64_t* timestamps, const uint3
     c->b_ts = (u64*)(c->b_start + off);
     memcpy(c->h_stage_ts, timestamps, nb * sizeof(u64));
     memcpy(c->h_stage_start, starts.data(), (nb + 1) * sizeof(u32));
-    HIP_CHECK(hipMemcpyAsync(c->b_start, c->h_stage_start, off * sizeof(u32) + nb * sizeof(u64), hipMemcpyHostToDevice,
-                             c->stream));
+    const u32 words = (u32)(off + 2 * nb);
+    k_upload_block<<<(words + 255) / 256, 256, 0, c->stream>>>(c->h_stage_dev, words, c->b_start, c->T.base,
+                                                               reset_replies ? 1u : 0u);
+    HIP_CHECK(hipGetLastError());
 }
 
 // Device replies are concatenated across the chunk's batches; the host C-ABI
@@ -972,10 +985,9 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
             HIP_CHECK(hipMemcpyAsync(c->ev_buf, ev_src + ev_off, (u64)n * 128, hipMemcpyHostToDevice, c->stream));
             ev = (const Transfer*)c->ev_buf;
         }
-        upload_batches(c, timestamps + b0, counts + b0, nb, starts);
         // the replies start at the front of `results` (device results: the call's first
         // chunk; host results: every chunk, staged in res_buf)
-        if (ev_off == 0 || !dst_device) set_base(c, BASE_REPLIES, 0);
+        upload_batches(c, timestamps + b0, counts + b0, nb, starts, ev_off == 0 || !dst_device);
         c->rt_ev_ts = nullptr;
         c->rt_ctl = nullptr;
         if (routed_device) {  // already in HBM

@@ -554,3 +554,55 @@ def test_small_call_tail_boundary(n):
         assert gpu.lookup_transfers(ids).tobytes() == orc.lookup_transfers(ids).tobytes()
     finally:
         gpu.close()
+
+
+def test_pinned_host_events_read_in_place():
+    """Small one-chunk calls whose events sit in page-locked host memory (here a pinned
+    torch buffer, at offsets inside it) are read by the kernels in place, without a
+    copy (engine.hip transfers_batches, zero copy): same results and state as the
+    oracle for accepted calls, calls with failures, chains, and a repeated id (the
+    fallback redoes the call from a copy)."""
+    import torch
+    from tigerbeetle_amd.types import TRANSFER_DTYPE, TransferFlags
+    rng = np.random.default_rng(77)
+    acc_n = 150
+    w = workload.config1(transfer_count=1, account_count=acc_n, seed=9)
+    ats, _ = w.timestamps()
+    orc = oracle.Oracle(acc_n, 1 << 20)
+    gpu = _engine()
+    n = 8190
+    kinds = ("fresh", "fail", "linked", "repeat", "fresh", "fresh")
+    pinned = torch.empty((len(kinds) + 1) * n * 128, dtype=torch.uint8, pin_memory=True)
+    view = pinned.numpy().view(TRANSFER_DTYPE)
+    next_id = 1
+    try:
+        for be in (orc, gpu):
+            be.create_accounts_batches(ats, w.account_counts, w.accounts)
+        ts = int(ats[-1])
+        for k, kind in enumerate(kinds):
+            m = n - 7 * k  # ragged sizes at offsets inside the pinned buffer
+            ev = view[k * n + 3:k * n + 3 + m]
+            ev[:] = np.zeros(m, dtype=TRANSFER_DTYPE)
+            ev["id_lo"] = np.arange(next_id, next_id + m)
+            next_id += m
+            d = rng.integers(1, acc_n + 1, m)
+            c = rng.integers(1, acc_n, m)
+            ev["debit_account_id_lo"], ev["credit_account_id_lo"] = d, np.where(c >= d, c + 1, c)
+            ev["amount_lo"] = rng.integers(1, 1000, m)
+            ev["ledger"], ev["code"] = 2, 1
+            if kind in ("fail", "linked"):
+                ev["code"][rng.random(m) < 0.02] = 0
+            if kind == "linked":
+                ev["flags"][0:m - 1:2] |= int(TransferFlags.linked)
+            if kind == "repeat":
+                ev["id_lo"][m // 2] = ev["id_lo"][1]
+            ts += m + 1
+            gr = gpu.create_transfers(ts, ev)
+            orr = orc.create_transfers(ts, np.array(ev))
+            assert gr.tobytes() == orr.tobytes(), (k, kind)
+        assert_state_equal(gpu, orc)
+        assert gpu.commit_timestamp() == orc.commit_timestamp()
+        ids = list(range(1, next_id, 97)) + [next_id + 1]
+        assert gpu.lookup_transfers(ids).tobytes() == orc.lookup_transfers(ids).tobytes()
+    finally:
+        gpu.close()

@@ -933,6 +933,23 @@ static bool run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
 }
 
 // TBGPU_NO_SPEC=1: every fast attempt waits for its own verdict (A/B timing)
+static bool zero_copy_disabled() {  // TBGPU_NO_ZERO_COPY=1: always copy (A/B timing)
+    static const bool d = getenv("TBGPU_NO_ZERO_COPY") != nullptr;
+    return d;
+}
+
+// The device address of page-locked host memory (hipHostMalloc, hipHostRegister, a
+// pinned torch tensor), or null for pageable memory.
+static const void* pinned_device_ptr(const void* p) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable: not an error of the call
+        return nullptr;
+    }
+    if (a.type != hipMemoryTypeHost || !a.devicePointer) return nullptr;
+    return a.devicePointer;
+}
+
 static bool spec_disabled() {
     static const bool d = getenv("TBGPU_NO_SPEC") != nullptr;
     return d;
@@ -977,8 +994,18 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         u32 n = 0;
         for (u32 b = b0; b < b1; b++) n += counts[b];
         const Transfer* ev;
+        // A small one-chunk call from pinned (or registered) host memory, on its fast
+        // attempt: the kernels read the events where they are, over PCIe (fp_commit
+        // reads each once): no copy and no DMA / compute hand-off.  A fallback redoes the
+        // call with a copy (slow_chunks).
+        const bool zc = !src_device && b0 == 0 && b1 == nb_total && n <= FP_TAIL_MAX && c->slow_chunks % 8 == 0 &&
+                        !c->rt_dry && !ev_ts_host && !ctl_host && !(c->opt.flags & TBGPU_OPT_FORCE_GENERAL) &&
+                        !spec_disabled() && !zero_copy_disabled();
+        const Transfer* ev_zc = zc ? (const Transfer*)pinned_device_ptr(ev_src + ev_off) : nullptr;
         if (src_device) {
             ev = ev_src + ev_off;
+        } else if (ev_zc) {
+            ev = ev_zc;
         } else {
             // the events' copy (a DMA engine) first, then the small uploads and resets on
             // the compute queue: one engine hand-off before the chunk's kernels, not two

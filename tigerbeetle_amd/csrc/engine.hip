@@ -141,6 +141,7 @@ struct tbgpu_ctx {
     u64* h_stage_ts = nullptr;  // pinned, bmax
     u32* h_stage_start = nullptr;  // pinned, bmax + 1
     u32* h_stage_dev = nullptr;    // its device address (k_upload_block reads it)
+    bool ev_in_host = false;       // this chunk's events are read in place from host memory
     // fast path (fast.hip)
     u32* f_gtab = nullptr;
     u32* f_gpos = nullptr;
@@ -644,7 +645,12 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_crea
     prof_mark(c, PH_PREP);
     fp_launch_prep(F, s);
     prof_mark(c, PH_CLASSIFY);
+    F.ev_copy = c->ev_in_host ? (Transfer*)c->ev_buf : nullptr;
     fp_launch_commit(c->T, F, s);
+    if (F.ev_copy) {  // the later launches read fp_commit's HBM copy of the events
+        F.ev = F.ev_copy;
+        F.ev_copy = nullptr;
+    }
     prof_mark(c, PH_INDEX);
     static const bool no_tail = getenv("TBGPU_NO_TAIL") != nullptr;  // A/B timing of the launch sequence
     if (n <= FP_TAIL_MAX && !no_tail) {
@@ -1006,6 +1012,7 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
             ev = ev_src + ev_off;
         } else if (ev_zc) {
             ev = ev_zc;
+            c->ev_in_host = true;
         } else {
             // the events' copy (a DMA engine) first, then the small uploads and resets on
             // the compute queue: one engine hand-off before the chunk's kernels, not two
@@ -1039,8 +1046,10 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         // decides whether it stands: that answer comes with the call's final wait
         const bool spec = try_fast_path && !c->rt_dry && b0 == 0 && b1 == nb_total &&
                           !(c->opt.flags & TBGPU_OPT_FORCE_GENERAL) && !spec_disabled();
-        if (!run_transfers_chunk(c, ev, n, nb, rdev, try_fast_path,
-                                 /*split=*/!c->rt_dry && nb > general_chunk_batches(), spec)) {
+        const bool stood = run_transfers_chunk(c, ev, n, nb, rdev, try_fast_path,
+                                               /*split=*/!c->rt_dry && nb > general_chunk_batches(), spec);
+        c->ev_in_host = false;
+        if (!stood) {
             small_until = b1;  // redo these batches in small chunks, on the general path
             c->slow_chunks = 1;
             continue;

@@ -26,6 +26,7 @@ struct FastArgs {
     u64* commit_ts;     // commit_timestamp sink (T.commit_ts, or a scratch word when dry)
     u32 dry;            // dry run: replies only, no state change
     u32 ablate;         // timing-only builds (TBGPU_ABLATE): skip parts of the work; results wrong
+    Transfer* ev_copy;  // ev is in host memory (zero copy): fp_commit leaves an HBM copy here, or null
 };
 constexpr u32 TILE_WORDS = 6;
 // calls of at most FP_TAIL_MAX events run fp_launch_tail (one workgroup) instead of

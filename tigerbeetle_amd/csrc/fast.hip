@@ -429,6 +429,8 @@ void fp_commit(Tables T, FastArgs F) {
             wave_lds_sync();
         }
     }
+    if (F.ev_copy && valid) F.ev_copy[i] = t;  // events read in place from host memory: an HBM
+                                               // copy for the launches after this one
 #endif
     // Linked-chain membership (execute, src/state_machine.zig:1018-1035): linked
     // here, or the batch's previous event is (the router may close a chain that

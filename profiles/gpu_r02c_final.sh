@@ -4,7 +4,7 @@
 # two-rank routed rehearsal (gloo collectives, both ranks on the one GPU), kernel
 # traces and PMC passes of configs 2 and 4
 set -o pipefail
-O=gpurun_out/r02c_final7; mkdir -p $O
+O=gpurun_out/r02c_final8; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/gpu_tests.txt 2>&1; rc=$?; echo "tests rc=$rc"; tail -1 $O/gpu_tests.txt
 [ $rc -eq 0 ] || exit 1

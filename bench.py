@@ -189,6 +189,72 @@ def host_path(eng, w, tts, counts, b0, nbs, torch):
                          "entry": "tbgpu_create_transfers_batches (host buffers, H2D inside the call)"}}
 
 
+ACCOUNT_BYTES = 272  # create_account reads 128 B, writes the 128-B row, probes 16 B
+
+
+def create_accounts_device(eng, torch, dev, ats, account_counts, accounts, rank=0):
+    """create_accounts with the account events resident in HBM (the metric's own
+    convention): every account batch in one streamed call, timed with HIP events
+    around the call on the engine's stream (engine stats).  Returns the
+    `create_accounts` object of the bench line (accounts/s and the roofline at §8d's
+    272 B per account, the whole call as the unit: no kernel dominates it)."""
+    n = int(np.sum(account_counts))
+    evd = torch.from_numpy(np.ascontiguousarray(accounts).view(np.uint8)).to(dev)
+    res = torch.empty(max(n, 1) * 8, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    eng.set_profiling(True)
+    t0 = time.perf_counter()
+    tot, _ = eng.create_accounts_batches_device(ats, account_counts, evd.data_ptr(), res.data_ptr())
+    wall = time.perf_counter() - t0
+    st = eng.stats()
+    eng.set_profiling(False)
+    if int(tot) != 0:
+        raise RuntimeError(f"[rank {rank}] account creation failed ({int(tot)} non-ok)")
+    del evd, res
+    return accounts_line(n, len(account_counts), st.device_ms, wall)
+
+
+def accounts_line(n, nb, device_ms, wall_s):
+    gbps = n * ACCOUNT_BYTES / (device_ms * 1e-3) / 1e9 if device_ms > 0 else 0.0
+    return {"accounts": n, "batches": nb, "device_ms": round(device_ms, 4), "wall_ms": round(wall_s * 1e3, 3),
+            "accounts_per_s": round(n / (device_ms * 1e-3), 1) if device_ms > 0 else None,
+            "roofline": {"bound": "hbm", "achieved": round(gbps, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(gbps / HBM_PEAK_GBPS, 5),
+                         "basis": f"{ACCOUNT_BYTES} B/account x {n} accounts / the call's device time (HIP events "
+                                  "on the engine stream; events resident in HBM)"}}
+
+
+def cpu_baseline_leg(args, acc_n, acc_cap, ats, account_counts, accounts, tts, counts, transfers):
+    """The CPU baseline (`cpu_baseline`, kind "port"): the oracle's commit loop over the
+    leading batches of the same stream, about `--cpu-seconds` of work, on one pinned
+    host core -- TigerBeetle commits on one core (docs/deploy/hardware.md:98).  Test
+    infrastructure as the measured baseline beside the GPU, never the product path."""
+    import oracle
+    allowed = sorted(os.sched_getaffinity(0))
+    core = allowed[min(2, len(allowed) - 1)]  # BASELINE.md: the third core the process may use
+    os.sched_setaffinity(0, {core})
+    try:
+        orc = oracle.Oracle(acc_cap, 4 << 20)
+        orc.create_accounts_batches(ats, account_counts, accounts)
+        done, spent, b = 0, 0.0, 0
+        nb_host = len(counts)
+        offs = np.concatenate([[0], np.cumsum(np.asarray(counts, np.int64))])
+        while spent < args.cpu_seconds and b < nb_host:
+            k = min(16, nb_host - b)
+            o0, o1 = int(offs[b]), int(offs[b + k])
+            _, _, el = orc.create_transfers_batches(tts[b:b + k], counts[b:b + k], transfers[o0:o1])
+            done += o1 - o0
+            spent += el
+            b += k
+        orc.close()
+    finally:
+        os.sched_setaffinity(0, set(allowed))
+    return {"value": round(done / spent, 1), "unit": "transfers/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/oracle.c commit loop (single thread pinned to host core {core}), first {b} "
+                      f"batches ({done} transfers) of the same config-{args.config} stream after creating "
+                      f"the {acc_n} accounts; {spent:.1f}s of CPU work on {cpu_model()}"}
+
+
 def routed_bench(args, rank, world, local_rank, torch, dist, backend="nccl"):
     """N > 1, BASELINE config 4 through the ledger-sharded router (SURVEY.md §8e,
     tigerbeetle_amd/shard.py): every rank receives its own client batches (1000
@@ -220,14 +286,16 @@ def routed_bench(args, rank, world, local_rank, torch, dist, backend="nccl"):
                  history_max=1024, events_per_call_max=int(per_step * 1.25) + BATCH_MAX,
                  dense_block_span=acc_n // 1000)
     ats, _ = w.timestamps()
-    _, rc = eng.create_accounts_batches(ats, w.account_counts, w.accounts)
-    assert int(rc.sum()) == 0, "account creation failed"
+    acc_line = create_accounts_device(eng, torch, torch.device("cuda", local_rank), ats, w.account_counts,
+                                      w.accounts, rank)
     cdev = dev if backend == "nccl" else torch.device("cpu")  # where the router's tensors live
     ssm = ShardedStateMachine(eng, Comm(rank, world, device=cdev))
     ssm.adopt_accounts(w.accounts, int(ats[-1]))
     ev_dev = torch.from_numpy(w.transfers.view(np.uint8)).to(cdev)
     counts = w.transfer_counts
-    del w
+    keep_host = rank == 0 and world == 1 and not args.no_cpu  # the CPU baseline leg reads the stream
+    if not keep_host:
+        del w
     torch.cuda.synchronize()
 
     def step_args(k):
@@ -241,24 +309,29 @@ def routed_bench(args, rank, world, local_rank, torch, dist, backend="nccl"):
     non_ok = 0
     # the timed steps; pipelined (the default on N > 1), step k + 1's all-to-all (xGMI)
     # runs while step k's owner commit (HBM) runs (shard.py create_transfers_device_stream)
+    eng.set_profiling(True)
+    commit_ms = []  # per step: the owner commit's fp_commit launch (HIP events on the engine stream)
     t0 = time.perf_counter()
     if args.pipelined:
         for reps in ssm.create_transfers_device_stream(step_args(k) for k in range(W, W + K)):
             non_ok += sum(len(r) for r in reps)
+            commit_ms.append(eng.stats().phase_ms[1])
     else:
         for k in range(W, W + K):
             non_ok += sum(len(r) for r in ssm.create_transfers_device(*step_args(k)))
+            commit_ms.append(eng.stats().phase_ms[1])
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0
+    eng.set_profiling(False)
     # one more step, unpipelined and synchronized per phase: where a step's time goes
     for key in ssm.timing:
         ssm.timing[key] = 0.0
     ssm.timed = True
     ssm.create_transfers_device(*step_args(W + K))
     ssm.timed = False
-    t = torch.tensor([elapsed, non_ok] + [ssm.timing[x] for x in sorted(ssm.timing)], dtype=torch.float64,
-                     device=cdev)
+    t = torch.tensor([elapsed, non_ok] + [ssm.timing[x] for x in sorted(ssm.timing)] + [float(np.mean(commit_ms))],
+                     dtype=torch.float64, device=cdev)
     tmax = t.clone()
     dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     tsum = t.clone()
@@ -268,7 +341,13 @@ def routed_bench(args, rank, world, local_rank, torch, dist, backend="nccl"):
     total = per_step * K * world
     value = total / elapsed
     phases = {x: round(float(tmax[2 + i]), 3) for i, x in enumerate(sorted(ssm.timing))}
+    fp_ms = float(tmax[-1])  # the slowest rank's mean fp_commit launch
+    cpu = None
+    if keep_host:
+        ats_c, tts_c = w.timestamps()
+        cpu = cpu_baseline_leg(args, acc_n, acc_n, ats_c, w.account_counts, w.accounts, tts_c, counts, w.transfers)
     if rank == 0:
+        fp_gbps = per_step * COMMIT_BYTES_PER_TRANSFER / (fp_ms * 1e-3) / 1e9 if fp_ms > 0 else 0.0
         e2e = value / world * ALGO_BYTES_PER_TRANSFER / 1e9
         a2a_bytes = per_step * ssm.wire_bytes_per_event * (world - 1) / world  # leaving each rank per step
         line = {
@@ -302,12 +381,18 @@ def routed_bench(args, rank, world, local_rank, torch, dist, backend="nccl"):
                        "cross_shard_prerun_steps": ssm.stats["preruns"] - st0["preruns"],
                        "dry_rounds": ssm.stats["dry_rounds"] - st0["dry_rounds"],
                        "fallbacks": ssm.stats["device_fallbacks"] - st0["device_fallbacks"]},
-            "roofline": {"bound": "hbm", "achieved": round(e2e, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(e2e / HBM_PEAK_GBPS, 5), "traffic": None,
-                         "kernel": "whole routed step per GPU",
-                         "basis": f"{ALGO_BYTES_PER_TRANSFER} B/transfer x per-GPU committed transfers/s "
-                                  "(partition, all-to-all, commit and replies inside the time)"},
-            "cpu_baseline": None,
+            "roofline": {"bound": "hbm", "achieved": round(fp_gbps, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(fp_gbps / HBM_PEAK_GBPS, 5), "traffic": None,
+                         "kernel": "fp_commit (the owner commit)",
+                         "basis": f"{COMMIT_BYTES_PER_TRANSFER} B/transfer x {per_step} transfers per launch / "
+                                  f"fp_commit launch time ({fp_ms:.4f} ms, HIP events on the engine stream, "
+                                  f"mean over steps, max over ranks)",
+                         "end_to_end": {"achieved": round(e2e, 2), "frac": round(e2e / HBM_PEAK_GBPS, 5),
+                                        "basis": f"{ALGO_BYTES_PER_TRANSFER} B/transfer x per-GPU committed "
+                                                 "transfers/s (partition, all-to-all, commit and replies inside "
+                                                 "the time)"}},
+            "cpu_baseline": cpu,
+            "create_accounts": acc_line,
         }
         emit(line)
     eng.close()
@@ -351,9 +436,35 @@ def verify_stream(eng, w, ats, tts, counts, B, steps, replies, acc_n):
         orc.close()
 
 
+def spawn_ranks(n: int) -> None:
+    """`--gpus N` without a launcher: start N rank processes (one per GPU, RCCL over
+    127.0.0.1) before this process touches the GPU, pass rank 0's result line through
+    and exit with the first failing rank's code.  (Children, never exec: this process
+    has not initialised the GPU, but a child keeps the rule simple.)"""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    for p in procs:
+        c = p.wait()
+        rc = rc or c
+    sys.exit(rc)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one per GPU (default: WORLD_SIZE, else 1).  Without a launcher, N > 1 starts "
+                         "the N rank processes itself; under a launcher it must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=None, help="default 3 (config 5: 14, ~the whole shard)")
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=None, choices=(1, 2, 3, 4, 5),
@@ -382,6 +493,18 @@ def main():
                     help="after the timed region, replay the same stream through the CPU oracle and compare "
                          "every reply and the final state bit for bit (configs 1-4)")
     args = ap.parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus is None:
+        args.gpus = int(env_world or 1)
+    if env_world is None and args.gpus > 1:
+        spawn_ranks(args.gpus)  # does not return
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}: launch one rank per GPU", file=sys.stderr)
+        sys.exit(2)
+    # Under a launcher (torchrun, or spawn_ranks) every N, N = 1 included, times the
+    # same workload: BASELINE config 4 through the ledger router.  A plain one-process
+    # run times BASELINE config 2 (configs[1], the metric's own configuration).
+    launched = env_world is not None
     _claim_stdout()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -399,6 +522,8 @@ def main():
 
     torch.cuda.set_device(local_rank)
     backend = os.environ.get("TB_DIST_BACKEND", "nccl")  # gloo: a CPU-collective rehearsal on one GPU
+    if launched and world == 1:
+        args.routed = True  # the scaling family's N = 1 point
     if world == 1 and args.routed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29517")
@@ -460,12 +585,22 @@ def main():
         buf = torch.empty(1221 * BATCH_MAX * 128, dtype=torch.uint8, device=dev)
         res = torch.empty(1221 * BATCH_MAX * 8, dtype=torch.uint8, device=dev)
         first = 1
+        acc_ms, acc_wall = 0.0, 0.0
+        eng.set_profiling(True)
         for b0 in range(0, len(ab), 1221):
             cnt = ab[b0:b0 + 1221]
             generate_accounts(local_rank, first, int(cnt.sum()), c5.accounts_per_ledger, buf.data_ptr())
+            torch.cuda.synchronize()
+            ta = time.perf_counter()
             tot, _ = eng.create_accounts_batches_device(ats[b0:b0 + len(cnt)], cnt, buf.data_ptr(), res.data_ptr())
-            assert tot == 0, "account creation failed"
+            acc_wall += time.perf_counter() - ta
+            acc_ms += eng.stats().device_ms
+            if int(tot) != 0:
+                raise RuntimeError("account creation failed")
             first += int(cnt.sum())
+        eng.set_profiling(False)
+        # the 100M accounts as 10M-account calls (1221 batches of 8190 each)
+        acc_line = accounts_line(acc_n, len(ab), acc_ms, acc_wall)
         del buf, res
         ev_dev = torch.empty(int(counts.sum()) * 128, dtype=torch.uint8, device=dev)
         generate_transfers(local_rank, c5.first_transfer_id, int(counts.sum()), c5.seed, c5.ledger0, c5.ledgers,
@@ -479,8 +614,7 @@ def main():
                      # config 4 numbers its accounts ledger << 32 | k: the blocked directory
                      dense_block_span=acc_n // 1000 if args.config == 4 else 0)
         ats, tts = w.timestamps()
-        _, rc = eng.create_accounts_batches(ats, w.account_counts, w.accounts)
-        assert int(rc.sum()) == 0, "account creation failed"
+        acc_line = create_accounts_device(eng, torch, dev, ats, w.account_counts, w.accounts, rank)
         ev_dev = torch.from_numpy(w.transfers.view(np.uint8)).to(dev)
         counts = w.transfer_counts
     res_dev = torch.empty(B * BATCH_MAX * 8, dtype=torch.uint8, device=dev)
@@ -498,6 +632,14 @@ def main():
             replies.append((np.array(rcs, dtype=np.uint32).copy(), res_dev[:int(total) * 8].cpu().numpy().copy()))
         return int(total)
 
+    prewarm = float(os.environ.get("TB_BENCH_PREWARM_S", "0"))  # diagnostics only: untimed device load first
+    if prewarm > 0:
+        a = torch.empty(1 << 28, dtype=torch.int32, device=dev)
+        t_pw = time.time()
+        while time.time() - t_pw < prewarm:
+            a.add_(1)
+        torch.cuda.synchronize()
+        del a
     for k in range(W):
         step(k)
     torch.cuda.synchronize()
@@ -509,11 +651,13 @@ def main():
     iters = []
     sorts = []
     paths = []
+    step_commit_ms = []  # per step: the dominant launch's HIP-event time (fp_commit on the fast path)
     non_ok = 0
     t0 = time.perf_counter()
     for k in range(W, W + K):
         non_ok += step(k)
         st = eng.stats()
+        step_commit_ms.append(st.phase_ms[1])
         phase += np.array(st.phase_ms[:8])
         dev_ms += st.device_ms
         iters.append(st.iterations)
@@ -589,6 +733,10 @@ def main():
         "end_to_end": {"achieved": round(e2e_gbps, 2), "frac": round(e2e_gbps / HBM_PEAK_GBPS, 5),
                        "basis": f"{ALGO_BYTES_PER_TRANSFER} B/transfer x per-GPU committed transfers/s"},
         "dominant_phase": names[dom],
+        "dominant_ms_per_step": {"min": round(min(step_commit_ms), 4),
+                                 "median": round(float(np.median(step_commit_ms)), 4),
+                                 "max": round(max(step_commit_ms), 4),
+                                 "first": round(step_commit_ms[0], 4), "last": round(step_commit_ms[-1], 4)},
         "phase_ms_per_step": phase_ms_per_step,
         "device_ms_per_step": round(dev_ms / K, 4),
     }
@@ -608,16 +756,8 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        import oracle  # the CPU baseline leg (test infrastructure, never the product path)
-        # TigerBeetle commits on one core (docs/deploy/hardware.md:98): pin the oracle
-        # to one host core (the third core the process may use)
-        allowed = sorted(os.sched_getaffinity(0))
-        core = allowed[min(2, len(allowed) - 1)]
-        os.sched_setaffinity(0, {core})
         if w is not None:
-            orc = oracle.Oracle(acc_n, 4 << 20)
-            orc.create_accounts_batches(ats, w.account_counts, w.accounts)
-            host_events = w.transfers
+            cpu = cpu_baseline_leg(args, acc_n, acc_n, ats, w.account_counts, w.accounts, tts, counts, w.transfers)
         else:
             # config 5: the leading 1024 batches, with the accounts they touch (the sample
             # need not create all 100M): their results do not depend on the others
@@ -629,23 +769,8 @@ def main():
             acc["id_lo"] = ids
             acc["ledger"] = ((ids - 1) // c5.accounts_per_ledger + 1).astype(np.uint32)
             acc["code"] = 1
-            orc = oracle.Oracle(len(ids), nh)
-            orc.create_accounts_batches(np.array([ats[-1]], np.uint64), np.array([len(acc)], np.uint32), acc)
-        done, spent, b = 0, 0.0, 0
-        nb_host = len(counts) if w is not None else 1024
-        while spent < args.cpu_seconds and b < nb_host:
-            k = min(16, nb_host - b)
-            off = int(counts[:b].sum())
-            n = int(counts[b:b + k].sum())
-            _, _, el = orc.create_transfers_batches(tts[b:b + k], counts[b:b + k], host_events[off:off + n])
-            done += n
-            spent += el
-            b += k
-        os.sched_setaffinity(0, set(allowed))
-        cpu = {"value": round(done / spent, 1), "unit": "transfers/s", "cores": 1, "kind": "port",
-               "sample": f"oracle/oracle.c commit loop (single thread pinned to host core {core}), first {b} "
-                         f"batches ({done} transfers) of the same config-{args.config} stream after creating "
-                         f"the {acc_n} accounts; {spent:.1f}s of CPU work on {cpu_model()}"}
+            cpu = cpu_baseline_leg(args, acc_n, len(ids), np.array([ats[-1]], np.uint64),
+                                   np.array([len(acc)], np.uint32), acc, tts, counts[:1024], host_events)
 
     if rank == 0:
         line = {
@@ -677,6 +802,7 @@ def main():
             "fixed_point_sorts": max(sorts) if sorts else 0,
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "create_accounts": acc_line,
             "host_path": host,
             "queries": queries,
             "verify": verify,

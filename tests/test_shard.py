@@ -193,3 +193,11 @@ def test_device_step_pipelined(kind):
     """create_transfers_device_stream: the next step routed while this one commits on a
     worker thread; the same results as the single state machine."""
     _check((kind, 101, 2, 3, 2), 2, device_step="stream")
+
+
+def test_device_step_pipelined_fallback_keeps_router_state():
+    """The pipelined stream with max_rounds = 1: steps whose spanning chains do not
+    settle fall back to the exact router; the next step is routed only after that
+    decision, so its timestamps and id filter follow the fallen-back step."""
+    stats = _check(("c4l", 57, 2, 4, 2), 2, device_step="stream", max_rounds=1)
+    assert stats["device_fallbacks"] > 0

@@ -35,9 +35,7 @@ __device__ __forceinline__ u32 ac_gtab_insert(const AcArgs& C, u128 key, u32 i) 
     }
 }
 
-__global__ void ac_classify(Tables T, AcArgs C) {
-    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= C.n) return;
+__device__ __forceinline__ u32 ac_classify_one(const Tables& T, const AcArgs& C, u32 i) {
     const u32 b = ac_batch_of(C.b_start, C.nb, i);
     const u32 bs = C.b_start[b], be = C.b_start[b + 1];
     const u32 nbatch = be - bs, k = i - bs;
@@ -76,7 +74,15 @@ __global__ void ac_classify(Tables T, AcArgs C) {
     C.pre[i] = pre;
     C.gslot[i] = gslot;
     C.prev_id[i] = NONE32;
-    if (fl) atomicOr(&C.counters[CNT_FLAGS], fl);
+    return fl;
+}
+
+__global__ void ac_classify(Tables T, AcArgs C) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    u32 fl = 0;
+    if (i < C.n) fl = ac_classify_one(T, C, i);
+    fl = wave_or_u32(fl);  // one flag atomic per wave, not per chain member
+    if (fl && wave_leader()) atomicOr(&C.counters[CNT_FLAGS], fl);
 }
 
 __global__ void ac_group1(AcArgs C) {
@@ -153,12 +159,11 @@ __global__ void ac_evaluate(Tables T, AcArgs C, const u8* res_s, const u8* ok_s,
     res_d[i] = r;
     ok_d[i] = r == 0 ? 1 : 0;
     if (r != 0 && csi != C.ce[i]) atomicMin(&cfail_d[csi], i);
-    if (r != res_s[i]) atomicAdd(&C.counters[CNT_CHANGES], 1u);
+    if (r != res_s[i]) atomicAdd(&C.counters[CNT_CHANGES], 1u);  // few: only events whose result moved
 }
 
-__global__ void ac_mask(AcArgs C, const u8* res, const u8* ok, const u32* cfail, u8* fres, u8* mask, u64* commit_ts) {
-    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= C.n) return;
+__device__ __forceinline__ u64 ac_mask_one(const AcArgs& C, const u8* res, const u8* ok, const u32* cfail, u8* fres,
+                                           u8* mask, u32 i) {
     const u32 cs = C.cs[i];
     const u32 cf = cs != C.ce[i] ? cfail[cs] : NONE32;
     u8 r;
@@ -169,8 +174,17 @@ __global__ void ac_mask(AcArgs C, const u8* res, const u8* ok, const u32* cfail,
     else r = TBGPU_CREATE_ACCOUNT_OK;
     fres[i] = r;
     mask[i] = ((ok[i] & 2) ? 1 : 0) | (r != 0 ? 2 : 0);
-    if ((ok[i] & 1) && (cf == NONE32 || i < cf))  // commit_timestamp survives rollback (:1223)
-        atomicMax((unsigned long long*)commit_ts, (unsigned long long)C.ts[i]);
+    // commit_timestamp survives rollback (:1223)
+    return ((ok[i] & 1) && (cf == NONE32 || i < cf)) ? C.ts[i] : 0;
+}
+
+// One atomicMax per wave on the single commit_timestamp word (one per accepted event
+// serialized at the memory side: 897 us for 10M accounts, SQ_WAIT_ANY 0.96 of the waves).
+__global__ void ac_mask(AcArgs C, const u8* res, const u8* ok, const u32* cfail, u8* fres, u8* mask, u64* commit_ts) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    u64 ts = i < C.n ? ac_mask_one(C, res, ok, cfail, fres, mask, i) : 0;
+    ts = wave_max_u64(ts);
+    if (ts && wave_leader()) atomicMax((unsigned long long*)commit_ts, (unsigned long long)ts);
 }
 
 __global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const uint4* rk, u64 row_base,
@@ -244,16 +258,28 @@ __global__ void k_get_posted(Tables T, u128 id, int* status) {
 
 // Foreign rows (tbgpu_import_transfers): stored rows + id index + key range, no
 // balance or posted effects.
-__global__ void import_transfers(Tables T, const Transfer* rows, u32 n, u64 row_base) {
+// The key range is folded per wave: four same-address atomics per row serialized at
+// the memory side (125M rows per GPU at config 5's tbgpu_open).
+__global__ void import_transfers(Tables T, const Transfer* rows, u32 n, u64 row_base, u32 in_place) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const Transfer t = rows[i];
-    T.xrows[row_base + i] = t;
-    xidx_insert(T, t.id, (u32)(row_base + i));
-    atomicMax((unsigned long long*)&T.idr[0], (unsigned long long)(u64)t.id);
-    atomicMax((unsigned long long*)&T.idr[1], (unsigned long long)(u64)(t.id >> 64));
-    atomicMin((unsigned long long*)&T.idr[2], (unsigned long long)(u64)t.id);
-    atomicMin((unsigned long long*)&T.idr[3], (unsigned long long)(u64)(t.id >> 64));
+    u64 mxl = 0, mxh = 0, mnl = ~0ull, mnh = ~0ull;
+    if (i < n) {
+        const Transfer t = rows[i];
+        if (!in_place) T.xrows[row_base + i] = t;
+        xidx_insert(T, t.id, (u32)(row_base + i));
+        mxl = mnl = (u64)t.id;
+        mxh = mnh = (u64)(t.id >> 64);
+    }
+    mxl = wave_max_u64(mxl);
+    mxh = wave_max_u64(mxh);
+    mnl = wave_min_u64(mnl);
+    mnh = wave_min_u64(mnh);
+    if (wave_leader() && mnl <= mxl) {
+        atomicMax((unsigned long long*)&T.idr[0], (unsigned long long)mxl);
+        atomicMax((unsigned long long*)&T.idr[1], (unsigned long long)mxh);
+        atomicMin((unsigned long long*)&T.idr[2], (unsigned long long)mnl);
+        atomicMin((unsigned long long*)&T.idr[3], (unsigned long long)mnh);
+    }
 }
 
 // tbgpu_open: the account index from the dense rows (ac_apply's insert).
@@ -336,6 +362,6 @@ void launch_get_posted(const Tables& T, u128 id, int* status, hipStream_t stream
 }
 
 void launch_import_transfers(const Tables& T, const Transfer* rows, u32 n, u64 row_base, hipStream_t stream) {
-    import_transfers<<<(n + 255) / 256, 256, 0, stream>>>(T, rows, n, row_base);
+    import_transfers<<<(n + 255) / 256, 256, 0, stream>>>(T, rows, n, row_base, rows == T.xrows + row_base ? 1u : 0u);
     HIP_CHECK(hipGetLastError());
 }

@@ -89,6 +89,27 @@ __host__ __device__ __forceinline__ u64 hash128(u64 lo, u64 hi) { return mix64(l
 __device__ __forceinline__ bool sum_overflows128(u128 a, u128 b) { return a + b < a; }
 __device__ __forceinline__ bool sum_overflows64(u64 a, u64 b) { return (u64)(a + b) < a; }
 
+// Wave-level reductions (64 lanes, every lane active in the call): same-address
+// device atomics serialize at the memory side (~5-10 ns each), so a kernel reduces
+// over its wave first and lane 0 issues the one atomic.
+__device__ __forceinline__ u64 wave_max_u64(u64 v) {
+    for (int off = 32; off > 0; off >>= 1) v = max(v, (u64)__shfl_xor((unsigned long long)v, off));
+    return v;
+}
+__device__ __forceinline__ u64 wave_min_u64(u64 v) {
+    for (int off = 32; off > 0; off >>= 1) v = min(v, (u64)__shfl_xor((unsigned long long)v, off));
+    return v;
+}
+__device__ __forceinline__ u32 wave_or_u32(u32 v) {
+    for (int off = 32; off > 0; off >>= 1) v |= (u32)__shfl_xor(v, off);
+    return v;
+}
+__device__ __forceinline__ u32 wave_sum_u32(u32 v) {
+    for (int off = 32; off > 0; off >>= 1) v += (u32)__shfl_xor(v, off);
+    return v;
+}
+__device__ __forceinline__ bool wave_leader() { return (threadIdx.x & 63) == 0; }
+
 #define HIP_CHECK(expr)                                                                   \
     do {                                                                                  \
         hipError_t _e = (expr);                                                           \

@@ -637,11 +637,6 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_crea
     F.fres2 = c->mask;
     F.dry = c->rt_dry ? 1u : 0u;
     F.commit_ts = c->rt_dry ? c->rt_dry_ts : c->T.commit_ts;
-    static const u32 ablate = [] {  // timing-only ablation (profiles/ablate.py); never set in production
-        const char* e = getenv("TBGPU_ABLATE");
-        return e ? (u32)strtoul(e, nullptr, 0) : 0u;
-    }();
-    F.ablate = ablate;
     prof_mark(c, PH_PREP);
     fp_launch_prep(F, s);
     prof_mark(c, PH_CLASSIFY);
@@ -944,15 +939,32 @@ static bool zero_copy_disabled() {  // TBGPU_NO_ZERO_COPY=1: always copy (A/B ti
     return d;
 }
 
-// The device address of page-locked host memory (hipHostMalloc, hipHostRegister, a
-// pinned torch tensor), or null for pageable memory.
-static const void* pinned_device_ptr(const void* p) {
-    hipPointerAttribute_t a{};
+// The device address of `bytes` of page-locked host memory at `p` (hipHostMalloc,
+// hipHostRegister, a pinned torch tensor), or null for pageable memory.  The last
+// byte must map into the same allocation, at the same offset: a buffer that runs past
+// one pinned allocation (a region registered only in part, two adjacent registered
+// regions) takes the copy path.
+static const void* pinned_device_ptr(const void* p, u64 bytes) {
+    hipPointerAttribute_t a{}, z{};
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();  // pageable: not an error of the call
         return nullptr;
     }
-    if (a.type != hipMemoryTypeHost || !a.devicePointer) return nullptr;
+    if (a.type != hipMemoryTypeHost || !a.devicePointer || bytes == 0) return nullptr;
+    const u8* last = (const u8*)p + bytes - 1;
+    if (hipPointerGetAttributes(&z, last) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (z.type != hipMemoryTypeHost || z.devicePointer != (const u8*)a.devicePointer + (bytes - 1)) return nullptr;
+    void* base = nullptr;
+    size_t size = 0;
+    if (hipPointerGetAttribute(&base, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p) == hipSuccess &&
+        hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) == hipSuccess && base) {
+        if (last >= (const u8*)base + size) return nullptr;  // past the allocation that holds p
+    } else {
+        (void)hipGetLastError();  // the range is not reported: the last byte's mapping decided
+    }
     return a.devicePointer;
 }
 
@@ -1007,7 +1019,7 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         const bool zc = !src_device && b0 == 0 && b1 == nb_total && n <= FP_TAIL_MAX && c->slow_chunks % 8 == 0 &&
                         !c->rt_dry && !ev_ts_host && !ctl_host && !(c->opt.flags & TBGPU_OPT_FORCE_GENERAL) &&
                         !spec_disabled() && !zero_copy_disabled();
-        const Transfer* ev_zc = zc ? (const Transfer*)pinned_device_ptr(ev_src + ev_off) : nullptr;
+        const Transfer* ev_zc = zc ? (const Transfer*)pinned_device_ptr(ev_src + ev_off, (u64)n * 128) : nullptr;
         if (src_device) {
             ev = ev_src + ev_off;
         } else if (ev_zc) {
@@ -1404,7 +1416,16 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
     HIP_CHECK(hipMemsetAsync(A->cfail, 0xFF, n * sizeof(u32), s));
     ac_launch_init(C, A->res, A->ok, A->cfail, s);
     u32 it = 0;
-    for (;; it++) {
+    // Without chains and repeated ids no event sees another (create_account depends on
+    // earlier events only through the id and the chain, :1198-1237): one evaluation
+    // against the committed accounts is the sequential result, no convergence check.
+    const bool independent = !(c->h_counters[CNT_FLAGS] & (FL_CHAINS | FL_MULTI_ID));
+    if (independent) {
+        HIP_CHECK(hipMemsetAsync(Bst->cfail, 0xFF, n * sizeof(u32), s));
+        ac_launch_evaluate(c->T, C, A->res, A->ok, Bst->res, Bst->ok, Bst->cfail, s);
+        std::swap(A, Bst);
+    }
+    for (; !independent; it++) {
         if (it > n + 2) tbgpu_fatal("create_accounts", "fixed point did not converge", __FILE__, __LINE__);
         HIP_CHECK(hipMemsetAsync(c->counters + CNT_CHANGES, 0, sizeof(u32), s));
         HIP_CHECK(hipMemsetAsync(Bst->cfail, 0xFF, n * sizeof(u32), s));
@@ -1430,6 +1451,7 @@ static uint64_t accounts_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t
                                  const Account* events, bool device, tbgpu_create_accounts_result_t* results,
                                  uint32_t* result_counts) {
     HIP_CHECK(hipSetDevice(c->device));
+    HIP_CHECK(hipEventRecord(c->ev0, c->stream));
     std::vector<u32> starts;
     u64 total = 0, ev_off = 0;
     for (u32 b0 = 0; b0 < nb_total;) {
@@ -1460,7 +1482,12 @@ static uint64_t accounts_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t
         ev_off += n;
         b0 = b1;
     }
-    wait_stream(c->stream);
+    HIP_CHECK(hipEventRecord(c->ev1, c->stream));
+    wait_event(c->ev1);
+    float ms = 0;
+    HIP_CHECK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    c->stats.events = ev_off;
+    c->stats.device_ms = ms;  // the call's device time (host round trips between chunks included)
     return total;
 }
 

@@ -25,7 +25,6 @@ struct FastArgs {
     u8* fres2;          // chain members' final results (fp_chains), scratch
     u64* commit_ts;     // commit_timestamp sink (T.commit_ts, or a scratch word when dry)
     u32 dry;            // dry run: replies only, no state change
-    u32 ablate;         // timing-only builds (TBGPU_ABLATE): skip parts of the work; results wrong
     Transfer* ev_copy;  // ev is in host memory (zero copy): fp_commit leaves an HBM copy here, or null
 };
 constexpr u32 TILE_WORDS = 6;
@@ -33,6 +32,12 @@ constexpr u32 TILE_WORDS = 6;
 // fp_launch_index + fp_launch_fix + fp_launch_advance
 constexpr u32 FP_TAIL_THREADS = 1024, FP_TAIL_MAX = 16384;
 enum { ABL_DUP = 1, ABL_BALANCES = 2, ABL_ROWS = 4, ABL_LOOKBACK = 8, ABL_EVENT = 16, ABL_PROBE = 32 };
+// Timing-only ablations exist only in variant builds (build.build_variant with
+// FP_ABLATE=<mask>, profiles/ablate.py): the product library compiles them out, so no
+// environment setting can make it skip work.
+#ifndef FP_ABLATE
+#define FP_ABLATE 0
+#endif
 
 void fp_launch_prep(const FastArgs& F, hipStream_t stream);
 void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream);

@@ -138,7 +138,7 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
     AccIdx A, B;
     const bool dd = dense_has(T, t.debit_account_id), dc = dense_has(T, t.credit_account_id);
     u64 EA = 0, EB = 0;
-    if (F.ablate & ABL_PROBE) {  // timing only: no index reads (slots and fields made up)
+    if (FP_ABLATE & ABL_PROBE) {  // timing only: no index reads (slots and fields made up)
         A = {(u64)t.debit_account_id, (u64)(t.debit_account_id >> 64), (u32)(hd % 1000) + 1, t.ledger, 0, 1, 0};
         B = {(u64)t.credit_account_id, (u64)(t.credit_account_id >> 64), (u32)(hc % 1000) + 1, t.ledger, 0, 1, 0};
     } else {
@@ -162,7 +162,7 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
     if (t.amount == 0) return TBGPU_CREATE_TRANSFER_AMOUNT_MUST_NOT_BE_ZERO;
     if (t.ledger == 0) return TBGPU_CREATE_TRANSFER_LEDGER_MUST_NOT_BE_ZERO;
     if (t.code == 0) return TBGPU_CREATE_TRANSFER_CODE_MUST_NOT_BE_ZERO;
-    if (!(F.ablate & ABL_PROBE)) {
+    if (!(FP_ABLATE & ABL_PROBE)) {
         if (dd) A = {(u64)t.debit_account_id, 0, (u32)(EA & 0x1FFFFFFFu), (u32)(EA >> 32), (u16)((EA >> 28) & 0xE), 0, 0};
         if (dc) B = {(u64)t.credit_account_id, 0, (u32)(EB & 0x1FFFFFFFu), (u32)(EB >> 32), (u16)((EB >> 28) & 0xE), 0, 0};
     }
@@ -339,7 +339,7 @@ void fp_commit(Tables T, FastArgs F) {
     // branch between them); they only reach lanes without an event.
     // (eight named registers: an array live across the loops below went to scratch)
     uint4 c0{}, c1{}, c2{}, c3{}, c4{}, c5{}, c6{}, c7{};
-    if (!(F.ablate & ABL_EVENT) && F.n) {
+    if (!(FP_ABLATE & ABL_EVENT) && F.n) {
         const uint4* src = (const uint4*)F.ev;
         const u64 last = (u64)F.n * 8 - 1, q0 = (u64)wbase * 8 + lane;
         c0 = src[min(q0, last)];
@@ -387,7 +387,7 @@ void fp_commit(Tables T, FastArgs F) {
         }
     }
     if (valid) {
-        if (F.ablate & ABL_EVENT) {  // timing only: a made-up plain event instead of the load
+        if (FP_ABLATE & ABL_EVENT) {  // timing only: a made-up plain event instead of the load
             t.id = (u128)i + 1 + F.row_base;
             t.debit_account_id = (i * 7919u) % 1000000u + 1;
             t.credit_account_id = (i * 104729u + 1) % 1000000u + 1;
@@ -403,7 +403,7 @@ void fp_commit(Tables T, FastArgs F) {
     }
 #if defined(FP_LDS_EVENTS)
     // the wave's events through LDS in rounds of STAGE_RECS, one record per lane
-    if (!(F.ablate & ABL_EVENT)) {
+    if (!(FP_ABLATE & ABL_EVENT)) {
         uint4* st = s_stage[wave];
         constexpr int ROUNDS = 64 / STAGE_RECS;
 #pragma unroll
@@ -429,9 +429,9 @@ void fp_commit(Tables T, FastArgs F) {
             wave_lds_sync();
         }
     }
+#endif
     if (F.ev_copy && valid) F.ev_copy[i] = t;  // events read in place from host memory: an HBM
                                                // copy for the launches after this one
-#endif
     // Linked-chain membership (execute, src/state_machine.zig:1018-1035): linked
     // here, or the batch's previous event is (the router may close a chain that
     // continues on another shard: TBGPU_CTL_CHAIN_END).
@@ -444,7 +444,7 @@ void fp_commit(Tables T, FastArgs F) {
     const bool member = lk || plk || (myctl & TBGPU_CTL_DOOM);
     if (__ballot(member) && lane == 0) atomicOr(&F.counters[CNT_FLAGS], (u32)FL_FCHAIN);
     bool own_ok = false;
-#define STORE_ROW() do { if (!(F.ablate & ABL_ROWS)) T.xrows[row_base + i] = t; } while (0)
+#define STORE_ROW() do { if (!(FP_ABLATE & ABL_ROWS)) T.xrows[row_base + i] = t; } while (0)
     if (valid) {
         id = t.id;
         u32 ds = NONE32, cs = NONE32;
@@ -470,7 +470,7 @@ void fp_commit(Tables T, FastArgs F) {
             // tile-local aggregation first: a hot account costs one global atomic per tile
             const u64 a = (u64)t.amount;
             const u32 pend = (t.flags & TF_PENDING) ? 0u : 1u;
-            if (!(F.ablate & ABL_BALANCES)) {
+            if (!(FP_ABLATE & ABL_BALANCES)) {
                 agg_add(s_keys, s_sums, s_carry, ds * 4 + pend, a);
                 agg_add(s_keys, s_sums, s_carry, cs * 4 + 2 + pend, a);
             }

@@ -302,9 +302,13 @@ class ShardedStateMachine:
                 if st is not None and not st.fallback:
                     self.exchange_device(st)
                 continue
+            # step k's cross-shard settle (dry rounds, or its fallback to the exact
+            # router) decides before step k + 1 is routed: routing moves the router's
+            # state (prepare_timestamp, max_id, amount_bound) that a fallback of step
+            # k restores and then advances by step k alone
+            self.commit_routed(st, background=True)
             nxt = next(it, None)
             st2 = self.route_device(*nxt) if nxt is not None else None
-            self.commit_routed(st, background=True)
             if st2 is not None and not st2.fallback:
                 self.exchange_device(st2)
             yield self.finish_routed(st)
@@ -641,7 +645,8 @@ class ShardedStateMachine:
                     nb_ = breaks(out, at)
                     if nb_ == brk:
                         out2, at2, cts = commit(ctl, False)
-                        assert out2.tobytes() == out.tobytes(), "sharded commit: dry run and commit disagree"
+                        if out2.tobytes() != out.tobytes():
+                            raise RuntimeError("sharded commit: dry run and commit disagree (engine invariant)")
                         st.out, st.at, st.cts = out2, at2, cts
                         clock("commit_ms")
                         return st
@@ -956,23 +961,34 @@ class ShardedStateMachine:
             if nb == brk:
                 sub = self._build_sub(mine, T, glob, span, last_member, brk)
                 res2 = self._commit(sub, False)
-                assert sorted(res2) == sorted(res), "sharded commit: dry run and commit disagree"
+                if sorted(res2) != sorted(res):
+                    raise RuntimeError("sharded commit: dry run and commit disagree (engine invariant)")
                 res = res2
                 break
-            if rounds >= self.max_rounds and len(span) > 1:
-                # Serial fallback: no fixed point yet and nothing committed.  Commit the
-                # prefix that holds only the first cross-shard chain (a single chain's
-                # break is found in two dry rounds: its parts before the break see the
-                # same shard states either way); the next round resumes at the second.
-                cut = sorted(span)[1]
-                mine = [x for x in mine if (x[0], x[1]) < cut]
-                span = {c: o for c, o in span.items() if c < cut}
-                stop = cut if stop is None else min(stop, cut)
-                self.stats["serial_fallbacks"] += 1
-                brk, rounds = {}, 0
-                continue
-            if rounds >= 4 * self.max_rounds + 4:
-                raise AssertionError("sharded commit: a single cross-shard chain did not settle")
+            if rounds >= self.max_rounds:
+                # Serial fallback: no fixed point yet and nothing committed.  Shrink the
+                # round to a prefix that makes progress and settles: the events before
+                # the first cross-shard chain (no chain spans there: no dry rounds), or,
+                # when that chain starts the round, the chain and what follows it up to
+                # the next spanning chain.  A chain with no spanning chain after it
+                # settles in two dry rounds: its parts before the break see the same
+                # shard states either way.  Every cut is a chain start after the resume
+                # point, so the rounds of a step stay bounded by its chains.
+                chains = sorted(span)
+                head = min((x[0], x[1]) for x in mine) if mine else None
+                head = min([h for h in self.comm.all_gather_object(head) if h is not None])
+                cut = chains[0] if chains[0] > head else (chains[1] if len(chains) > 1 else None)
+                if cut is not None:
+                    mine = [x for x in mine if (x[0], x[1]) < cut]
+                    span = {c: o for c, o in span.items() if c < cut}
+                    stop = cut if stop is None else min(stop, cut)
+                    self.stats["serial_fallbacks"] += 1
+                    brk, rounds = {}, 0
+                    continue
+                # a lone spanning chain at the head of the round settles within two rounds
+                if rounds >= self.max_rounds + 2:
+                    raise RuntimeError("sharded commit: a lone cross-shard chain did not settle "
+                                       "(its break depends on no other chain: an engine invariant failed)")
             brk = nb
 
         # ---- 7. replies to sources

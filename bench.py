@@ -163,7 +163,7 @@ def host_path(eng, w, tts, counts, b0, nbs, torch):
     pinned = torch.empty((o1 - o0) * 128, dtype=torch.uint8, pin_memory=True)
     view = pinned.numpy().view(TRANSFER_DTYPE)
     view[:] = w.transfers[o0:o1]
-    lat = []
+    lat, dev_us = [], []
     ev_single = 0
     for k in range(single):
         b = b0 + k
@@ -171,8 +171,10 @@ def host_path(eng, w, tts, counts, b0, nbs, torch):
         t0 = time.perf_counter()
         eng.create_transfers(int(tts[b]), ev)
         lat.append(time.perf_counter() - t0)
+        dev_us.append(eng.stats().device_ms * 1e3)  # HIP events around the call on the engine stream
         ev_single += len(ev)
     lat = np.array(lat) * 1e6
+    dev_us = np.array(dev_us)
     s0 = b0 + single
     ev = view[int(offs[s0]) - o0:]
     t0 = time.perf_counter()
@@ -182,6 +184,9 @@ def host_path(eng, w, tts, counts, b0, nbs, torch):
                        "latency_us": {"p50": round(float(np.percentile(lat, 50)), 1),
                                       "p99": round(float(np.percentile(lat, 99)), 1),
                                       "max": round(float(lat.max()), 1)},
+                       "device_us": {"p50": round(float(np.percentile(dev_us, 50)), 1),
+                                     "p99": round(float(np.percentile(dev_us, 99)), 1),
+                                     "max": round(float(dev_us.max()), 1)},
                        "transfers_per_s": round(ev_single / (lat.sum() * 1e-6), 1),
                        "entry": "tbgpu_create_transfers (one batch per call, pinned host buffers)"},
             "streamed": {"batches": streamed, "transfers": len(ev), "seconds": round(el, 6),

@@ -238,6 +238,9 @@ typedef struct tbgpu_options {
 
 enum {
     TBGPU_OPT_FORCE_GENERAL = 1u << 0, /* disable the balance-insensitive fast path (tests) */
+    TBGPU_OPT_WALK_EARLY = 1u << 1,    /* the fixed point hands its chunk to the sequential walk
+                                          after two passes instead of its pass budget (tests:
+                                          the walk's results are the passes' results) */
 };
 
 /* Replaces StateMachine.init/deinit (src/state_machine.zig:418-451).
@@ -515,13 +518,16 @@ uint64_t tbgpu_commit_timestamp(tbgpu_ctx* ctx);
 typedef struct tbgpu_stats {
     uint64_t events;          /* events in the last call                        */
     uint32_t iterations;      /* fixed-point passes of the last call            */
-    uint32_t path;            /* 0 general (scan + rescan), 1 fast (no rescan)  */
+    uint32_t path;            /* 0 general (scan + rescan), 1 fast (no rescan),
+                                 2 general, walked past the pass budget         */
     uint64_t sorts;           /* side sorts performed                           */
     double   device_ms;       /* HIP-event time of the last call's device work  */
     /* With profiling on: HIP-event time per phase of the last call, on the ctx
      * stream: [0] upload [1] classify+group [2] sort [3] balance scan
      * [4] evaluate [5] apply [6] reserved [7] reserved. */
     double   phase_ms[8];
+    uint64_t walks;           /* chunks, since init, whose fixed point reached its
+                                 pass budget and was walked in execute's order    */
 } tbgpu_stats;
 void tbgpu_last_stats(tbgpu_ctx* ctx, tbgpu_stats* out);
 /* Enable per-phase HIP-event timing (adds a few event records per call). */

@@ -65,7 +65,7 @@ def _check(w, **kw):
     from tigerbeetle_amd.engine import Engine
     orc = oracle.Oracle(len(w.accounts), len(w.transfers))
     gpu = Engine(accounts_max=1 << 10, transfers_max=1 << 15, history_max=1 << 12, events_per_call_max=1 << 13,
-                 force_general=kw.pop("force_general", False))
+                 force_general=kw.pop("force_general", False), walk_early=kw.pop("walk_early", False))
     try:
         oa, ot = run_workload(orc, w)
         ga, gt = run_workload(gpu, w, **kw)
@@ -89,3 +89,6 @@ def test_fuzz_mutations(seed):
     _check(w, split=1)
     if seed % 3 == 0:
         _check(w, force_general=True)
+    if seed % 3 == 1:
+        # the sequential walk from the front after two passes (the fixed point's bound)
+        _check(w, force_general=True, walk_early=True)

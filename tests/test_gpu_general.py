@@ -113,7 +113,27 @@ def _relay_chain(n: int, accounts: int, relay: int, fund: int = 0):
 
 @pytest.mark.parametrize("fund", [0, 10])
 def test_adversarial_relay_chain(fund):
-    """A whole batch is one dependency chain; exact results whatever the depth."""
+    """A whole batch is one dependency chain; exact results whatever the depth.  With
+    fund=0 the passes would need one per event (O(n^2)); past the pass budget the
+    engine walks the rest of the batch in execute's order (tr_walk), so the call is
+    bounded by O(n) work."""
     w = _relay_chain(BATCH_MAX - 1, accounts=BATCH_MAX + 1, relay=BATCH_MAX, fund=fund)
     st, _ = _parity(w)
-    print(f"relay chain fund={fund}: {st.iterations} passes")
+    print(f"relay chain fund={fund}: {st.iterations} passes, path {st.path}, {st.device_ms:.2f} ms device time "
+          f"for the {BATCH_MAX}-event batch")
+    if fund == 0:
+        assert st.path == 2 and st.iterations <= 64 + 48, (st.path, st.iterations)
+        assert st.device_ms < 100.0, st.device_ms
+    else:
+        assert st.iterations <= 2
+
+
+@pytest.mark.parametrize("kind", ["config3", "stress"])
+def test_walk_matches_the_passes(kind):
+    """The walk from the front after two passes (TBGPU_OPT_WALK_EARLY) on the flag-heavy
+    mixes: chains, two-phase, balancing, limits, duplicates, expiry -- the same results
+    and state as the oracle (and so as the converged passes)."""
+    mk = workload.config3 if kind == "config3" else workload.config3_stress
+    w = mk(batches=6, account_count=2_000, seed=21)
+    st, _ = _parity(w, split=2, force_general=True, walk_early=True)
+    assert st.walks > 0, st.walks

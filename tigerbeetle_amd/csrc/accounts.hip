@@ -264,11 +264,16 @@ __global__ void import_transfers(Tables T, const Transfer* rows, u32 n, u64 row_
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     u64 mxl = 0, mxh = 0, mnl = ~0ull, mnh = ~0ull;
     if (i < n) {
-        const Transfer t = rows[i];
-        if (!in_place) T.xrows[row_base + i] = t;
-        xidx_insert(T, t.id, (u32)(row_base + i));
-        mxl = mnl = (u64)t.id;
-        mxh = mnh = (u64)(t.id >> 64);
+        if (!in_place) {  // the row, 16 bytes at a time
+            const uint4* src = (const uint4*)&rows[i];
+            uint4* dst = (uint4*)&T.xrows[row_base + i];
+#pragma unroll
+            for (int k = 0; k < 8; k++) dst[k] = src[k];
+        }
+        const u128 id = rows[i].id;
+        xidx_insert(T, id, (u32)(row_base + i));
+        mxl = mnl = (u64)id;
+        mxh = mnh = (u64)(id >> 64);
     }
     mxl = wave_max_u64(mxl);
     mxh = wave_max_u64(mxh);

@@ -281,6 +281,8 @@ enum {
     CNT_PCUR = 9,       // general path: pending-group ranges reserved so far
     CNT_TS_SAVE = 12,   // fast path: commit_timestamp before the call (u64 in words 12-13)
     CNT_DBG = 16,       // diagnostics (words 16-21): changed events by kind, summed over a call's passes
+    CNT_NSIMPLE = 22,   // general path: events on the per-pass simple list (tr_lists)
+    CNT_NCOMPLEX = 23,  // general path: events on the per-pass complex list
     CNT_COUNT = 24,
 };
 enum {

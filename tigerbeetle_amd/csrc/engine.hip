@@ -84,10 +84,34 @@ T* dalloc(u64 count, u64* total) {
     return (T*)p;
 }
 
+// The tables every transfer probes at random (account rows and directory, the id
+// index): physically contiguous where the driver can place them, so their
+// translations stay few and large whatever earlier processes left the allocator with;
+// a plain allocation otherwise (same contents either way).
+template <typename T>
+T* dalloc_hot(u64 count, u64* total) {
+#if !defined(TBGPU_NO_CONTIG)
+    void* p = nullptr;
+    const u64 bytes = std::max<u64>(count * sizeof(T), 16);
+    if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous) == hipSuccess && p) {
+        *total += bytes;
+        return (T*)p;
+    }
+    (void)hipGetLastError();
+#endif
+    return dalloc<T>(count, total);
+}
+
 }  // namespace
 
 constexpr u32 PC_RING = 1024;        // pass-counter ring (passes in flight << ring)
 constexpr u32 PASS_GROUP_MAX = 48;   // passes enqueued between two host round trips
+// The fixed point's pass budget: past it the chunk's events from the front on are
+// walked in execute's order (transfers.hip tr_walk).  BASELINE config 3 converges in
+// 14-18 passes per 20-batch chunk; a chunk past 64 is a deep dependency chain, where
+// passes cost O(n) each and the walk O(1) per event.
+constexpr u32 WALK_PASSES = 64;
+constexpr u32 WALK_UNDO = 4 * 8192;   // a linked chain's balance moves (<= 2 per member, members <= a batch)
 constexpr u32 RPT_BASE = CNT_COUNT, RPT_COUNTS = CNT_COUNT + 8;  // k_report's layout (words)
 constexpr u32 PC_OFF = 32;           // the pass-change ring's offset behind the counter words
 static_assert(PC_OFF >= CNT_COUNT, "counter words overlap the pass-change ring");
@@ -125,6 +149,7 @@ struct tbgpu_ctx {
     u8* sq_ok = nullptr;
     u128 *sq_dpend = nullptr, *sq_dpost = nullptr;
     u32 *gkey_s, *gsorted;  // the id-group sort's output (the members of each id group, by event)
+    u32 *lst_simple, *lst_complex;  // the fixed point's per-pass work lists (tr_lists)
     Bal4* bb = nullptr;
     SortScratch ss{};
     void* side_tiles = nullptr;
@@ -183,8 +208,16 @@ struct tbgpu_ctx {
     u32 last_passes = 8;  // passes the last fixed point took (sizes the next pass group)
     bool long_segments = false;  // this call has an account segment too long for the fused scan
     // fixed-point pass counters, a ring of PC_RING words: changes per pass (the gate
-    // of the next pass); a second ring of PC_RING words is spare
+    // of the next pass); a second ring: the first event each pass changed (the
+    // walk's front); a third is spare (diagnostics)
     u32* pc = nullptr;
+    // the walk (tr_walk), allocated on first use: per side, its account segment's
+    // start, and per segment start the running balance; the open chain's undo log
+    u32* w_sstart = nullptr;
+    Bal4* w_bal = nullptr;
+    u32* w_undo_slot = nullptr;
+    Bal4* w_undo_val = nullptr;
+    u32* w_out = nullptr;
     u64* rg_part = nullptr;    // tr_range's per-block records
     u32* h_pc = nullptr;       // pinned mirror of the change ring
     u64* h_base = nullptr;     // pinned mirror of T.base
@@ -259,6 +292,8 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->sq_ok = dalloc<u8>(m, &B);
     c->sq_dpend = dalloc<u128>(m, &B);
     c->sq_dpost = dalloc<u128>(m, &B);
+    c->lst_simple = dalloc<u32>(n, &B);
+    c->lst_complex = dalloc<u32>(n, &B);
     c->gkey_s = dalloc<u32>(n, &B);
     c->gsorted = dalloc<u32>(n, &B);
     c->bb = dalloc<Bal4>(m, &B);
@@ -275,7 +310,7 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->res_buf = dalloc<u8>(n * 8, &B);
     c->counts = dalloc<u32>(c->bmax, &B);
     // the counters, then the pass-change ring: one copy brings both back per pass group
-    c->counters = dalloc<u32>(PC_OFF + 2 * PC_RING, &B);
+    c->counters = dalloc<u32>(PC_OFF + 3 * PC_RING, &B);
     c->status = dalloc<int>(4, &B);
     c->f_gcap = pow2_at_least(2 * nmax);
     c->f_gtab = dalloc<u32>(c->f_gcap, &B);
@@ -292,7 +327,7 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->rg_part = dalloc<u64>(tr_range_part_words(n), &B);
 
     HIP_CHECK(hipHostMalloc((void**)&c->h_base, 8 * sizeof(u64), hipHostMallocDefault));  // [4..5]: a uint4
-    HIP_CHECK(hipHostMalloc((void**)&c->h_counters, (PC_OFF + 2 * PC_RING) * sizeof(u32), hipHostMallocDefault));
+    HIP_CHECK(hipHostMalloc((void**)&c->h_counters, (PC_OFF + 3 * PC_RING) * sizeof(u32), hipHostMallocDefault));
     c->h_pc = c->h_counters + PC_OFF;
     HIP_CHECK(hipHostMalloc((void**)&c->h_report, (RPT_COUNTS + c->bmax) * sizeof(u32), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc((void**)&c->h_res, c->nmax * 8 + 8, hipHostMallocDefault));
@@ -366,12 +401,12 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     c->xidx_cap = pow2_at_least(2 * o.transfers_max);
     c->hist_cap = o.history_max;
     u64& B = c->bytes;
-    c->T.acc = dalloc<Account>(o.accounts_max, &B);
-    c->T.aidx = dalloc<AccIdx>(c->aidx_cap, &B);
+    c->T.acc = dalloc_hot<Account>(o.accounts_max, &B);
+    c->T.aidx = dalloc_hot<AccIdx>(c->aidx_cap, &B);
     c->T.aidx_mask = c->aidx_cap - 1;
     c->T.xrows = dalloc<Transfer>(c->xrow_cap, &B);
     c->T.xful = dalloc<u8>(c->xrow_cap, &B);
-    c->T.xidx = dalloc<u32>(c->xidx_cap, &B);
+    c->T.xidx = dalloc_hot<u32>(c->xidx_cap, &B);
     c->T.xidx_mask = c->xidx_cap - 1;
     c->T.hrows = dalloc<History>(c->hist_cap, &B);
     c->T.commit_ts = dalloc<u64>(2, &B);
@@ -390,7 +425,7 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
         c->T.dense_n = c->T.dense_span * c->T.dense_blocks;
         if (!o.dense_block_span) c->T.dense_n = o.accounts_max;
     }
-    c->T.dense = dalloc<u64>(c->T.dense_n, &B);
+    c->T.dense = dalloc_hot<u64>(c->T.dense_n, &B);
     alloc_scratch(c, o.events_per_call_max);
     tbgpu_reset(c);
     *out = c;
@@ -607,6 +642,8 @@ static TrArgs make_tr_args(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb) {
     C.commit_ts = c->rt_dry ? c->rt_dry_ts : c->T.commit_ts;
     static const bool debug = getenv("TBGPU_TRACE_PASSES") != nullptr;  // diagnostics only
     C.debug = debug ? 1u : 0u;
+    C.lst_simple = c->lst_simple;
+    C.lst_complex = c->lst_complex;
     return C;
 }
 
@@ -710,6 +747,60 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_crea
     return true;
 }
 
+// The fixed point's bounded worst case (transfers.hip tr_walk): the chunk's events
+// from the chain start of `front`'s event on, walked in execute's order in state D
+// (every earlier event final there).  The sides are rebuilt when a post/void resolves
+// to a pending outside them, and the walk resumes at its chain.
+template <typename Rebuild>
+static void walk(tbgpu_ctx* c, const TrArgs& C, u32 n, EvalState& D, const u32* front_dev, u64& m,
+                 Rebuild&& build_sides) {
+    hipStream_t s = c->stream;
+    if (!c->w_sstart) {
+        u64& B = c->bytes;
+        c->w_sstart = dalloc<u32>(c->scap, &B);
+        c->w_bal = dalloc<Bal4>(c->scap, &B);
+        c->w_undo_slot = dalloc<u32>(WALK_UNDO, &B);
+        c->w_undo_val = dalloc<Bal4>(WALK_UNDO, &B);
+        c->w_out = dalloc<u32>(4, &B);
+    }
+    // the front's chain start: every event before it is final
+    u32 f = 0;
+    HIP_CHECK(hipMemcpyAsync(c->h_base + 4, front_dev, sizeof(u32), hipMemcpyDeviceToHost, s));
+    wait_stream(s);
+    memcpy(&f, c->h_base + 4, sizeof f);
+    if (f >= n) f = 0;
+    HIP_CHECK(hipMemcpyAsync(c->h_base + 4, C.cs + f, sizeof(u32), hipMemcpyDeviceToHost, s));
+    wait_stream(s);
+    u32 start = 0;
+    memcpy(&start, c->h_base + 4, sizeof start);
+    u32* one = c->pc + 2 * PC_RING;  // the scan's open gate
+    for (;;) {
+        tr_launch_walk_prep(C, m, start, c->w_sstart, D.cfail, s);
+        HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)one, 1, 1, s));
+        SideScanArgs SA{};
+        SA.skey = c->skey_s; SA.sq_ev = c->sq_ev; SA.sq_cs = c->sq_cs; SA.sq_ok = c->sq_ok;
+        SA.sq_dpend = c->sq_dpend; SA.sq_dpost = c->sq_dpost; SA.n = n;
+        SA.cfail = D.cfail;
+        SA.cfail_clear = nullptr;
+        SA.gate = PassGate{one, c->counters + CNT_RESORT, 0};
+        // the balance of every side before the front's events (the walked ones' records are zero)
+        side_scan(SA, m, (u32)c->accounts_max, true, c->side_tiles, c->T.acc, c->bb, s);
+        tr_launch_walk(c->T, C, D, c->bb, m, c->w_sstart, c->w_bal, c->w_undo_slot, c->w_undo_val, WALK_UNDO, start,
+                       c->w_out, s);
+        HIP_CHECK(hipMemcpyAsync(c->h_base + 4, c->w_out, 2 * sizeof(u32), hipMemcpyDeviceToHost, s));
+        wait_stream(s);
+        u32 out[2];
+        memcpy(out, c->h_base + 4, sizeof out);
+        if (out[1]) tbgpu_fatal("create_transfers", "walk: a linked chain's undo log overflowed", __FILE__, __LINE__);
+        if (out[0] == NONE32) break;
+        // a post/void resolved to a pending outside its sides: rebuild them from D
+        // (its resolution is then a candidate) and walk on from its chain
+        HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)(c->counters + CNT_RESORT), 0, 1, s));
+        build_sides(D);
+        start = out[0];
+    }
+}
+
 // The general path's fixed point over one chunk (transfers.hip): classify, group,
 // the optimistic initial state, then Jacobi passes enqueued in groups without a
 // host round trip inside a group (the kernels of the passes after convergence
@@ -734,10 +825,12 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
     tr_launch_group(C, 0, s);
     tr_launch_group2(C, s);
     tr_launch_group(C, 1, s);
-    tr_launch_init(c->T, C, c->st[0], s);
+    tr_launch_init(c->T, C, c->st[0], c->st[1], s);
+    tr_launch_lists(C, s);
 
     // The sides of the events, sorted by account (one host round trip: their count).
     u64 m = 0;
+    u32 n_list[2] = {0, 0};  // the per-pass work lists' lengths (simple, complex)
     auto build_sides = [&](const EvalState& S) {
         prof_mark(c, PH_SORT);
         for (u32 kmax : {SIDE_CANDS, 1u}) {
@@ -745,8 +838,11 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
             scan3_exclusive(c->mask, c->ranks, n, c->sc, s);
             uint4 tot;
             HIP_CHECK(hipMemcpyAsync(c->h_base + 4, c->ranks + n, sizeof(uint4), hipMemcpyDeviceToHost, s));
+            // the work lists' lengths (tr_lists) come back with the side count
+            HIP_CHECK(hipMemcpyAsync(c->h_base + 6, c->counters + CNT_NSIMPLE, 2 * sizeof(u32), hipMemcpyDeviceToHost, s));
             wait_stream(s);
             memcpy(&tot, c->h_base + 4, sizeof tot);
+            memcpy(n_list, c->h_base + 6, sizeof n_list);
             m = 2ull * (tot.x + tot.y + tot.z);
             if (m <= c->scap) {
                 tr_launch_side_build(C, S, kmax, c->ranks, inv_acc, c->skey, c->sval, s);
@@ -780,7 +876,9 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
             SA.gate = G;
             if (c->long_segments) side_scan(SA, m, inv_acc, chains, c->side_tiles, c->T.acc, c->bb, s);
             else side_scan_fused(SA, m, inv_acc, c->tstart, c->counters + CNT_LONG, c->T.acc, c->bb, s);
-            tr_launch_evaluate(c->T, C, S, D, c->bb, G, chg + (q + 1) % PC_RING, chg + (q + 2) % PC_RING, s);
+            tr_launch_evaluate_lists(c->T, C, S, D, c->bb, G, chg + (q + 1) % PC_RING, chg + (q + 2) % PC_RING,
+                                     chg + PC_RING + (q + 1) % PC_RING, chg + PC_RING + (q + 2) % PC_RING,
+                                     n_list[0], n_list[1], s);
         }
         const u32 p0 = p;
         p += group;
@@ -824,6 +922,19 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
         for (u32 q = p0; q < p; q++)
             if (c->h_pc[(q + 1) % PC_RING] == 0) { done_at = q; break; }
         if (done_at != NONE32) break;
+        const u32 budget = (c->opt.flags & TBGPU_OPT_WALK_EARLY) ? 2u : WALK_PASSES;
+        if (p >= budget) {
+            // past the pass budget: the last pass (p - 1) wrote st[p & 1]; walk on from its front
+            walk(c, C, n, c->st[p & 1], c->pc + PC_RING + p % PC_RING, m, build_sides);
+            HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)(c->counters + EPI_WORD), (p & 1) ? 2 : 1, 1, s));
+            epilogue(m);
+            c->stats.iterations = p;
+            c->stats.path = 2;
+            c->last_passes = 8;
+            c->side_m = m;
+            c->stats.walks++;
+            return &c->st[p & 1];
+        }
         // the changes decay about geometrically: enqueue the passes that decay predicts
         const double last = c->h_pc[p % PC_RING], prev = c->h_pc[(p - 1) % PC_RING];
         const double r = prev > 0 ? std::min(0.9, std::max(0.05, last / prev)) : 0.5;
@@ -836,7 +947,7 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
         // under each probe mode: where a pass's evaluation time goes
         EvalState& S = c->st[(done_at + 1) & 1];
         EvalState& D = c->st[done_at & 1];
-        u32* one = c->pc + PC_RING;  // spare ring: an open gate
+        u32* one = c->pc + 2 * PC_RING;  // spare ring: an open gate
         HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)one, 1, 1, s));
         PassGate G{one, c->counters + CNT_RESORT, 0};
         for (u32 mode : {0u, 1u, 2u, 3u}) {
@@ -846,7 +957,7 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
             HIP_CHECK(hipEventCreate(&e0));
             HIP_CHECK(hipEventCreate(&e1));
             HIP_CHECK(hipEventRecord(e0, s));
-            for (int r = 0; r < 5; r++) tr_launch_evaluate(c->T, P, S, D, c->bb, G, one + 2, one + 3, s);
+            for (int r = 0; r < 5; r++) tr_launch_evaluate(c->T, P, S, D, c->bb, G, one + 2, one + 3, one + 4, one + 5, s);
             HIP_CHECK(hipEventRecord(e1, s));
             HIP_CHECK(hipEventSynchronize(e1));
             float ms = 0;

@@ -55,6 +55,13 @@ struct TrArgs {
     u32* plist;           // scratch: pending-group members in arrival order
     u64 gmask;
     u32* counters;
+    // Per-pass work lists (tr_lists, once per chunk): `simple` holds the transfers whose
+    // id nothing before them in the call or the state holds (their pass is create_transfer's
+    // balance tail alone) and the static failures inside chains (their failure breaks the
+    // chain every pass); `complex` the post/voids and possible `exists`.  Static failures
+    // outside chains are final after tr_init and never re-evaluated.
+    u32* lst_simple;
+    u32* lst_complex;
     u32 debug;            // diagnostics: count changed events by kind (TBGPU_TRACE_PASSES)
     u32 probe;            // timing probes only (TBGPU_EVAL_PROBE, after convergence): 1 skip post/void, 2 no side records
     Sides sd;             // the account sides of the call's events (engine.h)
@@ -76,15 +83,29 @@ void tr_launch_classify(const Tables& T, const TrArgs& C, hipStream_t stream);
 // without a sort: ranges reserved per group, members placed, then ranked in it.
 void tr_launch_group(const TrArgs& C, u32 kind, hipStream_t stream);
 void tr_launch_group2(const TrArgs& C, hipStream_t stream);
-void tr_launch_init(const Tables& T, const TrArgs& C, const EvalState& D, hipStream_t stream);
+// D: the first pass's input state; D2 (the other buffer) also receives the static
+// failures outside chains, which no pass evaluates again
+void tr_launch_init(const Tables& T, const TrArgs& C, const EvalState& D, const EvalState& D2, hipStream_t stream);
 void tr_launch_side_count(const TrArgs& C, const EvalState& S, u32 kmax, u8* mask, hipStream_t stream);
 void tr_launch_side_build(const TrArgs& C, const EvalState& S, u32 kmax, const uint4* pairs, u32 invalid, u32* skey,
                           u32* sval, hipStream_t stream);
 void tr_launch_side_pos(const TrArgs& C, const u32* sval_s, u64 m, hipStream_t stream);
 void tr_launch_side_rec(const TrArgs& C, const EvalState& S, hipStream_t stream);
 void tr_launch_evaluate(const Tables& T, const TrArgs& C, const EvalState& S, const EvalState& D, const Bal4* bb,
-                        const PassGate& g, u32* chg, u32* chg_next, hipStream_t stream);
+                        const PassGate& g, u32* chg, u32* chg_next, u32* front, u32* front_next, hipStream_t stream);
+// One pass over the work lists (tr_lists): the simple list's kernel, then evaluate_one
+// over the complex list (counts from the host's copy of CNT_NSIMPLE / CNT_NCOMPLEX).
+void tr_launch_lists(const TrArgs& C, hipStream_t stream);
+void tr_launch_evaluate_lists(const Tables& T, const TrArgs& C, const EvalState& S, const EvalState& D, const Bal4* bb,
+                              const PassGate& g, u32* chg, u32* chg_next, u32* front, u32* front_next, u32 n_simple,
+                              u32 n_complex, hipStream_t stream);
 void tr_launch_mask(const Tables& T, const TrArgs& C, const EvalState& S, u8* fres, u8* mask, hipStream_t stream);
+// The bounded worst case (transfers.hip tr_walk): the events from `start` (a chain
+// start; every earlier event final in D) walked in execute's order.  out[0]: the
+// chain start to resume from after a side rebuild (NONE32: done), out[1]: error.
+void tr_launch_walk_prep(const TrArgs& C, u64 m, u32 start, u32* sstart, u32* cfail, hipStream_t stream);
+void tr_launch_walk(const Tables& T, const TrArgs& C, const EvalState& D, Bal4* bb, u64 m, const u32* sstart,
+                    Bal4* wbal, u32* undo_slot, Bal4* undo_val, u32 undo_cap, u32 start, u32* out, hipStream_t stream);
 void tr_launch_apply(const Tables& T, const TrArgs& C, const EvalState& S, const u8* fres, const uint4* rk,
                      const Bal4* bb, tbgpu_create_transfers_result_t* results, u32* counts, u64* part,
                      hipStream_t stream);

@@ -65,6 +65,16 @@ __device__ __forceinline__ u32 block_sum(u32 v) {
         for (u32 k = 0; k < (blockDim.x + 63) / 64; k++) r += s_sum[k];
     return r;
 }
+__device__ __forceinline__ u32 block_min(u32 v) {
+    __shared__ u32 s_min[16];
+    for (int off = 32; off > 0; off >>= 1) v = min(v, (u32)__shfl_xor(v, off));
+    if ((threadIdx.x & 63) == 0) s_min[threadIdx.x >> 6] = v;
+    __syncthreads();
+    u32 r = NONE32;
+    if (threadIdx.x == 0)
+        for (u32 k = 0; k < (blockDim.x + 63) / 64; k++) r = min(r, s_min[k]);
+    return r;
+}
 __device__ __forceinline__ u32 wave_min(u32 v) {
     for (int off = 32; off > 0; off >>= 1) v = min(v, (u32)__shfl_xor(v, off));
     return v;
@@ -666,14 +676,124 @@ __device__ __forceinline__ bool evaluate_one(const Tables& T, const TrArgs& C, c
 
 // `chg` is a ring word: this pass's count of changed events; the pass clears the
 // word the pass after it writes (the host clears nothing per pass).
+// `front` (a ring word beside chg): the first event this pass changed.  Every event
+// before it is final (each depends only on earlier ones): the walk starts there.
 __global__ void tr_evaluate(Tables T, TrArgs C, EvalState S, EvalState D, const Bal4* __restrict__ bb, PassGate g,
-                            u32* chg, u32* chg_next) {
+                            u32* chg, u32* chg_next, u32* front, u32* front_next) {
     if (!gate_open(g)) return;
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) *chg_next = 0;
+    if (i == 0) {
+        *chg_next = 0;
+        *front_next = NONE32;
+    }
     const bool changed = i < C.n && evaluate_one(T, C, S, D, bb, g, i);
     const u32 c = block_sum(changed ? 1u : 0u);
-    if (threadIdx.x == 0 && c) atomicAdd(chg, c);
+    const u32 f = block_min(changed ? i : NONE32);
+    if (threadIdx.x == 0 && c) {
+        atomicAdd(chg, c);
+        atomicMin(front, f);
+    }
+}
+
+// The per-pass work lists (TrArgs::lst_simple / lst_complex), in event order within a
+// wave; one cursor atomic per wave and list.
+__global__ void tr_lists(TrArgs C) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    u32 cls = 0;  // 0 final after tr_init, 1 simple, 2 complex
+    if (i < C.n) {
+        const u8 sr = C.sres[i];
+        if (sr != SRES_DYN) cls = C.cs[i] != C.ce[i] ? 1 : 0;
+        else if (C.core[i].flags & (TF_POST | TF_VOID)) cls = 2;
+        else cls = (C.prev_id[i] == NONE32 && C.pre_e[i] == NONE32) ? 1 : 2;
+    }
+    const u32 lane = threadIdx.x & 63;
+#pragma unroll
+    for (u32 k = 1; k <= 2; k++) {
+        const u64 m = __ballot(cls == k);
+        if (!m) continue;
+        u32 base = 0;
+        if (lane == 0) base = atomicAdd(&C.counters[k == 1 ? CNT_NSIMPLE : CNT_NCOMPLEX], (u32)__popcll(m));
+        base = __shfl(base, 0);
+        if (cls == k) (k == 1 ? C.lst_simple : C.lst_complex)[base + __popcll(m & ((1ull << lane) - 1))] = i;
+    }
+}
+
+// A pass over the simple list: create_transfer's balance tail (src/state_machine.zig:
+// 1286-1322) for transfers whose id nothing before them holds, and the static failures
+// inside chains (they break their chain every pass).  What evaluate_one does for them,
+// without its post/void and `exists` registers (occupancy: this is most of a pass).
+__global__ __launch_bounds__(256) void tr_eval_simple(TrArgs C, EvalState S, EvalState D, const Bal4* __restrict__ bb,
+                                                      PassGate g, u32 cnt, u32* chg, u32* chg_next, u32* front,
+                                                      u32* front_next) {
+    if (!gate_open(g)) return;
+    const u32 k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k == 0) {
+        *chg_next = 0;
+        *front_next = NONE32;
+    }
+    bool changed = false;
+    u32 i = NONE32;
+    if (k < cnt) {
+        i = C.lst_simple[k];
+        const u8 sr = C.sres[i];
+        const u32 csi = C.cs[i];
+        if (sr != SRES_DYN) {  // a static failure inside a chain
+            D.res[i] = sr;
+            D.ok[i] = 0;
+            D.amt[i] = 0;
+            D.pamt[i] = 0;
+            D.pref[i] = NONE32;
+            atomicMin(&D.cfail[csi], i);
+        } else {
+            const EvCore e = C.core[i];
+            const uint2 ep = C.sd.epos[i];
+            const u8 s_res = S.res[i];
+            const u128 s_amt = S.amt[i];
+            const Bal4 bd = bb[ep.x], bc = bb[ep.y];
+            u128 amount = 0;
+            const u8 res = eval_balances(e, bd, bc, &amount);
+            const bool ok = res == TBGPU_CREATE_TRANSFER_OK;
+            const u128 amt = ok ? amount : 0;
+            D.res[i] = res;
+            D.ok[i] = ok ? 1 : 0;
+            D.amt[i] = amt;
+            D.pamt[i] = 0;
+            D.pref[i] = NONE32;
+            if (!ok && csi != C.ce[i]) atomicMin(&D.cfail[csi], i);
+            changed = res != s_res || amt != s_amt;
+            if (changed) {
+                const u128 dpe = ok && (e.flags & TF_PENDING) ? amt : 0, dpo = ok && !(e.flags & TF_PENDING) ? amt : 0;
+                C.sd.sq_ok[ep.x] = C.sd.sq_ok[ep.y] = ok ? 1 : 0;
+                C.sd.sq_dpend[ep.x] = C.sd.sq_dpend[ep.y] = dpe;
+                C.sd.sq_dpost[ep.x] = C.sd.sq_dpost[ep.y] = dpo;
+            }
+        }
+    }
+    const u32 c = block_sum(changed ? 1u : 0u);
+    const u32 f = block_min(changed ? i : NONE32);
+    if (threadIdx.x == 0 && c) {
+        atomicAdd(chg, c);
+        atomicMin(front, f);
+    }
+}
+
+// evaluate_one over the complex list
+__global__ void tr_eval_complex(Tables T, TrArgs C, EvalState S, EvalState D, const Bal4* __restrict__ bb, PassGate g,
+                                u32 cnt, u32* chg, u32* front) {
+    if (!gate_open(g)) return;
+    const u32 k = blockIdx.x * blockDim.x + threadIdx.x;
+    u32 i = NONE32;
+    bool changed = false;
+    if (k < cnt) {
+        i = C.lst_complex[k];
+        changed = evaluate_one(T, C, S, D, bb, g, i);
+    }
+    const u32 c = block_sum(changed ? 1u : 0u);
+    const u32 f = block_min(changed ? i : NONE32);
+    if (threadIdx.x == 0 && c) {
+        atomicAdd(chg, c);
+        atomicMin(front, f);
+    }
 }
 
 // The pending an unresolved post/void most likely resolves to: a committed transfer
@@ -687,9 +807,21 @@ __device__ __forceinline__ u32 pending_guess(const TrArgs& C, u32 i) {
 // Starting point: every statically valid event succeeds, except that an id already
 // committed, or seen earlier in the call, answers `exists` (the first event with an
 // id is the one that succeeds), and a post/void resolves to its likeliest pending.
-__global__ void tr_init(Tables T, TrArgs C, EvalState D) {
+__global__ void tr_init(Tables T, TrArgs C, EvalState D, EvalState D2) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= C.n) return;
+    if (C.sres[i] != SRES_DYN && C.cs[i] == C.ce[i]) {
+        // a static failure outside any chain: final, on no work list; both state
+        // buffers hold it for every pass
+        for (const EvalState* E : {&D, &D2}) {
+            E->res[i] = C.sres[i];
+            E->ok[i] = 0;
+            E->amt[i] = 0;
+            E->pamt[i] = 0;
+            E->pref[i] = NONE32;
+        }
+        return;
+    }
     u8 sr = C.sres[i];
     if (sr == SRES_DYN && (C.prev_id[i] != NONE32 || C.pre_e[i] != NONE32)) sr = TBGPU_CREATE_TRANSFER_EXISTS;
     u8 res = sr;
@@ -1071,6 +1203,266 @@ __global__ __launch_bounds__(256) void tr_advance(Tables T, TrArgs C, const uint
     T.base[BASE_HIST] += tot.z;
 }
 
+// ------------------------------------------------------------- walker ----
+// The fixed point's bounded worst case.  Its passes grow with a chunk's dependency
+// depth, at most n + 1: an 8190-event batch in which every event's outcome decides
+// the next one's takes 8190 passes, O(n^2) work where the reference's execute is
+// O(n) (src/state_machine.zig:1018-1083).  Past a pass budget the engine walks the
+// events from the front on -- the chain start of the first event the last pass
+// changed; every event before it is final -- in execute's own order, in one thread:
+// each account's balance as the walk has moved it, linked chains opened and closed
+// as scopes (src/state_machine.zig:972-1000: a broken chain's balance moves are
+// undone), every event evaluated by evaluate_one against a state whose predecessors
+// are all final.  The walk leaves exactly the state the passes converge to, side
+// records included, and the same apply kernels commit it.
+
+// Before the walk: the side records of the walked events zeroed (the scan that
+// follows then gives every side the balance of the events before the front alone),
+// each side's account segment start (a binary search over the sorted keys), and the
+// walked chains' first failures reset.
+__global__ void tr_walk_prep(TrArgs C, u64 m, u32 start, u32* sstart, u32* cfail) {
+    const u64 q = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < m) {
+        const u32 ev = C.sd.sq_ev[q] & 0x7FFFFFFFu;
+        if (ev >= start) {
+            C.sd.sq_ok[q] = 0;
+            C.sd.sq_dpend[q] = 0;
+            C.sd.sq_dpost[q] = 0;
+        }
+        const u32 key = C.sd.skey_s[q];
+        u64 lo = 0, hi = q;  // first position with this key
+        if (key >= C.sd.inert) lo = q;
+        while (lo < hi) {
+            const u64 mid = (lo + hi) / 2;
+            if (C.sd.skey_s[mid] < key) lo = mid + 1; else hi = mid;
+        }
+        sstart[q] = (u32)lo;
+    }
+    if (q >= start && q < C.n) cfail[q] = NONE32;
+}
+
+// After the scan: each account's balance before the walked events, at its segment
+// start -- the scanned balance of its first side that belongs to a walked event
+// (every earlier side is final; the walked sides' records are zero).
+__global__ void tr_walk_init(TrArgs C, u64 m, u32 start, const u32* sstart, const Bal4* bb, Bal4* wbal) {
+    const u64 q = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= m) return;
+    if ((C.sd.sq_ev[q] & 0x7FFFFFFFu) < start) return;
+    const u32 s0 = sstart[q];
+    if (q == s0 || (C.sd.sq_ev[q - 1] & 0x7FFFFFFFu) < start) wbal[s0] = bb[q];
+}
+
+struct WalkArgs {
+    const u32* sstart;  // [m] first side of each side's account segment
+    Bal4* wbal;         // [m] per segment start: the account's balance as the walk has moved it
+    u32* undo_slot;     // the open chain's balance moves, for its rollback
+    Bal4* undo_val;
+    u32 undo_cap;
+    u32 start;          // the first walked event (a chain start)
+    u32* out;           // [0] resume point when the walk stopped early (NONE32: walked to the end), [1] error
+};
+
+// What the walk reads of an event, staged 64 events at a time by the whole wave so
+// that the walking lane meets no memory latency but the balances'.
+struct WalkRec {
+    EvCore core;
+    uint2 ep;
+    u32 cs, ce, pid, pre_e, s0d, s0c;
+    u8 sr, pad[7];
+};
+constexpr int WK_CACHE = 64;  // recently moved balances, direct-mapped by segment start
+
+// u128 words read past the vector L1 (the walking lane's own recent stores are in L2)
+__device__ __forceinline__ Bal4 wk_load(const Bal4* p) {
+    const u64* w = (const u64*)p;
+    u64 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k] = __hip_atomic_load(&w[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    Bal4 b;
+    b.dp = (u128)v[1] << 64 | v[0];
+    b.dpo = (u128)v[3] << 64 | v[2];
+    b.cp = (u128)v[5] << 64 | v[4];
+    b.cpo = (u128)v[7] << 64 | v[6];
+    return b;
+}
+
+__global__ __launch_bounds__(64) void tr_walk(Tables T, TrArgs C, EvalState D, Bal4* bb, WalkArgs W) {
+    __shared__ WalkRec rec[64];
+    __shared__ Bal4 pre[64][2];          // the staged balances of each event's two sides
+    __shared__ u32 ctag[WK_CACHE];
+    __shared__ Bal4 cval[WK_CACHE];
+    __shared__ u32 s_stop;
+    const u32 lane = threadIdx.x;
+    const PassGate G{nullptr, nullptr, 0};
+    u32 undo_n = 0;
+    bool broken = false;
+    if (lane == 0) {
+        W.out[0] = NONE32;
+        s_stop = 0;
+    }
+    // a per-block bitmap of the segments moved in this block: their staged balances are stale
+    u64 moved[16];
+    for (u32 b0 = W.start; b0 < C.n; b0 += 64) {
+        {  // stage the block's events
+            const u32 i = b0 + lane;
+            if (i < C.n) {
+                WalkRec r;
+                r.core = C.core[i];
+                r.ep = C.sd.epos[i];
+                r.cs = C.cs[i];
+                r.ce = C.ce[i];
+                r.pid = C.prev_id[i];
+                r.pre_e = C.pre_e[i];
+                r.sr = C.sres[i];
+                r.s0d = W.sstart[r.ep.x];
+                r.s0c = W.sstart[r.ep.y];
+                rec[lane] = r;
+                if (r.sr == SRES_DYN && !(r.core.flags & (TF_POST | TF_VOID))) {
+                    pre[lane][0] = wk_load(&W.wbal[r.s0d]);
+                    pre[lane][1] = wk_load(&W.wbal[r.s0c]);
+                }
+            }
+            if (b0 == W.start) ctag[lane] = NONE32;
+        }
+        __syncthreads();
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < 16; k++) moved[k] = 0;
+            auto read_bal = [&](u32 s0, u32 k, int side) -> Bal4 {
+                const u32 c = s0 % WK_CACHE;
+                if (ctag[c] == s0) return cval[c];
+                if (moved[(s0 >> 6) & 15] >> (s0 & 63) & 1) return wk_load(&W.wbal[s0]);
+                return pre[k][side];
+            };
+            auto write_bal = [&](u32 s0, const Bal4& v) {
+                const u32 c = s0 % WK_CACHE;
+                ctag[c] = s0;
+                cval[c] = v;
+                moved[(s0 >> 6) & 15] |= 1ull << (s0 & 63);
+                W.wbal[s0] = v;  // write-through: an evicted segment is read back from memory
+            };
+            auto move = [&](u32 s0, const Bal4& old, bool chain, const Bal4& nv) -> bool {
+                if (chain) {  // the scope's undo log
+                    if (undo_n + 1 > W.undo_cap) return false;
+                    W.undo_slot[undo_n] = s0;
+                    W.undo_val[undo_n++] = old;
+                }
+                write_bal(s0, nv);
+                return true;
+            };
+            const u32 kn = min(64u, C.n - b0);
+            for (u32 k = 0; k < kn; k++) {
+                const u32 i = b0 + k;
+                const WalkRec& R = rec[k];
+                const bool chain = R.cs != R.ce;
+                if (chain && i == R.cs) {  // scope_open (:1022-1026)
+                    undo_n = 0;
+                    broken = false;
+                }
+                const bool pv = R.sr == SRES_DYN && (R.core.flags & (TF_POST | TF_VOID));
+                if (chain && broken) {
+                    // execute evaluates nothing after the break: linked_event_failed (tr_mask)
+                    D.res[i] = TBGPU_CREATE_TRANSFER_LINKED_EVENT_FAILED;
+                    D.ok[i] = 0;
+                    D.amt[i] = 0;
+                    D.pamt[i] = 0;
+                    D.pref[i] = NONE32;
+                } else if (R.sr == SRES_DYN && !pv && R.pid == NONE32 && R.pre_e == NONE32) {
+                    // a transfer whose id nothing before it holds: create_transfer's balance tail
+                    const Bal4 bd = read_bal(R.s0d, k, 0), bc = read_bal(R.s0c, k, 1);
+                    bb[R.ep.x] = bd;  // the balances it saw (history rows, tr_apply)
+                    bb[R.ep.y] = bc;
+                    u128 amount = 0;
+                    const u8 res = eval_balances(R.core, bd, bc, &amount);
+                    const bool ok = res == TBGPU_CREATE_TRANSFER_OK;
+                    D.res[i] = res;
+                    D.ok[i] = ok ? 1 : 0;
+                    D.amt[i] = ok ? amount : 0;
+                    D.pamt[i] = 0;
+                    D.pref[i] = NONE32;
+                    const u128 dpe = ok && (R.core.flags & TF_PENDING) ? amount : 0;
+                    const u128 dpo = ok && !(R.core.flags & TF_PENDING) ? amount : 0;
+                    write_sides(C, i, false, ok, NONE32, dpe, dpo);
+                    if (ok) {
+                        Bal4 nd = bd, nc = bc;
+                        nd.dp += dpe; nd.dpo += dpo;
+                        nc.cp += dpe; nc.cpo += dpo;
+                        if (!move(R.s0d, bd, chain, nd) || !move(R.s0c, bc, chain, nc)) {
+                            W.out[1] = 1;
+                            s_stop = 1;
+                            break;
+                        }
+                    } else if (chain) {
+                        if (D.cfail[R.cs] == NONE32) D.cfail[R.cs] = i;
+                        broken = true;
+                    }
+                } else {
+                    // everything else (repeated ids, post/void, static failures): evaluate_one
+                    // against the walked state (every predecessor final in D)
+                    u32 s0d = NONE32, s0c = NONE32;
+                    Bal4 bd{}, bc{};
+                    if (R.sr == SRES_DYN && !pv) {
+                        s0d = R.s0d;
+                        s0c = R.s0c;
+                        bd = read_bal(s0d, k, 0);
+                        bc = read_bal(s0c, k, 1);
+                        bb[R.ep.x] = bd;
+                        bb[R.ep.y] = bc;
+                    }
+                    evaluate_one(T, C, D, D, bb, G, i);
+                    const bool ok = D.ok[i] & 1;
+                    u128 dpe, dpo;
+                    state_deltas(C, D, i, &dpe, &dpo);
+                    if (R.sr == SRES_DYN && !write_sides(C, i, pv, ok, D.pref[i], dpe, dpo)) {
+                        W.out[0] = R.cs;  // its pending lies outside its sides: rebuild them, walk on from its chain
+                        s_stop = 1;
+                        break;
+                    }
+                    if (ok && R.sr == SRES_DYN) {
+                        if (pv) {
+                            for (u32 s = C.sd.soff[i]; s < C.sd.soff[i + 1]; s += 2)
+                                if (C.sd.scand[s] == D.pref[i]) {
+                                    s0d = W.sstart[C.sd.spos[s]];
+                                    s0c = W.sstart[C.sd.spos[s + 1]];
+                                    break;
+                                }
+                            if (s0d != NONE32) {
+                                const u32 cd = s0d % WK_CACHE, cc = s0c % WK_CACHE;
+                                bd = ctag[cd] == s0d ? cval[cd] : wk_load(&W.wbal[s0d]);
+                                bc = ctag[cc] == s0c ? cval[cc] : wk_load(&W.wbal[s0c]);
+                            }
+                        }
+                        if (s0d != NONE32) {
+                            Bal4 nd = bd, nc = bc;
+                            nd.dp += dpe; nd.dpo += dpo;
+                            if (s0c == s0d) nc = nd;
+                            nc.cp += dpe; nc.cpo += dpo;
+                            if (!move(s0d, bd, chain, nd) || !move(s0c, s0c == s0d ? nd : bc, chain, nc)) {
+                                W.out[1] = 1;
+                                s_stop = 1;
+                                break;
+                            }
+                        }
+                    } else if (!ok && chain) {
+                        broken = true;
+                    }
+                }
+                if (chain && i == R.ce && (broken || (C.ctl && (C.ctl[R.ce] & TBGPU_CTL_DOOM)))) {
+                    while (undo_n) {  // scope_close(.discard): the chain's balance moves, newest first
+                        undo_n--;
+                        const u32 s0 = W.undo_slot[undo_n];
+                        write_bal(s0, W.undo_val[undo_n]);
+                    }
+                }
+            }
+            // the block's stores before the next block's staged loads
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        }
+        __syncthreads();
+        if (s_stop) return;
+    }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------ launchers ----
@@ -1115,8 +1507,8 @@ void tr_launch_group(const TrArgs& C, u32 kind, hipStream_t stream) {
     tr_grp_rank<<<GRID(C.n)>>>(C, kind);
 }
 void tr_launch_group2(const TrArgs& C, hipStream_t stream) { tr_group2<<<GRID(C.n)>>>(C); }
-void tr_launch_init(const Tables& T, const TrArgs& C, const EvalState& D, hipStream_t stream) {
-    tr_init<<<GRID(C.n)>>>(T, C, D);
+void tr_launch_init(const Tables& T, const TrArgs& C, const EvalState& D, const EvalState& D2, hipStream_t stream) {
+    tr_init<<<GRID(C.n)>>>(T, C, D, D2);
 }
 void tr_launch_side_count(const TrArgs& C, const EvalState& S, u32 kmax, u8* mask, hipStream_t stream) {
     tr_side_count<<<GRID(C.n)>>>(C, S, kmax, mask);
@@ -1133,11 +1525,28 @@ void tr_launch_side_rec(const TrArgs& C, const EvalState& S, hipStream_t stream)
     tr_side_rec<<<GRID(C.n)>>>(C, S);
 }
 void tr_launch_evaluate(const Tables& T, const TrArgs& C, const EvalState& S, const EvalState& D, const Bal4* bb,
-                        const PassGate& g, u32* chg, u32* chg_next, hipStream_t stream) {
-    tr_evaluate<<<GRID(C.n)>>>(T, C, S, D, bb, g, chg, chg_next);
+                        const PassGate& g, u32* chg, u32* chg_next, u32* front, u32* front_next, hipStream_t stream) {
+    tr_evaluate<<<GRID(C.n)>>>(T, C, S, D, bb, g, chg, chg_next, front, front_next);
+}
+void tr_launch_lists(const TrArgs& C, hipStream_t stream) { tr_lists<<<GRID(C.n)>>>(C); }
+void tr_launch_evaluate_lists(const Tables& T, const TrArgs& C, const EvalState& S, const EvalState& D, const Bal4* bb,
+                              const PassGate& g, u32* chg, u32* chg_next, u32* front, u32* front_next, u32 n_simple,
+                              u32 n_complex, hipStream_t stream) {
+    // the simple kernel always runs (it clears the next pass's words)
+    tr_eval_simple<<<GRID(std::max<u32>(n_simple, 1))>>>(C, S, D, bb, g, n_simple, chg, chg_next, front, front_next);
+    if (n_complex) tr_eval_complex<<<GRID(n_complex)>>>(T, C, S, D, bb, g, n_complex, chg, front);
 }
 void tr_launch_mask(const Tables& T, const TrArgs& C, const EvalState& S, u8* fres, u8* mask, hipStream_t stream) {
     tr_mask<<<GRID(C.n)>>>(T, C, S, fres, mask);
+}
+void tr_launch_walk_prep(const TrArgs& C, u64 m, u32 start, u32* sstart, u32* cfail, hipStream_t stream) {
+    tr_walk_prep<<<GRID(std::max<u64>(m, C.n))>>>(C, m, start, sstart, cfail);
+}
+void tr_launch_walk(const Tables& T, const TrArgs& C, const EvalState& D, Bal4* bb, u64 m, const u32* sstart,
+                    Bal4* wbal, u32* undo_slot, Bal4* undo_val, u32 undo_cap, u32 start, u32* out, hipStream_t stream) {
+    if (m) tr_walk_init<<<GRID(m)>>>(C, m, start, sstart, bb, wbal);
+    WalkArgs W{sstart, wbal, undo_slot, undo_val, undo_cap, start, out};
+    tr_walk<<<1, 64, 0, stream>>>(T, C, D, bb, W);
 }
 void tr_launch_apply(const Tables& T, const TrArgs& C, const EvalState& S, const u8* fres, const uint4* rk,
                      const Bal4* bb, tbgpu_create_transfers_result_t* results, u32* counts, u64* part,

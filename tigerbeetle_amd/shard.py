@@ -276,6 +276,8 @@ class ShardedStateMachine:
         run to their fixed point, and past `max_rounds` the step goes to the exact
         router (create_transfers), which settles one cross-shard chain at a time.
         Anything else goes through create_transfers too."""
+        if self._single_rank(events):
+            return self._single_rank_step(events, counts)
         st = self.route_device(events, counts)
         if st.fallback:
             return self._host_step(st.ev, st.counts, st.offs_h)
@@ -291,6 +293,12 @@ class ShardedStateMachine:
         create_transfers_device's (the results do not depend on the overlap)."""
         it = iter(steps)
         nxt = next(it, None)
+        if nxt is not None and self._single_rank(nxt[0]):
+            # one rank: nothing to exchange, so nothing to overlap
+            while nxt is not None:
+                yield self._single_rank_step(*nxt)
+                nxt = next(it, None)
+            return
         st = self.route_device(*nxt) if nxt is not None else None
         if st is not None and not st.fallback:
             self.exchange_device(st)
@@ -313,6 +321,42 @@ class ShardedStateMachine:
                 self.exchange_device(st2)
             yield self.finish_routed(st)
             st = st2
+
+    def _single_rank(self, events) -> bool:
+        """One rank owns every ledger: the step is the engine's own streamed call."""
+        return self.world == 1 and getattr(events, "is_cuda", False) and \
+            hasattr(self.backend, "create_transfers_batches_device")
+
+    def _single_rank_step(self, events, counts):
+        """A one-rank group owns every ledger, so routing is the identity: the step is
+        one tbgpu_create_transfers_batches_device call over the rank's batches in
+        their order (the same global order, the same timestamps T_g - n_g + i + 1;
+        the engine is the whole state machine, so repeated or non-monotone ids and
+        post/void need no directory either).  Returns this rank's replies."""
+        torch = self.comm.torch
+        clock = self._clock()
+        cnt = np.asarray(list(map(int, counts)), dtype=np.int64)
+        n = int(cnt.sum())
+        T = self.prepare_timestamp + np.cumsum(cnt + 1)
+        if len(T):
+            self.prepare_timestamp = int(T[-1])
+        ev = events.view(torch.uint8).reshape(-1)[:n * 128]
+        res = torch.empty(max(n, 1) * 8, dtype=torch.uint8, device=ev.device)
+        torch.cuda.current_stream(ev.device).synchronize()  # the engine runs on its own stream
+        clock("order_ms")
+        total, rc = self.backend.create_transfers_batches_device(T.astype(np.uint64), cnt.astype(np.uint32),
+                                                                 ev.data_ptr(), res.data_ptr())
+        clock("commit_ms")
+        out = res[:int(total) * 8].cpu().numpy().view(RESULT_DTYPE) if total else np.zeros(0, RESULT_DTYPE)
+        replies, off = [], 0
+        for k in rc.tolist():
+            replies.append(out[off:off + k].copy() if k else _NO_REPLIES)
+            off += k
+        # (max_id, the multi-rank device step's id filter, is never read on one rank)
+        self.commit_timestamp = self.backend.commit_timestamp()
+        self.stats["steps"] += 1
+        clock("replies_ms")
+        return replies
 
     def _host_step(self, ev, counts, offs_h):
         host = ev.cpu().numpy().view(TRANSFER_DTYPE)

@@ -792,7 +792,12 @@ static void walk(tbgpu_ctx* c, const TrArgs& C, u32 n, EvalState& D, const u32* 
         u32 out[2];
         memcpy(out, c->h_base + 4, sizeof out);
         if (out[1]) tbgpu_fatal("create_transfers", "walk: a linked chain's undo log overflowed", __FILE__, __LINE__);
-        if (out[0] == NONE32) break;
+        if (out[0] == NONE32) {
+            // the balances every side sees in the walked state, as a converged pass leaves
+            // them for the apply kernels (bs_final's account balances, history rows)
+            side_scan(SA, m, (u32)c->accounts_max, true, c->side_tiles, c->T.acc, c->bb, s);
+            break;
+        }
         // a post/void resolved to a pending outside its sides: rebuild them from D
         // (its resolution is then a candidate) and walk on from its chain
         HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)(c->counters + CNT_RESORT), 0, 1, s));
@@ -863,6 +868,7 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
     const bool chains = true;  // whether the call has chains is on the device: scan with the chain part
     u32 p = 0;                  // next pass to enqueue
     u32 group = std::max<u32>(2, std::min<u32>(c->last_passes, PASS_GROUP_MAX));
+    if (c->opt.flags & TBGPU_OPT_WALK_EARLY) group = 2;  // (tests) the walk after the first two passes
     u32 done_at = NONE32;
     for (;;) {
         if (p > n + 2 + PC_RING) tbgpu_fatal("create_transfers", "fixed point did not converge", __FILE__, __LINE__);

@@ -161,19 +161,24 @@ __global__ __launch_bounds__(RT_THREADS) void rt_rank(RouteArgs A) {
     }
 }
 
-// Exclusive scan of blk (owner-major) in one workgroup, and the per-owner totals:
-// tiles of 4096 words, four consecutive words per thread (coalesced), wave scans by
-// shuffles, the sixteen wave sums through LDS, a running carry.
+// Exclusive scan of blk (owner-major), one workgroup per owner row: row o's
+// exclusive prefix in place and its total in counts[o] (the owner offsets, an
+// exclusive scan of the totals, are summed by the scatter itself).  Tiles of 4096
+// words, four consecutive words per thread (coalesced), wave scans by shuffles, the
+// sixteen wave sums through LDS, a running carry.  (One workgroup over every row was a
+// serial tail of the step at eight ranks: 256k words.)
 __global__ __launch_bounds__(1024) void rt_scan(RouteArgs A) {
     __shared__ u32 wsum[16];
-    const u64 total_n = (u64)A.world * A.nblk;
+    const u32 o = blockIdx.x;
+    u32* row = A.blk + (u64)o * A.nblk;
+    const u64 total_n = A.nblk;
     const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     u64 carry = 0;
     for (u64 base = 0; base < total_n; base += 4096) {
         const u64 k = base + (u64)tid * 4;
         u32 v[4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) v[j] = k + j < total_n ? A.blk[k + j] : 0u;
+        for (int j = 0; j < 4; j++) v[j] = k + j < total_n ? row[k + j] : 0u;
         const u32 s = v[0] + v[1] + v[2] + v[3];
         u32 x = s;  // inclusive over the wave
         for (int off = 1; off < 64; off <<= 1) {
@@ -194,18 +199,13 @@ __global__ __launch_bounds__(1024) void rt_scan(RouteArgs A) {
         u32 run = (u32)carry + (wave ? wsum[wave - 1] : 0) + x - s;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            if (k + j < total_n) A.blk[k + j] = run;
+            if (k + j < total_n) row[k + j] = run;
             run += v[j];
         }
         carry += wsum[15];
         __syncthreads();
     }
-    __syncthreads();
-    for (u32 o = tid; o < A.world; o += 1024) {
-        const u64 s0 = A.blk[(u64)o * A.nblk];
-        const u64 t = o + 1 < A.world ? A.blk[(u64)(o + 1) * A.nblk] : carry;
-        A.counts[o] = t - s0;
-    }
+    if (tid == 0) A.counts[o] = carry;
 }
 
 // The scatter.  The workgroup's 256 rows are staged in LDS by coalesced 16-byte loads
@@ -222,8 +222,16 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scatter(RouteArgs A) {
     __shared__ u64 s_rec[RT_THREADS];
     __shared__ u32 s_b0;
     __shared__ u8 s_sel[32];                 // the packed row's word k is row word s_sel[k]
+    __shared__ u32 s_obase[256];             // each owner's first row: exclusive scan of the owner totals
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const u32 blk0 = blockIdx.x * RT_THREADS;
+    if (tid == 0) {
+        u32 acc = 0;
+        for (u32 o = 0; o < A.world; o++) {
+            s_obase[o] = acc;
+            acc += (u32)A.counts[o];
+        }
+    }
     const u64 i = (u64)blk0 + tid;
     const u64 wbase = i - lane;
     if (tid == 0) {
@@ -261,7 +269,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scatter(RouteArgs A) {
     }
     __syncthreads();
     if (v) {
-        const u32 dst = A.blk[(u64)orr.x * A.nblk + blockIdx.x] + orr.y;
+        const u32 dst = s_obase[orr.x] + A.blk[(u64)orr.x * A.nblk + blockIdx.x] + orr.y;
         s_dst[tid] = dst;
         // the record: position, chain start, span / end bits, global batch
         u32 b = s_b0;
@@ -554,7 +562,8 @@ void route_scatter(const Transfer* ev, u64 n, u32 world, u32 nb, const u32* b_st
     A.orank = orank; A.blk = blk; A.nblk = (u32)route_block_count(n); A.counts = counts;
     A.out_ev = out_ev; A.out_side = out_side;
     if (n && !ranked) rt_rank<<<A.nblk, RT_THREADS, 0, stream>>>(A);
-    rt_scan<<<1, 1024, 0, stream>>>(A);
+    if (world > 256) tbgpu_fatal("route_scatter", "more than 256 owners", __FILE__, __LINE__);
+    rt_scan<<<world, 1024, 0, stream>>>(A);
     if (n) rt_scatter<<<A.nblk, RT_THREADS, 0, stream>>>(A);
     HIP_CHECK(hipGetLastError());
 }

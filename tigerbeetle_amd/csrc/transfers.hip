@@ -1272,19 +1272,11 @@ struct WalkRec {
 };
 constexpr int WK_CACHE = 64;  // recently moved balances, direct-mapped by segment start
 
-// u128 words read past the vector L1 (the walking lane's own recent stores are in L2)
-__device__ __forceinline__ Bal4 wk_load(const Bal4* p) {
-    const u64* w = (const u64*)p;
-    u64 v[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) v[k] = __hip_atomic_load(&w[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    Bal4 b;
-    b.dp = (u128)v[1] << 64 | v[0];
-    b.dpo = (u128)v[3] << 64 | v[2];
-    b.cp = (u128)v[5] << 64 | v[4];
-    b.cpo = (u128)v[7] << 64 | v[6];
-    return b;
-}
+// The walk's balances: written by the walking lane, read back by it and (staged) by
+// the wave's other lanes after the workgroup barrier -- plain accesses, which the
+// barrier orders within the workgroup (one CU, one L1).  (L1-bypassing loads read L2
+// before the walking lane's write-through stores had reached it.)
+__device__ __forceinline__ Bal4 wk_load(const Bal4* p) { return *p; }
 
 __global__ __launch_bounds__(64) void tr_walk(Tables T, TrArgs C, EvalState D, Bal4* bb, WalkArgs W) {
     __shared__ WalkRec rec[64];
@@ -1455,10 +1447,8 @@ __global__ __launch_bounds__(64) void tr_walk(Tables T, TrArgs C, EvalState D, B
                     }
                 }
             }
-            // the block's stores before the next block's staged loads
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         }
-        __syncthreads();
+        __syncthreads();  // the block's stores before the next block's staged loads
         if (s_stop) return;
     }
 }

@@ -11,7 +11,7 @@ import subprocess
 import numpy as np
 
 from tigerbeetle_amd.types import (ACCOUNT_DTYPE, BALANCE_DTYPE, FILTER_DTYPE, HISTORY_DTYPE, QUERY_MAX,
-                                   RESULT_DTYPE, TRANSFER_DTYPE, U64_MAX, u128_array)
+                                   RESULT_DTYPE, TRANSFER_DTYPE, U128_DTYPE, U64_MAX, u128_array)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "liboracle.so")
@@ -179,7 +179,7 @@ class Oracle:
         return out[:n].copy()
 
     def lookup_transfers(self, ids) -> np.ndarray:
-        q = u128_array(list(ids))
+        q = ids if isinstance(ids, np.ndarray) and ids.dtype == U128_DTYPE else u128_array(list(ids))
         out = np.zeros(max(len(q), 1), dtype=TRANSFER_DTYPE)
         n = self._L.orc_lookup_transfers(self._h, _ptr(q), len(q), _ptr(out))
         return out[:n].copy()

@@ -172,3 +172,32 @@ def config4_failing(seed: int, world: int, steps: int, batches_per_rank: int, ba
         out.append(b)
     sw.batches = out
     return sw
+
+
+def random_u128_ids(sw: ShardWorkload, seed: int) -> ShardWorkload:
+    """The same workload with every transfer id (and every pending id naming one) mapped
+    through a random bijection into the whole u128 space: ids neither rise along the
+    global order nor fit 64 bits (the general step's directory, not the fast step's
+    key-range filter, decides every `exists` and every pending)."""
+    rng = np.random.default_rng(seed)
+    vals = set()
+    for b in sw.batches:
+        for f in ("id", "pending_id"):
+            v = (b[f + "_hi"].astype(object) << 64) | b[f + "_lo"].astype(object)
+            vals.update(int(x) for x in v if x)
+    vals = sorted(vals)
+    out = set()
+    while len(out) < len(vals):
+        out.add((int(rng.integers(1, 1 << 63)) << 65) ^ int(rng.integers(1, 1 << 63)))
+    m = dict(zip(vals, rng.permutation(sorted(out)).tolist()))
+    batches = []
+    for b in sw.batches:
+        b = b.copy()
+        for f in ("id", "pending_id"):
+            v = (b[f + "_hi"].astype(object) << 64) | b[f + "_lo"].astype(object)
+            new = [m.get(int(x), 0) for x in v]
+            b[f + "_lo"] = np.array([x & 0xFFFFFFFFFFFFFFFF for x in new], dtype=np.uint64)
+            b[f + "_hi"] = np.array([x >> 64 for x in new], dtype=np.uint64)
+        batches.append(b)
+    sw.batches = batches
+    return sw

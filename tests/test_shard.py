@@ -18,7 +18,7 @@ import pytest
 
 import oracle
 from tigerbeetle_amd.types import TRANSFER_DTYPE
-from tests.shard_workload import ShardWorkload, config4_failing, config4_small
+from tests.shard_workload import ShardWorkload, config4_failing, config4_small, random_u128_ids
 
 
 def _free_port() -> int:
@@ -37,7 +37,7 @@ def _backend(kind, w):
     return oracle.Oracle(len(w.accounts), 1 << 14)
 
 
-def _worker(rank, world, port, out_dir, spec, kind="oracle", device_step=False, max_rounds=None):
+def _worker(rank, world, port, out_dir, spec, kind="oracle", device_step=False, max_rounds=None, vectorized=True):
     import torch.distributed as dist
     from tigerbeetle_amd.shard import Comm, ShardedStateMachine
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -48,6 +48,7 @@ def _worker(rank, world, port, out_dir, spec, kind="oracle", device_step=False, 
         sm = ShardedStateMachine(_backend(kind, w), Comm(rank, world))
         if max_rounds is not None:
             sm.max_rounds = max_rounds
+        sm.vectorized = vectorized
         acc_replies = sm.create_accounts(w.account_batches if rank == 0 else [])
         replies = []
         if device_step == "stream":
@@ -85,16 +86,18 @@ def _make(spec):
     kind, seed, world, steps, B = spec
     if kind == "mix":
         return ShardWorkload(seed, world, steps, B)
+    if kind == "mixr":
+        return random_u128_ids(ShardWorkload(seed, world, steps, B), seed)
     if kind in ("c4f", "c4l"):
         return config4_failing(seed, world, steps, B, limits=kind == "c4l")
     return config4_small(seed, world, steps, B)
 
 
-def _check(spec, world, kind="oracle", device_step=False, max_rounds=None):
+def _check(spec, world, kind="oracle", device_step=False, max_rounds=None, vectorized=True):
     import torch.multiprocessing as mp
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d, spec, kind, device_step, max_rounds), nprocs=world,
-                 join=True)
+        mp.spawn(_worker, args=(world, _free_port(), d, spec, kind, device_step, max_rounds, vectorized),
+                 nprocs=world, join=True)
         outs = [pickle.load(open(os.path.join(d, f"r{r}.pkl"), "rb")) for r in range(world)]
     return verify(_make(spec), outs, world)
 
@@ -201,3 +204,20 @@ def test_device_step_pipelined_fallback_keeps_router_state():
     decision, so its timestamps and id filter follow the fallen-back step."""
     stats = _check(("c4l", 57, 2, 4, 2), 2, device_step="stream", max_rounds=1)
     assert stats["device_fallbacks"] > 0
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_general_step_random_u128_ids(world):
+    """The flag-heavy mix (two-phase across steps and ranks, balancing, limits, chains
+    across ledgers, repeated ids) with random u128 ids through the device step: every
+    step takes the general step (shard_vec.round_vec: array directory, routing and
+    commit, tensor collectives), bit-exact against the single state machine."""
+    stats = _check(("mixr", 71 + world, world, 3, 2), world, device_step=True)
+    assert stats["steps"] > 0 and stats["dry_rounds"] > 0
+
+
+@pytest.mark.parametrize("spec", [("mix", 81, 2, 3, 2), ("mixr", 82, 3, 2, 2)])
+def test_reference_router_still_exact(spec):
+    """shard.py _round (the event-by-event statement of the general step) against the
+    same oracle: it stays the reference that round_vec is checked against."""
+    _check(spec, spec[2], vectorized=False)

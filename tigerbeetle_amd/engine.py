@@ -13,7 +13,7 @@ import re
 import numpy as np
 
 from .types import (ACCOUNT_DTYPE, BALANCE_DTYPE, FILTER_DTYPE, HISTORY_DTYPE, QUERY_MAX, RESULT_DTYPE,
-                    TRANSFER_DTYPE, U64_MAX, u128_array)
+                    TRANSFER_DTYPE, U128_DTYPE, U64_MAX, u128_array)
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
@@ -388,7 +388,7 @@ class Engine:
         return out[:n].copy()
 
     def lookup_transfers(self, ids) -> np.ndarray:
-        q = u128_array(list(ids))
+        q = ids if isinstance(ids, np.ndarray) and ids.dtype == U128_DTYPE else u128_array(list(ids))
         out = np.zeros(max(len(q), 1), dtype=TRANSFER_DTYPE)
         n = self._L.tbgpu_lookup_transfers(self._h, _ptr(q), len(q), _ptr(out))
         return out[:n].copy()

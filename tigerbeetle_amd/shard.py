@@ -158,7 +158,11 @@ class ShardedStateMachine:
         self.backend = backend
         self.comm = comm
         self.rank, self.world = comm.rank, comm.world
+        self._ledger_mod = owner_of_ledger is None
         self.owner_of_ledger = owner_of_ledger or (lambda ledger: int(ledger) % self.world)
+        # the general step's rounds over whole arrays (shard_vec.round_vec); False: the
+        # event-by-event reference form (_round), kept for the tests
+        self.vectorized = True
         self.prepare_timestamp = 0
         self.commit_timestamp = 0
         self.max_id = 0         # every transfer id seen so far is <= this (the fast step's id filter)
@@ -172,6 +176,13 @@ class ShardedStateMachine:
                        "commit_ms": 0.0, "replies_ms": 0.0}
         self.stats = {"steps": 0, "splits": 0, "dry_rounds": 0, "cross_chains": 0, "imports": 0,
                       "preruns": 0, "serial_fallbacks": 0, "device_fallbacks": 0}
+
+    def owners_vec(self, ledgers) -> np.ndarray:
+        """owner_of_ledger over an array of ledgers."""
+        led = np.asarray(ledgers).astype(np.int64)
+        if self._ledger_mod:
+            return led % self.world
+        return np.array([self.owner_of_ledger(int(x)) for x in led.tolist()], dtype=np.int64)
 
     def note_accounts(self, accounts: np.ndarray) -> None:
         """Record the balance-limited accounts among `accounts` (every rank sees every
@@ -241,7 +252,11 @@ class ShardedStateMachine:
         start = (0, 0)  # resume point (global batch, index) after a hazard split
         while True:
             self.stats["steps"] += 1
-            split = self._round(glob, T, my_events, replies, start)
+            if self.vectorized:
+                from .shard_vec import round_vec
+                split = round_vec(self, glob, T, my_events, replies, start)
+            else:
+                split = self._round(glob, T, my_events, replies, start)
             if split is None:
                 break
             self.stats["splits"] += 1

@@ -1,0 +1,447 @@
+"""One round of the exact sharded router over whole arrays (shard.py `_round`'s
+algorithm, without per-event Python objects or pickled collectives).
+
+The router's general step is what takes every step the device fast
+step cannot: post/void whose pending may live on another shard
+(src/state_machine.zig:1391-1498), repeated ids (`:1284`), ids that are not strictly
+rising along the global order.  `ShardedStateMachine._round` states it event by event
+(dicts, sorted tuples, `all_gather_object` of pickled lists): the reference form, kept
+for the tests.  This module computes the same round with sorts, segment reductions
+and tensor collectives (`all_gather` / `all_to_all_single` of int64 rows over the
+step's communicator: RCCL on GPUs, gloo in the CPU tests), so that a general step
+costs O(events log events) array work per rank:
+
+1. directory: every rank's id and pending-id records (position, kind, key, route
+   hint) are all-gathered; the unique keys are looked up in each shard's engine
+   (the engines are the directory of committed ids) and the owners all-reduced;
+   a sort by (key, position) gives each key's first occurrence in the step;
+2. routing of this rank's events by the rules of `_round` (committed id -> its
+   holder, duplicate on the same owner or in the same chain -> follow, post/void ->
+   its pending's holder), chains filled to one owner where members can go anywhere,
+   and the earliest hazard over all ranks splits the step;
+3. imports of colliding committed rows, the exchange of the events to their owners,
+   the spanning chains, the dry rounds and their serial fallback, the commit, and
+   the replies back to their sources -- all as arrays.
+
+Results are bit-identical to `_round` (tests/test_shard.py runs both against one
+oracle fed the global order).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .types import RESULT_DTYPE, TRANSFER_DTYPE, U128_DTYPE
+
+POST_VOID = 4 | 8          # TransferFlags post_pending_transfer | void_pending_transfer
+LINKED = 1
+ANY, PV = -1, -2           # route hints (shard.py)
+NEW, EXISTS, DUP, PEND, PEND_NONE, PEND_HAZARD = range(6)
+CTL_CHAIN_END, CTL_SKIP, CTL_DOOM = 1, 2, 4
+LINKED_EVENT_FAILED = 1
+INF = np.iinfo(np.int64).max
+U64_MAX = np.uint64(0xFFFFFFFFFFFFFFFF)
+HL = np.dtype([("hi", "<u8"), ("lo", "<u8")])  # u128 in numeric order (structured compare)
+LOOKUP_CHUNK = 4096
+
+
+# ----------------------------------------------------------- collectives --
+def gather_rows(comm, rows: np.ndarray) -> tuple[np.ndarray, list[int]]:
+    """All-gather an int64 [k, w] array of every rank (k may differ): the rows of
+    rank 0, then rank 1, ...; and each rank's row count."""
+    torch, dist = comm.torch, comm.dist
+    w = rows.shape[1]
+    k = torch.tensor([rows.shape[0]], dtype=torch.int64, device=comm.device)
+    ks = [torch.empty_like(k) for _ in range(comm.world)]
+    dist.all_gather(ks, k, group=comm.group)
+    counts = [int(x.item()) for x in ks]
+    mx = max(max(counts), 1)
+    pad = np.zeros((mx, w), dtype=np.int64)
+    pad[:rows.shape[0]] = rows
+    t = torch.from_numpy(pad).to(comm.device)
+    outs = [torch.empty_like(t) for _ in range(comm.world)]
+    dist.all_gather(outs, t, group=comm.group)
+    return np.concatenate([o.cpu().numpy()[:c] for o, c in zip(outs, counts)]), counts
+
+
+def allreduce_max(comm, a: np.ndarray) -> np.ndarray:
+    torch, dist = comm.torch, comm.dist
+    t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.int64)).to(comm.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=comm.group)
+    return t.cpu().numpy()
+
+
+def alltoall_rows(comm, parts: list[np.ndarray], width: int) -> list[np.ndarray]:
+    """parts[d]: int64 [k_d, width] rows for rank d; returns the rows received, by source."""
+    got = comm.alltoallv([np.ascontiguousarray(p, dtype=np.int64).reshape(-1).view(np.uint8) for p in parts])
+    return [g.view(np.int64).reshape(-1, width) if len(g) else np.zeros((0, width), np.int64) for g in got]
+
+
+def alltoall_events(comm, parts: list[np.ndarray]) -> list[np.ndarray]:
+    got = comm.alltoallv([np.ascontiguousarray(p, dtype=TRANSFER_DTYPE).view(np.uint8).reshape(-1) for p in parts])
+    return [g.view(TRANSFER_DTYPE) if len(g) else np.zeros(0, TRANSFER_DTYPE) for g in got]
+
+
+def min_over_ranks(comm, v: int) -> int:
+    return -int(allreduce_max(comm, np.array([-v], dtype=np.int64))[0])
+
+
+# ------------------------------------------------------------------ keys --
+def _hl(lo: np.ndarray, hi: np.ndarray) -> np.ndarray:
+    k = np.zeros(len(lo), dtype=HL)
+    k["lo"] = lo
+    k["hi"] = hi
+    return k
+
+
+def lookup_owners(sm, keys: np.ndarray) -> np.ndarray:
+    """Collective.  For sorted unique u128 keys (HL), the shard that holds each as a
+    committed transfer (the owner of its row's ledger; imported copies answer the same),
+    or -1: every rank looks the keys up in its engine, the owners are all-reduced."""
+    own = np.full(len(keys), -1, dtype=np.int64)
+    q = np.zeros(len(keys), dtype=U128_DTYPE)
+    q["lo"], q["hi"] = keys["lo"], keys["hi"]
+    for c0 in range(0, len(keys), LOOKUP_CHUNK):
+        rows = sm.backend.lookup_transfers(q[c0:c0 + LOOKUP_CHUNK])
+        if len(rows):
+            at = np.searchsorted(keys, _hl(rows["id_lo"], rows["id_hi"]))
+            own[at] = sm.owners_vec(rows["ledger"])
+    return allreduce_max(sm.comm, own)
+
+
+def segment_first(starts: np.ndarray, n: int) -> np.ndarray:
+    """Index of each element's segment start (starts: bool[n], starts[0] True)."""
+    return np.maximum.accumulate(np.where(starts, np.arange(n), 0)) if n else np.zeros(0, np.int64)
+
+
+# ----------------------------------------------------------------- round --
+def round_vec(sm, glob, T, my_events, replies, start):
+    """ShardedStateMachine._round over arrays: the same routing, splits, dry rounds
+    and commit; returns None when the round committed every remaining event, else the
+    (global batch, index) to resume from."""
+    comm = sm.comm
+    W, me = sm.world, sm.rank
+    g0, i0 = start
+    P0 = (g0 << 32) | i0
+    # ---- 1. my remaining events, in global order
+    evs, Gs, Is = [], [], []
+    for g in sorted(my_events):
+        if g < g0:
+            continue
+        b = my_events[g]
+        lo = i0 if g == g0 else 0
+        if lo < len(b):
+            evs.append(b[lo:])
+            Gs.append(np.full(len(b) - lo, g, np.int64))
+            Is.append(np.arange(lo, len(b), dtype=np.int64))
+    E = np.concatenate(evs) if evs else np.zeros(0, TRANSFER_DTYPE)
+    G = np.concatenate(Gs) if Gs else np.zeros(0, np.int64)
+    I = np.concatenate(Is) if Is else np.zeros(0, np.int64)
+    n = len(E)
+    P = (G << 32) | I
+    flags = E["flags"].astype(np.int64)
+    pv = (flags & POST_VOID) != 0
+    linked = (flags & LINKED) != 0
+    # chain key (position of its first member): a run of linked events and the event
+    # that ends it, within one batch (execute, src/state_machine.zig:1018-1035)
+    cstart = np.ones(n, dtype=bool)
+    if n > 1:
+        cstart[1:] = (G[1:] != G[:-1]) | ~linked[:-1]
+    chain = P[segment_first(cstart, n)] if n else np.zeros(0, np.int64)
+
+    # ---- 2. directory
+    xlo, xhi = E["id_lo"], E["id_hi"]
+    plo, phi = E["pending_id_lo"], E["pending_id_hi"]
+    zero = lambda lo, hi: (lo == 0) & (hi == 0)
+    imax = lambda lo, hi: (lo == U64_MAX) & (hi == U64_MAX)
+    xval = ~(zero(xlo, xhi) | imax(xlo, xhi))
+    pval = pv & ~(zero(plo, phi) | imax(plo, phi) | ((plo == xlo) & (phi == xhi)))
+    led = E["ledger"].astype(np.int64)
+    own = np.where(led != 0, sm.owners_vec(led), ANY)
+    hint = np.where(pv, PV, own)
+    r0, r1 = np.nonzero(xval)[0], np.nonzero(pval)[0]
+    R = np.zeros((len(r0) + len(r1), 5), dtype=np.int64)
+    R[:len(r0), 0] = P[r0]
+    R[:len(r0), 2] = xlo[r0].view(np.int64)
+    R[:len(r0), 3] = xhi[r0].view(np.int64)
+    R[:len(r0), 4] = hint[r0]
+    R[len(r0):, 0] = P[r1]
+    R[len(r0):, 1] = 1
+    R[len(r0):, 2] = plo[r1].view(np.int64)
+    R[len(r0):, 3] = phi[r1].view(np.int64)
+    R[len(r0):, 4] = ANY
+    A, counts = gather_rows(comm, R)
+    keys = _hl(A[:, 2].view(np.uint64), A[:, 3].view(np.uint64))
+    order = np.argsort(keys, kind="stable")
+    ks = keys[order]
+    newk = np.ones(len(ks), dtype=bool)
+    if len(ks) > 1:
+        newk[1:] = ks[1:] != ks[:-1]
+    uid = np.empty(len(A), dtype=np.int64)
+    uid[order] = np.cumsum(newk) - 1
+    U = ks[newk]
+    cown = lookup_owners(sm, U)[uid] if len(U) else np.zeros(len(A), np.int64)
+    # the first occurrence of each key among the id records of ids not committed
+    k0 = A[:, 1] == 0
+    cand = k0 & (cown < 0)
+    firstP = np.full(len(U), INF, dtype=np.int64)
+    np.minimum.at(firstP, uid[cand], A[cand, 0])
+    firstH = np.full(len(U), ANY, dtype=np.int64)
+    isfirst = cand & (A[:, 0] == firstP[uid])
+    firstH[uid[isfirst]] = A[isfirst, 4]
+    fP, fH = firstP[uid], firstH[uid]
+    typ = np.where(k0, np.where(cown >= 0, EXISTS, np.where(isfirst, NEW, DUP)),
+                   np.where(cown >= 0, PEND, np.where(fP < A[:, 0],
+                                                       np.where((fH == ANY) | (fH == PV), PEND_HAZARD, PEND),
+                                                       PEND_NONE)))
+    ahint = np.where(cown >= 0, cown, fH)
+    off = sum(counts[:me])
+    mine_t, mine_h, mine_p = typ[off:off + len(R)], ahint[off:off + len(R)], fP[off:off + len(R)]
+    id_t = np.full(n, NEW, np.int64)
+    id_h = np.full(n, ANY, np.int64)
+    id_p = np.full(n, INF, np.int64)
+    id_t[r0], id_h[r0], id_p[r0] = mine_t[:len(r0)], mine_h[:len(r0)], mine_p[:len(r0)]
+    p_t = np.full(n, PEND_NONE, np.int64)
+    p_h = np.full(n, ANY, np.int64)
+    p_p = np.full(n, INF, np.int64)
+    p_t[r1], p_h[r1], p_p[r1] = mine_t[len(r0):], mine_h[len(r0):], mine_p[len(r0):]
+
+    # ---- 3. routing of my events (shard.py _round, rule for rule)
+    def same_chain(pos):
+        j = np.clip(np.searchsorted(P, pos), 0, max(n - 1, 0))
+        ok = (pos != INF) & (n > 0)
+        ok &= P[j] == pos if n else ok
+        return ok & (chain[j] == chain), j
+
+    route = np.full(n, ANY, dtype=np.int64)
+    follow = np.full(n, -1, dtype=np.int64)
+    hazard = np.zeros(n, dtype=bool)
+    # post/void
+    sc_p, jp = same_chain(p_p)
+    r_pv = np.where(p_t == PEND, p_h, ANY)
+    fol_pv = pv & (p_t == PEND_HAZARD) & sc_p
+    hazard |= pv & (p_t == PEND_HAZARD) & ~sc_p
+    follow = np.where(fol_pv, jp, follow)
+    sc_i, ji = same_chain(id_p)
+    dup_moves = pv & (id_t == DUP) & (fol_pv | (id_h != r_pv) | (id_h == ANY) | (id_h == PV))
+    follow = np.where(dup_moves & sc_i, ji, follow)
+    hazard |= dup_moves & ~sc_i
+    route = np.where(pv, r_pv, route)
+    # regular transfers
+    reg = ~pv
+    route = np.where(reg & (id_t == EXISTS), id_h, route)
+    route = np.where(reg & (id_t == NEW), own, route)
+    dup = reg & (id_t == DUP)
+    follow = np.where(dup & sc_i, ji, follow)
+    route = np.where(dup & ~sc_i, own, route)
+    hazard |= dup & ~sc_i & (id_h != ANY) & (own != ANY) & (id_h != own)
+    # follows (their targets are earlier members of the same chain)
+    for k in np.nonzero(follow >= 0)[0]:
+        route[k] = route[follow[k]]
+    # members that can go anywhere follow their chain's first member that cannot
+    if n:
+        seg = np.nonzero(cstart)[0]
+        firstfix = np.minimum.reduceat(np.where(route != ANY, np.arange(n), INF), seg)
+        fill = np.where(firstfix == INF, me, route[np.minimum(firstfix, n - 1)])
+        route = np.where(route == ANY, np.repeat(fill, np.diff(np.append(seg, n))), route)
+    # post/voids whose id is committed on another shard: that row, imported
+    imp = pv & (id_t == EXISTS) & (id_h != route)
+
+    # ---- 4. the earliest hazard over all ranks splits the step
+    hz = int(chain[np.nonzero(hazard)[0]].min()) if hazard.any() else INF
+    stop = min_over_ranks(comm, hz)
+    if stop <= P0:
+        sm.stats["serial_fallbacks"] += 1
+        nxt = INF
+        if n and P[0] == P0:
+            c = chain[0]
+            after = np.nonzero((chain != c) & (P > P0))[0]
+            nxt = int(P[after[0]]) if len(after) else int(((P[chain == c][-1] >> 32) + 1) << 32)
+        stop = min_over_ranks(comm, nxt)
+    loc = P < stop
+    _do_imports(sm, xlo[imp], xhi[imp], id_h[imp], route[imp])
+
+    # ---- 5. events to their owners (global order kept per source)
+    dest = route[loc]
+    parts, meta = [], []
+    for d in range(W):
+        s = np.nonzero(loc)[0][dest == d]
+        parts.append(E[s])
+        meta.append(np.stack([P[s], chain[s]], axis=1))
+    recv = alltoall_events(comm, parts)
+    rmeta = alltoall_rows(comm, meta, 2)
+    mE = np.concatenate(recv) if recv else np.zeros(0, TRANSFER_DTYPE)
+    mM = np.concatenate(rmeta) if rmeta else np.zeros((0, 2), np.int64)
+    o = np.argsort(mM[:, 0], kind="stable")
+    mE, mP, mC = mE[o], mM[o, 0], mM[o, 1]
+
+    # spanning chains (the source knows every member's owner) and their last members
+    lp, lc, lr = P[loc], chain[loc], route[loc]
+    span_rows = np.zeros((0, 2), np.int64)
+    if len(lp):
+        sstart = np.ones(len(lp), dtype=bool)
+        sstart[1:] = lc[1:] != lc[:-1]
+        seg = np.nonzero(sstart)[0]
+        rmin = np.minimum.reduceat(lr, seg)
+        rmax = np.maximum.reduceat(lr, seg)
+        last = np.maximum.reduceat(lp, seg)
+        sp = rmin != rmax
+        span_rows = np.stack([lc[seg][sp], last[sp]], axis=1)
+    allspan, _ = gather_rows(comm, span_rows)
+    so = np.argsort(allspan[:, 0], kind="stable") if len(allspan) else np.zeros(0, np.int64)
+    span_keys, span_last = allspan[so, 0], allspan[so, 1]
+    if me == 0:
+        sm.stats["cross_chains"] += len(span_keys)
+
+    # ---- 6. commit (dry rounds while chains span shards)
+    in_span = np.isin(mC, span_keys)
+    mG, mI = mP >> 32, mP & 0xFFFFFFFF
+    lastloc = np.ones(len(mP), dtype=bool)  # the owner's last local member of its chain
+    if len(mP):
+        co = np.lexsort((mP, mC))
+        islast = np.ones(len(co), dtype=bool)
+        islast[:-1] = mC[co][1:] != mC[co][:-1]
+        lastloc = np.zeros(len(mP), dtype=bool)
+        lastloc[co[islast]] = True
+    mlast = span_last[np.clip(np.searchsorted(span_keys, mC), 0, max(len(span_keys) - 1, 0))] \
+        if len(span_keys) else np.full(len(mP), -1, np.int64)
+    brk = {}        # chain key -> position of its first failure (global)
+    rounds = 0
+    mask = np.ones(len(mP), dtype=bool)   # the events of this round (a serial fallback cuts it)
+    while True:
+        res = _commit_vec(sm, T, glob, mE[mask], mP[mask], mG[mask], mI[mask], mC[mask], in_span[mask],
+                          lastloc[mask], mlast[mask], brk, dry=bool(len(span_keys)))
+        if not len(span_keys):
+            break
+        rounds += 1
+        sm.stats["dry_rounds"] += 1
+        nb = _breaks(sm, mP[mask], mC[mask], in_span[mask], res)
+        if nb == brk:
+            res2 = _commit_vec(sm, T, glob, mE[mask], mP[mask], mG[mask], mI[mask], mC[mask], in_span[mask],
+                               lastloc[mask], mlast[mask], brk, dry=False)
+            if not np.array_equal(res2, res):
+                raise RuntimeError("sharded commit: dry run and commit disagree (engine invariant)")
+            res = res2
+            break
+        if rounds >= sm.max_rounds:
+            head = int(mP[mask].min()) if mask.any() else INF
+            head = min_over_ranks(comm, head)
+            ks_ = span_keys
+            cut = int(ks_[0]) if ks_[0] > head else (int(ks_[1]) if len(ks_) > 1 else None)
+            if cut is not None:
+                mask &= mP < cut
+                keep = span_keys < cut
+                span_keys, span_last = span_keys[keep], span_last[keep]
+                in_span = np.isin(mC, span_keys)
+                stop = min(stop, cut)
+                sm.stats["serial_fallbacks"] += 1
+                brk, rounds = {}, 0
+                continue
+            if rounds >= sm.max_rounds + 2:
+                raise RuntimeError("sharded commit: a lone cross-shard chain did not settle "
+                                   "(its break depends on no other chain: an engine invariant failed)")
+        brk = nb
+
+    # ---- 7. replies to their sources
+    rp, rg, ri = mP[mask], mG[mask], mI[mask]
+    bad = res != 0
+    src = np.array([glob[int(g)][0] for g in rg[bad]], dtype=np.int64) if bad.any() else np.zeros(0, np.int64)
+    rows = np.stack([rg[bad], ri[bad], res[bad]], axis=1) if bad.any() else np.zeros((0, 3), np.int64)
+    for got in alltoall_rows(comm, [rows[src == d] for d in range(W)], 3):
+        for g, i, code in got.tolist():
+            replies[g].append((i, code))
+    top = 0
+    if mask.any():
+        ids = _hl(mE["id_lo"][mask], mE["id_hi"][mask])
+        m = np.sort(ids)[-1]
+        top = (int(m["hi"]) << 64) | int(m["lo"])
+    sm.max_id = max(sm.max_id, sm.comm.allreduce_max(top))
+    if stop == INF:
+        return None
+    return (int(stop) >> 32, int(stop) & 0xFFFFFFFF)
+
+
+def _do_imports(sm, lo, hi, holder, dest):
+    """Rows of committed ids requested by this rank for `dest` shards, shipped from their
+    holders and imported there (rows are immutable: importing early is harmless)."""
+    W = sm.world
+    req = np.stack([lo.view(np.int64), hi.view(np.int64), dest], axis=1) if len(lo) else np.zeros((0, 3), np.int64)
+    if len(req):
+        req = np.unique(np.concatenate([req, holder[:, None]], axis=1), axis=0)
+    got = alltoall_rows(sm.comm, [req[req[:, 3] == h, :3] for h in range(W)] if len(req) else
+                        [np.zeros((0, 3), np.int64)] * W, 3)
+    send = [[] for _ in range(W)]
+    for rows in got:
+        if not len(rows):
+            continue
+        q = np.zeros(len(rows), dtype=U128_DTYPE)
+        q["lo"], q["hi"] = rows[:, 0].view(np.uint64), rows[:, 1].view(np.uint64)
+        found = sm.backend.lookup_transfers(q)
+        if len(found) != len(np.unique(_hl(q["lo"], q["hi"]))):
+            raise RuntimeError("sharded commit: the directory names a shard that does not hold the transfer")
+        fk = _hl(found["id_lo"], found["id_hi"])
+        fo = np.argsort(fk, kind="stable")
+        rows_by_q = found[fo[np.searchsorted(fk[fo], _hl(q["lo"], q["hi"]))]]
+        for d in range(W):
+            sel = rows[:, 2] == d
+            if sel.any():
+                send[d].append(rows_by_q[sel])
+    recv = alltoall_events(sm.comm, [np.concatenate(s) if s else np.zeros(0, TRANSFER_DTYPE) for s in send])
+    rows = np.concatenate(recv) if recv else np.zeros(0, TRANSFER_DTYPE)
+    if len(rows):
+        _, first = np.unique(_hl(rows["id_lo"], rows["id_hi"]), return_index=True)
+        rows = rows[np.sort(first)]
+        sm.backend.import_transfers(rows)
+        sm.stats["imports"] += len(rows)
+
+
+def _commit_vec(sm, T, glob, E, P, G, I, C, in_span, lastloc, mlast, brk, dry):
+    """The owner's sub-batches (one per source batch, global order) with the chain
+    control of the round; returns each event's result code (0 = ok)."""
+    m = len(P)
+    if not m:
+        return np.zeros(0, np.int64)
+    q = np.full(m, INF, dtype=np.int64)
+    if brk:
+        bk = np.array(sorted(brk), dtype=np.int64)
+        bv = np.array([brk[k] for k in bk.tolist()], dtype=np.int64)
+        ix = np.clip(np.searchsorted(bk, C), 0, len(bk) - 1)
+        q = np.where(bk[ix] == C, bv[ix], INF)
+    ctl = np.zeros(m, dtype=np.uint8)
+    ctl[in_span & (q != INF) & (P > q)] |= CTL_SKIP
+    end = in_span & lastloc & (P != mlast)
+    ctl[end] |= CTL_CHAIN_END
+    ctl[end & (q != INF) & (P < q)] |= CTL_DOOM
+    gstart = np.ones(m, dtype=bool)
+    gstart[1:] = G[1:] != G[:-1]
+    seg = np.nonzero(gstart)[0]
+    counts = np.diff(np.append(seg, m))
+    n_g = np.array([glob[int(g)][2] for g in G[seg]], dtype=np.int64)
+    Tg = np.array([T[int(g)] for g in G[seg]], dtype=np.int64)
+    ts = (np.repeat(Tg - n_g, counts) + I + 1).astype(np.uint64)
+    out, rc, _ = sm.backend.create_transfers_routed(counts.astype(np.uint32), E, ts,
+                                                    ctl if ctl.any() else None, dry)
+    res = np.zeros(m, dtype=np.int64)
+    rc = rc.astype(np.int64)
+    if rc.sum():
+        rows = np.concatenate([np.arange(s, s + k) for s, k in zip(seg, rc) if k])
+        base = np.repeat(seg, rc)
+        res[base + out["index"][rows].astype(np.int64)] = out["result"][rows]
+    return res
+
+
+def _breaks(sm, P, C, in_span, res):
+    """The all-gathered first failing member of every cross-shard chain."""
+    v = in_span & (res != 0) & (res != LINKED_EVENT_FAILED)
+    rows = np.zeros((0, 2), np.int64)
+    if v.any():
+        c, p = C[v], P[v]
+        o = np.lexsort((p, c))
+        c, p = c[o], p[o]
+        first = np.ones(len(c), dtype=bool)
+        first[1:] = c[1:] != c[:-1]
+        rows = np.stack([c[first], p[first]], axis=1)
+    allr, _ = gather_rows(sm.comm, rows)
+    nb = {}
+    for c, p in allr.tolist():
+        nb[c] = min(nb.get(c, INF), p)
+    return nb

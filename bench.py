@@ -557,7 +557,15 @@ def main():
     n_transfers = n_batches * BATCH_MAX
     t_gen = time.time()
     c5 = None
-    if args.config == 5:
+    cache = os.environ.get("TB_BENCH_CACHE")  # diagnostics only: reuse a generated workload across runs
+    ckey = f"c{args.config}_{args.accounts}_{n_batches}_{42 + rank}"
+    if cache and args.config != 5 and os.path.exists(os.path.join(cache, ckey + ".npz")):
+        z = np.load(os.path.join(cache, ckey + ".npz"))
+        w = workload.Workload(str(z["name"]), z["accounts"], z["account_counts"], z["transfers"], z["transfer_counts"],
+                              ticks={int(k): int(v) for k, v in z["ticks"]})
+        acc_n = args.accounts or {1: 10_000, 2: 1_000_000, 3: 10_000, 4: 10_000_000}[args.config]
+        n_batches = len(w.transfer_counts)
+    elif args.config == 5:
         c5 = workload.config5(shard=rank, shards=8)
         acc_n = c5.accounts
         w = None
@@ -576,6 +584,11 @@ def main():
         acc_n = args.accounts or 10_000
         w = workload.config1(transfer_count=n_transfers, account_count=acc_n, seed=42 + rank)
     log(f"[rank {rank}] generated {n_transfers} transfers / {acc_n} accounts in {time.time() - t_gen:.1f}s")
+    if cache and w is not None and not os.path.exists(os.path.join(cache, ckey + ".npz")):
+        os.makedirs(cache, exist_ok=True)
+        np.savez(os.path.join(cache, ckey + ".npz"), name=w.name, accounts=w.accounts,
+                 account_counts=w.account_counts, transfers=w.transfers, transfer_counts=w.transfer_counts,
+                 ticks=np.array(sorted(w.ticks.items()), dtype=np.int64).reshape(-1, 2))
 
     dev = torch.device("cuda", local_rank)
     if c5 is not None:

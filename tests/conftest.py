@@ -7,6 +7,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 TESTS = os.path.dirname(os.path.abspath(__file__))
+# a fatal engine error aborts the process before pytest shows the captured stderr:
+# the engine also appends its message here (csrc/engine.hip tbgpu_fatal)
+os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+os.environ.setdefault("TBGPU_FATAL_LOG", os.path.join(ROOT, "gpurun_out", "tbgpu_fatal.log"))
 if TESTS not in sys.path:
     sys.path.insert(0, TESTS)
 

@@ -35,7 +35,7 @@ __device__ __forceinline__ u32 ac_gtab_insert(const AcArgs& C, u128 key, u32 i) 
     }
 }
 
-__device__ __forceinline__ u32 ac_classify_one(const Tables& T, const AcArgs& C, u32 i) {
+__device__ __forceinline__ u32 ac_classify_one(const Tables& T, const AcArgs& C, u32 i, bool dup_check) {
     const u32 b = ac_batch_of(C.b_start, C.nb, i);
     const u32 bs = C.b_start[b], be = C.b_start[b + 1];
     const u32 nbatch = be - bs, k = i - bs;
@@ -67,8 +67,10 @@ __device__ __forceinline__ u32 ac_classify_one(const Tables& T, const AcArgs& C,
     else {
         sres = SRES_DYN;
         pre = acc_probe(T.aidx, T.aidx_mask, a.id);
-        gslot = ac_gtab_insert(C, a.id, i);
-        atomicAdd(&C.gcnt_id[gslot], 1u);
+        if (dup_check) {  // ids that rise strictly through the call cannot repeat (ac_mono)
+            gslot = ac_gtab_insert(C, a.id, i);
+            atomicAdd(&C.gcnt_id[gslot], 1u);
+        }
     }
     C.sres[i] = sres;
     C.pre[i] = pre;
@@ -77,10 +79,21 @@ __device__ __forceinline__ u32 ac_classify_one(const Tables& T, const AcArgs& C,
     return fl;
 }
 
+// Whether the call's ids rise strictly from event to event (the benchmark's sequential
+// ids): then no id repeats and classify skips the call-local group table (a CAS and a
+// count atomic per account).  One flag atomic per workgroup that sees a descent.
+__global__ void ac_mono(AcArgs C) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool down = false;
+    if (i > 0 && i < C.n) down = !(C.ev[i].id > C.ev[i - 1].id);
+    if (__syncthreads_or(down) && threadIdx.x == 0) atomicOr(&C.counters[CNT_FLAGS], (u32)FL_NONMONO);
+}
+
 __global__ void ac_classify(Tables T, AcArgs C) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool dup_check = C.counters[CNT_FLAGS] & FL_NONMONO;
     u32 fl = 0;
-    if (i < C.n) fl = ac_classify_one(T, C, i);
+    if (i < C.n) fl = ac_classify_one(T, C, i, dup_check);
     fl = wave_or_u32(fl);  // one flag atomic per wave, not per chain member
     if (fl && wave_leader()) atomicOr(&C.counters[CNT_FLAGS], fl);
 }
@@ -326,6 +339,7 @@ void launch_rebuild_accounts(const Tables& T, u64 n, hipStream_t stream) {
 }
 
 void ac_launch_classify(const Tables& T, const AcArgs& C, hipStream_t stream) {
+    ac_mono<<<GRID(C.n)>>>(C);
     ac_classify<<<GRID(C.n)>>>(T, C);
     ac_group1<<<GRID(C.n)>>>(C);
 }

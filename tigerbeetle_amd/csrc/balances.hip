@@ -338,6 +338,24 @@ __global__ __launch_bounds__(BF_THREADS) void bs_fused(SideScanArgs A, u64 m, u3
         for (u64 k = (u64)blockIdx.x * BF_THREADS + threadIdx.x; k < A.n; k += (u64)gridDim.x * BF_THREADS)
             A.cfail_clear[k] = NONE32;
     const u32 t = blockIdx.x, tid = threadIdx.x;
+    // Dirty tracking (engine.h Dirty): everything at a chunk's first pass and after a
+    // side rebuild; otherwise only the windows whose side records moved last pass.
+    const u32 pq = A.gate.p, par = pq & 1;
+    const bool all = A.gate.full || *A.dt.all == pq;
+    if (!all) {
+        // the complex events whose id / pending groups moved last pass are due, with
+        // their chains (decided here, before any evaluation of this pass reads it)
+        for (u64 k = (u64)blockIdx.x * BF_THREADS + tid; k < A.n_complex; k += (u64)gridDim.x * BF_THREADS) {
+            const u32 i = A.lst_complex[k];
+            const u32 gs = A.gslot[i], ps = A.pslot[i];
+            if ((gs != NONE32 && A.dt.slot[par * A.dt.g + gs] == pq) ||
+                (ps != NONE32 && A.dt.slot[par * A.dt.g + ps] == pq)) {
+                A.dt.ev[par * A.dt.n + i] = pq;
+                const u32 cs = A.cs[i];
+                if (cs != A.ce[i]) A.dt.chain[par * A.dt.n + cs] = pq;
+            }
+        }
+    }
     const u32 a0 = tstart[t];
     if (a0 == NONE32) return;  // no account starts in this window: the previous tile has its sides
     u32 b0 = (u32)m;
@@ -346,6 +364,11 @@ __global__ __launch_bounds__(BF_THREADS) void bs_fused(SideScanArgs A, u64 m, u3
     if (b0 - a0 > BF_THREADS * BF_IPT) {  // an account longer than a window
         if (tid == 0) atomicMax(long_flag, A.gate.p + 1);
         return;
+    }
+    if (!all) {
+        bool due = false;
+        for (u32 w = a0 / BF_TILE; w <= (b0 - 1) / BF_TILE; w++) due |= A.dt.win[w] == pq;
+        if (!due) return;  // no side of the tile moved: its balances stand
     }
     // the thread's two sides (contiguous), loaded before any barrier
     const u64 qa = (u64)a0 + BF_IPT * tid;
@@ -410,7 +433,19 @@ __global__ __launch_bounds__(BF_THREADS) void bs_fused(SideScanArgs A, u64 m, u3
                 while (j > 0 && s_key[j - 1] == key[k] && s_cs[j - 1] == cs[k]) H = add(H, s_h[--j]);
             Bal4 out = row[k];
             if (!(e[k].fl & 1)) out = add(out, run.F);
-            bb[q] = add(out, H);
+            out = add(out, H);
+            if (all) {
+                bb[q] = out;
+            } else {
+                const Bal4 old = bb[q];
+                if (old.dp != out.dp || old.dpo != out.dpo || old.cp != out.cp || old.cpo != out.cpo) {
+                    // a balance moved: its event is due this pass (with its chain)
+                    bb[q] = out;
+                    A.dt.ev[par * A.dt.n + (A.sq_ev[q] & 0x7FFFFFFFu)] = pq;
+                    const u32 c = A.sq_cs[q];
+                    if (!(c & SQ_STANDALONE)) A.dt.chain[par * A.dt.n + (c & SQ_CS)] = pq;
+                }
+            }
         }
         run = combine_f(run, e[k]);
     }

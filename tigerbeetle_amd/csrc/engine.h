@@ -105,6 +105,26 @@ struct PassGate {
     const u32* halt;    // [0] a post/void resolved outside its sides (rebuild them), [1] the fused
                         // balance scan met an account segment longer than its window: nonzero halts
     u32 p;              // this pass's number
+    u32 full;           // evaluate and rescan everything (no dirty tracking: the three-launch scan)
+};
+
+// Dirty tracking of the fixed point's passes (transfers.hip, balances.hip bs_fused).
+// A pass re-evaluates only the events whose inputs moved in the previous pass, and the
+// fused scan redoes only the windows whose side records moved.  Stamps hold the pass
+// number for which something is due (no clearing between passes); the event, chain and
+// slot stamps are kept per pass parity, so that marks for pass q + 1 never overwrite
+// the marks pass q is reading.  An event evaluated at pass q reads state q - 1 and
+// writes the other state buffer; a skipped event must hold the same outcome in both,
+// so an event that changed at pass q is evaluated again at q + 1.
+struct Dirty {
+    u32* ev;          // [2][n] the pass at which the event is evaluated
+    u32* chain;       // [2][n] by chain start: the pass at which every member is (a chain's first
+                      // failure is recomputed from all its members)
+    u32* slot;        // [2][g] by group-table slot: the pass at which the complex events of that id
+                      // (its repeats, the post/voids naming it as pending) are
+    u32* win;         // [windows] the pass at which the fused scan redoes the window
+    const u32* all;   // the pass at which everything is (0: a chunk's first; after a side rebuild)
+    u32 n, g;         // strides of ev / chain and of slot
 };
 __device__ __forceinline__ bool gate_open(const PassGate& g) { return *g.chg != 0 && g.halt[0] == 0 && g.halt[1] == 0; }
 
@@ -161,6 +181,12 @@ struct SideScanArgs {
     u32 probe;        // timing probes only (TBGPU_EVAL_PROBE): 1 no chain words, 2 no account rows, 4 no block scan
     const u32* epi;   // bs_final's gate (TrArgs::epi), or null; 2: use cfail_alt
     const u32* cfail_alt;
+    // dirty tracking (bs_fused): windows to redo, balances that moved mark their events;
+    // the complex list's events whose id / pending groups moved are marked here too
+    Dirty dt;
+    const u32* lst_complex;
+    u32 n_complex;
+    const u32 *gslot, *pslot, *cs, *ce;
 };
 
 // final-ok of a sorted side: evaluated-ok and its chain persisted
@@ -283,7 +309,8 @@ enum {
     CNT_DBG = 16,       // diagnostics (words 16-21): changed events by kind, summed over a call's passes
     CNT_NSIMPLE = 22,   // general path: events on the per-pass simple list (tr_lists)
     CNT_NCOMPLEX = 23,  // general path: events on the per-pass complex list
-    CNT_COUNT = 24,
+    CNT_ALL = 24,       // general path: the pass at which every event is evaluated (Dirty::all)
+    CNT_COUNT = 25,
 };
 enum {
     FL_CHAINS = 1u << 0,      // some event is in a linked chain

@@ -25,6 +25,12 @@
 [[noreturn]] void tbgpu_fatal(const char* what, const char* why, const char* file, int line) {
     fprintf(stderr, "tbgpu: fatal: %s: %s (%s:%d)\n", what, why, file, line);
     fflush(stderr);
+    if (const char* log = getenv("TBGPU_FATAL_LOG")) {  // where a test runner that captures stderr can find it
+        if (FILE* f = fopen(log, "a")) {
+            fprintf(f, "tbgpu: fatal: %s: %s (%s:%d)\n", what, why, file, line);
+            fclose(f);
+        }
+    }
     abort();
 }
 
@@ -150,6 +156,7 @@ struct tbgpu_ctx {
     u128 *sq_dpend = nullptr, *sq_dpost = nullptr;
     u32 *gkey_s, *gsorted;  // the id-group sort's output (the members of each id group, by event)
     u32 *lst_simple, *lst_complex;  // the fixed point's per-pass work lists (tr_lists)
+    u32 *d_ev, *d_chain, *d_slot, *d_win;  // the passes' dirty stamps (engine.h Dirty)
     Bal4* bb = nullptr;
     SortScratch ss{};
     void* side_tiles = nullptr;
@@ -294,6 +301,10 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->sq_dpost = dalloc<u128>(m, &B);
     c->lst_simple = dalloc<u32>(n, &B);
     c->lst_complex = dalloc<u32>(n, &B);
+    c->d_ev = dalloc<u32>(2 * n, &B);
+    c->d_chain = dalloc<u32>(2 * n, &B);
+    c->d_slot = dalloc<u32>(2 * c->gcap, &B);
+    c->d_win = dalloc<u32>(m / side_scan_fused_tile() + 2, &B);
     c->gkey_s = dalloc<u32>(n, &B);
     c->gsorted = dalloc<u32>(n, &B);
     c->bb = dalloc<Bal4>(m, &B);
@@ -644,6 +655,7 @@ static TrArgs make_tr_args(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb) {
     C.debug = debug ? 1u : 0u;
     C.lst_simple = c->lst_simple;
     C.lst_complex = c->lst_complex;
+    C.dt = Dirty{c->d_ev, c->d_chain, c->d_slot, c->d_win, c->counters + CNT_ALL, n, (u32)(C.gmask + 1)};
     return C;
 }
 
@@ -782,7 +794,7 @@ static void walk(tbgpu_ctx* c, const TrArgs& C, u32 n, EvalState& D, const u32* 
         SA.sq_dpend = c->sq_dpend; SA.sq_dpost = c->sq_dpost; SA.n = n;
         SA.cfail = D.cfail;
         SA.cfail_clear = nullptr;
-        SA.gate = PassGate{one, c->counters + CNT_RESORT, 0};
+        SA.gate = PassGate{one, c->counters + CNT_RESORT, 0, 1};
         // the balance of every side before the front's events (the walked ones' records are zero)
         side_scan(SA, m, (u32)c->accounts_max, true, c->side_tiles, c->T.acc, c->bb, s);
         tr_launch_walk(c->T, C, D, c->bb, m, c->w_sstart, c->w_bal, c->w_undo_slot, c->w_undo_val, WALK_UNDO, start,
@@ -865,7 +877,11 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
     SideScanArgs SA{};
     SA.skey = c->skey_s; SA.sq_ev = c->sq_ev; SA.sq_cs = c->sq_cs; SA.sq_ok = c->sq_ok;
     SA.sq_dpend = c->sq_dpend; SA.sq_dpost = c->sq_dpost; SA.n = n;
+    SA.dt = C.dt;
+    SA.lst_complex = c->lst_complex;
+    SA.gslot = c->gslot; SA.pslot = c->pslot; SA.cs = c->cs; SA.ce = c->ce;
     const bool chains = true;  // whether the call has chains is on the device: scan with the chain part
+    static const bool no_incr = getenv("TBGPU_NO_INCR") != nullptr;  // A/B timing: every event every pass
     u32 p = 0;                  // next pass to enqueue
     u32 group = std::max<u32>(2, std::min<u32>(c->last_passes, PASS_GROUP_MAX));
     if (c->opt.flags & TBGPU_OPT_WALK_EARLY) group = 2;  // (tests) the walk after the first two passes
@@ -873,10 +889,12 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
     for (;;) {
         if (p > n + 2 + PC_RING) tbgpu_fatal("create_transfers", "fixed point did not converge", __FILE__, __LINE__);
         prof_mark(c, PH_EVAL);  // the passes: balance scan + evaluation
+        SA.n_complex = n_list[1];
+        const u32 full = (no_incr || c->long_segments) ? 1u : 0u;
         for (u32 q = p; q < p + group; q++) {
             EvalState& S = c->st[q & 1];
             EvalState& D = c->st[(q + 1) & 1];
-            PassGate G{chg + q % PC_RING, c->counters + CNT_RESORT, q};
+            PassGate G{chg + q % PC_RING, c->counters + CNT_RESORT, q, full};
             SA.cfail = S.cfail;
             SA.cfail_clear = D.cfail;
             SA.gate = G;
@@ -921,6 +939,8 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
             const u32 r = resort - 1;
             build_sides(c->st[(r + 1) & 1]);
             HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)(c->counters + CNT_RESORT), 0, 1, s));
+            // new side positions: pass r + 1 evaluates and rescans everything
+            HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)(c->counters + CNT_ALL), r + 1, 1, s));
             HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)(chg + (r + 1) % PC_RING), 1, 1, s));
             p = r + 1;
             continue;
@@ -955,7 +975,7 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
         EvalState& D = c->st[done_at & 1];
         u32* one = c->pc + 2 * PC_RING;  // spare ring: an open gate
         HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)one, 1, 1, s));
-        PassGate G{one, c->counters + CNT_RESORT, 0};
+        PassGate G{one, c->counters + CNT_RESORT, 0, 1};
         for (u32 mode : {0u, 1u, 2u, 3u}) {
             TrArgs P = C;
             P.probe = mode;

@@ -444,7 +444,14 @@ void fp_commit(Tables T, FastArgs F) {
     const bool member = lk || plk || (myctl & TBGPU_CTL_DOOM);
     if (__ballot(member) && lane == 0) atomicOr(&F.counters[CNT_FLAGS], (u32)FL_FCHAIN);
     bool own_ok = false;
+#if defined(FP_NT_ROWS)  // timing variant: rows written with non-temporal stores
+#define STORE_ROW() do { if (!(FP_ABLATE & ABL_ROWS)) { \
+    typedef unsigned int v4u_ __attribute__((ext_vector_type(4))); \
+    v4u_* d_ = (v4u_*)&T.xrows[row_base + i]; const v4u_* s_ = (const v4u_*)&t; \
+    for (int c_ = 0; c_ < 8; c_++) __builtin_nontemporal_store(s_[c_], &d_[c_]); } } while (0)
+#else
 #define STORE_ROW() do { if (!(FP_ABLATE & ABL_ROWS)) T.xrows[row_base + i] = t; } while (0)
+#endif
     if (valid) {
         id = t.id;
         u32 ds = NONE32, cs = NONE32;

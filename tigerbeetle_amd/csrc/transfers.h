@@ -62,6 +62,7 @@ struct TrArgs {
     // outside chains are final after tr_init and never re-evaluated.
     u32* lst_simple;
     u32* lst_complex;
+    Dirty dt;             // dirty tracking of the passes (engine.h)
     u32 debug;            // diagnostics: count changed events by kind (TBGPU_TRACE_PASSES)
     u32 probe;            // timing probes only (TBGPU_EVAL_PROBE, after convergence): 1 skip post/void, 2 no side records
     Sides sd;             // the account sides of the call's events (engine.h)

@@ -301,7 +301,10 @@ __device__ __forceinline__ void grp_fields(const TrArgs& C, u32 kind, u32 i, u32
     *cnt = *slot == NONE32 ? 0u : (kind == 0 ? C.gcnt_id[*slot] : C.gcnt_pd[*slot]);
 }
 
-__global__ void tr_grp_reserve(TrArgs C, u32 kind) {
+constexpr u32 GR_THREADS = 1024;  // one cursor atomic per 1024 events (per wave: ~10 us per chunk)
+__global__ __launch_bounds__(GR_THREADS) void tr_grp_reserve(TrArgs C, u32 kind) {
+    __shared__ u32 s_tot[GR_THREADS / 64];
+    __shared__ u32 s_base;
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (!need(C, kind)) return;
     u32 slot = NONE32, cnt = 0;
@@ -309,16 +312,24 @@ __global__ void tr_grp_reserve(TrArgs C, u32 kind) {
     u32* beg = kind == 0 ? C.gbeg : C.pbeg;
     const bool win = cnt >= 2 && atomicCAS(&beg[slot], NONE32, NONE32 - 1) == NONE32;
     u32 mine = win ? cnt : 0u, pre = mine;
-    const u32 lane = threadIdx.x & 63;
+    const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int off = 1; off < 64; off <<= 1) {  // inclusive prefix over the wave
         const u32 o = __shfl_up(pre, off);
         if (lane >= (u32)off) pre += o;
     }
-    const u32 tot = __shfl(pre, 63);
-    u32 base = 0;
-    if (lane == 63 && tot) base = atomicAdd(&C.counters[kind == 0 ? CNT_GCUR : CNT_PCUR], tot);
-    base = __shfl(base, 63);
-    if (win) beg[slot] = base + pre - mine;
+    if (lane == 63) s_tot[w] = pre;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u32 tot = 0;
+        for (u32 k = 0; k < GR_THREADS / 64; k++) tot += s_tot[k];
+        s_base = tot ? atomicAdd(&C.counters[kind == 0 ? CNT_GCUR : CNT_PCUR], tot) : 0u;
+    }
+    __syncthreads();
+    if (win) {
+        u32 base = s_base;
+        for (u32 k = 0; k < w; k++) base += s_tot[k];
+        beg[slot] = base + pre - mine;
+    }
 }
 
 __global__ void tr_grp_place(TrArgs C, u32 kind) {
@@ -384,6 +395,10 @@ __global__ void tr_group2(TrArgs C) {
 }
 
 // ---------------------------------------------------------- evaluation ----
+
+__device__ __forceinline__ bool is_post_void_ev(const TrArgs& C, u32 i) {
+    return C.sres[i] == SRES_DYN && (C.core[i].flags & (TF_POST | TF_VOID));
+}
 
 struct Ctx {
     const Tables& T;
@@ -654,7 +669,17 @@ __device__ __forceinline__ bool evaluate_one(const Tables& T, const TrArgs& C, c
     D.amt[i] = amt;
     D.pamt[i] = pamt;
     D.pref[i] = pref;
-    if (res != TBGPU_CREATE_TRANSFER_OK && csi != C.ce[i]) atomicMin(&D.cfail[csi], i);
+    if (res != TBGPU_CREATE_TRANSFER_OK && csi != C.ce[i]) {
+        if (g.chg) {
+            atomicMin(&D.cfail[csi], i);
+        } else if (D.cfail[csi] == NONE32 || i < D.cfail[csi]) {
+            // the walk (tr_walk, one lane, D == S): a plain store.  An atomic here ran in
+            // L2 while the lane's later plain loads of the word (visible(), final_ok)
+            // could still hit the CU's L1 copy from before it: a broken chain looked
+            // persisted to the events after it.
+            D.cfail[csi] = i;
+        }
+    }
     const bool changed = res != s_res || amt != s_amt || pamt != s_pamt || pref != s_pref;
     if (C.debug && changed) {
         const u16 f = k.flags;
@@ -696,9 +721,13 @@ __global__ void tr_evaluate(Tables T, TrArgs C, EvalState S, EvalState D, const 
 }
 
 // The per-pass work lists (TrArgs::lst_simple / lst_complex), in event order within a
-// wave; one cursor atomic per wave and list.
-__global__ void tr_lists(TrArgs C) {
-    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+// 1024-event block; one cursor atomic per block and list (one per wave was 2.5k
+// same-address atomics per 164k-event chunk, serialized at the memory side: 60 us).
+constexpr u32 LS_THREADS = 1024;
+__global__ __launch_bounds__(LS_THREADS) void tr_lists(TrArgs C) {
+    __shared__ u32 s_cnt[2][LS_THREADS / 64];
+    __shared__ u32 s_base[2];
+    const u32 i = blockIdx.x * LS_THREADS + threadIdx.x;
     u32 cls = 0;  // 0 final after tr_init, 1 simple, 2 complex
     if (i < C.n) {
         const u8 sr = C.sres[i];
@@ -706,16 +735,69 @@ __global__ void tr_lists(TrArgs C) {
         else if (C.core[i].flags & (TF_POST | TF_VOID)) cls = 2;
         else cls = (C.prev_id[i] == NONE32 && C.pre_e[i] == NONE32) ? 1 : 2;
     }
-    const u32 lane = threadIdx.x & 63;
-#pragma unroll
-    for (u32 k = 1; k <= 2; k++) {
-        const u64 m = __ballot(cls == k);
-        if (!m) continue;
-        u32 base = 0;
-        if (lane == 0) base = atomicAdd(&C.counters[k == 1 ? CNT_NSIMPLE : CNT_NCOMPLEX], (u32)__popcll(m));
-        base = __shfl(base, 0);
-        if (cls == k) (k == 1 ? C.lst_simple : C.lst_complex)[base + __popcll(m & ((1ull << lane) - 1))] = i;
+    const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const u64 m[2] = {__ballot(cls == 1), __ballot(cls == 2)};
+    if (lane == 0) {
+        s_cnt[0][w] = (u32)__popcll(m[0]);
+        s_cnt[1][w] = (u32)__popcll(m[1]);
     }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        u32 tot = 0;
+        for (u32 k = 0; k < LS_THREADS / 64; k++) tot += s_cnt[threadIdx.x][k];
+        s_base[threadIdx.x] = tot ? atomicAdd(&C.counters[threadIdx.x == 0 ? CNT_NSIMPLE : CNT_NCOMPLEX], tot) : 0u;
+    }
+    __syncthreads();
+    if (cls) {
+        const u32 k = cls - 1;
+        u32 at = s_base[k] + (u32)__popcll(m[k] & ((1ull << lane) - 1));
+        for (u32 v = 0; v < w; v++) at += s_cnt[k][v];
+        (k == 0 ? C.lst_simple : C.lst_complex)[at] = i;
+    }
+}
+
+// ------------------------------------------------------- dirty tracking ----
+// (engine.h Dirty.)  Whether event i is due at pass q: everything is at a chunk's
+// first pass and after a side rebuild; otherwise an event whose balances moved (the
+// scan marked it), that changed last pass, whose chain has a member that is, or (the
+// scan's resolve step) whose id / pending group moved.
+__device__ __forceinline__ bool due(const TrArgs& C, const PassGate& g, u32 i, u32 cs, u32 ce) {
+    if (g.full) return true;
+    const u32 q = g.p, par = q & 1;
+    if (*C.dt.all == q) return true;
+    return C.dt.ev[par * C.dt.n + i] == q || (cs != ce && C.dt.chain[par * C.dt.n + cs] == q);
+}
+
+// What reads event j's outcome: the scan windows of its sides (every candidate pair of
+// a post/void), and the complex events keyed by its id or its pending id (later
+// repeats of the id, post/voids naming it, later post/voids of the same pending).
+__device__ __forceinline__ void mark_readers(const TrArgs& C, u32 j, u32 par, u32 nq) {
+    const u32 tile = C.sd.tile;
+    if (is_post_void_ev(C, j)) {
+        for (u32 s = C.sd.soff[j]; s < C.sd.soff[j + 1]; s++) C.dt.win[C.sd.spos[s] / tile] = nq;
+    } else {
+        const uint2 ep = C.sd.epos[j];
+        C.dt.win[ep.x / tile] = nq;
+        C.dt.win[ep.y / tile] = nq;
+    }
+    const u32 gs = C.gslot[j], ps = C.pslot[j];
+    if (gs != NONE32) C.dt.slot[par * C.dt.g + gs] = nq;
+    if (ps != NONE32) C.dt.slot[par * C.dt.g + ps] = nq;
+}
+
+// Event i changed at pass q: it is due again at q + 1 (the other state buffer still
+// holds its old outcome), and so is everything that reads it.  A chain member's
+// change can move the chain's first failure, which every member's visibility and
+// sides depend on: the whole chain is due, with its members' readers (marked once per
+// chain and pass).
+__device__ __forceinline__ void mark_changed(const TrArgs& C, u32 i, u32 q) {
+    const u32 nq = q + 1, par = nq & 1;
+    C.dt.ev[par * C.dt.n + i] = nq;
+    mark_readers(C, i, par, nq);
+    const u32 cs = C.cs[i], ce = C.ce[i];
+    if (cs != ce && atomicExch(&C.dt.chain[par * C.dt.n + cs], nq) != nq)
+        for (u32 j = cs; j <= ce; j++)
+            if (j != i) mark_readers(C, j, par, nq);
 }
 
 // A pass over the simple list: create_transfer's balance tail (src/state_machine.zig:
@@ -736,8 +818,12 @@ __global__ __launch_bounds__(256) void tr_eval_simple(TrArgs C, EvalState S, Eva
     if (k < cnt) {
         i = C.lst_simple[k];
         const u8 sr = C.sres[i];
-        const u32 csi = C.cs[i];
-        if (sr != SRES_DYN) {  // a static failure inside a chain
+        const u32 csi = C.cs[i], cei = C.ce[i];
+        if (!due(C, g, i, csi, cei)) {
+            // outcome unchanged in both buffers; a chain nobody re-evaluates keeps its
+            // first failure (the scan reset the next state's)
+            if (i == csi && csi != cei) D.cfail[csi] = S.cfail[csi];
+        } else if (sr != SRES_DYN) {  // a static failure inside a chain
             D.res[i] = sr;
             D.ok[i] = 0;
             D.amt[i] = 0;
@@ -766,6 +852,7 @@ __global__ __launch_bounds__(256) void tr_eval_simple(TrArgs C, EvalState S, Eva
                 C.sd.sq_ok[ep.x] = C.sd.sq_ok[ep.y] = ok ? 1 : 0;
                 C.sd.sq_dpend[ep.x] = C.sd.sq_dpend[ep.y] = dpe;
                 C.sd.sq_dpost[ep.x] = C.sd.sq_dpost[ep.y] = dpo;
+                mark_changed(C, i, g.p);
             }
         }
     }
@@ -786,7 +873,13 @@ __global__ void tr_eval_complex(Tables T, TrArgs C, EvalState S, EvalState D, co
     bool changed = false;
     if (k < cnt) {
         i = C.lst_complex[k];
-        changed = evaluate_one(T, C, S, D, bb, g, i);
+        const u32 csi = C.cs[i], cei = C.ce[i];
+        if (due(C, g, i, csi, cei)) {
+            changed = evaluate_one(T, C, S, D, bb, g, i);
+            if (changed) mark_changed(C, i, g.p);
+        } else if (i == csi && csi != cei) {
+            D.cfail[csi] = S.cfail[csi];
+        }
     }
     const u32 c = block_sum(changed ? 1u : 0u);
     const u32 f = block_min(changed ? i : NONE32);
@@ -1285,11 +1378,12 @@ __global__ __launch_bounds__(64) void tr_walk(Tables T, TrArgs C, EvalState D, B
     __shared__ Bal4 cval[WK_CACHE];
     __shared__ u32 s_stop;
     const u32 lane = threadIdx.x;
-    const PassGate G{nullptr, nullptr, 0};
+    const PassGate G{nullptr, nullptr, 0, 1};
     u32 undo_n = 0;
     bool broken = false;
     if (lane == 0) {
         W.out[0] = NONE32;
+        W.out[1] = 0;  // the error word: the buffer is not cleared anywhere else (recycled memory)
         s_stop = 0;
     }
     // a per-block bitmap of the segments moved in this block: their staged balances are stale
@@ -1473,7 +1567,12 @@ __global__ void tr_prep(TrArgs C, u32* cfail0, u32* pc, u32 ring) {
             C.gfill[k] = 0;
             C.pfill[k] = 0;
         }
-        if (k < C.n) cfail0[k] = NONE32;
+        if (k < C.n) {
+            cfail0[k] = NONE32;
+            C.dt.ev[k] = C.dt.ev[C.n + k] = NONE32;  // no stamp: pass 0 evaluates everything (Dirty::all)
+            C.dt.chain[k] = C.dt.chain[C.n + k] = NONE32;
+        }
+        if (k < g) C.dt.slot[k] = C.dt.slot[g + k] = NONE32;
         if (k < ring) {
             pc[k] = k == 0 ? 1u : 0u;
             pc[ring + k] = NONE32;
@@ -1492,7 +1591,7 @@ void tr_launch_classify(const Tables& T, const TrArgs& C, hipStream_t stream) {
     tr_group1<<<GRID(C.n)>>>(C);
 }
 void tr_launch_group(const TrArgs& C, u32 kind, hipStream_t stream) {
-    tr_grp_reserve<<<GRID(C.n)>>>(C, kind);
+    tr_grp_reserve<<<(C.n + GR_THREADS - 1) / GR_THREADS, GR_THREADS, 0, stream>>>(C, kind);
     tr_grp_place<<<GRID(C.n)>>>(C, kind);
     tr_grp_rank<<<GRID(C.n)>>>(C, kind);
 }
@@ -1509,6 +1608,7 @@ void tr_launch_side_build(const TrArgs& C, const EvalState& S, u32 kmax, const u
 }
 void tr_launch_side_pos(const TrArgs& C, const u32* sval_s, u64 m, hipStream_t stream) {
     HIP_CHECK(hipMemsetAsync(C.sd.tstart, 0xFF, ((m + C.sd.tile - 1) / C.sd.tile + 1) * sizeof(u32), stream));
+    HIP_CHECK(hipMemsetAsync(C.dt.win, 0xFF, ((m + C.sd.tile - 1) / C.sd.tile + 1) * sizeof(u32), stream));
     tr_side_pos<<<GRID(m)>>>(C, sval_s, m);
 }
 void tr_launch_side_rec(const TrArgs& C, const EvalState& S, hipStream_t stream) {
@@ -1518,7 +1618,9 @@ void tr_launch_evaluate(const Tables& T, const TrArgs& C, const EvalState& S, co
                         const PassGate& g, u32* chg, u32* chg_next, u32* front, u32* front_next, hipStream_t stream) {
     tr_evaluate<<<GRID(C.n)>>>(T, C, S, D, bb, g, chg, chg_next, front, front_next);
 }
-void tr_launch_lists(const TrArgs& C, hipStream_t stream) { tr_lists<<<GRID(C.n)>>>(C); }
+void tr_launch_lists(const TrArgs& C, hipStream_t stream) {
+    tr_lists<<<(C.n + LS_THREADS - 1) / LS_THREADS, LS_THREADS, 0, stream>>>(C);
+}
 void tr_launch_evaluate_lists(const Tables& T, const TrArgs& C, const EvalState& S, const EvalState& D, const Bal4* bb,
                               const PassGate& g, u32* chg, u32* chg_next, u32* front, u32* front_next, u32 n_simple,
                               u32 n_complex, hipStream_t stream) {

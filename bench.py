@@ -184,6 +184,7 @@ def host_path(eng, w, tts, counts, b0, nbs, torch):
                        "latency_us": {"p50": round(float(np.percentile(lat, 50)), 1),
                                       "p99": round(float(np.percentile(lat, 99)), 1),
                                       "max": round(float(lat.max()), 1)},
+                       "slowest_calls": [int(x) for x in np.argsort(lat)[::-1][:3]],
                        "device_us": {"p50": round(float(np.percentile(dev_us, 50)), 1),
                                      "p99": round(float(np.percentile(dev_us, 99)), 1),
                                      "max": round(float(dev_us.max()), 1)},

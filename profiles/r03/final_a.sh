@@ -1,0 +1,35 @@
+#!/bin/bash
+# Round 3 evidence on the final code, part A (one gpurun call, fresh MI355X):
+#   bash profiles/r03/final_a.sh gpurun_out/r03_final
+# the -m gpu suite, smoke, the driver's bench command, every BASELINE config's line,
+# config 3 with and without dirty tracking, the routed one-rank and gloo two-rank lines.
+OUT=${1:-gpurun_out/r03_final}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {  # name, seconds, command...: one GPU step under its own limit; stop at the first failure
+  local name=$1 secs=$2; shift 2
+  echo "== $name $(date +%T)"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
+  local rc=$?
+  [ $rc -eq 0 ] || { echo "$name rc=$rc"; tail -20 "$OUT/$name.err"; tail -30 "$OUT/$name.out"; cat gpurun_out/tbgpu_fatal.log 2>/dev/null; exit $rc; }
+}
+rm -f gpurun_out/tbgpu_fatal.log
+step gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
+tail -2 "$OUT/gpu_tests.out"
+step smoke 180 python3 -u __graft_entry__.py smoke
+cat "$OUT/smoke.out"
+step bench 400 python3 bench.py --gpus 1 --steps 20 --warmup 5
+python3 profiles/r03/line.py "$OUT/bench.out"
+step bench_config3 400 python3 bench.py --config 3 --no-queries --no-host
+python3 profiles/r03/line.py "$OUT/bench_config3.out"
+step bench_config3_noincr 400 env TBGPU_NO_INCR=1 python3 bench.py --config 3 --no-cpu --no-queries --no-host
+python3 profiles/r03/line.py "$OUT/bench_config3_noincr.out"
+for c in 1 4 5; do
+  step bench_config$c 400 python3 bench.py --config $c --no-queries --no-host
+  python3 profiles/r03/line.py "$OUT/bench_config$c.out"
+done
+step bench_routed_1rank 400 python3 bench.py --routed --no-queries
+python3 profiles/r03/line.py "$OUT/bench_routed_1rank.out"
+step bench_routed_gloo2 600 env TB_DIST_BACKEND=gloo python3 bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu --batches-per-step 100 --accounts 1000000
+python3 profiles/r03/line.py "$OUT/bench_routed_gloo2.out"
+echo "== done $(date +%T)"

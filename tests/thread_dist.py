@@ -1,5 +1,5 @@
 """In-process stand-in for the torch.distributed collectives the ledger router uses
-(all_gather, all_gather_object, all_to_all_single), with one thread per rank.
+(all_gather, all_gather_object, all_to_all_single, all_reduce), with one thread per rank.
 
 It lets the device-resident routed step run with several ranks on ONE GPU and with
 CUDA tensors -- the path `bench.py --gpus N` takes over RCCL -- where a real RCCL
@@ -19,6 +19,9 @@ class ThreadGroup:
 
 
 class ThreadDist:
+    class ReduceOp:
+        SUM, MAX = "sum", "max"
+
     def __init__(self, group: ThreadGroup, rank: int):
         self.g, self.rank, self.world = group, rank, group.world
 
@@ -57,3 +60,13 @@ class ThreadDist:
         if output.numel():
             output.copy_(torch.cat(mine))
         self._sync(output)
+
+    def all_reduce(self, tensor, op="sum", group=None):
+        import torch
+        self._sync(tensor)
+        got = self._exchange(tensor.clone())
+        out = got[0].clone()
+        for t in got[1:]:
+            out = torch.maximum(out, t) if op == "max" else out + t
+        tensor.copy_(out)
+        self._sync(tensor)

@@ -193,15 +193,18 @@ __device__ __forceinline__ u64 ac_mask_one(const AcArgs& C, const u8* res, const
 
 // One atomicMax per wave on the single commit_timestamp word (one per accepted event
 // serialized at the memory side: 897 us for 10M accounts, SQ_WAIT_ANY 0.96 of the waves).
-__global__ void ac_mask(AcArgs C, const u8* res, const u8* ok, const u32* cfail, u8* fres, u8* mask, u64* commit_ts) {
+__global__ void ac_mask(AcArgs C, const u8* res, const u8* ok, const u32* cfail, u8* fres, u8* mask, u64* commit_ts,
+                        const u32* gate) {
+    if (gate && *gate == 0) return;
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     u64 ts = i < C.n ? ac_mask_one(C, res, ok, cfail, fres, mask, i) : 0;
     ts = wave_max_u64(ts);
     if (ts && wave_leader()) atomicMax((unsigned long long*)commit_ts, (unsigned long long)ts);
 }
 
-__global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const uint4* rk, u64 row_base,
-                         tbgpu_create_accounts_result_t* results) {
+__global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const uint4* rk, u64 row_base, u64 cap,
+                         tbgpu_create_accounts_result_t* results, const u32* gate) {
+    if (gate && *gate == 0) return;
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= C.n) return;
     const u8 r = fres[i];
@@ -216,6 +219,10 @@ __global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const
     a.timestamp = C.ts[i];
     // accounts.insert: the row is the event's rank among the persisted accounts
     // (creation order); the index slot is claimed by CAS on its row word.
+    if (row_base + rk[i].x >= cap) {  // accounts_max exceeded: nothing past it is written (the host aborts)
+        atomicOr(&C.counters[CNT_FLAGS], (u32)FL_ERROR);
+        return;
+    }
     const u32 row = (u32)(row_base + rk[i].x);
     T.acc[row] = a;
     u64 h = hash128(a.id) & T.aidx_mask;
@@ -229,7 +236,8 @@ __global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const
     if (dense_has(T, a.id)) T.dense[dense_slot(T, a.id)] = dense_entry(row, a.ledger, a.flags);
 }
 
-__global__ void ac_batch_counts(const u32* b_start, u32 nb, const uint4* rk, u32* counts) {
+__global__ void ac_batch_counts(const u32* b_start, u32 nb, const uint4* rk, u32* counts, const u32* gate) {
+    if (gate && *gate == 0) return;
     const u32 b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b < nb) counts[b] = rk[b_start[b + 1]].y - rk[b_start[b]].y;
 }
@@ -359,14 +367,22 @@ void ac_launch_evaluate(const Tables& T, const AcArgs& C, const u8* res_s, const
     ac_finalize<<<GRID(C.n)>>>(C, ok_d, cfail_d);
 }
 void ac_launch_mask(const Tables& T, const AcArgs& C, const u8* res, const u8* ok, const u32* cfail, u8* fres,
-                    u8* mask, hipStream_t stream) {
-    ac_mask<<<GRID(C.n)>>>(C, res, ok, cfail, fres, mask, T.commit_ts);
+                    u8* mask, hipStream_t stream, const u32* gate) {
+    ac_mask<<<GRID(C.n)>>>(C, res, ok, cfail, fres, mask, T.commit_ts, gate);
 }
 void ac_launch_apply(const Tables& T, const AcArgs& C, const u8* ok, const u8* fres, const uint4* rk, u64 row_base,
-                     tbgpu_create_accounts_result_t* results, u32* counts, hipStream_t stream) {
-    ac_apply<<<GRID(C.n)>>>(T, C, ok, fres, rk, row_base, results);
-    ac_batch_counts<<<GRID(C.nb)>>>(C.b_start, C.nb, rk, counts);
+                     u64 cap, tbgpu_create_accounts_result_t* results, u32* counts, hipStream_t stream, const u32* gate) {
+    ac_apply<<<GRID(C.n)>>>(T, C, ok, fres, rk, row_base, cap, results, gate);
+    ac_batch_counts<<<GRID(C.nb)>>>(C.b_start, C.nb, rk, counts, gate);
 }
+namespace {
+// The speculative one-evaluation path of create_accounts runs iff classify found neither
+// a linked chain nor a repeated id (one thread).
+__global__ void ac_gate(AcArgs C, u32* gate) {
+    if (threadIdx.x == 0) *gate = (C.counters[CNT_FLAGS] & (FL_CHAINS | FL_MULTI_ID)) ? 0u : 1u;
+}
+}  // namespace
+void ac_launch_gate(const AcArgs& C, u32* gate, hipStream_t stream) { ac_gate<<<1, 64, 0, stream>>>(C, gate); }
 void launch_lookup_accounts(const Tables& T, const u128* ids, u32 n, Account* out, u8* found, hipStream_t stream) {
     if (n) k_lookup_accounts<<<GRID(n)>>>(T, ids, n, out, found);
 }

@@ -139,10 +139,15 @@ void ac_launch_group_sort(const AcArgs& C, u32 invalid, int bits, u32* k_in, u32
 void ac_launch_init(const AcArgs& C, u8* res, u8* ok, u32* cfail, hipStream_t stream);
 void ac_launch_evaluate(const Tables& T, const AcArgs& C, const u8* res_s, const u8* ok_s, u8* res_d, u8* ok_d,
                         u32* cfail_d, hipStream_t stream);
+// gate: run only while *gate != 0 (null: always); apply writes no row at or past `cap`
+// (it raises FL_ERROR instead)
 void ac_launch_mask(const Tables& T, const AcArgs& C, const u8* res, const u8* ok, const u32* cfail, u8* fres,
-                    u8* mask, hipStream_t stream);
+                    u8* mask, hipStream_t stream, const u32* gate = nullptr);
 void ac_launch_apply(const Tables& T, const AcArgs& C, const u8* ok, const u8* fres, const uint4* rk, u64 row_base,
-                     tbgpu_create_accounts_result_t* results, u32* counts, hipStream_t stream);
+                     u64 cap, tbgpu_create_accounts_result_t* results, u32* counts, hipStream_t stream,
+                     const u32* gate = nullptr);
+// *gate = 1 when classify found no chain and no repeated id (one evaluation is final)
+void ac_launch_gate(const AcArgs& C, u32* gate, hipStream_t stream);
 
 // lookups / maintenance (accounts.hip)
 void launch_lookup_accounts(const Tables& T, const u128* ids, u32 n, Account* out, u8* found, hipStream_t stream);

@@ -86,6 +86,9 @@ T* dalloc(u64 count, u64* total) {
     void* p = nullptr;
     const u64 bytes = std::max<u64>(count * sizeof(T), 16);
     HIP_CHECK(hipMalloc(&p, bytes));
+    // zeroed once: recycled device memory (an earlier ctx's buffers) never reaches a
+    // kernel as data a fresh allocation would not hold
+    HIP_CHECK(hipMemset(p, 0, bytes));
     *total += bytes;
     return (T*)p;
 }
@@ -100,6 +103,7 @@ T* dalloc_hot(u64 count, u64* total) {
     void* p = nullptr;
     const u64 bytes = std::max<u64>(count * sizeof(T), 16);
     if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous) == hipSuccess && p) {
+        HIP_CHECK(hipMemset(p, 0, bytes));
         *total += bytes;
         return (T*)p;
     }
@@ -483,7 +487,9 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
                     c->sc.tile_sums, c->fres, c->mask, c->ranks, c->res_buf, c->counts, c->counters, c->status,
                     c->f_gtab, c->f_gpos, c->f_keys, c->f_rows,
                     c->f_tile_idr, c->rt_ts_buf, c->rt_ctl_buf, c->rt_dry_ts, c->rt_stats, c->rg_part, c->T.base, c->q_key, c->q_val, c->q_tkey,
-                    c->q_tval, c->q_ss.keys_tmp, c->q_ss.vals_tmp, c->q_ss.hist, c->q_runs_dev, c->ximp};
+                    c->q_tval, c->q_ss.keys_tmp, c->q_ss.vals_tmp, c->q_ss.hist, c->q_runs_dev, c->ximp,
+                    c->lst_simple, c->lst_complex, c->d_ev, c->d_chain, c->d_slot, c->d_win, c->w_sstart, c->w_bal,
+                    c->w_undo_slot, c->w_undo_val, c->w_out};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     for (EvalState& s : c->st) {
         void* q[] = {s.res, s.ok, s.pref, s.cfail, s.amt, s.pamt};

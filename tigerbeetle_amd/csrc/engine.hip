@@ -81,14 +81,21 @@ inline void wait_event(hipEvent_t ev) {
     }
 }
 
+// A new allocation zeroed before it is handed out: recycled device memory (an earlier
+// ctx's buffers) never reaches a kernel as data a fresh allocation would not hold.
+// The memset runs on the null stream, which the ctx's non-blocking streams do not
+// wait for: it must be complete before the buffer is used, hence the wait.
+inline void zero_now(void* p, u64 bytes) {
+    HIP_CHECK(hipMemsetAsync(p, 0, bytes, nullptr));
+    HIP_CHECK(hipStreamSynchronize(nullptr));
+}
+
 template <typename T>
 T* dalloc(u64 count, u64* total) {
     void* p = nullptr;
     const u64 bytes = std::max<u64>(count * sizeof(T), 16);
     HIP_CHECK(hipMalloc(&p, bytes));
-    // zeroed once: recycled device memory (an earlier ctx's buffers) never reaches a
-    // kernel as data a fresh allocation would not hold
-    HIP_CHECK(hipMemset(p, 0, bytes));
+    zero_now(p, bytes);
     *total += bytes;
     return (T*)p;
 }
@@ -103,7 +110,7 @@ T* dalloc_hot(u64 count, u64* total) {
     void* p = nullptr;
     const u64 bytes = std::max<u64>(count * sizeof(T), 16);
     if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous) == hipSuccess && p) {
-        HIP_CHECK(hipMemset(p, 0, bytes));
+        zero_now(p, bytes);
         *total += bytes;
         return (T*)p;
     }
@@ -331,7 +338,6 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->status = dalloc<int>(4, &B);
     c->f_gcap = pow2_at_least(2 * nmax);
     c->f_gtab = dalloc<u32>(c->f_gcap, &B);
-    HIP_CHECK(hipMemset(c->f_gtab, 0, c->f_gcap * sizeof(u32)));
     c->f_gpos = dalloc<u32>(n, &B);
     c->f_keys = dalloc<u128>(n, &B);
     c->f_rows = dalloc<u32>(n, &B);

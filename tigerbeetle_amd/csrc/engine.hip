@@ -81,21 +81,11 @@ inline void wait_event(hipEvent_t ev) {
     }
 }
 
-// A new allocation zeroed before it is handed out: recycled device memory (an earlier
-// ctx's buffers) never reaches a kernel as data a fresh allocation would not hold.
-// The memset runs on the null stream, which the ctx's non-blocking streams do not
-// wait for: it must be complete before the buffer is used, hence the wait.
-inline void zero_now(void* p, u64 bytes) {
-    HIP_CHECK(hipMemsetAsync(p, 0, bytes, nullptr));
-    HIP_CHECK(hipStreamSynchronize(nullptr));
-}
-
 template <typename T>
 T* dalloc(u64 count, u64* total) {
     void* p = nullptr;
     const u64 bytes = std::max<u64>(count * sizeof(T), 16);
     HIP_CHECK(hipMalloc(&p, bytes));
-    zero_now(p, bytes);
     *total += bytes;
     return (T*)p;
 }
@@ -110,7 +100,6 @@ T* dalloc_hot(u64 count, u64* total) {
     void* p = nullptr;
     const u64 bytes = std::max<u64>(count * sizeof(T), 16);
     if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous) == hipSuccess && p) {
-        zero_now(p, bytes);
         *total += bytes;
         return (T*)p;
     }

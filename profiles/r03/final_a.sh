@@ -1,9 +1,10 @@
 #!/bin/bash
 # Round 3 evidence on the final code, part A (one gpurun call, fresh MI355X):
-#   bash profiles/r03/final_a.sh gpurun_out/r03_final
+#   bash profiles/r03/final_a.sh gpurun_out/r03_final [1|2]   (part 1, part 2, or both)
 # the -m gpu suite, smoke, the driver's bench command, every BASELINE config's line,
 # config 3 with and without dirty tracking, the routed one-rank and gloo two-rank lines.
 OUT=${1:-gpurun_out/r03_final}
+PART=${2:-all}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() {  # name, seconds, command...: one GPU step under its own limit; stop at the first failure
@@ -14,6 +15,7 @@ step() {  # name, seconds, command...: one GPU step under its own limit; stop at
   [ $rc -eq 0 ] || { echo "$name rc=$rc"; tail -20 "$OUT/$name.err"; tail -30 "$OUT/$name.out"; cat gpurun_out/tbgpu_fatal.log 2>/dev/null; exit $rc; }
 }
 rm -f gpurun_out/tbgpu_fatal.log
+if [ "$PART" != 2 ]; then
 step gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
 tail -2 "$OUT/gpu_tests.out"
 step smoke 180 python3 -u __graft_entry__.py smoke
@@ -24,6 +26,8 @@ step bench_config3 400 python3 bench.py --config 3 --no-queries --no-host
 python3 profiles/r03/line.py "$OUT/bench_config3.out"
 step bench_config3_noincr 400 env TBGPU_NO_INCR=1 python3 bench.py --config 3 --no-cpu --no-queries --no-host
 python3 profiles/r03/line.py "$OUT/bench_config3_noincr.out"
+fi
+[ "$PART" = 1 ] && { echo "== done $(date +%T)"; exit 0; }
 for c in 1 4 5; do
   step bench_config$c 400 python3 bench.py --config $c --no-queries --no-host
   python3 profiles/r03/line.py "$OUT/bench_config$c.out"

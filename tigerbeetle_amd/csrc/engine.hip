@@ -81,11 +81,29 @@ inline void wait_event(hipEvent_t ev) {
     }
 }
 
+// Every device allocation is zeroed on the stream of the ctx that allocates it
+// (ZeroOn names it for the allocating scope), ahead of any of its work: recycled
+// memory of an earlier ctx never reaches a kernel, and the zeroing is ordered with
+// the ctx's own copies (a null-stream memset is not: the ctx's streams are
+// non-blocking).
+thread_local hipStream_t t_zero_stream = nullptr;
+struct ZeroOn {
+    hipStream_t prev;
+    explicit ZeroOn(hipStream_t s) : prev(t_zero_stream) { t_zero_stream = s; }
+    ~ZeroOn() { t_zero_stream = prev; }
+};
+
+inline void zero_new(void* p, u64 bytes) {
+    if (!t_zero_stream) tbgpu_fatal("alloc", "device allocation outside a ZeroOn scope", __FILE__, __LINE__);
+    HIP_CHECK(hipMemsetAsync(p, 0, bytes, t_zero_stream));
+}
+
 template <typename T>
 T* dalloc(u64 count, u64* total) {
     void* p = nullptr;
     const u64 bytes = std::max<u64>(count * sizeof(T), 16);
     HIP_CHECK(hipMalloc(&p, bytes));
+    zero_new(p, bytes);
     *total += bytes;
     return (T*)p;
 }
@@ -100,6 +118,7 @@ T* dalloc_hot(u64 count, u64* total) {
     void* p = nullptr;
     const u64 bytes = std::max<u64>(count * sizeof(T), 16);
     if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous) == hipSuccess && p) {
+        zero_new(p, bytes);
         *total += bytes;
         return (T*)p;
     }
@@ -413,6 +432,7 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     c->xidx_cap = pow2_at_least(2 * o.transfers_max);
     c->hist_cap = o.history_max;
     u64& B = c->bytes;
+    ZeroOn zero_on(c->stream);
     c->T.acc = dalloc_hot<Account>(o.accounts_max, &B);
     c->T.aidx = dalloc_hot<AccIdx>(c->aidx_cap, &B);
     c->T.aidx_mask = c->aidx_cap - 1;
@@ -772,6 +792,7 @@ static void walk(tbgpu_ctx* c, const TrArgs& C, u32 n, EvalState& D, const u32* 
     hipStream_t s = c->stream;
     if (!c->w_sstart) {
         u64& B = c->bytes;
+        ZeroOn zero_on(s);
         c->w_sstart = dalloc<u32>(c->scap, &B);
         c->w_bal = dalloc<Bal4>(c->scap, &B);
         c->w_undo_slot = dalloc<u32>(WALK_UNDO, &B);
@@ -1306,7 +1327,8 @@ static uint64_t routed(tbgpu_ctx* c, uint32_t batch_count, const uint32_t* count
     c->rt_ev_ts = nullptr;
     c->rt_ctl = nullptr;
     u64 ts = 0;
-    HIP_CHECK(hipMemcpy(&ts, c->rt_dry ? c->rt_dry_ts : c->T.commit_ts, sizeof(u64), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpyAsync(&ts, c->rt_dry ? c->rt_dry_ts : c->T.commit_ts, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    wait_stream(c->stream);
     c->rt_dry = false;
     if (commit_timestamp) *commit_timestamp = ts;
     return total;
@@ -1338,8 +1360,8 @@ extern "C" int tbgpu_import_transfers(tbgpu_ctx* c, const tbgpu_transfer_t* rows
         HIP_CHECK(hipMemcpyAsync(c->ev_buf, keep.data() + off, (u64)k * 128, hipMemcpyHostToDevice, c->stream));
         launch_import_transfers(c->T, (const Transfer*)c->ev_buf, k, c->n_rows, c->stream);
         if (!c->ximp) {
+            ZeroOn zero_on(c->stream);
             c->ximp = dalloc<u8>(c->xrow_cap, &c->bytes);
-            HIP_CHECK(hipMemsetAsync(c->ximp, 0, c->xrow_cap, c->stream));
         }
         HIP_CHECK(hipMemsetAsync(c->ximp + c->n_rows, 1, k, c->stream));  // not this shard's: never queried
         wait_stream(c->stream);
@@ -1723,6 +1745,7 @@ extern "C" uint64_t tbgpu_compact(tbgpu_ctx* c) {
     if (r1 == r0) return r1;
     if (!c->q_key) {
         u64& B = c->bytes;
+        ZeroOn zero_on(c->stream);
         const u64 cap = 2 * c->xrow_cap;  // two entries per stored row
         c->q_key = dalloc<u32>(cap, &B);
         c->q_val = dalloc<u32>(cap, &B);
@@ -1778,7 +1801,8 @@ static uint32_t query_host(tbgpu_ctx* c, const tbgpu_account_filter_t* filter, v
     HIP_CHECK(hipMemcpyAsync(fd, filter, sizeof *filter, hipMemcpyHostToDevice, c->stream));
     uint32_t n = 0;
     run_queries(c, fd, 1, TBGPU_QUERY_MAX, c->ev_buf, history, &n);  // ev_buf: nmax * 128 B >= 8190 rows
-    if (n) HIP_CHECK(hipMemcpy(out, c->ev_buf, (u64)n * 128, hipMemcpyDeviceToHost));
+    if (n) HIP_CHECK(hipMemcpyAsync(out, c->ev_buf, (u64)n * 128, hipMemcpyDeviceToHost, c->stream));
+    wait_stream(c->stream);
     return n;
 }
 
@@ -1841,13 +1865,18 @@ extern "C" uint64_t tbgpu_checkpoint(tbgpu_ctx* c, void* out, uint64_t capacity)
     wait_stream(c->stream);
     u8* p = (u8*)out + sizeof(CkHeader);
     const u64 na = c->n_accounts, nr = c->n_rows, nh = c->n_hist;
-    if (na) HIP_CHECK(hipMemcpy(p, c->T.acc, na * 128, hipMemcpyDeviceToHost));
-    if (nr) HIP_CHECK(hipMemcpy(p + na * 128, c->T.xrows, nr * 128, hipMemcpyDeviceToHost));
-    if (nr) HIP_CHECK(hipMemcpy(p + na * 128 + nr * 128, c->T.xful, nr, hipMemcpyDeviceToHost));
+    if (na) HIP_CHECK(hipMemcpyAsync(p, c->T.acc, na * 128, hipMemcpyDeviceToHost, c->stream));
+    wait_stream(c->stream);
+    if (nr) HIP_CHECK(hipMemcpyAsync(p + na * 128, c->T.xrows, nr * 128, hipMemcpyDeviceToHost, c->stream));
+    wait_stream(c->stream);
+    if (nr) HIP_CHECK(hipMemcpyAsync(p + na * 128 + nr * 128, c->T.xful, nr, hipMemcpyDeviceToHost, c->stream));
+    wait_stream(c->stream);
     u8* imp = p + na * 128 + nr * 129;
-    if (nr && c->ximp) HIP_CHECK(hipMemcpy(imp, c->ximp, nr, hipMemcpyDeviceToHost));
+    if (nr && c->ximp) HIP_CHECK(hipMemcpyAsync(imp, c->ximp, nr, hipMemcpyDeviceToHost, c->stream));
     else memset(imp, 0, nr);
-    if (nh) HIP_CHECK(hipMemcpy(imp + nr, c->T.hrows, nh * 256, hipMemcpyDeviceToHost));
+    wait_stream(c->stream);
+    if (nh) HIP_CHECK(hipMemcpyAsync(imp + nr, c->T.hrows, nh * 256, hipMemcpyDeviceToHost, c->stream));
+    wait_stream(c->stream);
     CkHeader h{};
     h.magic = CK_MAGIC;
     h.version = 1;
@@ -1873,18 +1902,29 @@ extern "C" int tbgpu_open(tbgpu_ctx* c, const void* image, uint64_t size) {
     tbgpu_reset(c);
     const u64 na = h.n_accounts, nr = h.n_rows, nh = h.n_hist;
     hipStream_t s = c->stream;
-    if (na) HIP_CHECK(hipMemcpy(c->T.acc, p, na * 128, hipMemcpyHostToDevice));
-    if (nr) HIP_CHECK(hipMemcpy(c->T.xrows, p + na * 128, nr * 128, hipMemcpyHostToDevice));
-    if (nr) HIP_CHECK(hipMemcpy(c->T.xful, p + na * 128 + nr * 128, nr, hipMemcpyHostToDevice));
+    // the reset's memsets run on the ctx's non-blocking stream, which the blocking
+    // copies below do not wait for
+    wait_stream(s);
+    if (na) HIP_CHECK(hipMemcpyAsync(c->T.acc, p, na * 128, hipMemcpyHostToDevice, c->stream));
+    wait_stream(c->stream);
+    if (nr) HIP_CHECK(hipMemcpyAsync(c->T.xrows, p + na * 128, nr * 128, hipMemcpyHostToDevice, c->stream));
+    wait_stream(c->stream);
+    if (nr) HIP_CHECK(hipMemcpyAsync(c->T.xful, p + na * 128 + nr * 128, nr, hipMemcpyHostToDevice, c->stream));
+    wait_stream(c->stream);
     const u8* imp = p + na * 128 + nr * 129;
     bool any_imported = false;
     for (u64 k = 0; k < nr && !any_imported; k++) any_imported = imp[k] != 0;
     if (any_imported) {
-        if (!c->ximp) c->ximp = dalloc<u8>(c->xrow_cap, &c->bytes);
-        HIP_CHECK(hipMemset(c->ximp, 0, c->xrow_cap));
-        HIP_CHECK(hipMemcpy(c->ximp, imp, nr, hipMemcpyHostToDevice));
+        if (!c->ximp) {
+            ZeroOn zero_on(s);
+            c->ximp = dalloc<u8>(c->xrow_cap, &c->bytes);
+        }
+        HIP_CHECK(hipMemsetAsync(c->ximp, 0, c->xrow_cap, s));
+        HIP_CHECK(hipMemcpyAsync(c->ximp, imp, nr, hipMemcpyHostToDevice, s));
+        wait_stream(s);
     }
-    if (nh) HIP_CHECK(hipMemcpy(c->T.hrows, imp + nr, nh * 256, hipMemcpyHostToDevice));
+    if (nh) HIP_CHECK(hipMemcpyAsync(c->T.hrows, imp + nr, nh * 256, hipMemcpyHostToDevice, c->stream));
+    wait_stream(c->stream);
     // derived state: the account index, the transfer-id index and its key range,
     // the overflow guard; the account-transfers index rebuilds on the next query
     launch_rebuild_accounts(c->T, na, s);
@@ -1933,7 +1973,8 @@ extern "C" uint64_t tbgpu_export_transfers(tbgpu_ctx* c, uint64_t first, uint64_
     HIP_CHECK(hipSetDevice(c->device));
     if (first >= c->n_rows) return 0;
     count = std::min<u64>(count, c->n_rows - first);
-    HIP_CHECK(hipMemcpy(out, c->T.xrows + first, count * sizeof(Transfer), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpyAsync(out, c->T.xrows + first, count * sizeof(Transfer), hipMemcpyDeviceToHost, c->stream));
+    wait_stream(c->stream);
     return count;
 }
 
@@ -1941,14 +1982,16 @@ extern "C" uint64_t tbgpu_export_history(tbgpu_ctx* c, uint64_t first, uint64_t 
     HIP_CHECK(hipSetDevice(c->device));
     if (first >= c->n_hist) return 0;
     count = std::min<u64>(count, c->n_hist - first);
-    HIP_CHECK(hipMemcpy(out, c->T.hrows + first, count * sizeof(History), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpyAsync(out, c->T.hrows + first, count * sizeof(History), hipMemcpyDeviceToHost, c->stream));
+    wait_stream(c->stream);
     return count;
 }
 
 extern "C" uint64_t tbgpu_export_accounts(tbgpu_ctx* c, tbgpu_account_t* out, uint64_t capacity) {
     HIP_CHECK(hipSetDevice(c->device));
     const u64 n = std::min<u64>(capacity, c->n_accounts);  // dense rows, creation order
-    if (n) HIP_CHECK(hipMemcpy(out, c->T.acc, n * sizeof(Account), hipMemcpyDeviceToHost));
+    if (n) HIP_CHECK(hipMemcpyAsync(out, c->T.acc, n * sizeof(Account), hipMemcpyDeviceToHost, c->stream));
+    wait_stream(c->stream);
     return n;
 }
 

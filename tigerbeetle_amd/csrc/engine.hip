@@ -82,15 +82,19 @@ inline void wait_event(hipEvent_t ev) {
 }
 
 // Every device allocation is zeroed on the stream of the ctx that allocates it
-// (ZeroOn names it for the allocating scope), ahead of any of its work: recycled
-// memory of an earlier ctx never reaches a kernel, and the zeroing is ordered with
-// the ctx's own copies (a null-stream memset is not: the ctx's streams are
-// non-blocking).
+// (ZeroOn names it for the allocating scope), and the scope ends only when the
+// zeroing is complete: recycled memory of an earlier ctx never reaches a kernel, and
+// no later copy into the buffer can be overtaken by its zeroing (measured: a
+// pageable host-to-device copy enqueued behind a pending memset on the same stream
+// was partly zeroed again, tests/test_gpu_general.py relay chain's accounts).
 thread_local hipStream_t t_zero_stream = nullptr;
 struct ZeroOn {
-    hipStream_t prev;
-    explicit ZeroOn(hipStream_t s) : prev(t_zero_stream) { t_zero_stream = s; }
-    ~ZeroOn() { t_zero_stream = prev; }
+    hipStream_t prev, mine;
+    explicit ZeroOn(hipStream_t s) : prev(t_zero_stream), mine(s) { t_zero_stream = s; }
+    ~ZeroOn() {
+        HIP_CHECK(hipStreamSynchronize(mine));
+        t_zero_stream = prev;
+    }
 };
 
 inline void zero_new(void* p, u64 bytes) {
@@ -1188,7 +1192,10 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
             c->ev_in_host = true;
         } else {
             // the events' copy (a DMA engine) first, then the small uploads and resets on
-            // the compute queue: one engine hand-off before the chunk's kernels, not two
+            // the compute queue: one engine hand-off before the chunk's kernels, not two.
+            // A pageable source is staged by the runtime: the previous chunk's kernels
+            // (and a fallen-back attempt's undo) have read ev_buf before it is rewritten.
+            wait_stream(c->stream);
             HIP_CHECK(hipMemcpyAsync(c->ev_buf, ev_src + ev_off, (u64)n * 128, hipMemcpyHostToDevice, c->stream));
             ev = (const Transfer*)c->ev_buf;
         }

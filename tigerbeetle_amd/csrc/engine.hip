@@ -81,23 +81,29 @@ inline void wait_event(hipEvent_t ev) {
     }
 }
 
-// Every device allocation is zeroed on the stream of the ctx that allocates it
-// (ZeroOn names it for the allocating scope), and the scope ends only when the
-// zeroing is complete: recycled memory of an earlier ctx never reaches a kernel, and
-// no later copy into the buffer can be overtaken by its zeroing (measured: a
-// pageable host-to-device copy enqueued behind a pending memset on the same stream
-// was partly zeroed again, tests/test_gpu_general.py relay chain's accounts).
+// TBGPU_ZERO_ALLOC=1 (diagnostics): every device allocation is zeroed on the stream
+// of the ctx that allocates it (ZeroOn names it for the allocating scope), and the
+// scope ends only when the zeroing is complete, so no buffer starts with an earlier
+// ctx's contents.  Off by default: after 110 GPU tests in one process, a zeroed ctx's
+// first create_accounts read zero ids for scattered events of its relay-chain batch
+// (tests/test_gpu_general.py), which the same test alone and a fresh process do not
+// show (profiles/r03/acc_copy_probe.py) -- under investigation.
 thread_local hipStream_t t_zero_stream = nullptr;
+inline bool zero_alloc() {
+    static const bool z = getenv("TBGPU_ZERO_ALLOC") != nullptr;
+    return z;
+}
 struct ZeroOn {
     hipStream_t prev, mine;
     explicit ZeroOn(hipStream_t s) : prev(t_zero_stream), mine(s) { t_zero_stream = s; }
     ~ZeroOn() {
-        HIP_CHECK(hipStreamSynchronize(mine));
+        if (zero_alloc()) HIP_CHECK(hipStreamSynchronize(mine));
         t_zero_stream = prev;
     }
 };
 
 inline void zero_new(void* p, u64 bytes) {
+    if (!zero_alloc()) return;
     if (!t_zero_stream) tbgpu_fatal("alloc", "device allocation outside a ZeroOn scope", __FILE__, __LINE__);
     HIP_CHECK(hipMemsetAsync(p, 0, bytes, t_zero_stream));
 }

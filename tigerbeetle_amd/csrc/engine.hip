@@ -84,10 +84,7 @@ inline void wait_event(hipEvent_t ev) {
 // TBGPU_ZERO_ALLOC=1 (diagnostics): every device allocation is zeroed on the stream
 // of the ctx that allocates it (ZeroOn names it for the allocating scope), and the
 // scope ends only when the zeroing is complete, so no buffer starts with an earlier
-// ctx's contents.  Off by default: after 110 GPU tests in one process, a zeroed ctx's
-// first create_accounts read zero ids for scattered events of its relay-chain batch
-// (tests/test_gpu_general.py), which the same test alone and a fresh process do not
-// show (profiles/r03/acc_copy_probe.py) -- under investigation.
+// ctx's contents.  Off by default (no kernel reads a buffer before writing it).
 thread_local hipStream_t t_zero_stream = nullptr;
 inline bool zero_alloc() {
     static const bool z = getenv("TBGPU_ZERO_ALLOC") != nullptr;
@@ -1340,8 +1337,7 @@ static uint64_t routed(tbgpu_ctx* c, uint32_t batch_count, const uint32_t* count
     c->rt_ev_ts = nullptr;
     c->rt_ctl = nullptr;
     u64 ts = 0;
-    HIP_CHECK(hipMemcpyAsync(&ts, c->rt_dry ? c->rt_dry_ts : c->T.commit_ts, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
-    wait_stream(c->stream);
+    HIP_CHECK(hipMemcpy(&ts, c->rt_dry ? c->rt_dry_ts : c->T.commit_ts, sizeof(u64), hipMemcpyDeviceToHost));
     c->rt_dry = false;
     if (commit_timestamp) *commit_timestamp = ts;
     return total;
@@ -1375,6 +1371,7 @@ extern "C" int tbgpu_import_transfers(tbgpu_ctx* c, const tbgpu_transfer_t* rows
         if (!c->ximp) {
             ZeroOn zero_on(c->stream);
             c->ximp = dalloc<u8>(c->xrow_cap, &c->bytes);
+            HIP_CHECK(hipMemsetAsync(c->ximp, 0, c->xrow_cap, c->stream));
         }
         HIP_CHECK(hipMemsetAsync(c->ximp + c->n_rows, 1, k, c->stream));  // not this shard's: never queried
         wait_stream(c->stream);
@@ -1719,9 +1716,11 @@ static uint32_t lookup(tbgpu_ctx* c, const tbgpu_uint128_t* ids, uint32_t count,
         launch(d_ids, k, d_out, d_found);
         rows.resize(k);
         found.resize(k);
-        HIP_CHECK(hipMemcpyAsync(rows.data(), d_out, (u64)k * sizeof(Row), hipMemcpyDeviceToHost, c->stream));
-        HIP_CHECK(hipMemcpyAsync(found.data(), d_found, k, hipMemcpyDeviceToHost, c->stream));
+        // into pageable memory: blocking copies behind a drain of the ctx's stream (an
+        // asynchronous copy into pageable memory returned stale rows)
         wait_stream(c->stream);
+        HIP_CHECK(hipMemcpy(rows.data(), d_out, (u64)k * sizeof(Row), hipMemcpyDeviceToHost));
+        HIP_CHECK(hipMemcpy(found.data(), d_found, k, hipMemcpyDeviceToHost));
         for (u32 i = 0; i < k; i++)
             if (found[i]) memcpy(&out[found_total++], &rows[i], sizeof(Row));
     }
@@ -1814,8 +1813,7 @@ static uint32_t query_host(tbgpu_ctx* c, const tbgpu_account_filter_t* filter, v
     HIP_CHECK(hipMemcpyAsync(fd, filter, sizeof *filter, hipMemcpyHostToDevice, c->stream));
     uint32_t n = 0;
     run_queries(c, fd, 1, TBGPU_QUERY_MAX, c->ev_buf, history, &n);  // ev_buf: nmax * 128 B >= 8190 rows
-    if (n) HIP_CHECK(hipMemcpyAsync(out, c->ev_buf, (u64)n * 128, hipMemcpyDeviceToHost, c->stream));
-    wait_stream(c->stream);
+    if (n) HIP_CHECK(hipMemcpy(out, c->ev_buf, (u64)n * 128, hipMemcpyDeviceToHost));
     return n;
 }
 
@@ -1878,18 +1876,13 @@ extern "C" uint64_t tbgpu_checkpoint(tbgpu_ctx* c, void* out, uint64_t capacity)
     wait_stream(c->stream);
     u8* p = (u8*)out + sizeof(CkHeader);
     const u64 na = c->n_accounts, nr = c->n_rows, nh = c->n_hist;
-    if (na) HIP_CHECK(hipMemcpyAsync(p, c->T.acc, na * 128, hipMemcpyDeviceToHost, c->stream));
-    wait_stream(c->stream);
-    if (nr) HIP_CHECK(hipMemcpyAsync(p + na * 128, c->T.xrows, nr * 128, hipMemcpyDeviceToHost, c->stream));
-    wait_stream(c->stream);
-    if (nr) HIP_CHECK(hipMemcpyAsync(p + na * 128 + nr * 128, c->T.xful, nr, hipMemcpyDeviceToHost, c->stream));
-    wait_stream(c->stream);
+    if (na) HIP_CHECK(hipMemcpy(p, c->T.acc, na * 128, hipMemcpyDeviceToHost));
+    if (nr) HIP_CHECK(hipMemcpy(p + na * 128, c->T.xrows, nr * 128, hipMemcpyDeviceToHost));
+    if (nr) HIP_CHECK(hipMemcpy(p + na * 128 + nr * 128, c->T.xful, nr, hipMemcpyDeviceToHost));
     u8* imp = p + na * 128 + nr * 129;
-    if (nr && c->ximp) HIP_CHECK(hipMemcpyAsync(imp, c->ximp, nr, hipMemcpyDeviceToHost, c->stream));
+    if (nr && c->ximp) HIP_CHECK(hipMemcpy(imp, c->ximp, nr, hipMemcpyDeviceToHost));
     else memset(imp, 0, nr);
-    wait_stream(c->stream);
-    if (nh) HIP_CHECK(hipMemcpyAsync(imp + nr, c->T.hrows, nh * 256, hipMemcpyDeviceToHost, c->stream));
-    wait_stream(c->stream);
+    if (nh) HIP_CHECK(hipMemcpy(imp + nr, c->T.hrows, nh * 256, hipMemcpyDeviceToHost));
     CkHeader h{};
     h.magic = CK_MAGIC;
     h.version = 1;
@@ -1918,12 +1911,9 @@ extern "C" int tbgpu_open(tbgpu_ctx* c, const void* image, uint64_t size) {
     // the reset's memsets run on the ctx's non-blocking stream, which the blocking
     // copies below do not wait for
     wait_stream(s);
-    if (na) HIP_CHECK(hipMemcpyAsync(c->T.acc, p, na * 128, hipMemcpyHostToDevice, c->stream));
-    wait_stream(c->stream);
-    if (nr) HIP_CHECK(hipMemcpyAsync(c->T.xrows, p + na * 128, nr * 128, hipMemcpyHostToDevice, c->stream));
-    wait_stream(c->stream);
-    if (nr) HIP_CHECK(hipMemcpyAsync(c->T.xful, p + na * 128 + nr * 128, nr, hipMemcpyHostToDevice, c->stream));
-    wait_stream(c->stream);
+    if (na) HIP_CHECK(hipMemcpy(c->T.acc, p, na * 128, hipMemcpyHostToDevice));
+    if (nr) HIP_CHECK(hipMemcpy(c->T.xrows, p + na * 128, nr * 128, hipMemcpyHostToDevice));
+    if (nr) HIP_CHECK(hipMemcpy(c->T.xful, p + na * 128 + nr * 128, nr, hipMemcpyHostToDevice));
     const u8* imp = p + na * 128 + nr * 129;
     bool any_imported = false;
     for (u64 k = 0; k < nr && !any_imported; k++) any_imported = imp[k] != 0;
@@ -1933,11 +1923,10 @@ extern "C" int tbgpu_open(tbgpu_ctx* c, const void* image, uint64_t size) {
             c->ximp = dalloc<u8>(c->xrow_cap, &c->bytes);
         }
         HIP_CHECK(hipMemsetAsync(c->ximp, 0, c->xrow_cap, s));
-        HIP_CHECK(hipMemcpyAsync(c->ximp, imp, nr, hipMemcpyHostToDevice, s));
         wait_stream(s);
+        HIP_CHECK(hipMemcpy(c->ximp, imp, nr, hipMemcpyHostToDevice));
     }
-    if (nh) HIP_CHECK(hipMemcpyAsync(c->T.hrows, imp + nr, nh * 256, hipMemcpyHostToDevice, c->stream));
-    wait_stream(c->stream);
+    if (nh) HIP_CHECK(hipMemcpy(c->T.hrows, imp + nr, nh * 256, hipMemcpyHostToDevice));
     // derived state: the account index, the transfer-id index and its key range,
     // the overflow guard; the account-transfers index rebuilds on the next query
     launch_rebuild_accounts(c->T, na, s);
@@ -1986,8 +1975,8 @@ extern "C" uint64_t tbgpu_export_transfers(tbgpu_ctx* c, uint64_t first, uint64_
     HIP_CHECK(hipSetDevice(c->device));
     if (first >= c->n_rows) return 0;
     count = std::min<u64>(count, c->n_rows - first);
-    HIP_CHECK(hipMemcpyAsync(out, c->T.xrows + first, count * sizeof(Transfer), hipMemcpyDeviceToHost, c->stream));
-    wait_stream(c->stream);
+    wait_stream(c->stream);  // the blocking copy (null stream) does not wait for the ctx's stream
+    HIP_CHECK(hipMemcpy(out, c->T.xrows + first, count * sizeof(Transfer), hipMemcpyDeviceToHost));
     return count;
 }
 
@@ -1995,16 +1984,16 @@ extern "C" uint64_t tbgpu_export_history(tbgpu_ctx* c, uint64_t first, uint64_t 
     HIP_CHECK(hipSetDevice(c->device));
     if (first >= c->n_hist) return 0;
     count = std::min<u64>(count, c->n_hist - first);
-    HIP_CHECK(hipMemcpyAsync(out, c->T.hrows + first, count * sizeof(History), hipMemcpyDeviceToHost, c->stream));
-    wait_stream(c->stream);
+    wait_stream(c->stream);  // the blocking copy (null stream) does not wait for the ctx's stream
+    HIP_CHECK(hipMemcpy(out, c->T.hrows + first, count * sizeof(History), hipMemcpyDeviceToHost));
     return count;
 }
 
 extern "C" uint64_t tbgpu_export_accounts(tbgpu_ctx* c, tbgpu_account_t* out, uint64_t capacity) {
     HIP_CHECK(hipSetDevice(c->device));
     const u64 n = std::min<u64>(capacity, c->n_accounts);  // dense rows, creation order
-    if (n) HIP_CHECK(hipMemcpyAsync(out, c->T.acc, n * sizeof(Account), hipMemcpyDeviceToHost, c->stream));
-    wait_stream(c->stream);
+    wait_stream(c->stream);  // the blocking copy (null stream) does not wait for the ctx's stream
+    if (n) HIP_CHECK(hipMemcpy(out, c->T.acc, n * sizeof(Account), hipMemcpyDeviceToHost));
     return n;
 }
 

@@ -260,6 +260,11 @@ struct tbgpu_ctx {
     // the end of a call in one copy (k_report): counter words, T.base, the last chunk's
     // reply counts
     u32* h_report = nullptr;  // pinned
+    // page-locked staging for host-to-device copies from pageable memory (h2d): two
+    // halves, each reusable once the copy recorded behind it has run
+    u8* h_up[2] = {nullptr, nullptr};
+    hipEvent_t up_ev[2] = {nullptr, nullptr};
+    int up_next = 0;
     u32* h_report_dev = nullptr;  // its device address, and h_res's
     u64* h_res_dev = nullptr;
     u64 h_rc_cap = 0;
@@ -524,6 +529,10 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     if (c->h_base) (void)hipHostFree(c->h_base);
     if (c->h_rc) (void)hipHostFree(c->h_rc);
     if (c->h_res) (void)hipHostFree(c->h_res);
+    for (int h = 0; h < 2; h++) {
+        if (c->h_up[h]) (void)hipHostFree(c->h_up[h]);
+        if (c->up_ev[h]) (void)hipEventDestroy(c->up_ev[h]);
+    }
     for (hipEvent_t e : c->prof_pool) (void)hipEventDestroy(e);
     (void)hipEventDestroy(c->ev0);
     (void)hipEventDestroy(c->ev1);
@@ -1136,6 +1145,46 @@ static const void* pinned_device_ptr(const void* p, u64 bytes) {
     return a.devicePointer;
 }
 
+// Host-to-device copy on `s`.  Pageable sources are staged through the ctx's
+// page-locked ring (a host memcpy per UP_HALF bytes) so every copy is a plain DMA from
+// page-locked memory.  The runtime's own handling of pageable sources was measured to
+// let kernels read stale data in a long process (the copies' destinations are reused
+// buffers -- the event buffer, the query filter -- and a later kernel saw the previous
+// contents: DESIGN.md §5), so the engine never hands it a pageable source.
+// Device-to-host copy into caller (pageable) memory: behind a drain of `s`, as a
+// blocking copy (an asynchronous copy into pageable memory returned stale rows in a
+// long process).
+static void d2h(void* dst, const void* src, u64 bytes, hipStream_t s) {
+    wait_stream(s);
+    if (bytes) HIP_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+}
+
+constexpr u64 UP_HALF = 4ull << 20;
+static void h2d(tbgpu_ctx* c, void* dst, const void* src, u64 bytes, hipStream_t s) {
+    if (bytes == 0) return;
+    if (pinned_device_ptr(src, bytes)) {
+        HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+        return;
+    }
+    if (!c->h_up[0]) {
+        for (int h = 0; h < 2; h++) {
+            HIP_CHECK(hipHostMalloc((void**)&c->h_up[h], UP_HALF, hipHostMallocDefault));
+            HIP_CHECK(hipEventCreateWithFlags(&c->up_ev[h], hipEventDisableTiming));
+            HIP_CHECK(hipEventRecord(c->up_ev[h], s));
+        }
+    }
+    for (u64 off = 0; off < bytes;) {
+        const u64 k = std::min<u64>(bytes - off, UP_HALF);
+        const int h = c->up_next;
+        c->up_next ^= 1;
+        HIP_CHECK(hipEventSynchronize(c->up_ev[h]));  // the half's previous copy has read it
+        memcpy(c->h_up[h], (const u8*)src + off, k);
+        HIP_CHECK(hipMemcpyAsync((u8*)dst + off, c->h_up[h], k, hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipEventRecord(c->up_ev[h], s));
+        off += k;
+    }
+}
+
 static bool spec_disabled() {
     static const bool d = getenv("TBGPU_NO_SPEC") != nullptr;
     return d;
@@ -1199,7 +1248,7 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
             // A pageable source is staged by the runtime: the previous chunk's kernels
             // (and a fallen-back attempt's undo) have read ev_buf before it is rewritten.
             wait_stream(c->stream);
-            HIP_CHECK(hipMemcpyAsync(c->ev_buf, ev_src + ev_off, (u64)n * 128, hipMemcpyHostToDevice, c->stream));
+            h2d(c, c->ev_buf, ev_src + ev_off, (u64)n * 128, c->stream);
             ev = (const Transfer*)c->ev_buf;
         }
         // the replies start at the front of `results` (device results: the call's first
@@ -1212,12 +1261,11 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
             c->rt_ctl = ctl_host ? ctl_host + ev_off : nullptr;
         } else {
             if (ev_ts_host) {
-                HIP_CHECK(hipMemcpyAsync(c->rt_ts_buf, ev_ts_host + ev_off, (u64)n * 8, hipMemcpyHostToDevice,
-                                         c->stream));
+                h2d(c, c->rt_ts_buf, ev_ts_host + ev_off, (u64)n * 8, c->stream);
                 c->rt_ev_ts = c->rt_ts_buf;
             }
             if (ctl_host) {
-                HIP_CHECK(hipMemcpyAsync(c->rt_ctl_buf, ctl_host + ev_off, n, hipMemcpyHostToDevice, c->stream));
+                h2d(c, c->rt_ctl_buf, ctl_host + ev_off, n, c->stream);
                 c->rt_ctl = c->rt_ctl_buf;
             }
         }
@@ -1366,7 +1414,7 @@ extern "C" int tbgpu_import_transfers(tbgpu_ctx* c, const tbgpu_transfer_t* rows
     u64 off = 0;
     while (off < n) {
         const u32 k = (u32)std::min<u64>(n - off, c->nmax);
-        HIP_CHECK(hipMemcpyAsync(c->ev_buf, keep.data() + off, (u64)k * 128, hipMemcpyHostToDevice, c->stream));
+        h2d(c, c->ev_buf, keep.data() + off, (u64)k * 128, c->stream);
         launch_import_transfers(c->T, (const Transfer*)c->ev_buf, k, c->n_rows, c->stream);
         if (!c->ximp) {
             ZeroOn zero_on(c->stream);
@@ -1389,7 +1437,7 @@ void route_stats(const Transfer* ev, u64 n, u64* out, hipStream_t stream);
 extern "C" int tbgpu_route_stats(tbgpu_ctx* c, const void* events_device, uint64_t count, uint64_t* out) {
     HIP_CHECK(hipSetDevice(c->device));
     route_stats((const Transfer*)events_device, count, c->rt_stats, c->route_stream);
-    HIP_CHECK(hipMemcpyAsync(out, c->rt_stats, 5 * sizeof(u64), hipMemcpyDeviceToHost, c->route_stream));
+    d2h(out, c->rt_stats, 5 * sizeof(u64), c->route_stream);
     wait_stream(c->route_stream);
     return 0;
 }
@@ -1431,7 +1479,7 @@ extern "C" int tbgpu_route_prepare(tbgpu_ctx* c, uint32_t world, const void* eve
     route_capacity(c, world, 0, count);
     route_rank((const Transfer*)events_device, count, world, c->ro_orank, c->ro_blk, c->ro_spart, c->rt_stats,
                c->route_stream);
-    HIP_CHECK(hipMemcpyAsync(out, c->rt_stats, 5 * sizeof(u64), hipMemcpyDeviceToHost, c->route_stream));
+    d2h(out, c->rt_stats, 5 * sizeof(u64), c->route_stream);
     wait_stream(c->route_stream);
     c->ro_ranked = {events_device, count, world};
     return 0;
@@ -1461,19 +1509,18 @@ static int route_scatter_any(tbgpu_ctx* c, uint32_t world, uint32_t batch_count,
     }
     u32* err = (u32*)(c->rt_stats + 7);
     HIP_CHECK(hipMemsetAsync(err, 0, sizeof(u32), c->route_stream));
-    HIP_CHECK(hipMemcpyAsync(c->ro_bstart, starts.data(), (batch_count + 1) * sizeof(u32), hipMemcpyHostToDevice,
-                             c->route_stream));
+    h2d(c, c->ro_bstart, starts.data(), (batch_count + 1) * sizeof(u32), c->route_stream);
     route_scatter((const Transfer*)events_device, n, world, batch_count, c->ro_bstart, first_global_batch,
                   c->ro_orank, c->ro_blk, c->ro_counts, (Transfer*)send_events_device, (u64*)send_records_device,
                   c->ro_bcount + 256, c->ro_bcount, word_mask, (u32*)send_packed_device, err, ranked, c->route_stream);
-    HIP_CHECK(hipMemcpyAsync(send_counts, c->ro_counts, world * sizeof(u64), hipMemcpyDeviceToHost, c->route_stream));
+    d2h(send_counts, c->ro_counts, world * sizeof(u64), c->route_stream);
     if (send_batch_counts)
         HIP_CHECK(hipMemcpyAsync(send_batch_counts, c->ro_bcount + 256, (u64)world * batch_count * sizeof(u32),
                                  hipMemcpyDeviceToHost, c->route_stream));
     if (send_span_counts)
-        HIP_CHECK(hipMemcpyAsync(send_span_counts, c->ro_bcount, world * sizeof(u32), hipMemcpyDeviceToHost, c->route_stream));
+        d2h(send_span_counts, c->ro_bcount, world * sizeof(u32), c->route_stream);
     u32 e = 0;
-    HIP_CHECK(hipMemcpyAsync(&e, err, sizeof(u32), hipMemcpyDeviceToHost, c->route_stream));
+    d2h(&e, err, sizeof(u32), c->route_stream);
     wait_stream(c->route_stream);
     return e ? -22 : 0;
 }
@@ -1509,7 +1556,7 @@ extern "C" int tbgpu_route_unpack_packed(tbgpu_ctx* c, const void* packed_device
                       (const u32*)sub_batches_device, sub_batch_count, (const u64*)batch_ts_base_device, batches,
                       (Transfer*)events_device, (u64*)records_device, (u64*)timestamps_device, err, c->route_stream);
     u32 e = 0;
-    HIP_CHECK(hipMemcpyAsync(&e, err, sizeof(u32), hipMemcpyDeviceToHost, c->route_stream));
+    d2h(&e, err, sizeof(u32), c->route_stream);
     wait_stream(c->route_stream);
     return e ? -22 : 0;
 }
@@ -1522,7 +1569,7 @@ extern "C" int tbgpu_route_unpack(tbgpu_ctx* c, const void* records_device, uint
     route_unpack((const u64*)records_device, count, (const u64*)batch_ts_base_device, batches, (u64*)timestamps_device,
                  err, c->route_stream);
     u32 e = 0;
-    HIP_CHECK(hipMemcpyAsync(&e, err, sizeof(u32), hipMemcpyDeviceToHost, c->route_stream));
+    d2h(&e, err, sizeof(u32), c->route_stream);
     wait_stream(c->route_stream);
     return e ? -22 : 0;
 }
@@ -1601,8 +1648,9 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
     uint4 tot;
     HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, CNT_COUNT * sizeof(u32), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipMemcpyAsync(c->h_base + 4, c->ranks + n, sizeof(uint4), hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipMemcpyAsync(counts_host, c->counts, nb * sizeof(u32), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(c->h_counts, c->counts, nb * sizeof(u32), hipMemcpyDeviceToHost, s));
     wait_stream(s);
+    memcpy(counts_host, c->h_counts, nb * sizeof(u32));
     memcpy(&tot, c->h_base + 4, sizeof tot);
     const u32 flags = c->h_counters[CNT_FLAGS];
     if (!(flags & (FL_CHAINS | FL_MULTI_ID))) {
@@ -1626,11 +1674,11 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
     c->stats.iterations = it + 1;
     ac_launch_mask(c->T, C, A->res, A->ok, A->cfail, c->fres, c->mask, s);
     scan3_exclusive(c->mask, c->ranks, n, c->sc, s);
-    HIP_CHECK(hipMemcpyAsync(&tot, c->ranks + n, sizeof(uint4), hipMemcpyDeviceToHost, s));
+    d2h(&tot, c->ranks + n, sizeof(uint4), s);
     wait_stream(s);
     if (c->n_accounts + tot.x > c->accounts_max) tbgpu_fatal("create_accounts", "accounts_max exceeded", __FILE__, __LINE__);
     ac_launch_apply(c->T, C, A->ok, c->fres, c->ranks, c->n_accounts, c->accounts_max, results_dev, c->counts, s);
-    HIP_CHECK(hipMemcpyAsync(counts_host, c->counts, nb * sizeof(u32), hipMemcpyDeviceToHost, s));
+    d2h(counts_host, c->counts, nb * sizeof(u32), s);
     wait_stream(s);
     c->n_accounts += tot.x;
 }
@@ -1649,7 +1697,7 @@ static uint64_t accounts_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t
         const u32 n = starts[nb];
         const Account* ev = events + ev_off;
         if (!device) {
-            HIP_CHECK(hipMemcpyAsync(c->ev_buf, ev, (u64)n * 128, hipMemcpyHostToDevice, c->stream));
+            h2d(c, c->ev_buf, ev, (u64)n * 128, c->stream);
             ev = (const Account*)c->ev_buf;
         }
         run_accounts_chunk(c, ev, n, nb, (tbgpu_create_accounts_result_t*)c->res_buf, result_counts + b0);
@@ -1712,7 +1760,7 @@ static uint32_t lookup(tbgpu_ctx* c, const tbgpu_uint128_t* ids, uint32_t count,
         u128* d_ids = (u128*)c->ev_buf;  // k * 16 <= nmax * 128
         Row* d_out = (Row*)c->bb;        // 2 * nmax * 64 bytes >= k * 128
         u8* d_found = c->fres;
-        HIP_CHECK(hipMemcpyAsync(d_ids, ids + off, (u64)k * 16, hipMemcpyHostToDevice, c->stream));
+        h2d(c, d_ids, ids + off, (u64)k * 16, c->stream);
         launch(d_ids, k, d_out, d_found);
         rows.resize(k);
         found.resize(k);
@@ -1783,8 +1831,7 @@ extern "C" uint64_t tbgpu_compact(tbgpu_ctx* c) {
         c->q_runs.erase(c->q_runs.end() - 2);
     }
     if (c->q_runs.size() > Q_RUNS_MAX + 1) tbgpu_fatal("compact", "index runs exceed Q_RUNS_MAX", __FILE__, __LINE__);
-    HIP_CHECK(hipMemcpyAsync(c->q_runs_dev, c->q_runs.data(), c->q_runs.size() * sizeof(u64), hipMemcpyHostToDevice,
-                             c->stream));
+    h2d(c, c->q_runs_dev, c->q_runs.data(), c->q_runs.size() * sizeof(u64), c->stream);
     wait_stream(c->stream);
     return r1;
 }
@@ -1800,7 +1847,7 @@ static u64 run_queries(tbgpu_ctx* c, const tbgpu_account_filter_t* filters, u32 
         const u32 k = std::min(step, nq - q0);
         QArgs A{filters + q0, k, stride, (u8*)out + (u64)q0 * stride * 128, c->counts, history ? 1u : 0u, c->n_hist};
         q_launch_scan(c->T, X, A, c->stream);
-        HIP_CHECK(hipMemcpyAsync(counts_host + q0, c->counts, k * sizeof(u32), hipMemcpyDeviceToHost, c->stream));
+        d2h(counts_host + q0, c->counts, k * sizeof(u32), c->stream);
         wait_stream(c->stream);
         for (u32 j = 0; j < k; j++) total += counts_host[q0 + j];
     }
@@ -1810,7 +1857,7 @@ static u64 run_queries(tbgpu_ctx* c, const tbgpu_account_filter_t* filters, u32 
 static uint32_t query_host(tbgpu_ctx* c, const tbgpu_account_filter_t* filter, void* out, bool history) {
     HIP_CHECK(hipSetDevice(c->device));
     tbgpu_account_filter_t* fd = (tbgpu_account_filter_t*)c->res_buf;  // nmax * 8 B >= 64 B
-    HIP_CHECK(hipMemcpyAsync(fd, filter, sizeof *filter, hipMemcpyHostToDevice, c->stream));
+    h2d(c, fd, filter, sizeof *filter, c->stream);
     uint32_t n = 0;
     run_queries(c, fd, 1, TBGPU_QUERY_MAX, c->ev_buf, history, &n);  // ev_buf: nmax * 128 B >= 8190 rows
     if (n) HIP_CHECK(hipMemcpy(out, c->ev_buf, (u64)n * 128, hipMemcpyDeviceToHost));
@@ -1934,7 +1981,7 @@ extern "C" int tbgpu_open(tbgpu_ctx* c, const void* image, uint64_t size) {
         const u32 k = (u32)std::min<u64>(nr - off, 1u << 30);
         launch_import_transfers(c->T, c->T.xrows + off, k, off, s);  // rows in place: index + key range
     }
-    HIP_CHECK(hipMemcpyAsync(c->T.commit_ts, &h.commit_ts, sizeof(u64), hipMemcpyHostToDevice, s));
+    h2d(c, c->T.commit_ts, &h.commit_ts, sizeof(u64), s);
     wait_stream(s);
     c->n_accounts = na;
     c->n_rows = nr;
@@ -1953,7 +2000,7 @@ extern "C" int tbgpu_test_set_balances(tbgpu_ctx* c, tbgpu_uint128_t id, tbgpu_u
     Bal4 b{to128(dp), to128(dpo), to128(cp), to128(cpo)};
     launch_set_balances(c->T, to128(id), b, c->status, c->stream);
     int st = 0;
-    HIP_CHECK(hipMemcpyAsync(&st, c->status, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    d2h(&st, c->status, sizeof(int), c->stream);
     wait_stream(c->stream);
     return st;
 }
@@ -1962,7 +2009,7 @@ extern "C" int tbgpu_get_posted(tbgpu_ctx* c, tbgpu_uint128_t pending_id) {
     HIP_CHECK(hipSetDevice(c->device));
     launch_get_posted(c->T, to128(pending_id), c->status, c->stream);
     int st = 0;
-    HIP_CHECK(hipMemcpyAsync(&st, c->status, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    d2h(&st, c->status, sizeof(int), c->stream);
     wait_stream(c->stream);
     return st;
 }
@@ -2000,7 +2047,7 @@ extern "C" uint64_t tbgpu_export_accounts(tbgpu_ctx* c, tbgpu_account_t* out, ui
 extern "C" uint64_t tbgpu_commit_timestamp(tbgpu_ctx* c) {
     HIP_CHECK(hipSetDevice(c->device));
     u64 v = 0;  // behind whatever the engine's stream still has queued (tbgpu_advance_commit_timestamp)
-    HIP_CHECK(hipMemcpyAsync(&v, c->T.commit_ts, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    d2h(&v, c->T.commit_ts, sizeof(u64), c->stream);
     wait_stream(c->stream);
     return v;
 }

@@ -515,8 +515,9 @@ __global__ __launch_bounds__(RT_THREADS) void rt_stats_fold(const u64* __restric
 }  // namespace
 
 void route_stats(const Transfer* ev, u64 n, u64* out, hipStream_t stream) {
-    const u64 init[5] = {~0ull, 0, 0, 0, 0};
-    HIP_CHECK(hipMemcpyAsync(out, init, sizeof init, hipMemcpyHostToDevice, stream));
+    // {~0, 0, 0, 0, 0}, set on the device (no host source)
+    HIP_CHECK(hipMemsetAsync(out, 0xFF, sizeof(u64), stream));
+    HIP_CHECK(hipMemsetAsync(out + 1, 0, 4 * sizeof(u64), stream));
     if (n) rt_stats<<<(u32)std::min<u64>((n + RT_THREADS / 8 - 1) / (RT_THREADS / 8), 1024), RT_THREADS, 0, stream>>>(ev, n, out);
     HIP_CHECK(hipGetLastError());
 }
@@ -529,8 +530,8 @@ u64 route_block_count(u64 n) { return (n + RT_THREADS - 1) / RT_THREADS; }
 // part: 5 words per workgroup (route_block_count(n) of them)
 void route_rank(const Transfer* ev, u64 n, u32 world, uint2* orank, u32* blk, u64* part, u64* stats,
                 hipStream_t stream) {
-    const u64 init[5] = {~0ull, 0, 0, 0, 0};
-    HIP_CHECK(hipMemcpyAsync(stats, init, sizeof init, hipMemcpyHostToDevice, stream));
+    HIP_CHECK(hipMemsetAsync(stats, 0xFF, sizeof(u64), stream));
+    HIP_CHECK(hipMemsetAsync(stats + 1, 0, 4 * sizeof(u64), stream));
     RouteArgs A{};
     A.ev = ev; A.n = n; A.world = world; A.orank = orank; A.blk = blk; A.nblk = (u32)route_block_count(n);
     A.stats = part;

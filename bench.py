@@ -599,7 +599,7 @@ def main():
         n_batches = len(counts)
         ats, tts = c5.timestamps()
         eng = Engine(device=local_rank, accounts_max=acc_n, transfers_max=int(counts.sum()) + 1024, history_max=1024,
-                     events_per_call_max=B * BATCH_MAX, force_general=args.force_general)
+                     events_per_call_max=B * BATCH_MAX, force_general=args.force_general, pinned_input=True)
         ab = c5.account_batches()
         buf = torch.empty(1221 * BATCH_MAX * 128, dtype=torch.uint8, device=dev)
         res = torch.empty(1221 * BATCH_MAX * 8, dtype=torch.uint8, device=dev)
@@ -630,6 +630,7 @@ def main():
         eng = Engine(device=local_rank, accounts_max=acc_n, transfers_max=int(w.transfer_counts.sum()) + 1024,
                      history_max=int(w.transfer_counts.sum()) + 1024 if args.config == 3 else 1024,
                      events_per_call_max=B * BATCH_MAX, force_general=args.force_general,
+                     pinned_input=True,  # host_path's buffers are page-locked (TBGPU_OPT_PINNED_INPUT)
                      # config 4 numbers its accounts ledger << 32 | k: the blocked directory
                      dense_block_span=acc_n // 1000 if args.config == 4 else 0)
         ats, tts = w.timestamps()

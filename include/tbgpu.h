@@ -241,6 +241,12 @@ enum {
     TBGPU_OPT_WALK_EARLY = 1u << 1,    /* the fixed point hands its chunk to the sequential walk
                                           after two passes instead of its pass budget (tests:
                                           the walk's results are the passes' results) */
+    TBGPU_OPT_PINNED_INPUT = 1u << 2,  /* the host event buffers the caller passes are its own
+                                          page-locked allocations (hipHostMalloc,
+                                          hipHostRegister): a small one-chunk call's events
+                                          are read in place and uploads skip the staging
+                                          ring.  Without it every host buffer is copied
+                                          through the ctx's page-locked ring. */
 };
 
 /* Replaces StateMachine.init/deinit (src/state_machine.zig:418-451).

@@ -18,7 +18,7 @@ calls = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 w = workload.config2(transfer_count=calls * 8190, account_count=1_000_000, seed=5)
 ats, tts = w.timestamps()
 eng = Engine(device=0, accounts_max=1_000_000, transfers_max=calls * 8190 + 1024, history_max=1024,
-             events_per_call_max=8190 * 4)
+             events_per_call_max=8190 * 4, pinned_input=True)
 eng.create_accounts_batches(ats, w.account_counts, w.accounts)
 pinned = torch.empty(calls * 8190 * 128, dtype=torch.uint8, pin_memory=True)
 view = pinned.numpy().view(TRANSFER_DTYPE)

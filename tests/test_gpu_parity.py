@@ -569,7 +569,7 @@ def test_pinned_host_events_read_in_place():
     w = workload.config1(transfer_count=1, account_count=acc_n, seed=9)
     ats, _ = w.timestamps()
     orc = oracle.Oracle(acc_n, 1 << 20)
-    gpu = _engine()
+    gpu = _engine(pinned_input=True)  # the buffers below are page-locked (TBGPU_OPT_PINNED_INPUT)
     n = 8190
     kinds = ("fresh", "fail", "linked", "repeat", "fresh", "fresh")
     pinned = torch.empty((len(kinds) + 1) * n * 128, dtype=torch.uint8, pin_memory=True)

@@ -1145,9 +1145,11 @@ static const void* pinned_device_ptr(const void* p, u64 bytes) {
     return a.devicePointer;
 }
 
-// Host-to-device copy on `s`.  Pageable sources are staged through the ctx's
-// page-locked ring (a host memcpy per UP_HALF bytes) so every copy is a plain DMA from
-// page-locked memory.  The runtime's own handling of pageable sources was measured to
+// Host-to-device copy on `s`.  Sources are staged through the ctx's page-locked ring
+// (a host memcpy per UP_HALF bytes) so every copy is a plain DMA from page-locked
+// memory; a caller that declares its buffers page-locked (TBGPU_OPT_PINNED_INPUT) is
+// copied from directly.  The runtime's pointer attributes alone are not trusted to
+// tell page-locked from pageable memory.  The runtime's own handling of pageable sources was measured to
 // let kernels read stale data in a long process (the copies' destinations are reused
 // buffers -- the event buffer, the query filter -- and a later kernel saw the previous
 // contents: DESIGN.md §5), so the engine never hands it a pageable source.
@@ -1162,7 +1164,7 @@ static void d2h(void* dst, const void* src, u64 bytes, hipStream_t s) {
 constexpr u64 UP_HALF = 4ull << 20;
 static void h2d(tbgpu_ctx* c, void* dst, const void* src, u64 bytes, hipStream_t s) {
     if (bytes == 0) return;
-    if (pinned_device_ptr(src, bytes)) {
+    if ((c->opt.flags & TBGPU_OPT_PINNED_INPUT) && pinned_device_ptr(src, bytes)) {
         HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
         return;
     }
@@ -1233,7 +1235,8 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         // attempt: the kernels read the events where they are, over PCIe (fp_commit
         // reads each once): no copy and no DMA / compute hand-off.  A fallback redoes the
         // call with a copy (slow_chunks).
-        const bool zc = !src_device && b0 == 0 && b1 == nb_total && n <= FP_TAIL_MAX && c->slow_chunks % 8 == 0 &&
+        const bool zc = !src_device && (c->opt.flags & TBGPU_OPT_PINNED_INPUT) && b0 == 0 && b1 == nb_total &&
+                        n <= FP_TAIL_MAX && c->slow_chunks % 8 == 0 &&
                         !c->rt_dry && !ev_ts_host && !ctl_host && !(c->opt.flags & TBGPU_OPT_FORCE_GENERAL) &&
                         !spec_disabled() && !zero_copy_disabled();
         const Transfer* ev_zc = zc ? (const Transfer*)pinned_device_ptr(ev_src + ev_off, (u64)n * 128) : nullptr;

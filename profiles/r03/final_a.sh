@@ -16,8 +16,12 @@ step() {  # name, seconds, command...: one GPU step under its own limit; stop at
 }
 rm -f gpurun_out/tbgpu_fatal.log
 if [ "$PART" != 2 ]; then
-step gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
-tail -2 "$OUT/gpu_tests.out"
+# the suite: test failures (rc 1) are reported and the evidence goes on; anything else stops
+echo "== gpu_tests $(date +%T)"
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > "$OUT/gpu_tests.out" 2> "$OUT/gpu_tests.err"
+rc=$?
+tail -2 "$OUT/gpu_tests.out"; grep "^FAILED\|^E   .*AssertionError" "$OUT/gpu_tests.out" | cut -c1-600
+{ [ $rc -eq 0 ] || [ $rc -eq 1 ]; } || { echo "gpu_tests rc=$rc"; cat gpurun_out/tbgpu_fatal.log 2>/dev/null; exit $rc; }
 step smoke 180 python3 -u __graft_entry__.py smoke
 cat "$OUT/smoke.out"
 step bench 400 python3 bench.py --gpus 1 --steps 20 --warmup 5

@@ -20,6 +20,12 @@ def _engine(w, **kw):
     return Engine(**args)
 
 
+def _rows(t):
+    """(id, debit account, credit account, timestamp, flags) of each row, for failure messages."""
+    return [(int(x["id_lo"]), int(x["debit_account_id_lo"]), int(x["credit_account_id_lo"]), int(x["timestamp"]),
+             int(x["flags"])) for x in t[:4]]
+
+
 def _interleaved(w, rounds, n_filters, seed, history_ids=None):
     orc, gpu = oracle.Oracle(len(w.accounts), len(w.transfers)), _engine(w)
     rng = np.random.default_rng(seed)
@@ -41,7 +47,8 @@ def _interleaved(w, rounds, n_filters, seed, history_ids=None):
             rows = orc.export_transfers()
             for f in random_filters(rng, w.accounts["id_lo"], rows, n_filters):
                 g, o = gpu.get_account_transfers(f), orc.get_account_transfers(f)
-                assert g.tobytes() == o.tobytes(), (r, f, len(g), len(o))
+                assert g.tobytes() == o.tobytes(), (r, f, _rows(g), _rows(o), _rows(gpu.lookup_transfers(
+                    o["id_lo"].astype(object) + (o["id_hi"].astype(object) << 64))) if len(o) else None)
                 checked += len(o) > 0
             if history_ids is not None:
                 for f in random_filters(rng, history_ids, rows, n_filters // 2):

@@ -260,11 +260,14 @@ struct tbgpu_ctx {
     // the end of a call in one copy (k_report): counter words, T.base, the last chunk's
     // reply counts
     u32* h_report = nullptr;  // pinned
-    // page-locked staging for host-to-device copies from pageable memory (h2d): two
-    // halves, each reusable once the copy recorded behind it has run
-    u8* h_up[2] = {nullptr, nullptr};
-    hipEvent_t up_ev[2] = {nullptr, nullptr};
-    int up_next = 0;
+    // page-locked staging for copies to and from caller memory (h2d / d2h): one ring
+    // per stream (the routed pipeline's threads use the ctx's two streams at once), two
+    // halves each, a half reusable once the copy recorded behind it has run
+    struct UpRing {
+        u8* h[2] = {nullptr, nullptr};
+        hipEvent_t ev[2] = {nullptr, nullptr};
+        int next = 0;
+    } up[2];
     u32* h_report_dev = nullptr;  // its device address, and h_res's
     u64* h_res_dev = nullptr;
     u64 h_rc_cap = 0;
@@ -529,10 +532,12 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     if (c->h_base) (void)hipHostFree(c->h_base);
     if (c->h_rc) (void)hipHostFree(c->h_rc);
     if (c->h_res) (void)hipHostFree(c->h_res);
-    for (int h = 0; h < 2; h++) {
-        if (c->h_up[h]) (void)hipHostFree(c->h_up[h]);
-        if (c->up_ev[h]) (void)hipEventDestroy(c->up_ev[h]);
-    }
+    (void)hipStreamSynchronize(c->route_stream);
+    for (auto& R : c->up)
+        for (int h = 0; h < 2; h++) {
+            if (R.h[h]) (void)hipHostFree(R.h[h]);
+            if (R.ev[h]) (void)hipEventDestroy(R.ev[h]);
+        }
     for (hipEvent_t e : c->prof_pool) (void)hipEventDestroy(e);
     (void)hipEventDestroy(c->ev0);
     (void)hipEventDestroy(c->ev1);
@@ -1153,36 +1158,52 @@ static const void* pinned_device_ptr(const void* p, u64 bytes) {
 // let kernels read stale data in a long process (the copies' destinations are reused
 // buffers -- the event buffer, the query filter -- and a later kernel saw the previous
 // contents: DESIGN.md §5), so the engine never hands it a pageable source.
-// Device-to-host copy into caller (pageable) memory: behind a drain of `s`, as a
-// blocking copy (an asynchronous copy into pageable memory returned stale rows in a
-// long process).
-static void d2h(void* dst, const void* src, u64 bytes, hipStream_t s) {
-    wait_stream(s);
-    if (bytes) HIP_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+constexpr u64 UP_HALF = 4ull << 20;
+static tbgpu_ctx::UpRing& up_ring(tbgpu_ctx* c, hipStream_t s) {
+    tbgpu_ctx::UpRing& R = c->up[s == c->route_stream ? 1 : 0];
+    if (R.h[0]) return R;
+    for (int h = 0; h < 2; h++) {
+        HIP_CHECK(hipHostMalloc((void**)&R.h[h], UP_HALF, hipHostMallocDefault));
+        HIP_CHECK(hipEventCreateWithFlags(&R.ev[h], hipEventDisableTiming));
+        HIP_CHECK(hipEventRecord(R.ev[h], s));
+    }
+    return R;
 }
 
-constexpr u64 UP_HALF = 4ull << 20;
 static void h2d(tbgpu_ctx* c, void* dst, const void* src, u64 bytes, hipStream_t s) {
     if (bytes == 0) return;
     if ((c->opt.flags & TBGPU_OPT_PINNED_INPUT) && pinned_device_ptr(src, bytes)) {
         HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
         return;
     }
-    if (!c->h_up[0]) {
-        for (int h = 0; h < 2; h++) {
-            HIP_CHECK(hipHostMalloc((void**)&c->h_up[h], UP_HALF, hipHostMallocDefault));
-            HIP_CHECK(hipEventCreateWithFlags(&c->up_ev[h], hipEventDisableTiming));
-            HIP_CHECK(hipEventRecord(c->up_ev[h], s));
-        }
-    }
+    tbgpu_ctx::UpRing& R = up_ring(c, s);
     for (u64 off = 0; off < bytes;) {
         const u64 k = std::min<u64>(bytes - off, UP_HALF);
-        const int h = c->up_next;
-        c->up_next ^= 1;
-        HIP_CHECK(hipEventSynchronize(c->up_ev[h]));  // the half's previous copy has read it
-        memcpy(c->h_up[h], (const u8*)src + off, k);
-        HIP_CHECK(hipMemcpyAsync((u8*)dst + off, c->h_up[h], k, hipMemcpyHostToDevice, s));
-        HIP_CHECK(hipEventRecord(c->up_ev[h], s));
+        const int h = R.next;
+        R.next ^= 1;
+        HIP_CHECK(hipEventSynchronize(R.ev[h]));  // the half's previous copy has read it
+        memcpy(R.h[h], (const u8*)src + off, k);
+        HIP_CHECK(hipMemcpyAsync((u8*)dst + off, R.h[h], k, hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipEventRecord(R.ev[h], s));
+        off += k;
+    }
+}
+
+// Device-to-host copy into caller memory, in stream order on `s`, complete on return:
+// a DMA into the ctx's page-locked ring, then a host memcpy per UP_HALF bytes.  Copies
+// into pageable memory are never handed to the runtime.
+static void d2h(tbgpu_ctx* c, void* dst, const void* src, u64 bytes, hipStream_t s) {
+    if (bytes == 0) return;
+    tbgpu_ctx::UpRing& R = up_ring(c, s);
+    for (u64 off = 0; off < bytes;) {
+        const u64 k = std::min<u64>(bytes - off, UP_HALF);
+        const int h = R.next;
+        R.next ^= 1;
+        HIP_CHECK(hipEventSynchronize(R.ev[h]));
+        HIP_CHECK(hipMemcpyAsync(R.h[h], (const u8*)src + off, k, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipEventRecord(R.ev[h], s));
+        HIP_CHECK(hipEventSynchronize(R.ev[h]));
+        memcpy((u8*)dst + off, R.h[h], k);
         off += k;
     }
 }
@@ -1388,7 +1409,7 @@ static uint64_t routed(tbgpu_ctx* c, uint32_t batch_count, const uint32_t* count
     c->rt_ev_ts = nullptr;
     c->rt_ctl = nullptr;
     u64 ts = 0;
-    HIP_CHECK(hipMemcpy(&ts, c->rt_dry ? c->rt_dry_ts : c->T.commit_ts, sizeof(u64), hipMemcpyDeviceToHost));
+    d2h(c, &ts, c->rt_dry ? c->rt_dry_ts : c->T.commit_ts, sizeof(u64), c->stream);
     c->rt_dry = false;
     if (commit_timestamp) *commit_timestamp = ts;
     return total;
@@ -1440,7 +1461,7 @@ void route_stats(const Transfer* ev, u64 n, u64* out, hipStream_t stream);
 extern "C" int tbgpu_route_stats(tbgpu_ctx* c, const void* events_device, uint64_t count, uint64_t* out) {
     HIP_CHECK(hipSetDevice(c->device));
     route_stats((const Transfer*)events_device, count, c->rt_stats, c->route_stream);
-    d2h(out, c->rt_stats, 5 * sizeof(u64), c->route_stream);
+    d2h(c, out, c->rt_stats, 5 * sizeof(u64), c->route_stream);
     wait_stream(c->route_stream);
     return 0;
 }
@@ -1482,7 +1503,7 @@ extern "C" int tbgpu_route_prepare(tbgpu_ctx* c, uint32_t world, const void* eve
     route_capacity(c, world, 0, count);
     route_rank((const Transfer*)events_device, count, world, c->ro_orank, c->ro_blk, c->ro_spart, c->rt_stats,
                c->route_stream);
-    d2h(out, c->rt_stats, 5 * sizeof(u64), c->route_stream);
+    d2h(c, out, c->rt_stats, 5 * sizeof(u64), c->route_stream);
     wait_stream(c->route_stream);
     c->ro_ranked = {events_device, count, world};
     return 0;
@@ -1516,14 +1537,13 @@ static int route_scatter_any(tbgpu_ctx* c, uint32_t world, uint32_t batch_count,
     route_scatter((const Transfer*)events_device, n, world, batch_count, c->ro_bstart, first_global_batch,
                   c->ro_orank, c->ro_blk, c->ro_counts, (Transfer*)send_events_device, (u64*)send_records_device,
                   c->ro_bcount + 256, c->ro_bcount, word_mask, (u32*)send_packed_device, err, ranked, c->route_stream);
-    d2h(send_counts, c->ro_counts, world * sizeof(u64), c->route_stream);
+    d2h(c, send_counts, c->ro_counts, world * sizeof(u64), c->route_stream);
     if (send_batch_counts)
-        HIP_CHECK(hipMemcpyAsync(send_batch_counts, c->ro_bcount + 256, (u64)world * batch_count * sizeof(u32),
-                                 hipMemcpyDeviceToHost, c->route_stream));
+        d2h(c, send_batch_counts, c->ro_bcount + 256, (u64)world * batch_count * sizeof(u32), c->route_stream);
     if (send_span_counts)
-        d2h(send_span_counts, c->ro_bcount, world * sizeof(u32), c->route_stream);
+        d2h(c, send_span_counts, c->ro_bcount, world * sizeof(u32), c->route_stream);
     u32 e = 0;
-    d2h(&e, err, sizeof(u32), c->route_stream);
+    d2h(c, &e, err, sizeof(u32), c->route_stream);
     wait_stream(c->route_stream);
     return e ? -22 : 0;
 }
@@ -1559,7 +1579,7 @@ extern "C" int tbgpu_route_unpack_packed(tbgpu_ctx* c, const void* packed_device
                       (const u32*)sub_batches_device, sub_batch_count, (const u64*)batch_ts_base_device, batches,
                       (Transfer*)events_device, (u64*)records_device, (u64*)timestamps_device, err, c->route_stream);
     u32 e = 0;
-    d2h(&e, err, sizeof(u32), c->route_stream);
+    d2h(c, &e, err, sizeof(u32), c->route_stream);
     wait_stream(c->route_stream);
     return e ? -22 : 0;
 }
@@ -1572,7 +1592,7 @@ extern "C" int tbgpu_route_unpack(tbgpu_ctx* c, const void* records_device, uint
     route_unpack((const u64*)records_device, count, (const u64*)batch_ts_base_device, batches, (u64*)timestamps_device,
                  err, c->route_stream);
     u32 e = 0;
-    d2h(&e, err, sizeof(u32), c->route_stream);
+    d2h(c, &e, err, sizeof(u32), c->route_stream);
     wait_stream(c->route_stream);
     return e ? -22 : 0;
 }
@@ -1677,11 +1697,11 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
     c->stats.iterations = it + 1;
     ac_launch_mask(c->T, C, A->res, A->ok, A->cfail, c->fres, c->mask, s);
     scan3_exclusive(c->mask, c->ranks, n, c->sc, s);
-    d2h(&tot, c->ranks + n, sizeof(uint4), s);
+    d2h(c, &tot, c->ranks + n, sizeof(uint4), s);
     wait_stream(s);
     if (c->n_accounts + tot.x > c->accounts_max) tbgpu_fatal("create_accounts", "accounts_max exceeded", __FILE__, __LINE__);
     ac_launch_apply(c->T, C, A->ok, c->fres, c->ranks, c->n_accounts, c->accounts_max, results_dev, c->counts, s);
-    d2h(counts_host, c->counts, nb * sizeof(u32), s);
+    d2h(c, counts_host, c->counts, nb * sizeof(u32), s);
     wait_stream(s);
     c->n_accounts += tot.x;
 }
@@ -1770,8 +1790,8 @@ static uint32_t lookup(tbgpu_ctx* c, const tbgpu_uint128_t* ids, uint32_t count,
         // into pageable memory: blocking copies behind a drain of the ctx's stream (an
         // asynchronous copy into pageable memory returned stale rows)
         wait_stream(c->stream);
-        HIP_CHECK(hipMemcpy(rows.data(), d_out, (u64)k * sizeof(Row), hipMemcpyDeviceToHost));
-        HIP_CHECK(hipMemcpy(found.data(), d_found, k, hipMemcpyDeviceToHost));
+        d2h(c, rows.data(), d_out, (u64)k * sizeof(Row), c->stream);
+        d2h(c, found.data(), d_found, k, c->stream);
         for (u32 i = 0; i < k; i++)
             if (found[i]) memcpy(&out[found_total++], &rows[i], sizeof(Row));
     }
@@ -1850,7 +1870,7 @@ static u64 run_queries(tbgpu_ctx* c, const tbgpu_account_filter_t* filters, u32 
         const u32 k = std::min(step, nq - q0);
         QArgs A{filters + q0, k, stride, (u8*)out + (u64)q0 * stride * 128, c->counts, history ? 1u : 0u, c->n_hist};
         q_launch_scan(c->T, X, A, c->stream);
-        d2h(counts_host + q0, c->counts, k * sizeof(u32), c->stream);
+        d2h(c, counts_host + q0, c->counts, k * sizeof(u32), c->stream);
         wait_stream(c->stream);
         for (u32 j = 0; j < k; j++) total += counts_host[q0 + j];
     }
@@ -1863,7 +1883,7 @@ static uint32_t query_host(tbgpu_ctx* c, const tbgpu_account_filter_t* filter, v
     h2d(c, fd, filter, sizeof *filter, c->stream);
     uint32_t n = 0;
     run_queries(c, fd, 1, TBGPU_QUERY_MAX, c->ev_buf, history, &n);  // ev_buf: nmax * 128 B >= 8190 rows
-    if (n) HIP_CHECK(hipMemcpy(out, c->ev_buf, (u64)n * 128, hipMemcpyDeviceToHost));
+    if (n) d2h(c, out, c->ev_buf, (u64)n * 128, c->stream);
     return n;
 }
 
@@ -1926,13 +1946,13 @@ extern "C" uint64_t tbgpu_checkpoint(tbgpu_ctx* c, void* out, uint64_t capacity)
     wait_stream(c->stream);
     u8* p = (u8*)out + sizeof(CkHeader);
     const u64 na = c->n_accounts, nr = c->n_rows, nh = c->n_hist;
-    if (na) HIP_CHECK(hipMemcpy(p, c->T.acc, na * 128, hipMemcpyDeviceToHost));
-    if (nr) HIP_CHECK(hipMemcpy(p + na * 128, c->T.xrows, nr * 128, hipMemcpyDeviceToHost));
-    if (nr) HIP_CHECK(hipMemcpy(p + na * 128 + nr * 128, c->T.xful, nr, hipMemcpyDeviceToHost));
+    if (na) d2h(c, p, c->T.acc, na * 128, c->stream);
+    if (nr) d2h(c, p + na * 128, c->T.xrows, nr * 128, c->stream);
+    if (nr) d2h(c, p + na * 128 + nr * 128, c->T.xful, nr, c->stream);
     u8* imp = p + na * 128 + nr * 129;
-    if (nr && c->ximp) HIP_CHECK(hipMemcpy(imp, c->ximp, nr, hipMemcpyDeviceToHost));
+    if (nr && c->ximp) d2h(c, imp, c->ximp, nr, c->stream);
     else memset(imp, 0, nr);
-    if (nh) HIP_CHECK(hipMemcpy(imp + nr, c->T.hrows, nh * 256, hipMemcpyDeviceToHost));
+    if (nh) d2h(c, imp + nr, c->T.hrows, nh * 256, c->stream);
     CkHeader h{};
     h.magic = CK_MAGIC;
     h.version = 1;
@@ -1961,9 +1981,9 @@ extern "C" int tbgpu_open(tbgpu_ctx* c, const void* image, uint64_t size) {
     // the reset's memsets run on the ctx's non-blocking stream, which the blocking
     // copies below do not wait for
     wait_stream(s);
-    if (na) HIP_CHECK(hipMemcpy(c->T.acc, p, na * 128, hipMemcpyHostToDevice));
-    if (nr) HIP_CHECK(hipMemcpy(c->T.xrows, p + na * 128, nr * 128, hipMemcpyHostToDevice));
-    if (nr) HIP_CHECK(hipMemcpy(c->T.xful, p + na * 128 + nr * 128, nr, hipMemcpyHostToDevice));
+    if (na) h2d(c, c->T.acc, p, na * 128, c->stream);
+    if (nr) h2d(c, c->T.xrows, p + na * 128, nr * 128, c->stream);
+    if (nr) h2d(c, c->T.xful, p + na * 128 + nr * 128, nr, c->stream);
     const u8* imp = p + na * 128 + nr * 129;
     bool any_imported = false;
     for (u64 k = 0; k < nr && !any_imported; k++) any_imported = imp[k] != 0;
@@ -1974,9 +1994,9 @@ extern "C" int tbgpu_open(tbgpu_ctx* c, const void* image, uint64_t size) {
         }
         HIP_CHECK(hipMemsetAsync(c->ximp, 0, c->xrow_cap, s));
         wait_stream(s);
-        HIP_CHECK(hipMemcpy(c->ximp, imp, nr, hipMemcpyHostToDevice));
+        h2d(c, c->ximp, imp, nr, c->stream);
     }
-    if (nh) HIP_CHECK(hipMemcpy(c->T.hrows, imp + nr, nh * 256, hipMemcpyHostToDevice));
+    if (nh) h2d(c, c->T.hrows, imp + nr, nh * 256, c->stream);
     // derived state: the account index, the transfer-id index and its key range,
     // the overflow guard; the account-transfers index rebuilds on the next query
     launch_rebuild_accounts(c->T, na, s);
@@ -2003,7 +2023,7 @@ extern "C" int tbgpu_test_set_balances(tbgpu_ctx* c, tbgpu_uint128_t id, tbgpu_u
     Bal4 b{to128(dp), to128(dpo), to128(cp), to128(cpo)};
     launch_set_balances(c->T, to128(id), b, c->status, c->stream);
     int st = 0;
-    d2h(&st, c->status, sizeof(int), c->stream);
+    d2h(c, &st, c->status, sizeof(int), c->stream);
     wait_stream(c->stream);
     return st;
 }
@@ -2012,7 +2032,7 @@ extern "C" int tbgpu_get_posted(tbgpu_ctx* c, tbgpu_uint128_t pending_id) {
     HIP_CHECK(hipSetDevice(c->device));
     launch_get_posted(c->T, to128(pending_id), c->status, c->stream);
     int st = 0;
-    d2h(&st, c->status, sizeof(int), c->stream);
+    d2h(c, &st, c->status, sizeof(int), c->stream);
     wait_stream(c->stream);
     return st;
 }
@@ -2026,7 +2046,7 @@ extern "C" uint64_t tbgpu_export_transfers(tbgpu_ctx* c, uint64_t first, uint64_
     if (first >= c->n_rows) return 0;
     count = std::min<u64>(count, c->n_rows - first);
     wait_stream(c->stream);  // the blocking copy (null stream) does not wait for the ctx's stream
-    HIP_CHECK(hipMemcpy(out, c->T.xrows + first, count * sizeof(Transfer), hipMemcpyDeviceToHost));
+    d2h(c, out, c->T.xrows + first, count * sizeof(Transfer), c->stream);
     return count;
 }
 
@@ -2035,7 +2055,7 @@ extern "C" uint64_t tbgpu_export_history(tbgpu_ctx* c, uint64_t first, uint64_t 
     if (first >= c->n_hist) return 0;
     count = std::min<u64>(count, c->n_hist - first);
     wait_stream(c->stream);  // the blocking copy (null stream) does not wait for the ctx's stream
-    HIP_CHECK(hipMemcpy(out, c->T.hrows + first, count * sizeof(History), hipMemcpyDeviceToHost));
+    d2h(c, out, c->T.hrows + first, count * sizeof(History), c->stream);
     return count;
 }
 
@@ -2043,14 +2063,14 @@ extern "C" uint64_t tbgpu_export_accounts(tbgpu_ctx* c, tbgpu_account_t* out, ui
     HIP_CHECK(hipSetDevice(c->device));
     const u64 n = std::min<u64>(capacity, c->n_accounts);  // dense rows, creation order
     wait_stream(c->stream);  // the blocking copy (null stream) does not wait for the ctx's stream
-    if (n) HIP_CHECK(hipMemcpy(out, c->T.acc, n * sizeof(Account), hipMemcpyDeviceToHost));
+    if (n) d2h(c, out, c->T.acc, n * sizeof(Account), c->stream);
     return n;
 }
 
 extern "C" uint64_t tbgpu_commit_timestamp(tbgpu_ctx* c) {
     HIP_CHECK(hipSetDevice(c->device));
     u64 v = 0;  // behind whatever the engine's stream still has queued (tbgpu_advance_commit_timestamp)
-    d2h(&v, c->T.commit_ts, sizeof(u64), c->stream);
+    d2h(c, &v, c->T.commit_ts, sizeof(u64), c->stream);
     wait_stream(c->stream);
     return v;
 }

@@ -503,6 +503,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->route_stream);
     // Free every device allocation by walking the struct's pointers.
     for (void* p : {(void*)c->ro_orank, (void*)c->ro_blk, (void*)c->ro_bstart, (void*)c->ro_counts,
                     (void*)c->ro_bcount, (void*)c->ro_spart})
@@ -532,7 +533,6 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     if (c->h_base) (void)hipHostFree(c->h_base);
     if (c->h_rc) (void)hipHostFree(c->h_rc);
     if (c->h_res) (void)hipHostFree(c->h_res);
-    (void)hipStreamSynchronize(c->route_stream);
     for (auto& R : c->up)
         for (int h = 0; h < 2; h++) {
             if (R.h[h]) (void)hipHostFree(R.h[h]);

@@ -1159,6 +1159,20 @@ static const void* pinned_device_ptr(const void* p, u64 bytes) {
 // buffers -- the event buffer, the query filter -- and a later kernel saw the previous
 // contents: DESIGN.md §5), so the engine never hands it a pageable source.
 constexpr u64 UP_HALF = 4ull << 20;
+// Device-to-device copy as a kernel on `s` (whole 4-byte words): the runtime's copy
+// engines are not used between device buffers that kernels just wrote (a merged query
+// index copied that way came back with entries missing in a long process).
+__global__ void k_copy_words(u32* __restrict__ dst, const u32* __restrict__ src, u64 n) {
+    for (u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (u64)gridDim.x * blockDim.x) dst[k] = src[k];
+}
+static void dcopy(void* dst, const void* src, u64 bytes, hipStream_t s) {
+    if (bytes % 4) tbgpu_fatal("dcopy", "not whole words", __FILE__, __LINE__);
+    const u64 n = bytes / 4;
+    if (n == 0) return;
+    k_copy_words<<<(u32)std::min<u64>((n + 255) / 256, 4096), 256, 0, s>>>((u32*)dst, (const u32*)src, n);
+    HIP_CHECK(hipGetLastError());
+}
+
 static tbgpu_ctx::UpRing& up_ring(tbgpu_ctx* c, hipStream_t s) {
     tbgpu_ctx::UpRing& R = c->up[s == c->route_stream ? 1 : 0];
     if (R.h[0]) return R;
@@ -1401,7 +1415,7 @@ static uint64_t routed(tbgpu_ctx* c, uint32_t batch_count, const uint32_t* count
     std::vector<u64> bts(batch_count, 0);
     c->rt_dry = dry_run != 0;
     if (c->rt_dry) {
-        HIP_CHECK(hipMemcpyAsync(c->rt_dry_ts, c->T.commit_ts, sizeof(u64), hipMemcpyDeviceToDevice, c->stream));
+        dcopy(c->rt_dry_ts, c->T.commit_ts, sizeof(u64), c->stream);
     }
     const u64 total = transfers_batches(c, batch_count, bts.data(), counts, (const Transfer*)events, device,
                                         (tbgpu_create_transfers_result_t*)results, device, result_counts,
@@ -1728,8 +1742,7 @@ static uint64_t accounts_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t
         for (u32 b = 0; b < nb; b++) chunk_total += result_counts[b0 + b];
         if (device) {  // replies concatenated in device memory, as for create_transfers
             if (chunk_total)
-                HIP_CHECK(hipMemcpyAsync(results + total, c->res_buf, chunk_total * 8, hipMemcpyDeviceToDevice,
-                                         c->stream));
+                dcopy(results + total, c->res_buf, chunk_total * 8, c->stream);
         } else {
             if (chunk_total) {
                 HIP_CHECK(hipMemcpyAsync(c->h_res, c->res_buf, chunk_total * 8, hipMemcpyDeviceToHost, c->stream));
@@ -1818,8 +1831,8 @@ static void q_sort(tbgpu_ctx* c, u64 e0, u64 e1) {
     const u64 m = e1 - e0;
     radix_sort_pairs(c->q_key + e0, c->q_val + e0, c->q_tkey + e0, c->q_tval + e0, m, log2u(c->accounts_max + 1),
                      c->q_ss, c->stream);
-    HIP_CHECK(hipMemcpyAsync(c->q_key + e0, c->q_tkey + e0, m * 4, hipMemcpyDeviceToDevice, c->stream));
-    HIP_CHECK(hipMemcpyAsync(c->q_val + e0, c->q_tval + e0, m * 4, hipMemcpyDeviceToDevice, c->stream));
+    dcopy(c->q_key + e0, c->q_tkey + e0, m * 4, c->stream);
+    dcopy(c->q_val + e0, c->q_tval + e0, m * 4, c->stream);
 }
 
 extern "C" uint64_t tbgpu_compact(tbgpu_ctx* c) {

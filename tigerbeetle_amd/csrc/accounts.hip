@@ -191,15 +191,33 @@ __device__ __forceinline__ u64 ac_mask_one(const AcArgs& C, const u8* res, const
     return ((ok[i] & 1) && (cf == NONE32 || i < cf)) ? C.ts[i] : 0;
 }
 
-// One atomicMax per wave on the single commit_timestamp word (one per accepted event
-// serialized at the memory side: 897 us for 10M accounts, SQ_WAIT_ANY 0.96 of the waves).
-__global__ void ac_mask(AcArgs C, const u8* res, const u8* ok, const u32* cfail, u8* fres, u8* mask, u64* commit_ts,
-                        const u32* gate) {
+// The accepted events' max timestamp goes to a per-workgroup word, folded by one
+// workgroup (ac_ts_fold) into the single commit_timestamp word: same-address atomics
+// serialize at the memory side (one per accepted event took 897 us for 10M accounts,
+// one per wave still 890 us).
+__global__ void ac_mask(AcArgs C, const u8* res, const u8* ok, const u32* cfail, u8* fres, u8* mask, const u32* gate) {
     if (gate && *gate == 0) return;
+    __shared__ u64 s_w[4];
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     u64 ts = i < C.n ? ac_mask_one(C, res, ok, cfail, fres, mask, i) : 0;
     ts = wave_max_u64(ts);
-    if (ts && wave_leader()) atomicMax((unsigned long long*)commit_ts, (unsigned long long)ts);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = ts;
+    __syncthreads();
+    if (threadIdx.x == 0) C.ts_part[blockIdx.x] = max(max(s_w[0], s_w[1]), max(s_w[2], s_w[3]));
+}
+
+__global__ void ac_ts_fold(const u64* part, u32 nparts, u64* commit_ts, const u32* gate) {
+    if (gate && *gate == 0) return;
+    __shared__ u64 s_w[16];
+    u64 m = 0;
+    for (u32 k = threadIdx.x; k < nparts; k += blockDim.x) m = max(m, part[k]);
+    m = wave_max_u64(m);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (u32 w = 1; w < blockDim.x / 64; w++) m = max(m, s_w[w]);
+        if (m) atomicMax((unsigned long long*)commit_ts, (unsigned long long)m);
+    }
 }
 
 __global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const uint4* rk, u64 row_base, u64 cap,
@@ -368,7 +386,9 @@ void ac_launch_evaluate(const Tables& T, const AcArgs& C, const u8* res_s, const
 }
 void ac_launch_mask(const Tables& T, const AcArgs& C, const u8* res, const u8* ok, const u32* cfail, u8* fres,
                     u8* mask, hipStream_t stream, const u32* gate) {
-    ac_mask<<<GRID(C.n)>>>(C, res, ok, cfail, fres, mask, T.commit_ts, gate);
+    static_assert(256 == 4 * 64, "ac_mask folds four waves per workgroup");
+    ac_mask<<<GRID(C.n)>>>(C, res, ok, cfail, fres, mask, gate);
+    ac_ts_fold<<<1, 1024, 0, stream>>>(C.ts_part, (C.n + 255) / 256, T.commit_ts, gate);
 }
 void ac_launch_apply(const Tables& T, const AcArgs& C, const u8* ok, const u8* fres, const uint4* rk, u64 row_base,
                      u64 cap, tbgpu_create_accounts_result_t* results, u32* counts, hipStream_t stream, const u32* gate) {

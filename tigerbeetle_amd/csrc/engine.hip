@@ -254,6 +254,7 @@ struct tbgpu_ctx {
     Bal4* w_undo_val = nullptr;
     u32* w_out = nullptr;
     u64* rg_part = nullptr;    // tr_range's per-block records
+    u64* ac_part = nullptr;    // ac_mask's per-workgroup max accepted timestamp
     u32* h_pc = nullptr;       // pinned mirror of the change ring
     u64* h_base = nullptr;     // pinned mirror of T.base
     u32* h_rc = nullptr;       // pinned per-batch reply counts of the current call
@@ -371,6 +372,7 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->rt_stats = dalloc<u64>(8, &B);
     c->pc = c->counters + PC_OFF;
     c->rg_part = dalloc<u64>(tr_range_part_words(n), &B);
+    c->ac_part = dalloc<u64>(n / 256 + 2, &B);
 
     HIP_CHECK(hipHostMalloc((void**)&c->h_base, 8 * sizeof(u64), hipHostMallocDefault));  // [4..5]: a uint4
     HIP_CHECK(hipHostMalloc((void**)&c->h_counters, (PC_OFF + 3 * PC_RING) * sizeof(u32), hipHostMallocDefault));
@@ -520,7 +522,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
                     c->f_tile_idr, c->rt_ts_buf, c->rt_ctl_buf, c->rt_dry_ts, c->rt_stats, c->rg_part, c->T.base, c->q_key, c->q_val, c->q_tkey,
                     c->q_tval, c->q_ss.keys_tmp, c->q_ss.vals_tmp, c->q_ss.hist, c->q_runs_dev, c->ximp,
                     c->lst_simple, c->lst_complex, c->d_ev, c->d_chain, c->d_slot, c->d_win, c->w_sstart, c->w_bal,
-                    c->w_undo_slot, c->w_undo_val, c->w_out};
+                    c->w_undo_slot, c->w_undo_val, c->w_out, c->ac_part};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     for (EvalState& s : c->st) {
         void* q[] = {s.res, s.ok, s.pref, s.cfail, s.amt, s.pamt};
@@ -1660,6 +1662,7 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
     const u64 g = std::min<u64>(c->gcap, pow2_at_least(4ull * n));
     C.gmask = g - 1;
     C.counters = c->counters;
+    C.ts_part = c->ac_part;
     HIP_CHECK(hipMemsetAsync(c->counters, 0, CNT_COUNT * sizeof(u32), s));
     HIP_CHECK(hipMemsetAsync(c->gclaim, 0, g * sizeof(u32), s));
     HIP_CHECK(hipMemsetAsync(c->gcnt_id, 0, g * sizeof(u32), s));

@@ -126,6 +126,7 @@ struct AcArgs {
     u32* ce;
     u8* sres;
     u32* pre;       // slot of an existing account with the same id
+    u64* ts_part;   // ac_mask's per-workgroup max accepted timestamp (GRID(n) words)
     u32* gslot;
     u32* prev_id;
     u32* gclaim;

@@ -377,13 +377,18 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     HIP_CHECK(hipHostMalloc((void**)&c->h_base, 8 * sizeof(u64), hipHostMallocDefault));  // [4..5]: a uint4
     HIP_CHECK(hipHostMalloc((void**)&c->h_counters, (PC_OFF + 3 * PC_RING) * sizeof(u32), hipHostMallocDefault));
     c->h_pc = c->h_counters + PC_OFF;
-    HIP_CHECK(hipHostMalloc((void**)&c->h_report, (RPT_COUNTS + c->bmax) * sizeof(u32), hipHostMallocDefault));
-    HIP_CHECK(hipHostMalloc((void**)&c->h_res, c->nmax * 8 + 8, hipHostMallocDefault));
+    // Host buffers that kernels read or write in place (k_report's stores, k_upload_block's
+    // loads) are coherent: the GPU does not keep their lines in its caches, so a kernel
+    // never reads a previous call's staged block and the host never reads a report the
+    // device has not written back.
+    constexpr unsigned HOST_COHERENT = hipHostMallocMapped | hipHostMallocCoherent;
+    HIP_CHECK(hipHostMalloc((void**)&c->h_report, (RPT_COUNTS + c->bmax) * sizeof(u32), HOST_COHERENT));
+    HIP_CHECK(hipHostMalloc((void**)&c->h_res, c->nmax * 8 + 8, HOST_COHERENT));
     HIP_CHECK(hipHostGetDevicePointer((void**)&c->h_res_dev, c->h_res, 0));
     HIP_CHECK(hipHostGetDevicePointer((void**)&c->h_report_dev, c->h_report, 0));
     HIP_CHECK(hipHostMalloc((void**)&c->h_counts, c->bmax * sizeof(u32), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc((void**)&c->h_stage_start, (batch_ts_offset(c->bmax) + 2 * c->bmax) * sizeof(u32),
-                            hipHostMallocDefault));
+                            HOST_COHERENT));
     c->h_stage_ts = (u64*)(c->h_stage_start + batch_ts_offset(c->bmax));
     HIP_CHECK(hipHostGetDevicePointer((void**)&c->h_stage_dev, c->h_stage_start, 0));
 }

@@ -442,6 +442,51 @@ def verify_stream(eng, w, ats, tts, counts, B, steps, replies, acc_n):
         orc.close()
 
 
+SUBCONFIGS = (
+    # (key in the line, arguments): BASELINE configs 1 and 3 on one GPU, and the routed
+    # config-4 step on a one-rank group (the same workload `--gpus N > 1` times), each
+    # a bench.py child with a bounded CPU-baseline sample
+    ("config1", ["--config", "1", "--steps", "3", "--warmup", "1"]),
+    ("config3", ["--config", "3", "--steps", "3", "--warmup", "1"]),
+    ("scaling_n1", ["--routed", "--steps", "3", "--warmup", "1"]),
+)
+SUB_DROP = ("metric", "higher_is_better", "vs_baseline", "dtype", "data", "scaling", "unit", "queries", "host_path",
+            "verify", "configs", "scaling_n1")
+
+
+def run_subconfigs(args) -> dict:
+    """The driver's default command (`--gpus 1`, no --config) also measures BASELINE
+    configs 1 and 3 and the scaling family's N = 1 point, each in a child process run
+    before this process touches the GPU (children, never exec), so the line carries
+    them with their own roofline and cpu_baseline.  Returns {key: compact line}."""
+    import subprocess
+    out = {}
+    for key, argv in SUBCONFIGS:
+        cmd = [sys.executable, os.path.abspath(__file__), *argv, "--no-queries", "--no-host",
+               "--cpu-seconds", str(args.sub_cpu_seconds)]
+        t0 = time.time()
+        try:
+            r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=None, timeout=args.sub_timeout, text=True,
+                               env=dict(os.environ, TB_BENCH_SUB="1"))
+            lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+            if r.returncode != 0 or not lines:
+                out[key] = {"error": f"exit {r.returncode}", "argv": argv}
+                continue
+            d = json.loads(lines[-1])
+        except subprocess.TimeoutExpired:
+            out[key] = {"error": f"timeout {args.sub_timeout}s", "argv": argv}
+            continue
+        for k in SUB_DROP:
+            d.pop(k, None)
+        if isinstance(d.get("roofline"), dict):
+            d["roofline"].pop("phase_ms_per_step", None)
+        d["argv"] = " ".join(argv)
+        d["wall_s"] = round(time.time() - t0, 1)
+        out[key] = d
+        log(f"[bench] {key}: {d.get('value')} transfers/s ({d['wall_s']} s)")
+    return out
+
+
 def spawn_ranks(n: int) -> None:
     """`--gpus N` without a launcher: start N rank processes (one per GPU, RCCL over
     127.0.0.1) before this process touches the GPU, pass rank 0's result line through
@@ -498,12 +543,20 @@ def main():
     ap.add_argument("--verify", action="store_true",
                     help="after the timed region, replay the same stream through the CPU oracle and compare "
                          "every reply and the final state bit for bit (configs 1-4)")
+    ap.add_argument("--no-subconfigs", action="store_true",
+                    help="the default one-GPU run: skip the config-1 / config-3 / routed N = 1 sub-measurements")
+    ap.add_argument("--sub-cpu-seconds", type=float, default=5.0, help="CPU-baseline sample of each sub-measurement")
+    ap.add_argument("--sub-timeout", type=float, default=240.0, help="seconds allowed to each sub-measurement")
     args = ap.parse_args()
     env_world = os.environ.get("WORLD_SIZE")
     if args.gpus is None:
         args.gpus = int(env_world or 1)
     if env_world is None and args.gpus > 1:
         spawn_ranks(args.gpus)  # does not return
+    subs = None
+    if (env_world is None and args.gpus == 1 and args.config is None and not args.routed and not args.no_subconfigs
+            and not os.environ.get("TB_BENCH_SUB")):
+        subs = run_subconfigs(args)  # before this process touches the GPU
     if env_world is not None and int(env_world) != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}: launch one rank per GPU", file=sys.stderr)
         sys.exit(2)
@@ -827,6 +880,9 @@ def main():
             "queries": queries,
             "verify": verify,
         }
+        if subs is not None:
+            line["configs"] = {k: v for k, v in subs.items() if k != "scaling_n1"}
+            line["scaling_n1"] = subs.get("scaling_n1")
         emit(line)
     eng.close()
     if world > 1:

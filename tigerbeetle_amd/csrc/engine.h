@@ -325,4 +325,5 @@ enum {
     FL_ERROR = 1u << 9,       // device-side protocol error (bounded spin expired)
     FL_NONMONO = 1u << 10,    // fast path: ids of the call are not strictly increasing
     FL_FCHAIN = 1u << 11,     // fast path: linked chains, resolved by fp_chains
+    FL_CAPACITY = 1u << 12,   // create_accounts: accounts_max reached (ac_apply wrote nothing past it)
 };

@@ -81,15 +81,24 @@ inline void wait_event(hipEvent_t ev) {
     }
 }
 
-// TBGPU_ZERO_ALLOC=1 (diagnostics): every device allocation is zeroed on the stream
-// of the ctx that allocates it (ZeroOn names it for the allocating scope), and the
-// scope ends only when the zeroing is complete, so no buffer starts with an earlier
-// ctx's contents.  Off by default (no kernel reads a buffer before writing it).
+// TBGPU_POISON_ALLOC=<byte> (diagnostics; "1" means 0xA5): every device allocation
+// and every page-locked host buffer the ctx owns starts filled with that byte instead
+// of whatever an earlier ctx (or a fresh page's zeros) left there.  A kernel or host
+// step that reads a word before this ctx wrote it then goes wrong deterministically,
+// in the test that does it, instead of only after earlier tests recycled the memory.
+// The fill runs on the stream of the ctx that allocates (ZeroOn names it for the
+// allocating scope), and the scope ends only when the fill is complete.
 thread_local hipStream_t t_zero_stream = nullptr;
-inline bool zero_alloc() {
-    static const bool z = getenv("TBGPU_ZERO_ALLOC") != nullptr;
-    return z;
+inline int poison_byte() {
+    static const int b = [] {
+        const char* e = getenv("TBGPU_POISON_ALLOC");
+        if (!e || !*e) return -1;
+        const long v = strtol(e, nullptr, 0);
+        return v == 1 ? 0xA5 : (int)(v & 0xFF);
+    }();
+    return b;
 }
+inline bool zero_alloc() { return poison_byte() >= 0; }
 struct ZeroOn {
     hipStream_t prev, mine;
     explicit ZeroOn(hipStream_t s) : prev(t_zero_stream), mine(s) { t_zero_stream = s; }
@@ -102,7 +111,11 @@ struct ZeroOn {
 inline void zero_new(void* p, u64 bytes) {
     if (!zero_alloc()) return;
     if (!t_zero_stream) tbgpu_fatal("alloc", "device allocation outside a ZeroOn scope", __FILE__, __LINE__);
-    HIP_CHECK(hipMemsetAsync(p, 0, bytes, t_zero_stream));
+    HIP_CHECK(hipMemsetAsync(p, poison_byte(), bytes, t_zero_stream));
+}
+// page-locked host memory: filled by the host (no kernel has seen it yet)
+inline void poison_host(void* p, u64 bytes) {
+    if (zero_alloc()) memset(p, poison_byte(), bytes);
 }
 
 template <typename T>
@@ -391,6 +404,12 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
                             HOST_COHERENT));
     c->h_stage_ts = (u64*)(c->h_stage_start + batch_ts_offset(c->bmax));
     HIP_CHECK(hipHostGetDevicePointer((void**)&c->h_stage_dev, c->h_stage_start, 0));
+    poison_host(c->h_base, 8 * sizeof(u64));
+    poison_host(c->h_counters, (PC_OFF + 3 * PC_RING) * sizeof(u32));
+    poison_host(c->h_report, (RPT_COUNTS + c->bmax) * sizeof(u32));
+    poison_host(c->h_res, c->nmax * 8 + 8);
+    poison_host(c->h_counts, c->bmax * sizeof(u32));
+    poison_host(c->h_stage_start, (batch_ts_offset(c->bmax) + 2 * c->bmax) * sizeof(u32));
 }
 
 enum { PH_UPLOAD = 0, PH_CLASSIFY = 1, PH_SORT = 2, PH_SCAN = 3, PH_EVAL = 4, PH_APPLY = 5, PH_INDEX = 6, PH_PREP = 7, PH_END = -1 };
@@ -603,6 +622,7 @@ static void ensure_h_rc(tbgpu_ctx* c, u64 nb) {
     if (c->h_rc) HIP_CHECK(hipHostFree(c->h_rc));
     c->h_rc_cap = std::max<u64>(nb, 1024);
     HIP_CHECK(hipHostMalloc((void**)&c->h_rc, c->h_rc_cap * sizeof(u32), hipHostMallocDefault));
+    poison_host(c->h_rc, c->h_rc_cap * sizeof(u32));
 }
 
 // Splits batches [b0, b_end) into chunks of whole batches of <= nmax events.
@@ -1185,6 +1205,7 @@ static tbgpu_ctx::UpRing& up_ring(tbgpu_ctx* c, hipStream_t s) {
     if (R.h[0]) return R;
     for (int h = 0; h < 2; h++) {
         HIP_CHECK(hipHostMalloc((void**)&R.h[h], UP_HALF, hipHostMallocDefault));
+        poison_host(R.h[h], UP_HALF);
         HIP_CHECK(hipEventCreateWithFlags(&R.ev[h], hipEventDisableTiming));
         HIP_CHECK(hipEventRecord(R.ev[h], s));
     }
@@ -1505,14 +1526,16 @@ static void route_capacity(tbgpu_ctx* c, u32 world, u32 batch_count, u64 n) {
                         (void*)c->ro_bcount, (void*)c->ro_spart})
             if (p) HIP_CHECK(hipFree(p));
         c->ro_cap = std::max<u64>(std::max<u64>(n, batch_count + 1), c->ro_cap);
-        HIP_CHECK(hipMalloc((void**)&c->ro_spart, 5 * (route_block_count(c->ro_cap) + 1) * sizeof(u64)));
+        u64 ro_bytes = 0;
+        ZeroOn zero_on(c->route_stream);
+        c->ro_spart = dalloc<u64>(5 * (route_block_count(c->ro_cap) + 1), &ro_bytes);
         c->ro_bcap = 256ull * std::max<u64>(route_block_count(c->ro_cap), 1);
-        HIP_CHECK(hipMalloc((void**)&c->ro_orank, c->ro_cap * sizeof(uint2)));
-        HIP_CHECK(hipMalloc((void**)&c->ro_blk, c->ro_bcap * sizeof(u32)));
-        HIP_CHECK(hipMalloc((void**)&c->ro_bstart, (c->ro_cap + 3) * sizeof(u32)));
-        HIP_CHECK(hipMalloc((void**)&c->ro_counts, 256 * sizeof(u64)));
+        c->ro_orank = dalloc<uint2>(c->ro_cap, &ro_bytes);
+        c->ro_blk = dalloc<u32>(c->ro_bcap, &ro_bytes);
+        c->ro_bstart = dalloc<u32>(c->ro_cap + 3, &ro_bytes);
+        c->ro_counts = dalloc<u64>(256, &ro_bytes);
         c->ro_bc_cap = std::max<u64>((u64)world * std::max<u32>(batch_count, 1), 256ull * 64);
-        HIP_CHECK(hipMalloc((void**)&c->ro_bcount, (c->ro_bc_cap + 256) * sizeof(u32)));
+        c->ro_bcount = dalloc<u32>(c->ro_bc_cap + 256, &ro_bytes);
         c->ro_ranked = {};
     }
 }
@@ -1668,6 +1691,22 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
     C.gmask = g - 1;
     C.counters = c->counters;
     C.ts_part = c->ac_part;
+    C.counts_out = c->counts;
+    static const bool no_fast = getenv("TBGPU_NO_AC_FAST") != nullptr;  // A/B timing of the general path
+    if (!no_fast && !(c->opt.flags & TBGPU_OPT_FORCE_GENERAL) && c->n_accounts + n <= c->accounts_max) {
+        // the clean call (accounts.hip ac_fast_*): one round trip decides whether it stood
+        HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)(c->counters + CNT_FLAGS), 0, 1, s));
+        ac_launch_fast(c->T, C, c->n_accounts, s);
+        HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, CNT_COUNT * sizeof(u32), hipMemcpyDeviceToHost, s));
+        wait_stream(s);
+        if (!(c->h_counters[CNT_FLAGS] & FL_SLOW)) {
+            std::fill(counts_host, counts_host + nb, 0u);
+            c->n_accounts += n;
+            c->stats.iterations = 1;
+            return;
+        }
+        // not clean: nothing visible changed (rows past n_accounts are free); the general path below
+    }
     HIP_CHECK(hipMemsetAsync(c->counters, 0, CNT_COUNT * sizeof(u32), s));
     HIP_CHECK(hipMemsetAsync(c->gclaim, 0, g * sizeof(u32), s));
     HIP_CHECK(hipMemsetAsync(c->gcnt_id, 0, g * sizeof(u32), s));
@@ -1699,7 +1738,8 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
     memcpy(&tot, c->h_base + 4, sizeof tot);
     const u32 flags = c->h_counters[CNT_FLAGS];
     if (!(flags & (FL_CHAINS | FL_MULTI_ID))) {
-        if (flags & FL_ERROR) tbgpu_fatal("create_accounts", "accounts_max exceeded", __FILE__, __LINE__);
+        if (flags & FL_CAPACITY) tbgpu_fatal("create_accounts", "accounts_max exceeded", __FILE__, __LINE__);
+        if (flags & FL_ERROR) tbgpu_fatal("create_accounts", "device error", __FILE__, __LINE__);
         c->stats.iterations = 1;
         c->n_accounts += tot.x;
         return;
@@ -1843,6 +1883,40 @@ static void q_sort(tbgpu_ctx* c, u64 e0, u64 e1) {
     dcopy(c->q_val + e0, c->q_tval + e0, m * 4, c->stream);
 }
 
+// TBGPU_CHECK_INDEX=1 (diagnostics): after every compaction, the whole index against
+// its definition.  Entries are rebuilt from the stored rows into the sort's output
+// buffers (free between compactions); then every run [2 runs[k], 2 runs[k+1]) must
+// hold exactly the entries of its rows, ordered by (account row, transfer row << 1 |
+// side), each with the key its row's account probe gives.
+static void check_index(tbgpu_ctx* c) {
+    const u64 rows = c->q_runs.back();
+    if (rows == 0) return;
+    q_launch_entries(c->T, 0, rows, c->ximp, (u32)c->accounts_max, c->q_tkey, c->q_tval, c->stream);
+    std::vector<u32> want(2 * rows), key(2 * rows), val(2 * rows);
+    d2h(c, want.data(), c->q_tkey, 2 * rows * 4, c->stream);
+    d2h(c, key.data(), c->q_key, 2 * rows * 4, c->stream);
+    d2h(c, val.data(), c->q_val, 2 * rows * 4, c->stream);
+    wait_stream(c->stream);
+    char why[200];
+    for (size_t k = 0; k + 1 < c->q_runs.size(); k++) {
+        const u64 e0 = 2 * c->q_runs[k], e1 = 2 * c->q_runs[k + 1];
+        std::vector<u8> seen(e1 - e0, 0);
+        for (u64 e = e0; e < e1; e++) {
+            const u32 v = val[e];
+            const bool order = e == e0 || key[e - 1] < key[e] || (key[e - 1] == key[e] && val[e - 1] < v);
+            const bool inside = v >= e0 && v < e1;
+            if (!order || !inside || seen[v - e0] || key[e] != want[v]) {
+                snprintf(why, sizeof why, "index run %zu [%llu, %llu) entry %llu: key %u val %u (expected key %u, %s)",
+                         k, (unsigned long long)e0, (unsigned long long)e1, (unsigned long long)e, key[e], v,
+                         inside ? want[v] : ~0u, !order ? "out of order" : !inside ? "foreign" :
+                         seen[v - e0] ? "repeated" : "wrong key");
+                tbgpu_fatal("compact", why, __FILE__, __LINE__);
+            }
+            seen[v - e0] = 1;
+        }
+    }
+}
+
 extern "C" uint64_t tbgpu_compact(tbgpu_ctx* c) {
     HIP_CHECK(hipSetDevice(c->device));
     const u64 r0 = c->q_runs.back(), r1 = c->n_rows;
@@ -1877,6 +1951,8 @@ extern "C" uint64_t tbgpu_compact(tbgpu_ctx* c) {
     if (c->q_runs.size() > Q_RUNS_MAX + 1) tbgpu_fatal("compact", "index runs exceed Q_RUNS_MAX", __FILE__, __LINE__);
     h2d(c, c->q_runs_dev, c->q_runs.data(), c->q_runs.size() * sizeof(u64), c->stream);
     wait_stream(c->stream);
+    static const bool check = getenv("TBGPU_CHECK_INDEX") != nullptr;  // diagnostics (tests)
+    if (check) check_index(c);
     return r1;
 }
 

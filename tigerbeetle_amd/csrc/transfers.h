@@ -133,7 +133,12 @@ struct AcArgs {
     u32* gcnt_id;
     u64 gmask;
     u32* counters;
+    u32* counts_out;  // per-batch reply counts (the clean two-pass call writes zeros)
 };
+// The clean call (accounts.hip ac_fast_*): raises FL_SLOW in counters[CNT_FLAGS] and
+// changes nothing visible when the call is not clean (ids rising, all fields valid,
+// no chain, no existing id); otherwise commits it.  The caller ensures row capacity.
+void ac_launch_fast(const Tables& T, const AcArgs& C, u64 row_base, hipStream_t stream);
 void ac_launch_classify(const Tables& T, const AcArgs& C, hipStream_t stream);
 void ac_launch_group_sort(const AcArgs& C, u32 invalid, int bits, u32* k_in, u32* v_in, u32* k_out, u32* v_out,
                           SortScratch& ss, hipStream_t stream);

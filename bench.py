@@ -148,51 +148,85 @@ def query_phase(eng, w, acc_n, torch, dev, count=100, batch=1024):
                         "ns_per_row": round(compact_s / max(rows, 1) * 1e9, 3)}}
 
 
+HOST_WARMUP = 8  # untimed drop-in calls before each timed set (first-call allocations, page faults)
+
+
 def host_path(eng, w, tts, counts, b0, nbs, torch):
     """The drop-in's own call rate (INTEGRATION.md's Zig shim): events in pinned host
     memory, replies back in host memory, PCIe inside the timing.
     - `single`: one tbgpu_create_transfers call per 8190-event batch, as the shim
       issues it once per committed prepare (src/state_machine.zig:894-928,
       src/vsr/replica.zig:3755-3762): per-call latency and the rate it implies;
+    - `prefetched`: the same with StateMachine.prefetch before each commit
+      (tbgpu_prefetch_transfers, then its wait: the replica commits only after the
+      prefetch callback, src/vsr/replica.zig:3384-3415): the commit's own latency, and
+      prefetch + commit;
     - `streamed`: tbgpu_create_transfers_batches over many batches from host memory.
     Reported beside the metric, never as `value` (which is HBM-resident)."""
     from tigerbeetle_amd.types import TRANSFER_DTYPE
-    single, streamed = nbs
+    single, prefetched, streamed = nbs
     offs = np.concatenate([[0], np.cumsum(counts.astype(np.int64))])
-    o0, o1 = int(offs[b0]), int(offs[b0 + single + streamed])
+    o0, o1 = int(offs[b0]), int(offs[b0 + single + prefetched + streamed])
     pinned = torch.empty((o1 - o0) * 128, dtype=torch.uint8, pin_memory=True)
     view = pinned.numpy().view(TRANSFER_DTYPE)
     view[:] = w.transfers[o0:o1]
-    lat, dev_us = [], []
-    ev_single = 0
+
+    def batch(b):
+        return view[int(offs[b]) - o0:int(offs[b + 1]) - o0]
+
+    def pct(x):
+        x = np.asarray(x)
+        return {"p50": round(float(np.percentile(x, 50)), 1), "p99": round(float(np.percentile(x, 99)), 1),
+                "max": round(float(x.max()), 1)}
+
+    lat, dev_us, ev_single = [], [], 0
     for k in range(single):
-        b = b0 + k
-        ev = view[int(offs[b]) - o0:int(offs[b + 1]) - o0]
+        ev = batch(b0 + k)
         t0 = time.perf_counter()
-        eng.create_transfers(int(tts[b]), ev)
-        lat.append(time.perf_counter() - t0)
-        dev_us.append(eng.stats().device_ms * 1e3)  # HIP events around the call on the engine stream
-        ev_single += len(ev)
-    lat = np.array(lat) * 1e6
-    dev_us = np.array(dev_us)
-    s0 = b0 + single
+        eng.create_transfers(int(tts[b0 + k]), ev)
+        if k >= HOST_WARMUP:
+            lat.append((time.perf_counter() - t0) * 1e6)
+            dev_us.append(eng.stats().device_ms * 1e3)  # HIP events around the call on the engine stream
+            ev_single += len(ev)
+    lat = np.array(lat)
+    p0 = b0 + single
+    pre_us, com_us, both_us, ev_pre = [], [], [], 0
+    for k in range(prefetched):
+        ev = batch(p0 + k)
+        t0 = time.perf_counter()
+        eng.prefetch_transfers(ev)
+        eng.prefetch_wait()
+        t1 = time.perf_counter()
+        eng.create_transfers(int(tts[p0 + k]), ev)
+        t2 = time.perf_counter()
+        if k >= HOST_WARMUP:
+            pre_us.append((t1 - t0) * 1e6)
+            com_us.append((t2 - t1) * 1e6)
+            both_us.append((t2 - t0) * 1e6)
+            ev_pre += len(ev)
+    s0 = p0 + prefetched
     ev = view[int(offs[s0]) - o0:]
     t0 = time.perf_counter()
     eng.create_transfers_batches(tts[s0:s0 + streamed], counts[s0:s0 + streamed], ev)
     el = time.perf_counter() - t0
-    return {"single": {"calls": single, "events_per_call": int(ev_single // max(single, 1)),
-                       "latency_us": {"p50": round(float(np.percentile(lat, 50)), 1),
-                                      "p99": round(float(np.percentile(lat, 99)), 1),
-                                      "max": round(float(lat.max()), 1)},
-                       "slowest_calls": [int(x) for x in np.argsort(lat)[::-1][:3]],
-                       "device_us": {"p50": round(float(np.percentile(dev_us, 50)), 1),
-                                     "p99": round(float(np.percentile(dev_us, 99)), 1),
-                                     "max": round(float(dev_us.max()), 1)},
-                       "transfers_per_s": round(ev_single / (lat.sum() * 1e-6), 1),
-                       "entry": "tbgpu_create_transfers (one batch per call, pinned host buffers)"},
-            "streamed": {"batches": streamed, "transfers": len(ev), "seconds": round(el, 6),
-                         "transfers_per_s": round(len(ev) / el, 1),
-                         "entry": "tbgpu_create_transfers_batches (host buffers, H2D inside the call)"}}
+    out = {"single": {"calls": len(lat), "warmup_calls": HOST_WARMUP,
+                      "events_per_call": int(ev_single // max(len(lat), 1)),
+                      "latency_us": pct(lat),
+                      "slowest_calls": [int(x) + HOST_WARMUP for x in np.argsort(lat)[::-1][:3]],
+                      "device_us": pct(dev_us),
+                      "transfers_per_s": round(ev_single / (lat.sum() * 1e-6), 1),
+                      "entry": "tbgpu_create_transfers (one batch per call, pinned host buffers)"},
+           "streamed": {"batches": streamed, "transfers": len(ev), "seconds": round(el, 6),
+                        "transfers_per_s": round(len(ev) / el, 1),
+                        "entry": "tbgpu_create_transfers_batches (host buffers, H2D inside the call)"}}
+    if len(com_us):
+        out["prefetched"] = {"calls": len(com_us), "warmup_calls": HOST_WARMUP,
+                             "commit_latency_us": pct(com_us), "prefetch_latency_us": pct(pre_us),
+                             "prefetch_plus_commit_us": pct(both_us),
+                             "commit_transfers_per_s": round(ev_pre / (np.sum(com_us) * 1e-6), 1),
+                             "entry": "tbgpu_prefetch_transfers + tbgpu_prefetch_wait, then tbgpu_create_transfers "
+                                      "(the batch staged in HBM before the commit)"}
+    return out
 
 
 ACCOUNT_BYTES = 272  # SURVEY.md §8d: create_account reads 128 B, writes the 128-B row, probes 16 B
@@ -605,8 +639,9 @@ def main():
     B, K, W = args.batches_per_step, args.steps, args.warmup
     if (world > 1 or args.routed) and args.config == 4 and not args.unrouted:
         return routed_bench(args, rank, world, local_rank, torch, dist, backend)
-    host_nb = (0, 0) if (args.no_host or world > 1 or args.config == 5) else \
-        ((args.host_batches or 64, (args.host_batches or 64) * 4) if args.config != 3 else (16, 48))
+    host_nb = (0, 0, 0) if (args.no_host or world > 1 or args.config == 5) else \
+        ((args.host_batches or 136, args.host_batches or 136, (args.host_batches or 64) * 4) if args.config != 3
+         else (16, 16, 48))
     n_batches = (K + W) * B + sum(host_nb)
     n_transfers = n_batches * BATCH_MAX
     t_gen = time.time()

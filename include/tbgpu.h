@@ -269,6 +269,18 @@ uint32_t tbgpu_create_transfers(tbgpu_ctx* ctx, uint64_t timestamp,
                                 const tbgpu_transfer_t* events, uint32_t count,
                                 tbgpu_create_transfers_result_t* results);
 
+/* StateMachine.prefetch for create_transfers (src/state_machine.zig:514-655,
+ * prefetch_create_transfers :598-655; the replica awaits its callback before commit,
+ * src/vsr/replica.zig:3384-3415).  The tables are HBM-resident, so what prefetch has
+ * left to do is the batch's host-to-device copy: this enqueues it into the ctx's
+ * staging slot and returns; tbgpu_prefetch_wait returns once the copy has landed (the
+ * callback's point).  The next tbgpu_create_transfers with the same `events` pointer
+ * and `count` commits from the staged copy (no copy inside the commit); any other
+ * create call discards it.  As in the reference, the prepare's body must not change
+ * between prefetch and commit.  Returns 0, or -22 when count exceeds a batch. */
+int tbgpu_prefetch_transfers(tbgpu_ctx* ctx, const tbgpu_transfer_t* events, uint32_t count);
+int tbgpu_prefetch_wait(tbgpu_ctx* ctx);
+
 /* Streaming form: `batch_count` consecutive commits of create_transfers, with
  * identical results to calling tbgpu_create_transfers once per batch in order.
  * Batch b has `counts[b]` events starting after the previous batch's events and

@@ -286,6 +286,12 @@ struct tbgpu_ctx {
     u64* h_res_dev = nullptr;
     u64 h_rc_cap = 0;
     u64 rows_hi = 0;           // upper bound of T.base[BASE_ROWS] (n_rows + events enqueued since)
+    // tbgpu_prefetch_transfers: one batch staged in HBM ahead of its commit
+    u8* pf_buf = nullptr;          // TBGPU_BATCH_MAX * 128 bytes
+    const void* pf_src = nullptr;  // the caller's buffer it was copied from
+    u32 pf_n = 0;
+    bool pf_valid = false;
+    hipEvent_t pf_ev = nullptr;    // recorded behind the copy
     // account-transfers index (query.hip), allocated by the first compaction
     u32 *q_key = nullptr, *q_val = nullptr, *q_tkey = nullptr, *q_tval = nullptr;
     SortScratch q_ss{};
@@ -386,6 +392,8 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->pc = c->counters + PC_OFF;
     c->rg_part = dalloc<u64>(tr_range_part_words(n), &B);
     c->ac_part = dalloc<u64>(n / 256 + 2, &B);
+    c->pf_buf = dalloc<u8>((u64)TBGPU_BATCH_MAX * 128, &B);
+    HIP_CHECK(hipEventCreateWithFlags(&c->pf_ev, hipEventDisableTiming));
 
     HIP_CHECK(hipHostMalloc((void**)&c->h_base, 8 * sizeof(u64), hipHostMallocDefault));  // [4..5]: a uint4
     HIP_CHECK(hipHostMalloc((void**)&c->h_counters, (PC_OFF + 3 * PC_RING) * sizeof(u32), hipHostMallocDefault));
@@ -546,7 +554,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
                     c->f_tile_idr, c->rt_ts_buf, c->rt_ctl_buf, c->rt_dry_ts, c->rt_stats, c->rg_part, c->T.base, c->q_key, c->q_val, c->q_tkey,
                     c->q_tval, c->q_ss.keys_tmp, c->q_ss.vals_tmp, c->q_ss.hist, c->q_runs_dev, c->ximp,
                     c->lst_simple, c->lst_complex, c->d_ev, c->d_chain, c->d_slot, c->d_win, c->w_sstart, c->w_bal,
-                    c->w_undo_slot, c->w_undo_val, c->w_out, c->ac_part};
+                    c->w_undo_slot, c->w_undo_val, c->w_out, c->ac_part, c->pf_buf};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     for (EvalState& s : c->st) {
         void* q[] = {s.res, s.ok, s.pref, s.cfail, s.amt, s.pamt};
@@ -565,6 +573,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
             if (R.ev[h]) (void)hipEventDestroy(R.ev[h]);
         }
     for (hipEvent_t e : c->prof_pool) (void)hipEventDestroy(e);
+    if (c->pf_ev) (void)hipEventDestroy(c->pf_ev);
     (void)hipEventDestroy(c->ev0);
     (void)hipEventDestroy(c->ev1);
     (void)hipStreamDestroy(c->stream);
@@ -1311,8 +1320,9 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         } else {
             // the events' copy (a DMA engine) first, then the small uploads and resets on
             // the compute queue: one engine hand-off before the chunk's kernels, not two.
-            // A pageable source is staged by the runtime: the previous chunk's kernels
-            // (and a fallen-back attempt's undo) have read ev_buf before it is rewritten.
+            // A pageable source is staged through the ctx's page-locked ring (h2d); the
+            // drain first: the previous chunk's kernels (and a fallen-back attempt's undo)
+            // have read ev_buf before it is rewritten.
             wait_stream(c->stream);
             h2d(c, c->ev_buf, ev_src + ev_off, (u64)n * 128, c->stream);
             ev = (const Transfer*)c->ev_buf;
@@ -1652,16 +1662,43 @@ extern "C" void tbgpu_advance_commit_timestamp(tbgpu_ctx* c, uint64_t timestamp)
     HIP_CHECK(hipGetLastError());
 }
 
+extern "C" int tbgpu_prefetch_transfers(tbgpu_ctx* c, const tbgpu_transfer_t* events, uint32_t count) {
+    HIP_CHECK(hipSetDevice(c->device));
+    c->pf_valid = false;
+    if (count > TBGPU_BATCH_MAX) return -22;
+    // behind the previous commit on the ctx's stream (that commit has returned: its
+    // kernels no longer read the slot); a DMA engine moves it while the caller goes on
+    h2d(c, c->pf_buf, events, (u64)count * 128, c->stream);
+    HIP_CHECK(hipEventRecord(c->pf_ev, c->stream));
+    c->pf_src = events;
+    c->pf_n = count;
+    c->pf_valid = true;
+    return 0;
+}
+
+extern "C" int tbgpu_prefetch_wait(tbgpu_ctx* c) {
+    HIP_CHECK(hipSetDevice(c->device));
+    if (c->pf_valid) wait_event(c->pf_ev);
+    return 0;
+}
+
 extern "C" uint32_t tbgpu_create_transfers(tbgpu_ctx* c, uint64_t timestamp, const tbgpu_transfer_t* events,
                                            uint32_t count, tbgpu_create_transfers_result_t* results) {
     uint32_t rc = 0;
     const uint64_t ts = timestamp;
+    if (c->pf_valid && c->pf_src == (const void*)events && c->pf_n == count) {
+        // prefetched: the events are in HBM already (the copy is ahead on the stream)
+        c->pf_valid = false;
+        return (uint32_t)transfers_batches(c, 1, &ts, &count, (const Transfer*)c->pf_buf, true, results, false, &rc);
+    }
+    c->pf_valid = false;
     return (uint32_t)transfers_batches(c, 1, &ts, &count, (const Transfer*)events, false, results, false, &rc);
 }
 
 extern "C" uint64_t tbgpu_create_transfers_batches(tbgpu_ctx* c, uint32_t batch_count, const uint64_t* timestamps,
                                                    const uint32_t* counts, const tbgpu_transfer_t* events,
                                                    tbgpu_create_transfers_result_t* results, uint32_t* result_counts) {
+    c->pf_valid = false;
     return transfers_batches(c, batch_count, timestamps, counts, (const Transfer*)events, false, results, false,
                              result_counts);
 }

@@ -87,6 +87,10 @@ def lib():
     for name in ("tbgpu_lookup_accounts", "tbgpu_lookup_transfers"):
         getattr(L, name).restype = u32
         getattr(L, name).argtypes = [vp, vp, u32, vp]
+    L.tbgpu_prefetch_transfers.restype = ctypes.c_int
+    L.tbgpu_prefetch_transfers.argtypes = [vp, vp, u32]
+    L.tbgpu_prefetch_wait.restype = ctypes.c_int
+    L.tbgpu_prefetch_wait.argtypes = [vp]
     L.tbgpu_test_set_balances.restype = ctypes.c_int
     L.tbgpu_test_set_balances.argtypes = [vp, U128, U128, U128, U128, U128]
     for name in ("tbgpu_account_count", "tbgpu_transfer_count", "tbgpu_history_count", "tbgpu_commit_timestamp"):
@@ -202,6 +206,19 @@ class Engine:
         out = np.zeros(max(len(events), 1), dtype=RESULT_DTYPE)
         n = self._L.tbgpu_create_transfers(self._h, timestamp, _ptr(events), len(events), _ptr(out))
         return out[:n].copy()
+
+    def prefetch_transfers(self, events: np.ndarray) -> None:
+        """StateMachine.prefetch for create_transfers (tbgpu_prefetch_transfers): the
+        batch's copy to HBM is enqueued; create_transfers on the same array commits from
+        it.  `events` must be contiguous TRANSFER_DTYPE and unchanged until that commit."""
+        if events.dtype != TRANSFER_DTYPE or not events.flags["C_CONTIGUOUS"]:
+            raise ValueError("prefetch_transfers needs the contiguous event array create_transfers will get")
+        if self._L.tbgpu_prefetch_transfers(self._h, _ptr(events), len(events)) != 0:
+            raise ValueError("prefetch_transfers: more events than a batch")
+
+    def prefetch_wait(self) -> None:
+        """The prefetch's completion (the reference's prefetch callback point)."""
+        self._L.tbgpu_prefetch_wait(self._h)
 
     def create_transfers_batches(self, timestamps, counts, events):
         ts = np.ascontiguousarray(timestamps, dtype=np.uint64)

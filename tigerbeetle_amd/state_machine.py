@@ -25,6 +25,7 @@ class StateMachine:
         self.engine = engine or Engine(**engine_options)
         self.prepare_timestamp = 0
         self.commit_timestamp = 0
+        self._prefetched = None  # the create_transfers body prefetch staged (its array view)
 
     # src/state_machine.zig:503-512
     def prepare(self, operation: Operation, input: bytes) -> None:
@@ -37,9 +38,16 @@ class StateMachine:
         self.engine.compact()
         callback(self)
 
-    # src/state_machine.zig:514-576 — the HBM tables need no prefetch; the callback
-    # still runs (the reference delivers it asynchronously via the grid's next tick).
+    # src/state_machine.zig:514-655 — the tables are HBM-resident, so prefetch has only
+    # the batch's host-to-device copy left to do: create_transfers stages it
+    # (tbgpu_prefetch_transfers) and the commit of the same body skips its copy.  The
+    # callback runs once the copy has landed (the reference delivers it asynchronously
+    # via the grid's next tick).
     def prefetch(self, callback, op: int, operation: Operation, input: bytes) -> None:
+        if operation == Operation.create_transfers and input:
+            self._prefetched = np.frombuffer(input, dtype=TRANSFER_DTYPE)
+            self.engine.prefetch_transfers(self._prefetched)
+            self.engine.prefetch_wait()
         callback(self)
 
     # src/state_machine.zig:894-928
@@ -50,7 +58,11 @@ class StateMachine:
             events = np.frombuffer(input, dtype=ACCOUNT_DTYPE)
             out = self.engine.create_accounts(timestamp, events)
         elif operation == Operation.create_transfers:
-            events = np.frombuffer(input, dtype=TRANSFER_DTYPE)
+            pre = getattr(self, "_prefetched", None)
+            # the prefetched view of this very body (same buffer): the staged copy is used
+            events = pre if pre is not None and pre.base is not None and pre.base is input else \
+                np.frombuffer(input, dtype=TRANSFER_DTYPE)
+            self._prefetched = None
             out = self.engine.create_transfers(timestamp, events)
         elif operation == Operation.lookup_accounts:
             ids = np.frombuffer(input, dtype=U128_DTYPE)

@@ -232,8 +232,18 @@ typedef struct tbgpu_options {
     uint64_t history_max;         /* account-history rows                            */
     uint64_t events_per_call_max; /* events one (multi-batch) call may carry        */
     uint32_t flags;               /* TBGPU_OPT_*                                    */
-    uint32_t dense_block_span;    /* 0, or S: ids (b << 32) | k, b < accounts_max / S + 2,
+    uint32_t dense_block_span;    /* 0, or S: ids (b << 32) | k, b < directory_max / S + 2,
                                      1 <= k <= S, sit in the direct-mapped directory  */
+    uint64_t directory_max;       /* accounts the directory must know (0: accounts_max); more
+                                     than accounts_max only for a ledger shard (below)  */
+    uint64_t hashed_max;          /* accounts whose ids fall outside the direct-mapped
+                                     directory (0: directory_max): sizes the hash index */
+    uint32_t shard_world;         /* 0 or 1: one state machine.  N >= 2: this ctx is the
+                                     ledger shard shard_rank of N (ledger % N == rank owns
+                                     the ledger): it stores 128-byte rows only for accounts
+                                     of its ledgers, and a directory entry (id, ledger) for
+                                     every other account                */
+    uint32_t shard_rank;
 } tbgpu_options;
 
 enum {
@@ -325,6 +335,15 @@ uint64_t tbgpu_create_accounts_batches_device(tbgpu_ctx* ctx, uint32_t batch_cou
  * reference counterpart: they carry what `execute` (src/state_machine.zig:1018-1083)
  * derives from a batch's position -- the event timestamps and the linked-chain
  * bounds -- for sub-batches whose events are not contiguous in their batch. */
+enum {
+    /* A ledger shard's create_accounts reply for an event whose id names an account of
+     * another shard's ledger (create_account_exists, src/state_machine.zig:1227-1237,
+     * compares the existing row, which only its owner stores): a failure like every
+     * `exists*` code, whose exact code the owner's reply for the same event carries
+     * (tigerbeetle_amd/shard.py merges them).  Never returned by an unsharded ctx. */
+    TBGPU_SHARD_ACCOUNT_EXISTS_ELSEWHERE = 255,
+};
+
 enum {
     /* The chain this event belongs to continues on another shard after it: the
      * event closes the local part of the chain (no linked_event_chain_open). */

@@ -16,7 +16,7 @@ from tests.thread_dist import ThreadDist, ThreadGroup
 pytestmark = pytest.mark.gpu
 
 
-def _run(w, world, pipelined=False, expect_wire=True):
+def _run(w, world, pipelined=False, expect_wire=True, shard_rows=False):
     import torch
 
     from tigerbeetle_amd.engine import Engine
@@ -29,8 +29,13 @@ def _run(w, world, pipelined=False, expect_wire=True):
     def worker(rank):
         eng = None
         try:
-            eng = Engine(device=0, accounts_max=len(w.accounts) + 16, transfers_max=1 << 16, history_max=1 << 12,
-                         events_per_call_max=1 << 14)
+            if shard_rows:  # a ledger shard: rows of its own ledgers' accounts, directory entries for all
+                eng = Engine(device=0, accounts_max=len(w.accounts) + 16, directory_max=len(w.accounts) + 16,
+                             transfers_max=1 << 16, history_max=1 << 12, events_per_call_max=1 << 14,
+                             shard_world=world, shard_rank=rank)
+            else:
+                eng = Engine(device=0, accounts_max=len(w.accounts) + 16, transfers_max=1 << 16, history_max=1 << 12,
+                             events_per_call_max=1 << 14)
             comm = Comm(rank, world, device=dev)
             comm.dist = ThreadDist(group, rank)
             sm = ShardedStateMachine(eng, comm)
@@ -111,3 +116,17 @@ def test_general_step_random_u128_ids_on_gpu(world):
     w = random_u128_ids(ShardWorkload(131 + world, world, 3, 2), 131 + world)
     stats = _run(w, world, expect_wire=False)
     assert stats["steps"] > 0 and stats["dry_rounds"] > 0
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ledger_shard_engines(world):
+    """Ledger-shard engines (tbgpu_options.shard_world): each keeps the 128-byte rows
+    of its own ledgers' accounts only; re-created accounts answer the exact exists_*
+    code through the router's merge; the flag-heavy mix and config 4's cross-ledger
+    pairs commit as on replicated engines."""
+    from tests.shard_backends import with_account_recreates
+    stats = _run(with_account_recreates(ShardWorkload(141 + world, world, 3, 2), 141 + world), world,
+                 expect_wire=False, shard_rows=True)
+    assert stats["steps"] > 0
+    stats = _run(config4_failing(151 + world, world, 3, 2), world, shard_rows=True)
+    assert stats["preruns"] > 0

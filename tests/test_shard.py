@@ -29,7 +29,10 @@ def _free_port() -> int:
     return p
 
 
-def _backend(kind, w):
+def _backend(kind, w, rank=0, world=1):
+    if kind == "ledgershard":  # the oracle standing in for a ledger-shard engine (tests/shard_backends.py)
+        from tests.shard_backends import LedgerShardOracle
+        return LedgerShardOracle(oracle.Oracle(len(w.accounts), 1 << 14), world, rank)
     if kind == "gpu":
         from tigerbeetle_amd.engine import Engine
         return Engine(device=0, accounts_max=len(w.accounts) + 16, transfers_max=1 << 15, history_max=1 << 14,
@@ -45,7 +48,7 @@ def _worker(rank, world, port, out_dir, spec, kind="oracle", device_step=False, 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         w = _make(spec)
-        sm = ShardedStateMachine(_backend(kind, w), Comm(rank, world))
+        sm = ShardedStateMachine(_backend(kind, w, rank, world), Comm(rank, world))
         if max_rounds is not None:
             sm.max_rounds = max_rounds
         sm.vectorized = vectorized
@@ -88,6 +91,9 @@ def _make(spec):
         return ShardWorkload(seed, world, steps, B)
     if kind == "mixr":
         return random_u128_ids(ShardWorkload(seed, world, steps, B), seed)
+    if kind == "mixa":
+        from tests.shard_backends import with_account_recreates
+        return with_account_recreates(ShardWorkload(seed, world, steps, B), seed)
     if kind in ("c4f", "c4l"):
         return config4_failing(seed, world, steps, B, limits=kind == "c4l")
     return config4_small(seed, world, steps, B)
@@ -221,3 +227,14 @@ def test_reference_router_still_exact(spec):
     """shard.py _round (the event-by-event statement of the general step) against the
     same oracle: it stays the reference that round_vec is checked against."""
     _check(spec, spec[2], vectorized=False)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ledger_shard_rows_exists_codes_from_the_owner(world):
+    """Ledger-shard backends (each rank keeps the rows of its own ledgers' accounts, a
+    directory entry for the others): accounts re-created with a changed field answer
+    the exact exists_with_different_* code, which only the row's owner can compare
+    (src/state_machine.zig:1227-1237), through the router's merge; chains of new
+    accounts that those failures break roll back alike on every rank."""
+    stats = _check(("mixa", 41 + world, world, 2, 2), world, kind="ledgershard")
+    assert stats["steps"] > 0

@@ -66,7 +66,7 @@ __device__ __forceinline__ u32 ac_classify_one(const Tables& T, const AcArgs& C,
     else if (a.code == 0) sres = TBGPU_CREATE_ACCOUNT_CODE_MUST_NOT_BE_ZERO;
     else {
         sres = SRES_DYN;
-        pre = acc_probe(T.aidx, T.aidx_mask, a.id);
+        pre = acc_row(T, a.id);  // ROW_FOREIGN: an account another ledger shard stores
         if (dup_check) {  // ids that rise strictly through the call cannot repeat (ac_mono)
             gslot = ac_gtab_insert(C, a.id, i);
             atomicAdd(&C.gcnt_id[gslot], 1u);
@@ -166,6 +166,7 @@ __global__ void ac_evaluate(Tables T, AcArgs C, const u8* res_s, const u8* ok_s,
             if (C.cs[j] == csi ? (o & 1) : (o & 2)) { e = j; break; }
         }
         if (e != NONE32) r = account_exists(a, C.ev[e]);
+        else if (C.pre[i] == ROW_FOREIGN) r = TBGPU_SHARD_ACCOUNT_EXISTS_ELSEWHERE;  // its owner compares
         else if (C.pre[i] != NONE32) r = account_exists(a, T.acc[C.pre[i]]);
         else r = TBGPU_CREATE_ACCOUNT_OK;
     }
@@ -175,8 +176,8 @@ __global__ void ac_evaluate(Tables T, AcArgs C, const u8* res_s, const u8* ok_s,
     if (r != res_s[i]) atomicAdd(&C.counters[CNT_CHANGES], 1u);  // few: only events whose result moved
 }
 
-__device__ __forceinline__ u64 ac_mask_one(const AcArgs& C, const u8* res, const u8* ok, const u32* cfail, u8* fres,
-                                           u8* mask, u32 i) {
+__device__ __forceinline__ u64 ac_mask_one(const Tables& T, const AcArgs& C, const u8* res, const u8* ok,
+                                           const u32* cfail, u8* fres, u8* mask, u32 i) {
     const u32 cs = C.cs[i];
     const u32 cf = cs != C.ce[i] ? cfail[cs] : NONE32;
     u8 r;
@@ -186,7 +187,10 @@ __device__ __forceinline__ u64 ac_mask_one(const AcArgs& C, const u8* res, const
     else if (cf != NONE32) r = TBGPU_CREATE_ACCOUNT_LINKED_EVENT_FAILED;
     else r = TBGPU_CREATE_ACCOUNT_OK;
     fres[i] = r;
-    mask[i] = ((ok[i] & 2) ? 1 : 0) | (r != 0 ? 2 : 0);
+    // bit 0: a row here (persisted, this shard's ledger); bit 2: persisted on another
+    // shard's ledger (a directory entry only)
+    const bool kept = ok[i] & 2, own = ledger_owned(T, C.ev[i].ledger);
+    mask[i] = (kept && own ? 1 : 0) | (r != 0 ? 2 : 0) | (kept && !own ? 4 : 0);
     // commit_timestamp survives rollback (:1223)
     return ((ok[i] & 1) && (cf == NONE32 || i < cf)) ? C.ts[i] : 0;
 }
@@ -195,11 +199,12 @@ __device__ __forceinline__ u64 ac_mask_one(const AcArgs& C, const u8* res, const
 // workgroup (ac_ts_fold) into the single commit_timestamp word: same-address atomics
 // serialize at the memory side (one per accepted event took 897 us for 10M accounts,
 // one per wave still 890 us).
-__global__ void ac_mask(AcArgs C, const u8* res, const u8* ok, const u32* cfail, u8* fres, u8* mask, const u32* gate) {
+__global__ void ac_mask(Tables T, AcArgs C, const u8* res, const u8* ok, const u32* cfail, u8* fres, u8* mask,
+                        const u32* gate) {
     if (gate && *gate == 0) return;
     __shared__ u64 s_w[4];
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    u64 ts = i < C.n ? ac_mask_one(C, res, ok, cfail, fres, mask, i) : 0;
+    u64 ts = i < C.n ? ac_mask_one(T, C, res, ok, cfail, fres, mask, i) : 0;
     ts = wave_max_u64(ts);
     if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = ts;
     __syncthreads();
@@ -234,24 +239,20 @@ __global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const
     }
     if (!(ok[i] & 2)) return;
     Account a = C.ev[i];
+    if (!ledger_owned(T, a.ledger)) {  // another ledger shard stores the row: the directory entry only
+        acc_insert(T, a.id, ROW_FOREIGN, a.ledger, a.flags, a.code);
+        return;
+    }
     a.timestamp = C.ts[i];
     // accounts.insert: the row is the event's rank among the persisted accounts
-    // (creation order); the index slot is claimed by CAS on its row word.
+    // (creation order); the directory entry (or index slot) names it.
     if (row_base + rk[i].x >= cap) {  // accounts_max exceeded: nothing past it is written (the host aborts)
         atomicOr(&C.counters[CNT_FLAGS], (u32)FL_CAPACITY);
         return;
     }
     const u32 row = (u32)(row_base + rk[i].x);
     T.acc[row] = a;
-    u64 h = hash128(a.id) & T.aidx_mask;
-    while (atomicCAS(&T.aidx[h].row1, 0u, row + 1) != 0) h = (h + 1) & T.aidx_mask;
-    AccIdx& e = T.aidx[h];
-    e.id_lo = (u64)a.id;
-    e.id_hi = (u64)(a.id >> 64);
-    e.ledger = a.ledger;
-    e.flags = a.flags;
-    e.code = a.code;
-    if (dense_has(T, a.id)) T.dense[dense_slot(T, a.id)] = dense_entry(row, a.ledger, a.flags);
+    acc_insert(T, a.id, row, a.ledger, a.flags, a.code);
 }
 
 // ---------------------------------------------- the clean call in two passes --
@@ -320,15 +321,7 @@ __global__ __launch_bounds__(AF_THREADS) void ac_fast_index(Tables T, AcArgs C, 
         const uint4 m = ((const uint4*)&T.acc[row])[7];
         const u128 id = ((u128)(((u64)k.w << 32) | k.z) << 64) | (((u64)k.y << 32) | k.x);
         const u16 code = (u16)(m.y & 0xFFFFu), flags = (u16)(m.y >> 16);
-        u64 h = hash128(id) & T.aidx_mask;
-        while (atomicCAS(&T.aidx[h].row1, 0u, row + 1) != 0) h = (h + 1) & T.aidx_mask;
-        AccIdx& x = T.aidx[h];
-        x.id_lo = (u64)id;
-        x.id_hi = (u64)(id >> 64);
-        x.ledger = m.x;
-        x.flags = flags;
-        x.code = code;
-        if (dense_has(T, id)) T.dense[dense_slot(T, id)] = dense_entry(row, m.x, flags);
+        acc_insert(T, id, row, m.x, flags, code);
     }
     if (blockIdx.x == 0) {
         // replies: none; commit_timestamp: the latest event's (every event is accepted)
@@ -352,9 +345,9 @@ __global__ void ac_batch_counts(const u32* b_start, u32 nb, const uint4* rk, u32
 __global__ void k_lookup_accounts(Tables T, const u128* ids, u32 n, Account* out, u8* found) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const u32 s = acc_probe(T.aidx, T.aidx_mask, ids[i]);
-    found[i] = s != NONE32;
-    if (s != NONE32) out[i] = T.acc[s];
+    const u32 s = acc_row(T, ids[i]);
+    found[i] = s != NONE32 && s != ROW_FOREIGN;  // another shard's account: its owner answers
+    if (found[i]) out[i] = T.acc[s];
 }
 __global__ void k_lookup_transfers(Tables T, const u128* ids, u32 n, Transfer* out, u8* found) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -364,8 +357,8 @@ __global__ void k_lookup_transfers(Tables T, const u128* ids, u32 n, Transfer* o
     if (r != NONE32) out[i] = T.xrows[r];
 }
 __global__ void k_set_balances(Tables T, u128 id, Bal4 b, int* status) {
-    const u32 s = acc_probe(T.aidx, T.aidx_mask, id);
-    if (s == NONE32) { *status = -1; return; }
+    const u32 s = acc_row(T, id);
+    if (s == NONE32 || s == ROW_FOREIGN) { *status = -1; return; }
     Account& a = T.acc[s];
     a.debits_pending = b.dp;
     a.debits_posted = b.dpo;
@@ -419,15 +412,44 @@ __global__ void k_rebuild_aidx(Tables T, u64 n) {
     const u64 row = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (row >= n) return;
     const Account& a = T.acc[row];
-    u64 h = hash128(a.id) & T.aidx_mask;
-    while (atomicCAS(&T.aidx[h].row1, 0u, (u32)row + 1) != 0) h = (h + 1) & T.aidx_mask;
-    AccIdx& e = T.aidx[h];
-    e.id_lo = (u64)a.id;
-    e.id_hi = (u64)(a.id >> 64);
-    e.ledger = a.ledger;
-    e.flags = a.flags;
-    e.code = a.code;
-    if (dense_has(T, a.id)) T.dense[dense_slot(T, a.id)] = dense_entry((u32)row, a.ledger, a.flags);
+    acc_insert(T, a.id, (u32)row, a.ledger, a.flags, a.code);
+}
+
+// tbgpu_open of a ledger shard: the other shards' accounts' directory entries.
+__global__ void k_insert_foreign(Tables T, const ForeignAccount* f, u64 n) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    acc_insert(T, ((u128)f[k].id_hi << 64) | f[k].id_lo, ROW_FOREIGN, f[k].ledger, 0, 0);
+}
+
+// tbgpu_checkpoint of a ledger shard: the directory entries of other shards'
+// accounts, gathered (in no particular order; the host sorts them) from the
+// direct-mapped directory and the hash index.
+__global__ void k_collect_foreign(Tables T, ForeignAccount* out, u32* cursor, u64 cap) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    ForeignAccount f{};
+    bool hit = false;
+    if (k < T.dense_n) {
+        const u64 e = T.dense[k];
+        if (e != 0 && ((u32)e & DENSE_ROW1_MASK) == DENSE_FOREIGN1) {
+            const u64 b = k / T.dense_span, j = k % T.dense_span + 1;
+            f.id_lo = (b << 32) | j;
+            f.ledger = (u32)(e >> 32);
+            hit = true;
+        }
+    } else if (k - T.dense_n <= T.aidx_mask) {
+        const AccIdx& e = T.aidx[k - T.dense_n];
+        if (e.row1 == ROW_FOREIGN + 1) {
+            f.id_lo = e.id_lo;
+            f.id_hi = e.id_hi;
+            f.ledger = e.ledger;
+            hit = true;
+        }
+    }
+    if (hit) {
+        const u32 at = atomicAdd(cursor, 1u);
+        if (at < cap) out[at] = f;
+    }
 }
 
 // tbgpu_open: the fast path's overflow guard (fast.hip) from the restored balances.
@@ -445,6 +467,16 @@ __global__ void k_scan_big(Tables T, u64 n) {
 
 #define GRID(n) (u32)(((n) + 255) / 256), 256, 0, stream
 
+void launch_insert_foreign(const Tables& T, const ForeignAccount* f, u64 n, hipStream_t stream) {
+    if (!n) return;
+    k_insert_foreign<<<GRID(n)>>>(T, f, n);
+    HIP_CHECK(hipGetLastError());
+}
+void launch_collect_foreign(const Tables& T, ForeignAccount* out, u32* cursor, u64 cap, hipStream_t stream) {
+    const u64 n = T.dense_n + T.aidx_mask + 1;
+    k_collect_foreign<<<GRID(n)>>>(T, out, cursor, cap);
+    HIP_CHECK(hipGetLastError());
+}
 void launch_rebuild_accounts(const Tables& T, u64 n, hipStream_t stream) {
     if (!n) return;
     k_rebuild_aidx<<<GRID(n)>>>(T, n);
@@ -475,7 +507,7 @@ void ac_launch_evaluate(const Tables& T, const AcArgs& C, const u8* res_s, const
 void ac_launch_mask(const Tables& T, const AcArgs& C, const u8* res, const u8* ok, const u32* cfail, u8* fres,
                     u8* mask, hipStream_t stream, const u32* gate) {
     static_assert(256 == 4 * 64, "ac_mask folds four waves per workgroup");
-    ac_mask<<<GRID(C.n)>>>(C, res, ok, cfail, fres, mask, gate);
+    ac_mask<<<GRID(C.n)>>>(T, C, res, ok, cfail, fres, mask, gate);
     ac_ts_fold<<<1, 1024, 0, stream>>>(C.ts_part, (C.n + 255) / 256, T.commit_ts, gate);
 }
 void ac_launch_fast(const Tables& T, const AcArgs& C, u64 row_base, hipStream_t stream) {

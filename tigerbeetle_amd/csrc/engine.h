@@ -59,8 +59,28 @@ struct Tables {
     // sequential ids never touch the hash index).  xrun[2..3] the first id (lo, hi),
     // xrun[4..5] the last; empty when xrun[0] == xrun[1].
     u64* xrun;
+    // Ledger shard (tbgpu_options.shard_world >= 2): rows are stored only for accounts
+    // of the ledgers this ctx owns (ledger % shard_world == shard_rank); every other
+    // account has a directory entry whose row is ROW_FOREIGN (its id and ledger: what
+    // create_transfer's checks of :1273-1281 read of an account on another ledger).
+    u32 shard_world, shard_rank;
 };
 enum { BASE_ROWS = 0, BASE_HIST = 1, BASE_REPLIES = 2 };
+
+// A ledger shard's record of another shard's account (checkpoint image, tbgpu_open).
+struct ForeignAccount {
+    u64 id_lo, id_hi;
+    u32 ledger, pad;
+};
+static_assert(sizeof(ForeignAccount) == 24, "ForeignAccount layout");
+
+// The row of an account another shard stores (directory entry only).
+constexpr u32 ROW_FOREIGN = 0xFFFFFFFEu;
+constexpr u32 DENSE_ROW1_MASK = 0x1FFFFFFFu;   // row + 1 in the directory entry's low 29 bits
+constexpr u32 DENSE_FOREIGN1 = DENSE_ROW1_MASK;  // ... all ones: ROW_FOREIGN
+__device__ __forceinline__ bool ledger_owned(const Tables& T, u32 ledger) {
+    return T.shard_world < 2 || ledger % T.shard_world == T.shard_rank;
+}
 
 __device__ __forceinline__ bool dense_has(const Tables& T, u128 id) {
     const u64 lo = (u64)id;
@@ -72,12 +92,19 @@ __device__ __forceinline__ u64 dense_slot(const Tables& T, u128 id) {
     return (lo >> 32) * T.dense_span + (u32)lo - 1;
 }
 __device__ __forceinline__ u64 dense_entry(u32 row, u32 ledger, u16 flags) {
-    return (u64)(row + 1) | ((u64)(flags & 0xEu) << 28) | ((u64)ledger << 32);
+    const u64 r1 = row == ROW_FOREIGN ? DENSE_FOREIGN1 : row + 1;
+    return r1 | ((u64)(flags & 0xEu) << 28) | ((u64)ledger << 32);
+}
+__device__ __forceinline__ u32 dense_row(u64 e) {  // of a nonzero entry
+    const u32 r1 = (u32)e & DENSE_ROW1_MASK;
+    return r1 == DENSE_FOREIGN1 ? ROW_FOREIGN : r1 - 1;
 }
 
 // Account lookup: the direct-mapped directory for ids 1..dense_n (8 bytes), the
-// hash index otherwise.  Returns the row (NONE32 when absent) with its ledger and
-// flags (limit / history bits), which are immutable after create_account.
+// hash index otherwise (it holds only ids outside the directory).  Returns the row
+// (NONE32 when absent, ROW_FOREIGN for an account another ledger shard stores) with
+// its ledger and flags (limit / history bits), which are immutable after
+// create_account.
 __device__ __forceinline__ u32 acc_find(const Tables& T, u128 id, u32* ledger, u16* flags);
 
 __device__ __forceinline__ bool xidx_maybe_present(const Tables& T, u128 id) {
@@ -226,7 +253,7 @@ __device__ __forceinline__ u32 acc_find(const Tables& T, u128 id, u32* ledger, u
         if (e == 0) return NONE32;
         *ledger = (u32)(e >> 32);
         *flags = (u16)((e >> 28) & 0xE);
-        return (u32)(e & 0x1FFFFFFFu) - 1;
+        return dense_row(e);
     }
     const u64 lo = (u64)id, hi = (u64)(id >> 64);
     u64 h = hash128(lo, hi) & T.aidx_mask;
@@ -240,6 +267,31 @@ __device__ __forceinline__ u32 acc_find(const Tables& T, u128 id, u32* ledger, u
         }
         h = (h + 1) & T.aidx_mask;
     }
+}
+
+// The row of an account (NONE32 absent, ROW_FOREIGN on another shard).
+__device__ __forceinline__ u32 acc_row(const Tables& T, u128 id) {
+    u32 led;
+    u16 fl;
+    return acc_find(T, id, &led, &fl);
+}
+
+// Insert of a new account's directory entry: the direct-mapped entry for ids it
+// covers, a hash-index slot (claimed by CAS on its row word) for the others.  `row`
+// may be ROW_FOREIGN (a ledger shard's entry for another shard's account).
+__device__ __forceinline__ void acc_insert(const Tables& T, u128 id, u32 row, u32 ledger, u16 flags, u16 code) {
+    if (dense_has(T, id)) {
+        T.dense[dense_slot(T, id)] = dense_entry(row, ledger, flags);
+        return;
+    }
+    u64 h = hash128(id) & T.aidx_mask;
+    while (atomicCAS(&T.aidx[h].row1, 0u, row + 1) != 0) h = (h + 1) & T.aidx_mask;
+    AccIdx& e = T.aidx[h];
+    e.id_lo = (u64)id;
+    e.id_hi = (u64)(id >> 64);
+    e.ledger = ledger;
+    e.flags = flags;
+    e.code = code;
 }
 
 // Transfer-id index hash: runs of 16 consecutive ids share one 64-byte line of
@@ -326,4 +378,5 @@ enum {
     FL_NONMONO = 1u << 10,    // fast path: ids of the call are not strictly increasing
     FL_FCHAIN = 1u << 11,     // fast path: linked chains, resolved by fp_chains
     FL_CAPACITY = 1u << 12,   // create_accounts: accounts_max reached (ac_apply wrote nothing past it)
+    FL_FOREIGN = 1u << 13,    // ledger shard: a transfer on a ledger another shard owns reached its balances
 };

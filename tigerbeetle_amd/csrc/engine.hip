@@ -173,6 +173,7 @@ struct tbgpu_ctx {
     u64 aidx_cap = 0, xrow_cap = 0, xidx_cap = 0, hist_cap = 0;
     u64 accounts_max = 0;
     u64 n_accounts = 0, n_rows = 0, n_hist = 0;
+    u64 n_foreign = 0;  // ledger shard: other shards' accounts in the directory
     u64 bytes = 0;
 
     // per-call scratch (nmax events, bmax batches)
@@ -464,6 +465,10 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     if (!o.events_per_call_max) o.events_per_call_max = 1u << 20;
     if (o.events_per_call_max < TBGPU_BATCH_MAX) o.events_per_call_max = TBGPU_BATCH_MAX;
     if (o.transfers_max >= 0x7FFFFFFFull || o.events_per_call_max >= (1ull << 29)) return -22;
+    if (!o.directory_max) o.directory_max = o.accounts_max;
+    if (o.directory_max < o.accounts_max) return -22;
+    if (!o.hashed_max) o.hashed_max = o.directory_max;
+    if (o.shard_world >= 2 && o.shard_rank >= o.shard_world) return -22;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return -19;  // ENODEV
     if (o.device < 0 || o.device >= ndev) return -19;
@@ -476,7 +481,7 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     HIP_CHECK(hipEventCreate(&c->ev0));
     HIP_CHECK(hipEventCreate(&c->ev1));
     c->accounts_max = o.accounts_max;
-    c->aidx_cap = pow2_at_least(2 * o.accounts_max);
+    c->aidx_cap = pow2_at_least(2 * o.hashed_max);  // ids outside the direct-mapped directory
     c->xrow_cap = o.transfers_max;
     c->xidx_cap = pow2_at_least(2 * o.transfers_max);
     c->hist_cap = o.history_max;
@@ -495,16 +500,20 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     c->T.xrun = dalloc<u64>(8, &B);
     c->T.big = dalloc<u32>(4, &B);
     c->T.base = dalloc<u64>(4, &B);
+    c->T.shard_world = o.shard_world >= 2 ? o.shard_world : 0;
+    c->T.shard_rank = o.shard_world >= 2 ? o.shard_rank : 0;
     c->T.xrow_cap = c->xrow_cap;
     c->T.hist_cap = c->hist_cap;
-    // row + 1 in 29 bits; ids below 2^32 in block 0, or dense_block_span-wide blocks
-    // for ledger-major ids, one spare block (ledgers are numbered from 1)
-    if (o.accounts_max > 0 && o.accounts_max < (1ull << 29) - 1) {
-        const u64 span = o.dense_block_span ? o.dense_block_span : std::max<u64>(o.accounts_max, 1);
+    // row + 1 in 29 bits (all ones: another shard's account); ids below 2^32 in block
+    // 0, or dense_block_span-wide blocks for ledger-major ids, one spare block (ledgers
+    // are numbered from 1)
+    if (o.accounts_max > 0 && o.accounts_max < (1ull << 29) - 2) {
+        const u64 dm = o.directory_max;
+        const u64 span = o.dense_block_span ? o.dense_block_span : std::max<u64>(dm, 1);
         c->T.dense_span = span;
-        c->T.dense_blocks = o.dense_block_span ? (o.accounts_max + span - 1) / span + 2 : 1;
+        c->T.dense_blocks = o.dense_block_span ? (dm + span - 1) / span + 2 : 1;
         c->T.dense_n = c->T.dense_span * c->T.dense_blocks;
-        if (!o.dense_block_span) c->T.dense_n = o.accounts_max;
+        if (!o.dense_block_span) c->T.dense_n = dm;
     }
     c->T.dense = dalloc_hot<u64>(c->T.dense_n, &B);
     alloc_scratch(c, o.events_per_call_max);
@@ -529,6 +538,7 @@ extern "C" void tbgpu_reset(tbgpu_ctx* c) {
     HIP_CHECK(hipMemsetAsync(c->f_gtab, 0, c->f_gcap * sizeof(u32), c->stream));  // fast path's claim table
     wait_stream(c->stream);
     c->n_accounts = c->n_rows = c->n_hist = 0;
+    c->n_foreign = 0;
     c->rows_hi = 0;
     c->q_runs.assign(1, 0);
 }
@@ -993,6 +1003,9 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
         HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, (PC_OFF + PC_RING) * sizeof(u32), hipMemcpyDeviceToHost,
                                  s));
         wait_stream(s);
+        if (c->h_counters[CNT_FLAGS] & FL_FOREIGN)
+            tbgpu_fatal("create_transfers", "a transfer of a ledger another shard owns (ledger shard ctx)", __FILE__,
+                        __LINE__);
         if (c->h_counters[CNT_FLAGS] & FL_ERROR) tbgpu_fatal("create_transfers", "device error", __FILE__, __LINE__);
         static const bool trace = getenv("TBGPU_TRACE_PASSES") != nullptr;  // diagnostics only
         if (trace) {
@@ -1730,7 +1743,8 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
     C.ts_part = c->ac_part;
     C.counts_out = c->counts;
     static const bool no_fast = getenv("TBGPU_NO_AC_FAST") != nullptr;  // A/B timing of the general path
-    if (!no_fast && !(c->opt.flags & TBGPU_OPT_FORCE_GENERAL) && c->n_accounts + n <= c->accounts_max) {
+    if (!no_fast && !(c->opt.flags & TBGPU_OPT_FORCE_GENERAL) && c->n_accounts + n <= c->accounts_max &&
+        !c->T.shard_world) {
         // the clean call (accounts.hip ac_fast_*): one round trip decides whether it stood
         HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)(c->counters + CNT_FLAGS), 0, 1, s));
         ac_launch_fast(c->T, C, c->n_accounts, s);
@@ -1779,6 +1793,7 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
         if (flags & FL_ERROR) tbgpu_fatal("create_accounts", "device error", __FILE__, __LINE__);
         c->stats.iterations = 1;
         c->n_accounts += tot.x;
+        c->n_foreign += tot.z;
         return;
     }
     if (flags & FL_MULTI_ID)
@@ -1803,6 +1818,7 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
     d2h(c, counts_host, c->counts, nb * sizeof(u32), s);
     wait_stream(s);
     c->n_accounts += tot.x;
+    c->n_foreign += tot.z;
 }
 
 static uint64_t accounts_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t* timestamps, const uint32_t* counts,
@@ -2046,15 +2062,20 @@ extern "C" uint64_t tbgpu_get_account_history_device(tbgpu_ctx* c, uint32_t coun
 
 namespace {
 constexpr u64 CK_MAGIC = 0x314B435550474254ull;  // "TBGPUCK1"
+// version 1: one state machine; version 2: a ledger shard's image, which also lists
+// the other shards' accounts its directory knows (n_foreign ForeignAccount records,
+// sorted by id, after the history rows)
 struct CkHeader {
     u64 magic;
     u32 version, reserved;
     u64 n_accounts, n_rows, n_hist, commit_ts, checksum;
-    u64 pad;
+    u64 n_foreign;
 };
 static_assert(sizeof(CkHeader) == 64, "checkpoint header");
 
-u64 ck_payload_bytes(u64 na, u64 nr, u64 nh) { return na * 128 + nr * 128 + 2 * nr + nh * 256; }
+u64 ck_payload_bytes(u64 na, u64 nr, u64 nh, u64 nf) {
+    return na * 128 + nr * 128 + 2 * nr + nh * 256 + nf * sizeof(ForeignAccount);
+}
 
 // Checksum of the payload: four interleaved multiply-xor lanes over u64 words
 // (integrity against truncation and corruption, not an adversary).
@@ -2070,7 +2091,7 @@ u64 ck_checksum(const u8* p, u64 n) {
 }  // namespace
 
 extern "C" uint64_t tbgpu_checkpoint_size(tbgpu_ctx* c) {
-    return sizeof(CkHeader) + ck_payload_bytes(c->n_accounts, c->n_rows, c->n_hist);
+    return sizeof(CkHeader) + ck_payload_bytes(c->n_accounts, c->n_rows, c->n_hist, c->n_foreign);
 }
 
 extern "C" uint64_t tbgpu_checkpoint(tbgpu_ctx* c, void* out, uint64_t capacity) {
@@ -2087,9 +2108,32 @@ extern "C" uint64_t tbgpu_checkpoint(tbgpu_ctx* c, void* out, uint64_t capacity)
     if (nr && c->ximp) d2h(c, imp, c->ximp, nr, c->stream);
     else memset(imp, 0, nr);
     if (nh) d2h(c, imp + nr, c->T.hrows, nh * 256, c->stream);
+    const u64 nf = c->n_foreign;
+    if (nf) {
+        // the directory's entries for other shards' accounts, gathered, then sorted by id
+        // (the gather's order is not deterministic; the image is)
+        ForeignAccount* buf = nullptr;
+        u32* cur = nullptr;
+        HIP_CHECK(hipMalloc((void**)&buf, nf * sizeof(ForeignAccount)));
+        HIP_CHECK(hipMalloc((void**)&cur, sizeof(u32)));
+        HIP_CHECK(hipMemsetAsync(cur, 0, sizeof(u32), c->stream));
+        launch_collect_foreign(c->T, buf, cur, nf, c->stream);
+        u32 got = 0;
+        d2h(c, &got, cur, sizeof(u32), c->stream);
+        ForeignAccount* fa = (ForeignAccount*)(imp + nr + nh * 256);
+        d2h(c, fa, buf, nf * sizeof(ForeignAccount), c->stream);
+        wait_stream(c->stream);
+        HIP_CHECK(hipFree(buf));
+        HIP_CHECK(hipFree(cur));
+        if (got != nf) tbgpu_fatal("checkpoint", "directory holds another count of foreign accounts", __FILE__, __LINE__);
+        std::sort(fa, fa + nf, [](const ForeignAccount& a, const ForeignAccount& b) {
+            return a.id_hi != b.id_hi ? a.id_hi < b.id_hi : a.id_lo < b.id_lo;
+        });
+    }
     CkHeader h{};
     h.magic = CK_MAGIC;
-    h.version = 1;
+    h.version = nf ? 2 : 1;
+    h.n_foreign = nf;
     h.n_accounts = na;
     h.n_rows = nr;
     h.n_hist = nh;
@@ -2104,8 +2148,10 @@ extern "C" int tbgpu_open(tbgpu_ctx* c, const void* image, uint64_t size) {
     if (size < sizeof(CkHeader)) return -22;
     CkHeader h;
     memcpy(&h, image, sizeof h);
-    if (h.magic != CK_MAGIC || h.version != 1) return -22;
-    if (size != sizeof(CkHeader) + ck_payload_bytes(h.n_accounts, h.n_rows, h.n_hist)) return -22;
+    if (h.magic != CK_MAGIC || (h.version != 1 && h.version != 2)) return -22;
+    if (h.version == 1 && h.n_foreign != 0) return -22;
+    if (h.version == 2 && !c->T.shard_world) return -22;  // a ledger shard's image needs a shard ctx
+    if (size != sizeof(CkHeader) + ck_payload_bytes(h.n_accounts, h.n_rows, h.n_hist, h.n_foreign)) return -22;
     const u8* p = (const u8*)image + sizeof(CkHeader);
     if (ck_checksum(p, size - sizeof(CkHeader)) != h.checksum) return -22;
     if (h.n_accounts > c->accounts_max || h.n_rows > c->xrow_cap || h.n_hist > c->hist_cap) return -28;
@@ -2134,6 +2180,15 @@ extern "C" int tbgpu_open(tbgpu_ctx* c, const void* image, uint64_t size) {
     // derived state: the account index, the transfer-id index and its key range,
     // the overflow guard; the account-transfers index rebuilds on the next query
     launch_rebuild_accounts(c->T, na, s);
+    const u64 nf = h.n_foreign;
+    if (nf) {  // a ledger shard: the other shards' accounts back into the directory
+        ForeignAccount* buf = nullptr;
+        HIP_CHECK(hipMalloc((void**)&buf, nf * sizeof(ForeignAccount)));
+        h2d(c, buf, imp + nr + nh * 256, nf * sizeof(ForeignAccount), s);
+        launch_insert_foreign(c->T, buf, nf, s);
+        wait_stream(s);
+        HIP_CHECK(hipFree(buf));
+    }
     for (u64 off = 0; off < nr; off += 1u << 30) {
         const u32 k = (u32)std::min<u64>(nr - off, 1u << 30);
         launch_import_transfers(c->T, c->T.xrows + off, k, off, s);  // rows in place: index + key range
@@ -2141,6 +2196,7 @@ extern "C" int tbgpu_open(tbgpu_ctx* c, const void* image, uint64_t size) {
     h2d(c, c->T.commit_ts, &h.commit_ts, sizeof(u64), s);
     wait_stream(s);
     c->n_accounts = na;
+    c->n_foreign = nf;
     c->n_rows = nr;
     c->n_hist = nh;
     c->rows_hi = nr;

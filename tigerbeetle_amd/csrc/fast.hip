@@ -174,6 +174,7 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
     if (B.row1 == 0) return TBGPU_CREATE_TRANSFER_CREDIT_ACCOUNT_NOT_FOUND;
     if (A.ledger != B.ledger) return TBGPU_CREATE_TRANSFER_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
     if (t.ledger != A.ledger) return TBGPU_CREATE_TRANSFER_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
+    if (!ledger_owned(T, t.ledger)) return FRES_SLOW;  // another shard's ledger (the general path refuses it)
     if ((A.flags | B.flags) & (AF_DNEC | AF_CNED | AF_HISTORY)) return FRES_SLOW;  // limits / history
     if (x_r1 != 0) {
         const u32 pre = T.xrows[x_r1 - 1].id == t.id ? x_r1 - 1 : xidx_probe_from(T, hx, t.id);
@@ -221,16 +222,19 @@ __device__ __forceinline__ u8 fp_classify_guarded(const Tables& T, const FastArg
     if (!(f & (TF_BDR | TF_BCR)) && t.amount == 0) return TBGPU_CREATE_TRANSFER_AMOUNT_MUST_NOT_BE_ZERO;
     if (t.ledger == 0) return TBGPU_CREATE_TRANSFER_LEDGER_MUST_NOT_BE_ZERO;
     if (t.code == 0) return TBGPU_CREATE_TRANSFER_CODE_MUST_NOT_BE_ZERO;
-    const u32 ds = acc_probe(T.aidx, T.aidx_mask, t.debit_account_id);
+    u32 dled, cled;
+    u16 dfl, cfl;
+    const u32 ds = acc_find(T, t.debit_account_id, &dled, &dfl);
     if (ds == NONE32) return TBGPU_CREATE_TRANSFER_DEBIT_ACCOUNT_NOT_FOUND;
-    const u32 cs = acc_probe(T.aidx, T.aidx_mask, t.credit_account_id);
+    const u32 cs = acc_find(T, t.credit_account_id, &cled, &cfl);
     if (cs == NONE32) return TBGPU_CREATE_TRANSFER_CREDIT_ACCOUNT_NOT_FOUND;
+    if (dled != cled) return TBGPU_CREATE_TRANSFER_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
+    if (t.ledger != dled) return TBGPU_CREATE_TRANSFER_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
+    if (!ledger_owned(T, t.ledger)) return FRES_SLOW;  // another shard's ledger (the general path refuses it)
+    if (f & (TF_BDR | TF_BCR)) return FRES_SLOW;                     // balancing
+    if ((dfl | cfl) & (AF_DNEC | AF_CNED | AF_HISTORY)) return FRES_SLOW;  // limits / history
     const Account& dr = T.acc[ds];
     const Account& cr = T.acc[cs];
-    if (dr.ledger != cr.ledger) return TBGPU_CREATE_TRANSFER_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
-    if (t.ledger != dr.ledger) return TBGPU_CREATE_TRANSFER_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
-    if (f & (TF_BDR | TF_BCR)) return FRES_SLOW;                                  // balancing
-    if ((dr.flags | cr.flags) & (AF_DNEC | AF_CNED | AF_HISTORY)) return FRES_SLOW;  // limits / history
     const u32 pre = xidx_probe(T, t.id);
     if (pre != NONE32) return fp_exists(t, T.xrows[pre]);
     // an id repeated within the call is caught by fp_dupcheck, as on the unguarded path
@@ -1043,8 +1047,8 @@ __global__ void fp_undo(Tables T, FastArgs F) {
     if (F.dry || i >= F.n) return;
     if (F.fres[i] != TBGPU_CREATE_TRANSFER_OK) return;
     const Transfer& t = F.ev[i];
-    const u32 ds = acc_probe(T.aidx, T.aidx_mask, t.debit_account_id);
-    const u32 cs = acc_probe(T.aidx, T.aidx_mask, t.credit_account_id);
+    const u32 ds = acc_row(T, t.debit_account_id);
+    const u32 cs = acc_row(T, t.credit_account_id);
     const u64 a = (u64)t.amount;
     if (t.flags & TF_PENDING) {
         atomic_sub_u128_small(&T.acc[ds].debits_pending, a);

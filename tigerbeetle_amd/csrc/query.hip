@@ -42,8 +42,10 @@ __global__ void q_entries(Tables T, u64 row0, u64 n, const u8* imported, u32 inv
     u32 kd = invalid, kc = invalid;
     if (!imported || !imported[r]) {
         const Transfer& t = T.xrows[r];
-        kd = acc_probe(T.aidx, T.aidx_mask, t.debit_account_id);
-        kc = acc_probe(T.aidx, T.aidx_mask, t.credit_account_id);
+        kd = acc_row(T, t.debit_account_id);
+        kc = acc_row(T, t.credit_account_id);
+        if (kd == ROW_FOREIGN) kd = invalid;  // (a shard stores transfers of its own ledgers only)
+        if (kc == ROW_FOREIGN) kc = invalid;
     }
     key[2 * k] = kd;
     key[2 * k + 1] = kc;
@@ -101,7 +103,8 @@ __global__ __launch_bounds__(Q_THREADS) void q_scan(Tables T, QIndex X, QArgs A)
     const tbgpu_account_filter_t f = A.filters[q];
     const u128 fid = ((u128)f.account_id.hi << 64) | f.account_id.lo;
     if (tid == 0) {
-        u32 acc = filter_valid(f) ? acc_probe(T.aidx, T.aidx_mask, fid) : NONE32;
+        u32 acc = filter_valid(f) ? acc_row(T, fid) : NONE32;
+        if (acc == ROW_FOREIGN) acc = NONE32;  // another ledger shard's account: its owner answers
         // get_account_history: the account must exist and keep history (:756-797)
         if (A.history && acc != NONE32 && !(T.acc[acc].flags & AF_HISTORY)) acc = NONE32;
         s_acc = acc;

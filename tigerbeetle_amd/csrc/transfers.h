@@ -162,3 +162,6 @@ void launch_set_balances(const Tables& T, u128 id, Bal4 b, int* status, hipStrea
 void launch_import_transfers(const Tables& T, const Transfer* rows, u32 n, u64 row_base, hipStream_t stream);
 void launch_get_posted(const Tables& T, u128 id, int* status, hipStream_t stream);
 void launch_rebuild_accounts(const Tables& T, u64 n, hipStream_t stream);
+// ledger shards: other shards' accounts into / out of the directory
+void launch_insert_foreign(const Tables& T, const ForeignAccount* f, u64 n, hipStream_t stream);
+void launch_collect_foreign(const Tables& T, ForeignAccount* out, u32* cursor, u64 cap, hipStream_t stream);

@@ -227,7 +227,12 @@ __device__ __forceinline__ u32 classify_one(const Tables& T, const TrArgs& C, u3
     } else {
         if (dled != cled) sres = TBGPU_CREATE_TRANSFER_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
         else if (t.ledger != dled) sres = TBGPU_CREATE_TRANSFER_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
-        else {
+        else if (!ledger_owned(T, t.ledger)) {
+            // a ledger shard got a transfer of another shard's ledger (the router never
+            // sends one): its rows are not here, the host aborts the call
+            sres = TBGPU_CREATE_TRANSFER_LINKED_EVENT_FAILED;
+            fl |= FL_FOREIGN;
+        } else {
             sres = SRES_DYN;
             pre_e = xidx_probe(T, t.id);
             gslot = gtab_find_or_insert(C, t.id, i, 0);

@@ -35,7 +35,8 @@ class Options(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("reserved0", ctypes.c_uint32), ("accounts_max", ctypes.c_uint64),
                 ("transfers_max", ctypes.c_uint64), ("history_max", ctypes.c_uint64),
                 ("events_per_call_max", ctypes.c_uint64), ("flags", ctypes.c_uint32),
-                ("dense_block_span", ctypes.c_uint32)]
+                ("dense_block_span", ctypes.c_uint32), ("directory_max", ctypes.c_uint64),
+                ("hashed_max", ctypes.c_uint64), ("shard_world", ctypes.c_uint32), ("shard_rank", ctypes.c_uint32)]
 
 
 class Stats(ctypes.Structure):
@@ -162,18 +163,24 @@ class Engine:
 
     def __init__(self, device: int = 0, accounts_max: int = 1 << 16, transfers_max: int = 1 << 20,
                  history_max: int = 1 << 16, events_per_call_max: int = 1 << 17, force_general: bool = False,
-                 dense_block_span: int = 0, walk_early: bool = False, pinned_input: bool = False):
+                 dense_block_span: int = 0, walk_early: bool = False, pinned_input: bool = False,
+                 directory_max: int = 0, hashed_max: int = 0, shard_world: int = 0, shard_rank: int = 0):
         """dense_block_span = S > 0: account ids of the form (b << 32) | k with 1 <= k <= S
         (e.g. ledger-major numbering) are looked up in the direct-mapped directory, one
         8-byte read; other ids use the hash index.  0: the directory covers ids
-        1..accounts_max (the reference benchmark's numbering)."""
+        1..directory_max (the reference benchmark's numbering).
+        shard_world = N >= 2: a ledger shard (include/tbgpu.h): rows only for accounts of
+        ledgers with ledger % N == shard_rank (accounts_max of them), a directory entry
+        for each of the directory_max accounts."""
         self._L = lib()
         opt = Options(device=device, accounts_max=accounts_max, transfers_max=transfers_max,
                       history_max=history_max, events_per_call_max=events_per_call_max,
                       flags=(OPT_FORCE_GENERAL if force_general else 0) | (OPT_WALK_EARLY if walk_early else 0)
                       | (OPT_PINNED_INPUT if pinned_input else 0),
-                      dense_block_span=dense_block_span)
+                      dense_block_span=dense_block_span, directory_max=directory_max, hashed_max=hashed_max,
+                      shard_world=shard_world, shard_rank=shard_rank)
         self.device = device
+        self.shard_world, self.shard_rank = shard_world, shard_rank
         h = ctypes.c_void_p()
         rc = self._L.tbgpu_init(ctypes.byref(h), ctypes.byref(opt))
         if rc != 0:

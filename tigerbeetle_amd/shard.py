@@ -28,8 +28,12 @@ Per step (`create_transfers`):
    earlier code, so no balance moves); post/void goes to the pending's shard,
    with a colliding committed id imported there (tbgpu_import_transfers) for the
    `exists` comparison.  Events that fail state-independently stay with their
-   chain.  Accounts are replicated on every rank (create_accounts runs
-   everywhere), so the account checks (:1273-1281) are exact on any shard.
+   chain.  create_accounts runs on every rank over every rank's batches, so the
+   account directory (id -> ledger, what the checks of :1273-1281 read) is
+   complete everywhere; with ledger-shard engines (tbgpu_options.shard_world)
+   each rank stores the 128-byte rows of its own ledgers' accounts only, and the
+   `exists*` comparison against another ledger's account (:1227-1237) comes from
+   the rank that stores it (create_accounts below merges it).
 4. Exchange.  Events travel to their owners with one all-to-all (RCCL over
    xGMI on GPUs, gloo in the CPU tests); each owner commits its sub-batches in
    global order with tbgpu_create_transfers_routed (per-event timestamps).
@@ -66,6 +70,8 @@ CTL_CHAIN_END = 1  # include/tbgpu.h TBGPU_CTL_CHAIN_END
 CTL_SKIP = 2       # include/tbgpu.h TBGPU_CTL_SKIP
 CTL_DOOM = 4       # include/tbgpu.h TBGPU_CTL_DOOM
 LINKED_EVENT_FAILED = 1
+SHARD_EXISTS_ELSEWHERE = 255  # include/tbgpu.h TBGPU_SHARD_ACCOUNT_EXISTS_ELSEWHERE
+ACCOUNT_EXISTS_CODES = range(15, 22)  # CreateAccountResult exists_with_different_flags .. exists
 LINKED = int(TransferFlags.linked)
 POST_VOID = int(TransferFlags.post_pending_transfer | TransferFlags.void_pending_transfer)
 ANY = -1           # route: state-independent failure, any shard computes it
@@ -223,12 +229,38 @@ class ShardedStateMachine:
         out, rc = self.backend.create_accounts_batches(np.array(ts, np.uint64), np.array(counts, np.uint32),
                                                        events)
         self._sync_commit_timestamp()
-        mine, off = [], 0
-        for (r, j), c, k in zip(owner, counts, rc):
-            if r == self.rank:
-                mine.append(out[off:off + int(k)].copy())
+        per = []  # per global batch: its replies
+        off = 0
+        for c, k in zip(counts, rc):
+            per.append(out[off:off + int(k)].copy())
             off += c
-        return mine
+        if getattr(self.backend, "shard_world", 0) >= 2:
+            self._merge_elsewhere(per)
+        return [per[g] for g, (r, _) in enumerate(owner) if r == self.rank]
+
+    def _merge_elsewhere(self, per: list[np.ndarray]) -> None:
+        """Ledger-shard engines: an event whose id names an account created before the
+        call on another shard's ledger gets TBGPU_SHARD_ACCOUNT_EXISTS_ELSEWHERE on every
+        rank but that account's owner, whose engine compared the row
+        (create_account_exists, src/state_machine.zig:1227-1237).  Every rank fails the
+        same events (any `exists*` is a failure, so chains break alike); the owner's
+        code replaces the placeholder (one all-gather of the `exists*` replies)."""
+        mine = {}
+        for g, r in enumerate(per):
+            for ix, code in zip(r["index"].tolist(), r["result"].tolist()):
+                if code in ACCOUNT_EXISTS_CODES:
+                    mine[(g, ix)] = code
+        exact = {}
+        for d in self.comm.all_gather_object(mine):
+            exact.update(d)
+        for g, r in enumerate(per):
+            hole = r["result"] == SHARD_EXISTS_ELSEWHERE
+            if hole.any():
+                for k in np.nonzero(hole)[0].tolist():
+                    key = (g, int(r["index"][k]))
+                    if key not in exact:
+                        raise AssertionError(f"create_accounts: no shard compared the existing account of {key}")
+                    r["result"][k] = exact[key]
 
     # ----------------------------------------------------------- transfers --
     def create_transfers(self, batches: list[np.ndarray]) -> list[np.ndarray]:

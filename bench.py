@@ -322,9 +322,14 @@ def routed_bench(args, rank, world, local_rank, torch, dist, backend="nccl"):
     w.transfers["id_hi"] = 0
     log(f"[rank {rank}] generated {len(w.transfers)} transfers / {acc_n} accounts in {time.time() - t_gen:.1f}s")
     dev = torch.device("cuda", local_rank)
-    eng = Engine(device=local_rank, accounts_max=acc_n, transfers_max=int((K + W + P) * per_step * 1.25) + 4096,
+    # N > 1: ledger shards (tbgpu_options.shard_world): rows only for this rank's
+    # ledgers (ledger % N == rank), a directory entry for every account
+    apl = acc_n // 1000
+    owned = (len(range(rank, 1001, world)) - (1 if rank == 0 else 0)) * apl if world > 1 else acc_n
+    eng = Engine(device=local_rank, accounts_max=owned, directory_max=acc_n, hashed_max=1024 if world > 1 else 0,
+                 transfers_max=int((K + W + P) * per_step * 1.25) + 4096,
                  history_max=1024, events_per_call_max=int(per_step * 1.25) + BATCH_MAX,
-                 dense_block_span=acc_n // 1000)
+                 dense_block_span=apl, shard_world=world if world > 1 else 0, shard_rank=rank if world > 1 else 0)
     ats, _ = w.timestamps()
     acc_line = create_accounts_device(eng, torch, torch.device("cuda", local_rank), ats, w.account_counts,
                                       w.accounts, rank)
@@ -403,7 +408,7 @@ def routed_bench(args, rank, world, local_rank, torch, dist, backend="nccl"):
             "vs_baseline": None,
             "dtype": "u128",
             "data": "synthetic",
-            "config": {"workload": f"config4 routed: {acc_n} accounts (replicated), 1000 ledgers sharded by "
+            "config": {"workload": f"config4 routed: {acc_n} accounts ({'rows on their ledger owner, a directory entry on every rank' if world > 1 else 'one rank'}), 1000 ledgers sharded by "
                                    f"ledger % {world}, uniform pairs within a ledger, 1% cross-ledger linked "
                                    f"pairs; per rank {B} x 8190-transfer client batches per step, scattered to "
                                    f"their ledger owners by RCCL all-to-all and replied to by all-to-all",
@@ -686,8 +691,12 @@ def main():
         counts = c5.transfer_batches()[:n_batches]
         n_batches = len(counts)
         ats, tts = c5.timestamps()
-        eng = Engine(device=local_rank, accounts_max=acc_n, transfers_max=int(counts.sum()) + 1024, history_max=1024,
-                     events_per_call_max=B * BATCH_MAX, force_general=args.force_general, pinned_input=True)
+        # a ledger shard (tbgpu_options.shard_world = 8): the directory knows all 100M
+        # accounts, the 128-byte rows are this shard's 12.5M (ledger % 8 == rank)
+        eng = Engine(device=local_rank, accounts_max=c5.owned_accounts(), directory_max=acc_n, hashed_max=1024,
+                     transfers_max=int(counts.sum()) + 1024, history_max=1024, events_per_call_max=B * BATCH_MAX,
+                     force_general=args.force_general, pinned_input=True, shard_world=c5.shards,
+                     shard_rank=c5.shard)
         ab = c5.account_batches()
         buf = torch.empty(1221 * BATCH_MAX * 128, dtype=torch.uint8, device=dev)
         res = torch.empty(1221 * BATCH_MAX * 8, dtype=torch.uint8, device=dev)
@@ -711,7 +720,7 @@ def main():
         del buf, res
         ev_dev = torch.empty(int(counts.sum()) * 128, dtype=torch.uint8, device=dev)
         generate_transfers(local_rank, c5.first_transfer_id, int(counts.sum()), c5.seed, c5.ledger0, c5.ledgers,
-                           c5.accounts_per_ledger, ev_dev.data_ptr())
+                           c5.accounts_per_ledger, ev_dev.data_ptr(), ledger_stride=c5.ledger_stride)
         log(f"[rank {rank}] config 5: {acc_n} accounts created, {int(counts.sum())} transfers generated in HBM "
             f"in {time.time() - t_gen:.1f}s")
     else:

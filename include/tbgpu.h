@@ -501,15 +501,16 @@ uint64_t tbgpu_get_account_history_device(tbgpu_ctx* ctx, uint32_t count, const 
 /* The `tigerbeetle benchmark` load at BASELINE config 5's scale, written straight
  * into device memory by a counter-based generator (record i depends only on
  * (seed, first_id + i)).  Accounts: ids first_id.., ledger (id - 1) /
- * accounts_per_ledger + 1, code 1.  Transfers: ids first_id.., a ledger in
- * [ledger0, ledger0 + ledgers), uniform distinct debit/credit accounts of that
+ * accounts_per_ledger + 1, code 1.  Transfers: ids first_id.., a ledger among
+ * ledger0 + ledger_stride * [0, ledgers) (stride N: the ledgers of one shard of N,
+ * ledger % N), uniform distinct debit/credit accounts of that
  * ledger, amount floor(Exp(1) * 10000) + 1, random user data and code, flags 0.
  * Synchronous; 0 or a negative errno. */
 int tbgpu_bench_generate_accounts(int device, uint64_t first_id, uint64_t count,
                                   uint32_t accounts_per_ledger, void* out_device);
 int tbgpu_bench_generate_transfers(int device, uint64_t first_id, uint64_t count, uint64_t seed,
-                                   uint32_t ledger0, uint32_t ledgers, uint32_t accounts_per_ledger,
-                                   void* out_device);
+                                   uint32_t ledger0, uint32_t ledgers, uint32_t ledger_stride,
+                                   uint32_t accounts_per_ledger, void* out_device);
 
 /* Test harness `setup` action (src/state_machine.zig:1892-1908): overwrite an
  * existing account's four balances.  Returns 0, or -1 if the account is missing. */

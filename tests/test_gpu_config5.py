@@ -1,12 +1,13 @@
 """BASELINE config 5 at its per-GPU size on one MI355X.
 
-100M accounts (the replicated account directory of the ledger-sharded design:
-every shard holds them all) and one shard's 125M transfers (1B over 8 ledger
-shards), streamed as back-to-back 8190-transfer batches, the load generated in HBM
-(workload.config5, csrc/loadgen.hip).  Checked over the whole state:
+100M accounts and one shard's 125M transfers (1B over 8 ledger shards), streamed as
+back-to-back 8190-transfer batches, the load generated in HBM (workload.config5,
+csrc/loadgen.hip), on a ledger-shard ctx (tbgpu_options.shard_world = 8): the
+directory knows all 100M accounts, the 128-byte rows are the shard's own 12.5M.
+Checked over the whole state:
 
-- capacity: 100M accounts sit in the direct-mapped directory (row + 1 in 29 bits)
-  and 125M stored rows in the transfer-id index (u32 row + 1);
+- capacity: 100M accounts in the direct-mapped directory (row + 1 in 29 bits, rows
+  only for the shard's ledgers) and 125M stored rows in the transfer-id index;
 - every transfer is accepted (all accounts exist, ids are new) and stored;
 - conservation: total debits_posted == total credits_posted == the sum of the
   amounts, and accounts outside the shard's ledgers never move;
@@ -41,8 +42,10 @@ def test_config5_per_gpu_shard():
     assert c5.accounts < (1 << 29) - 1, "the directory's row field is 29 bits"
     assert c5.transfers < (1 << 31) - 1, "the transfer-id index holds u32 row + 1"
     per_call = 1000  # batches per streamed call
-    eng = E.Engine(accounts_max=c5.accounts, transfers_max=c5.transfers + 2 * BATCH_MAX, history_max=1024,
-                   events_per_call_max=per_call * BATCH_MAX)
+    owned = c5.owned_accounts()
+    eng = E.Engine(accounts_max=owned, directory_max=c5.accounts, hashed_max=1024,
+                   transfers_max=c5.transfers + 2 * BATCH_MAX, history_max=1024,
+                   events_per_call_max=per_call * BATCH_MAX, shard_world=c5.shards, shard_rank=c5.shard)
     try:
         ats, tts = c5.timestamps()
         # accounts, 10M per generated slice
@@ -58,7 +61,7 @@ def test_config5_per_gpu_shard():
             total, _ = eng.create_accounts_batches_device(ats[b0:b0 + len(cnt)], cnt, buf.data_ptr(), res.data_ptr())
             assert total == 0, "account creation failed"
             first += n
-        assert eng.account_count() == c5.accounts
+        assert eng.account_count() == owned  # rows: this shard's ledgers only
         del buf, res
 
         tb = c5.transfer_batches()
@@ -71,7 +74,7 @@ def test_config5_per_gpu_shard():
         lead = 4
         n_lead = int(offs[lead])
         E.generate_transfers(0, c5.first_transfer_id, n_lead, c5.seed, c5.ledger0, c5.ledgers,
-                             c5.accounts_per_ledger, ev.data_ptr())
+                             c5.accounts_per_ledger, ev.data_ptr(), ledger_stride=c5.ledger_stride)
         lead_ev = ev[:n_lead * 128].cpu().numpy().view(TRANSFER_DTYPE).copy()
         total, rc = eng.create_transfers_batches_device(tts[:lead], tb[:lead], ev.data_ptr(), res.data_ptr())
         assert total == 0
@@ -101,7 +104,7 @@ def test_config5_per_gpu_shard():
             k = min(per_call, len(tb) - b)
             n = int(offs[b + k] - offs[b])
             E.generate_transfers(0, c5.first_transfer_id + int(offs[b]), n, c5.seed, c5.ledger0, c5.ledgers,
-                                 c5.accounts_per_ledger, ev.data_ptr())
+                                 c5.accounts_per_ledger, ev.data_ptr(), ledger_stride=c5.ledger_stride)
             amount_sum += int(ev[:n * 128].view(torch.int64).view(n, 16)[:, 6].sum().item())
             total, _ = eng.create_transfers_batches_device(tts[b:b + k], tb[b:b + k], ev.data_ptr(), res.data_ptr())
             assert total == 0, f"calls at batch {b}: {total} failures"
@@ -110,19 +113,21 @@ def test_config5_per_gpu_shard():
 
         # conservation over the whole state
         a = eng.export_accounts()
-        assert len(a) == c5.accounts
+        assert len(a) == owned
+        assert (a["ledger"] % c5.shards == c5.shard).all()
         dpo = _sum128(a["debits_posted_lo"], a["debits_posted_hi"])
         cpo = _sum128(a["credits_posted_lo"], a["credits_posted_hi"])
         assert dpo == cpo == amount_sum
         assert not a["debits_pending_lo"].any() and not a["credits_pending_lo"].any()
-        led = a["ledger"]
-        outside = (led < c5.ledger0) | (led >= c5.ledger0 + c5.ledgers)
-        assert not a["debits_posted_lo"][outside].any() and not a["credits_posted_lo"][outside].any()
         del a
+        # another shard's account: in the directory (a transfer naming it with this
+        # shard's ledger fails on the ledger, not as not-found), but no row here
+        other = c5.accounts_per_ledger + 1  # ledger 2 (shard 2 of 8)
+        assert len(eng.lookup_accounts([other])) == 0
 
         # idempotence: the first batch again (a new prepare timestamp)
         E.generate_transfers(0, c5.first_transfer_id, BATCH_MAX, c5.seed, c5.ledger0, c5.ledgers,
-                             c5.accounts_per_ledger, ev.data_ptr())
+                             c5.accounts_per_ledger, ev.data_ptr(), ledger_stride=c5.ledger_stride)
         before = eng.lookup_accounts([int(x) for x in ids[:1000]])
         total, rc = eng.create_transfers_batches_device(np.array([tts[-1] + BATCH_MAX + 1], np.uint64),
                                                         np.array([BATCH_MAX], np.uint32), ev.data_ptr(),

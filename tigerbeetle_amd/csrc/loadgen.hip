@@ -34,20 +34,20 @@ __global__ void lg_accounts(Account* out, u64 first_id, u64 count, u32 accounts_
     out[i] = a;
 }
 
-// Transfer `first_id + i`: a ledger among [ledger0, ledger0 + ledgers), then a
+// Transfer `first_id + i`: a ledger among ledger0 + stride * [0, ledgers), then a
 // uniform debit account and a different uniform credit account of that ledger
 // (ids (ledger - 1) * accounts_per_ledger + 1 ...), amount floor(Exp(1) * 10000) + 1
 // (benchmark_load.zig:304-313; src/testing/fuzz.zig:16-24), code rand_u16 +| 1,
 // random user data, flags 0.
 __global__ void lg_transfers(Transfer* out, u64 first_id, u64 count, u64 seed, u32 ledger0, u32 ledgers,
-                             u32 accounts_per_ledger) {
+                             u32 ledger_stride, u32 accounts_per_ledger) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
     const u64 id = first_id + i;
     const u64 base = lg_mix(seed * 0x9E3779B97F4A7C15ull + id);
     const u64 r1 = lg_mix(base ^ 0x1), r2 = lg_mix(base ^ 0x2), r3 = lg_mix(base ^ 0x3), r4 = lg_mix(base ^ 0x4);
     const u64 r5 = lg_mix(base ^ 0x5), r6 = lg_mix(base ^ 0x6);
-    const u32 ledger = ledger0 + (u32)(base % ledgers);
+    const u32 ledger = ledger0 + ledger_stride * (u32)(base % ledgers);
     const u64 apl = accounts_per_ledger;
     const u64 dr = r1 % apl;
     u64 cr = r2 % (apl - 1);
@@ -82,10 +82,12 @@ extern "C" int tbgpu_bench_generate_accounts(int device, uint64_t first_id, uint
 }
 
 extern "C" int tbgpu_bench_generate_transfers(int device, uint64_t first_id, uint64_t count, uint64_t seed,
-                                              uint32_t ledger0, uint32_t ledgers, uint32_t accounts_per_ledger,
-                                              void* out_device) {
-    if (hipSetDevice(device) != hipSuccess || ledgers == 0 || ledger0 == 0 || accounts_per_ledger < 2) return -22;
+                                              uint32_t ledger0, uint32_t ledgers, uint32_t ledger_stride,
+                                              uint32_t accounts_per_ledger, void* out_device) {
+    if (hipSetDevice(device) != hipSuccess || ledgers == 0 || ledger0 == 0 || ledger_stride == 0 ||
+        accounts_per_ledger < 2)
+        return -22;
     if (count) lg_transfers<<<(u32)((count + 255) / 256), 256>>>((Transfer*)out_device, first_id, count, seed,
-                                                                ledger0, ledgers, accounts_per_ledger);
+                                                                ledger0, ledgers, ledger_stride, accounts_per_ledger);
     return hipDeviceSynchronize() == hipSuccess ? 0 : -5;
 }

@@ -145,7 +145,7 @@ def lib():
     L.tbgpu_bench_generate_accounts.restype = ctypes.c_int
     L.tbgpu_bench_generate_accounts.argtypes = [ctypes.c_int, u64, u64, u32, vp]
     L.tbgpu_bench_generate_transfers.restype = ctypes.c_int
-    L.tbgpu_bench_generate_transfers.argtypes = [ctypes.c_int, u64, u64, u64, u32, u32, u32, vp]
+    L.tbgpu_bench_generate_transfers.argtypes = [ctypes.c_int, u64, u64, u64, u32, u32, u32, u32, vp]
     L.tbgpu_last_error.restype = ctypes.c_int
     L.tbgpu_last_error.argtypes = [vp, ctypes.c_char_p, u32]
     _lib = L
@@ -509,9 +509,10 @@ def generate_accounts(device: int, first_id: int, count: int, accounts_per_ledge
 
 
 def generate_transfers(device: int, first_id: int, count: int, seed: int, ledger0: int, ledgers: int,
-                       accounts_per_ledger: int, out_ptr: int) -> None:
-    """The benchmark's transfers in device memory (tbgpu_bench_generate_transfers)."""
-    rc = lib().tbgpu_bench_generate_transfers(device, first_id, count, seed, ledger0, ledgers, accounts_per_ledger,
-                                              ctypes.c_void_p(out_ptr))
+                       accounts_per_ledger: int, out_ptr: int, ledger_stride: int = 1) -> None:
+    """The benchmark's transfers in device memory (tbgpu_bench_generate_transfers): ledgers
+    ledger0 + ledger_stride * [0, ledgers)."""
+    rc = lib().tbgpu_bench_generate_transfers(device, first_id, count, seed, ledger0, ledgers, ledger_stride,
+                                              accounts_per_ledger, ctypes.c_void_p(out_ptr))
     if rc != 0:
         raise RuntimeError(f"tbgpu_bench_generate_transfers failed ({rc})")

@@ -526,10 +526,11 @@ class DeviceLoad:
     counter-based generator (engine.generate_accounts / generate_transfers,
     csrc/loadgen.hip): record i depends only on (seed, first id + i).
 
-    100M accounts over 1000 ledgers (ids 1..100M, ledger (id - 1) / 100k + 1,
-    every shard holds them all: the replicated account directory of the sharded
-    design), 1B transfers split evenly over `shards` ledger shards: shard s draws
-    its transfers from ledgers [ledger0, ledger0 + ledgers), uniform distinct
+    100M accounts over 1000 ledgers (ids 1..100M, ledger (id - 1) / 100k + 1;
+    every shard's directory knows them all, its rows are its own ledgers'), 1B
+    transfers split evenly over `shards` ledger shards: shard s owns the ledgers
+    with ledger % shards == s (the router's owner_of_ledger) and draws its
+    transfers from them, ledger0 + ledger_stride * [0, ledgers), uniform distinct
     debit / credit accounts within a ledger, amount floor(Exp(1) * 10000) + 1 --
     the `tigerbeetle benchmark` distribution (src/tigerbeetle/benchmark_load.zig:
     266-330) within each ledger."""
@@ -540,6 +541,15 @@ class DeviceLoad:
     transfers: int
     seed: int
     first_transfer_id: int = 1
+    ledger_stride: int = 1
+    shard: int = 0
+    shards: int = 1
+
+    def owned_ledgers(self) -> np.ndarray:
+        return self.ledger0 + self.ledger_stride * np.arange(self.ledgers, dtype=np.int64)
+
+    def owned_accounts(self) -> int:
+        return self.ledgers * self.accounts_per_ledger
 
     def account_batches(self, batch: int = BATCH_MAX) -> np.ndarray:
         return _batches(self.accounts, batch)
@@ -559,9 +569,10 @@ class DeviceLoad:
 def config5(shard: int = 0, shards: int = 8, accounts: int = 100_000_000, ledgers: int = 1000,
             transfers_total: int = 1_000_000_000, seed: int = 42) -> DeviceLoad:
     per = ledgers // shards
-    return DeviceLoad(accounts=accounts, accounts_per_ledger=accounts // ledgers, ledger0=shard * per + 1,
+    return DeviceLoad(accounts=accounts, accounts_per_ledger=accounts // ledgers, ledger0=shard if shard else shards,
                       ledgers=per, transfers=transfers_total // shards, seed=seed + shard,
-                      first_transfer_id=shard * (transfers_total // shards) + 1)
+                      first_transfer_id=shard * (transfers_total // shards) + 1, ledger_stride=shards,
+                      shard=shard, shards=shards)
 
 
 def make(config: int, **kw) -> Workload:

@@ -736,8 +736,13 @@ class ShardedStateMachine:
                     nb_ = breaks(out, at)
                     if nb_ == brk:
                         out2, at2, cts = commit(ctl, False)
-                        if out2.tobytes() != out.tobytes():
-                            raise RuntimeError("sharded commit: dry run and commit disagree (engine invariant)")
+                        # the commit is exact as long as it breaks every spanning chain where
+                        # its control said (decided collectively: every rank alike)
+                        if self.comm.allreduce_max(int(out2.tobytes() != out.tobytes())):
+                            self.stats["dry_commit_mismatch"] = self.stats.get("dry_commit_mismatch", 0) + 1
+                            if breaks(out2, at2) != brk:
+                                raise AssertionError("sharded commit: a committed chain broke elsewhere than its "
+                                                     "dry run (engine invariant)")
                         st.out, st.at, st.cts = out2, at2, cts
                         clock("commit_ms")
                         return st
@@ -1052,8 +1057,22 @@ class ShardedStateMachine:
             if nb == brk:
                 sub = self._build_sub(mine, T, glob, span, last_member, brk)
                 res2 = self._commit(sub, False)
-                if sorted(res2) != sorted(res):
-                    raise RuntimeError("sharded commit: dry run and commit disagree (engine invariant)")
+                # exact as long as every spanning chain broke where its control said
+                if self.comm.allreduce_max(int(sorted(res2) != sorted(res))):
+                    self.stats["dry_commit_mismatch"] = self.stats.get("dry_commit_mismatch", 0) + 1
+                    fails2 = {}
+                    for (g, i, c), code in res2:
+                        if c in span and code not in (0, LINKED_EVENT_FAILED):
+                            if c not in fails2 or (g, i) < fails2[c]:
+                                fails2[c] = (g, i)
+                    nb2 = {}
+                    for d in self.comm.all_gather_object(fails2):
+                        for c, p in d.items():
+                            if c not in nb2 or p < nb2[c]:
+                                nb2[c] = p
+                    if nb2 != brk:
+                        raise AssertionError("sharded commit: a committed chain broke elsewhere than its dry run "
+                                             "(engine invariant)")
                 res = res2
                 break
             if rounds >= self.max_rounds:
@@ -1069,6 +1088,14 @@ class ShardedStateMachine:
                 head = min((x[0], x[1]) for x in mine) if mine else None
                 head = min([h for h in self.comm.all_gather_object(head) if h is not None])
                 cut = chains[0] if chains[0] > head else (chains[1] if len(chains) > 1 else None)
+                if cut is None:
+                    # the lone spanning chain heads the round: commit it alone (its members'
+                    # outcomes then depend on the committed state only), the rest after it
+                    tail = max((x[0], x[1]) for x in mine) if mine else None
+                    tail = max([t for t in self.comm.all_gather_object(tail) if t is not None], default=None)
+                    lm = last_member[chains[0]]
+                    if tail is not None and tail > lm:
+                        cut = (lm[0], lm[1] + 1)
                 if cut is not None:
                     mine = [x for x in mine if (x[0], x[1]) < cut]
                     span = {c: o for c, o in span.items() if c < cut}

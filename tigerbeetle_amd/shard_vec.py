@@ -319,7 +319,12 @@ def round_vec(sm, glob, T, my_events, replies, start):
             res2 = _commit_vec(sm, T, glob, mE[mask], mP[mask], mG[mask], mI[mask], mC[mask], in_span[mask],
                                lastloc[mask], mlast[mask], brk, dry=False)
             if not np.array_equal(res2, res):
-                raise RuntimeError("sharded commit: dry run and commit disagree (engine invariant)")
+                # the commit is exact as long as it breaks every spanning chain where its
+                # control said (collective: every rank decides alike)
+                sm.stats["dry_commit_mismatch"] = sm.stats.get("dry_commit_mismatch", 0) + 1
+                if _breaks(sm, mP[mask], mC[mask], in_span[mask], res2) != brk:
+                    raise AssertionError("sharded commit: a committed chain broke elsewhere than its dry run "
+                                         "(engine invariant: the same events and state gave other results)")
             res = res2
             break
         if rounds >= sm.max_rounds:
@@ -327,6 +332,11 @@ def round_vec(sm, glob, T, my_events, replies, start):
             head = min_over_ranks(comm, head)
             ks_ = span_keys
             cut = int(ks_[0]) if ks_[0] > head else (int(ks_[1]) if len(ks_) > 1 else None)
+            tail = -min_over_ranks(comm, -(int(mP[mask].max()) if mask.any() else -1))  # collective
+            if cut is None and tail > int(span_last[0]):
+                # the lone spanning chain heads the round: commit it alone (its members'
+                # outcomes then depend on the committed state only), the rest after it
+                cut = int(span_last[0]) + 1
             if cut is not None:
                 mask &= mP < cut
                 keep = span_keys < cut

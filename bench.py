@@ -129,7 +129,7 @@ def query_phase(eng, w, acc_n, torch, dev, count=100, batch=1024):
     lat = np.array(lat) * 1e6
     filters = np.concatenate([account_filter(int(ids[int(rng.integers(0, acc_n))]), limit=QUERY_MAX)
                               for _ in range(batch)]).astype(FILTER_DTYPE)
-    fd = torch.from_numpy(filters.view(np.uint8).copy()).to(dev)
+    fd = eng.to_device(filters, dev)
     out = torch.empty(batch * QUERY_MAX * 128, dtype=torch.uint8, device=dev)
     eng.query_device(fd.data_ptr(), batch, QUERY_MAX, out.data_ptr())  # warm
     torch.cuda.synchronize()
@@ -239,7 +239,7 @@ def create_accounts_device(eng, torch, dev, ats, account_counts, accounts, rank=
     `create_accounts` object of the bench line (accounts/s and the roofline at §8d's
     272 B per account, the whole call as the unit: no kernel dominates it)."""
     n = int(np.sum(account_counts))
-    evd = torch.from_numpy(np.ascontiguousarray(accounts).view(np.uint8)).to(dev)
+    evd = eng.to_device(np.ascontiguousarray(accounts), dev)  # written by the engine's copy kernel
     res = torch.empty(max(n, 1) * 8, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     eng.set_profiling(True)
@@ -336,7 +336,7 @@ def routed_bench(args, rank, world, local_rank, torch, dist, backend="nccl"):
     cdev = dev if backend == "nccl" else torch.device("cpu")  # where the router's tensors live
     ssm = ShardedStateMachine(eng, Comm(rank, world, device=cdev))
     ssm.adopt_accounts(w.accounts, int(ats[-1]))
-    ev_dev = torch.from_numpy(w.transfers.view(np.uint8)).to(cdev)
+    ev_dev = eng.to_device(w.transfers, cdev) if cdev.type == "cuda" else torch.from_numpy(w.transfers.view(np.uint8))
     counts = w.transfer_counts
     keep_host = rank == 0 and world == 1 and not args.no_cpu  # the CPU baseline leg reads the stream
     if not keep_host:
@@ -593,8 +593,11 @@ def main():
     if env_world is None and args.gpus > 1:
         spawn_ranks(args.gpus)  # does not return
     subs = None
+    # (not under a profiler: its preloaded library has initialised the GPU in this
+    # process already, and the sub-measurements are children of it)
+    profiled = "rocprof" in os.environ.get("LD_PRELOAD", "") or any(k.startswith("ROCPROF") for k in os.environ)
     if (env_world is None and args.gpus == 1 and args.config is None and not args.routed and not args.no_subconfigs
-            and not os.environ.get("TB_BENCH_SUB")):
+            and not os.environ.get("TB_BENCH_SUB") and not profiled):
         subs = run_subconfigs(args)  # before this process touches the GPU
     if env_world is not None and int(env_world) != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}: launch one rank per GPU", file=sys.stderr)
@@ -732,7 +735,7 @@ def main():
                      dense_block_span=acc_n // 1000 if args.config == 4 else 0)
         ats, tts = w.timestamps()
         acc_line = create_accounts_device(eng, torch, dev, ats, w.account_counts, w.accounts, rank)
-        ev_dev = torch.from_numpy(w.transfers.view(np.uint8)).to(dev)
+        ev_dev = eng.to_device(w.transfers, dev)  # HBM-resident events, written by the engine's copy kernel
         counts = w.transfer_counts
     res_dev = torch.empty(B * BATCH_MAX * 8, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()

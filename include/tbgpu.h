@@ -518,6 +518,13 @@ int tbgpu_test_set_balances(tbgpu_ctx* ctx, tbgpu_uint128_t id,
                             tbgpu_uint128_t debits_pending, tbgpu_uint128_t debits_posted,
                             tbgpu_uint128_t credits_pending, tbgpu_uint128_t credits_posted);
 
+/* Host memory into device memory by the engine's own copy kernel (the ctx's
+ * page-locked staging ring, read by a kernel on the ctx's stream), for device
+ * buffers the engine's kernels will read (the *_device entry points' inputs): such
+ * buffers are then written by a kernel, never by a copy engine.  Synchronous;
+ * returns 0. */
+int tbgpu_copy_to_device(tbgpu_ctx* ctx, void* dst_device, const void* src_host, uint64_t bytes);
+
 /* State export for parity checks (not on the reference's hot path). */
 uint64_t tbgpu_account_count(tbgpu_ctx* ctx);
 uint64_t tbgpu_transfer_count(tbgpu_ctx* ctx);

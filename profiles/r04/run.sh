@@ -17,12 +17,18 @@ run() {  # name, seconds, command...
     echo "== $name rc=$rc"
     return $rc
 }
+ok1() {  # a suite whose tests failed (pytest rc 1) lets the next step run; anything else ends the script
+    local rc=$?
+    [ $rc -eq 1 ] || exit 1
+}
 for step in "$@"; do
     case $step in
-    suite) run suite 600 $PT tests -m gpu || exit 1 ;;
+    suite) run suite 600 $PT tests -m gpu || ok1 ;;
     suite_x) run suite_x 600 $PT -x tests -m gpu || exit 1 ;;
     poison_queries) run poison_queries 300 env TBGPU_POISON_ALLOC=1 TBGPU_CHECK_INDEX=1 $PT tests/test_gpu_queries.py || exit 1 ;;
-    poison_suite) run poison_suite 700 env TBGPU_POISON_ALLOC=1 TBGPU_CHECK_INDEX=1 $PT tests -m gpu || exit 1 ;;
+    poison_suite) run poison_suite 700 env TBGPU_POISON_ALLOC=1 TBGPU_CHECK_INDEX=1 $PT tests -m gpu || ok1 ;;
+    sdma_suite) run sdma_suite 600 env TBGPU_SDMA_H2D=1 $PT tests -m gpu || ok1 ;;
+    sdma_off_suite) run sdma_off_suite 600 env TBGPU_SDMA_H2D=1 HSA_ENABLE_SDMA=0 $PT tests -m gpu || ok1 ;;
     smoke) run smoke 180 python -u __graft_entry__.py smoke || exit 1 ;;
     bench) run bench 400 python bench.py || exit 1 ;;
     bench_cfg*) run "bench_cfg${step#bench_cfg}" 400 python bench.py --config "${step#bench_cfg}" || exit 1 ;;

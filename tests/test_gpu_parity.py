@@ -606,3 +606,54 @@ def test_pinned_host_events_read_in_place():
         assert gpu.lookup_transfers(ids).tobytes() == orc.lookup_transfers(ids).tobytes()
     finally:
         gpu.close()
+
+
+@pytest.mark.parametrize("dense", [True, False], ids=["directory", "hashed"])
+def test_create_accounts_clean_and_dirty_calls(dense):
+    """create_accounts' two-pass clean call (accounts.hip ac_fast_*: rising ids, every
+    field valid, no chain, no existing id) and its hand-over to the general path: a
+    call with one existing id, one invalid field or falling ids in the middle commits
+    nothing through the clean pass (its optimistic rows lie past the committed ones)
+    and answers exactly like the oracle; clean calls before and after stay exact."""
+    rng = np.random.default_rng(11)
+    hi = 0 if dense else 64  # ids 1..N sit in the direct-mapped directory; (64 << 64) | k are hashed
+    calls = []
+    nxt = 0
+
+    def fresh(n):
+        nonlocal nxt
+        a = workload.make_accounts(np.arange(nxt + 1, nxt + 1 + n, dtype=np.uint64),
+                                   ledger=rng.integers(1, 4, n).astype(np.uint32))
+        a["id_hi"] = hi
+        a["user_data_64"] = rng.integers(0, 1 << 40, n, dtype=np.uint64)
+        nxt += n
+        return a
+
+    calls.append(fresh(3000))                     # clean
+    c = fresh(2000)
+    c[700] = calls[0][5]                          # an existing id in the middle
+    calls.append(c)
+    c = fresh(1500)
+    c[20]["code"] = 0                             # an invalid field
+    calls.append(c)
+    c = fresh(1200)
+    c[[100, 101]] = c[[101, 100]]                 # ids falling once (no repeat)
+    calls.append(c)
+    c = fresh(1000)
+    c[999] = c[3]                                 # a repeat within the call
+    calls.append(c)
+    calls.append(fresh(2500))                     # clean again
+    orc, gpu = oracle.Oracle(20000, 1024), _engine(accounts_max=20000)
+    try:
+        ts = 0
+        for c in calls:
+            ts += 1 + len(c)
+            want = orc.create_accounts(ts, c)
+            got = gpu.create_accounts(ts, c)
+            assert got.tobytes() == want.tobytes(), (got[:5], want[:5])
+        assert_state_equal(gpu, orc)
+        ids = np.concatenate([c["id_lo"] for c in calls])
+        q = [int(x) | (hi << 64) for x in ids[::97]]
+        assert gpu.lookup_accounts(q).tobytes() == orc.lookup_accounts(q).tobytes()
+    finally:
+        gpu.close()

@@ -94,7 +94,7 @@ def test_queries_device_batch_matches_single():
         fl = random_filters(np.random.default_rng(9), w.accounts["id_lo"], rows, 200)
         filters = np.concatenate(fl).astype(FILTER_DTYPE)
         stride = 256
-        fd = torch.from_numpy(filters.view(np.uint8).copy()).cuda()
+        fd = gpu.to_device(filters)
         out = torch.empty(len(fl) * stride * 128, dtype=torch.uint8, device="cuda")
         torch.cuda.synchronize()
         total, rc = gpu.query_device(fd.data_ptr(), len(fl), stride, out.data_ptr())

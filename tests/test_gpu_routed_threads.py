@@ -45,7 +45,8 @@ def _run(w, world, pipelined=False, expect_wire=True, shard_rows=False):
             for s in range(w.steps):
                 batches = w.step_batches(s, rank)
                 flat = np.concatenate(batches) if batches else np.zeros(0, dtype=TRANSFER_DTYPE)
-                steps.append((torch.from_numpy(flat.view(np.uint8).copy()).to(dev), [len(b) for b in batches]))
+                # uploaded by the engine's copy kernel (tbgpu_copy_to_device), as bench.py does
+                steps.append((eng.to_device(flat, dev), [len(b) for b in batches]))
             if pipelined:
                 for got in sm.create_transfers_device_stream(steps):
                     replies.append([r.tobytes() for r in got])

@@ -280,6 +280,7 @@ struct tbgpu_ctx {
     // halves each, a half reusable once the copy recorded behind it has run
     struct UpRing {
         u8* h[2] = {nullptr, nullptr};
+        const u8* d[2] = {nullptr, nullptr};  // their device addresses (k_copy_in reads them)
         hipEvent_t ev[2] = {nullptr, nullptr};
         int next = 0;
     } up[2];
@@ -626,14 +627,14 @@ static void refresh_bases(tbgpu_ctx* c) {
     c->rows_hi = c->n_rows;
 }
 
+// A device word written by a kernel (the value travels as its argument): device
+// memory that kernels read is only ever written by kernels (see h2d).
+__global__ void k_store_u64(u64* p, u64 v) {
+    if (threadIdx.x == 0) *p = v;
+}
 static void set_base(tbgpu_ctx* c, int k, u64 v) {
-    if (v == 0) {  // (the common reset: no staging, no round trip)
-        HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)(c->T.base + k), 0, 2, c->stream));
-        return;
-    }
-    c->h_base[3] = v;  // staged through pinned memory (async copy), then waited for
-    HIP_CHECK(hipMemcpyAsync(c->T.base + k, c->h_base + 3, sizeof(u64), hipMemcpyHostToDevice, c->stream));
-    wait_stream(c->stream);
+    k_store_u64<<<1, 64, 0, c->stream>>>(c->T.base + k, v);
+    HIP_CHECK(hipGetLastError());
 }
 
 static void ensure_h_rc(tbgpu_ctx* c, u64 nb) {
@@ -1222,11 +1223,41 @@ static void dcopy(void* dst, const void* src, u64 bytes, hipStream_t s) {
     HIP_CHECK(hipGetLastError());
 }
 
+// Host memory (page-locked, mapped) into device memory by a kernel: the kernel's loads
+// cross PCIe uncached and its stores go through the L2s like every other kernel's, so
+// later kernels see them.  (A copy engine writes HBM behind the L2s: kernels that had
+// read the buffer before could go on reading their L2's old lines -- DESIGN.md §5.)
+__global__ void k_copy_in(u8* __restrict__ dst, const u8* __restrict__ src, u64 n) {
+    const u64 stride = (u64)gridDim.x * blockDim.x;
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0) {
+        const u64 n16 = n / 16;
+        for (u64 k = t; k < n16; k += stride) ((uint4*)dst)[k] = ((const uint4*)src)[k];
+        for (u64 k = n16 * 16 + t; k < n; k += stride) dst[k] = src[k];
+    } else {
+        for (u64 k = t; k < n; k += stride) dst[k] = src[k];
+    }
+}
+static void copy_in(void* dst, const void* src_dev, u64 bytes, hipStream_t s) {
+    const u64 items = std::max<u64>(bytes / 16, 1);
+    const u32 blocks = (u32)std::min<u64>((items + 255) / 256, 1024);
+    k_copy_in<<<blocks, 256, 0, s>>>((u8*)dst, (const u8*)src_dev, bytes);
+    HIP_CHECK(hipGetLastError());
+}
+
+static bool sdma_h2d() {  // TBGPU_SDMA_H2D=1: uploads by the copy engine (A/B diagnostics)
+    static const bool b = getenv("TBGPU_SDMA_H2D") != nullptr;
+    return b;
+}
+
 static tbgpu_ctx::UpRing& up_ring(tbgpu_ctx* c, hipStream_t s) {
     tbgpu_ctx::UpRing& R = c->up[s == c->route_stream ? 1 : 0];
     if (R.h[0]) return R;
     for (int h = 0; h < 2; h++) {
-        HIP_CHECK(hipHostMalloc((void**)&R.h[h], UP_HALF, hipHostMallocDefault));
+        HIP_CHECK(hipHostMalloc((void**)&R.h[h], UP_HALF, hipHostMallocMapped | hipHostMallocCoherent));
+        void* d = nullptr;
+        HIP_CHECK(hipHostGetDevicePointer(&d, R.h[h], 0));
+        R.d[h] = (const u8*)d;
         poison_host(R.h[h], UP_HALF);
         HIP_CHECK(hipEventCreateWithFlags(&R.ev[h], hipEventDisableTiming));
         HIP_CHECK(hipEventRecord(R.ev[h], s));
@@ -1236,9 +1267,12 @@ static tbgpu_ctx::UpRing& up_ring(tbgpu_ctx* c, hipStream_t s) {
 
 static void h2d(tbgpu_ctx* c, void* dst, const void* src, u64 bytes, hipStream_t s) {
     if (bytes == 0) return;
-    if ((c->opt.flags & TBGPU_OPT_PINNED_INPUT) && pinned_device_ptr(src, bytes)) {
-        HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
-        return;
+    if (c->opt.flags & TBGPU_OPT_PINNED_INPUT) {
+        if (const void* dev = pinned_device_ptr(src, bytes)) {
+            if (sdma_h2d()) HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+            else copy_in(dst, dev, bytes, s);
+            return;
+        }
     }
     tbgpu_ctx::UpRing& R = up_ring(c, s);
     for (u64 off = 0; off < bytes;) {
@@ -1247,7 +1281,8 @@ static void h2d(tbgpu_ctx* c, void* dst, const void* src, u64 bytes, hipStream_t
         R.next ^= 1;
         HIP_CHECK(hipEventSynchronize(R.ev[h]));  // the half's previous copy has read it
         memcpy(R.h[h], (const u8*)src + off, k);
-        HIP_CHECK(hipMemcpyAsync((u8*)dst + off, R.h[h], k, hipMemcpyHostToDevice, s));
+        if (sdma_h2d()) HIP_CHECK(hipMemcpyAsync((u8*)dst + off, R.h[h], k, hipMemcpyHostToDevice, s));
+        else copy_in((u8*)dst + off, R.d[h], k, s);
         HIP_CHECK(hipEventRecord(R.ev[h], s));
         off += k;
     }
@@ -1673,6 +1708,13 @@ extern "C" void tbgpu_advance_commit_timestamp(tbgpu_ctx* c, uint64_t timestamp)
     HIP_CHECK(hipSetDevice(c->device));
     k_advance_commit_ts<<<1, 64, 0, c->stream>>>(c->T.commit_ts, timestamp);
     HIP_CHECK(hipGetLastError());
+}
+
+extern "C" int tbgpu_copy_to_device(tbgpu_ctx* c, void* dst_device, const void* src_host, uint64_t bytes) {
+    HIP_CHECK(hipSetDevice(c->device));
+    h2d(c, dst_device, src_host, bytes, c->stream);
+    wait_stream(c->stream);
+    return 0;
 }
 
 extern "C" int tbgpu_prefetch_transfers(tbgpu_ctx* c, const tbgpu_transfer_t* events, uint32_t count) {

@@ -227,12 +227,10 @@ __device__ __forceinline__ u32 classify_one(const Tables& T, const TrArgs& C, u3
     } else {
         if (dled != cled) sres = TBGPU_CREATE_TRANSFER_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
         else if (t.ledger != dled) sres = TBGPU_CREATE_TRANSFER_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
-        else if (!ledger_owned(T, t.ledger)) {
-            // a ledger shard got a transfer of another shard's ledger (the router never
-            // sends one): its rows are not here, the host aborts the call
-            sres = TBGPU_CREATE_TRANSFER_LINKED_EVENT_FAILED;
-            fl |= FL_FOREIGN;
-        } else {
+        else {
+            // (a ledger shard: the accounts may be another shard's, ROW_FOREIGN, when the
+            // router sent the event here because its id is committed or first seen here:
+            // it can only answer `exists*`, which evaluate_one checks before any balance)
             sres = SRES_DYN;
             pre_e = xidx_probe(T, t.id);
             gslot = gtab_find_or_insert(C, t.id, i, 0);
@@ -575,6 +573,11 @@ __device__ __forceinline__ bool evaluate_one(const Tables& T, const TrArgs& C, c
                 Transfer t = C.ev[i];
                 t.timestamp = k.ts;
                 res = create_transfer_exists(t, load_ref(T, C, S, e));
+            } else if (C.dslot[i] == ROW_FOREIGN || C.cslot[i] == ROW_FOREIGN) {
+                // a ledger shard's event with another shard's accounts that is not a
+                // repeat: the router never sends one (its rows are not here)
+                atomicOr(&C.counters[CNT_FLAGS], (u32)FL_FOREIGN);
+                res = TBGPU_CREATE_TRANSFER_LINKED_EVENT_FAILED;
             } else {
                 u128 amount = 0;
                 res = eval_balances(k, bd, bc, &amount);
@@ -738,6 +741,7 @@ __global__ __launch_bounds__(LS_THREADS) void tr_lists(TrArgs C) {
         const u8 sr = C.sres[i];
         if (sr != SRES_DYN) cls = C.cs[i] != C.ce[i] ? 1 : 0;
         else if (C.core[i].flags & (TF_POST | TF_VOID)) cls = 2;
+        else if (C.dslot[i] == ROW_FOREIGN || C.cslot[i] == ROW_FOREIGN) cls = 2;  // can only answer exists*
         else cls = (C.prev_id[i] == NONE32 && C.pre_e[i] == NONE32) ? 1 : 2;
     }
     const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1051,7 +1055,7 @@ __global__ void tr_side_build(TrArgs C, EvalState S, u32 kmax, const uint4* pair
     }
     for (u32 j = 0; j < k; j++) {
         if (is_post_void(C, i)) cand_slots(C, i, cand[j], &d, &c);
-        if (d == NONE32 || c == NONE32) d = c = invalid;
+        if (d == NONE32 || c == NONE32 || d == ROW_FOREIGN || c == ROW_FOREIGN) d = c = invalid;
         const u32 s = s0 + 2 * j;
         skey[s] = d;
         skey[s + 1] = c;
@@ -1188,6 +1192,10 @@ __global__ void tr_apply(Tables T, TrArgs C, EvalState S, const u8* __restrict__
         const u64 prow = (p & PREF_ROW) ? (u64)(p & ~PREF_ROW) : row_base + rk[p].x;
         T.xful[prow] = (t.flags & TF_POST) ? 1 : 2;
     } else {
+        if (C.dslot[i] == ROW_FOREIGN || C.cslot[i] == ROW_FOREIGN) {  // (never: evaluate_one flagged it)
+            atomicOr(&C.counters[CNT_FLAGS], (u32)FL_FOREIGN);
+            return;
+        }
         const Account& dra = T.acc[C.dslot[i]];
         const Account& cra = T.acc[C.cslot[i]];
         if ((dra.flags | cra.flags) & AF_HISTORY) {
@@ -1458,7 +1466,8 @@ __global__ __launch_bounds__(64) void tr_walk(Tables T, TrArgs C, EvalState D, B
                     D.amt[i] = 0;
                     D.pamt[i] = 0;
                     D.pref[i] = NONE32;
-                } else if (R.sr == SRES_DYN && !pv && R.pid == NONE32 && R.pre_e == NONE32) {
+                } else if (R.sr == SRES_DYN && !pv && R.pid == NONE32 && R.pre_e == NONE32 &&
+                           C.dslot[i] != ROW_FOREIGN && C.cslot[i] != ROW_FOREIGN) {
                     // a transfer whose id nothing before it holds: create_transfer's balance tail
                     const Bal4 bd = read_bal(R.s0d, k, 0), bc = read_bal(R.s0c, k, 1);
                     bb[R.ep.x] = bd;  // the balances it saw (history rows, tr_apply)

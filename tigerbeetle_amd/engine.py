@@ -88,6 +88,8 @@ def lib():
     for name in ("tbgpu_lookup_accounts", "tbgpu_lookup_transfers"):
         getattr(L, name).restype = u32
         getattr(L, name).argtypes = [vp, vp, u32, vp]
+    L.tbgpu_copy_to_device.restype = ctypes.c_int
+    L.tbgpu_copy_to_device.argtypes = [vp, vp, vp, u64]
     L.tbgpu_prefetch_transfers.restype = ctypes.c_int
     L.tbgpu_prefetch_transfers.argtypes = [vp, vp, u32]
     L.tbgpu_prefetch_wait.restype = ctypes.c_int
@@ -213,6 +215,19 @@ class Engine:
         out = np.zeros(max(len(events), 1), dtype=RESULT_DTYPE)
         n = self._L.tbgpu_create_transfers(self._h, timestamp, _ptr(events), len(events), _ptr(out))
         return out[:n].copy()
+
+    def to_device(self, host, torch_device=None):
+        """A device copy (torch uint8 tensor) of a numpy array / bytes, written by the
+        engine's copy kernel (tbgpu_copy_to_device) rather than a copy engine: the way
+        to hand the *_device entry points their inputs."""
+        import torch
+        a = np.ascontiguousarray(np.frombuffer(host, dtype=np.uint8) if isinstance(host, (bytes, bytearray))
+                                 else np.asarray(host)).view(np.uint8).reshape(-1)
+        out = torch.empty(max(len(a), 1), dtype=torch.uint8, device=torch_device or f"cuda:{self.device}")
+        torch.cuda.current_stream(out.device).synchronize()  # the allocation's previous users are done
+        if len(a):
+            self._L.tbgpu_copy_to_device(self._h, ctypes.c_void_p(out.data_ptr()), _ptr(a), len(a))
+        return out[:len(a)]
 
     def prefetch_transfers(self, events: np.ndarray) -> None:
         """StateMachine.prefetch for create_transfers (tbgpu_prefetch_transfers): the

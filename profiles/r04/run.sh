@@ -29,6 +29,9 @@ for step in "$@"; do
     poison_suite) run poison_suite 700 env TBGPU_POISON_ALLOC=1 TBGPU_CHECK_INDEX=1 $PT tests -m gpu || ok1 ;;
     sdma_suite) run sdma_suite 600 env TBGPU_SDMA_H2D=1 $PT tests -m gpu || ok1 ;;
     sdma_off_suite) run sdma_off_suite 600 env TBGPU_SDMA_H2D=1 HSA_ENABLE_SDMA=0 $PT tests -m gpu || ok1 ;;
+    nocontig_suite) run nocontig_suite 600 env TBGPU_NO_CONTIG=1 $PT tests -m gpu || ok1 ;;
+    flush_suite) run flush_suite 600 env TBGPU_FLUSH_CALLS=1 $PT tests -m gpu || ok1 ;;
+    nosdma_suite) run nosdma_suite 600 env HSA_ENABLE_SDMA=0 $PT tests -m gpu || ok1 ;;
     smoke) run smoke 180 python -u __graft_entry__.py smoke || exit 1 ;;
     bench) run bench 400 python bench.py || exit 1 ;;
     bench_cfg*) run "bench_cfg${step#bench_cfg}" 400 python bench.py --config "${step#bench_cfg}" || exit 1 ;;

@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "common.h"
@@ -118,27 +119,104 @@ inline void poison_host(void* p, u64 bytes) {
     if (zero_alloc()) memset(p, poison_byte(), bytes);
 }
 
+// TBGPU_GUARD=1 (diagnostics): every device allocation gets GUARD_BYTES of a known
+// word pattern behind it, and every entry point first checks all live guards: a
+// kernel that writes past the end of its buffer fails the next call, naming the
+// buffer (its size and allocation number), instead of corrupting a neighbour.
+constexpr u64 GUARD_BYTES = 64 << 10;
+constexpr u32 GUARD_WORD = 0xA5C3A5C3u;
+struct Guard {
+    void* base;
+    u64 offset;  // the guard's start: the buffer's bytes rounded up to 256
+    u64 bytes, elem;
+    u64 serial;
+};
+std::mutex g_guard_mu;
+std::vector<Guard> g_guards;
+u64 g_guard_serial = 0;
+inline bool guard_on() {
+    static const bool g = getenv("TBGPU_GUARD") != nullptr;
+    return g;
+}
+__global__ void k_guard_check(const u32* g, u32 words, u32* bad) {
+    for (u32 k = blockIdx.x * blockDim.x + threadIdx.x; k < words; k += gridDim.x * blockDim.x)
+        if (g[k] != GUARD_WORD) atomicAdd(bad, 1u);
+}
+// every live guard intact, else fatal (naming the first broken one)
+void guard_check_all(hipStream_t s) {
+    if (!guard_on()) return;
+    std::lock_guard<std::mutex> lk(g_guard_mu);
+    static u32* bad = nullptr;
+    if (!bad) HIP_CHECK(hipMalloc(&bad, 4 * 4096));
+    const size_t n = std::min<size_t>(g_guards.size(), 4096);
+    HIP_CHECK(hipMemsetAsync(bad, 0, 4 * n, s));
+    for (size_t k = 0; k < n; k++)
+        k_guard_check<<<16, 256, 0, s>>>((const u32*)((u8*)g_guards[k].base + g_guards[k].offset),
+                                         (u32)(GUARD_BYTES / 4), bad + k);
+    std::vector<u32> h(n);
+    HIP_CHECK(hipMemcpyAsync(h.data(), bad, 4 * n, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    for (size_t k = 0; k < n; k++)
+        if (h[k]) {
+            char why[200];
+            snprintf(why, sizeof why, "%u guard words past allocation #%llu (%llu bytes, element %llu B) overwritten",
+                     h[k], (unsigned long long)g_guards[k].serial, (unsigned long long)g_guards[k].bytes,
+                     (unsigned long long)g_guards[k].elem);
+            tbgpu_fatal("guard", why, __FILE__, __LINE__);
+        }
+}
+void guard_release(void* p) {
+    if (!guard_on() || !p) return;
+    std::lock_guard<std::mutex> lk(g_guard_mu);
+    for (size_t k = 0; k < g_guards.size(); k++)
+        if (g_guards[k].base == p) {
+            g_guards[k] = g_guards.back();
+            g_guards.pop_back();
+            return;
+        }
+}
+inline u64 guard_extra(u64 bytes) { return guard_on() ? ((bytes + 255) & ~255ull) - bytes + GUARD_BYTES : 0; }
+inline void guard_arm(void* p, u64 bytes, u64 elem) {
+    if (!guard_on()) return;
+    const u64 off = (bytes + 255) & ~255ull;
+    if (t_zero_stream) {
+        HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)((u8*)p + off), GUARD_WORD, GUARD_BYTES / 4, t_zero_stream));
+        HIP_CHECK(hipStreamSynchronize(t_zero_stream));
+    } else {
+        HIP_CHECK(hipMemsetD32((hipDeviceptr_t)((u8*)p + off), GUARD_WORD, GUARD_BYTES / 4));
+    }
+    std::lock_guard<std::mutex> lk(g_guard_mu);
+    g_guards.push_back(Guard{p, off, bytes, elem, g_guard_serial++});
+}
+
 template <typename T>
 T* dalloc(u64 count, u64* total) {
     void* p = nullptr;
     const u64 bytes = std::max<u64>(count * sizeof(T), 16);
-    HIP_CHECK(hipMalloc(&p, bytes));
+    HIP_CHECK(hipMalloc(&p, bytes + guard_extra(bytes)));
     zero_new(p, bytes);
+    guard_arm(p, bytes, sizeof(T));
     *total += bytes;
     return (T*)p;
 }
 
 // The tables every transfer probes at random (account rows and directory, the id
-// index): physically contiguous where the driver can place them, so their
-// translations stay few and large whatever earlier processes left the allocator with;
-// a plain allocation otherwise (same contents either way).
+// index).  Rounds 2-3 allocated them physically contiguous
+// (hipExtMallocWithFlags(hipDeviceMallocContiguous)) for fewer translations.  In a
+// process whose earlier contexts had freed such allocations, later contexts then
+// read and wrote data that was not theirs (wrong query rows, account rows of an
+// earlier state, an illegal address): the whole GPU suite passes with plain
+// allocations and fails without them (gpurun_out/r04e).  Plain
+// allocations it is; TBGPU_CONTIG=1 restores the contiguous ones for experiments.
 template <typename T>
 T* dalloc_hot(u64 count, u64* total) {
 #if !defined(TBGPU_NO_CONTIG)
+    static const bool contig = getenv("TBGPU_CONTIG") != nullptr;
     void* p = nullptr;
     const u64 bytes = std::max<u64>(count * sizeof(T), 16);
-    if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous) == hipSuccess && p) {
+    if (contig && hipExtMallocWithFlags(&p, bytes + guard_extra(bytes), hipDeviceMallocContiguous) == hipSuccess && p) {
         zero_new(p, bytes);
+        guard_arm(p, bytes, sizeof(T));
         *total += bytes;
         return (T*)p;
     }
@@ -148,6 +226,20 @@ T* dalloc_hot(u64 count, u64* total) {
 }
 
 }  // namespace
+
+// TBGPU_FLUSH_CALLS=1 (diagnostics): every entry point first writes back and
+// invalidates every XCD's L2 (system-scope release + acquire in many workgroups), so
+// no kernel of the call can hit a line an earlier kernel or ctx left in an L2.
+__global__ void k_flush_caches() {
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+}
+static void entry_flush(hipStream_t s) {
+    guard_check_all(s);
+    static const bool on = getenv("TBGPU_FLUSH_CALLS") != nullptr;
+    if (!on) return;
+    k_flush_caches<<<4096, 64, 0, s>>>();
+    HIP_CHECK(hipGetLastError());
+}
 
 constexpr u32 PC_RING = 1024;        // pass-counter ring (passes in flight << ring)
 constexpr u32 PASS_GROUP_MAX = 48;   // passes enqueued between two host round trips
@@ -550,9 +642,10 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamSynchronize(c->route_stream);
     // Free every device allocation by walking the struct's pointers.
+    guard_check_all(c->stream);
     for (void* p : {(void*)c->ro_orank, (void*)c->ro_blk, (void*)c->ro_bstart, (void*)c->ro_counts,
                     (void*)c->ro_bcount, (void*)c->ro_spart})
-        if (p) (void)hipFree(p);
+        if (p) { guard_release(p); (void)hipFree(p); }
     void* ptrs[] = {c->T.dense, c->T.acc, c->T.aidx, c->T.xrows, c->T.xful, c->T.xidx, c->T.hrows, c->T.commit_ts, c->T.idr, c->T.xrun, c->T.big, c->ev_buf,
                     c->b_start, c->ts, c->cs, c->ce, c->sres, c->dslot, c->cslot, c->pre_e, c->pre_p,
                     c->pp_dslot, c->pp_cslot, c->gslot, c->pslot, c->prev_id, c->pend_last, c->pend_first, c->prev_pend,
@@ -566,10 +659,10 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
                     c->q_tval, c->q_ss.keys_tmp, c->q_ss.vals_tmp, c->q_ss.hist, c->q_runs_dev, c->ximp,
                     c->lst_simple, c->lst_complex, c->d_ev, c->d_chain, c->d_slot, c->d_win, c->w_sstart, c->w_bal,
                     c->w_undo_slot, c->w_undo_val, c->w_out, c->ac_part, c->pf_buf};
-    for (void* p : ptrs) if (p) (void)hipFree(p);
+    for (void* p : ptrs) if (p) { guard_release(p); (void)hipFree(p); }
     for (EvalState& s : c->st) {
         void* q[] = {s.res, s.ok, s.pref, s.cfail, s.amt, s.pamt};
-        for (void* p : q) if (p) (void)hipFree(p);
+        for (void* p : q) if (p) { guard_release(p); (void)hipFree(p); }
     }
     if (c->h_counters) (void)hipHostFree(c->h_counters);
     if (c->h_report) (void)hipHostFree(c->h_report);
@@ -1330,6 +1423,7 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
                                   bool dst_device, uint32_t* result_counts, const uint64_t* ev_ts_host = nullptr,
                                   const uint8_t* ctl_host = nullptr, bool routed_device = false) {
     HIP_CHECK(hipSetDevice(c->device));
+    entry_flush(c->stream);
     HIP_CHECK(hipEventRecord(c->ev0, c->stream));
     ensure_h_rc(c, nb_total);
     std::vector<u32> starts;
@@ -1582,7 +1676,7 @@ static void route_capacity(tbgpu_ctx* c, u32 world, u32 batch_count, u64 n) {
         wait_stream(c->route_stream);
         for (void* p : {(void*)c->ro_orank, (void*)c->ro_blk, (void*)c->ro_bstart, (void*)c->ro_counts,
                         (void*)c->ro_bcount, (void*)c->ro_spart})
-            if (p) HIP_CHECK(hipFree(p));
+            if (p) { guard_release(p); HIP_CHECK(hipFree(p)); }
         c->ro_cap = std::max<u64>(std::max<u64>(n, batch_count + 1), c->ro_cap);
         u64 ro_bytes = 0;
         ZeroOn zero_on(c->route_stream);
@@ -1601,6 +1695,7 @@ static void route_capacity(tbgpu_ctx* c, u32 world, u32 batch_count, u64 n) {
 extern "C" int tbgpu_route_prepare(tbgpu_ctx* c, uint32_t world, const void* events_device, uint64_t count,
                                    uint64_t* out) {
     HIP_CHECK(hipSetDevice(c->device));
+    entry_flush(c->route_stream);
     if (world == 0 || world > 256) return -22;
     route_capacity(c, world, 0, count);
     route_rank((const Transfer*)events_device, count, world, c->ro_orank, c->ro_blk, c->ro_spart, c->rt_stats,
@@ -1616,6 +1711,7 @@ static int route_scatter_any(tbgpu_ctx* c, uint32_t world, uint32_t batch_count,
                              void* send_records_device, uint32_t word_mask, void* send_packed_device,
                              uint64_t* send_counts, uint32_t* send_batch_counts, uint32_t* send_span_counts) {
     HIP_CHECK(hipSetDevice(c->device));
+    entry_flush(c->route_stream);
     if (world == 0 || world > 256) return -22;
     std::vector<u32> starts(batch_count + 1, 0);
     for (u32 b = 0; b < batch_count; b++) {
@@ -1867,6 +1963,7 @@ static uint64_t accounts_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t
                                  const Account* events, bool device, tbgpu_create_accounts_result_t* results,
                                  uint32_t* result_counts) {
     HIP_CHECK(hipSetDevice(c->device));
+    entry_flush(c->stream);
     HIP_CHECK(hipEventRecord(c->ev0, c->stream));
     std::vector<u32> starts;
     u64 total = 0, ev_off = 0;
@@ -1930,6 +2027,7 @@ extern "C" uint32_t tbgpu_create_accounts(tbgpu_ctx* c, uint64_t timestamp, cons
 template <typename Row, typename Launch>
 static uint32_t lookup(tbgpu_ctx* c, const tbgpu_uint128_t* ids, uint32_t count, Row* out, Launch launch) {
     HIP_CHECK(hipSetDevice(c->device));
+    entry_flush(c->stream);
     uint32_t found_total = 0;
     std::vector<Row> rows;
     std::vector<u8> found;
@@ -2014,6 +2112,7 @@ static void check_index(tbgpu_ctx* c) {
 
 extern "C" uint64_t tbgpu_compact(tbgpu_ctx* c) {
     HIP_CHECK(hipSetDevice(c->device));
+    entry_flush(c->stream);
     const u64 r0 = c->q_runs.back(), r1 = c->n_rows;
     if (r1 == r0) return r1;
     if (!c->q_key) {

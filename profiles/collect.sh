@@ -8,7 +8,7 @@
 # config + accounts); TB_CALLS = warmup + steps of the profiled command.
 set -e
 OUT=${1:-gpurun_out/pmc}; shift || true
-ARGS=${@:---steps 2 --warmup 1 --no-cpu --no-queries --no-subconfigs}
+ARGS=${@:---steps 2 --warmup 1 --no-cpu --no-queries --no-subconfigs --no-host}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 B="python3 bench.py $ARGS"

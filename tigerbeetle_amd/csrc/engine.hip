@@ -342,6 +342,7 @@ struct tbgpu_ctx {
     const u8* rt_ctl = nullptr;
     bool rt_dry = false;
     u32 slow_chunks = 0;  // consecutive chunks that needed the fixed point
+    u32 fast_misses = 0;  // consecutive fast attempts that fell back (they back off: fast_due)
     // a fast attempt enqueued without its round trip (try_fast spec): settled at the
     // call's next wait (spec_settle), undone there if it fell back
     bool spec_pending = false;
@@ -1213,6 +1214,13 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
 // to `results_dev` after the device reply cursor, per-batch reply counts to c->counts.
 // Returns false (nothing committed, every effect undone) when the fast path does
 // not apply and `split` asks the caller to redo these batches in smaller chunks.
+// Whether a chunk of a slow run tries the fast path first: every 8th chunk while the
+// attempts are new, backing off to every 64th while they keep falling back (a failed
+// attempt costs its fp_commit and its undo, ~0.15 ms per config-3 chunk).
+static bool fast_due(const tbgpu_ctx* c) {
+    return c->slow_chunks % (8u << std::min<u32>(c->fast_misses, 3u)) == 0;
+}
+
 static bool run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
                                 tbgpu_create_transfers_result_t* results_dev, bool try_fast_path, bool split,
                                 bool spec = false) {
@@ -1227,8 +1235,10 @@ static bool run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
     if (fast_ok) {
         if (try_fast(c, ev, n, nb, results_dev, spec)) {
             c->slow_chunks = 0;
+            if (!spec) c->fast_misses = 0;
             return true;
         }
+        c->fast_misses++;
         if (split) return false;
     }
     c->slow_chunks++;
@@ -1412,9 +1422,13 @@ static bool spec_settle(tbgpu_ctx* c) {
     c->spec_pending = false;
     const u32 flags = c->h_counters[CNT_FLAGS];
     if (flags & FL_ERROR) tbgpu_fatal("create_transfers", "fast path look-back did not complete", __FILE__, __LINE__);
-    if (!(flags & FL_SLOW)) return true;
+    if (!(flags & FL_SLOW)) {
+        c->fast_misses = 0;
+        return true;
+    }
     fp_launch_undo(c->T, c->spec_F, c->stream);  // commit_timestamp back; the deltas
     c->slow_chunks = 1;                          // the redo goes to the fixed point
+    c->fast_misses++;
     return false;
 }
 
@@ -1450,7 +1464,7 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         // reads each once): no copy and no DMA / compute hand-off.  A fallback redoes the
         // call with a copy (slow_chunks).
         const bool zc = !src_device && (c->opt.flags & TBGPU_OPT_PINNED_INPUT) && b0 == 0 && b1 == nb_total &&
-                        n <= FP_TAIL_MAX && c->slow_chunks % 8 == 0 &&
+                        n <= FP_TAIL_MAX && fast_due(c) &&
                         !c->rt_dry && !ev_ts_host && !ctl_host && !(c->opt.flags & TBGPU_OPT_FORCE_GENERAL) &&
                         !spec_disabled() && !zero_copy_disabled();
         const Transfer* ev_zc = zc ? (const Transfer*)pinned_device_ptr(ev_src + ev_off, (u64)n * 128) : nullptr;
@@ -1490,7 +1504,7 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         // device results: the call's buffer (cursor-relative); host results: staged in
         // res_buf one chunk at a time
         tbgpu_create_transfers_result_t* rdev = dst_device ? results : (tbgpu_create_transfers_result_t*)c->res_buf;
-        const bool try_fast_path = c->slow_chunks % 8 == 0;
+        const bool try_fast_path = fast_due(c);
         // a call that is one chunk makes its fast attempt without the round trip that
         // decides whether it stands: that answer comes with the call's final wait
         const bool spec = try_fast_path && !c->rt_dry && b0 == 0 && b1 == nb_total &&

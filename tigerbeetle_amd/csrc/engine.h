@@ -312,16 +312,37 @@ __device__ __forceinline__ bool xrun_maybe(const Tables& T, u128 id) {
     return id >= (((u128)r[3] << 64) | r[2]) && id <= (((u128)r[5] << 64) | r[4]);
 }
 
-// the row of `id` in the sorted run, or NONE32
+__device__ __forceinline__ double u128_to_double(u128 x) {
+    return (double)(u64)(x >> 64) * 18446744073709551616.0 + (double)(u64)x;
+}
+
+// the row of `id` in the sorted run, or NONE32.  Interpolation search between rows of
+// known ids (the run's ids rise, and in practice nearly evenly: the benchmark's are
+// consecutive with the failed ones missing), then bisection after a few steps, so an
+// uneven run costs at most a few probes more than a binary search.  A binary search
+// over 2M rows read ~20 random rows per lookup (tr_classify: 520 B per event).
 __device__ __forceinline__ u32 xrun_find(const Tables& T, u128 id) {
-    u64 lo = T.xrun[0], hi = T.xrun[1];
-    while (lo < hi) {
-        const u64 mid = (lo + hi) / 2;
+    const u64* r = T.xrun;
+    if (r[0] == r[1]) return NONE32;
+    u64 a = r[0], b = r[1] - 1;  // rows with known ids ka, kb; ka <= id <= kb holds
+    u128 ka = ((u128)r[3] << 64) | r[2], kb = ((u128)r[5] << 64) | r[4];
+    if (id < ka || id > kb) return NONE32;
+    for (int it = 0;; it++) {
+        if (id == ka) return (u32)a;
+        if (id == kb) return (u32)b;
+        if (b - a <= 1) return NONE32;
+        u64 mid;
+        if (it < 4) {
+            const double f = u128_to_double(id - ka) / u128_to_double(kb - ka);
+            mid = a + (u64)(f * (double)(b - a) + 0.5);
+            mid = mid <= a ? a + 1 : (mid >= b ? b - 1 : mid);
+        } else {
+            mid = a + (b - a) / 2;
+        }
         const u128 k = T.xrows[mid].id;
         if (k == id) return (u32)mid;
-        if (k < id) lo = mid + 1; else hi = mid;
+        if (k < id) { a = mid; ka = k; } else { b = mid; kb = k; }
     }
-    return NONE32;
 }
 
 __device__ __forceinline__ u32 xidx_probe(const Tables& T, u128 id) {

@@ -343,6 +343,10 @@ struct tbgpu_ctx {
     bool rt_dry = false;
     u32 slow_chunks = 0;  // consecutive chunks that needed the fixed point
     u32 fast_misses = 0;  // consecutive fast attempts that fell back (they back off: fast_due)
+    // a small chunk's batch block held back for fp_prep (upload_batches with
+    // allow_inline): flush_block launches k_upload_block if no fp_prep took it
+    BlockInline blk{};
+    u32 blk_words = 0;
     // a fast attempt enqueued without its round trip (try_fast spec): settled at the
     // call's next wait (spec_settle), undone there if it fell back
     bool spec_pending = false;
@@ -394,6 +398,7 @@ struct tbgpu_ctx {
     std::vector<u64> q_runs{0};  // row boundaries of the index runs; back() = rows indexed
     u8* ximp = nullptr;          // per stored row: 1 = imported from another shard
     hipEvent_t ev0, ev1;
+    hipEvent_t ev_side, ev_lists;  // fixed_point's side count and work-list lengths landed
     // phase profiler: consecutive marks on the ctx stream; segment k belongs to
     // the phase opened by mark k.
     bool prof = false;
@@ -574,6 +579,8 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     HIP_CHECK(hipStreamCreateWithFlags(&c->route_stream, hipStreamNonBlocking));
     HIP_CHECK(hipEventCreate(&c->ev0));
     HIP_CHECK(hipEventCreate(&c->ev1));
+    HIP_CHECK(hipEventCreateWithFlags(&c->ev_side, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&c->ev_lists, hipEventDisableTiming));
     c->accounts_max = o.accounts_max;
     c->aidx_cap = pow2_at_least(2 * o.hashed_max);  // ids outside the direct-mapped directory
     c->xrow_cap = o.transfers_max;
@@ -681,6 +688,8 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     if (c->pf_ev) (void)hipEventDestroy(c->pf_ev);
     (void)hipEventDestroy(c->ev0);
     (void)hipEventDestroy(c->ev1);
+    (void)hipEventDestroy(c->ev_side);
+    (void)hipEventDestroy(c->ev_lists);
     (void)hipStreamDestroy(c->stream);
     (void)hipStreamDestroy(c->route_stream);
     delete c;
@@ -772,8 +781,32 @@ __global__ void k_upload_block(const u32* host_block, u32 words, u32* block, u64
     if (i == 0 && reset_replies) base[BASE_REPLIES] = 0;
 }
 
+static void flush_block(tbgpu_ctx* c) {
+    if (!c->blk_words) return;
+    k_upload_block<<<1, 256, 0, c->stream>>>(c->h_stage_dev, c->blk_words, c->b_start, c->T.base,
+                                             c->blk.reset_replies);
+    HIP_CHECK(hipGetLastError());
+    c->blk_words = 0;
+}
+
+// The held-back block for fp_prep (consumed: the caller launches fp_prep with it).
+static BlockInline take_block(tbgpu_ctx* c) {
+    BlockInline b{};
+    if (c->blk_words) {
+        b = c->blk;
+        b.words = c->blk_words;
+        c->blk_words = 0;
+    }
+    return b;
+}
+
+static bool inline_disabled() {
+    static const bool d = getenv("TBGPU_NO_INLINE_BLOCK") != nullptr;  // A/B timing
+    return d;
+}
+
 static void upload_batches(tbgpu_ctx* c, const uint64_t* timestamps, const uint32_t* counts, u32 nb,
-                           std::vector<u32>& starts, bool reset_replies = false) {
+                           std::vector<u32>& starts, bool reset_replies = false, bool allow_inline = false) {
     starts.resize(nb + 1);
     starts[0] = 0;
     for (u32 b = 0; b < nb; b++) starts[b + 1] = starts[b] + counts[b];
@@ -787,6 +820,19 @@ static void upload_batches(tbgpu_ctx* c, const uint64_t* timestamps, const uint3
     memcpy(c->h_stage_ts, timestamps, nb * sizeof(u64));
     memcpy(c->h_stage_start, starts.data(), (nb + 1) * sizeof(u32));
     const u32 words = (u32)(off + 2 * nb);
+    // a block still held back belongs to a chunk none of whose kernels ran (a fast
+    // attempt refused before its launches, the chunk redone): this one supersedes it
+    c->blk_words = 0;
+    if (allow_inline && words <= BLOCK_INLINE_WORDS && !inline_disabled()) {
+        // a small call: fp_prep writes the block from its arguments (one launch less);
+        // any other first kernel is preceded by flush_block
+        c->blk.block = c->b_start;
+        c->blk.base = c->T.base;
+        c->blk.reset_replies = reset_replies ? 1u : 0u;
+        memcpy(c->blk.w, c->h_stage_start, words * sizeof(u32));
+        c->blk_words = words;
+        return;
+    }
     k_upload_block<<<(words + 255) / 256, 256, 0, c->stream>>>(c->h_stage_dev, words, c->b_start, c->T.base,
                                                                reset_replies ? 1u : 0u);
     HIP_CHECK(hipGetLastError());
@@ -872,7 +918,7 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_crea
     F.dry = c->rt_dry ? 1u : 0u;
     F.commit_ts = c->rt_dry ? c->rt_dry_ts : c->T.commit_ts;
     prof_mark(c, PH_PREP);
-    fp_launch_prep(F, s);
+    fp_launch_prep(F, s, take_block(c));
     prof_mark(c, PH_CLASSIFY);
     F.ev_copy = c->ev_in_host ? (Transfer*)c->ev_buf : nullptr;
     fp_launch_commit(c->T, F, s);
@@ -1024,28 +1070,38 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
     prof_mark(c, PH_CLASSIFY);
     tr_launch_prep(C, c->st[0].cfail, c->pc, PC_RING, s);
     tr_launch_classify(c->T, C, s);
+
+    // The sides of the events, sorted by account.  Their count (tr_side_count's bound,
+    // which classify's results decide) is enqueued right behind classify, so its host
+    // round trip overlaps the grouping and the initial state instead of idling the GPU.
+    u64 m = 0;
+    u32 n_list[2] = {0, 0};  // the per-pass work lists' lengths (simple, complex)
+    auto count_sides = [&](u32 kmax) {
+        tr_launch_side_count(C, kmax, c->mask, s);
+        scan3_exclusive(c->mask, c->ranks, n, c->sc, s);
+        HIP_CHECK(hipMemcpyAsync(c->h_base + 4, c->ranks + n, sizeof(uint4), hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipEventRecord(c->ev_side, s));
+    };
+    count_sides(SIDE_CANDS);
+    bool counted = true;  // a count is in flight for the first build
+
     // grouping by id / pending id: each step runs only when classify found the need
     tr_launch_group(C, 0, s);
     tr_launch_group2(C, s);
     tr_launch_group(C, 1, s);
     tr_launch_init(c->T, C, c->st[0], c->st[1], s);
     tr_launch_lists(C, s);
+    HIP_CHECK(hipMemcpyAsync(c->h_base + 6, c->counters + CNT_NSIMPLE, 2 * sizeof(u32), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipEventRecord(c->ev_lists, s));
 
-    // The sides of the events, sorted by account (one host round trip: their count).
-    u64 m = 0;
-    u32 n_list[2] = {0, 0};  // the per-pass work lists' lengths (simple, complex)
     auto build_sides = [&](const EvalState& S) {
         prof_mark(c, PH_SORT);
         for (u32 kmax : {SIDE_CANDS, 1u}) {
-            tr_launch_side_count(C, S, kmax, c->mask, s);
-            scan3_exclusive(c->mask, c->ranks, n, c->sc, s);
+            if (!counted) count_sides(kmax);
+            counted = false;
+            wait_event(c->ev_side);
             uint4 tot;
-            HIP_CHECK(hipMemcpyAsync(c->h_base + 4, c->ranks + n, sizeof(uint4), hipMemcpyDeviceToHost, s));
-            // the work lists' lengths (tr_lists) come back with the side count
-            HIP_CHECK(hipMemcpyAsync(c->h_base + 6, c->counters + CNT_NSIMPLE, 2 * sizeof(u32), hipMemcpyDeviceToHost, s));
-            wait_stream(s);
             memcpy(&tot, c->h_base + 4, sizeof tot);
-            memcpy(n_list, c->h_base + 6, sizeof n_list);
             m = 2ull * (tot.x + tot.y + tot.z);
             if (m <= c->scap) {
                 tr_launch_side_build(C, S, kmax, c->ranks, inv_acc, c->skey, c->sval, s);
@@ -1059,6 +1115,8 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
         c->stats.sorts++;
     };
     build_sides(c->st[0]);
+    wait_event(c->ev_lists);  // (long landed: the sort is queued behind it)
+    memcpy(n_list, c->h_base + 6, sizeof n_list);
 
     SideScanArgs SA{};
     SA.skey = c->skey_s; SA.sq_ev = c->sq_ev; SA.sq_cs = c->sq_cs; SA.sq_ok = c->sq_ok;
@@ -1228,6 +1286,7 @@ static bool run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
     c->stats.iterations = 0;
     c->stats.path = 0;
     if (n == 0) {
+        flush_block(c);
         HIP_CHECK(hipMemsetAsync(c->counts, 0, nb * sizeof(u32), s));
         return true;
     }
@@ -1242,6 +1301,7 @@ static bool run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
         if (split) return false;
     }
     c->slow_chunks++;
+    flush_block(c);  // (a fast attempt's fp_prep has written it already)
     TrArgs C = make_tr_args(c, ev, n, nb);
     C.epi = c->counters + EPI_WORD;  // the apply kernels run only behind a converged pass group
     C.epi_alt = c->st[1];
@@ -1485,7 +1545,7 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         }
         // the replies start at the front of `results` (device results: the call's first
         // chunk; host results: every chunk, staged in res_buf)
-        upload_batches(c, timestamps + b0, counts + b0, nb, starts, ev_off == 0 || !dst_device);
+        upload_batches(c, timestamps + b0, counts + b0, nb, starts, ev_off == 0 || !dst_device, /*allow_inline=*/true);
         c->rt_ev_ts = nullptr;
         c->rt_ctl = nullptr;
         if (routed_device) {  // already in HBM

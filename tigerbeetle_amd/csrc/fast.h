@@ -39,7 +39,17 @@ enum { ABL_DUP = 1, ABL_BALANCES = 2, ABL_ROWS = 4, ABL_LOOKBACK = 8, ABL_EVENT 
 #define FP_ABLATE 0
 #endif
 
-void fp_launch_prep(const FastArgs& F, hipStream_t stream);
+// A small call's batch block (starts, then timestamps: engine.hip upload_batches)
+// written by fp_prep from its arguments instead of by a launch of its own.
+constexpr u32 BLOCK_INLINE_WORDS = 8;
+struct BlockInline {
+    u32* block;          // c->b_start
+    u64* base;           // T.base (the reply cursor's reset)
+    u32 words;           // 0: nothing to write
+    u32 reset_replies;
+    u32 w[BLOCK_INLINE_WORDS];
+};
+void fp_launch_prep(const FastArgs& F, hipStream_t stream, const BlockInline& bi = BlockInline{});
 void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream);
 void fp_launch_index(const Tables& T, const FastArgs& F, hipStream_t stream);
 void fp_launch_fix(const Tables& T, const FastArgs& F, u8* mask, uint4* ranks, Scan3Scratch& sc, hipStream_t stream);

@@ -908,8 +908,10 @@ __global__ void fp_advance(Tables T, FastArgs F) {
 // commit_timestamp for the fallback: fp_commit raises it for every event it
 // classifies ok against the pre-call state, which the sequential result may not
 // (an id repeated later in the call answers `exists`).
-__global__ void fp_prep(FastArgs F) {
+__global__ void fp_prep(FastArgs F, BlockInline bi) {
     const u32 k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < bi.words) bi.block[k] = bi.w[k];
+    if (k == 0 && bi.words && bi.reset_replies) bi.base[BASE_REPLIES] = 0;
     if (k < CNT_TS_SAVE) F.counters[k] = 0;
     if (k == 0) *(u64*)&F.counters[CNT_TS_SAVE] = *F.commit_ts;
     if (k < F.nb) F.batch_counts[k] = 0;
@@ -1063,8 +1065,8 @@ __global__ void fp_undo(Tables T, FastArgs F) {
 
 #define GRID(n) (u32)(((n) + 255) / 256), 256, 0, stream
 
-void fp_launch_prep(const FastArgs& F, hipStream_t stream) {
-    fp_prep<<<GRID(std::max<u32>(F.nb, CNT_COUNT))>>>(F);
+void fp_launch_prep(const FastArgs& F, hipStream_t stream, const BlockInline& bi) {
+    fp_prep<<<GRID(std::max<u32>(std::max<u32>(F.nb, CNT_COUNT), BLOCK_INLINE_WORDS))>>>(F, bi);
     HIP_CHECK(hipGetLastError());
 }
 

@@ -87,7 +87,7 @@ void tr_launch_group2(const TrArgs& C, hipStream_t stream);
 // D: the first pass's input state; D2 (the other buffer) also receives the static
 // failures outside chains, which no pass evaluates again
 void tr_launch_init(const Tables& T, const TrArgs& C, const EvalState& D, const EvalState& D2, hipStream_t stream);
-void tr_launch_side_count(const TrArgs& C, const EvalState& S, u32 kmax, u8* mask, hipStream_t stream);
+void tr_launch_side_count(const TrArgs& C, u32 kmax, u8* mask, hipStream_t stream);
 void tr_launch_side_build(const TrArgs& C, const EvalState& S, u32 kmax, const uint4* pairs, u32 invalid, u32* skey,
                           u32* sval, hipStream_t stream);
 void tr_launch_side_pos(const TrArgs& C, const u32* sval_s, u64 m, hipStream_t stream);

@@ -812,20 +812,11 @@ __device__ __forceinline__ void mark_changed(const TrArgs& C, u32 i, u32 q) {
 // A pass over the simple list: create_transfer's balance tail (src/state_machine.zig:
 // 1286-1322) for transfers whose id nothing before them holds, and the static failures
 // inside chains (they break their chain every pass).  What evaluate_one does for them,
-// without its post/void and `exists` registers (occupancy: this is most of a pass).
-__global__ __launch_bounds__(256) void tr_eval_simple(TrArgs C, EvalState S, EvalState D, const Bal4* __restrict__ bb,
-                                                      PassGate g, u32 cnt, u32* chg, u32* chg_next, u32* front,
-                                                      u32* front_next) {
-    if (!gate_open(g)) return;
-    const u32 k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k == 0) {
-        *chg_next = 0;
-        *front_next = NONE32;
-    }
+// without its post/void and `exists` work (most of a pass's events are here).
+__device__ __forceinline__ bool eval_simple_one(const TrArgs& C, const EvalState& S, const EvalState& D,
+                                                const Bal4* __restrict__ bb, const PassGate& g, u32 i) {
     bool changed = false;
-    u32 i = NONE32;
-    if (k < cnt) {
-        i = C.lst_simple[k];
+    {
         const u8 sr = C.sres[i];
         const u32 csi = C.cs[i], cei = C.ce[i];
         if (!due(C, g, i, csi, cei)) {
@@ -865,29 +856,49 @@ __global__ __launch_bounds__(256) void tr_eval_simple(TrArgs C, EvalState S, Eva
             }
         }
     }
-    const u32 c = block_sum(changed ? 1u : 0u);
-    const u32 f = block_min(changed ? i : NONE32);
-    if (threadIdx.x == 0 && c) {
-        atomicAdd(chg, c);
-        atomicMin(front, f);
-    }
+    return changed;
 }
 
 // evaluate_one over the complex list
-__global__ void tr_eval_complex(Tables T, TrArgs C, EvalState S, EvalState D, const Bal4* __restrict__ bb, PassGate g,
-                                u32 cnt, u32* chg, u32* front) {
-    if (!gate_open(g)) return;
-    const u32 k = blockIdx.x * blockDim.x + threadIdx.x;
-    u32 i = NONE32;
+__device__ __forceinline__ bool eval_complex_one(const Tables& T, const TrArgs& C, const EvalState& S,
+                                                 const EvalState& D, const Bal4* __restrict__ bb, const PassGate& g,
+                                                 u32 k, u32& i) {
+    i = C.lst_complex[k];
+    const u32 csi = C.cs[i], cei = C.ce[i];
     bool changed = false;
-    if (k < cnt) {
-        i = C.lst_complex[k];
-        const u32 csi = C.cs[i], cei = C.ce[i];
-        if (due(C, g, i, csi, cei)) {
-            changed = evaluate_one(T, C, S, D, bb, g, i);
-            if (changed) mark_changed(C, i, g.p);
-        } else if (i == csi && csi != cei) {
-            D.cfail[csi] = S.cfail[csi];
+    if (due(C, g, i, csi, cei)) {
+        changed = evaluate_one(T, C, S, D, bb, g, i);
+        if (changed) mark_changed(C, i, g.p);
+    } else if (i == csi && csi != cei) {
+        D.cfail[csi] = S.cfail[csi];
+    }
+    return changed;
+}
+
+// One pass's evaluation of both work lists in one launch: the first `nbc` workgroups
+// take the complex list (dispatched first: their events are the longer dependent-load
+// chains), the rest the simple list.  Two launches ran the lists one after the other;
+// here the complex list's latency hides under the simple list's work.
+constexpr u32 EV_THREADS = 256;
+__global__ __launch_bounds__(EV_THREADS) void tr_eval_lists(Tables T, TrArgs C, EvalState S, EvalState D,
+                                                            const Bal4* __restrict__ bb, PassGate g, u32 n_simple,
+                                                            u32 n_complex, u32 nbc, u32* chg, u32* chg_next,
+                                                            u32* front, u32* front_next) {
+    if (!gate_open(g)) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *chg_next = 0;
+        *front_next = NONE32;
+    }
+    bool changed = false;
+    u32 i = NONE32;
+    if (blockIdx.x < nbc) {
+        const u32 k = blockIdx.x * EV_THREADS + threadIdx.x;
+        if (k < n_complex) changed = eval_complex_one(T, C, S, D, bb, g, k, i);
+    } else {
+        const u32 k = (blockIdx.x - nbc) * EV_THREADS + threadIdx.x;
+        if (k < n_simple) {
+            i = C.lst_simple[k];
+            changed = eval_simple_one(C, S, D, bb, g, i);
         }
     }
     const u32 c = block_sum(changed ? 1u : 0u);
@@ -1015,13 +1026,19 @@ __device__ __forceinline__ bool is_post_void(const TrArgs& C, u32 i) {
 }
 
 // Side pairs per event, as a popcount mask for scan3: 1 -> 0b001, 2 -> 0b011, 3 -> 0b111.
-__global__ void tr_side_count(TrArgs C, EvalState S, u32 kmax, u8* mask) {
+// An upper bound of post_candidates' count that classify's results alone decide (every
+// candidate is the committed pending or an earlier event with the pending id, whatever
+// the state), so the count and its round trip run before the grouping and the initial
+// state, and overlap them; tr_side_build pads a post/void's unused pairs with inert keys.
+// (In practice the bound is the count: a pending id is rarely repeated.)
+__global__ void tr_side_count(TrArgs C, u32 kmax, u8* mask) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= C.n) return;
     u32 pairs = 1;
     if (is_post_void(C, i)) {
-        u32 cand[SIDE_CANDS];
-        pairs = max(1u, post_candidates(C, S, i, kmax, cand));
+        const u32 p = C.pslot[i];
+        const u32 k = (C.pre_p[i] != NONE32 ? 1u : 0u) + (p != NONE32 ? C.gcnt_id[p] : 0u);
+        pairs = max(1u, min(kmax, k));
     }
     mask[i] = (u8)((1u << pairs) - 1);
 }
@@ -1036,11 +1053,23 @@ __device__ __forceinline__ void cand_slots(const TrArgs& C, u32 i, u32 cand, u32
 
 __global__ void tr_side_build(TrArgs C, EvalState S, u32 kmax, const uint4* pairs, u32 invalid, u32* skey, u32* sval) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    {
+        // the fused scan's window words start empty (tr_side_pos lowers tstart, the
+        // passes stamp win): cleared here rather than by two fills of their own
+        const uint4 tot = pairs[C.n];
+        const u64 m = 2ull * (tot.x + tot.y + tot.z), nwin = (m + C.sd.tile - 1) / C.sd.tile + 1;
+        for (u64 k = i; k < nwin; k += (u64)gridDim.x * blockDim.x) {
+            C.sd.tstart[k] = NONE32;
+            C.dt.win[k] = NONE32;
+        }
+    }
     if (i > C.n) return;
     const uint4 pr = pairs[i];
     const u32 s0 = 2 * (pr.x + pr.y + pr.z);
     C.sd.soff[i] = s0;
     if (i == C.n) return;
+    const uint4 pr1 = pairs[i + 1];
+    const u32 slots = (2 * (pr1.x + pr1.y + pr1.z) - s0) / 2;  // tr_side_count's bound
     u32 cand[SIDE_CANDS];
     u32 k = 1;
     u32 d = NONE32, c = NONE32;
@@ -1053,8 +1082,16 @@ __global__ void tr_side_build(TrArgs C, EvalState S, u32 kmax, const uint4* pair
             k = max(1u, post_candidates(C, S, i, kmax, cand));
         }
     }
-    for (u32 j = 0; j < k; j++) {
-        if (is_post_void(C, i)) cand_slots(C, i, cand[j], &d, &c);
+    if (k > slots) {  // (the bound holds by construction: a broken one is a device error)
+        atomicOr(&C.counters[CNT_FLAGS], (u32)FL_ERROR);
+        k = slots;
+    }
+    for (u32 j = 0; j < slots; j++) {
+        if (j >= k) {
+            d = c = NONE32;  // padding: an inert pair that no resolution names
+        } else if (is_post_void(C, i)) {
+            cand_slots(C, i, cand[j], &d, &c);
+        }
         if (d == NONE32 || c == NONE32 || d == ROW_FOREIGN || c == ROW_FOREIGN) d = c = invalid;
         const u32 s = s0 + 2 * j;
         skey[s] = d;
@@ -1063,7 +1100,7 @@ __global__ void tr_side_build(TrArgs C, EvalState S, u32 kmax, const uint4* pair
         sval[s + 1] = s + 1;
         C.sd.sev[s] = i;
         C.sd.sev[s + 1] = i | (1u << 31);
-        C.sd.scand[s] = C.sd.scand[s + 1] = is_post_void(C, i) ? cand[j] : NONE32;
+        C.sd.scand[s] = C.sd.scand[s + 1] = (is_post_void(C, i) && j < k) ? cand[j] : NONE32;
     }
 }
 
@@ -1613,17 +1650,15 @@ void tr_launch_group2(const TrArgs& C, hipStream_t stream) { tr_group2<<<GRID(C.
 void tr_launch_init(const Tables& T, const TrArgs& C, const EvalState& D, const EvalState& D2, hipStream_t stream) {
     tr_init<<<GRID(C.n)>>>(T, C, D, D2);
 }
-void tr_launch_side_count(const TrArgs& C, const EvalState& S, u32 kmax, u8* mask, hipStream_t stream) {
-    tr_side_count<<<GRID(C.n)>>>(C, S, kmax, mask);
+void tr_launch_side_count(const TrArgs& C, u32 kmax, u8* mask, hipStream_t stream) {
+    tr_side_count<<<GRID(C.n)>>>(C, kmax, mask);
 }
 void tr_launch_side_build(const TrArgs& C, const EvalState& S, u32 kmax, const uint4* pairs, u32 invalid, u32* skey,
                           u32* sval, hipStream_t stream) {
     tr_side_build<<<GRID(C.n + 1)>>>(C, S, kmax, pairs, invalid, skey, sval);
 }
 void tr_launch_side_pos(const TrArgs& C, const u32* sval_s, u64 m, hipStream_t stream) {
-    HIP_CHECK(hipMemsetAsync(C.sd.tstart, 0xFF, ((m + C.sd.tile - 1) / C.sd.tile + 1) * sizeof(u32), stream));
-    HIP_CHECK(hipMemsetAsync(C.dt.win, 0xFF, ((m + C.sd.tile - 1) / C.sd.tile + 1) * sizeof(u32), stream));
-    tr_side_pos<<<GRID(m)>>>(C, sval_s, m);
+    tr_side_pos<<<GRID(m)>>>(C, sval_s, m);  // (tstart and win cleared by tr_side_build)
 }
 void tr_launch_side_rec(const TrArgs& C, const EvalState& S, hipStream_t stream) {
     tr_side_rec<<<GRID(C.n)>>>(C, S);
@@ -1638,9 +1673,10 @@ void tr_launch_lists(const TrArgs& C, hipStream_t stream) {
 void tr_launch_evaluate_lists(const Tables& T, const TrArgs& C, const EvalState& S, const EvalState& D, const Bal4* bb,
                               const PassGate& g, u32* chg, u32* chg_next, u32* front, u32* front_next, u32 n_simple,
                               u32 n_complex, hipStream_t stream) {
-    // the simple kernel always runs (it clears the next pass's words)
-    tr_eval_simple<<<GRID(std::max<u32>(n_simple, 1))>>>(C, S, D, bb, g, n_simple, chg, chg_next, front, front_next);
-    if (n_complex) tr_eval_complex<<<GRID(n_complex)>>>(T, C, S, D, bb, g, n_complex, chg, front);
+    // always launched (its first thread clears the next pass's words)
+    const u32 nbc = (n_complex + EV_THREADS - 1) / EV_THREADS, nbs = (n_simple + EV_THREADS - 1) / EV_THREADS;
+    tr_eval_lists<<<std::max<u32>(nbc + nbs, 1), EV_THREADS, 0, stream>>>(T, C, S, D, bb, g, n_simple, n_complex, nbc,
+                                                                          chg, chg_next, front, front_next);
 }
 void tr_launch_mask(const Tables& T, const TrArgs& C, const EvalState& S, u8* fres, u8* mask, hipStream_t stream) {
     tr_mask<<<GRID(C.n)>>>(T, C, S, fres, mask);

@@ -247,14 +247,16 @@ __device__ __forceinline__ u32 acc_probe(const AccIdx* __restrict__ aidx, u64 ma
     }
 }
 
+// A directory entry decoded (acc_find's direct-mapped case).
+__device__ __forceinline__ u32 acc_from_dense(u64 e, u32* ledger, u16* flags) {
+    if (e == 0) return NONE32;
+    *ledger = (u32)(e >> 32);
+    *flags = (u16)((e >> 28) & 0xE);
+    return dense_row(e);
+}
+
 __device__ __forceinline__ u32 acc_find(const Tables& T, u128 id, u32* ledger, u16* flags) {
-    if (dense_has(T, id)) {
-        const u64 e = T.dense[dense_slot(T, id)];
-        if (e == 0) return NONE32;
-        *ledger = (u32)(e >> 32);
-        *flags = (u16)((e >> 28) & 0xE);
-        return dense_row(e);
-    }
+    if (dense_has(T, id)) return acc_from_dense(T.dense[dense_slot(T, id)], ledger, flags);
     const u64 lo = (u64)id, hi = (u64)(id >> 64);
     u64 h = hash128(lo, hi) & T.aidx_mask;
     for (;;) {

@@ -36,22 +36,15 @@ __global__ __launch_bounds__(RS_THREADS) void rs_hist(const u32* __restrict__ ke
 }
 
 // Exclusive scan of `total` u32 words in place (total is a multiple of 256), one
-// workgroup of 1024 threads: each thread sums a contiguous run of the words (16-byte
-// loads), one workgroup scan of the 1024 sums (wave shuffles, the 16 wave sums
-// through LDS), then each thread rewrites its run from its prefix.  (A sweep of
-// 4096-word tiles with a running carry took 12 us per 41k words: ten barriered rounds.)
-constexpr u32 RSS_THREADS = 1024;
-__global__ __launch_bounds__(RSS_THREADS) void rs_scan(u32* __restrict__ data, u64 total, const u32* pred, u32 pmask) {
-    if (rs_off(pred, pmask)) return;
-    __shared__ u32 wsum[RSS_THREADS / 64];
+// workgroup of 1024 threads.  Up to 64k words: each thread loads a contiguous run of
+// at most 16 uint4 into registers at once (independent loads, one memory latency),
+// one workgroup scan of the 1024 run sums (wave shuffles, the 16 wave sums through
+// LDS), and each thread writes its run from its prefix.  Larger: a sweep of 4096-word
+// tiles with a running carry (ten barriered rounds per 41k words took 12 us; a run
+// loop without the register staging, 18 us).
+constexpr u32 RSS_THREADS = 1024, RSS_RUN = 16;
+__device__ __forceinline__ u32 rss_block_excl(u32 s, u32* wsum, u32& all) {
     const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const u64 run = ((total + RSS_THREADS - 1) / RSS_THREADS + 3) & ~3ull;  // words per thread, 16-byte aligned
-    const u64 lo = min((u64)tid * run, total), hi = min(lo + run, total);
-    u32 s = 0;
-    for (u64 k = lo; k < hi; k += 4) {
-        const uint4 v = *(const uint4*)(data + k);
-        s += v.x + v.y + v.z + v.w;
-    }
     u32 x = s;  // inclusive scan over the wave
     for (int off = 1; off < 64; off <<= 1) {
         const u32 y = __shfl_up(x, off);
@@ -68,11 +61,47 @@ __global__ __launch_bounds__(RSS_THREADS) void rs_scan(u32* __restrict__ data, u
         if (lane < RSS_THREADS / 64) wsum[lane] = t;  // inclusive prefix of the wave sums
     }
     __syncthreads();
-    u32 excl = (wave ? wsum[wave - 1] : 0) + x - s;
-    for (u64 k = lo; k < hi; k += 4) {
-        const uint4 v = *(const uint4*)(data + k);
-        *(uint4*)(data + k) = make_uint4(excl, excl + v.x, excl + v.x + v.y, excl + v.x + v.y + v.z);
-        excl += v.x + v.y + v.z + v.w;
+    const u32 excl = (wave ? wsum[wave - 1] : 0) + x - s;
+    all = wsum[RSS_THREADS / 64 - 1];
+    __syncthreads();  // wsum is free again
+    return excl;
+}
+__global__ __launch_bounds__(RSS_THREADS) void rs_scan(u32* __restrict__ data, u64 total, const u32* pred, u32 pmask) {
+    if (rs_off(pred, pmask)) return;
+    __shared__ u32 wsum[RSS_THREADS / 64];
+    const u32 tid = threadIdx.x;
+    const u64 q = total / 4;  // uint4 words
+    if (q <= (u64)RSS_THREADS * RSS_RUN) {
+        const u32 run = (u32)((q + RSS_THREADS - 1) / RSS_THREADS);
+        const u64 lo = (u64)tid * run;
+        uint4 v[RSS_RUN];
+        u32 s = 0;
+#pragma unroll
+        for (u32 k = 0; k < RSS_RUN; k++) {
+            v[k] = (k < run && lo + k < q) ? ((const uint4*)data)[lo + k] : make_uint4(0, 0, 0, 0);
+            s += v[k].x + v[k].y + v[k].z + v[k].w;
+        }
+        u32 all;
+        u32 excl = rss_block_excl(s, wsum, all);
+#pragma unroll
+        for (u32 k = 0; k < RSS_RUN; k++) {
+            if (k < run && lo + k < q)
+                ((uint4*)data)[lo + k] = make_uint4(excl, excl + v[k].x, excl + v[k].x + v[k].y,
+                                                    excl + v[k].x + v[k].y + v[k].z);
+            excl += v[k].x + v[k].y + v[k].z + v[k].w;
+        }
+        return;
+    }
+    u32 carry = 0;
+    for (u64 base = 0; base < total; base += 4 * RSS_THREADS) {
+        const u64 k = base + (u64)tid * 4;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (k < total) v = *(const uint4*)(data + k);
+        const u32 s = v.x + v.y + v.z + v.w;
+        u32 all;
+        const u32 excl = carry + rss_block_excl(s, wsum, all);
+        if (k < total) *(uint4*)(data + k) = make_uint4(excl, excl + v.x, excl + v.x + v.y, excl + v.x + v.y + v.z);
+        carry += all;
     }
 }
 

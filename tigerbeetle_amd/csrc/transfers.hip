@@ -122,10 +122,19 @@ __device__ __forceinline__ u32 gtab_find(const TrArgs& C, u128 key) {
 // bookkeeping of execute (:1018-1035), and the probes that replace prefetch
 // (:598-655): debit/credit account slots, pre-existing id, pending transfer.
 __device__ __forceinline__ u32 classify_one(const Tables& T, const TrArgs& C, u32 i) {
-    const u32 b = batch_of(C.b_start, C.nb, i);
+    // the batch: one uniform (scalar) search per wave for its first event; a wave
+    // spans 64 events, so lanes past a batch boundary walk on a step or two
+    const u32 w0 = __builtin_amdgcn_readfirstlane(i - (threadIdx.x & 63));
+    const Transfer t = C.ev[i];
+    const u32 wb = batch_of(C.b_start, C.nb, w0);
+    u32 b = wb;
+    while (C.b_start[b + 1] <= i) b++;
     const u32 bs = C.b_start[b], be = C.b_start[b + 1];
     const u32 nbatch = be - bs, k = i - bs;
-    const Transfer t = C.ev[i];
+    // the accounts' directory entries, issued before the checks that order their use
+    const bool dd = dense_has(T, t.debit_account_id), dc = dense_has(T, t.credit_account_id);
+    const u64 ed = dd ? T.dense[dense_slot(T, t.debit_account_id)] : 0;
+    const u64 ec = dc ? T.dense[dense_slot(T, t.credit_account_id)] : 0;
     const u64 ts = C.ev_ts ? C.ev_ts[i] : C.b_ts[b] - nbatch + k + 1;
     C.ts[i] = ts;
 
@@ -136,7 +145,7 @@ __device__ __forceinline__ u32 classify_one(const Tables& T, const TrArgs& C, u3
     };
     // within the wave from one ballot of the lanes' own flags; only a chain that
     // crosses the wave's edge walks on (lanes below an active lane are active)
-    const u32 lane = threadIdx.x & 63, w0 = i - lane;
+    const u32 lane = threadIdx.x & 63;
     const u64 lm = __ballot((t.flags & TF_LINKED) && !(C.ctl && (C.ctl[i] & TBGPU_CTL_CHAIN_END)));
     const u64 below = ~lm & ((1ull << lane) - 1), above = ~lm & (~0ull << lane);
     u32 s, e;
@@ -220,9 +229,11 @@ __device__ __forceinline__ u32 classify_one(const Tables& T, const TrArgs& C, u3
         sres = TBGPU_CREATE_TRANSFER_LEDGER_MUST_NOT_BE_ZERO;
     } else if (t.code == 0) {
         sres = TBGPU_CREATE_TRANSFER_CODE_MUST_NOT_BE_ZERO;
-    } else if ((dslot = acc_find(T, t.debit_account_id, &dled, &dfl)) == NONE32) {
+    } else if ((dslot = dd ? acc_from_dense(ed, &dled, &dfl) : acc_find(T, t.debit_account_id, &dled, &dfl)) ==
+               NONE32) {
         sres = TBGPU_CREATE_TRANSFER_DEBIT_ACCOUNT_NOT_FOUND;
-    } else if ((cslot = acc_find(T, t.credit_account_id, &cled, &cfl)) == NONE32) {
+    } else if ((cslot = dc ? acc_from_dense(ec, &cled, &cfl) : acc_find(T, t.credit_account_id, &cled, &cfl)) ==
+               NONE32) {
         sres = TBGPU_CREATE_TRANSFER_CREDIT_ACCOUNT_NOT_FOUND;
     } else {
         if (dled != cled) sres = TBGPU_CREATE_TRANSFER_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
@@ -1051,47 +1062,59 @@ __device__ __forceinline__ void cand_slots(const TrArgs& C, u32 i, u32 cand, u32
     *c = C.cslot[cand];
 }
 
+// Every input is loaded into registers before the first store: the stores go through
+// TrArgs pointers the compiler must assume alias the inputs, so a load issued after a
+// store waited for its own round trip (three dependent trips per candidate pair: 33 us
+// per 164k-event chunk).
 __global__ void tr_side_build(TrArgs C, EvalState S, u32 kmax, const uint4* pairs, u32 invalid, u32* skey, u32* sval) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint4 tot = pairs[C.n];
+    const bool ev = i < C.n;
+    const uint4 pr = i <= C.n ? pairs[i] : make_uint4(0, 0, 0, 0);
+    const uint4 pr1 = ev ? pairs[i + 1] : make_uint4(0, 0, 0, 0);
+    const u8 sr = ev ? C.sres[i] : 0;
+    const u16 fl = ev ? C.core[i].flags : 0;
+    const u32 ds = ev ? C.dslot[i] : NONE32, cs = ev ? C.cslot[i] : NONE32;
+    const u32 pd = ev ? C.pp_dslot[i] : NONE32, pc = ev ? C.pp_cslot[i] : NONE32;
+    const bool pv = sr == SRES_DYN && (fl & (TF_POST | TF_VOID));
+    u32 cand[SIDE_CANDS], cd[SIDE_CANDS], cc[SIDE_CANDS];
+    u32 k = 1;
+    cand[0] = NONE32;  // (a post/void without candidates keeps one inert pair)
+    if (pv) k = max(1u, post_candidates(C, S, i, kmax, cand));
+#pragma unroll
+    for (u32 j = 0; j < SIDE_CANDS; j++) {  // the candidates' account slots, issued together
+        cd[j] = cc[j] = NONE32;
+        if (pv && j < k && cand[j] != NONE32) {
+            if (cand[j] & PREF_ROW) { cd[j] = pd; cc[j] = pc; }
+            else { cd[j] = C.dslot[cand[j]]; cc[j] = C.cslot[cand[j]]; }
+        }
+    }
     {
         // the fused scan's window words start empty (tr_side_pos lowers tstart, the
         // passes stamp win): cleared here rather than by two fills of their own
-        const uint4 tot = pairs[C.n];
         const u64 m = 2ull * (tot.x + tot.y + tot.z), nwin = (m + C.sd.tile - 1) / C.sd.tile + 1;
-        for (u64 k = i; k < nwin; k += (u64)gridDim.x * blockDim.x) {
-            C.sd.tstart[k] = NONE32;
-            C.dt.win[k] = NONE32;
+        for (u64 q = i; q < nwin; q += (u64)gridDim.x * blockDim.x) {
+            C.sd.tstart[q] = NONE32;
+            C.dt.win[q] = NONE32;
         }
     }
     if (i > C.n) return;
-    const uint4 pr = pairs[i];
     const u32 s0 = 2 * (pr.x + pr.y + pr.z);
     C.sd.soff[i] = s0;
     if (i == C.n) return;
-    const uint4 pr1 = pairs[i + 1];
     const u32 slots = (2 * (pr1.x + pr1.y + pr1.z) - s0) / 2;  // tr_side_count's bound
-    u32 cand[SIDE_CANDS];
-    u32 k = 1;
-    u32 d = NONE32, c = NONE32;
-    cand[0] = NONE32;
-    if (C.sres[i] == SRES_DYN) {
-        if (!(C.core[i].flags & (TF_POST | TF_VOID))) {
-            d = C.dslot[i];
-            c = C.cslot[i];
-        } else {
-            k = max(1u, post_candidates(C, S, i, kmax, cand));
-        }
-    }
     if (k > slots) {  // (the bound holds by construction: a broken one is a device error)
         atomicOr(&C.counters[CNT_FLAGS], (u32)FL_ERROR);
         k = slots;
     }
-    for (u32 j = 0; j < slots; j++) {
-        if (j >= k) {
-            d = c = NONE32;  // padding: an inert pair that no resolution names
-        } else if (is_post_void(C, i)) {
-            cand_slots(C, i, cand[j], &d, &c);
-        }
+#pragma unroll
+    for (u32 j = 0; j < SIDE_CANDS; j++) {
+        if (j >= slots) break;
+        u32 d = NONE32, c = NONE32;
+        if (j < k) {
+            if (pv) { d = cd[j]; c = cc[j]; }
+            else if (sr == SRES_DYN) { d = ds; c = cs; }
+        }  // else padding: an inert pair that no resolution names
         if (d == NONE32 || c == NONE32 || d == ROW_FOREIGN || c == ROW_FOREIGN) d = c = invalid;
         const u32 s = s0 + 2 * j;
         skey[s] = d;
@@ -1100,7 +1123,7 @@ __global__ void tr_side_build(TrArgs C, EvalState S, u32 kmax, const uint4* pair
         sval[s + 1] = s + 1;
         C.sd.sev[s] = i;
         C.sd.sev[s + 1] = i | (1u << 31);
-        C.sd.scand[s] = C.sd.scand[s + 1] = (is_post_void(C, i) && j < k) ? cand[j] : NONE32;
+        C.sd.scand[s] = C.sd.scand[s + 1] = (pv && j < k) ? cand[j] : NONE32;
     }
 }
 
@@ -1117,14 +1140,15 @@ __global__ void tr_side_pos(TrArgs C, const u32* sval_s, u64 m) {
     start = wave_min(start);
     if (start != NONE32 && q == start) atomicMin(&C.sd.tstart[q / C.sd.tile], start);
     if (q >= m) return;
+    // loads before stores (they may alias for the compiler: see tr_side_build)
     const u32 s = sval_s[q];
-    C.sd.spos[s] = (u32)q;
     const u32 ev = C.sd.sev[s];
-    C.sd.sq_ev[q] = ev;
     const u32 i = ev & 0x7FFFFFFFu;
-    if (s - C.sd.soff[i] < 2) ((u32*)&C.sd.epos[i])[ev >> 31] = (u32)q;
-    const u32 cs = C.cs[i], ce = C.ce[i];
+    const u32 so = C.sd.soff[i], cs = C.cs[i], ce = C.ce[i];
     const bool doom = C.ctl && (C.ctl[ce] & TBGPU_CTL_DOOM);
+    C.sd.spos[s] = (u32)q;
+    C.sd.sq_ev[q] = ev;
+    if (s - so < 2) ((u32*)&C.sd.epos[i])[ev >> 31] = (u32)q;
     C.sd.sq_cs[q] = cs | (cs == ce ? SQ_STANDALONE : 0u) | (doom ? SQ_DOOM : 0u);
 }
 
@@ -1233,9 +1257,12 @@ __global__ void tr_apply(Tables T, TrArgs C, EvalState S, const u8* __restrict__
             atomicOr(&C.counters[CNT_FLAGS], (u32)FL_FOREIGN);
             return;
         }
-        const Account& dra = T.acc[C.dslot[i]];
-        const Account& cra = T.acc[C.cslot[i]];
-        if ((dra.flags | cra.flags) & AF_HISTORY) {
+        // the accounts' history flags are in the event's core (classify): the rows are
+        // read only for a history row
+        const u8 af = C.core[i].aflags;
+        if ((af | (af >> 4)) & AF_HISTORY) {
+            const Account& dra = T.acc[C.dslot[i]];
+            const Account& cra = T.acc[C.cslot[i]];
             // balances after this transfer (src/state_machine.zig:1342-1364)
             const u32 s0 = C.sd.soff[i];
             Bal4 d = bb[C.sd.spos[s0]], c = bb[C.sd.spos[s0 + 1]];

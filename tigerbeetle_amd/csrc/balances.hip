@@ -330,6 +330,11 @@ __global__ __launch_bounds__(BF_THREADS) void bs_fused(SideScanArgs A, u64 m, u3
                                                        u32 ntiles, u32* long_flag, const Account* __restrict__ acc,
                                                        Bal4* __restrict__ bb) {
     if (!gate_open(A.gate)) return;
+    if (A.epi) {  // the Bal4 scan behind a converged headroom fixed point: its state by the gate word
+        const u32 e = *A.epi;
+        if (e == 0) return;
+        if (e == 2) A.cfail = A.cfail_alt;
+    }
     __shared__ SF wtot[BF_THREADS / 64];
     __shared__ u32 s_key[BF_THREADS * BF_IPT], s_cs[BF_THREADS * BF_IPT];
     __shared__ Bal4 s_h[BF_THREADS * BF_IPT];
@@ -451,6 +456,150 @@ __global__ __launch_bounds__(BF_THREADS) void bs_fused(SideScanArgs A, u64 m, u3
     }
 }
 
+// ------------------------------------------------- headroom (narrow) scan ----
+// What a pass's evaluation reads of a balance, when no overflow check can fire (the
+// chunk's amounts < 2^64 and every committed balance < 2^126: FL_WIDE clear): a debit
+// side's limit and balancing checks read only H_d = credits_posted - debits_pending -
+// debits_posted of its account (src/state_machine.zig:1290-1322: dr.debits_* + amount
+// > dr.credits_posted <=> amount > H_d), a credit side only H_c = debits_posted -
+// credits_pending - credits_posted.  Both are linear in the sides' deltas, so the scan
+// carries (H_d, H_c) -- two u128 instead of four -- and writes one u128 per side.  The
+// fixed point is the same; the apply kernels get the Bal4 form from one full scan
+// after convergence.
+struct SN {
+    u128 hd, hc;
+    u32 fl;
+};
+__device__ __forceinline__ SN combine_n(const SN& a, const SN& b) {
+    SN c;
+    if (b.fl & 1) { c.hd = b.hd; c.hc = b.hc; }
+    else { c.hd = a.hd + b.hd; c.hc = a.hc + b.hc; }
+    c.fl = a.fl | b.fl;
+    return c;
+}
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ void dpp_step_n(SN& v) {
+    SN o;
+    o.hd = dpp128<CTRL, ROW_MASK>(v.hd);
+    o.hc = dpp128<CTRL, ROW_MASK>(v.hc);
+    o.fl = dpp32<CTRL, ROW_MASK>(v.fl);
+    v = combine_n(o, v);
+}
+__device__ __forceinline__ SN block_excl_n(SN v, SN* wtot) {
+    const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    dpp_step_n<0x111, 0xf>(v);
+    dpp_step_n<0x112, 0xf>(v);
+    dpp_step_n<0x114, 0xf>(v);
+    dpp_step_n<0x118, 0xf>(v);
+    dpp_step_n<0x142, 0xa>(v);
+    dpp_step_n<0x143, 0xc>(v);
+    SN ex;
+    ex.hd = shup128(v.hd, 1);
+    ex.hc = shup128(v.hc, 1);
+    ex.fl = __shfl_up(v.fl, 1);
+    if (lane == 0) { ex.hd = ex.hc = 0; ex.fl = 0; }
+    if (lane == 63) wtot[w] = v;
+    __syncthreads();
+    SN pre;
+    pre.hd = pre.hc = 0;
+    pre.fl = 0;
+    for (u32 k = 0; k < w; k++) pre = combine_n(pre, wtot[k]);
+    return combine_n(pre, ex);
+}
+
+__global__ __launch_bounds__(BF_THREADS) void bs_fused_narrow(SideScanArgs A, u64 m, u32 invalid,
+                                                              const u32* __restrict__ tstart, u32 ntiles,
+                                                              u32* long_flag, const Account* __restrict__ acc) {
+    if (!gate_open(A.gate)) return;
+    __shared__ SN wtot[BF_THREADS / 64];
+    __shared__ u32 s_key[BF_THREADS], s_cs[BF_THREADS];
+    __shared__ u128 s_hd[BF_THREADS], s_hc[BF_THREADS];
+    if (A.cfail_clear)
+        for (u64 k = (u64)blockIdx.x * BF_THREADS + threadIdx.x; k < A.n; k += (u64)gridDim.x * BF_THREADS)
+            A.cfail_clear[k] = NONE32;
+    const u32 t = blockIdx.x, tid = threadIdx.x;
+    const u32 pq = A.gate.p, par = pq & 1;
+    const bool all = A.gate.full || *A.dt.all == pq;
+    if (!all) {
+        for (u64 k = (u64)blockIdx.x * BF_THREADS + tid; k < A.n_complex; k += (u64)gridDim.x * BF_THREADS) {
+            const u32 i = A.lst_complex[k];
+            const u32 gs = A.gslot[i], ps = A.pslot[i];
+            if ((gs != NONE32 && A.dt.slot[par * A.dt.g + gs] == pq) ||
+                (ps != NONE32 && A.dt.slot[par * A.dt.g + ps] == pq)) {
+                A.dt.ev[par * A.dt.n + i] = pq;
+                const u32 cs = A.cs[i];
+                if (cs != A.ce[i]) A.dt.chain[par * A.dt.n + cs] = pq;
+            }
+        }
+    }
+    const u32 a0 = tstart[t];
+    if (a0 == NONE32) return;
+    u32 b0 = (u32)m;
+    for (u32 k = t + 1; k < ntiles; k++)
+        if (tstart[k] != NONE32) { b0 = tstart[k]; break; }
+    if (b0 - a0 > BF_THREADS) {
+        if (tid == 0) atomicMax(long_flag, A.gate.p + 1);
+        return;
+    }
+    if (!all) {
+        bool due = false;
+        for (u32 w = a0 / BF_TILE; w <= (b0 - 1) / BF_TILE; w++) due |= A.dt.win[w] == pq;
+        if (!due) return;
+    }
+    const u64 q = (u64)a0 + tid;
+    const u32 key = q < b0 ? A.skey[q] : invalid;
+    const u32 c = q < b0 ? A.sq_cs[q] : SQ_STANDALONE;
+    const u32 ev = q < b0 ? A.sq_ev[q] : 0;
+    const bool credit = ev >> 31;
+    u128 old = 0;
+    if (!all && key < invalid) old = A.bh[q];
+    u128 r_hd = 0, r_hc = 0;  // the account's pre-chunk headroom
+    if (key < invalid) {
+        const Account& ac = acc[key];
+        const u128 dp = ac.debits_pending, dpo = ac.debits_posted, cp = ac.credits_pending, cpo = ac.credits_posted;
+        r_hd = cpo - dp - dpo;
+        r_hc = dpo - cp - cpo;
+    }
+    // the side's delta on (H_d, H_c): final-ok -> F, evaluated-ok in a chain that does
+    // not persist -> H (visible only behind it in its own chain)
+    u128 f_hd = 0, f_hc = 0, h_hd = 0, h_hc = 0;
+    SN e;
+    e.fl = 1;
+    if (key < invalid) {
+        if (A.sq_ok[q] & 1) {
+            const u128 dpe = A.sq_dpend[q], dpo = A.sq_dpost[q];
+            const u128 dhd = credit ? dpo : (u128)0 - dpe - dpo;
+            const u128 dhc = credit ? (u128)0 - dpe - dpo : dpo;
+            if (side_final(A, q)) { f_hd = dhd; f_hc = dhc; } else { h_hd = dhd; h_hc = dhc; }
+        }
+        const u32 prev = q == a0 ? invalid : A.skey[q - 1];
+        e.fl = prev != key ? 1u : 0u;
+    }
+    e.hd = f_hd;
+    e.hc = f_hc;
+    s_key[tid] = key;
+    s_cs[tid] = (c & SQ_STANDALONE) ? NONE32 : (c & SQ_CS);
+    if (!(c & SQ_STANDALONE)) { s_hd[tid] = h_hd; s_hc[tid] = h_hc; }
+    const SN run = block_excl_n(e, wtot);  // (its barrier publishes s_key / s_cs / s_h*)
+    if (key < invalid) {
+        u128 h = 0;
+        u32 j = tid;
+        const u32 cs = c & SQ_CS;
+        if (s_cs[j] != NONE32)
+            while (j > 0 && s_key[j - 1] == key && s_cs[j - 1] == cs) { --j; h += credit ? s_hc[j] : s_hd[j]; }
+        u128 out = credit ? r_hc : r_hd;
+        if (!(e.fl & 1)) out += credit ? run.hc : run.hd;
+        out += h;
+        if (all) {
+            A.bh[q] = out;
+        } else if (old != out) {
+            A.bh[q] = out;  // a balance moved: its event is due this pass (with its chain)
+            A.dt.ev[par * A.dt.n + (ev & 0x7FFFFFFFu)] = pq;
+            if (!(c & SQ_STANDALONE)) A.dt.chain[par * A.dt.n + (c & SQ_CS)] = pq;
+        }
+    }
+}
+
 }  // namespace
 
 void side_scan_fused(const SideScanArgs& A, u64 m, u32 invalid, const u32* tstart, u32* long_flag,
@@ -458,6 +607,14 @@ void side_scan_fused(const SideScanArgs& A, u64 m, u32 invalid, const u32* tstar
     if (m == 0) return;
     const u32 ntiles = (u32)((m + BF_TILE - 1) / BF_TILE);
     bs_fused<<<ntiles, BF_THREADS, 0, stream>>>(A, m, invalid, tstart, ntiles, long_flag, acc, bb);
+    HIP_CHECK(hipGetLastError());
+}
+
+void side_scan_fused_narrow(const SideScanArgs& A, u64 m, u32 invalid, const u32* tstart, u32* long_flag,
+                            const Account* acc, hipStream_t stream) {
+    if (m == 0) return;
+    const u32 ntiles = (u32)((m + BF_TILE - 1) / BF_TILE);
+    bs_fused_narrow<<<ntiles, BF_THREADS, 0, stream>>>(A, m, invalid, tstart, ntiles, long_flag, acc);
     HIP_CHECK(hipGetLastError());
 }
 

@@ -214,6 +214,9 @@ struct SideScanArgs {
     const u32* lst_complex;
     u32 n_complex;
     const u32 *gslot, *pslot, *cs, *ce;
+    // headroom passes (side_scan_fused_narrow): the side's one balance figure its
+    // evaluation reads, or null (the Bal4 passes)
+    u128* bh;
 };
 
 // final-ok of a sorted side: evaluated-ok and its chain persisted
@@ -232,6 +235,11 @@ void side_scan(const SideScanArgs& A, u64 m, u32 invalid, bool has_chains, void*
 void side_scan_fused(const SideScanArgs& A, u64 m, u32 invalid, const u32* tstart, u32* long_flag,
                      const Account* acc, Bal4* bb, hipStream_t stream);
 u32 side_scan_fused_tile();
+// The passes' scan in headroom form (balances.hip): per side, the debit account's
+// credits_posted - debits_pending - debits_posted (a debit side) or the credit account's
+// debits_posted - credits_pending - credits_posted (a credit side), modulo 2^128, in A.bh.
+void side_scan_fused_narrow(const SideScanArgs& A, u64 m, u32 invalid, const u32* tstart, u32* long_flag,
+                            const Account* acc, hipStream_t stream);
 void side_final_balances(const SideScanArgs& A, u64 m, u32 invalid, const Bal4* bb, Account* acc, u32* big,
                          hipStream_t stream);
 
@@ -401,5 +409,6 @@ enum {
     FL_NONMONO = 1u << 10,    // fast path: ids of the call are not strictly increasing
     FL_FCHAIN = 1u << 11,     // fast path: linked chains, resolved by fp_chains
     FL_CAPACITY = 1u << 12,   // create_accounts: accounts_max reached (ac_apply wrote nothing past it)
+    FL_WIDE = 1u << 14,       // general path: an amount >= 2^64 or a balance near 2^128 (no headroom passes)
     FL_FOREIGN = 1u << 13,    // ledger shard: a transfer on a ledger another shard owns reached its balances
 };

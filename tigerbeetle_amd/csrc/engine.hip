@@ -292,6 +292,7 @@ struct tbgpu_ctx {
     u32 *lst_simple, *lst_complex;  // the fixed point's per-pass work lists (tr_lists)
     u32 *d_ev, *d_chain, *d_slot, *d_win;  // the passes' dirty stamps (engine.h Dirty)
     Bal4* bb = nullptr;
+    u128* bh = nullptr;  // headroom passes: one balance figure per side (balances.hip)
     SortScratch ss{};
     void* side_tiles = nullptr;
     Scan3Scratch sc{};
@@ -464,6 +465,7 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->gkey_s = dalloc<u32>(n, &B);
     c->gsorted = dalloc<u32>(n, &B);
     c->bb = dalloc<Bal4>(m, &B);
+    c->bh = dalloc<u128>(m, &B);
     c->ss.keys_tmp = dalloc<u32>(m, &B);
     c->ss.vals_tmp = dalloc<u32>(m, &B);
     c->ss.hist = dalloc<u32>(radix_sort_hist_words(m), &B);
@@ -660,7 +662,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
                     c->gclaim, c->gcnt_id, c->gcnt_pd, c->gmem, c->gbeg, c->gend, c->gfill, c->pfill, c->pbeg, c->skey, c->sval, c->skey_s,
                     c->soff, c->core, c->tstart, c->epos, c->sev, c->scand, c->sq_ev, c->sq_cs, c->sq_ok, c->sq_dpend, c->sq_dpost, c->gkey_s,
                     c->gsorted,
-                    c->sval_s, c->spos, c->bb, c->ss.keys_tmp, c->ss.vals_tmp, c->ss.hist, c->side_tiles,
+                    c->sval_s, c->spos, c->bb, c->bh, c->ss.keys_tmp, c->ss.vals_tmp, c->ss.hist, c->side_tiles,
                     c->sc.tile_sums, c->fres, c->mask, c->ranks, c->res_buf, c->counts, c->counters, c->status,
                     c->f_gtab, c->f_gpos, c->f_keys, c->f_rows,
                     c->f_tile_idr, c->rt_ts_buf, c->rt_ctl_buf, c->rt_dry_ts, c->rt_stats, c->rg_part, c->T.base, c->q_key, c->q_val, c->q_tkey,
@@ -1092,6 +1094,7 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
     tr_launch_init(c->T, C, c->st[0], c->st[1], s);
     tr_launch_lists(C, s);
     HIP_CHECK(hipMemcpyAsync(c->h_base + 6, c->counters + CNT_NSIMPLE, 2 * sizeof(u32), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(c->h_base + 7, c->counters + CNT_FLAGS, sizeof(u32), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipEventRecord(c->ev_lists, s));
 
     auto build_sides = [&](const EvalState& S) {
@@ -1117,6 +1120,13 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
     build_sides(c->st[0]);
     wait_event(c->ev_lists);  // (long landed: the sort is queued behind it)
     memcpy(n_list, c->h_base + 6, sizeof n_list);
+    u32 cflags = 0;
+    memcpy(&cflags, c->h_base + 7, sizeof cflags);
+    // Headroom passes (balances.hip side_scan_fused_narrow) unless an amount or a
+    // committed balance is too large for them (FL_WIDE); the Bal4 form then comes from
+    // one full scan behind the converged group, for the apply kernels.
+    static const bool no_narrow = getenv("TBGPU_NO_HEADROOM") != nullptr;  // A/B timing
+    const bool narrow = !(cflags & FL_WIDE) && !no_narrow;
 
     SideScanArgs SA{};
     SA.skey = c->skey_s; SA.sq_ev = c->sq_ev; SA.sq_cs = c->sq_cs; SA.sq_ok = c->sq_ok;
@@ -1142,15 +1152,35 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
             SA.cfail = S.cfail;
             SA.cfail_clear = D.cfail;
             SA.gate = G;
-            if (c->long_segments) side_scan(SA, m, inv_acc, chains, c->side_tiles, c->T.acc, c->bb, s);
-            else side_scan_fused(SA, m, inv_acc, c->tstart, c->counters + CNT_LONG, c->T.acc, c->bb, s);
-            tr_launch_evaluate_lists(c->T, C, S, D, c->bb, G, chg + (q + 1) % PC_RING, chg + (q + 2) % PC_RING,
+            const bool hr = narrow && !c->long_segments;
+            TrArgs CE = C;
+            CE.bh = hr ? c->bh : nullptr;
+            if (c->long_segments) {
+                side_scan(SA, m, inv_acc, chains, c->side_tiles, c->T.acc, c->bb, s);
+            } else if (hr) {
+                SideScanArgs SN = SA;
+                SN.bh = c->bh;
+                side_scan_fused_narrow(SN, m, inv_acc, c->tstart, c->counters + CNT_LONG, c->T.acc, s);
+            } else {
+                side_scan_fused(SA, m, inv_acc, c->tstart, c->counters + CNT_LONG, c->T.acc, c->bb, s);
+            }
+            tr_launch_evaluate_lists(c->T, CE, S, D, c->bb, G, chg + (q + 1) % PC_RING, chg + (q + 2) % PC_RING,
                                      chg + PC_RING + (q + 1) % PC_RING, chg + PC_RING + (q + 2) % PC_RING,
                                      n_list[0], n_list[1], s);
         }
         const u32 p0 = p;
         p += group;
         tr_launch_converged(chg, PC_RING, p0, p, c->counters, c->counters + EPI_WORD, s);
+        if (narrow && !c->long_segments) {
+            // the Bal4 balances of the converged state (tr_apply's history rows, bs_final)
+            SideScanArgs SF = SA;
+            SF.gate = PassGate{c->pc + 2 * PC_RING, c->counters + CNT_RESORT, 0, 1};  // open, full
+            SF.cfail = c->st[0].cfail;
+            SF.cfail_alt = c->st[1].cfail;
+            SF.cfail_clear = nullptr;
+            SF.epi = c->counters + EPI_WORD;
+            side_scan_fused(SF, m, inv_acc, c->tstart, c->counters + CNT_LONG, c->T.acc, c->bb, s);
+        }
         epilogue(m);
         prof_mark(c, PH_END);
         HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, (PC_OFF + PC_RING) * sizeof(u32), hipMemcpyDeviceToHost,

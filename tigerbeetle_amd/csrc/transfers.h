@@ -63,6 +63,7 @@ struct TrArgs {
     u32* lst_simple;
     u32* lst_complex;
     Dirty dt;             // dirty tracking of the passes (engine.h)
+    const u128* bh;       // headroom passes: the side's balance figure (balances.hip), or null (Bal4)
     u32 debug;            // diagnostics: count changed events by kind (TBGPU_TRACE_PASSES)
     u32 probe;            // timing probes only (TBGPU_EVAL_PROBE, after convergence): 1 skip post/void, 2 no side records
     Sides sd;             // the account sides of the call's events (engine.h)

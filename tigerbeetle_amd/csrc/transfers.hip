@@ -199,8 +199,10 @@ __device__ __forceinline__ u32 classify_one(const Tables& T, const TrArgs& C, u3
             fl |= FL_POSTVOID;
             pre_e = xidx_probe(T, t.id);
             pre_p = xidx_probe(T, t.pending_id);
+            if ((u64)(t.amount >> 64) != 0) fl |= FL_WIDE;
             if (pre_p != NONE32) {
                 const Transfer& p = T.xrows[pre_p];
+                if ((u64)(p.amount >> 64) != 0) fl |= FL_WIDE;
                 u32 lg;
                 u16 af;
                 ppd = acc_find(T, p.debit_account_id, &lg, &af);
@@ -247,6 +249,7 @@ __device__ __forceinline__ u32 classify_one(const Tables& T, const TrArgs& C, u3
             gslot = gtab_find_or_insert(C, t.id, i, 0);
             if (f & (TF_BDR | TF_BCR)) fl |= FL_BALANCING;
             if (f & TF_PENDING) fl |= FL_PENDING;
+            if ((u64)(t.amount >> 64) != 0) fl |= FL_WIDE;
             if ((dfl | cfl) & (AF_DNEC | AF_CNED)) fl |= FL_LIMITS;
             if ((dfl | cfl) & AF_HISTORY) fl |= FL_HISTORY;
         }
@@ -280,7 +283,8 @@ __device__ __forceinline__ u32 classify_one(const Tables& T, const TrArgs& C, u3
 
 __global__ void tr_classify(Tables T, TrArgs C) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    const u32 fl = block_or(i < C.n ? classify_one(T, C, i) : 0u);
+    u32 fl = block_or(i < C.n ? classify_one(T, C, i) : 0u);
+    if (i == 0 && *T.big) fl |= FL_WIDE;  // a committed balance near 2^128
     if (threadIdx.x == 0 && fl) atomicOr(&C.counters[CNT_FLAGS], fl);
 }
 
@@ -534,6 +538,35 @@ __device__ __forceinline__ u8 eval_balances(const EvCore& t, const Bal4& dr, con
     return TBGPU_CREATE_TRANSFER_OK;
 }
 
+// The same tail in headroom form (balances.hip side_scan_fused_narrow), for passes of a
+// chunk whose amounts are < 2^64 and whose committed balances are < 2^126 (FL_WIDE
+// clear): then no overflow check can fire (a balance moves by < 2^84 inside a chunk),
+// and the limit and balancing checks read hd = dr.credits_posted - dr.debits_pending -
+// dr.debits_posted and hc = cr.debits_posted - cr.credits_pending - cr.credits_posted.
+__device__ __forceinline__ u8 eval_balances_narrow(const EvCore& t, u128 hd, u128 hc, u128* amount_out) {
+    typedef __int128 i128;
+    const u16 f = t.flags;
+    const u16 dr_flags = t.aflags & 0xF, cr_flags = t.aflags >> 4;
+    const i128 sd = (i128)hd, sc = (i128)hc;
+    u128 amount = t.amount;
+    if ((f & (TF_BDR | TF_BCR)) && amount == 0) amount = (u128)0xFFFFFFFFFFFFFFFFull;  // maxInt(u64)
+    if (f & TF_BDR) {
+        const u128 avail = sd > 0 ? (u128)sd : 0;  // cpo -| (dp + dpo)
+        if (avail < amount) amount = avail;
+        if (amount == 0) return TBGPU_CREATE_TRANSFER_EXCEEDS_CREDITS;
+    }
+    if (f & TF_BCR) {
+        const u128 avail = sc > 0 ? (u128)sc : 0;
+        if (avail < amount) amount = avail;
+        if (amount == 0) return TBGPU_CREATE_TRANSFER_EXCEEDS_DEBITS;
+    }
+    if (sum_overflows64(t.ts, (u64)t.timeout * NS_PER_S)) return TBGPU_CREATE_TRANSFER_OVERFLOWS_TIMEOUT;
+    if ((dr_flags & AF_DNEC) && (i128)amount > sd) return TBGPU_CREATE_TRANSFER_EXCEEDS_CREDITS;
+    if ((cr_flags & AF_CNED) && (i128)amount > sc) return TBGPU_CREATE_TRANSFER_EXCEEDS_DEBITS;
+    *amount_out = amount;
+    return TBGPU_CREATE_TRANSFER_OK;
+}
+
 // What event j's effects look like to a later event of chain csi (execute's scopes,
 // src/state_machine.zig:1018-1083): evaluated inside the same open chain, final
 // (chain persisted) outside it.
@@ -552,23 +585,44 @@ __device__ __forceinline__ bool fin_ok(const TrArgs& C, const EvalState& S, u32 
 // pending resolved to an event with other accounts) asks the host to re-sort.
 __device__ __forceinline__ bool write_sides(const TrArgs& C, u32 i, bool pv, bool ok, u32 pref, u128 dpe, u128 dpo);
 
+// DUE: the pass's dirty check (Dirty) is made here, after the event's own words are
+// issued, so that a due event's loads are already in flight when the check resolves.
+template <bool DUE = false>
 __device__ __forceinline__ bool evaluate_one(const Tables& T, const TrArgs& C, const EvalState& S,
                                              const EvalState& D, const Bal4* __restrict__ bb, const PassGate& g,
                                              u32 i) {
     // Everything a regular transfer reads is issued up front, unconditionally (the
     // indices are valid for every event; unused values are dropped): one memory
-    // round trip for the event's records, one for its two balances.
+    // round trip for the event's records, one for its two balances.  A post/void's
+    // pending references are issued in the same round.
     const u8 sr = C.sres[i];
     const u32 csi = C.cs[i];
     const EvCore k = C.core[i];
-    if ((C.probe & 1) && (k.flags & (TF_POST | TF_VOID))) return false;
     const u32 pid = C.prev_id[i], pre_e = C.pre_e[i];
     const uint2 ep = C.sd.epos[i];
     const u8 s_res = S.res[i];
     const u128 s_amt = S.amt[i], s_pamt = S.pamt[i];
     const u32 s_pref = S.pref[i];
-    const Bal4 bd = bb[ep.x];
-    const Bal4 bc = bb[ep.y];
+    const u32 pl = C.pend_last[i], pp = C.pre_p[i], pvp = C.prev_pend[i];
+    if (DUE) {
+        const u32 cei = C.ce[i], q = g.p, par = q & 1;
+        bool is_due = g.full || C.dt.ev[par * C.dt.n + i] == q || *C.dt.all == q;
+        if (!is_due && csi != cei) is_due = C.dt.chain[par * C.dt.n + csi] == q;
+        if (!is_due) {
+            if (i == csi && csi != cei) D.cfail[csi] = S.cfail[csi];
+            return false;
+        }
+    }
+    if ((C.probe & 1) && (k.flags & (TF_POST | TF_VOID))) return false;
+    Bal4 bd, bc;
+    u128 hd = 0, hc = 0;
+    if (C.bh) {
+        hd = C.bh[ep.x];
+        hc = C.bh[ep.y];
+    } else {
+        bd = bb[ep.x];
+        bc = bb[ep.y];
+    }
     u8 res;
     u128 amt = 0, pamt = 0, dpe = 0, dpo = 0;
     u32 pref = NONE32;
@@ -591,7 +645,7 @@ __device__ __forceinline__ bool evaluate_one(const Tables& T, const TrArgs& C, c
                 res = TBGPU_CREATE_TRANSFER_LINKED_EVENT_FAILED;
             } else {
                 u128 amount = 0;
-                res = eval_balances(k, bd, bc, &amount);
+                res = C.bh ? eval_balances_narrow(k, hd, hc, &amount) : eval_balances(k, bd, bc, &amount);
                 if (res == TBGPU_CREATE_TRANSFER_OK) {
                     amt = amount;
                     if (k.flags & TF_PENDING) dpe = amount; else dpo = amount;
@@ -605,7 +659,6 @@ __device__ __forceinline__ bool evaluate_one(const Tables& T, const TrArgs& C, c
             // of a walk of dependent loads.  The walks below stay for the other cases.
             Transfer t = C.ev[i];
             t.timestamp = k.ts;
-            const u32 pl = C.pend_last[i], pp = C.pre_p[i], pvp = C.prev_pend[i];
             const bool pl_v = pl != NONE32, pp_v = pp != NONE32, pvp_v = pvp != NONE32;
             const u32 pl_cs = pl_v ? C.cs[pl] : 0u, pl_ce = pl_v ? C.ce[pl] : 0u;
             const u8 pl_ok = pl_v ? S.ok[pl] : 0;
@@ -781,12 +834,7 @@ __global__ __launch_bounds__(LS_THREADS) void tr_lists(TrArgs C) {
 // first pass and after a side rebuild; otherwise an event whose balances moved (the
 // scan marked it), that changed last pass, whose chain has a member that is, or (the
 // scan's resolve step) whose id / pending group moved.
-__device__ __forceinline__ bool due(const TrArgs& C, const PassGate& g, u32 i, u32 cs, u32 ce) {
-    if (g.full) return true;
-    const u32 q = g.p, par = q & 1;
-    if (*C.dt.all == q) return true;
-    return C.dt.ev[par * C.dt.n + i] == q || (cs != ce && C.dt.chain[par * C.dt.n + cs] == q);
-}
+// (evaluated inline by eval_simple_one and evaluate_one<true>, with the event's loads in flight)
 
 // What reads event j's outcome: the scan windows of its sides (every candidate pair of
 // a post/void), and the complex events keyed by its id or its pending id (later
@@ -826,46 +874,63 @@ __device__ __forceinline__ void mark_changed(const TrArgs& C, u32 i, u32 q) {
 // without its post/void and `exists` work (most of a pass's events are here).
 __device__ __forceinline__ bool eval_simple_one(const TrArgs& C, const EvalState& S, const EvalState& D,
                                                 const Bal4* __restrict__ bb, const PassGate& g, u32 i) {
-    bool changed = false;
-    {
-        const u8 sr = C.sres[i];
-        const u32 csi = C.cs[i], cei = C.ce[i];
-        if (!due(C, g, i, csi, cei)) {
-            // outcome unchanged in both buffers; a chain nobody re-evaluates keeps its
-            // first failure (the scan reset the next state's)
-            if (i == csi && csi != cei) D.cfail[csi] = S.cfail[csi];
-        } else if (sr != SRES_DYN) {  // a static failure inside a chain
-            D.res[i] = sr;
-            D.ok[i] = 0;
-            D.amt[i] = 0;
+    // The event's own words and its due stamp in one round of loads (most events are
+    // due in the early passes, which dominate), the chain stamp and the balances in a
+    // second: two memory round trips before the evaluation instead of four.
+    const u32 q = g.p, par = q & 1;
+    const u8 sr = C.sres[i];
+    const u32 csi = C.cs[i], cei = C.ce[i];
+    const u32 dte = g.full ? q : C.dt.ev[par * C.dt.n + i];
+    const EvCore e = C.core[i];
+    const uint2 ep = C.sd.epos[i];
+    const u8 s_res = S.res[i];
+    const u128 s_amt = S.amt[i];
+    bool is_due = g.full || dte == q || *C.dt.all == q;
+    if (!is_due && csi != cei) is_due = C.dt.chain[par * C.dt.n + csi] == q;
+    if (!is_due) {
+        // outcome unchanged in both buffers; a chain nobody re-evaluates keeps its
+        // first failure (the scan reset the next state's)
+        if (i == csi && csi != cei) D.cfail[csi] = S.cfail[csi];
+        return false;
+    }
+    // (pamt and pref of a simple event are zero / none in both buffers after tr_init and
+    // pass 0: later passes leave them)
+    if (sr != SRES_DYN) {  // a static failure inside a chain
+        D.res[i] = sr;
+        D.ok[i] = 0;
+        D.amt[i] = 0;
+        if (q == 0) {
             D.pamt[i] = 0;
             D.pref[i] = NONE32;
-            atomicMin(&D.cfail[csi], i);
-        } else {
-            const EvCore e = C.core[i];
-            const uint2 ep = C.sd.epos[i];
-            const u8 s_res = S.res[i];
-            const u128 s_amt = S.amt[i];
-            const Bal4 bd = bb[ep.x], bc = bb[ep.y];
-            u128 amount = 0;
-            const u8 res = eval_balances(e, bd, bc, &amount);
-            const bool ok = res == TBGPU_CREATE_TRANSFER_OK;
-            const u128 amt = ok ? amount : 0;
-            D.res[i] = res;
-            D.ok[i] = ok ? 1 : 0;
-            D.amt[i] = amt;
-            D.pamt[i] = 0;
-            D.pref[i] = NONE32;
-            if (!ok && csi != C.ce[i]) atomicMin(&D.cfail[csi], i);
-            changed = res != s_res || amt != s_amt;
-            if (changed) {
-                const u128 dpe = ok && (e.flags & TF_PENDING) ? amt : 0, dpo = ok && !(e.flags & TF_PENDING) ? amt : 0;
-                C.sd.sq_ok[ep.x] = C.sd.sq_ok[ep.y] = ok ? 1 : 0;
-                C.sd.sq_dpend[ep.x] = C.sd.sq_dpend[ep.y] = dpe;
-                C.sd.sq_dpost[ep.x] = C.sd.sq_dpost[ep.y] = dpo;
-                mark_changed(C, i, g.p);
-            }
         }
+        atomicMin(&D.cfail[csi], i);
+        return false;
+    }
+    u128 amount = 0;
+    u8 res;
+    if (C.bh) {
+        res = eval_balances_narrow(e, C.bh[ep.x], C.bh[ep.y], &amount);
+    } else {
+        const Bal4 bd = bb[ep.x], bc = bb[ep.y];
+        res = eval_balances(e, bd, bc, &amount);
+    }
+    const bool ok = res == TBGPU_CREATE_TRANSFER_OK;
+    const u128 amt = ok ? amount : 0;
+    D.res[i] = res;
+    D.ok[i] = ok ? 1 : 0;
+    D.amt[i] = amt;
+    if (q == 0) {
+        D.pamt[i] = 0;
+        D.pref[i] = NONE32;
+    }
+    if (!ok && csi != cei) atomicMin(&D.cfail[csi], i);
+    const bool changed = res != s_res || amt != s_amt;
+    if (changed) {
+        const u128 dpe = ok && (e.flags & TF_PENDING) ? amt : 0, dpo = ok && !(e.flags & TF_PENDING) ? amt : 0;
+        C.sd.sq_ok[ep.x] = C.sd.sq_ok[ep.y] = ok ? 1 : 0;
+        C.sd.sq_dpend[ep.x] = C.sd.sq_dpend[ep.y] = dpe;
+        C.sd.sq_dpost[ep.x] = C.sd.sq_dpost[ep.y] = dpo;
+        mark_changed(C, i, q);
     }
     return changed;
 }
@@ -875,14 +940,8 @@ __device__ __forceinline__ bool eval_complex_one(const Tables& T, const TrArgs& 
                                                  const EvalState& D, const Bal4* __restrict__ bb, const PassGate& g,
                                                  u32 k, u32& i) {
     i = C.lst_complex[k];
-    const u32 csi = C.cs[i], cei = C.ce[i];
-    bool changed = false;
-    if (due(C, g, i, csi, cei)) {
-        changed = evaluate_one(T, C, S, D, bb, g, i);
-        if (changed) mark_changed(C, i, g.p);
-    } else if (i == csi && csi != cei) {
-        D.cfail[csi] = S.cfail[csi];
-    }
+    const bool changed = evaluate_one<true>(T, C, S, D, bb, g, i);
+    if (changed) mark_changed(C, i, g.p);
     return changed;
 }
 
@@ -1655,6 +1714,7 @@ __global__ void tr_prep(TrArgs C, u32* cfail0, u32* pc, u32 ring) {
             pc[k] = k == 0 ? 1u : 0u;
             pc[ring + k] = NONE32;
         }
+        if (k == 0) pc[2 * ring] = 1;  // an open gate (the full scans after a headroom fixed point, the walk)
         if (k < CNT_COUNT) C.counters[k] = 0;
     }
 }

@@ -443,6 +443,22 @@ int tbgpu_route_unpack_packed(tbgpu_ctx* ctx, const void* packed_device, uint64_
 int tbgpu_route_unpack(tbgpu_ctx* ctx, const void* records_device, uint64_t count, const void* ts_base_device,
                        uint64_t batches, void* timestamps_device);
 
+/* The general step's id directory (tigerbeetle_amd/shard_vec.py round_vec), on the
+ * device.  `records_device`: `count` rows of five int64 (position in the step's global
+ * order, kind 0 id / 1 pending id, key lo, key hi, route hint), all ranks' records
+ * all-gathered.  _owners writes, per record, the owner (ledger % world) of this shard's
+ * committed transfer with that key, or -1; the caller all-reduces them (MAX) over the
+ * ranks.  tbgpu_route_directory then writes three int64 per record: its type (0 new,
+ * 1 exists, 2 repeat, 3 pending found, 4 pending none, 5 pending created earlier by an
+ * event that may land anywhere), its hint (the owner, or the first record's hint), and
+ * the earliest position among the key's records of ids not committed (INT64_MAX: none).
+ * The types follow src/state_machine.zig:1284 (exists) and :1409-1428 (the pending's
+ * lookup); the key grouping is a hash table, not a sort.  Synchronous; 0, or -22. */
+int tbgpu_route_directory_owners(tbgpu_ctx* ctx, uint32_t world, const void* records_device, uint64_t count,
+                                 void* owners_device);
+int tbgpu_route_directory(tbgpu_ctx* ctx, const void* records_device, const void* owners_device, uint64_t count,
+                          void* out_device);
+
 /* Copy committed transfers of another shard into this ctx's transfer table and id
  * index, without balance or posted effects: the `exists` comparisons of
  * :1370-1389 / :1500-1561 then see a colliding id committed elsewhere.  Returns 0. */

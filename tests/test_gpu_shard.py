@@ -182,3 +182,75 @@ def test_route_stats_matches_numpy():
                 assert asum == want % (1 << 128), world
     finally:
         eng.close()
+
+
+@pytest.mark.gpu
+def test_route_directory_matches_the_host_form():
+    """tbgpu_route_directory_owners + tbgpu_route_directory (csrc/directory.hip, the
+    general step's directory on the device) against shard_vec's host form of the same
+    rule (a stable sort by key): committed ids and pendings (owner = ledger % world),
+    ids first seen in the step and their repeats, pendings created earlier in the step
+    with each kind of route hint, unknown pendings, u128 keys."""
+    import numpy as np
+    import torch
+
+    from tigerbeetle_amd import workload
+    from tigerbeetle_amd.engine import Engine
+    from tigerbeetle_amd.shard_vec import ANY, DUP, EXISTS, INF, NEW, PEND, PEND_HAZARD, PEND_NONE, PV
+    from tigerbeetle_amd.types import TRANSFER_DTYPE
+    rng = np.random.default_rng(11)
+    W = 3
+    eng = Engine(device=0, accounts_max=64, transfers_max=4096, history_max=16, events_per_call_max=1 << 12)
+    try:
+        ids = np.arange(1, 61, dtype=np.uint64)
+        eng.create_accounts(10, workload.make_accounts(ids, ledger=(ids - 1) // 10 + 1))
+        k = 500
+        t = np.zeros(k, dtype=TRANSFER_DTYPE)
+        t["id_lo"] = np.arange(1000, 1000 + k)
+        led = rng.integers(1, 7, k)
+        t["debit_account_id_lo"] = (led - 1) * 10 + 1 + rng.integers(0, 5, k)
+        t["credit_account_id_lo"] = (led - 1) * 10 + 6 + rng.integers(0, 5, k)
+        t["amount_lo"] = 1
+        t["ledger"] = led
+        t["code"] = 1
+        assert len(eng.create_transfers(1000, t)) == 0
+        committed = {1000 + j: int(led[j]) % W for j in range(k)}
+        # the step's records: ids (kind 0, unique positions) and pending ids (kind 1)
+        n = 3000
+        pool = np.concatenate([np.arange(1000, 1500), np.arange(5000, 5300), [2**64 + 7, 2**65 + 9]]).astype(object)
+        key = [int(pool[j]) for j in rng.integers(0, len(pool), n)]
+        kind = rng.integers(0, 2, n)
+        pos = np.where(kind == 0, np.arange(n) * 2, rng.integers(0, 2 * n, n)).astype(np.int64)
+        hint = rng.choice([ANY, PV, 0, 1, 2], n).astype(np.int64)
+        R = np.zeros((n, 5), dtype=np.int64)
+        R[:, 0], R[:, 1], R[:, 4] = pos, kind, hint
+        R[:, 2] = np.array([x & (2**64 - 1) for x in key], dtype=np.uint64).view(np.int64)
+        R[:, 3] = np.array([x >> 64 for x in key], dtype=np.uint64).view(np.int64)
+        dev = torch.device("cuda", 0)
+        A = torch.from_numpy(R).to(dev)
+        owners = torch.empty(n, dtype=torch.int64, device=dev)
+        eng.route_directory_owners(W, A, owners)
+        out = torch.empty((n, 3), dtype=torch.int64, device=dev)
+        eng.route_directory(A, owners, out)
+        got = out.cpu().numpy()
+        cown = np.array([committed.get(x, -1) for x in key], dtype=np.int64)
+        assert np.array_equal(owners.cpu().numpy(), cown)
+        # the host form (shard_vec._directory_host) on the same records
+        k0 = kind == 0
+        cand = k0 & (cown < 0)
+        first_p, first_h = {}, {}
+        for j in np.argsort(pos, kind="stable"):
+            if cand[j] and key[j] not in first_p:
+                first_p[key[j]], first_h[key[j]] = int(pos[j]), int(hint[j])
+        fP = np.array([first_p.get(x, INF) for x in key], dtype=np.int64)
+        fH = np.array([first_h.get(x, ANY) for x in key], dtype=np.int64)
+        isfirst = cand & (pos == fP)
+        typ = np.where(k0, np.where(cown >= 0, EXISTS, np.where(isfirst, NEW, DUP)),
+                       np.where(cown >= 0, PEND, np.where(fP < pos, np.where((fH == ANY) | (fH == PV), PEND_HAZARD,
+                                                                              PEND), PEND_NONE)))
+        assert np.array_equal(got[:, 0], typ)
+        assert np.array_equal(got[:, 1], np.where(cown >= 0, cown, fH))
+        assert np.array_equal(got[:, 2], fP)
+        assert {int(x) for x in typ} >= {NEW, DUP, EXISTS, PEND, PEND_NONE, PEND_HAZARD}
+    finally:
+        eng.close()

@@ -395,6 +395,10 @@ enum {
     CNT_ALL = 24,       // general path: the pass at which every event is evaluated (Dirty::all)
     CNT_COUNT = 25,
 };
+// A call's report in host memory (k_report, or fp_tail's last phase): counters, then the
+// device cursors, then the reply count of each batch (words).
+constexpr u32 RPT_BASE = CNT_COUNT, RPT_COUNTS = CNT_COUNT + 8;
+
 enum {
     FL_CHAINS = 1u << 0,      // some event is in a linked chain
     FL_POSTVOID = 1u << 1,    // some post/void passed static validation

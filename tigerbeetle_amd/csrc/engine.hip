@@ -249,7 +249,6 @@ constexpr u32 PASS_GROUP_MAX = 48;   // passes enqueued between two host round t
 // passes cost O(n) each and the walk O(1) per event.
 constexpr u32 WALK_PASSES = 64;
 constexpr u32 WALK_UNDO = 4 * 8192;   // a linked chain's balance moves (<= 2 per member, members <= a batch)
-constexpr u32 RPT_BASE = CNT_COUNT, RPT_COUNTS = CNT_COUNT + 8;  // k_report's layout (words)
 constexpr u32 PC_OFF = 32;           // the pass-change ring's offset behind the counter words
 static_assert(PC_OFF >= CNT_COUNT, "counter words overlap the pass-change ring");
 constexpr u32 EPI_WORD = 28;         // the apply kernels' gate (TrArgs::epi), between the counters and the ring
@@ -334,6 +333,11 @@ struct tbgpu_ctx {
     u32* ro_bcount = nullptr;  // [256] spanning counts per owner, then [world * batches] per (owner, batch)
     u64 ro_bc_cap = 0;
     u64* ro_spart = nullptr;  // rt_rank's per-workgroup eligibility records
+    // the general step's device directory (directory.hip), grown on demand
+    u64 rd_cap = 0;
+    u32* rd_claim = nullptr;
+    int64_t* rd_first = nullptr;  // [2 * table]: first positions, then their hints
+    u32* rd_slot = nullptr;
     struct {
         const void* events;
         u64 n;
@@ -351,6 +355,10 @@ struct tbgpu_ctx {
     // a fast attempt enqueued without its round trip (try_fast spec): settled at the
     // call's next wait (spec_settle), undone there if it fell back
     bool spec_pending = false;
+    // a one-chunk call's report written by fp_tail (try_fast's small speculative path)
+    // instead of k_report: requested per call by transfers_batches, done when set
+    bool rep_want = false, rep_done = false;
+    u64* rep_replies_out = nullptr;
     FastArgs spec_F{};
     u32 last_passes = 8;  // passes the last fixed point took (sizes the next pass group)
     bool long_segments = false;  // this call has an account segment too long for the fused scan
@@ -654,7 +662,8 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     // Free every device allocation by walking the struct's pointers.
     guard_check_all(c->stream);
     for (void* p : {(void*)c->ro_orank, (void*)c->ro_blk, (void*)c->ro_bstart, (void*)c->ro_counts,
-                    (void*)c->ro_bcount, (void*)c->ro_spart})
+                    (void*)c->ro_bcount, (void*)c->ro_spart, (void*)c->rd_claim, (void*)c->rd_first,
+                    (void*)c->rd_slot})
         if (p) { guard_release(p); (void)hipFree(p); }
     void* ptrs[] = {c->T.dense, c->T.acc, c->T.aidx, c->T.xrows, c->T.xful, c->T.xidx, c->T.hrows, c->T.commit_ts, c->T.idr, c->T.xrun, c->T.big, c->ev_buf,
                     c->b_start, c->ts, c->cs, c->ce, c->sres, c->dslot, c->cslot, c->pre_e, c->pre_p,
@@ -933,11 +942,17 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_crea
     if (n <= FP_TAIL_MAX && !no_tail) {
         // a small call: index, fix and advance in one workgroup, gated on the device's
         // flags like the speculative launches below
+        if (spec && c->rep_want) {  // the call's report from fp_tail's last phase (no k_report)
+            F.rep_out = c->h_report_dev;
+            F.rep_replies = (const u64*)c->res_buf;
+            F.rep_replies_out = c->rep_replies_out;
+            c->rep_done = true;
+        }
         fp_launch_tail(c->T, F, s);
         prof_mark(c, PH_END);
         c->stats.path = 1;
         c->stats.iterations = 1;
-        if (spec) {  // the flags come back with the call's k_report
+        if (spec) {  // the flags come back with the call's report
             c->spec_F = F;
             c->spec_pending = true;
             return true;
@@ -1500,6 +1515,11 @@ static void d2h(tbgpu_ctx* c, void* dst, const void* src, u64 bytes, hipStream_t
     }
 }
 
+static bool tail_report_disabled() {  // TBGPU_NO_TAIL_REPORT=1: k_report after fp_tail (A/B timing)
+    static const bool d = getenv("TBGPU_NO_TAIL_REPORT") != nullptr;
+    return d;
+}
+
 static bool spec_disabled() {
     static const bool d = getenv("TBGPU_NO_SPEC") != nullptr;
     return d;
@@ -1599,8 +1619,12 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         // decides whether it stands: that answer comes with the call's final wait
         const bool spec = try_fast_path && !c->rt_dry && b0 == 0 && b1 == nb_total &&
                           !(c->opt.flags & TBGPU_OPT_FORCE_GENERAL) && !spec_disabled();
+        c->rep_want = spec && !tail_report_disabled();
+        c->rep_done = false;
+        c->rep_replies_out = dst_device ? nullptr : c->h_res_dev;
         const bool stood = run_transfers_chunk(c, ev, n, nb, rdev, try_fast_path,
                                                /*split=*/!c->rt_dry && nb > general_chunk_batches(), spec);
+        c->rep_want = false;
         c->ev_in_host = false;
         if (!stood) {
             small_until = b1;  // redo these batches in small chunks, on the general path
@@ -1610,10 +1634,14 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         if (b1 == nb_total) {
             // the call's end: counters, cursors and reply counts in one copy, with the
             // replies, and one wait
-            const u32 rb = std::max<u32>((RPT_COUNTS + nb + 255) / 256, dst_device ? 1u : std::min<u32>(n / 256, 1024));
-            k_report<<<rb, 256, 0, c->stream>>>(c->counters, c->T.base, c->counts, nb, c->h_report_dev,
-                                                (const u64*)c->res_buf, dst_device ? nullptr : c->h_res_dev);
-            HIP_CHECK(hipGetLastError());
+            if (!c->rep_done) {
+                const u32 rb =
+                    std::max<u32>((RPT_COUNTS + nb + 255) / 256, dst_device ? 1u : std::min<u32>(n / 256, 1024));
+                k_report<<<rb, 256, 0, c->stream>>>(c->counters, c->T.base, c->counts, nb, c->h_report_dev,
+                                                    (const u64*)c->res_buf, dst_device ? nullptr : c->h_res_dev);
+                HIP_CHECK(hipGetLastError());
+            }
+            c->rep_done = false;
             HIP_CHECK(hipEventRecord(c->ev1, c->stream));
             wait_event(c->ev1);
             memcpy(c->h_counters, c->h_report, CNT_COUNT * sizeof(u32));
@@ -1773,6 +1801,10 @@ void route_rank(const Transfer* ev, u64 n, u32 world, uint2* orank, u32* blk, u6
                 hipStream_t stream);
 void route_unpack(const u64* rec, u64 n, const u64* ts_base, u64 batches, u64* ts, u32* error, hipStream_t stream);
 
+void route_dir_owners(const Tables& T, const void* records, u64 n, u32 world, int64_t* owner, hipStream_t stream);
+void route_dir_finish(const void* records, const int64_t* owner, u64 n, u32* claim, int64_t* first_p,
+                      int64_t* first_h, u64 g, u32* slot, int64_t* out, hipStream_t stream);
+
 static void route_capacity(tbgpu_ctx* c, u32 world, u32 batch_count, u64 n) {
     const u64 nblk = route_block_count(n);
     if (n > c->ro_cap || world * std::max<u64>(nblk, 1) > c->ro_bcap || batch_count + 1 > c->ro_cap + 2 ||
@@ -1897,6 +1929,37 @@ extern "C" int tbgpu_route_unpack(tbgpu_ctx* c, const void* records_device, uint
     d2h(c, &e, err, sizeof(u32), c->route_stream);
     wait_stream(c->route_stream);
     return e ? -22 : 0;
+}
+
+extern "C" int tbgpu_route_directory_owners(tbgpu_ctx* c, uint32_t world, const void* records_device, uint64_t count,
+                                            void* owners_device) {
+    HIP_CHECK(hipSetDevice(c->device));
+    if (world == 0) return -22;
+    route_dir_owners(c->T, records_device, count, world, (int64_t*)owners_device, c->stream);
+    wait_stream(c->stream);
+    return 0;
+}
+
+extern "C" int tbgpu_route_directory(tbgpu_ctx* c, const void* records_device, const void* owners_device,
+                                     uint64_t count, void* out_device) {
+    HIP_CHECK(hipSetDevice(c->device));
+    if (count >= 0xFFFFFFFFull) return -22;
+    const u64 g = pow2_at_least(2 * std::max<u64>(count, 8));
+    if (g > c->rd_cap) {
+        wait_stream(c->stream);
+        for (void* p : {(void*)c->rd_claim, (void*)c->rd_first, (void*)c->rd_slot})
+            if (p) { guard_release(p); HIP_CHECK(hipFree(p)); }
+        u64 b = 0;
+        ZeroOn zero_on(c->stream);
+        c->rd_cap = g;
+        c->rd_claim = dalloc<u32>(g, &b);
+        c->rd_first = dalloc<int64_t>(2 * g, &b);
+        c->rd_slot = dalloc<u32>(g / 2, &b);
+    }
+    route_dir_finish(records_device, (const int64_t*)owners_device, count, c->rd_claim, c->rd_first, c->rd_first + g,
+                     g, c->rd_slot, (int64_t*)out_device, c->stream);
+    wait_stream(c->stream);
+    return 0;
 }
 
 // max into the device scalar, ordered on the engine's stream (no host round trip)

@@ -127,6 +127,10 @@ def lib():
     L.tbgpu_route_unpack_packed.argtypes = [vp, vp, u64, u32, u32, vp, vp, vp, u64, vp, vp, vp]
     L.tbgpu_route_unpack.restype = ctypes.c_int
     L.tbgpu_route_unpack.argtypes = [vp, vp, u64, vp, u64, vp]
+    L.tbgpu_route_directory_owners.restype = ctypes.c_int
+    L.tbgpu_route_directory_owners.argtypes = [vp, u32, vp, u64, vp]
+    L.tbgpu_route_directory.restype = ctypes.c_int
+    L.tbgpu_route_directory.argtypes = [vp, vp, vp, u64, vp]
     L.tbgpu_import_transfers.restype = ctypes.c_int
     L.tbgpu_import_transfers.argtypes = [vp, vp, u32]
     L.tbgpu_advance_commit_timestamp.argtypes = [vp, u64]
@@ -398,6 +402,28 @@ class Engine:
                                         ctypes.c_void_p(timestamps.data_ptr()))
         if rc != 0:
             raise ValueError("tbgpu_route_unpack: a record names an unknown batch")
+
+    def route_directory_owners(self, world: int, records, owners) -> None:
+        """tbgpu_route_directory_owners: per record (int64 device tensor [k, 5]: position,
+        kind, key lo, key hi, hint) the owner of this shard's committed transfer with that
+        key, or -1, into `owners` (int64 device tensor [k])."""
+        import torch
+        torch.cuda.current_stream(records.device).synchronize()
+        rc = self._L.tbgpu_route_directory_owners(self._h, int(world), ctypes.c_void_p(records.data_ptr()),
+                                                  int(records.shape[0]), ctypes.c_void_p(owners.data_ptr()))
+        if rc != 0:
+            raise ValueError("tbgpu_route_directory_owners: bad arguments")
+
+    def route_directory(self, records, owners, out) -> None:
+        """tbgpu_route_directory: each record's (type, hint, first position) into `out`
+        (int64 device tensor [k, 3]), from the records and their all-reduced owners."""
+        import torch
+        torch.cuda.current_stream(records.device).synchronize()
+        rc = self._L.tbgpu_route_directory(self._h, ctypes.c_void_p(records.data_ptr()),
+                                           ctypes.c_void_p(owners.data_ptr()), int(records.shape[0]),
+                                           ctypes.c_void_p(out.data_ptr()))
+        if rc != 0:
+            raise ValueError("tbgpu_route_directory: bad arguments")
 
     def advance_commit_timestamp(self, ts: int) -> None:
         self._L.tbgpu_advance_commit_timestamp(self._h, int(ts))

@@ -108,9 +108,75 @@ def lookup_owners(sm, keys: np.ndarray) -> np.ndarray:
     return allreduce_max(sm.comm, own)
 
 
+def directory_device(sm, R: np.ndarray) -> np.ndarray | None:
+    """Collective.  The directory step of the round on the device (csrc/directory.hip),
+    when this rank's backend is the HIP engine and the step's collectives run on a GPU
+    (RCCL): every rank's records all-gathered into one device tensor, each shard's
+    committed owners (tbgpu_route_directory_owners) all-reduced, then the key grouping
+    (tbgpu_route_directory).  Returns this rank's rows (type, hint, first position), or
+    None where the host form applies (CPU ranks: the oracle backend of the CPU tests;
+    an owner map other than ledger % world)."""
+    comm = sm.comm
+    torch, dist = comm.torch, comm.dist
+    if not (hasattr(sm.backend, "route_directory") and comm.device.type == "cuda" and sm._ledger_mod):
+        return None
+    k = torch.tensor([R.shape[0]], dtype=torch.int64, device=comm.device)
+    ks = [torch.empty_like(k) for _ in range(comm.world)]
+    dist.all_gather(ks, k, group=comm.group)
+    counts = [int(x.item()) for x in ks]
+    mx = max(max(counts), 1)
+    pad = np.zeros((mx, 5), dtype=np.int64)
+    pad[:R.shape[0]] = R
+    t = torch.from_numpy(pad).to(comm.device)
+    outs = [torch.empty_like(t) for _ in range(comm.world)]
+    dist.all_gather(outs, t, group=comm.group)
+    A = torch.cat([o[:c] for o, c in zip(outs, counts)]).contiguous()
+    owners = torch.empty(A.shape[0], dtype=torch.int64, device=comm.device)
+    sm.backend.route_directory_owners(sm.world, A, owners)
+    dist.all_reduce(owners, op=dist.ReduceOp.MAX, group=comm.group)
+    out = torch.empty((A.shape[0], 3), dtype=torch.int64, device=comm.device)
+    sm.backend.route_directory(A, owners, out)
+    off = sum(counts[:comm.rank])
+    return out[off:off + R.shape[0]].cpu().numpy()
+
+
 def segment_first(starts: np.ndarray, n: int) -> np.ndarray:
     """Index of each element's segment start (starts: bool[n], starts[0] True)."""
     return np.maximum.accumulate(np.where(starts, np.arange(n), 0)) if n else np.zeros(0, np.int64)
+
+
+def _directory_host(sm, R: np.ndarray):
+    """Collective.  The directory step on the host (numpy): the same types, hints and
+    first positions as directory_device, by a stable sort of every record by key."""
+    comm = sm.comm
+    A, counts = gather_rows(comm, R)
+    keys = _hl(A[:, 2].view(np.uint64), A[:, 3].view(np.uint64))
+    order = np.argsort(keys, kind="stable")
+    ks = keys[order]
+    newk = np.ones(len(ks), dtype=bool)
+    if len(ks) > 1:
+        newk[1:] = ks[1:] != ks[:-1]
+    uid = np.empty(len(A), dtype=np.int64)
+    uid[order] = np.cumsum(newk) - 1
+    U = ks[newk]
+    cown = lookup_owners(sm, U)[uid] if len(U) else np.zeros(len(A), np.int64)
+    # the first occurrence of each key among the id records of ids not committed
+    k0 = A[:, 1] == 0
+    cand = k0 & (cown < 0)
+    firstP = np.full(len(U), INF, dtype=np.int64)
+    np.minimum.at(firstP, uid[cand], A[cand, 0])
+    firstH = np.full(len(U), ANY, dtype=np.int64)
+    isfirst = cand & (A[:, 0] == firstP[uid])
+    firstH[uid[isfirst]] = A[isfirst, 4]
+    fP, fH = firstP[uid], firstH[uid]
+    typ = np.where(k0, np.where(cown >= 0, EXISTS, np.where(isfirst, NEW, DUP)),
+                   np.where(cown >= 0, PEND, np.where(fP < A[:, 0],
+                                                       np.where((fH == ANY) | (fH == PV), PEND_HAZARD, PEND),
+                                                       PEND_NONE)))
+    ahint = np.where(cown >= 0, cown, fH)
+    off = sum(counts[:comm.rank])
+    mine_t, mine_h, mine_p = typ[off:off + len(R)], ahint[off:off + len(R)], fP[off:off + len(R)]
+    return mine_t, mine_h, mine_p
 
 
 # ----------------------------------------------------------------- round --
@@ -169,33 +235,11 @@ def round_vec(sm, glob, T, my_events, replies, start):
     R[len(r0):, 2] = plo[r1].view(np.int64)
     R[len(r0):, 3] = phi[r1].view(np.int64)
     R[len(r0):, 4] = ANY
-    A, counts = gather_rows(comm, R)
-    keys = _hl(A[:, 2].view(np.uint64), A[:, 3].view(np.uint64))
-    order = np.argsort(keys, kind="stable")
-    ks = keys[order]
-    newk = np.ones(len(ks), dtype=bool)
-    if len(ks) > 1:
-        newk[1:] = ks[1:] != ks[:-1]
-    uid = np.empty(len(A), dtype=np.int64)
-    uid[order] = np.cumsum(newk) - 1
-    U = ks[newk]
-    cown = lookup_owners(sm, U)[uid] if len(U) else np.zeros(len(A), np.int64)
-    # the first occurrence of each key among the id records of ids not committed
-    k0 = A[:, 1] == 0
-    cand = k0 & (cown < 0)
-    firstP = np.full(len(U), INF, dtype=np.int64)
-    np.minimum.at(firstP, uid[cand], A[cand, 0])
-    firstH = np.full(len(U), ANY, dtype=np.int64)
-    isfirst = cand & (A[:, 0] == firstP[uid])
-    firstH[uid[isfirst]] = A[isfirst, 4]
-    fP, fH = firstP[uid], firstH[uid]
-    typ = np.where(k0, np.where(cown >= 0, EXISTS, np.where(isfirst, NEW, DUP)),
-                   np.where(cown >= 0, PEND, np.where(fP < A[:, 0],
-                                                       np.where((fH == ANY) | (fH == PV), PEND_HAZARD, PEND),
-                                                       PEND_NONE)))
-    ahint = np.where(cown >= 0, cown, fH)
-    off = sum(counts[:me])
-    mine_t, mine_h, mine_p = typ[off:off + len(R)], ahint[off:off + len(R)], fP[off:off + len(R)]
+    dev = directory_device(sm, R)
+    if dev is not None:
+        mine_t, mine_h, mine_p = dev[:, 0], dev[:, 1], dev[:, 2]
+    else:
+        mine_t, mine_h, mine_p = _directory_host(sm, R)
     id_t = np.full(n, NEW, np.int64)
     id_h = np.full(n, ANY, np.int64)
     id_p = np.full(n, INF, np.int64)

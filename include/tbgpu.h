@@ -260,7 +260,15 @@ enum {
 };
 
 /* Replaces StateMachine.init/deinit (src/state_machine.zig:418-451).
- * Returns 0 on success; on failure *out is NULL and the return is a negative errno-like code. */
+ * Returns 0 on success; on failure *out is NULL and the return is a negative errno-like code.
+ *
+ * Concurrency: a ctx serves one caller at a time, as the reference's StateMachine serves
+ * its replica's one thread.  The one exception is the router's send side
+ * (tbgpu_route_stats, _prepare, _scatter, _scatter_packed, _unpack, _unpack_packed: they
+ * run on the ctx's route stream with buffers of their own), which may run on one thread
+ * while another thread commits on the same ctx (tbgpu_create_transfers_routed[_device]:
+ * tigerbeetle_amd/shard.py's pipelined stream).  Any other overlap aborts the process
+ * with "concurrent calls on one ctx" (a nested call on the same thread is allowed). */
 int  tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options);
 void tbgpu_deinit(tbgpu_ctx* ctx);
 /* StateMachine.reset (src/state_machine.zig:453): forget all state. */

@@ -70,6 +70,21 @@ inline void wait_stream(hipStream_t s) {
         if (e != hipErrorNotReady) HIP_CHECK(e);
     }
 }
+// A small call's last wait spins (hipEventQuery) instead of blocking: the blocking
+// wait's wake-up is an interrupt, ≈10-20 us on a call whose device work is ≈25 us
+// (TBGPU_BLOCKING_SMALL=1 restores it for A/B timing).
+inline void wait_event_small(hipEvent_t ev) {
+    static const bool blocking = getenv("TBGPU_BLOCKING_SMALL") != nullptr;
+    if (blocking) {
+        HIP_CHECK(hipEventSynchronize(ev));
+        return;
+    }
+    for (;;) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e == hipSuccess) return;
+        if (e != hipErrorNotReady) HIP_CHECK(e);
+    }
+}
 inline void wait_event(hipEvent_t ev) {
     if (blocking_sync()) {
         HIP_CHECK(hipEventSynchronize(ev));
@@ -354,11 +369,10 @@ struct tbgpu_ctx {
     u32 blk_words = 0;
     // a fast attempt enqueued without its round trip (try_fast spec): settled at the
     // call's next wait (spec_settle), undone there if it fell back
+    // one caller at a time (tbgpu.h "Concurrency"): main entry points, and the router's
+    // send side, which may overlap a commit (its own stream and buffers)
+    std::recursive_mutex call_mu, route_mu;
     bool spec_pending = false;
-    // a one-chunk call's report written by fp_tail (try_fast's small speculative path)
-    // instead of k_report: requested per call by transfers_batches, done when set
-    bool rep_want = false, rep_done = false;
-    u64* rep_replies_out = nullptr;
     FastArgs spec_F{};
     u32 last_passes = 8;  // passes the last fixed point took (sizes the next pass group)
     bool long_segments = false;  // this call has an account segment too long for the fused scan
@@ -416,6 +430,23 @@ struct tbgpu_ctx {
     tbgpu_stats stats{};
     char err[256] = {0};
 };
+
+// Entry guard (tbgpu.h "Concurrency"): a ctx serves one caller at a time, except that
+// the router's send side (tbgpu_route_stats / _prepare / _scatter / _scatter_packed /
+// _unpack / _unpack_packed: the route stream and buffers of their own) may run on one
+// thread while another commits on the same ctx (shard.py's pipelined stream).  Nested
+// entry on the same thread is allowed; overlapping calls otherwise abort.
+struct CallGuard {
+    std::recursive_mutex& mu;
+    CallGuard(tbgpu_ctx* c, bool route) : mu(route ? c->route_mu : c->call_mu) {
+        HIP_CHECK(hipSetDevice(c->device));
+        if (!mu.try_lock())
+            tbgpu_fatal("ctx", route ? "concurrent router calls on one ctx" : "concurrent calls on one ctx", __FILE__,
+                        __LINE__);
+    }
+    ~CallGuard() { mu.unlock(); }
+};
+
 
 static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     u64& B = c->bytes;
@@ -634,7 +665,7 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
 }
 
 extern "C" void tbgpu_reset(tbgpu_ctx* c) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, false);
     HIP_CHECK(hipMemsetAsync(c->T.aidx, 0, c->aidx_cap * sizeof(AccIdx), c->stream));
     HIP_CHECK(hipMemsetAsync(c->T.xful, 0, c->xrow_cap, c->stream));
     HIP_CHECK(hipMemsetAsync(c->T.xidx, 0, c->xidx_cap * sizeof(u32), c->stream));
@@ -942,17 +973,11 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_crea
     if (n <= FP_TAIL_MAX && !no_tail) {
         // a small call: index, fix and advance in one workgroup, gated on the device's
         // flags like the speculative launches below
-        if (spec && c->rep_want) {  // the call's report from fp_tail's last phase (no k_report)
-            F.rep_out = c->h_report_dev;
-            F.rep_replies = (const u64*)c->res_buf;
-            F.rep_replies_out = c->rep_replies_out;
-            c->rep_done = true;
-        }
         fp_launch_tail(c->T, F, s);
         prof_mark(c, PH_END);
         c->stats.path = 1;
         c->stats.iterations = 1;
-        if (spec) {  // the flags come back with the call's report
+        if (spec) {  // the flags come back with the call's k_report
             c->spec_F = F;
             c->spec_pending = true;
             return true;
@@ -1080,8 +1105,6 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
     const u64 g = C.gmask + 1;
     const u32 inv_acc = (u32)c->accounts_max;  // side keys are account rows
     const int bits_acc = log2u(c->accounts_max + 1);
-    const u32 inv_g = (u32)g;
-    const int bits_g = log2u(g + 1);
 
     u32* chg = c->pc;
     prof_mark(c, PH_CLASSIFY);
@@ -1515,11 +1538,6 @@ static void d2h(tbgpu_ctx* c, void* dst, const void* src, u64 bytes, hipStream_t
     }
 }
 
-static bool tail_report_disabled() {  // TBGPU_NO_TAIL_REPORT=1: k_report after fp_tail (A/B timing)
-    static const bool d = getenv("TBGPU_NO_TAIL_REPORT") != nullptr;
-    return d;
-}
-
 static bool spec_disabled() {
     static const bool d = getenv("TBGPU_NO_SPEC") != nullptr;
     return d;
@@ -1619,12 +1637,8 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         // decides whether it stands: that answer comes with the call's final wait
         const bool spec = try_fast_path && !c->rt_dry && b0 == 0 && b1 == nb_total &&
                           !(c->opt.flags & TBGPU_OPT_FORCE_GENERAL) && !spec_disabled();
-        c->rep_want = spec && !tail_report_disabled();
-        c->rep_done = false;
-        c->rep_replies_out = dst_device ? nullptr : c->h_res_dev;
         const bool stood = run_transfers_chunk(c, ev, n, nb, rdev, try_fast_path,
                                                /*split=*/!c->rt_dry && nb > general_chunk_batches(), spec);
-        c->rep_want = false;
         c->ev_in_host = false;
         if (!stood) {
             small_until = b1;  // redo these batches in small chunks, on the general path
@@ -1634,16 +1648,13 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         if (b1 == nb_total) {
             // the call's end: counters, cursors and reply counts in one copy, with the
             // replies, and one wait
-            if (!c->rep_done) {
-                const u32 rb =
-                    std::max<u32>((RPT_COUNTS + nb + 255) / 256, dst_device ? 1u : std::min<u32>(n / 256, 1024));
-                k_report<<<rb, 256, 0, c->stream>>>(c->counters, c->T.base, c->counts, nb, c->h_report_dev,
-                                                    (const u64*)c->res_buf, dst_device ? nullptr : c->h_res_dev);
-                HIP_CHECK(hipGetLastError());
-            }
-            c->rep_done = false;
+            const u32 rb = std::max<u32>((RPT_COUNTS + nb + 255) / 256, dst_device ? 1u : std::min<u32>(n / 256, 1024));
+            k_report<<<rb, 256, 0, c->stream>>>(c->counters, c->T.base, c->counts, nb, c->h_report_dev,
+                                                (const u64*)c->res_buf, dst_device ? nullptr : c->h_res_dev);
+            HIP_CHECK(hipGetLastError());
             HIP_CHECK(hipEventRecord(c->ev1, c->stream));
-            wait_event(c->ev1);
+            if (events + n <= FP_TAIL_MAX) wait_event_small(c->ev1);
+            else wait_event(c->ev1);
             memcpy(c->h_counters, c->h_report, CNT_COUNT * sizeof(u32));
             memcpy(c->h_base, c->h_report + RPT_BASE, 4 * sizeof(u64));
             memcpy(c->h_rc + b0, c->h_report + RPT_COUNTS, nb * sizeof(u32));
@@ -1742,7 +1753,7 @@ static uint64_t routed(tbgpu_ctx* c, uint32_t batch_count, const uint32_t* count
 }
 
 extern "C" int tbgpu_import_transfers(tbgpu_ctx* c, const tbgpu_transfer_t* rows, uint32_t count) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, false);
     if (count == 0) return 0;
     // rows already held (committed here or imported before) are skipped: rows are
     // immutable, and the id index must hold each id once
@@ -1785,7 +1796,7 @@ u64 route_block_count(u64 n);
 void route_stats(const Transfer* ev, u64 n, u64* out, hipStream_t stream);
 
 extern "C" int tbgpu_route_stats(tbgpu_ctx* c, const void* events_device, uint64_t count, uint64_t* out) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, true);
     route_stats((const Transfer*)events_device, count, c->rt_stats, c->route_stream);
     d2h(c, out, c->rt_stats, 5 * sizeof(u64), c->route_stream);
     wait_stream(c->route_stream);
@@ -1830,7 +1841,7 @@ static void route_capacity(tbgpu_ctx* c, u32 world, u32 batch_count, u64 n) {
 
 extern "C" int tbgpu_route_prepare(tbgpu_ctx* c, uint32_t world, const void* events_device, uint64_t count,
                                    uint64_t* out) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, true);
     entry_flush(c->route_stream);
     if (world == 0 || world > 256) return -22;
     route_capacity(c, world, 0, count);
@@ -1905,7 +1916,7 @@ extern "C" int tbgpu_route_unpack_packed(tbgpu_ctx* c, const void* packed_device
                                          const void* sub_batches_device, const void* batch_ts_base_device,
                                          uint64_t batches, void* events_device, void* records_device,
                                          void* timestamps_device) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, true);
     if (word_mask == 0 || (count && sub_batch_count == 0)) return -22;
     u32* err = (u32*)(c->rt_stats + 6);
     HIP_CHECK(hipMemsetAsync(err, 0, sizeof(u32), c->route_stream));
@@ -1920,7 +1931,7 @@ extern "C" int tbgpu_route_unpack_packed(tbgpu_ctx* c, const void* packed_device
 
 extern "C" int tbgpu_route_unpack(tbgpu_ctx* c, const void* records_device, uint64_t count,
                                   const void* batch_ts_base_device, uint64_t batches, void* timestamps_device) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, true);
     u32* err = (u32*)(c->rt_stats + 6);
     HIP_CHECK(hipMemsetAsync(err, 0, sizeof(u32), c->route_stream));
     route_unpack((const u64*)records_device, count, (const u64*)batch_ts_base_device, batches, (u64*)timestamps_device,
@@ -1933,7 +1944,7 @@ extern "C" int tbgpu_route_unpack(tbgpu_ctx* c, const void* records_device, uint
 
 extern "C" int tbgpu_route_directory_owners(tbgpu_ctx* c, uint32_t world, const void* records_device, uint64_t count,
                                             void* owners_device) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, false);
     if (world == 0) return -22;
     route_dir_owners(c->T, records_device, count, world, (int64_t*)owners_device, c->stream);
     wait_stream(c->stream);
@@ -1942,7 +1953,7 @@ extern "C" int tbgpu_route_directory_owners(tbgpu_ctx* c, uint32_t world, const 
 
 extern "C" int tbgpu_route_directory(tbgpu_ctx* c, const void* records_device, const void* owners_device,
                                      uint64_t count, void* out_device) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, false);
     if (count >= 0xFFFFFFFFull) return -22;
     const u64 g = pow2_at_least(2 * std::max<u64>(count, 8));
     if (g > c->rd_cap) {
@@ -1968,20 +1979,20 @@ __global__ void k_advance_commit_ts(u64* ts, u64 v) {
 }
 
 extern "C" void tbgpu_advance_commit_timestamp(tbgpu_ctx* c, uint64_t timestamp) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, false);
     k_advance_commit_ts<<<1, 64, 0, c->stream>>>(c->T.commit_ts, timestamp);
     HIP_CHECK(hipGetLastError());
 }
 
 extern "C" int tbgpu_copy_to_device(tbgpu_ctx* c, void* dst_device, const void* src_host, uint64_t bytes) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, false);
     h2d(c, dst_device, src_host, bytes, c->stream);
     wait_stream(c->stream);
     return 0;
 }
 
 extern "C" int tbgpu_prefetch_transfers(tbgpu_ctx* c, const tbgpu_transfer_t* events, uint32_t count) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, false);
     c->pf_valid = false;
     if (count > TBGPU_BATCH_MAX) return -22;
     // behind the previous commit on the ctx's stream (that commit has returned: its
@@ -1995,7 +2006,7 @@ extern "C" int tbgpu_prefetch_transfers(tbgpu_ctx* c, const tbgpu_transfer_t* ev
 }
 
 extern "C" int tbgpu_prefetch_wait(tbgpu_ctx* c) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, false);
     if (c->pf_valid) wait_event(c->pf_ev);
     return 0;
 }
@@ -2278,7 +2289,7 @@ static void check_index(tbgpu_ctx* c) {
 }
 
 extern "C" uint64_t tbgpu_compact(tbgpu_ctx* c) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, false);
     entry_flush(c->stream);
     const u64 r0 = c->q_runs.back(), r1 = c->n_rows;
     if (r1 == r0) return r1;
@@ -2356,13 +2367,13 @@ extern "C" uint32_t tbgpu_get_account_history(tbgpu_ctx* c, const tbgpu_account_
 
 extern "C" uint64_t tbgpu_get_account_transfers_device(tbgpu_ctx* c, uint32_t count, const void* filters_device,
                                                        uint32_t stride, void* out_device, uint32_t* result_counts) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, false);
     return run_queries(c, (const tbgpu_account_filter_t*)filters_device, count, stride, out_device, false, result_counts);
 }
 
 extern "C" uint64_t tbgpu_get_account_history_device(tbgpu_ctx* c, uint32_t count, const void* filters_device,
                                                      uint32_t stride, void* out_device, uint32_t* result_counts) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, false);
     return run_queries(c, (const tbgpu_account_filter_t*)filters_device, count, stride, out_device, true, result_counts);
 }
 
@@ -2403,7 +2414,7 @@ extern "C" uint64_t tbgpu_checkpoint_size(tbgpu_ctx* c) {
 }
 
 extern "C" uint64_t tbgpu_checkpoint(tbgpu_ctx* c, void* out, uint64_t capacity) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, false);
     const u64 size = tbgpu_checkpoint_size(c);
     if (capacity < size) return 0;
     wait_stream(c->stream);
@@ -2452,7 +2463,7 @@ extern "C" uint64_t tbgpu_checkpoint(tbgpu_ctx* c, void* out, uint64_t capacity)
 }
 
 extern "C" int tbgpu_open(tbgpu_ctx* c, const void* image, uint64_t size) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, false);
     if (size < sizeof(CkHeader)) return -22;
     CkHeader h;
     memcpy(&h, image, sizeof h);
@@ -2517,7 +2528,7 @@ static u128 to128(tbgpu_uint128_t x) { return ((u128)x.hi << 64) | x.lo; }
 
 extern "C" int tbgpu_test_set_balances(tbgpu_ctx* c, tbgpu_uint128_t id, tbgpu_uint128_t dp, tbgpu_uint128_t dpo,
                                        tbgpu_uint128_t cp, tbgpu_uint128_t cpo) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, false);
     Bal4 b{to128(dp), to128(dpo), to128(cp), to128(cpo)};
     launch_set_balances(c->T, to128(id), b, c->status, c->stream);
     int st = 0;
@@ -2527,7 +2538,7 @@ extern "C" int tbgpu_test_set_balances(tbgpu_ctx* c, tbgpu_uint128_t id, tbgpu_u
 }
 
 extern "C" int tbgpu_get_posted(tbgpu_ctx* c, tbgpu_uint128_t pending_id) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, false);
     launch_get_posted(c->T, to128(pending_id), c->status, c->stream);
     int st = 0;
     d2h(c, &st, c->status, sizeof(int), c->stream);
@@ -2540,7 +2551,7 @@ extern "C" uint64_t tbgpu_transfer_count(tbgpu_ctx* c) { return c->n_rows; }
 extern "C" uint64_t tbgpu_history_count(tbgpu_ctx* c) { return c->n_hist; }
 
 extern "C" uint64_t tbgpu_export_transfers(tbgpu_ctx* c, uint64_t first, uint64_t count, tbgpu_transfer_t* out) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, false);
     if (first >= c->n_rows) return 0;
     count = std::min<u64>(count, c->n_rows - first);
     wait_stream(c->stream);  // the blocking copy (null stream) does not wait for the ctx's stream
@@ -2549,7 +2560,7 @@ extern "C" uint64_t tbgpu_export_transfers(tbgpu_ctx* c, uint64_t first, uint64_
 }
 
 extern "C" uint64_t tbgpu_export_history(tbgpu_ctx* c, uint64_t first, uint64_t count, tbgpu_account_history_t* out) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, false);
     if (first >= c->n_hist) return 0;
     count = std::min<u64>(count, c->n_hist - first);
     wait_stream(c->stream);  // the blocking copy (null stream) does not wait for the ctx's stream
@@ -2558,7 +2569,7 @@ extern "C" uint64_t tbgpu_export_history(tbgpu_ctx* c, uint64_t first, uint64_t 
 }
 
 extern "C" uint64_t tbgpu_export_accounts(tbgpu_ctx* c, tbgpu_account_t* out, uint64_t capacity) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, false);
     const u64 n = std::min<u64>(capacity, c->n_accounts);  // dense rows, creation order
     wait_stream(c->stream);  // the blocking copy (null stream) does not wait for the ctx's stream
     if (n) d2h(c, out, c->T.acc, n * sizeof(Account), c->stream);
@@ -2566,7 +2577,7 @@ extern "C" uint64_t tbgpu_export_accounts(tbgpu_ctx* c, tbgpu_account_t* out, ui
 }
 
 extern "C" uint64_t tbgpu_commit_timestamp(tbgpu_ctx* c) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, false);
     u64 v = 0;  // behind whatever the engine's stream still has queued (tbgpu_advance_commit_timestamp)
     d2h(c, &v, c->T.commit_ts, sizeof(u64), c->stream);
     wait_stream(c->stream);

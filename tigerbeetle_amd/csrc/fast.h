@@ -26,11 +26,6 @@ struct FastArgs {
     u64* commit_ts;     // commit_timestamp sink (T.commit_ts, or a scratch word when dry)
     u32 dry;            // dry run: replies only, no state change
     Transfer* ev_copy;  // ev is in host memory (zero copy): fp_commit leaves an HBM copy here, or null
-    // fp_tail's last phase, for a call that is this one small chunk: the call's report
-    // (engine.hip k_report) in host memory, so that no launch of its own follows.  Null: none.
-    u32* rep_out;
-    const u64* rep_replies;   // the replies to copy (device), to rep_replies_out (host), or null
-    u64* rep_replies_out;
 };
 constexpr u32 TILE_WORDS = 6;
 // calls of at most FP_TAIL_MAX events run fp_launch_tail (one workgroup) instead of

@@ -1038,22 +1038,6 @@ __global__ __launch_bounds__(FP_TAIL_THREADS) void fp_tail(Tables T, FastArgs F)
         T.base[BASE_REPLIES] += fp_cnt(F, CNT_BAD);
         if (!F.dry) T.base[BASE_ROWS] += fp_cnt(F, CNT_OK);
     }
-    if (!F.rep_out) return;
-    // the call's report (k_report): its words are read past L1 (agent scope), after
-    // every store of this launch has completed
-    __threadfence();
-    __syncthreads();
-    for (u32 k = tid; k < RPT_COUNTS + F.nb; k += FP_TAIL_THREADS) {
-        const u32* src = k < RPT_BASE ? &F.counters[k]
-                       : k < RPT_COUNTS ? &((const u32*)T.base)[k - RPT_BASE] : &F.batch_counts[k - RPT_COUNTS];
-        F.rep_out[k] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (F.rep_replies_out) {
-        const u64 total = __hip_atomic_load(&T.base[BASE_REPLIES], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (u64 j = tid; j < total; j += FP_TAIL_THREADS)
-            F.rep_replies_out[j] = __hip_atomic_load(&F.rep_replies[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __threadfence_system();
 }
 
 // Exact inverse of fp_commit's effects, before the general path redoes the call:

@@ -1129,8 +1129,7 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
     tr_launch_group(C, 0, s);
     tr_launch_group2(C, s);
     tr_launch_group(C, 1, s);
-    tr_launch_init(c->T, C, c->st[0], c->st[1], s);
-    tr_launch_lists(C, s);
+    tr_launch_init_lists(c->T, C, c->st[0], c->st[1], s);
     HIP_CHECK(hipMemcpyAsync(c->h_base + 6, c->counters + CNT_NSIMPLE, 2 * sizeof(u32), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipMemcpyAsync(c->h_base + 7, c->counters + CNT_FLAGS, sizeof(u32), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipEventRecord(c->ev_lists, s));
@@ -1525,15 +1524,27 @@ static void h2d(tbgpu_ctx* c, void* dst, const void* src, u64 bytes, hipStream_t
 static void d2h(tbgpu_ctx* c, void* dst, const void* src, u64 bytes, hipStream_t s) {
     if (bytes == 0) return;
     tbgpu_ctx::UpRing& R = up_ring(c, s);
-    for (u64 off = 0; off < bytes;) {
-        const u64 k = std::min<u64>(bytes - off, UP_HALF);
-        const int h = R.next;
-        R.next ^= 1;
-        HIP_CHECK(hipEventSynchronize(R.ev[h]));
-        HIP_CHECK(hipMemcpyAsync(R.h[h], (const u8*)src + off, k, hipMemcpyDeviceToHost, s));
-        HIP_CHECK(hipEventRecord(R.ev[h], s));
-        HIP_CHECK(hipEventSynchronize(R.ev[h]));
-        memcpy((u8*)dst + off, R.h[h], k);
+    // the copy into one half runs while the host copies the other half out
+    int pend = -1;
+    u64 pend_off = 0, pend_k = 0;
+    for (u64 off = 0; off < bytes || pend >= 0;) {
+        int h = -1;
+        u64 k = 0;
+        if (off < bytes) {
+            k = std::min<u64>(bytes - off, UP_HALF);
+            h = R.next;
+            R.next ^= 1;
+            HIP_CHECK(hipEventSynchronize(R.ev[h]));  // (its previous contents were copied out)
+            HIP_CHECK(hipMemcpyAsync(R.h[h], (const u8*)src + off, k, hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipEventRecord(R.ev[h], s));
+        }
+        if (pend >= 0) {
+            HIP_CHECK(hipEventSynchronize(R.ev[pend]));
+            memcpy((u8*)dst + pend_off, R.h[pend], pend_k);
+        }
+        pend = h;
+        pend_off = off;
+        pend_k = k;
         off += k;
     }
 }

@@ -87,7 +87,7 @@ void tr_launch_group(const TrArgs& C, u32 kind, hipStream_t stream);
 void tr_launch_group2(const TrArgs& C, hipStream_t stream);
 // D: the first pass's input state; D2 (the other buffer) also receives the static
 // failures outside chains, which no pass evaluates again
-void tr_launch_init(const Tables& T, const TrArgs& C, const EvalState& D, const EvalState& D2, hipStream_t stream);
+void tr_launch_init_lists(const Tables& T, const TrArgs& C, const EvalState& D, const EvalState& D2, hipStream_t stream);
 void tr_launch_side_count(const TrArgs& C, u32 kmax, u8* mask, hipStream_t stream);
 void tr_launch_side_build(const TrArgs& C, const EvalState& S, u32 kmax, const uint4* pairs, u32 invalid, u32* skey,
                           u32* sval, hipStream_t stream);
@@ -97,7 +97,6 @@ void tr_launch_evaluate(const Tables& T, const TrArgs& C, const EvalState& S, co
                         const PassGate& g, u32* chg, u32* chg_next, u32* front, u32* front_next, hipStream_t stream);
 // One pass over the work lists (tr_lists): the simple list's kernel, then evaluate_one
 // over the complex list (counts from the host's copy of CNT_NSIMPLE / CNT_NCOMPLEX).
-void tr_launch_lists(const TrArgs& C, hipStream_t stream);
 void tr_launch_evaluate_lists(const Tables& T, const TrArgs& C, const EvalState& S, const EvalState& D, const Bal4* bb,
                               const PassGate& g, u32* chg, u32* chg_next, u32* front, u32* front_next, u32 n_simple,
                               u32 n_complex, hipStream_t stream);

@@ -795,12 +795,15 @@ __global__ void tr_evaluate(Tables T, TrArgs C, EvalState S, EvalState D, const 
 // The per-pass work lists (TrArgs::lst_simple / lst_complex), in event order within a
 // 1024-event block; one cursor atomic per block and list (one per wave was 2.5k
 // same-address atomics per 164k-event chunk, serialized at the memory side: 60 us).
+__device__ __forceinline__ void init_one(const Tables& T, const TrArgs& C, const EvalState& D, const EvalState& D2,
+                                         u32 i);
 constexpr u32 LS_THREADS = 1024;
-__global__ __launch_bounds__(LS_THREADS) void tr_lists(TrArgs C) {
+__global__ __launch_bounds__(LS_THREADS) void tr_lists(Tables T, TrArgs C, EvalState D, EvalState D2) {
     __shared__ u32 s_cnt[2][LS_THREADS / 64];
     __shared__ u32 s_base[2];
     const u32 i = blockIdx.x * LS_THREADS + threadIdx.x;
-    u32 cls = 0;  // 0 final after tr_init, 1 simple, 2 complex
+    if (i < C.n) init_one(T, C, D, D2, i);  // the initial state (one launch with the lists)
+    u32 cls = 0;  // 0 final after the initial state, 1 simple, 2 complex
     if (i < C.n) {
         const u8 sr = C.sres[i];
         if (sr != SRES_DYN) cls = C.cs[i] != C.ce[i] ? 1 : 0;
@@ -990,9 +993,8 @@ __device__ __forceinline__ u32 pending_guess(const TrArgs& C, u32 i) {
 // Starting point: every statically valid event succeeds, except that an id already
 // committed, or seen earlier in the call, answers `exists` (the first event with an
 // id is the one that succeeds), and a post/void resolves to its likeliest pending.
-__global__ void tr_init(Tables T, TrArgs C, EvalState D, EvalState D2) {
-    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= C.n) return;
+__device__ __forceinline__ void init_one(const Tables& T, const TrArgs& C, const EvalState& D, const EvalState& D2,
+                                         u32 i) {
     if (C.sres[i] != SRES_DYN && C.cs[i] == C.ce[i]) {
         // a static failure outside any chain: final, on no work list; both state
         // buffers hold it for every pass
@@ -1008,7 +1010,7 @@ __global__ void tr_init(Tables T, TrArgs C, EvalState D, EvalState D2) {
     u8 sr = C.sres[i];
     if (sr == SRES_DYN && (C.prev_id[i] != NONE32 || C.pre_e[i] != NONE32)) sr = TBGPU_CREATE_TRANSFER_EXISTS;
     u8 res = sr;
-    u128 amt = 0, pamt = 0, dpe = 0, dpo = 0;
+    u128 amt = 0, pamt = 0;
     u32 pref = NONE32;
     if (sr == SRES_DYN) {
         const Transfer& t = C.ev[i];
@@ -1016,7 +1018,6 @@ __global__ void tr_init(Tables T, TrArgs C, EvalState D, EvalState D2) {
             res = 0;
             amt = t.amount;
             if ((t.flags & (TF_BDR | TF_BCR)) && amt == 0) amt = (u128)0xFFFFFFFFFFFFFFFFull;
-            if (t.flags & TF_PENDING) dpe = amt; else dpo = amt;
         } else {
             pref = pending_guess(C, i);
             if (pref == NONE32) {
@@ -1025,8 +1026,6 @@ __global__ void tr_init(Tables T, TrArgs C, EvalState D, EvalState D2) {
                 res = 0;
                 pamt = (pref & PREF_ROW) ? T.xrows[pref & ~PREF_ROW].amount : C.ev[pref].amount;
                 amt = t.amount > 0 ? t.amount : pamt;
-                dpe = (u128)0 - pamt;
-                dpo = (t.flags & TF_POST) ? amt : 0;
             }
         }
     }
@@ -1734,8 +1733,10 @@ void tr_launch_group(const TrArgs& C, u32 kind, hipStream_t stream) {
     tr_grp_rank<<<GRID(C.n)>>>(C, kind);
 }
 void tr_launch_group2(const TrArgs& C, hipStream_t stream) { tr_group2<<<GRID(C.n)>>>(C); }
-void tr_launch_init(const Tables& T, const TrArgs& C, const EvalState& D, const EvalState& D2, hipStream_t stream) {
-    tr_init<<<GRID(C.n)>>>(T, C, D, D2);
+// the initial state and the per-pass work lists, in one launch
+void tr_launch_init_lists(const Tables& T, const TrArgs& C, const EvalState& D, const EvalState& D2,
+                          hipStream_t stream) {
+    tr_lists<<<(C.n + LS_THREADS - 1) / LS_THREADS, LS_THREADS, 0, stream>>>(T, C, D, D2);
 }
 void tr_launch_side_count(const TrArgs& C, u32 kmax, u8* mask, hipStream_t stream) {
     tr_side_count<<<GRID(C.n)>>>(C, kmax, mask);
@@ -1753,9 +1754,6 @@ void tr_launch_side_rec(const TrArgs& C, const EvalState& S, hipStream_t stream)
 void tr_launch_evaluate(const Tables& T, const TrArgs& C, const EvalState& S, const EvalState& D, const Bal4* bb,
                         const PassGate& g, u32* chg, u32* chg_next, u32* front, u32* front_next, hipStream_t stream) {
     tr_evaluate<<<GRID(C.n)>>>(T, C, S, D, bb, g, chg, chg_next, front, front_next);
-}
-void tr_launch_lists(const TrArgs& C, hipStream_t stream) {
-    tr_lists<<<(C.n + LS_THREADS - 1) / LS_THREADS, LS_THREADS, 0, stream>>>(C);
 }
 void tr_launch_evaluate_lists(const Tables& T, const TrArgs& C, const EvalState& S, const EvalState& D, const Bal4* bb,
                               const PassGate& g, u32* chg, u32* chg_next, u32* front, u32* front_next, u32 n_simple,

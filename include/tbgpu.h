@@ -488,6 +488,47 @@ uint32_t tbgpu_lookup_transfers(tbgpu_ctx* ctx, const tbgpu_uint128_t* ids, uint
  * 128 B (src/state_machine.zig:53-76). */
 #define TBGPU_QUERY_MAX 8190u
 
+/* The grooves' field index trees (src/state_machine.zig:1575-1641 tree_options_index):
+ * Groove.insert puts (field, timestamp) into a field's tree for every stored object whose
+ * field is nonzero (src/lsm/groove.zig:911-936); a scan of a tree with a field value as
+ * its prefix yields the objects with that value in timestamp order.  The transfers groove
+ * indexes every field below, the accounts groove user_data_128/64/32, ledger and code.
+ * No operation of this snapshot's state machine reads them except through
+ * debit/credit_account_id (get_account_transfers); the scans below expose them. */
+enum tbgpu_index_field {
+    TBGPU_INDEX_DEBIT_ACCOUNT_ID = 0,   /* transfers */
+    TBGPU_INDEX_CREDIT_ACCOUNT_ID = 1,  /* transfers */
+    TBGPU_INDEX_USER_DATA_128 = 2,
+    TBGPU_INDEX_USER_DATA_64 = 3,
+    TBGPU_INDEX_USER_DATA_32 = 4,
+    TBGPU_INDEX_PENDING_ID = 5,         /* transfers */
+    TBGPU_INDEX_TIMEOUT = 6,            /* transfers */
+    TBGPU_INDEX_LEDGER = 7,
+    TBGPU_INDEX_CODE = 8,
+    TBGPU_INDEX_AMOUNT = 9,             /* transfers */
+};
+enum { TBGPU_INDEX_REVERSED = 1 << 0 };
+
+typedef struct tbgpu_index_filter_t {
+    tbgpu_uint128_t value;     /* the field's value (0: not indexed, so nothing matches) */
+    uint64_t timestamp_min;    /* 0 = unbounded (src/lsm/timestamp_range.zig) */
+    uint64_t timestamp_max;
+    uint32_t limit;            /* at most min(limit, TBGPU_QUERY_MAX) objects */
+    uint32_t field;            /* tbgpu_index_field */
+    uint32_t flags;            /* TBGPU_INDEX_REVERSED: descending timestamps */
+    uint32_t reserved;         /* 0 */
+} tbgpu_index_filter_t;
+
+/* The stored transfers (accounts) whose `field` equals `value`, timestamps within
+ * [timestamp_min, timestamp_max], ascending (or descending), at most
+ * min(limit, TBGPU_QUERY_MAX) whole objects into `out`.  Returns the count.  A filter
+ * that is invalid (a field the groove does not index, a zero limit, timestamp_min >
+ * timestamp_max != 0, a bound of UINT64_MAX, reserved flags or bytes) yields 0, as an
+ * invalid account filter does.  The trees are built on demand: a scan first indexes
+ * the objects stored since that tree's last scan. */
+uint32_t tbgpu_scan_transfers(tbgpu_ctx* ctx, const tbgpu_index_filter_t* filter, tbgpu_transfer_t* out);
+uint32_t tbgpu_scan_accounts(tbgpu_ctx* ctx, const tbgpu_index_filter_t* filter, tbgpu_account_t* out);
+
 /* StateMachine.compact (src/state_machine.zig:930-955): fold the transfers stored
  * since the previous compaction into the account-transfers index (the
  * debit_account_id / credit_account_id index trees of the transfers groove,

@@ -20,6 +20,7 @@
 #include "common.h"
 #include "engine.h"
 #include "transfers.h"
+#include "index.h"
 #include "fast.h"
 #include "query.h"
 
@@ -419,6 +420,16 @@ struct tbgpu_ctx {
     SortScratch q_ss{};
     u64* q_runs_dev = nullptr;
     std::vector<u64> q_runs{0};  // row boundaries of the index runs; back() = rows indexed
+    // the grooves' field index trees (index.hip), per (groove, field), built on demand
+    struct FieldIx {
+        u32* key = nullptr;
+        u32* val = nullptr;
+        std::vector<u64> runs{0};  // object row boundaries of the runs; back() = rows indexed
+        u64* runs_dev = nullptr;
+    } ix[2][10];
+    u32* ix_tkey = nullptr;
+    u32* ix_tval = nullptr;
+    SortScratch ix_ss{};
     u8* ximp = nullptr;          // per stored row: 1 = imported from another shard
     hipEvent_t ev0, ev1;
     hipEvent_t ev_side, ev_lists;  // fixed_point's side count and work-list lengths landed
@@ -683,6 +694,8 @@ extern "C" void tbgpu_reset(tbgpu_ctx* c) {
     c->n_foreign = 0;
     c->rows_hi = 0;
     c->q_runs.assign(1, 0);
+    for (auto& g : c->ix)
+        for (auto& x : g) x.runs.assign(1, 0);
 }
 
 extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
@@ -710,6 +723,13 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
                     c->lst_simple, c->lst_complex, c->d_ev, c->d_chain, c->d_slot, c->d_win, c->w_sstart, c->w_bal,
                     c->w_undo_slot, c->w_undo_val, c->w_out, c->ac_part, c->pf_buf};
     for (void* p : ptrs) if (p) { guard_release(p); (void)hipFree(p); }
+    for (auto& g : c->ix)
+        for (auto& x : g)
+            for (void* p : {(void*)x.key, (void*)x.val, (void*)x.runs_dev})
+                if (p) { guard_release(p); (void)hipFree(p); }
+    for (void* p : {(void*)c->ix_tkey, (void*)c->ix_tval, (void*)c->ix_ss.keys_tmp, (void*)c->ix_ss.vals_tmp,
+                    (void*)c->ix_ss.hist})
+        if (p) { guard_release(p); (void)hipFree(p); }
     for (EvalState& s : c->st) {
         void* q[] = {s.res, s.ok, s.pref, s.cfail, s.amt, s.pamt};
         for (void* p : q) if (p) { guard_release(p); (void)hipFree(p); }
@@ -2365,6 +2385,92 @@ static uint32_t query_host(tbgpu_ctx* c, const tbgpu_account_filter_t* filter, v
     run_queries(c, fd, 1, TBGPU_QUERY_MAX, c->ev_buf, history, &n);  // ev_buf: nmax * 128 B >= 8190 rows
     if (n) d2h(c, out, c->ev_buf, (u64)n * 128, c->stream);
     return n;
+}
+
+// ---------------------------------------------------------- index trees ----
+// The grooves' field index trees (index.hip): a tree indexes the objects stored since
+// its last scan into a new run, then merges runs as tbgpu_compact does.
+static bool ix_field_ok(u32 kind, u32 field) {
+    if (kind == TBGPU_INDEX_TRANSFERS) return field <= TBGPU_INDEX_AMOUNT;
+    return field == TBGPU_INDEX_USER_DATA_128 || field == TBGPU_INDEX_USER_DATA_64 ||
+           field == TBGPU_INDEX_USER_DATA_32 || field == TBGPU_INDEX_LEDGER || field == TBGPU_INDEX_CODE;
+}
+
+static bool ix_filter_ok(u32 kind, const tbgpu_index_filter_t& f) {
+    return ix_field_ok(kind, f.field) && f.limit != 0 && (f.flags & ~(u32)TBGPU_INDEX_REVERSED) == 0 &&
+           f.reserved == 0 && f.timestamp_min != ~0ull && f.timestamp_max != ~0ull &&
+           (f.timestamp_max == 0 || f.timestamp_min <= f.timestamp_max);
+}
+
+static void ix_sort(tbgpu_ctx* c, tbgpu_ctx::FieldIx& x, u32 field, u64 e0, u64 e1) {
+    const u64 m = e1 - e0;
+    if (m < 2) return;
+    radix_sort_pairs(x.key + e0, x.val + e0, c->ix_tkey, c->ix_tval, m, (int)std::min<u32>(ix_field_bits(field), 32),
+                     c->ix_ss, c->stream);
+    dcopy(x.key + e0, c->ix_tkey, m * 4, c->stream);
+    dcopy(x.val + e0, c->ix_tval, m * 4, c->stream);
+}
+
+static tbgpu_ctx::FieldIx& ix_extend(tbgpu_ctx* c, u32 kind, u32 field) {
+    tbgpu_ctx::FieldIx& x = c->ix[kind][field];
+    if (kind == TBGPU_INDEX_TRANSFERS) refresh_bases(c);
+    const u64 cap = kind == TBGPU_INDEX_TRANSFERS ? c->xrow_cap : c->accounts_max;
+    const u64 r0 = x.runs.back(), r1 = kind == TBGPU_INDEX_TRANSFERS ? c->n_rows : c->n_accounts;
+    if (!c->ix_tkey) {
+        u64& B = c->bytes;
+        ZeroOn zero_on(c->stream);
+        const u64 sc = std::max<u64>(c->xrow_cap, c->accounts_max);
+        c->ix_tkey = dalloc<u32>(sc, &B);
+        c->ix_tval = dalloc<u32>(sc, &B);
+        c->ix_ss.keys_tmp = dalloc<u32>(sc, &B);
+        c->ix_ss.vals_tmp = dalloc<u32>(sc, &B);
+        c->ix_ss.hist = dalloc<u32>(radix_sort_hist_words(sc), &B);
+        c->ix_ss.capacity = sc;
+    }
+    if (!x.key) {
+        u64& B = c->bytes;
+        ZeroOn zero_on(c->stream);
+        x.key = dalloc<u32>(cap, &B);
+        x.val = dalloc<u32>(cap, &B);
+        x.runs_dev = dalloc<u64>(Q_RUNS_MAX + 1, &B);
+    }
+    if (r1 == r0) return x;
+    ix_launch_entries(c->T, kind, field, r0, r1 - r0, c->ximp, x.key + r0, x.val + r0, c->stream);
+    ix_sort(c, x, field, r0, r1);
+    x.runs.push_back(r1);
+    while (x.runs.size() >= 3) {  // binary-counter merging (tbgpu_compact)
+        const size_t k = x.runs.size() - 1;
+        const u64 older = x.runs[k - 1] - x.runs[k - 2], newer = x.runs[k] - x.runs[k - 1];
+        if (2 * newer < older) break;
+        ix_sort(c, x, field, x.runs[k - 2], x.runs[k]);
+        x.runs.erase(x.runs.end() - 2);
+    }
+    if (x.runs.size() > Q_RUNS_MAX + 1) tbgpu_fatal("scan", "index runs exceed Q_RUNS_MAX", __FILE__, __LINE__);
+    h2d(c, x.runs_dev, x.runs.data(), x.runs.size() * sizeof(u64), c->stream);
+    return x;
+}
+
+static uint32_t scan_objects(tbgpu_ctx* c, u32 kind, const tbgpu_index_filter_t* filter, void* out) {
+    if (!ix_filter_ok(kind, *filter)) return 0;
+    tbgpu_ctx::FieldIx& x = ix_extend(c, kind, filter->field);
+    tbgpu_index_filter_t* fd = (tbgpu_index_filter_t*)c->res_buf;  // nmax * 8 B >= 48 B
+    h2d(c, fd, filter, sizeof *filter, c->stream);
+    IxArgs A{fd, kind, 1u, x.key, x.val, x.runs_dev, (u32)(x.runs.size() - 1), c->ev_buf, c->counts};
+    ix_launch_scan(c->T, A, c->stream);
+    uint32_t n = 0;
+    d2h(c, &n, c->counts, sizeof n, c->stream);
+    if (n) d2h(c, out, c->ev_buf, (u64)n * 128, c->stream);
+    return n;
+}
+
+extern "C" uint32_t tbgpu_scan_transfers(tbgpu_ctx* c, const tbgpu_index_filter_t* filter, tbgpu_transfer_t* out) {
+    CallGuard guard_(c, false);
+    return scan_objects(c, TBGPU_INDEX_TRANSFERS, filter, out);
+}
+
+extern "C" uint32_t tbgpu_scan_accounts(tbgpu_ctx* c, const tbgpu_index_filter_t* filter, tbgpu_account_t* out) {
+    CallGuard guard_(c, false);
+    return scan_objects(c, TBGPU_INDEX_ACCOUNTS, filter, out);
 }
 
 extern "C" uint32_t tbgpu_get_account_transfers(tbgpu_ctx* c, const tbgpu_account_filter_t* filter, tbgpu_transfer_t* out) {

@@ -12,8 +12,8 @@ import re
 
 import numpy as np
 
-from .types import (ACCOUNT_DTYPE, BALANCE_DTYPE, FILTER_DTYPE, HISTORY_DTYPE, QUERY_MAX, RESULT_DTYPE,
-                    TRANSFER_DTYPE, U128_DTYPE, U64_MAX, u128_array)
+from .types import (ACCOUNT_DTYPE, BALANCE_DTYPE, FILTER_DTYPE, HISTORY_DTYPE, INDEX_FILTER_DTYPE, QUERY_MAX,
+                    RESULT_DTYPE, TRANSFER_DTYPE, U128_DTYPE, U64_MAX, u128_array)
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
@@ -143,6 +143,9 @@ def lib():
     L.tbgpu_compact.restype = u64
     L.tbgpu_compact.argtypes = [vp]
     for name in ("tbgpu_get_account_transfers", "tbgpu_get_account_history"):
+        getattr(L, name).restype = u32
+        getattr(L, name).argtypes = [vp, vp, vp]
+    for name in ("tbgpu_scan_transfers", "tbgpu_scan_accounts"):
         getattr(L, name).restype = u32
         getattr(L, name).argtypes = [vp, vp, vp]
     for name in ("tbgpu_get_account_transfers_device", "tbgpu_get_account_history_device"):
@@ -486,6 +489,20 @@ class Engine:
         f = np.ascontiguousarray(filt, dtype=FILTER_DTYPE).reshape(1)
         out = np.zeros(QUERY_MAX, dtype=BALANCE_DTYPE)
         n = self._L.tbgpu_get_account_history(self._h, _ptr(f), _ptr(out))
+        return out[:n].copy()
+
+    def scan_transfers(self, filt: np.ndarray) -> np.ndarray:
+        """tbgpu_scan_transfers: one scan of a transfers index tree (INDEX_FILTER_DTYPE)."""
+        f = np.ascontiguousarray(filt, dtype=INDEX_FILTER_DTYPE).reshape(1)
+        out = np.zeros(QUERY_MAX, dtype=TRANSFER_DTYPE)
+        n = self._L.tbgpu_scan_transfers(self._h, _ptr(f), _ptr(out))
+        return out[:n].copy()
+
+    def scan_accounts(self, filt: np.ndarray) -> np.ndarray:
+        """tbgpu_scan_accounts: one scan of an accounts index tree (INDEX_FILTER_DTYPE)."""
+        f = np.ascontiguousarray(filt, dtype=INDEX_FILTER_DTYPE).reshape(1)
+        out = np.zeros(QUERY_MAX, dtype=ACCOUNT_DTYPE)
+        n = self._L.tbgpu_scan_accounts(self._h, _ptr(f), _ptr(out))
         return out[:n].copy()
 
     def query_device(self, filters_ptr: int, count: int, stride: int, out_ptr: int, history: bool = False):

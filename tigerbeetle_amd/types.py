@@ -48,6 +48,29 @@ FILTER_DTYPE = np.dtype(_u128("account_id") + [("timestamp_min", "<u8"), ("times
 BALANCE_DTYPE = np.dtype(_u128("debits_pending") + _u128("debits_posted") + _u128("credits_pending")
                          + _u128("credits_posted") + [("timestamp", "<u8"), ("reserved", "u1", (56,))])
 QUERY_MAX = 8190  # constants.batch_max.get_account_transfers / _history (src/state_machine.zig:53-76)
+# tbgpu_index_filter_t (include/tbgpu.h): a scan of one groove index tree
+INDEX_FILTER_DTYPE = np.dtype(_u128("value") + [("timestamp_min", "<u8"), ("timestamp_max", "<u8"),
+                                               ("limit", "<u4"), ("field", "<u4"), ("flags", "<u4"),
+                                               ("reserved", "<u4")])
+
+
+class IndexField(enum.IntEnum):
+    """tbgpu_index_field: the grooves' index trees (src/state_machine.zig:1575-1641)."""
+    debit_account_id = 0
+    credit_account_id = 1
+    user_data_128 = 2
+    user_data_64 = 3
+    user_data_32 = 4
+    pending_id = 5
+    timeout = 6
+    ledger = 7
+    code = 8
+    amount = 9
+
+
+TRANSFER_INDEX_FIELDS = tuple(IndexField)
+ACCOUNT_INDEX_FIELDS = (IndexField.user_data_128, IndexField.user_data_64, IndexField.user_data_32,
+                        IndexField.ledger, IndexField.code)
 
 assert ACCOUNT_DTYPE.itemsize == 128
 assert TRANSFER_DTYPE.itemsize == 128
@@ -55,6 +78,7 @@ assert RESULT_DTYPE.itemsize == 8
 assert HISTORY_DTYPE.itemsize == 256
 assert FILTER_DTYPE.itemsize == 64
 assert BALANCE_DTYPE.itemsize == 128
+assert INDEX_FILTER_DTYPE.itemsize == 48
 
 ACCOUNT_U128_FIELDS = ("id", "debits_pending", "debits_posted", "credits_pending", "credits_posted",
                        "user_data_128")

@@ -71,21 +71,6 @@ inline void wait_stream(hipStream_t s) {
         if (e != hipErrorNotReady) HIP_CHECK(e);
     }
 }
-// A small call's last wait spins (hipEventQuery) instead of blocking: the blocking
-// wait's wake-up is an interrupt, ≈10-20 us on a call whose device work is ≈25 us
-// (TBGPU_BLOCKING_SMALL=1 restores it for A/B timing).
-inline void wait_event_small(hipEvent_t ev) {
-    static const bool blocking = getenv("TBGPU_BLOCKING_SMALL") != nullptr;
-    if (blocking) {
-        HIP_CHECK(hipEventSynchronize(ev));
-        return;
-    }
-    for (;;) {
-        const hipError_t e = hipEventQuery(ev);
-        if (e == hipSuccess) return;
-        if (e != hipErrorNotReady) HIP_CHECK(e);
-    }
-}
 inline void wait_event(hipEvent_t ev) {
     if (blocking_sync()) {
         HIP_CHECK(hipEventSynchronize(ev));
@@ -1684,8 +1669,7 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
                                                 (const u64*)c->res_buf, dst_device ? nullptr : c->h_res_dev);
             HIP_CHECK(hipGetLastError());
             HIP_CHECK(hipEventRecord(c->ev1, c->stream));
-            if (events + n <= FP_TAIL_MAX) wait_event_small(c->ev1);
-            else wait_event(c->ev1);
+            wait_event(c->ev1);
             memcpy(c->h_counters, c->h_report, CNT_COUNT * sizeof(u32));
             memcpy(c->h_base, c->h_report + RPT_BASE, 4 * sizeof(u64));
             memcpy(c->h_rc + b0, c->h_report + RPT_COUNTS, nb * sizeof(u32));

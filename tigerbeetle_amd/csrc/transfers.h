@@ -65,6 +65,8 @@ struct TrArgs {
     Dirty dt;             // dirty tracking of the passes (engine.h)
     const u128* bh;       // headroom passes: the side's balance figure (balances.hip), or null (Bal4)
     u32 debug;            // diagnostics: count changed events by kind (TBGPU_TRACE_PASSES)
+    u32 sparse;           // a pass whose previous pass changed fewer than n >> sparse events checks
+                          // each event's due stamp before issuing its loads (0: never)
     u32 probe;            // timing probes only (TBGPU_EVAL_PROBE, after convergence): 1 skip post/void, 2 no side records
     Sides sd;             // the account sides of the call's events (engine.h)
     // The apply kernels' gate (tr_launch_converged): they run only when *epi != 0, so the

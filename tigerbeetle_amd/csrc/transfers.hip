@@ -585,12 +585,27 @@ __device__ __forceinline__ bool fin_ok(const TrArgs& C, const EvalState& S, u32 
 // pending resolved to an event with other accounts) asks the host to re-sort.
 __device__ __forceinline__ bool write_sides(const TrArgs& C, u32 i, bool pv, bool ok, u32 pref, u128 dpe, u128 dpo);
 
+// A sparse pass (tr_eval_lists: few events changed in the previous one) checks the
+// event's due stamps before anything else, so that an event that is not due costs one
+// round of loads, not the event's whole record.
+__device__ __forceinline__ bool due_first(const TrArgs& C, const EvalState& S, const EvalState& D, const PassGate& g,
+                                          u32 i) {
+    const u32 q = g.p, par = q & 1;
+    const u32 csi = C.cs[i], cei = C.ce[i];
+    bool is_due = C.dt.ev[par * C.dt.n + i] == q;  // (a sparse pass is neither full nor after a rebuild)
+    if (!is_due && csi != cei) is_due = C.dt.chain[par * C.dt.n + csi] == q;
+    if (!is_due && i == csi && csi != cei) D.cfail[csi] = S.cfail[csi];
+    return is_due;
+}
+
 // DUE: the pass's dirty check (Dirty) is made here, after the event's own words are
-// issued, so that a due event's loads are already in flight when the check resolves.
-template <bool DUE = false>
+// issued, so that a due event's loads are already in flight when the check resolves
+// (SPARSE: the check was made before, by due_first).
+template <bool DUE = false, bool SPARSE = false>
 __device__ __forceinline__ bool evaluate_one(const Tables& T, const TrArgs& C, const EvalState& S,
                                              const EvalState& D, const Bal4* __restrict__ bb, const PassGate& g,
                                              u32 i) {
+    if (SPARSE && !due_first(C, S, D, g, i)) return false;
     // Everything a regular transfer reads is issued up front, unconditionally (the
     // indices are valid for every event; unused values are dropped): one memory
     // round trip for the event's records, one for its two balances.  A post/void's
@@ -604,7 +619,7 @@ __device__ __forceinline__ bool evaluate_one(const Tables& T, const TrArgs& C, c
     const u128 s_amt = S.amt[i], s_pamt = S.pamt[i];
     const u32 s_pref = S.pref[i];
     const u32 pl = C.pend_last[i], pp = C.pre_p[i], pvp = C.prev_pend[i];
-    if (DUE) {
+    if (DUE && !SPARSE) {
         const u32 cei = C.ce[i], q = g.p, par = q & 1;
         bool is_due = g.full || C.dt.ev[par * C.dt.n + i] == q || *C.dt.all == q;
         if (!is_due && csi != cei) is_due = C.dt.chain[par * C.dt.n + csi] == q;
@@ -875,26 +890,31 @@ __device__ __forceinline__ void mark_changed(const TrArgs& C, u32 i, u32 q) {
 // 1286-1322) for transfers whose id nothing before them holds, and the static failures
 // inside chains (they break their chain every pass).  What evaluate_one does for them,
 // without its post/void and `exists` work (most of a pass's events are here).
+template <bool SPARSE>
 __device__ __forceinline__ bool eval_simple_one(const TrArgs& C, const EvalState& S, const EvalState& D,
                                                 const Bal4* __restrict__ bb, const PassGate& g, u32 i) {
     // The event's own words and its due stamp in one round of loads (most events are
     // due in the early passes, which dominate), the chain stamp and the balances in a
-    // second: two memory round trips before the evaluation instead of four.
+    // second: two memory round trips before the evaluation instead of four.  A sparse
+    // pass checks the stamps first (due_first).
+    if (SPARSE && !due_first(C, S, D, g, i)) return false;
     const u32 q = g.p, par = q & 1;
     const u8 sr = C.sres[i];
     const u32 csi = C.cs[i], cei = C.ce[i];
-    const u32 dte = g.full ? q : C.dt.ev[par * C.dt.n + i];
+    const u32 dte = (g.full || SPARSE) ? q : C.dt.ev[par * C.dt.n + i];
     const EvCore e = C.core[i];
     const uint2 ep = C.sd.epos[i];
     const u8 s_res = S.res[i];
     const u128 s_amt = S.amt[i];
-    bool is_due = g.full || dte == q || *C.dt.all == q;
-    if (!is_due && csi != cei) is_due = C.dt.chain[par * C.dt.n + csi] == q;
-    if (!is_due) {
-        // outcome unchanged in both buffers; a chain nobody re-evaluates keeps its
-        // first failure (the scan reset the next state's)
-        if (i == csi && csi != cei) D.cfail[csi] = S.cfail[csi];
-        return false;
+    if (!SPARSE) {
+        bool is_due = g.full || dte == q || *C.dt.all == q;
+        if (!is_due && csi != cei) is_due = C.dt.chain[par * C.dt.n + csi] == q;
+        if (!is_due) {
+            // outcome unchanged in both buffers; a chain nobody re-evaluates keeps its
+            // first failure (the scan reset the next state's)
+            if (i == csi && csi != cei) D.cfail[csi] = S.cfail[csi];
+            return false;
+        }
     }
     // (pamt and pref of a simple event are zero / none in both buffers after tr_init and
     // pass 0: later passes leave them)
@@ -939,11 +959,12 @@ __device__ __forceinline__ bool eval_simple_one(const TrArgs& C, const EvalState
 }
 
 // evaluate_one over the complex list
+template <bool SPARSE>
 __device__ __forceinline__ bool eval_complex_one(const Tables& T, const TrArgs& C, const EvalState& S,
                                                  const EvalState& D, const Bal4* __restrict__ bb, const PassGate& g,
                                                  u32 k, u32& i) {
     i = C.lst_complex[k];
-    const bool changed = evaluate_one<true>(T, C, S, D, bb, g, i);
+    const bool changed = evaluate_one<true, SPARSE>(T, C, S, D, bb, g, i);
     if (changed) mark_changed(C, i, g.p);
     return changed;
 }
@@ -962,16 +983,20 @@ __global__ __launch_bounds__(EV_THREADS) void tr_eval_lists(Tables T, TrArgs C, 
         *chg_next = 0;
         *front_next = NONE32;
     }
+    // sparse: the previous pass changed few events, so few are due (uniform)
+    const bool sparse = C.sparse && !g.full && *C.dt.all != g.p && *g.chg < ((n_simple + n_complex) >> C.sparse);
     bool changed = false;
     u32 i = NONE32;
     if (blockIdx.x < nbc) {
         const u32 k = blockIdx.x * EV_THREADS + threadIdx.x;
-        if (k < n_complex) changed = eval_complex_one(T, C, S, D, bb, g, k, i);
+        if (k < n_complex)
+            changed = sparse ? eval_complex_one<true>(T, C, S, D, bb, g, k, i)
+                             : eval_complex_one<false>(T, C, S, D, bb, g, k, i);
     } else {
         const u32 k = (blockIdx.x - nbc) * EV_THREADS + threadIdx.x;
         if (k < n_simple) {
             i = C.lst_simple[k];
-            changed = eval_simple_one(C, S, D, bb, g, i);
+            changed = sparse ? eval_simple_one<true>(C, S, D, bb, g, i) : eval_simple_one<false>(C, S, D, bb, g, i);
         }
     }
     const u32 c = block_sum(changed ? 1u : 0u);

@@ -20,6 +20,7 @@ prepare_timestamp += 1 + len(batch) and the commit timestamp is that value.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -129,6 +130,8 @@ def config2(transfer_count: int = 8_190_000, account_count: int = 1_000_000, see
             batch: int = BATCH_MAX) -> Workload:
     rng = np.random.default_rng(seed)
     perm = rng.permutation(account_count).astype(np.uint64)  # rank -> account index
+    if os.environ.get("TB_ZIPF_IDENTITY") == "1":  # timing experiments only: rank r is row r (profiles/r04/var_c2.sh)
+        perm = np.arange(account_count, dtype=np.uint64)
     acc_ids = np.arange(1, account_count + 1, dtype=np.uint64)
     accounts = make_accounts(acc_ids, ledger=1)
     draw = zipf_sampler(rng, account_count, s)

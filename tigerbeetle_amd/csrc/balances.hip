@@ -344,9 +344,13 @@ __device__ __forceinline__ bool tile_due(const SideScanArgs& A, const u32* __res
 }
 
 // The complex events whose id / pending groups moved last pass are due, with their
-// chains (decided here, before any evaluation of this pass reads it).
+// chains (decided here, before any evaluation of this pass reads it).  The fused scans
+// give this its own leading workgroups (resolve_blocks), one complex event per thread:
+// its three dependent loads then run beside the tiles' scans instead of ahead of them.
+__host__ __device__ __forceinline__ u32 resolve_blocks(u32 n_complex) { return (n_complex + BF_THREADS - 1) / BF_THREADS; }
 __device__ __forceinline__ void resolve_groups(const SideScanArgs& A, u32 par, u32 pq) {
-    for (u64 k = (u64)blockIdx.x * BF_THREADS + threadIdx.x; k < A.n_complex; k += (u64)gridDim.x * BF_THREADS) {
+    const u64 k = (u64)blockIdx.x * BF_THREADS + threadIdx.x;
+    if (k < A.n_complex) {
         const u32 i = A.lst_complex[k];
         const u32 gs = A.gslot[i], ps = A.pslot[i];
         if ((gs != NONE32 && A.dt.slot[par * A.dt.g + gs] == pq) ||
@@ -374,12 +378,16 @@ __global__ __launch_bounds__(BF_THREADS) void bs_fused(SideScanArgs A, u64 m, u3
     if (A.cfail_clear)
         for (u64 k = (u64)blockIdx.x * BF_THREADS + threadIdx.x; k < A.n; k += (u64)gridDim.x * BF_THREADS)
             A.cfail_clear[k] = NONE32;
-    const u32 t = blockIdx.x, tid = threadIdx.x;
+    const u32 nres = resolve_blocks(A.n_complex);
+    const u32 t = blockIdx.x - nres, tid = threadIdx.x;
     // Dirty tracking (engine.h Dirty): everything at a chunk's first pass and after a
     // side rebuild; otherwise only the windows whose side records moved last pass.
     const u32 pq = A.gate.p, par = pq & 1;
     const bool all = A.gate.full || *A.dt.all == pq;
-    if (!all) resolve_groups(A, par, pq);
+    if (blockIdx.x < nres) {
+        if (!all) resolve_groups(A, par, pq);
+        return;
+    }
     u32 a0, b0;
     const bool due = tile_due(A, tstart, t, ntiles, (u32)m, BF_THREADS * BF_IPT, all, a0, b0);
     if (a0 == NONE32) return;  // no account starts in this window: the previous tile has its sides
@@ -530,10 +538,14 @@ __global__ __launch_bounds__(BF_THREADS) void bs_fused_narrow(SideScanArgs A, u6
     if (A.cfail_clear)
         for (u64 k = (u64)blockIdx.x * BF_THREADS + threadIdx.x; k < A.n; k += (u64)gridDim.x * BF_THREADS)
             A.cfail_clear[k] = NONE32;
-    const u32 t = blockIdx.x, tid = threadIdx.x;
+    const u32 nres = resolve_blocks(A.n_complex);
+    const u32 t = blockIdx.x - nres, tid = threadIdx.x;
     const u32 pq = A.gate.p, par = pq & 1;
     const bool all = A.gate.full || *A.dt.all == pq;
-    if (!all) resolve_groups(A, par, pq);
+    if (blockIdx.x < nres) {
+        if (!all) resolve_groups(A, par, pq);
+        return;
+    }
     u32 a0, b0;
     const bool due = tile_due(A, tstart, t, ntiles, (u32)m, BF_THREADS, all, a0, b0);
     if (a0 == NONE32) return;
@@ -542,19 +554,29 @@ __global__ __launch_bounds__(BF_THREADS) void bs_fused_narrow(SideScanArgs A, u6
         return;
     }
     if (!due) return;
+    // Every word of the side in one round of loads (the deltas count only on an ok
+    // side), then the account row and the chain's first failure in a second.
     const u64 q = (u64)a0 + tid;
-    const u32 key = q < b0 ? A.skey[q] : invalid;
-    const u32 c = q < b0 ? A.sq_cs[q] : SQ_STANDALONE;
-    const u32 ev = q < b0 ? A.sq_ev[q] : 0;
-    const bool credit = ev >> 31;
+    const bool in = q < b0;
+    const u32 key = in ? A.skey[q] : invalid;
+    const u32 prev = (in && q > a0) ? A.skey[q - 1] : invalid;
+    const u32 c = in ? A.sq_cs[q] : SQ_STANDALONE;
+    const u32 ev = in ? A.sq_ev[q] : 0;
+    const u8 okw = in ? A.sq_ok[q] : 0;
+    const u128 dpe = in ? A.sq_dpend[q] : 0, dpo = in ? A.sq_dpost[q] : 0;
     u128 old = 0;
-    if (!all && key < invalid) old = A.bh[q];
+    if (!all && in) old = A.bh[q];
+    const bool credit = ev >> 31;
+    const bool live = key < invalid && (okw & 1);
+    const bool chained = !(c & (SQ_STANDALONE | SQ_DOOM));
+    const u32 cf = live && chained ? A.cfail[c & SQ_CS] : NONE32;
     u128 r_hd = 0, r_hc = 0;  // the account's pre-chunk headroom
     if (key < invalid) {
         const Account& ac = acc[key];
-        const u128 dp = ac.debits_pending, dpo = ac.debits_posted, cp = ac.credits_pending, cpo = ac.credits_posted;
-        r_hd = cpo - dp - dpo;
-        r_hc = dpo - cp - cpo;
+        const u128 adp = ac.debits_pending, adpo = ac.debits_posted, acp = ac.credits_pending,
+                   acpo = ac.credits_posted;
+        r_hd = acpo - adp - adpo;
+        r_hc = adpo - acp - acpo;
     }
     // the side's delta on (H_d, H_c): final-ok -> F, evaluated-ok in a chain that does
     // not persist -> H (visible only behind it in its own chain)
@@ -562,13 +584,12 @@ __global__ __launch_bounds__(BF_THREADS) void bs_fused_narrow(SideScanArgs A, u6
     SN e;
     e.fl = 1;
     if (key < invalid) {
-        if (A.sq_ok[q] & 1) {
-            const u128 dpe = A.sq_dpend[q], dpo = A.sq_dpost[q];
+        if (live) {
             const u128 dhd = credit ? dpo : (u128)0 - dpe - dpo;
             const u128 dhc = credit ? (u128)0 - dpe - dpo : dpo;
-            if (side_final(A, q)) { f_hd = dhd; f_hc = dhc; } else { h_hd = dhd; h_hc = dhc; }
+            const bool fin = !(c & SQ_DOOM) && ((c & SQ_STANDALONE) || cf == NONE32);  // side_final
+            if (fin) { f_hd = dhd; f_hc = dhc; } else { h_hd = dhd; h_hc = dhc; }
         }
-        const u32 prev = q == a0 ? invalid : A.skey[q - 1];
         e.fl = prev != key ? 1u : 0u;
     }
     e.hd = f_hd;
@@ -602,7 +623,8 @@ void side_scan_fused(const SideScanArgs& A, u64 m, u32 invalid, const u32* tstar
                      const Account* acc, Bal4* bb, hipStream_t stream) {
     if (m == 0) return;
     const u32 ntiles = (u32)((m + BF_TILE - 1) / BF_TILE);
-    bs_fused<<<ntiles, BF_THREADS, 0, stream>>>(A, m, invalid, tstart, ntiles, long_flag, acc, bb);
+    bs_fused<<<resolve_blocks(A.n_complex) + ntiles, BF_THREADS, 0, stream>>>(A, m, invalid, tstart, ntiles, long_flag,
+                                                                              acc, bb);
     HIP_CHECK(hipGetLastError());
 }
 
@@ -610,7 +632,8 @@ void side_scan_fused_narrow(const SideScanArgs& A, u64 m, u32 invalid, const u32
                             const Account* acc, hipStream_t stream) {
     if (m == 0) return;
     const u32 ntiles = (u32)((m + BF_TILE - 1) / BF_TILE);
-    bs_fused_narrow<<<ntiles, BF_THREADS, 0, stream>>>(A, m, invalid, tstart, ntiles, long_flag, acc);
+    bs_fused_narrow<<<resolve_blocks(A.n_complex) + ntiles, BF_THREADS, 0, stream>>>(A, m, invalid, tstart, ntiles,
+                                                                                     long_flag, acc);
     HIP_CHECK(hipGetLastError());
 }
 

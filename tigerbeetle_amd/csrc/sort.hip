@@ -105,6 +105,46 @@ __global__ __launch_bounds__(RSS_THREADS) void rs_scan(u32* __restrict__ data, u
     }
 }
 
+// The histogram's digit rows scanned in parallel, one wave per digit: row d (every
+// tile's count of digit d) becomes its exclusive prefix, and tot[d] the row's total.
+// rs_scatter adds the digits' exclusive prefix of tot (a 256-entry scan per tile), so
+// no single workgroup walks the whole histogram (rs_scan, 13-14 us per pass for the
+// 41k words of a 330k-side sort, its per-thread runs far from coalesced).
+__global__ __launch_bounds__(256) void rs_rowscan(u32* __restrict__ hist, u32 nblocks, u32* __restrict__ tot,
+                                                  const u32* pred, u32 pmask) {
+    if (rs_off(pred, pmask)) return;
+    const u32 lane = threadIdx.x & 63, d = blockIdx.x * 4 + (threadIdx.x >> 6);
+    u32* row = hist + (u64)d * nblocks;
+    u32 carry = 0;
+    for (u32 base = 0; base < nblocks; base += 64) {
+        const u32 k = base + lane;
+        const u32 v = k < nblocks ? row[k] : 0;
+        u32 x = v;
+        for (int off = 1; off < 64; off <<= 1) {
+            const u32 y = __shfl_up(x, off);
+            if (lane >= (u32)off) x += y;
+        }
+        if (k < nblocks) row[k] = carry + x - v;
+        carry += __shfl(x, 63);
+    }
+    if (lane == 0) tot[d] = carry;
+}
+
+// Exclusive scan of one value per thread over a 256-thread workgroup.
+__device__ __forceinline__ u32 rs_block_excl256(u32 v, u32* wsum) {
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    u32 x = v;
+    for (int off = 1; off < 64; off <<= 1) {
+        const u32 y = __shfl_up(x, off);
+        if (lane >= (u32)off) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    u32 pre = 0;
+    for (u32 w = 0; w < wave; w++) pre += wsum[w];
+    return pre + x - v;
+}
+
 // Stable scatter: item order within a tile is r*256 + tid (round-major), i.e.
 // index order.  Ranks within a wave come from 8 ballots (one per digit bit);
 // ranks across the 4 waves and the rounds come from LDS counters.
@@ -112,13 +152,15 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter(const u32* __restrict__
                                                          const u32* __restrict__ vals_in, u32* __restrict__ keys_out,
                                                          u32* __restrict__ vals_out, u64 n, int shift,
                                                          const u32* __restrict__ hist, u32 nblocks,
-                                                         const u32* pred, u32 pmask) {
+                                                         const u32* __restrict__ tot, const u32* pred, u32 pmask) {
     if (rs_off(pred, pmask)) return;
     __shared__ u32 run_base[256];
     __shared__ u32 wcnt[RS_WAVES][256];
+    __shared__ u32 wsum[RS_WAVES];
     const u32 tid = threadIdx.x;
     const u32 wave = tid >> 6;
-    run_base[tid] = hist[(u64)tid * nblocks + blockIdx.x];
+    const u32 row = hist[(u64)tid * nblocks + blockIdx.x];
+    run_base[tid] = row + (tot ? rs_block_excl256(tot[tid], wsum) : 0u);
     for (int w = 0; w < RS_WAVES; w++) wcnt[w][tid] = 0;
     __syncthreads();
     const u64 base = (u64)blockIdx.x * RS_TILE;
@@ -261,6 +303,10 @@ void radix_sort_pairs(const u32* keys_in, const u32* vals_in, u32* keys_out, u32
     if (n > s.capacity) tbgpu_fatal("radix_sort_pairs", "n exceeds scratch capacity", __FILE__, __LINE__);
     const u32 nblocks = (u32)((n + RS_TILE - 1) / RS_TILE);
     const int passes = bits <= 0 ? 1 : (bits + 7) / 8;
+    // the digit totals after the histogram (radix_sort_hist_words leaves 256 words);
+    // TBGPU_SORT_ONE_SCAN=1: the single-workgroup scan (A/B timing)
+    static const bool row_scan = getenv("TBGPU_SORT_ONE_SCAN") == nullptr;
+    u32* tot = s.hist + 256ull * nblocks;
     const u32* ks = keys_in;
     const u32* vs = vals_in;
     for (int p = 0; p < passes; p++) {
@@ -269,8 +315,13 @@ void radix_sort_pairs(const u32* keys_in, const u32* vals_in, u32* keys_out, u32
         u32* vd = to_out ? vals_out : s.vals_tmp;
         const int shift = 8 * p;
         rs_hist<<<nblocks, RS_THREADS, 0, stream>>>(ks, n, shift, s.hist, nblocks, pred, pred_mask);
-        rs_scan<<<1, RSS_THREADS, 0, stream>>>(s.hist, 256ull * nblocks, pred, pred_mask);
-        rs_scatter<<<nblocks, RS_THREADS, 0, stream>>>(ks, vs, kd, vd, n, shift, s.hist, nblocks, pred, pred_mask);
+        if (row_scan) {
+            rs_rowscan<<<64, 256, 0, stream>>>(s.hist, nblocks, tot, pred, pred_mask);
+        } else {
+            rs_scan<<<1, RSS_THREADS, 0, stream>>>(s.hist, 256ull * nblocks, pred, pred_mask);
+        }
+        rs_scatter<<<nblocks, RS_THREADS, 0, stream>>>(ks, vs, kd, vd, n, shift, s.hist, nblocks,
+                                                       row_scan ? tot : nullptr, pred, pred_mask);
         ks = kd;
         vs = vd;
     }

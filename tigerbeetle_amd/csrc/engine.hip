@@ -1134,9 +1134,8 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
     bool counted = true;  // a count is in flight for the first build
 
     // grouping by id / pending id: each step runs only when classify found the need
-    tr_launch_group(C, 0, s);
+    tr_launch_group(C, 2, s);  // id and pending groups together
     tr_launch_group2(C, s);
-    tr_launch_group(C, 1, s);
     tr_launch_init_lists(c->T, C, c->st[0], c->st[1], s);
     HIP_CHECK(hipMemcpyAsync(c->h_base + 6, c->counters + CNT_NSIMPLE, 2 * sizeof(u32), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipMemcpyAsync(c->h_base + 7, c->counters + CNT_FLAGS, sizeof(u32), hipMemcpyDeviceToHost, s));

@@ -320,10 +320,13 @@ __device__ __forceinline__ void grp_fields(const TrArgs& C, u32 kind, u32 i, u32
 }
 
 constexpr u32 GR_THREADS = 1024;  // one cursor atomic per 1024 events (per wave: ~10 us per chunk)
-__global__ __launch_bounds__(GR_THREADS) void tr_grp_reserve(TrArgs C, u32 kind) {
+// The id groups (kind 0) and the pending groups (kind 1) do not read each other: each
+// launch takes both, `nb` workgroups per kind (kind0 + blockIdx.x / nb).
+__global__ __launch_bounds__(GR_THREADS) void tr_grp_reserve(TrArgs C, u32 kind0, u32 nb) {
     __shared__ u32 s_tot[GR_THREADS / 64];
     __shared__ u32 s_base;
-    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    const u32 kind = kind0 + blockIdx.x / nb;
+    const u32 i = (blockIdx.x % nb) * blockDim.x + threadIdx.x;
     if (!need(C, kind)) return;
     u32 slot = NONE32, cnt = 0;
     if (i < C.n) grp_fields(C, kind, i, &slot, &cnt);
@@ -350,8 +353,9 @@ __global__ __launch_bounds__(GR_THREADS) void tr_grp_reserve(TrArgs C, u32 kind)
     }
 }
 
-__global__ void tr_grp_place(TrArgs C, u32 kind) {
-    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void tr_grp_place(TrArgs C, u32 kind0, u32 nb) {
+    const u32 kind = kind0 + blockIdx.x / nb;
+    const u32 i = (blockIdx.x % nb) * blockDim.x + threadIdx.x;
     if (i >= C.n || !need(C, kind)) return;
     u32 slot, cnt;
     grp_fields(C, kind, i, &slot, &cnt);
@@ -361,8 +365,9 @@ __global__ void tr_grp_place(TrArgs C, u32 kind) {
     (kind == 0 ? C.glist : C.plist)[b + k] = i;
 }
 
-__global__ void tr_grp_rank(TrArgs C, u32 kind) {
-    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void tr_grp_rank(TrArgs C, u32 kind0, u32 nb) {
+    const u32 kind = kind0 + blockIdx.x / nb;
+    const u32 i = (blockIdx.x % nb) * blockDim.x + threadIdx.x;
     if (i >= C.n || !need(C, kind)) return;
     u32 slot, cnt;
     grp_fields(C, kind, i, &slot, &cnt);
@@ -1752,10 +1757,14 @@ void tr_launch_classify(const Tables& T, const TrArgs& C, hipStream_t stream) {
     tr_classify<<<GRID(C.n)>>>(T, C);
     tr_group1<<<GRID(C.n)>>>(C);
 }
-void tr_launch_group(const TrArgs& C, u32 kind, hipStream_t stream) {
-    tr_grp_reserve<<<(C.n + GR_THREADS - 1) / GR_THREADS, GR_THREADS, 0, stream>>>(C, kind);
-    tr_grp_place<<<GRID(C.n)>>>(C, kind);
-    tr_grp_rank<<<GRID(C.n)>>>(C, kind);
+// kinds: 0 the id groups, 1 the pending groups, 2 both
+void tr_launch_group(const TrArgs& C, u32 kinds, hipStream_t stream) {
+    const u32 k0 = kinds == 2 ? 0u : kinds, nk = kinds == 2 ? 2u : 1u;
+    const u32 nr = (C.n + GR_THREADS - 1) / GR_THREADS, nt = (C.n + 255) / 256;
+    if (!nr) return;
+    tr_grp_reserve<<<nk * nr, GR_THREADS, 0, stream>>>(C, k0, nr);
+    tr_grp_place<<<nk * nt, 256, 0, stream>>>(C, k0, nt);
+    tr_grp_rank<<<nk * nt, 256, 0, stream>>>(C, k0, nt);
 }
 void tr_launch_group2(const TrArgs& C, hipStream_t stream) { tr_group2<<<GRID(C.n)>>>(C); }
 // the initial state and the per-pass work lists, in one launch

@@ -1,13 +1,14 @@
 """Kernel timeline of the drop-in call (run under rocprofv3 --kernel-trace): 100k accounts,
 then 120 single tbgpu_create_transfers calls of one 8190-transfer batch each from page-locked
 host memory, the last 60 after tbgpu_prefetch_transfers + wait (bench.py host_path's legs)."""
+import os
 import sys
 import time
 
 import numpy as np
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from tigerbeetle_amd import workload  # noqa: E402
 from tigerbeetle_amd.engine import Engine  # noqa: E402
 from tigerbeetle_amd.types import TRANSFER_DTYPE  # noqa: E402

@@ -931,8 +931,8 @@ static TrArgs make_tr_args(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb) {
     C.commit_ts = c->rt_dry ? c->rt_dry_ts : c->T.commit_ts;
     static const bool debug = getenv("TBGPU_TRACE_PASSES") != nullptr;  // diagnostics only
     C.debug = debug ? 1u : 0u;
-    // sparse passes below n / 16 changes (TBGPU_SPARSE_SHIFT: A/B timing, 0 = never)
-    static const u32 sparse = getenv("TBGPU_SPARSE_SHIFT") ? (u32)atoi(getenv("TBGPU_SPARSE_SHIFT")) : 4u;
+    // sparse passes below n / 8 changes (TBGPU_SPARSE_SHIFT: A/B timing, 0 = never)
+    static const u32 sparse = getenv("TBGPU_SPARSE_SHIFT") ? (u32)atoi(getenv("TBGPU_SPARSE_SHIFT")) : 3u;
     C.sparse = sparse;
     C.lst_simple = c->lst_simple;
     C.lst_complex = c->lst_complex;

@@ -348,8 +348,8 @@ __device__ __forceinline__ bool tile_due(const SideScanArgs& A, const u32* __res
 // give this its own leading workgroups (resolve_blocks), one complex event per thread:
 // its three dependent loads then run beside the tiles' scans instead of ahead of them.
 __host__ __device__ __forceinline__ u32 resolve_blocks(u32 n_complex) { return (n_complex + BF_THREADS - 1) / BF_THREADS; }
-__device__ __forceinline__ void resolve_groups(const SideScanArgs& A, u32 par, u32 pq) {
-    const u64 k = (u64)blockIdx.x * BF_THREADS + threadIdx.x;
+__device__ __forceinline__ void resolve_groups(const SideScanArgs& A, u32 par, u32 pq, u32 threads = BF_THREADS) {
+    const u64 k = (u64)blockIdx.x * threads + threadIdx.x;
     if (k < A.n_complex) {
         const u32 i = A.lst_complex[k];
         const u32 gs = A.gslot[i], ps = A.pslot[i];
@@ -528,92 +528,123 @@ __device__ __forceinline__ SN block_excl_n(SN v, SN* wtot) {
     return combine_n(pre, ex);
 }
 
-__global__ __launch_bounds__(BF_THREADS) void bs_fused_narrow(SideScanArgs A, u64 m, u32 invalid,
+// Two sides per thread in 256-thread workgroups (the same 512-side window): the
+// launch's 4-wave workgroups then all fit the chip at once, where 8-wave ones took a
+// second round for the last fifth of the tiles.
+constexpr int NF_THREADS = 256, NF_IPT = 2;
+static_assert(NF_THREADS * NF_IPT == 2 * BF_TILE, "a workgroup scans two nominal tiles");
+__host__ __device__ __forceinline__ u32 resolve_blocks_n(u32 n_complex) {
+    return (n_complex + NF_THREADS - 1) / NF_THREADS;
+}
+
+__global__ __launch_bounds__(NF_THREADS) void bs_fused_narrow(SideScanArgs A, u64 m, u32 invalid,
                                                               const u32* __restrict__ tstart, u32 ntiles,
                                                               u32* long_flag, const Account* __restrict__ acc) {
     if (!gate_open(A.gate)) return;
-    __shared__ SN wtot[BF_THREADS / 64];
-    __shared__ u32 s_key[BF_THREADS], s_cs[BF_THREADS];
-    __shared__ u128 s_hd[BF_THREADS], s_hc[BF_THREADS];
+    __shared__ SN wtot[NF_THREADS / 64];
+    __shared__ u32 s_key[NF_THREADS * NF_IPT], s_cs[NF_THREADS * NF_IPT];
+    __shared__ u128 s_hd[NF_THREADS * NF_IPT], s_hc[NF_THREADS * NF_IPT];
     if (A.cfail_clear)
-        for (u64 k = (u64)blockIdx.x * BF_THREADS + threadIdx.x; k < A.n; k += (u64)gridDim.x * BF_THREADS)
+        for (u64 k = (u64)blockIdx.x * NF_THREADS + threadIdx.x; k < A.n; k += (u64)gridDim.x * NF_THREADS)
             A.cfail_clear[k] = NONE32;
-    const u32 nres = resolve_blocks(A.n_complex);
+    const u32 nres = resolve_blocks_n(A.n_complex);
     const u32 t = blockIdx.x - nres, tid = threadIdx.x;
     const u32 pq = A.gate.p, par = pq & 1;
     const bool all = A.gate.full || *A.dt.all == pq;
     if (blockIdx.x < nres) {
-        if (!all) resolve_groups(A, par, pq);
+        if (!all) resolve_groups(A, par, pq, NF_THREADS);
         return;
     }
     u32 a0, b0;
-    const bool due = tile_due(A, tstart, t, ntiles, (u32)m, BF_THREADS, all, a0, b0);
+    const bool due = tile_due(A, tstart, t, ntiles, (u32)m, NF_THREADS * NF_IPT, all, a0, b0);
     if (a0 == NONE32) return;
-    if (b0 - a0 > BF_THREADS) {
+    if (b0 - a0 > NF_THREADS * NF_IPT) {
         if (tid == 0) atomicMax(long_flag, A.gate.p + 1);
         return;
     }
     if (!due) return;
-    // Every word of the side in one round of loads (the deltas count only on an ok
-    // side), then the account row and the chain's first failure in a second.
-    const u64 q = (u64)a0 + tid;
-    const bool in = q < b0;
-    const u32 key = in ? A.skey[q] : invalid;
-    const u32 prev = (in && q > a0) ? A.skey[q - 1] : invalid;
-    const u32 c = in ? A.sq_cs[q] : SQ_STANDALONE;
-    const u32 ev = in ? A.sq_ev[q] : 0;
-    const u8 okw = in ? A.sq_ok[q] : 0;
-    const u128 dpe = in ? A.sq_dpend[q] : 0, dpo = in ? A.sq_dpost[q] : 0;
-    u128 old = 0;
-    if (!all && in) old = A.bh[q];
-    const bool credit = ev >> 31;
-    const bool live = key < invalid && (okw & 1);
-    const bool chained = !(c & (SQ_STANDALONE | SQ_DOOM));
-    const u32 cf = live && chained ? A.cfail[c & SQ_CS] : NONE32;
-    u128 r_hd = 0, r_hc = 0;  // the account's pre-chunk headroom
-    if (key < invalid) {
-        const Account& ac = acc[key];
-        const u128 adp = ac.debits_pending, adpo = ac.debits_posted, acp = ac.credits_pending,
-                   acpo = ac.credits_posted;
-        r_hd = acpo - adp - adpo;
-        r_hc = adpo - acp - acpo;
+    // Every word of the thread's two sides in one round of loads (the deltas count only
+    // on an ok side), then the account rows and the chains' first failures in a second.
+    const u64 qa = (u64)a0 + NF_IPT * tid;
+    u32 key[NF_IPT], c[NF_IPT], ev[NF_IPT];
+    u8 okw[NF_IPT];
+    u128 dpe[NF_IPT], dpo[NF_IPT], old[NF_IPT];
+#pragma unroll
+    for (int k = 0; k < NF_IPT; k++) {
+        const u64 q = qa + k;
+        const bool in = q < b0;
+        key[k] = in ? A.skey[q] : invalid;
+        c[k] = in ? A.sq_cs[q] : SQ_STANDALONE;
+        ev[k] = in ? A.sq_ev[q] : 0;
+        okw[k] = in ? A.sq_ok[q] : 0;
+        dpe[k] = in ? A.sq_dpend[q] : 0;
+        dpo[k] = in ? A.sq_dpost[q] : 0;
+        old[k] = (!all && in) ? A.bh[q] : 0;
     }
-    // the side's delta on (H_d, H_c): final-ok -> F, evaluated-ok in a chain that does
+    const u32 prev0 = (qa < b0 && qa > a0) ? A.skey[qa - 1] : invalid;
+    u32 cf[NF_IPT];
+    u128 r_hd[NF_IPT], r_hc[NF_IPT];  // the accounts' pre-chunk headroom
+#pragma unroll
+    for (int k = 0; k < NF_IPT; k++) {
+        const bool live = key[k] < invalid && (okw[k] & 1);
+        cf[k] = live && !(c[k] & (SQ_STANDALONE | SQ_DOOM)) ? A.cfail[c[k] & SQ_CS] : NONE32;
+        r_hd[k] = r_hc[k] = 0;
+        if (key[k] < invalid) {
+            const Account& ac = acc[key[k]];
+            const u128 adp = ac.debits_pending, adpo = ac.debits_posted, acp = ac.credits_pending,
+                       acpo = ac.credits_posted;
+            r_hd[k] = acpo - adp - adpo;
+            r_hc[k] = adpo - acp - acpo;
+        }
+    }
+    // each side's delta on (H_d, H_c): final-ok -> F, evaluated-ok in a chain that does
     // not persist -> H (visible only behind it in its own chain)
-    u128 f_hd = 0, f_hc = 0, h_hd = 0, h_hc = 0;
-    SN e;
-    e.fl = 1;
-    if (key < invalid) {
-        if (live) {
-            const u128 dhd = credit ? dpo : (u128)0 - dpe - dpo;
-            const u128 dhc = credit ? (u128)0 - dpe - dpo : dpo;
-            const bool fin = !(c & SQ_DOOM) && ((c & SQ_STANDALONE) || cf == NONE32);  // side_final
-            if (fin) { f_hd = dhd; f_hc = dhc; } else { h_hd = dhd; h_hc = dhc; }
+    SN e[NF_IPT];
+#pragma unroll
+    for (int k = 0; k < NF_IPT; k++) {
+        const bool credit = ev[k] >> 31;
+        u128 f_hd = 0, f_hc = 0, h_hd = 0, h_hc = 0;
+        e[k].fl = 1;
+        if (key[k] < invalid) {
+            if (okw[k] & 1) {
+                const u128 dhd = credit ? dpo[k] : (u128)0 - dpe[k] - dpo[k];
+                const u128 dhc = credit ? (u128)0 - dpe[k] - dpo[k] : dpo[k];
+                const bool fin = !(c[k] & SQ_DOOM) && ((c[k] & SQ_STANDALONE) || cf[k] == NONE32);  // side_final
+                if (fin) { f_hd = dhd; f_hc = dhc; } else { h_hd = dhd; h_hc = dhc; }
+            }
+            const u32 prev = k == 0 ? prev0 : key[k - 1];
+            e[k].fl = prev != key[k] ? 1u : 0u;
         }
-        e.fl = prev != key ? 1u : 0u;
+        e[k].hd = f_hd;
+        e[k].hc = f_hc;
+        const u32 j = NF_IPT * tid + k;
+        s_key[j] = key[k];
+        s_cs[j] = (c[k] & SQ_STANDALONE) ? NONE32 : (c[k] & SQ_CS);
+        if (!(c[k] & SQ_STANDALONE)) { s_hd[j] = h_hd; s_hc[j] = h_hc; }
     }
-    e.hd = f_hd;
-    e.hc = f_hc;
-    s_key[tid] = key;
-    s_cs[tid] = (c & SQ_STANDALONE) ? NONE32 : (c & SQ_CS);
-    if (!(c & SQ_STANDALONE)) { s_hd[tid] = h_hd; s_hc[tid] = h_hc; }
-    const SN run = block_excl_n(e, wtot);  // (its barrier publishes s_key / s_cs / s_h*)
-    if (key < invalid) {
-        u128 h = 0;
-        u32 j = tid;
-        const u32 cs = c & SQ_CS;
-        if (s_cs[j] != NONE32)
-            while (j > 0 && s_key[j - 1] == key && s_cs[j - 1] == cs) { --j; h += credit ? s_hc[j] : s_hd[j]; }
-        u128 out = credit ? r_hc : r_hd;
-        if (!(e.fl & 1)) out += credit ? run.hc : run.hd;
-        out += h;
-        if (all) {
-            A.bh[q] = out;
-        } else if (old != out) {
-            A.bh[q] = out;  // a balance moved: its event is due this pass (with its chain)
-            A.dt.ev[par * A.dt.n + (ev & 0x7FFFFFFFu)] = pq;
-            if (!(c & SQ_STANDALONE)) A.dt.chain[par * A.dt.n + (c & SQ_CS)] = pq;
+    SN run = block_excl_n(combine_n(e[0], e[1]), wtot);  // (its barrier publishes s_key / s_cs / s_h*)
+#pragma unroll
+    for (int k = 0; k < NF_IPT; k++) {
+        const u64 q = qa + k;
+        if (key[k] < invalid) {
+            const bool credit = ev[k] >> 31;
+            u128 h = 0;
+            u32 j = NF_IPT * tid + k;
+            const u32 cs = c[k] & SQ_CS;
+            if (s_cs[j] != NONE32)
+                while (j > 0 && s_key[j - 1] == key[k] && s_cs[j - 1] == cs) { --j; h += credit ? s_hc[j] : s_hd[j]; }
+            u128 out = credit ? r_hc[k] : r_hd[k];
+            if (!(e[k].fl & 1)) out += credit ? run.hc : run.hd;
+            out += h;
+            if (all) {
+                A.bh[q] = out;
+            } else if (old[k] != out) {
+                A.bh[q] = out;  // a balance moved: its event is due this pass (with its chain)
+                A.dt.ev[par * A.dt.n + (ev[k] & 0x7FFFFFFFu)] = pq;
+                if (!(c[k] & SQ_STANDALONE)) A.dt.chain[par * A.dt.n + (c[k] & SQ_CS)] = pq;
+            }
         }
+        run = combine_n(run, e[k]);
     }
 }
 
@@ -632,7 +663,7 @@ void side_scan_fused_narrow(const SideScanArgs& A, u64 m, u32 invalid, const u32
                             const Account* acc, hipStream_t stream) {
     if (m == 0) return;
     const u32 ntiles = (u32)((m + BF_TILE - 1) / BF_TILE);
-    bs_fused_narrow<<<resolve_blocks(A.n_complex) + ntiles, BF_THREADS, 0, stream>>>(A, m, invalid, tstart, ntiles,
+    bs_fused_narrow<<<resolve_blocks_n(A.n_complex) + ntiles, NF_THREADS, 0, stream>>>(A, m, invalid, tstart, ntiles,
                                                                                      long_flag, acc);
     HIP_CHECK(hipGetLastError());
 }

@@ -5,6 +5,9 @@ pending transfers and posts/voids of earlier ones, timeouts, balancing -- commit
 whole-call, batch by batch and on the forced general path, every reply and the
 whole state bit-exact vs the oracle.  The fast path's eligibility boundaries are
 where such mutations land."""
+import os
+import sys
+
 import numpy as np
 import pytest
 
@@ -92,3 +95,26 @@ def test_fuzz_mutations(seed):
     if seed % 3 == 1:
         # the sequential walk from the front after two passes (the fixed point's bound)
         _check(w, force_general=True, walk_early=True)
+
+
+STRESS = os.environ.get("TB_FUZZ_STRESS")  # "first:count": a wider sweep on demand (profiles/r04/fuzz_stress.sh)
+
+
+@pytest.mark.skipif(not STRESS, reason="the wider sweep runs only with TB_FUZZ_STRESS=first:count")
+def test_fuzz_stress_sweep():
+    """The same mutations over many more seeds, every one also on the forced general path
+    (the passes, the side sort and the headroom scan this sweep is for)."""
+    first, count = (int(x) for x in STRESS.split(":"))
+    for seed in range(first, first + count):
+        rng = np.random.default_rng(1000 + seed)
+        nb = int(rng.integers(2, 6))
+        batch = int(rng.integers(50, 700))
+        w = workload.config1(transfer_count=nb * batch, account_count=int(rng.integers(3, 40)), seed=seed,
+                             batch=batch)
+        w = _mutate(w, rng, [0.0005, 0.005, 0.03, 0.15][seed % 4])
+        _check(w)
+        _check(w, force_general=True)
+        if seed % 5 == 0:
+            _check(w, split=1)
+        if seed % 50 == 0:
+            print(f"fuzz stress: seed {seed} ok", flush=True, file=sys.stderr)

@@ -67,7 +67,9 @@ def _mutate(w, rng, rate):
 def _check(w, **kw):
     from tigerbeetle_amd.engine import Engine
     orc = oracle.Oracle(len(w.accounts), len(w.transfers))
-    gpu = Engine(accounts_max=1 << 10, transfers_max=1 << 15, history_max=1 << 12, events_per_call_max=1 << 13,
+    nt = len(w.transfers)
+    gpu = Engine(accounts_max=1 << 10, transfers_max=max(1 << 15, 2 * nt), history_max=max(1 << 12, 2 * nt),
+                 events_per_call_max=max(1 << 13, nt),
                  force_general=kw.pop("force_general", False), walk_early=kw.pop("walk_early", False))
     try:
         oa, ot = run_workload(orc, w)
@@ -105,16 +107,19 @@ def test_fuzz_stress_sweep():
     """The same mutations over many more seeds, every one also on the forced general path
     (the passes, the side sort and the headroom scan this sweep is for)."""
     first, count = (int(x) for x in STRESS.split(":"))
+    big = os.environ.get("TB_FUZZ_BIG") == "1"  # full-size batches, more accounts
     for seed in range(first, first + count):
         rng = np.random.default_rng(1000 + seed)
         nb = int(rng.integers(2, 6))
-        batch = int(rng.integers(50, 700))
-        w = workload.config1(transfer_count=nb * batch, account_count=int(rng.integers(3, 40)), seed=seed,
-                             batch=batch)
+        batch = int(rng.integers(500, 8191)) if big else int(rng.integers(50, 700))
+        w = workload.config1(transfer_count=nb * batch, account_count=int(rng.integers(3, 300 if big else 40)),
+                             seed=seed, batch=batch)
         w = _mutate(w, rng, [0.0005, 0.005, 0.03, 0.15][seed % 4])
         _check(w)
         _check(w, force_general=True)
         if seed % 5 == 0:
             _check(w, split=1)
+        if seed % 7 == 0:
+            _check(w, force_general=True, walk_early=True)
         if seed % 50 == 0:
             print(f"fuzz stress: seed {seed} ok", flush=True, file=sys.stderr)

@@ -802,12 +802,20 @@ static void ensure_h_rc(tbgpu_ctx* c, u64 nb) {
 static u32 general_chunk_batches() {
     static const u32 v = [] {  // TBGPU_CHUNK_BATCHES: experiments only
         const char* e = getenv("TBGPU_CHUNK_BATCHES");
-        return e ? (u32)strtoul(e, nullptr, 0) : 20u;  // config 3 (r02): 8: 104, 12: 130, 16: 140, 20: 148, 24: 143, 30: 146, 40: 139 M/s
+        // config 3, 60-batch calls (r04, profiles/r04/chunk_sweep2.sh): 16: 167-170, 20: 184-188,
+        // 24: 182-186, 32 (then 28): 189-196, 40 (then 20): 182-183 M/s; cut evenly since
+        return e ? (u32)strtoul(e, nullptr, 0) : 32u;
     }();
     return v;
 }
 
+// A chunk limit cuts the remaining batches into equal chunks (60 batches at a limit of
+// 32: two of 30, not 32 + 28), so no short chunk pays the fixed point's setup alone.
 static u32 chunk_end(const tbgpu_ctx* c, const uint32_t* counts, u32 b0, u32 nb, u32 max_batches = ~0u) {
+    if (max_batches != ~0u && max_batches > 0 && nb > b0) {
+        const u32 rest = nb - b0, k = (rest + max_batches - 1) / max_batches;
+        max_batches = (rest + k - 1) / k;
+    }
     u64 ev = 0;
     u32 b = b0;
     while (b < nb && b - b0 < c->bmax - 2 && b - b0 < max_batches) {

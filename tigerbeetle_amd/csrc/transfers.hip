@@ -978,7 +978,10 @@ __device__ __forceinline__ bool eval_complex_one(const Tables& T, const TrArgs& 
 // take the complex list (dispatched first: their events are the longer dependent-load
 // chains), the rest the simple list.  Two launches ran the lists one after the other;
 // here the complex list's latency hides under the simple list's work.
-constexpr u32 EV_THREADS = 256;
+#ifndef TR_EV_THREADS
+#define TR_EV_THREADS 256
+#endif
+constexpr u32 EV_THREADS = TR_EV_THREADS;
 __global__ __launch_bounds__(EV_THREADS) void tr_eval_lists(Tables T, TrArgs C, EvalState S, EvalState D,
                                                             const Bal4* __restrict__ bb, PassGate g, u32 n_simple,
                                                             u32 n_complex, u32 nbc, u32* chg, u32* chg_next,

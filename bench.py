@@ -74,7 +74,7 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def pmc_traffic(config: int, accounts: int, kernel=None):
+def pmc_traffic(config: int, accounts: int, kernel=None, id_order: str = "sequential"):
     """HBM bytes per launch from the newest committed rocprofv3 PMC summary of THIS
     workload (profiles/rNN/traffic*.json, written by profiles/collect.sh +
     summarize.py on the same bench command and tagged with its config and account
@@ -89,7 +89,8 @@ def pmc_traffic(config: int, accounts: int, kernel=None):
             meta = d["_meta"]
         except (OSError, KeyError, ValueError, TypeError):
             continue
-        if meta.get("config") != config or meta.get("accounts") != accounts:
+        if meta.get("config") != config or meta.get("accounts") != accounts or \
+                meta.get("id_order", "sequential") != id_order:
             continue
         rel = os.path.relpath(f, ROOT)
         ev = meta["events_per_step"]
@@ -102,7 +103,8 @@ def pmc_traffic(config: int, accounts: int, kernel=None):
         else:
             continue
         return round(per), f"{rel}: 2xFETCH_SIZE+WRITE_SIZE, {what} ({per / ev:.1f} B/transfer)"
-    return None, f"no rocprofv3 PMC summary of config {config} with {accounts} accounts under profiles/"
+    return None, (f"no rocprofv3 PMC summary of config {config} with {accounts} accounts"
+                  f"{'' if id_order == 'sequential' else ', ' + id_order + ' ids'} under profiles/")
 
 
 def query_phase(eng, w, acc_n, torch, dev, count=100, batch=1024):
@@ -495,7 +497,13 @@ SUBCONFIGS = (
     # config-4 step on a one-rank group (the same workload `--gpus N > 1` times), each
     # a bench.py child with a bounded CPU-baseline sample
     ("config1", ["--config", "1", "--steps", "3", "--warmup", "1"]),
+    # the reference benchmark's --id-order=random (src/tigerbeetle/cli.zig:205): u128
+    # pseudo-UUID ids, so the hashed account index, the hashed id insert and the call's
+    # duplicate check instead of the direct-mapped directory and the sorted id run
+    ("config1_random", ["--config", "1", "--id-order", "random", "--steps", "3", "--warmup", "1"]),
     ("config3", ["--config", "3", "--steps", "3", "--warmup", "1"]),
+    # config 5's per-GPU ledger shard (100M accounts, 1/8 of 1B transfers), generated in HBM
+    ("config5", ["--config", "5", "--steps", "3", "--warmup", "1"]),
     ("scaling_n1", ["--routed", "--steps", "3", "--warmup", "1"]),
 )
 SUB_DROP = ("metric", "higher_is_better", "vs_baseline", "dtype", "data", "scaling", "unit", "queries", "host_path",
@@ -582,6 +590,9 @@ def main():
     ap.add_argument("--batches-per-step", type=int, default=None,
                     help="default 1000 (config 1/2: a whole BASELINE config-2 run per call), 60 for config 3")
     ap.add_argument("--accounts", type=int, default=None)
+    ap.add_argument("--id-order", default="sequential", choices=("sequential", "random", "reversed"),
+                    help="configs 1 and 2: the reference benchmark's --id-order (src/tigerbeetle/cli.zig:205, "
+                         "IdPermutation, src/testing/id.zig:28-48) for account and transfer ids")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-queries", action="store_true", help="skip the query phase (after the timed region)")
@@ -664,7 +675,7 @@ def main():
     t_gen = time.time()
     c5 = None
     cache = os.environ.get("TB_BENCH_CACHE")  # diagnostics only: reuse a generated workload across runs
-    ckey = f"c{args.config}_{args.accounts}_{n_batches}_{42 + rank}"
+    ckey = f"c{args.config}_{args.accounts}_{n_batches}_{42 + rank}_{args.id_order}"
     if cache and args.config != 5 and os.path.exists(os.path.join(cache, ckey + ".npz")):
         z = np.load(os.path.join(cache, ckey + ".npz"))
         w = workload.Workload(str(z["name"]), z["accounts"], z["account_counts"], z["transfers"], z["transfer_counts"],
@@ -677,7 +688,7 @@ def main():
         w = None
     elif args.config == 2:
         acc_n = args.accounts or 1_000_000
-        w = workload.config2(transfer_count=n_transfers, account_count=acc_n, seed=42 + rank)
+        w = workload.config2(transfer_count=n_transfers, account_count=acc_n, seed=42 + rank, id_order=args.id_order)
     elif args.config == 4:
         acc_n = args.accounts or 10_000_000
         w = workload.config4(transfer_count=n_transfers, ledgers=1000, accounts_per_ledger=acc_n // 1000,
@@ -688,7 +699,7 @@ def main():
         n_batches = len(w.transfer_counts)  # + the funding batches
     else:
         acc_n = args.accounts or 10_000
-        w = workload.config1(transfer_count=n_transfers, account_count=acc_n, seed=42 + rank)
+        w = workload.config1(transfer_count=n_transfers, account_count=acc_n, seed=42 + rank, id_order=args.id_order)
     log(f"[rank {rank}] generated {n_transfers} transfers / {acc_n} accounts in {time.time() - t_gen:.1f}s")
     if cache and w is not None and not os.path.exists(os.path.join(cache, ckey + ".npz")):
         os.makedirs(cache, exist_ok=True)
@@ -831,7 +842,7 @@ def main():
     if fast:
         commit_ms = phase[names.index("classify")] / K
         achieved = per_rank / K * COMMIT_BYTES_PER_TRANSFER / (commit_ms * 1e-3) / 1e9 if commit_ms > 0 else 0.0
-        traffic, traffic_src = pmc_traffic(args.config, acc_n, kernel="fp_commit")
+        traffic, traffic_src = pmc_traffic(args.config, acc_n, kernel="fp_commit", id_order=args.id_order)
         kernel = "fp_commit"
         basis = (f"{COMMIT_BYTES_PER_TRANSFER} B/transfer x {B * BATCH_MAX} transfers per launch "
                  f"/ fp_commit launch time ({commit_ms:.4f} ms, HIP events on the engine stream)")
@@ -839,7 +850,7 @@ def main():
         call_ms = dev_ms / K
         algo = (per_rank - n_pv) * ALGO_BYTES_PER_TRANSFER + n_pv * PV_BYTES + 8 * non_ok // world
         achieved = algo / K / (call_ms * 1e-3) / 1e9 if call_ms > 0 else 0.0
-        traffic, traffic_src = pmc_traffic(args.config, acc_n, kernel=None)
+        traffic, traffic_src = pmc_traffic(args.config, acc_n, kernel=None, id_order=args.id_order)
         kernel = "general path (every kernel of the call)"
         basis = (f"{ALGO_BYTES_PER_TRANSFER} B x {per_rank - n_pv} transfers + {PV_BYTES} B x {n_pv} posts/voids "
                  f"+ 8 B x {non_ok // world} non-ok replies over {K} calls / call device time "
@@ -922,6 +933,8 @@ def main():
                                          "linked pairs (ids ledger << 32 | k: the blocked directory)",
                                       5: "1000 ledgers, one 1/8 ledger shard of 1B transfers (the per-GPU shard), "
                                          "uniform pairs within a ledger, generated in HBM"}[args.config]
+                                   + ("" if args.id_order == "sequential" else
+                                      f", --id-order={args.id_order} account and transfer ids (IdPermutation)")
                                    + f", {B} x 8190-transfer batches per step (streamed, HBM-resident)",
                        "batches_per_step": B, "transfers_per_step_per_gpu": B * BATCH_MAX,
                        "parallelism": f"ledger-shard x{world}"},

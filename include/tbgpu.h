@@ -294,7 +294,8 @@ uint32_t tbgpu_create_transfers(tbgpu_ctx* ctx, uint64_t timestamp,
  * staging slot and returns; tbgpu_prefetch_wait returns once the copy has landed (the
  * callback's point).  The next tbgpu_create_transfers with the same `events` pointer
  * and `count` commits from the staged copy (no copy inside the commit); any other
- * create call discards it.  As in the reference, the prepare's body must not change
+ * create call (accounts, transfers, batches, device and routed forms), an import,
+ * tbgpu_reset and tbgpu_open discard it.  As in the reference, the prepare's body must not change
  * between prefetch and commit.  Returns 0, or -22 when count exceeds a batch. */
 int tbgpu_prefetch_transfers(tbgpu_ctx* ctx, const tbgpu_transfer_t* events, uint32_t count);
 int tbgpu_prefetch_wait(tbgpu_ctx* ctx);

@@ -8,7 +8,7 @@ import time
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from tigerbeetle_amd import workload  # noqa: E402
 from tigerbeetle_amd.engine import Engine  # noqa: E402
 from tigerbeetle_amd.types import TRANSFER_DTYPE  # noqa: E402

@@ -82,3 +82,76 @@ def test_open_rejects_bad_images():
         assert a.transfer_count() == len(w.transfers)
     finally:
         a.close()
+
+
+def _shard_engine(n_acc, world, rank, hashed_max=0):
+    from tigerbeetle_amd.engine import Engine
+    return Engine(accounts_max=n_acc + 16, directory_max=n_acc + 16, hashed_max=hashed_max or n_acc + 16,
+                  transfers_max=1 << 16, history_max=1024, events_per_call_max=1 << 14,
+                  shard_world=world, shard_rank=rank)
+
+
+def test_ledger_shard_checkpoint_round_trip():
+    """A ledger shard's image: it names its world and rank, opens only
+    into the ctx of the same shard (not another rank's, not an unsharded ctx, and an
+    unsharded image not into a shard ctx), and checkpoint -> open -> checkpoint gives
+    the same bytes.  Accounts have random u128 ids (hash index) and sequential ones
+    (directory), across 8 ledgers; each shard commits transfers of its own ledgers."""
+    from tigerbeetle_amd.types import ACCOUNT_DTYPE, TRANSFER_DTYPE
+    rng = np.random.default_rng(5)
+    n = 800
+    acc = np.zeros(n, dtype=ACCOUNT_DTYPE)
+    acc["id_lo"] = np.arange(1, n + 1, dtype=np.uint64)
+    rnd = np.arange(n) % 2 == 1  # every other account: a random u128 id
+    acc["id_lo"][rnd] = rng.integers(1, 1 << 62, rnd.sum(), dtype=np.uint64)
+    acc["id_hi"][rnd] = rng.integers(1, 1 << 62, rnd.sum(), dtype=np.uint64)
+    acc["ledger"] = (np.arange(n) % 8 + 1).astype(np.uint32)
+    acc["code"] = 1
+    world = 2
+    engines = [_shard_engine(n, world, r) for r in range(world)]
+    other = _shard_engine(n, world, 1)
+    plain = _engine(workload.config1(transfer_count=10, account_count=n, seed=1))
+    try:
+        for r, e in enumerate(engines):
+            _, rc = e.create_accounts_batches(np.array([n + 1], np.uint64), np.array([n], np.uint32), acc)
+            assert int(rc.sum()) == 0
+            own = np.nonzero(acc["ledger"] % world == r)[0]
+            t = np.zeros(400, dtype=TRANSFER_DTYPE)
+            t["id_lo"] = np.arange(1, 401) + 1000 * r
+            pick = own[rng.integers(0, len(own), (400, 2))]
+            same = acc["ledger"][pick[:, 0]] == acc["ledger"][pick[:, 1]]
+            pick[~same, 1] = pick[~same, 0]  # (an account with itself: accounts_must_be_different)
+            t["debit_account_id_lo"], t["debit_account_id_hi"] = acc["id_lo"][pick[:, 0]], acc["id_hi"][pick[:, 0]]
+            t["credit_account_id_lo"], t["credit_account_id_hi"] = acc["id_lo"][pick[:, 1]], acc["id_hi"][pick[:, 1]]
+            t["ledger"] = acc["ledger"][pick[:, 0]]
+            t["code"] = 1
+            t["amount_lo"] = 5
+            e.create_transfers_batches(np.array([n + 403 + r], np.uint64), np.array([400], np.uint32), t)
+        for r, e in enumerate(engines):
+            image = e.checkpoint()
+            assert image[8:12].view(np.uint32)[0] == 2  # version 2: a shard's image
+            assert image[12:16].view(np.uint32)[0] == (world << 16 | r)
+            wrong = other if r == 0 else _shard_engine(n, world, 0)
+            try:
+                assert wrong.open(image) == -22, "another rank's ctx accepted the image"
+            finally:
+                if wrong is not other:
+                    wrong.close()
+            assert plain.open(image) == -22, "an unsharded ctx accepted a shard image"
+            fresh = _shard_engine(n, world, r)
+            try:
+                assert fresh.open(image) == 0
+                assert np.array_equal(fresh.checkpoint(), image), "restored shard image differs"
+                # an image whose hashed ids exceed the ctx's account index is refused
+                small = _shard_engine(n, world, r, hashed_max=64)
+                try:
+                    assert small.open(image) == -28
+                finally:
+                    small.close()
+            finally:
+                fresh.close()
+        plain_img = plain.checkpoint()
+        assert engines[0].open(plain_img) == -22, "a shard ctx accepted an unsharded image"
+    finally:
+        for e in engines + [other, plain]:
+            e.close()

@@ -40,9 +40,12 @@ def _backend(kind, w, rank=0, world=1):
     return oracle.Oracle(len(w.accounts), 1 << 14)
 
 
-def _worker(rank, world, port, out_dir, spec, kind="oracle", device_step=False, max_rounds=None, vectorized=True):
+def _worker(rank, world, port, out_dir, spec, kind="oracle", device_step=False, max_rounds=None, vectorized=True,
+            skew_dry_rank=None):
     import torch.distributed as dist
     from tigerbeetle_amd.shard import Comm, ShardedStateMachine
+    if skew_dry_rank == rank:
+        _skew_dry_runs()
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -85,6 +88,23 @@ def _worker(rank, world, port, out_dir, spec, kind="oracle", device_step=False, 
         dist.destroy_process_group()
 
 
+def _skew_dry_runs():
+    """This rank's dry runs answer a wrong code for every event outside a spanning
+    chain (the dry run's breaks, which only read spanning members, stay right), so
+    this rank alone sees its commit differ from its dry run."""
+    from tigerbeetle_amd import shard_vec
+    real = shard_vec._commit_vec
+
+    def skewed(sm, T, glob, E, P, G, I, C, in_span, lastloc, mlast, brk, dry):
+        res = real(sm, T, glob, E, P, G, I, C, in_span, lastloc, mlast, brk, dry)
+        if dry:
+            res = res.copy()
+            res[~in_span] = 999
+        return res
+
+    shard_vec._commit_vec = skewed
+
+
 def _make(spec):
     kind, seed, world, steps, B = spec
     if kind == "mix":
@@ -99,10 +119,11 @@ def _make(spec):
     return config4_small(seed, world, steps, B)
 
 
-def _check(spec, world, kind="oracle", device_step=False, max_rounds=None, vectorized=True):
+def _check(spec, world, kind="oracle", device_step=False, max_rounds=None, vectorized=True, skew_dry_rank=None):
     import torch.multiprocessing as mp
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d, spec, kind, device_step, max_rounds, vectorized),
+        mp.spawn(_worker, args=(world, _free_port(), d, spec, kind, device_step, max_rounds, vectorized,
+                                skew_dry_rank),
                  nprocs=world, join=True)
         outs = [pickle.load(open(os.path.join(d, f"r{r}.pkl"), "rb")) for r in range(world)]
     return verify(_make(spec), outs, world)
@@ -238,3 +259,14 @@ def test_ledger_shard_rows_exists_codes_from_the_owner(world):
     accounts that those failures break roll back alike on every rank."""
     stats = _check(("mixa", 41 + world, world, 2, 2), world, kind="ledgershard")
     assert stats["steps"] > 0
+
+
+@pytest.mark.timeout(300)
+def test_dry_commit_mismatch_on_one_rank_only():
+    """when only one rank's commit differs from its dry run, the
+    check of the breaks (a collective) must still be entered by every rank or none:
+    the decision is all-reduced first.  Rank 1's dry runs are skewed outside the
+    spanning chains; the step completes on both ranks, bit-exact, and rank 0 (whose
+    own results agree) counts the mismatch too."""
+    stats = _check(("mixr", 73, 2, 3, 2), 2, device_step=True, skew_dry_rank=1)
+    assert stats.get("dry_commit_mismatch", 0) > 0

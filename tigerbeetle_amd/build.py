@@ -6,6 +6,7 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -28,14 +29,38 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def build_stamp(sources, headers, defines) -> str:
+    """sha256 of every source and header the library is built from, the compiler
+    flags and the defines: the library is rebuilt whenever its stamp differs, whatever
+    the files' modification times say (a copied tree keeps mtimes that need not order
+    sources before the library)."""
+    h = hashlib.sha256()
+    for f in list(sources) + list(headers):
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    h.update(" ".join([HIPCC, *CXXFLAGS, *defines]).encode())
+    return h.hexdigest()
+
+
 def build_lib(verbose: bool = False, force: bool = False, defines=(), build_dir: str = BUILD,
               lib: str = LIB) -> str:
     """Compile csrc/*.hip and link `lib`.  `defines` (e.g. ["FP_WAVES_PER_EU=8"]) and
     a separate `build_dir`/`lib` build timing variants for experiments; the product
-    library is the default one."""
+    library is the default one, and it never takes TBGPU_TIMING_VARIANTS (which admits
+    the results-changing ablations, csrc/fast.h)."""
+    if os.path.abspath(lib) == LIB and any(d.split("=")[0] == "TBGPU_TIMING_VARIANTS" for d in defines):
+        raise ValueError("the product library is never built with TBGPU_TIMING_VARIANTS")
     os.makedirs(build_dir, exist_ok=True)
     sources = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     headers = sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(ROOT, "include", "tbgpu.h")]
+    stamp = build_stamp(sources, headers, defines)
+    stamp_file = lib + ".stamp"
+    try:
+        with open(stamp_file) as fh:
+            force = force or fh.read().strip() != stamp
+    except OSError:
+        force = True
     objs = []
     jobs = []
     for src in sources:
@@ -55,6 +80,8 @@ def build_lib(verbose: bool = False, force: bool = False, defines=(), build_dir:
         if r.returncode != 0:
             sys.stderr.write(r.stdout + r.stderr)
             raise RuntimeError("link failed")
+        with open(stamp_file, "w") as fh:
+            fh.write(stamp + "\n")
     return lib
 
 
@@ -62,7 +89,8 @@ def build_variant(name: str, defines) -> str:
     """build/var_<name>/libtbgpu.so, loaded instead of the product library when
     TBGPU_LIB points at it (profiles/variants.py)."""
     d = os.path.join(BUILD, "var_" + name)
-    return build_lib(defines=defines, build_dir=d, lib=os.path.join(d, "libtbgpu.so"), force=True)
+    return build_lib(defines=["TBGPU_TIMING_VARIANTS", *defines], build_dir=d, lib=os.path.join(d, "libtbgpu.so"),
+                     force=True)
 
 
 def build_oracle() -> str:

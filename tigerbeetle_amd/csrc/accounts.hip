@@ -240,7 +240,8 @@ __global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const
     if (!(ok[i] & 2)) return;
     Account a = C.ev[i];
     if (!ledger_owned(T, a.ledger)) {  // another ledger shard stores the row: the directory entry only
-        acc_insert(T, a.id, ROW_FOREIGN, a.ledger, a.flags, a.code);
+        if (!acc_insert(T, a.id, ROW_FOREIGN, a.ledger, a.flags, a.code))
+            atomicOr(&C.counters[CNT_FLAGS], (u32)FL_CAPACITY);  // the account index is full
         return;
     }
     a.timestamp = C.ts[i];
@@ -252,7 +253,7 @@ __global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const
     }
     const u32 row = (u32)(row_base + rk[i].x);
     T.acc[row] = a;
-    acc_insert(T, a.id, row, a.ledger, a.flags, a.code);
+    if (!acc_insert(T, a.id, row, a.ledger, a.flags, a.code)) atomicOr(&C.counters[CNT_FLAGS], (u32)FL_CAPACITY);
 }
 
 // ---------------------------------------------- the clean call in two passes --
@@ -321,7 +322,7 @@ __global__ __launch_bounds__(AF_THREADS) void ac_fast_index(Tables T, AcArgs C, 
         const uint4 m = ((const uint4*)&T.acc[row])[7];
         const u128 id = ((u128)(((u64)k.w << 32) | k.z) << 64) | (((u64)k.y << 32) | k.x);
         const u16 code = (u16)(m.y & 0xFFFFu), flags = (u16)(m.y >> 16);
-        acc_insert(T, id, row, m.x, flags, code);
+        if (!acc_insert(T, id, row, m.x, flags, code)) atomicOr(&C.counters[CNT_FLAGS], (u32)FL_CAPACITY);
     }
     if (blockIdx.x == 0) {
         // replies: none; commit_timestamp: the latest event's (every event is accepted)

@@ -36,6 +36,12 @@ struct Tables {
     // Set once any balance high word reaches 2^62: until then a call of < 2^32
     // events with amounts < 2^64 cannot overflow a u128 sum (fast.hip).
     u32* big;
+    // Account index occupancy: [0] hash-index entries reserved so far, [1] nonzero once
+    // an insert was refused because `hash_limit` (half the slots: load <= 0.5, so every
+    // probe ends at an empty slot) was reached.  Ledger shards insert other shards'
+    // accounts here too, which the owned-row capacity check does not cover.
+    u32* hcount;
+    u64 hash_limit;
     // Direct-mapped account directory.  Ids (b << 32) | k with b < dense_blocks and
     // 1 <= k <= dense_span have entry b * dense_span + k - 1, describing the account
     // as (row + 1) | (flags & 0xE) << 28 | ledger << 32, 0 = no such account.  Every
@@ -289,10 +295,23 @@ __device__ __forceinline__ u32 acc_row(const Tables& T, u128 id) {
 // Insert of a new account's directory entry: the direct-mapped entry for ids it
 // covers, a hash-index slot (claimed by CAS on its row word) for the others.  `row`
 // may be ROW_FOREIGN (a ledger shard's entry for another shard's account).
-__device__ __forceinline__ void acc_insert(const Tables& T, u128 id, u32 row, u32 ledger, u16 flags, u16 code) {
+// Returns false (inserting nothing, T.hcount[1] raised) when the hash index is at
+// its load limit: the caller reports FL_CAPACITY and the host aborts the call.
+__device__ __forceinline__ bool acc_insert(const Tables& T, u128 id, u32 row, u32 ledger, u16 flags, u16 code) {
     if (dense_has(T, id)) {
         T.dense[dense_slot(T, id)] = dense_entry(row, ledger, flags);
-        return;
+        return true;
+    }
+    {  // reserve an entry: one atomic per wave for the lanes inserting here
+        const u64 act = __ballot(1);
+        const u32 lane = threadIdx.x & 63, lead = (u32)__ffsll((unsigned long long)act) - 1;
+        u32 base = 0;
+        if (lane == lead) base = atomicAdd(&T.hcount[0], (u32)__popcll(act));
+        base = __shfl(base, lead);
+        if ((u64)base + __popcll(act & ((1ull << lane) - 1)) >= T.hash_limit) {
+            atomicOr(&T.hcount[1], 1u);
+            return false;
+        }
     }
     u64 h = hash128(id) & T.aidx_mask;
     while (atomicCAS(&T.aidx[h].row1, 0u, row + 1) != 0) h = (h + 1) & T.aidx_mask;
@@ -302,6 +321,7 @@ __device__ __forceinline__ void acc_insert(const Tables& T, u128 id, u32 row, u3
     e.ledger = ledger;
     e.flags = flags;
     e.code = code;
+    return true;
 }
 
 // Transfer-id index hash: runs of 16 consecutive ids share one 64-byte line of

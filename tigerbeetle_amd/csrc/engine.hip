@@ -637,6 +637,8 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     c->T.idr = dalloc<u64>(4, &B);
     c->T.xrun = dalloc<u64>(8, &B);
     c->T.big = dalloc<u32>(4, &B);
+    c->T.hcount = c->T.big + 1;        // [1] entries, [2] refused
+    c->T.hash_limit = c->aidx_cap / 2;  // load <= 0.5
     c->T.base = dalloc<u64>(4, &B);
     c->T.shard_world = o.shard_world >= 2 ? o.shard_world : 0;
     c->T.shard_rank = o.shard_world >= 2 ? o.shard_rank : 0;
@@ -662,6 +664,7 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
 
 extern "C" void tbgpu_reset(tbgpu_ctx* c) {
     CallGuard guard_(c, false);
+    c->pf_valid = false;
     HIP_CHECK(hipMemsetAsync(c->T.aidx, 0, c->aidx_cap * sizeof(AccIdx), c->stream));
     HIP_CHECK(hipMemsetAsync(c->T.xful, 0, c->xrow_cap, c->stream));
     HIP_CHECK(hipMemsetAsync(c->T.xidx, 0, c->xidx_cap * sizeof(u32), c->stream));
@@ -669,7 +672,7 @@ extern "C" void tbgpu_reset(tbgpu_ctx* c) {
     HIP_CHECK(hipMemsetAsync(c->T.idr, 0, 2 * sizeof(u64), c->stream));                  // max = 0
     HIP_CHECK(hipMemsetAsync(c->T.idr + 2, 0xFF, 2 * sizeof(u64), c->stream));           // min = ~0
     HIP_CHECK(hipMemsetAsync(c->T.xrun, 0, 8 * sizeof(u64), c->stream));                 // empty run
-    HIP_CHECK(hipMemsetAsync(c->T.big, 0, sizeof(u32), c->stream));
+    HIP_CHECK(hipMemsetAsync(c->T.big, 0, 4 * sizeof(u32), c->stream));  // the guard and the index occupancy
     HIP_CHECK(hipMemsetAsync(c->T.base, 0, 4 * sizeof(u64), c->stream));
     if (c->T.dense_n) HIP_CHECK(hipMemsetAsync(c->T.dense, 0, c->T.dense_n * sizeof(u64), c->stream));
     if (c->ximp) HIP_CHECK(hipMemsetAsync(c->ximp, 0, c->xrow_cap, c->stream));
@@ -1754,7 +1757,8 @@ extern "C" uint64_t tbgpu_create_transfers_routed_device(tbgpu_ctx* c, uint32_t 
 static uint64_t routed(tbgpu_ctx* c, uint32_t batch_count, const uint32_t* counts, const void* events,
                        const uint64_t* event_timestamps, const uint8_t* ctl, int dry_run, void* results,
                        uint32_t* result_counts, uint64_t* commit_timestamp, bool device) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, false);
+    c->pf_valid = false;  // any other create call discards a prefetched batch
     u64 n = 0;
     for (u32 b = 0; b < batch_count; b++) n += counts[b];
     if (dry_run && (n > c->nmax || batch_count > c->bmax - 2))
@@ -1779,6 +1783,7 @@ static uint64_t routed(tbgpu_ctx* c, uint32_t batch_count, const uint32_t* count
 
 extern "C" int tbgpu_import_transfers(tbgpu_ctx* c, const tbgpu_transfer_t* rows, uint32_t count) {
     CallGuard guard_(c, false);
+    c->pf_valid = false;
     if (count == 0) return 0;
     // rows already held (committed here or imported before) are skipped: rows are
     // immutable, and the id index must hold each id once
@@ -1882,7 +1887,7 @@ static int route_scatter_any(tbgpu_ctx* c, uint32_t world, uint32_t batch_count,
                              uint64_t first_global_batch, const void* events_device, void* send_events_device,
                              void* send_records_device, uint32_t word_mask, void* send_packed_device,
                              uint64_t* send_counts, uint32_t* send_batch_counts, uint32_t* send_span_counts) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, true);  // the router's send side (may overlap a commit on another thread)
     entry_flush(c->route_stream);
     if (world == 0 || world > 256) return -22;
     std::vector<u32> starts(batch_count + 1, 0);
@@ -2038,6 +2043,7 @@ extern "C" int tbgpu_prefetch_wait(tbgpu_ctx* c) {
 
 extern "C" uint32_t tbgpu_create_transfers(tbgpu_ctx* c, uint64_t timestamp, const tbgpu_transfer_t* events,
                                            uint32_t count, tbgpu_create_transfers_result_t* results) {
+    CallGuard guard_(c, false);
     uint32_t rc = 0;
     const uint64_t ts = timestamp;
     if (c->pf_valid && c->pf_src == (const void*)events && c->pf_n == count) {
@@ -2052,6 +2058,7 @@ extern "C" uint32_t tbgpu_create_transfers(tbgpu_ctx* c, uint64_t timestamp, con
 extern "C" uint64_t tbgpu_create_transfers_batches(tbgpu_ctx* c, uint32_t batch_count, const uint64_t* timestamps,
                                                    const uint32_t* counts, const tbgpu_transfer_t* events,
                                                    tbgpu_create_transfers_result_t* results, uint32_t* result_counts) {
+    CallGuard guard_(c, false);
     c->pf_valid = false;
     return transfers_batches(c, batch_count, timestamps, counts, (const Transfer*)events, false, results, false,
                              result_counts);
@@ -2061,6 +2068,8 @@ extern "C" uint64_t tbgpu_create_transfers_batches_device(tbgpu_ctx* c, uint32_t
                                                           const uint64_t* timestamps, const uint32_t* counts,
                                                           const void* events_device, void* results_device,
                                                           uint32_t* result_counts) {
+    CallGuard guard_(c, false);
+    c->pf_valid = false;
     return transfers_batches(c, batch_count, timestamps, counts, (const Transfer*)events_device, true,
                              (tbgpu_create_transfers_result_t*)results_device, true, result_counts);
 }
@@ -2092,6 +2101,8 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
         HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, CNT_COUNT * sizeof(u32), hipMemcpyDeviceToHost, s));
         wait_stream(s);
         if (!(c->h_counters[CNT_FLAGS] & FL_SLOW)) {
+            if (c->h_counters[CNT_FLAGS] & FL_CAPACITY)
+                tbgpu_fatal("create_accounts", "account index full (hashed_max exceeded)", __FILE__, __LINE__);
             std::fill(counts_host, counts_host + nb, 0u);
             c->n_accounts += n;
             c->stats.iterations = 1;
@@ -2130,7 +2141,9 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
     memcpy(&tot, c->h_base + 4, sizeof tot);
     const u32 flags = c->h_counters[CNT_FLAGS];
     if (!(flags & (FL_CHAINS | FL_MULTI_ID))) {
-        if (flags & FL_CAPACITY) tbgpu_fatal("create_accounts", "accounts_max exceeded", __FILE__, __LINE__);
+        if (flags & FL_CAPACITY)
+            tbgpu_fatal("create_accounts", "account capacity exceeded (accounts_max, or hashed_max for the account "
+                        "index)", __FILE__, __LINE__);
         if (flags & FL_ERROR) tbgpu_fatal("create_accounts", "device error", __FILE__, __LINE__);
         c->stats.iterations = 1;
         c->n_accounts += tot.x;
@@ -2157,7 +2170,9 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
     if (c->n_accounts + tot.x > c->accounts_max) tbgpu_fatal("create_accounts", "accounts_max exceeded", __FILE__, __LINE__);
     ac_launch_apply(c->T, C, A->ok, c->fres, c->ranks, c->n_accounts, c->accounts_max, results_dev, c->counts, s);
     d2h(c, counts_host, c->counts, nb * sizeof(u32), s);
-    wait_stream(s);
+    read_counters(c);
+    if (c->h_counters[CNT_FLAGS] & FL_CAPACITY)
+        tbgpu_fatal("create_accounts", "account index full (hashed_max exceeded)", __FILE__, __LINE__);
     c->n_accounts += tot.x;
     c->n_foreign += tot.z;
 }
@@ -2165,7 +2180,8 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
 static uint64_t accounts_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t* timestamps, const uint32_t* counts,
                                  const Account* events, bool device, tbgpu_create_accounts_result_t* results,
                                  uint32_t* result_counts) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, false);
+    c->pf_valid = false;  // any other create call discards a prefetched batch
     entry_flush(c->stream);
     HIP_CHECK(hipEventRecord(c->ev0, c->stream));
     std::vector<u32> starts;
@@ -2229,7 +2245,7 @@ extern "C" uint32_t tbgpu_create_accounts(tbgpu_ctx* c, uint64_t timestamp, cons
 
 template <typename Row, typename Launch>
 static uint32_t lookup(tbgpu_ctx* c, const tbgpu_uint128_t* ids, uint32_t count, Row* out, Launch launch) {
-    HIP_CHECK(hipSetDevice(c->device));
+    CallGuard guard_(c, false);
     entry_flush(c->stream);
     uint32_t found_total = 0;
     std::vector<Row> rows;
@@ -2494,10 +2510,12 @@ namespace {
 constexpr u64 CK_MAGIC = 0x314B435550474254ull;  // "TBGPUCK1"
 // version 1: one state machine; version 2: a ledger shard's image, which also lists
 // the other shards' accounts its directory knows (n_foreign ForeignAccount records,
-// sorted by id, after the history rows)
+// sorted by id, after the history rows) and names its shard: `shard` = world << 16 |
+// rank.  An image opens only into a ctx of the same kind and, for a shard, the same
+// world and rank.
 struct CkHeader {
     u64 magic;
-    u32 version, reserved;
+    u32 version, shard;
     u64 n_accounts, n_rows, n_hist, commit_ts, checksum;
     u64 n_foreign;
 };
@@ -2562,7 +2580,8 @@ extern "C" uint64_t tbgpu_checkpoint(tbgpu_ctx* c, void* out, uint64_t capacity)
     }
     CkHeader h{};
     h.magic = CK_MAGIC;
-    h.version = nf ? 2 : 1;
+    h.version = c->T.shard_world ? 2 : 1;
+    h.shard = c->T.shard_world ? (c->T.shard_world << 16 | c->T.shard_rank) : 0;
     h.n_foreign = nf;
     h.n_accounts = na;
     h.n_rows = nr;
@@ -2579,12 +2598,27 @@ extern "C" int tbgpu_open(tbgpu_ctx* c, const void* image, uint64_t size) {
     CkHeader h;
     memcpy(&h, image, sizeof h);
     if (h.magic != CK_MAGIC || (h.version != 1 && h.version != 2)) return -22;
-    if (h.version == 1 && h.n_foreign != 0) return -22;
-    if (h.version == 2 && !c->T.shard_world) return -22;  // a ledger shard's image needs a shard ctx
+    if (h.version == 1 && (h.n_foreign != 0 || h.shard != 0)) return -22;
+    // a ledger shard's image only into the ctx of the same shard, and an unsharded one
+    // only into an unsharded ctx
+    if (h.version == 1 && c->T.shard_world) return -22;
+    if (h.version == 2 && (!c->T.shard_world || h.shard != (c->T.shard_world << 16 | c->T.shard_rank))) return -22;
     if (size != sizeof(CkHeader) + ck_payload_bytes(h.n_accounts, h.n_rows, h.n_hist, h.n_foreign)) return -22;
     const u8* p = (const u8*)image + sizeof(CkHeader);
     if (ck_checksum(p, size - sizeof(CkHeader)) != h.checksum) return -22;
     if (h.n_accounts > c->accounts_max || h.n_rows > c->xrow_cap || h.n_hist > c->hist_cap) return -28;
+    {  // the account index: every id outside the directory takes a hash slot (load <= 0.5)
+        auto hashed = [&](u64 lo, u64 hi) {
+            return !(hi == 0 && (lo >> 32) < c->T.dense_blocks && (u64)(u32)lo - 1 < c->T.dense_span);
+        };
+        u64 nhash = 0;
+        const Account* acc = (const Account*)p;
+        for (u64 k = 0; k < h.n_accounts; k++) nhash += hashed((u64)acc[k].id, (u64)(acc[k].id >> 64));
+        const ForeignAccount* fa =
+            (const ForeignAccount*)(p + h.n_accounts * 128 + h.n_rows * 130 + h.n_hist * 256);
+        for (u64 k = 0; k < h.n_foreign; k++) nhash += hashed(fa[k].id_lo, fa[k].id_hi);
+        if (nhash > c->T.hash_limit) return -28;
+    }
     tbgpu_reset(c);
     const u64 na = h.n_accounts, nr = h.n_rows, nh = h.n_hist;
     hipStream_t s = c->stream;
@@ -2624,7 +2658,9 @@ extern "C" int tbgpu_open(tbgpu_ctx* c, const void* image, uint64_t size) {
         launch_import_transfers(c->T, c->T.xrows + off, k, off, s);  // rows in place: index + key range
     }
     h2d(c, c->T.commit_ts, &h.commit_ts, sizeof(u64), s);
-    wait_stream(s);
+    u32 refused = 0;
+    d2h(c, &refused, c->T.hcount + 1, sizeof(u32), s);
+    if (refused) tbgpu_fatal("open", "account index full after the capacity check", __FILE__, __LINE__);
     c->n_accounts = na;
     c->n_foreign = nf;
     c->n_rows = nr;

@@ -38,6 +38,11 @@ enum { ABL_DUP = 1, ABL_BALANCES = 2, ABL_ROWS = 4, ABL_LOOKBACK = 8, ABL_EVENT 
 #ifndef FP_ABLATE
 #define FP_ABLATE 0
 #endif
+// Variants whose results are wrong (ablations that skip work, for timing only) build
+// only with TBGPU_TIMING_VARIANTS, which build.py never passes to the product library.
+#if (FP_ABLATE != 0 || defined(FP_NOFLUSH) || defined(FP_SKIP_HOT)) && !defined(TBGPU_TIMING_VARIANTS)
+#error "results-changing timing variant without TBGPU_TIMING_VARIANTS (never the product build)"
+#endif
 
 // A small call's batch block (starts, then timestamps: engine.hip upload_batches)
 // written by fp_prep from its arguments instead of by a launch of its own.

@@ -362,9 +362,10 @@ def round_vec(sm, glob, T, my_events, replies, start):
         if nb == brk:
             res2 = _commit_vec(sm, T, glob, mE[mask], mP[mask], mG[mask], mI[mask], mC[mask], in_span[mask],
                                lastloc[mask], mlast[mask], brk, dry=False)
-            if not np.array_equal(res2, res):
-                # the commit is exact as long as it breaks every spanning chain where its
-                # control said (collective: every rank decides alike)
+            # the commit is exact as long as it breaks every spanning chain where its
+            # control said.  Whether to check is decided collectively first: `_breaks`
+            # runs collectives, so every rank must enter it or none
+            if int(allreduce_max(comm, np.array([int(not np.array_equal(res2, res))], np.int64))[0]):
                 sm.stats["dry_commit_mismatch"] = sm.stats.get("dry_commit_mismatch", 0) + 1
                 if _breaks(sm, mP[mask], mC[mask], in_span[mask], res2) != brk:
                     raise AssertionError("sharded commit: a committed chain broke elsewhere than its dry run "

@@ -77,9 +77,46 @@ def _codes(rng, n):
     return np.minimum(c, 0xFFFF).astype(np.uint16)  # +| saturating
 
 
-def make_accounts(ids: np.ndarray, ledger, code=1, flags=None) -> np.ndarray:
+ID_ORDERS = ("sequential", "random", "reversed")
+
+
+def _mix64(x: np.ndarray) -> np.ndarray:
+    """splitmix64's finalizer over a u64 array (wrapping arithmetic)."""
+    with np.errstate(over="ignore"):
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return x ^ (x >> np.uint64(31))
+
+
+def encode_ids(data: np.ndarray, order: str = "sequential", seed: int = 0):
+    """IdPermutation.encode (src/testing/id.zig:28-48) as the benchmark applies it
+    (`--id-order`, src/tigerbeetle/cli.zig:205, benchmark_load.zig:134-138): returns
+    the u128 ids of `data` (u64 indices, the benchmark's index + 1) as (lo, hi).
+      sequential  identity;
+      reversed    maxInt(u128) - data;
+      random      data << 32 with bits 0..32 and 96..128 random (a pseudo-UUID whose
+                  index is recoverable).  The reference seeds Zig's DefaultPrng with
+                  seed + data; here a splitmix64 stream of seed + data gives the bits
+                  (the layout, not Zig's stream, is reproduced)."""
+    d = np.asarray(data, dtype=np.uint64)
+    if order == "sequential":
+        return d.copy(), np.zeros_like(d)
+    if order == "reversed":
+        return ~d, np.full_like(d, U64_MAX)
+    if order != "random":
+        raise ValueError(f"id order {order!r}")
+    with np.errstate(over="ignore"):
+        k = np.uint64(seed & U64_MAX) + d
+        r0 = _mix64(k * np.uint64(2) + np.uint64(0x9E3779B97F4A7C15))
+        r1 = _mix64(k * np.uint64(2) + np.uint64(1) + np.uint64(0x9E3779B97F4A7C15))
+    lo = (d << np.uint64(32)) | (r0 & np.uint64(0xFFFFFFFF))
+    hi = (d >> np.uint64(32)) | (r1 & np.uint64(0xFFFFFFFF00000000))
+    return lo, hi
+
+
+def make_accounts(ids: np.ndarray, ledger, code=1, flags=None, ids_hi=None) -> np.ndarray:
     a = np.zeros(len(ids), dtype=ACCOUNT_DTYPE)
-    _set128(a, "id", ids.astype(np.uint64))
+    _set128(a, "id", ids.astype(np.uint64), None if ids_hi is None else ids_hi.astype(np.uint64))
     a["ledger"] = ledger
     a["code"] = code
     if flags is not None:
@@ -87,12 +124,14 @@ def make_accounts(ids: np.ndarray, ledger, code=1, flags=None) -> np.ndarray:
     return a
 
 
-def _transfers(rng, ids, dr, cr, ledger):
+def _transfers(rng, ids, dr, cr, ledger, order="sequential", id_seed=0):
+    """Transfers with ids encode(ids), accounts encode(dr), encode(cr) under the id
+    order (the benchmark uses one permutation for both, benchmark_load.zig:296-301)."""
     n = len(ids)
     t = np.zeros(n, dtype=TRANSFER_DTYPE)
-    _set128(t, "id", ids.astype(np.uint64))
-    _set128(t, "debit_account_id", dr.astype(np.uint64))
-    _set128(t, "credit_account_id", cr.astype(np.uint64))
+    _set128(t, "id", *encode_ids(ids, order, id_seed))
+    _set128(t, "debit_account_id", *encode_ids(dr, order, id_seed))
+    _set128(t, "credit_account_id", *encode_ids(cr, order, id_seed))
     _set128(t, "user_data_128", rng.integers(0, U64_MAX, n, dtype=np.uint64, endpoint=True),
             rng.integers(0, U64_MAX, n, dtype=np.uint64, endpoint=True))
     t["user_data_64"] = rng.integers(0, U64_MAX, n, dtype=np.uint64, endpoint=True)
@@ -103,17 +142,26 @@ def _transfers(rng, ids, dr, cr, ledger):
     return t
 
 
+def _id_seed(seed: int) -> int:
+    """The permutation's seed, drawn from the workload's seed as the benchmark draws it
+    from its PRNG (`.random = random.int(u64)`, benchmark_load.zig:134-138)."""
+    return int(np.random.default_rng(seed ^ 0x1D0D).integers(0, U64_MAX, dtype=np.uint64, endpoint=True))
+
+
 def config1(transfer_count: int = 10_000_000, account_count: int = 10_000, seed: int = 42,
-            batch: int = BATCH_MAX) -> Workload:
+            batch: int = BATCH_MAX, id_order: str = "sequential") -> Workload:
     rng = np.random.default_rng(seed)
+    ids_seed = _id_seed(seed)
     acc_ids = np.arange(1, account_count + 1, dtype=np.uint64)
-    accounts = make_accounts(acc_ids, ledger=2)
+    lo, hi = encode_ids(acc_ids, id_order, ids_seed)
+    accounts = make_accounts(lo, ledger=2, ids_hi=hi)
     dr = rng.integers(0, account_count, transfer_count, dtype=np.uint64)
     cr = rng.integers(0, account_count, transfer_count, dtype=np.uint64)
     cr = np.where(dr == cr, (cr + 1) % account_count, cr)  # benchmark_load.zig:291-295
     ids = np.arange(1, transfer_count + 1, dtype=np.uint64)
-    transfers = _transfers(rng, ids, dr + 1, cr + 1, ledger=2)
-    return Workload("config1", accounts, _batches(account_count), transfers, _batches(transfer_count, batch))
+    transfers = _transfers(rng, ids, dr + 1, cr + 1, ledger=2, order=id_order, id_seed=ids_seed)
+    name = "config1" if id_order == "sequential" else f"config1-{id_order}"
+    return Workload(name, accounts, _batches(account_count), transfers, _batches(transfer_count, batch))
 
 
 def zipf_sampler(rng, n: int, s: float):
@@ -127,20 +175,23 @@ def zipf_sampler(rng, n: int, s: float):
 
 
 def config2(transfer_count: int = 8_190_000, account_count: int = 1_000_000, seed: int = 42, s: float = 0.99,
-            batch: int = BATCH_MAX) -> Workload:
+            batch: int = BATCH_MAX, id_order: str = "sequential") -> Workload:
     rng = np.random.default_rng(seed)
+    ids_seed = _id_seed(seed)
     perm = rng.permutation(account_count).astype(np.uint64)  # rank -> account index
     if os.environ.get("TB_ZIPF_IDENTITY") == "1":  # timing experiments only: rank r is row r (profiles/r04/var_c2.sh)
         perm = np.arange(account_count, dtype=np.uint64)
     acc_ids = np.arange(1, account_count + 1, dtype=np.uint64)
-    accounts = make_accounts(acc_ids, ledger=1)
+    lo, hi = encode_ids(acc_ids, id_order, ids_seed)
+    accounts = make_accounts(lo, ledger=1, ids_hi=hi)
     draw = zipf_sampler(rng, account_count, s)
     dr = perm[draw(transfer_count)]
     cr = perm[draw(transfer_count)]
     cr = np.where(dr == cr, (cr + 1) % account_count, cr)
     ids = np.arange(1, transfer_count + 1, dtype=np.uint64)
-    transfers = _transfers(rng, ids, dr + 1, cr + 1, ledger=1)
-    return Workload("config2", accounts, _batches(account_count), transfers, _batches(transfer_count, batch))
+    transfers = _transfers(rng, ids, dr + 1, cr + 1, ledger=1, order=id_order, id_seed=ids_seed)
+    name = "config2" if id_order == "sequential" else f"config2-{id_order}"
+    return Workload(name, accounts, _batches(account_count), transfers, _batches(transfer_count, batch))
 
 
 def config4(transfer_count: int = 16_380_000, ledgers: int = 1000, accounts_per_ledger: int = 10_000,

@@ -22,15 +22,22 @@ pinned = torch.empty(len(w.transfers) * 128, dtype=torch.uint8, pin_memory=True)
 view = pinned.numpy().view(TRANSFER_DTYPE)
 view[:] = w.transfers
 offs = np.concatenate([[0], np.cumsum(w.transfer_counts.astype(np.int64))])
+# argv[1]: "single" / "prefetched" (one kind of call only, e.g. for TBGPU_HOST_TRACE=1,
+# whose averages are printed at close), default both
+mode = sys.argv[1] if len(sys.argv) > 1 else "both"
 lat = []
 for k in range(120):
     ev = view[offs[k]:offs[k + 1]]
     t0 = time.perf_counter()
-    if k >= 60:
+    pre = mode == "prefetched" or (mode == "both" and k >= 60)
+    if pre:
         eng.prefetch_transfers(ev)
         eng.prefetch_wait()
     t1 = time.perf_counter()
     eng.create_transfers(int(tts[k]), ev)
     lat.append((time.perf_counter() - t1) * 1e6)
-print("single p50 %.1f us, prefetched commit p50 %.1f us" % (np.median(lat[10:60]), np.median(lat[70:])))
+if mode == "both":
+    print("single p50 %.1f us, prefetched commit p50 %.1f us" % (np.median(lat[10:60]), np.median(lat[70:])))
+else:
+    print("%s p50 %.1f us, p99 %.1f us" % (mode, np.median(lat[10:]), np.percentile(lat[10:], 99)))
 eng.close()

@@ -62,7 +62,7 @@ step() {
     hostpath)
       mkdir -p "$OUT/hostpath"
       timeout -k 10 300 python3 -u profiles/hostpath_trace.py > "$OUT/hostpath/plain.txt" 2>&1 || return 1
-      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/hostpath/kt" -o kt -- \
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/hostpath/kt" -o kt --output-format csv -- \
         python3 -u "$ROOT/profiles/hostpath_trace.py" > "$ROOT/$OUT/hostpath/kt.log" 2>&1) ;;
     fuzz)
       local first=${rest%%:*} r2=${rest#*:} count big=""

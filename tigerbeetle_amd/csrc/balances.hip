@@ -467,7 +467,7 @@ __global__ __launch_bounds__(BF_THREADS) void bs_fused(SideScanArgs A, u64 m, u3
                 if (old.dp != out.dp || old.dpo != out.dpo || old.cp != out.cp || old.cpo != out.cpo) {
                     // a balance moved: its event is due this pass (with its chain)
                     bb[q] = out;
-                    A.dt.ev[par * A.dt.n + (A.sq_ev[q] & 0x7FFFFFFFu)] = pq;
+                    A.dt.ev[par * A.dt.n + (A.sq_ev[q] & SQ_EV)] = pq;
                     const u32 c = A.sq_cs[q];
                     if (!(c & SQ_STANDALONE)) A.dt.chain[par * A.dt.n + (c & SQ_CS)] = pq;
                 }
@@ -639,9 +639,13 @@ __global__ __launch_bounds__(NF_THREADS) void bs_fused_narrow(SideScanArgs A, u6
             if (all) {
                 A.bh[q] = out;
             } else if (old[k] != out) {
-                A.bh[q] = out;  // a balance moved: its event is due this pass (with its chain)
-                A.dt.ev[par * A.dt.n + (ev[k] & 0x7FFFFFFFu)] = pq;
-                if (!(c[k] & SQ_STANDALONE)) A.dt.chain[par * A.dt.n + (c[k] & SQ_CS)] = pq;
+                // a balance moved: its event is due this pass (with its chain) when this
+                // balance can decide its outcome (SQ_SENS); otherwise only the figure moves
+                A.bh[q] = out;
+                if ((ev[k] & SQ_SENS) || A.all_sides) {
+                    A.dt.ev[par * A.dt.n + (ev[k] & SQ_EV)] = pq;
+                    if (!(c[k] & SQ_STANDALONE)) A.dt.chain[par * A.dt.n + (c[k] & SQ_CS)] = pq;
+                }
             }
         }
         run = combine_n(run, e[k]);

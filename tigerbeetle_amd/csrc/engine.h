@@ -184,11 +184,11 @@ constexpr u32 SIDE_CANDS = 3;
 struct Sides {
     u32 m;            // sides of the chunk
     u32* soff;        // [n + 1] first side (unsorted id) of each event
-    u32* sev;         // [m] unsorted: event | side << 31 (0 debit, 1 credit)
+    u32* sev;         // [m] unsorted: event | side << 31 (0 debit, 1 credit) | SQ_SENS (bit 30)
     u32* scand;       // [m] unsorted: the candidate pending of a post/void pair (pref encoding), else NONE32
     u32* spos;        // [m] sorted position of unsorted side s
     const u32* skey_s;  // [m] sorted keys (account row; >= invalid: no account)
-    u32* sq_ev;       // [m] sorted: event | side << 31
+    u32* sq_ev;       // [m] sorted: event | side << 31 | SQ_SENS
     u32* sq_cs;       // [m] sorted: chain start | standalone << 31 | doomed << 30
     u8* sq_ok;        // [m] sorted, per pass: the side's effect is evaluated-ok
     u128* sq_dpend;   // [m] sorted, per pass: its delta on the *_pending balance
@@ -199,6 +199,12 @@ struct Sides {
     u32 inert;        // the key of sides that touch no account (each stands alone)
 };
 constexpr u32 SQ_STANDALONE = 1u << 31, SQ_DOOM = 1u << 30, SQ_CS = (1u << 30) - 1;
+// sq_ev / sev: bit 30 set when the side's balance can decide its event's outcome in a
+// headroom pass -- a debit side of an account with debits_must_not_exceed_credits or of
+// a balancing_debit transfer, a credit side likewise (eval_balances_narrow reads nothing
+// else of a balance; post/void and static failures read none).  The headroom scan marks
+// an event due only through such a side.  Events fit 29 bits (events_per_call_max).
+constexpr u32 SQ_SENS = 1u << 30, SQ_EV = (1u << 30) - 1;
 
 struct SideScanArgs {
     const u32* skey;  // sorted side keys (account row; >= invalid for inert)
@@ -223,6 +229,8 @@ struct SideScanArgs {
     // headroom passes (side_scan_fused_narrow): the side's one balance figure its
     // evaluation reads, or null (the Bal4 passes)
     u128* bh;
+    u32 all_sides;    // headroom passes: a moved balance marks its event whatever SQ_SENS says
+                      // (TBGPU_NO_SENS=1, A/B timing)
 };
 
 // final-ok of a sorted side: evaluated-ok and its chain persisted
@@ -375,13 +383,17 @@ __device__ __forceinline__ u32 xrun_find(const Tables& T, u128 id) {
     }
 }
 
+// A slot whose claim was withdrawn (fast.hip's eager claims: a chain of the call broke,
+// or its event failed a later check): probes walk past it, inserts never reuse it.
+constexpr u32 XIDX_TOMB = 0xFFFFFFFFu;
+
 __device__ __forceinline__ u32 xidx_probe(const Tables& T, u128 id) {
     if (xidx_maybe_present(T, id)) {  // else outside the hashed ids' key range
         u64 h = xidx_hash(id) & T.xidx_mask;
         for (;;) {
             const u32 r1 = T.xidx[h];
             if (r1 == 0) break;
-            if (T.xrows[r1 - 1].id == id) return r1 - 1;
+            if (r1 != XIDX_TOMB && T.xrows[r1 - 1].id == id) return r1 - 1;
             h = (h + XIDX_STEP) & T.xidx_mask;
         }
     }

@@ -10,6 +10,7 @@
 //
 // See transfers.hip for why the fixed point reproduces execute() exactly.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -360,6 +361,21 @@ struct tbgpu_ctx {
     std::recursive_mutex call_mu, route_mu;
     bool spec_pending = false;
     FastArgs spec_F{};
+    // a small one-chunk call's end stored by fp_tail (fp_commit_small's mode) instead of
+    // k_report: where to (set for the call's last chunk), and whether it did
+    TailReport tail_rp{};
+    bool tail_reported = false;
+    u32 call_seq = 0;          // the last small call's sequence number (fp_tail stores it last)
+    // TBGPU_HOST_TRACE=1 (diagnostics): host time of the drop-in call's steps, averaged
+    // over its calls and printed at deinit
+    std::chrono::steady_clock::time_point ht0{};
+    double ht_sum[8] = {};
+    u64 ht_calls = 0;
+    bool ht_on = false;
+    bool stats_lazy = false;   // stats.device_ms still to be read from ev0 / ev1 (tbgpu_last_stats)
+    // whether the last fast attempt's ids did not rise (FL_NONMONO): the next attempt then
+    // claims its ids eagerly in fp_commit (FastArgs::eager)
+    bool ids_nonmono = false;
     u32 last_passes = 8;  // passes the last fixed point took (sizes the next pass group)
     bool long_segments = false;  // this call has an account segment too long for the fused scan
     // fixed-point pass counters, a ring of PC_RING words: changes per pass (the gate
@@ -444,6 +460,16 @@ struct CallGuard {
 };
 
 
+static bool host_trace() {
+    static const bool on = getenv("TBGPU_HOST_TRACE") != nullptr;
+    return on;
+}
+// mark k of the drop-in call's host timeline (no-op unless the call is being traced)
+static inline void ht_mark(tbgpu_ctx* c, int k) {
+    if (!c->ht_on || c->ht_calls <= 16) return;  // (the first calls load code objects)
+    c->ht_sum[k] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - c->ht0).count();
+}
+
 static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     u64& B = c->bytes;
     c->nmax = nmax;
@@ -521,7 +547,7 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->f_gpos = dalloc<u32>(n, &B);
     c->f_keys = dalloc<u128>(n, &B);
     c->f_rows = dalloc<u32>(n, &B);
-    c->f_tile_idr = dalloc<u64>(TILE_WORDS * (fp_tiles(nmax) + 1), &B);
+    c->f_tile_idr = dalloc<u64>(TILE_WORDS * (std::max<u64>(fp_tiles(nmax), FP_TAIL_MAX / FP_SMALL_TILE) + 1), &B);
     c->rt_ts_buf = dalloc<u64>(n, &B);
     c->rt_ctl_buf = dalloc<u8>(n, &B);
     c->rt_dry_ts = dalloc<u64>(1, &B);
@@ -540,7 +566,8 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     // never reads a previous call's staged block and the host never reads a report the
     // device has not written back.
     constexpr unsigned HOST_COHERENT = hipHostMallocMapped | hipHostMallocCoherent;
-    HIP_CHECK(hipHostMalloc((void**)&c->h_report, (RPT_COUNTS + c->bmax) * sizeof(u32), HOST_COHERENT));
+    // (+1: the small calls' sequence word, fp_tail's last store)
+    HIP_CHECK(hipHostMalloc((void**)&c->h_report, (RPT_COUNTS + c->bmax + 1) * sizeof(u32), HOST_COHERENT));
     HIP_CHECK(hipHostMalloc((void**)&c->h_res, c->nmax * 8 + 8, HOST_COHERENT));
     HIP_CHECK(hipHostGetDevicePointer((void**)&c->h_res_dev, c->h_res, 0));
     HIP_CHECK(hipHostGetDevicePointer((void**)&c->h_report_dev, c->h_report, 0));
@@ -551,7 +578,7 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     HIP_CHECK(hipHostGetDevicePointer((void**)&c->h_stage_dev, c->h_stage_start, 0));
     poison_host(c->h_base, 8 * sizeof(u64));
     poison_host(c->h_counters, (PC_OFF + 3 * PC_RING) * sizeof(u32));
-    poison_host(c->h_report, (RPT_COUNTS + c->bmax) * sizeof(u32));
+    poison_host(c->h_report, (RPT_COUNTS + c->bmax + 1) * sizeof(u32));
     poison_host(c->h_res, c->nmax * 8 + 8);
     poison_host(c->h_counts, c->bmax * sizeof(u32));
     poison_host(c->h_stage_start, (batch_ts_offset(c->bmax) + 2 * c->bmax) * sizeof(u32));
@@ -688,6 +715,15 @@ extern "C" void tbgpu_reset(tbgpu_ctx* c) {
 
 extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     if (!c) return;
+    if (c->ht_calls) {
+        static const char* what[8] = {"guard", "ev0 recorded", "batch block", "fp_commit launched",
+                                      "fp_tail launched", "ev1 recorded", "end seen", "returned"};
+        const double nc = (double)(c->ht_calls > 16 ? c->ht_calls - 16 : 1);
+        fprintf(stderr, "tbgpu host trace: %llu drop-in calls after 16, mean us since entry:",
+                (unsigned long long)(c->ht_calls > 16 ? c->ht_calls - 16 : 0));
+        for (int k = 0; k < 8; k++) fprintf(stderr, " %s %.2f;", what[k], c->ht_sum[k] / nc);
+        fprintf(stderr, "\n");
+    }
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamSynchronize(c->route_stream);
@@ -978,21 +1014,34 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_crea
     F.fres2 = c->mask;
     F.dry = c->rt_dry ? 1u : 0u;
     F.commit_ts = c->rt_dry ? c->rt_dry_ts : c->T.commit_ts;
+    static const bool no_tail = getenv("TBGPU_NO_TAIL") != nullptr;  // A/B timing of the launch sequence
+    static const bool no_small = getenv("TBGPU_NO_SMALL") != nullptr;  // A/B timing: 512-event tiles, fp_prep
+    // A drop-in call (one chunk of at most FP_TAIL_MAX events, its verdict read with the
+    // call's end): two launches, fp_commit_small (64-event tiles over 128 CUs for 8190
+    // events, no fp_prep before it) and fp_tail, which also stores the call's end into
+    // pinned host memory (no k_report after it).
+    F.small = (spec && n <= FP_TAIL_MAX && !no_tail && !no_small) ? 1u : 0u;
+    F.tile = F.small ? FP_SMALL_TILE : fp_tile_events();
+    static const bool no_eager = getenv("TBGPU_NO_EAGER") != nullptr;  // A/B timing: fp_dupcheck + inserts
+    F.eager = (c->ids_nonmono && !F.dry && !no_eager) ? 1u : 0u;
+    const BlockInline bi = take_block(c);
     prof_mark(c, PH_PREP);
-    fp_launch_prep(F, s, take_block(c));
+    if (!F.small) fp_launch_prep(F, s, bi);
     prof_mark(c, PH_CLASSIFY);
     F.ev_copy = c->ev_in_host ? (Transfer*)c->ev_buf : nullptr;
-    fp_launch_commit(c->T, F, s);
+    fp_launch_commit(c->T, F, s, F.small ? bi : BlockInline{});
+    ht_mark(c, 3);
     if (F.ev_copy) {  // the later launches read fp_commit's HBM copy of the events
         F.ev = F.ev_copy;
         F.ev_copy = nullptr;
     }
     prof_mark(c, PH_INDEX);
-    static const bool no_tail = getenv("TBGPU_NO_TAIL") != nullptr;  // A/B timing of the launch sequence
     if (n <= FP_TAIL_MAX && !no_tail) {
         // a small call: index, fix and advance in one workgroup, gated on the device's
         // flags like the speculative launches below
-        fp_launch_tail(c->T, F, s);
+        c->tail_reported = F.small && c->tail_rp.out;
+        fp_launch_tail(c->T, F, s, F.small ? bi : BlockInline{}, F.small ? c->tail_rp : TailReport{});
+        ht_mark(c, 4);
         prof_mark(c, PH_END);
         c->stats.path = 1;
         c->stats.iterations = 1;
@@ -1004,6 +1053,7 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_crea
         HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, CNT_COUNT * sizeof(u32), hipMemcpyDeviceToHost, s));
         wait_stream(s);
         const u32 flags = c->h_counters[CNT_FLAGS];
+        if (!F.dry) c->ids_nonmono = (flags & FL_NONMONO) != 0;
         if (flags & FL_ERROR) tbgpu_fatal("create_transfers", "fast path look-back did not complete", __FILE__, __LINE__);
         if (flags & FL_SLOW) {
             fp_launch_undo(c->T, F, s);
@@ -1033,6 +1083,7 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_crea
     HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, CNT_COUNT * sizeof(u32), hipMemcpyDeviceToHost, s));
     wait_stream(s);
     const u32 flags = c->h_counters[CNT_FLAGS];
+    if (!F.dry) c->ids_nonmono = (flags & FL_NONMONO) != 0;
     if (flags & FL_ERROR) tbgpu_fatal("create_transfers", "fast path look-back did not complete", __FILE__, __LINE__);
     if (flags & FL_SLOW) {
         fp_launch_undo(c->T, F, s);  // commit_timestamp back; the deltas (a dry run applied none)
@@ -1215,6 +1266,8 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
             } else if (hr) {
                 SideScanArgs SN = SA;
                 SN.bh = c->bh;
+                static const bool no_sens = getenv("TBGPU_NO_SENS") != nullptr;  // A/B timing
+                SN.all_sides = no_sens ? 1u : 0u;
                 side_scan_fused_narrow(SN, m, inv_acc, c->tstart, c->counters + CNT_LONG, c->T.acc, s);
             } else {
                 side_scan_fused(SA, m, inv_acc, c->tstart, c->counters + CNT_LONG, c->T.acc, c->bb, s);
@@ -1578,6 +1631,7 @@ static bool spec_settle(tbgpu_ctx* c) {
     if (!c->spec_pending) return true;
     c->spec_pending = false;
     const u32 flags = c->h_counters[CNT_FLAGS];
+    if (!c->spec_F.dry) c->ids_nonmono = (flags & FL_NONMONO) != 0;
     if (flags & FL_ERROR) tbgpu_fatal("create_transfers", "fast path look-back did not complete", __FILE__, __LINE__);
     if (!(flags & FL_SLOW)) {
         c->fast_misses = 0;
@@ -1595,7 +1649,11 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
                                   const uint8_t* ctl_host = nullptr, bool routed_device = false) {
     HIP_CHECK(hipSetDevice(c->device));
     entry_flush(c->stream);
-    HIP_CHECK(hipEventRecord(c->ev0, c->stream));
+    c->stats_lazy = false;
+    static const bool no_call_events = getenv("TBGPU_NO_CALL_EVENTS") != nullptr;  // experiment
+    const bool call_events = !no_call_events || c->prof;
+    if (call_events) HIP_CHECK(hipEventRecord(c->ev0, c->stream));
+    ht_mark(c, 1);
     ensure_h_rc(c, nb_total);
     std::vector<u32> starts;
     u64 ev_off = 0, events = 0;
@@ -1643,6 +1701,7 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         // the replies start at the front of `results` (device results: the call's first
         // chunk; host results: every chunk, staged in res_buf)
         upload_batches(c, timestamps + b0, counts + b0, nb, starts, ev_off == 0 || !dst_device, /*allow_inline=*/true);
+        ht_mark(c, 2);
         c->rt_ev_ts = nullptr;
         c->rt_ctl = nullptr;
         if (routed_device) {  // already in HBM
@@ -1666,6 +1725,11 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         // decides whether it stands: that answer comes with the call's final wait
         const bool spec = try_fast_path && !c->rt_dry && b0 == 0 && b1 == nb_total &&
                           !(c->opt.flags & TBGPU_OPT_FORCE_GENERAL) && !spec_disabled();
+        c->tail_rp = TailReport{};
+        c->tail_reported = false;
+        if (b1 == nb_total)
+            c->tail_rp = TailReport{c->h_report_dev, nb, (const u64*)c->res_buf, dst_device ? nullptr : c->h_res_dev,
+                                    c->h_report_dev + RPT_COUNTS + c->bmax, ++c->call_seq};
         const bool stood = run_transfers_chunk(c, ev, n, nb, rdev, try_fast_path,
                                                /*split=*/!c->rt_dry && nb > general_chunk_batches(), spec);
         c->ev_in_host = false;
@@ -1677,12 +1741,36 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         if (b1 == nb_total) {
             // the call's end: counters, cursors and reply counts in one copy, with the
             // replies, and one wait
-            const u32 rb = std::max<u32>((RPT_COUNTS + nb + 255) / 256, dst_device ? 1u : std::min<u32>(n / 256, 1024));
-            k_report<<<rb, 256, 0, c->stream>>>(c->counters, c->T.base, c->counts, nb, c->h_report_dev,
-                                                (const u64*)c->res_buf, dst_device ? nullptr : c->h_res_dev);
-            HIP_CHECK(hipGetLastError());
-            HIP_CHECK(hipEventRecord(c->ev1, c->stream));
-            wait_event(c->ev1);
+            if (!c->tail_reported) {  // (fp_tail stored it already: a small call)
+                const u32 rb = std::max<u32>((RPT_COUNTS + nb + 255) / 256,
+                                             dst_device ? 1u : std::min<u32>(n / 256, 1024));
+                k_report<<<rb, 256, 0, c->stream>>>(c->counters, c->T.base, c->counts, nb, c->h_report_dev,
+                                                    (const u64*)c->res_buf, dst_device ? nullptr : c->h_res_dev);
+                HIP_CHECK(hipGetLastError());
+            }
+            c->tail_reported = false;
+            if (call_events || !c->tail_reported) HIP_CHECK(hipEventRecord(c->ev1, c->stream));
+            ht_mark(c, 5);
+            if (c->tail_reported && !c->prof) {
+                // a small call: fp_tail's last store is its sequence word in pinned host
+                // memory, after everything it reported; spin on it (no completion signal,
+                // no wake-up), and only past a bound wait for the launch as any other call
+                const volatile u32* seqw = c->h_report + RPT_COUNTS + c->bmax;
+                const u32 want = c->tail_rp.seq;
+                for (u32 k = 0;; k++) {
+                    if (__atomic_load_n(seqw, __ATOMIC_ACQUIRE) == want) break;
+                    // now and then: has the launch ended (or failed) without the word?
+                    if ((k & 1023) == 1023 && (call_events ? hipEventQuery(c->ev1) : hipStreamQuery(c->stream)) !=
+                                                  hipErrorNotReady) {
+                        if (call_events) wait_event(c->ev1); else wait_stream(c->stream);  // (reports a failure)
+                        break;
+                    }
+                }
+                c->stats_lazy = call_events;
+            } else {
+                wait_event(c->ev1);
+            }
+            ht_mark(c, 6);
             memcpy(c->h_counters, c->h_report, CNT_COUNT * sizeof(u32));
             memcpy(c->h_base, c->h_report + RPT_BASE, 4 * sizeof(u64));
             memcpy(c->h_rc + b0, c->h_report + RPT_COUNTS, nb * sizeof(u32));
@@ -1717,7 +1805,7 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         return transfers_batches(c, nb_total, timestamps, counts, ev_src, src_device, results, dst_device,
                                  result_counts, ev_ts_host, ctl_host, routed_device);
     float ms = 0;
-    HIP_CHECK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    if (!c->stats_lazy && call_events) HIP_CHECK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     c->n_rows = c->h_base[BASE_ROWS];
     c->n_hist = c->h_base[BASE_HIST];
     c->rows_hi = c->n_rows;
@@ -2043,16 +2131,27 @@ extern "C" int tbgpu_prefetch_wait(tbgpu_ctx* c) {
 
 extern "C" uint32_t tbgpu_create_transfers(tbgpu_ctx* c, uint64_t timestamp, const tbgpu_transfer_t* events,
                                            uint32_t count, tbgpu_create_transfers_result_t* results) {
+    if (host_trace()) {
+        c->ht_on = true;
+        c->ht0 = std::chrono::steady_clock::now();
+        c->ht_calls++;
+    }
     CallGuard guard_(c, false);
+    ht_mark(c, 0);
     uint32_t rc = 0;
     const uint64_t ts = timestamp;
+    uint32_t out;
     if (c->pf_valid && c->pf_src == (const void*)events && c->pf_n == count) {
         // prefetched: the events are in HBM already (the copy is ahead on the stream)
         c->pf_valid = false;
-        return (uint32_t)transfers_batches(c, 1, &ts, &count, (const Transfer*)c->pf_buf, true, results, false, &rc);
+        out = (uint32_t)transfers_batches(c, 1, &ts, &count, (const Transfer*)c->pf_buf, true, results, false, &rc);
+    } else {
+        c->pf_valid = false;
+        out = (uint32_t)transfers_batches(c, 1, &ts, &count, (const Transfer*)events, false, results, false, &rc);
     }
-    c->pf_valid = false;
-    return (uint32_t)transfers_batches(c, 1, &ts, &count, (const Transfer*)events, false, results, false, &rc);
+    ht_mark(c, 7);
+    c->ht_on = false;
+    return out;
 }
 
 extern "C" uint64_t tbgpu_create_transfers_batches(tbgpu_ctx* c, uint32_t batch_count, const uint64_t* timestamps,
@@ -2183,6 +2282,7 @@ static uint64_t accounts_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t
     CallGuard guard_(c, false);
     c->pf_valid = false;  // any other create call discards a prefetched batch
     entry_flush(c->stream);
+    c->stats_lazy = false;
     HIP_CHECK(hipEventRecord(c->ev0, c->stream));
     std::vector<u32> starts;
     u64 total = 0, ev_off = 0;
@@ -2731,7 +2831,16 @@ extern "C" uint64_t tbgpu_commit_timestamp(tbgpu_ctx* c) {
     return v;
 }
 
-extern "C" void tbgpu_last_stats(tbgpu_ctx* c, tbgpu_stats* out) { *out = c->stats; }
+extern "C" void tbgpu_last_stats(tbgpu_ctx* c, tbgpu_stats* out) {
+    if (c->stats_lazy) {  // a polled small call: its device time once the launch has ended
+        c->stats_lazy = false;
+        wait_event(c->ev1);
+        float ms = 0;
+        HIP_CHECK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        c->stats.device_ms = ms;
+    }
+    *out = c->stats;
+}
 
 extern "C" int tbgpu_last_error(tbgpu_ctx* c, char* buf, uint32_t len) {
     if (!buf || !len) return 0;

@@ -26,8 +26,21 @@ struct FastArgs {
     u64* commit_ts;     // commit_timestamp sink (T.commit_ts, or a scratch word when dry)
     u32 dry;            // dry run: replies only, no state change
     Transfer* ev_copy;  // ev is in host memory (zero copy): fp_commit leaves an HBM copy here, or null
+    u32 tile;           // events per fp_commit workgroup (FP_SMALL_TILE for a small call, else fp_tiles')
+    u32 small;          // fp_commit_small ran: no fp_prep; fp_tail sets the counters from the tile records
+    // Eager id claims (a call predicted not to rise: random or reversed ids): fp_commit
+    // claims each accepted id's slot of the transfer-id index at its optimistic row by CAS,
+    // which also finds a repeat within the call (-> FL_SLOW); gpos[i] is the slot.  No
+    // fp_dupcheck, no inserts after; the fix moves a slot to its row's rank, a broken
+    // chain withdraws its members' claims (XIDX_TOMB), a fallback clears every claim.
+    u32 eager;
 };
-constexpr u32 TILE_WORDS = 6;
+// per tile: max lo, max hi, min lo, min hi of the accepted ids; max accepted timestamp;
+// accepted count; (fp_commit_small) failures and FL_* flags
+constexpr u32 TILE_WORDS = 8;
+// a drop-in call's tile: 64 events (one wave) per workgroup, so one 8190-event
+// prepare spans 128 workgroups instead of 16
+constexpr u32 FP_SMALL_TILE = 64;
 // calls of at most FP_TAIL_MAX events run fp_launch_tail (one workgroup) instead of
 // fp_launch_index + fp_launch_fix + fp_launch_advance
 constexpr u32 FP_TAIL_THREADS = 1024, FP_TAIL_MAX = 16384;
@@ -55,10 +68,23 @@ struct BlockInline {
     u32 w[BLOCK_INLINE_WORDS];
 };
 void fp_launch_prep(const FastArgs& F, hipStream_t stream, const BlockInline& bi = BlockInline{});
-void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream);
+void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream, const BlockInline& bi = BlockInline{});
 void fp_launch_index(const Tables& T, const FastArgs& F, hipStream_t stream);
 void fp_launch_fix(const Tables& T, const FastArgs& F, u8* mask, uint4* ranks, Scan3Scratch& sc, hipStream_t stream);
 void fp_launch_undo(const Tables& T, const FastArgs& F, hipStream_t stream);
-void fp_launch_tail(const Tables& T, const FastArgs& F, hipStream_t stream);
+// k_report's stores made by fp_tail at its end (a small one-chunk call): counters,
+// T.base and the reply counts into out (pinned host memory), the replies when
+// out_replies is set
+struct TailReport {
+    u32* out;
+    u32 nb;
+    const u64* replies;
+    u64* out_replies;
+    u32* seq_out;  // pinned host word: `seq` stored last, after every other store is visible
+    u32 seq;
+};
+void fp_launch_tail(const Tables& T, const FastArgs& F, hipStream_t stream, const BlockInline& bi = BlockInline{},
+                    const TailReport& rp = TailReport{});
 void fp_launch_advance(const Tables& T, const FastArgs& F, hipStream_t stream);
 u64 fp_tiles(u64 n);
+u32 fp_tile_events();  // events per fp_commit workgroup (streamed calls)

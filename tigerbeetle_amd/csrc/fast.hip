@@ -112,7 +112,29 @@ __device__ __forceinline__ u32 xidx_probe_from(const Tables& T, u64 h, u128 id) 
         h = (h + XIDX_STEP) & T.xidx_mask;
         const u32 r1 = T.xidx[h];
         if (r1 == 0) return NONE32;
-        if (T.xrows[r1 - 1].id == id) return r1 - 1;
+        if (r1 != XIDX_TOMB && T.xrows[r1 - 1].id == id) return r1 - 1;
+    }
+}
+
+// Eager claim of accepted event i's id (FastArgs::eager) at its optimistic row: the
+// first empty slot of its probe sequence, by CAS.  The pre-call index was probed by
+// classify (no committed row has this id), so any slot met on the way that names this
+// call's rows (>= row_base: event row - row_base, whose id is read from the events)
+// with the same id is a repeat within the call: returns true (nothing claimed).
+__device__ __forceinline__ bool fp_claim_is_dup(const Tables& T, const FastArgs& F, u128 id, u64 row_base, u32 i,
+                                                u32* slot) {
+    u64 h = xidx_hash(id) & T.xidx_mask;
+    for (;;) {
+        const u32 prev = atomicCAS(&T.xidx[h], 0u, (u32)(row_base + i) + 1);
+        if (prev == 0) {
+            *slot = (u32)h;
+            return false;
+        }
+        if (prev != XIDX_TOMB && prev - 1 >= row_base && F.ev[prev - 1 - row_base].id == id) {
+            *slot = NONE32;
+            return true;
+        }
+        h = (h + XIDX_STEP) & T.xidx_mask;
     }
 }
 
@@ -177,7 +199,7 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
     if (!ledger_owned(T, t.ledger)) return FRES_SLOW;  // another shard's ledger (the general path refuses it)
     if ((A.flags | B.flags) & (AF_DNEC | AF_CNED | AF_HISTORY)) return FRES_SLOW;  // limits / history
     if (x_r1 != 0) {
-        const u32 pre = T.xrows[x_r1 - 1].id == t.id ? x_r1 - 1 : xidx_probe_from(T, hx, t.id);
+        const u32 pre = (x_r1 != XIDX_TOMB && T.xrows[x_r1 - 1].id == t.id) ? x_r1 - 1 : xidx_probe_from(T, hx, t.id);
         if (pre != NONE32) return fp_exists(t, T.xrows[pre]);
     }
     if (xrun_maybe(T, t.id)) {  // the sorted run (an id replayed from an earlier call)
@@ -257,8 +279,9 @@ __device__ __forceinline__ u128* acc_field(const Tables& T, u32 key) {
 
 // Add `a` to the tile's LDS partial sum for `key` (= slot * 4 + field).  Sums
 // are 64-bit with a carry counter, so no precision is lost.
+template <int SLOTS>
 __device__ __forceinline__ void agg_add(u32* keys, u64* sums, u32* carries, u32 key, u64 a) {
-    u32 h = (u32)(mix64(key) & (AGG_SLOTS - 1));
+    u32 h = (u32)(mix64(key) & (SLOTS - 1));
     for (;;) {
         u32 k = keys[h];
         if (k == AGG_EMPTY) {
@@ -266,7 +289,7 @@ __device__ __forceinline__ void agg_add(u32* keys, u64* sums, u32* carries, u32 
             if (k == AGG_EMPTY) k = key;
         }
         if (k == key) break;
-        h = (h + 1) & (AGG_SLOTS - 1);
+        h = (h + 1) & (SLOTS - 1);
     }
     const u64 old = atomicAdd((unsigned long long*)&sums[h], (unsigned long long)a);
     if (old + a < old) atomicAdd(&carries[h], 1u);
@@ -300,25 +323,42 @@ __device__ __forceinline__ void wave_lds_sync() {
 #ifndef FP_WAVES_PER_EU
 #define FP_WAVES_PER_EU 5  // 3..5 measured alike, 7..8 slower (profiles/micro/README.md)
 #endif
-// One tile of FP_THREADS events per workgroup.  Rows are stored optimistically at
+// One tile of TILE events per workgroup.  Rows are stored optimistically at
 // row_base + event (every event accepted, the benchmark's case); failures are
 // counted and, if there are any, fp_fix moves the rows to their ranks afterwards.
-__global__ __launch_bounds__(FP_THREADS) __attribute__((amdgpu_waves_per_eu(FP_WAVES_PER_EU)))
-void fp_commit(Tables T, FastArgs F) {
-    __shared__ u64 s_maxts[FP_THREADS / 64];
-    __shared__ u32 s_cnt[FP_THREADS / 64][2];
-    __shared__ u64 s_idr[FP_THREADS / 64][4];
-    __shared__ u32 s_keys[AGG_SLOTS];
-    __shared__ u64 s_sums[AGG_SLOTS];
-    __shared__ u32 s_carry[AGG_SLOTS];
+// SMALL (a drop-in call of at most FP_TAIL_MAX events, fp_commit_small): 64-event
+// tiles, so one 8190-event prepare spans 128 CUs instead of 16; no fp_prep before it
+// (its batch block comes in the kernel arguments, and the tile's flags and failure
+// count go to its tile record instead of the call's counters, which fp_tail sets
+// from the records: nothing here needs them reset first).
+template <int TILE, bool SMALL>
+__device__ __forceinline__ void fp_commit_body(const Tables& T, FastArgs F, const BlockInline& bi) {
+    constexpr int AGG = 4 * TILE;  // LDS aggregation table (2x the sides of a tile)
+    __shared__ u64 s_maxts[TILE / 64];
+    __shared__ u32 s_cnt[TILE / 64][2];
+    __shared__ u64 s_idr[TILE / 64][4];
+    __shared__ u32 s_keys[AGG];
+    __shared__ u64 s_sums[AGG];
+    __shared__ u32 s_carry[AGG];
+    __shared__ u32 s_flags;
+    __shared__ u32 s_blk[BLOCK_INLINE_WORDS];
 #if defined(FP_LDS_EVENTS)
-    __shared__ uint4 s_stage[FP_THREADS / 64][STAGE_RECS * 8];
+    __shared__ uint4 s_stage[TILE / 64][STAGE_RECS * 8];
 #endif
     const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const u32 tile = blockIdx.x;
-    const u32 i = tile * FP_THREADS + tid;
+    const u32 i = tile * TILE + tid;
     const bool valid = i < F.n;
-    const u32 wbase = tile * FP_THREADS + wave * 64;
+    const u32 wbase = tile * TILE + wave * 64;
+    if (SMALL) {
+        // the call's batch block from the arguments (nothing has written it to memory yet)
+        if (bi.words) {
+            if (tid < bi.words) s_blk[tid] = bi.w[tid];
+            F.b_start = s_blk;
+            F.b_ts = (const u64*)(s_blk + ((F.nb + 2) & ~1u));  // batch_ts_offset
+        }
+        if (tid == 0) s_flags = 0;
+    }
     const u64 row_base = T.base[BASE_ROWS];  // device cursor: no host round trip between calls
     // When this call's rows will extend the id index's sorted run if every event is
     // accepted with rising ids (the benchmark's case: fp_run), nothing needs the id
@@ -330,7 +370,7 @@ void fp_commit(Tables T, FastArgs F) {
 #if defined(FP_KEYS_ALWAYS)  // timing variant: the copies as before
         keys = true;
 #endif
-        if (tile == 0 && tid == 0) F.counters[CNT_NOKEYS] = keys ? 0u : 1u;
+        if (tile == 0 && tid == 0) F.counters[CNT_NOKEYS] = keys ? 0u : 1u;  // (fp_tail keeps it)
     }
 #if defined(FP_LDS_EVENTS)
     // The wave's 64 events as coalesced 16-byte loads (lane k of load j holds chunk
@@ -356,7 +396,7 @@ void fp_commit(Tables T, FastArgs F) {
         c7 = src[min(q0 + 448, last)];
     }
 #endif
-    for (u32 h = tid; h < AGG_SLOTS; h += FP_THREADS) {
+    for (u32 h = tid; h < AGG; h += TILE) {
         s_keys[h] = AGG_EMPTY;
         s_sums[h] = 0;
         s_carry[h] = 0;
@@ -446,7 +486,7 @@ void fp_commit(Tables T, FastArgs F) {
         plk = (F.ev[i - 1].flags & TF_LINKED) && !(F.ctl && (F.ctl[i - 1] & TBGPU_CTL_CHAIN_END));
     plk = plk && valid && i > bs;
     const bool member = lk || plk || (myctl & TBGPU_CTL_DOOM);
-    if (__ballot(member) && lane == 0) atomicOr(&F.counters[CNT_FLAGS], (u32)FL_FCHAIN);
+    if (__ballot(member) && lane == 0) atomicOr(SMALL ? &s_flags : &F.counters[CNT_FLAGS], (u32)FL_FCHAIN);
     bool own_ok = false;
 #if defined(FP_NT_ROWS)  // timing variant: rows written with non-temporal stores
 #define STORE_ROW() do { if (!(FP_ABLATE & ABL_ROWS)) { \
@@ -463,6 +503,14 @@ void fp_commit(Tables T, FastArgs F) {
         else if (myctl & TBGPU_CTL_SKIP) r = TBGPU_CREATE_TRANSFER_LINKED_EVENT_FAILED;    // broken on another shard
         else r = fp_classify(T, F, t, i, ts, &ds, &cs);
         own_ok = r == TBGPU_CREATE_TRANSFER_OK;
+        if (F.eager) {
+            u32 slot = NONE32;
+            if (own_ok && fp_claim_is_dup(T, F, t.id, row_base, i, &slot)) {
+                r = FRES_SLOW;  // an id repeated within the call: the fixed point decides it
+                own_ok = false;
+            }
+            F.gpos[i] = slot;
+        }
         if (member && r != FRES_SLOW) {
             // deferred to fp_chains: no balance delta, no count; the optimistic row
             // and the id claim as for any accepted event
@@ -482,16 +530,16 @@ void fp_commit(Tables T, FastArgs F) {
             const u64 a = (u64)t.amount;
             const u32 pend = (t.flags & TF_PENDING) ? 0u : 1u;
             if (!(FP_ABLATE & ABL_BALANCES)) {
-                agg_add(s_keys, s_sums, s_carry, ds * 4 + pend, a);
-                agg_add(s_keys, s_sums, s_carry, cs * 4 + 2 + pend, a);
+                agg_add<AGG>(s_keys, s_sums, s_carry, ds * 4 + pend, a);
+                agg_add<AGG>(s_keys, s_sums, s_carry, cs * 4 + 2 + pend, a);
             }
             // optimistic stored row (every predecessor accepted); fp_fix re-places it otherwise
             t.timestamp = ts;
             STORE_ROW();
         } else if (r == FRES_SLOW) {
-            atomicOr(&F.counters[CNT_FLAGS], (u32)FL_SLOW);
-        } else if (r != FRES_CHAIN) {
-            atomicAdd(&F.batch_counts[b], 1u);
+            atomicOr(SMALL ? &s_flags : &F.counters[CNT_FLAGS], (u32)FL_SLOW);
+        } else if (r != FRES_CHAIN && !SMALL) {
+            atomicAdd(&F.batch_counts[b], 1u);  // (SMALL: fp_tail counts each batch's replies)
         }
     }
 #undef STORE_ROW
@@ -513,7 +561,7 @@ void fp_commit(Tables T, FastArgs F) {
             }
         }
         const bool up = !valid || i == 0 || hi > phi || (hi == phi && lo > plo);
-        if (__ballot(!up) && lane == 0) atomicOr(&F.counters[CNT_FLAGS], (u32)FL_NONMONO);
+        if (__ballot(!up) && lane == 0) atomicOr(SMALL ? &s_flags : &F.counters[CNT_FLAGS], (u32)FL_NONMONO);
     }
     const u64 okm = __ballot(ok), badm = __ballot(bad);
     u64 mts = ok ? ts : 0;
@@ -541,13 +589,13 @@ void fp_commit(Tables T, FastArgs F) {
     if (wave == 0) {
         if (lane < 4) {
             u64 v = s_idr[0][lane];
-            for (int w = 1; w < FP_THREADS / 64; w++) v = lane < 2 ? max(v, s_idr[w][lane]) : min(v, s_idr[w][lane]);
+            for (int w = 1; w < TILE / 64; w++) v = lane < 2 ? max(v, s_idr[w][lane]) : min(v, s_idr[w][lane]);
             F.tile_idr[TILE_WORDS * tile + lane] = v;
         }
         if (lane == 0) {
             u32 nok = 0, nbad = 0;
             u64 maxts = 0;
-            for (int w = 0; w < FP_THREADS / 64; w++) {
+            for (int w = 0; w < TILE / 64; w++) {
                 nok += s_cnt[w][0];
                 nbad += s_cnt[w][1];
                 maxts = max(maxts, s_maxts[w]);
@@ -556,20 +604,25 @@ void fp_commit(Tables T, FastArgs F) {
             // tile on one address would serialize 16k tiles at the memory side)
             F.tile_idr[TILE_WORDS * tile + 4] = maxts;
             F.tile_idr[TILE_WORDS * tile + 5] = nok;
-            if (nbad) atomicAdd(&F.counters[CNT_BAD], nbad);
+            if (SMALL) {
+                F.tile_idr[TILE_WORDS * tile + 6] = nbad;
+                F.tile_idr[TILE_WORDS * tile + 7] = s_flags;
+            } else if (nbad) {
+                atomicAdd(&F.counters[CNT_BAD], nbad);
+            }
         }
     }
     // flush the tile's partial sums: u128 += (carry:sum) with u64 atomics.  All of a
     // thread's low-word atomics are issued before any returns (memory-level
     // parallelism); the rare carries follow.
     if (F.dry) return;  // a dry run moves no balance
-    constexpr int PER = AGG_SLOTS / FP_THREADS;
+    constexpr int PER = AGG / TILE;
     u64* wp[PER];
     u64 av[PER], old[PER];
     u32 cv[PER];
 #pragma unroll
     for (int k = 0; k < PER; k++) {
-        const u32 h = tid + k * FP_THREADS;
+        const u32 h = tid + k * TILE;
         const u32 key = s_keys[h];
         wp[k] = key == AGG_EMPTY ? nullptr : (u64*)acc_field(T, key);
         av[k] = s_sums[h];
@@ -586,7 +639,7 @@ void fp_commit(Tables T, FastArgs F) {
 #if defined(FP_SKIP_HOT)  // timing-only variant (profiles/variants.py): no flush for the hottest rows; results wrong
 #pragma unroll
     for (int k = 0; k < PER; k++)
-        if (wp[k] && (s_keys[tid + k * FP_THREADS] >> 2) < FP_SKIP_HOT) wp[k] = nullptr;
+        if (wp[k] && (s_keys[tid + k * TILE] >> 2) < FP_SKIP_HOT) wp[k] = nullptr;
 #endif
 #pragma unroll
     for (int k = 0; k < PER; k++)
@@ -600,6 +653,15 @@ void fp_commit(Tables T, FastArgs F) {
             if (hi + c >= (1ull << 62)) atomicOr(T.big, 1u);  // later calls must prove no overflow
         }
     }
+}
+
+__global__ __launch_bounds__(FP_THREADS) __attribute__((amdgpu_waves_per_eu(FP_WAVES_PER_EU)))
+void fp_commit(Tables T, FastArgs F) {
+    fp_commit_body<FP_THREADS, false>(T, F, BlockInline{});
+}
+
+__global__ __launch_bounds__(FP_SMALL_TILE) void fp_commit_small(Tables T, FastArgs F, BlockInline bi) {
+    fp_commit_body<FP_SMALL_TILE, true>(T, F, bi);
 }
 
 // Only when the call's ids were not increasing: claim every accepted id once.
@@ -618,7 +680,7 @@ __device__ __forceinline__ void fp_dupcheck_one(const FastArgs& F, u32 i) {
 
 __global__ void fp_dupcheck(Tables T, FastArgs F) {
     // Every event records its claim (or NONE) so fp_index can clear the table.
-    if (!(F.counters[CNT_FLAGS] & FL_NONMONO)) return;
+    if (F.eager || !(F.counters[CNT_FLAGS] & FL_NONMONO)) return;  // (eager: fp_commit's claims found repeats)
     FOR_EACH_EVENT(i) fp_dupcheck_one(F, i);
 }
 
@@ -628,7 +690,7 @@ __global__ void fp_dupcheck(Tables T, FastArgs F) {
 // fp_index inserts nothing; otherwise fp_index hashes them as before.  One thread.
 __device__ void fp_run_one(const Tables& T, const FastArgs& F, u32 flags, u32 bad) {
     u32 take = 0;
-    if (!F.dry && F.n && !(flags & (FL_SLOW | FL_ERROR | FL_NONMONO)) && bad == 0) {
+    if (!F.dry && !F.eager && F.n && !(flags & (FL_SLOW | FL_ERROR | FL_NONMONO)) && bad == 0) {
         u64* r = T.xrun;
         const u64 row0 = T.base[BASE_ROWS];
         const u128 first = F.ev[0].id, last = F.ev[F.n - 1].id;
@@ -682,20 +744,20 @@ __device__ __forceinline__ void fp_fold_idr(const Tables& T, const FastArgs& F, 
 __global__ void fp_index(Tables T, FastArgs F, bool fixed) {
     if (fixed) {  // after fp_fix: the accepted ids at their final rows (grid-stride; gated like the fix)
         if (!F.counters[CNT_FIX] || F.dry) return;
-        const u32 ntiles = (F.n + FP_THREADS - 1) / FP_THREADS;
+        const u32 ntiles = (F.n + F.tile - 1) / F.tile;
         if (threadIdx.x < 64)
             for (u32 k0 = blockIdx.x * 64; k0 < ntiles; k0 += gridDim.x * 64) fp_fold_idr(T, F, k0, ntiles);
-        FOR_EACH_EVENT(j) if (F.fres[j] == TBGPU_CREATE_TRANSFER_OK) xidx_insert(T, fp_key(F, j), F.rows[j]);
+        if (!F.eager) FOR_EACH_EVENT(j) if (F.fres[j] == TBGPU_CREATE_TRANSFER_OK) xidx_insert(T, fp_key(F, j), F.rows[j]);
         return;
     }
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     const u32 flags = F.counters[CNT_FLAGS];
-    if (!fixed && (flags & FL_NONMONO) && i < F.n) {
+    if (!fixed && !F.eager && (flags & FL_NONMONO) && i < F.n) {
         // leave the claim table all-zero for the next call (also when falling back)
         const u32 g = F.gpos[i];
         if (g != NONE32) F.gtab[g] = 0;
     }
-    const u32 ntiles = (F.n + FP_THREADS - 1) / FP_THREADS;
+    const u32 ntiles = (F.n + F.tile - 1) / F.tile;
     if (!fixed && threadIdx.x < 64 && blockIdx.x * 64 < ntiles) {
         // the call's accepted count and commit timestamp from fp_commit's tiles
         // (also for dry runs and calls with failures; fp_undo restores the timestamp
@@ -722,7 +784,7 @@ __global__ void fp_index(Tables T, FastArgs F, bool fixed) {
     // fold the tiles' id ranges into the index's key range: one wave per 64 tiles (a
     // single wave over 16k tiles was a serial tail of this launch)
     if (threadIdx.x < 64) fp_fold_idr(T, F, blockIdx.x * 64, ntiles);
-    if (i >= F.n) return;
+    if (i >= F.n || F.eager) return;  // (eager: claimed by fp_commit at these rows)
     if (F.fres[i] != TBGPU_CREATE_TRANSFER_OK) return;
     xidx_insert(T, fp_key(F, i), (u32)(T.base[BASE_ROWS] + i));
 }
@@ -791,7 +853,8 @@ __device__ void fp_chains_one(const Tables& T, const FastArgs& F, u32 i, u32& n_
         }
     } else {
         n_bad++;
-        atomicAdd(&F.batch_counts[b], 1u);
+        if (!F.small) atomicAdd(&F.batch_counts[b], 1u);  // (small: fp_tail counts each batch's replies)
+        if (F.eager && F.gpos[i] != NONE32) T.xidx[F.gpos[i]] = XIDX_TOMB;  // its claim withdrawn
     }
 }
 
@@ -889,6 +952,7 @@ __device__ __forceinline__ void fp_fix_one(const FastArgs& F, const Tables& T, u
     t.timestamp = F.ev_ts ? F.ev_ts[i] : F.b_ts[b] - (F.b_start[b + 1] - bs) + (i - bs) + 1;
     T.xrows[row] = t;
     F.rows[i] = row;
+    if (F.eager) T.xidx[F.gpos[i]] = row + 1;  // the claim follows its row
 }
 
 __global__ void fp_fix(FastArgs F, Tables T, const uint4* rk) {
@@ -929,18 +993,62 @@ __device__ __forceinline__ u32 fp_cnt(const FastArgs& F, int k) {
     return __hip_atomic_load(&F.counters[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(FP_TAIL_THREADS) void fp_tail(Tables T, FastArgs F) {
+__global__ __launch_bounds__(FP_TAIL_THREADS) void fp_tail(Tables T, FastArgs F, BlockInline bi, TailReport rp) {
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6, n = F.n;
-    const u32 ntiles = (n + FP_THREADS - 1) / FP_THREADS;
-    __shared__ u32 s_flags, s_bad, s_run, s_ok;
+    const u32 ntiles = (n + F.tile - 1) / F.tile;
+    __shared__ u32 s_flags, s_bad, s_run, s_ok, s_fix;
     __shared__ u32 s_wsum[FP_TAIL_THREADS / 64];
-    if (tid == 0) s_flags = fp_cnt(F, CNT_FLAGS);
-    __syncthreads();
-    // fp_dupcheck
-    if (s_flags & FL_NONMONO)
+    if (F.small) {
+        // fp_prep's work (no launch of its own before fp_commit_small): the batch block
+        // into memory for the launches after this one, the reply cursor, the timestamp
+        // the fallback restores; then the call's counters from the tiles' records
+        if (tid < bi.words) bi.block[tid] = bi.w[tid];
+        if (tid == 0 && bi.words && bi.reset_replies) bi.base[BASE_REPLIES] = 0;
+        for (u32 b = tid; b < F.nb; b += FP_TAIL_THREADS) F.batch_counts[b] = 0;
+        if (w == 0) {
+            // the tiles' records in one round: flags, failures, accepted, latest timestamp
+            u32 fl = 0, nbad = 0, nok = 0;
+            u64 mts = 0;
+            for (u32 k = lane; k < ntiles; k += 64) {
+                mts = max(mts, F.tile_idr[TILE_WORDS * k + 4]);
+                nok += (u32)F.tile_idr[TILE_WORDS * k + 5];
+                nbad += (u32)F.tile_idr[TILE_WORDS * k + 6];
+                fl |= (u32)F.tile_idr[TILE_WORDS * k + 7];
+            }
+            for (int off = 32; off > 0; off >>= 1) {
+                nbad += __shfl_xor(nbad, off);
+                nok += __shfl_xor(nok, off);
+                fl |= __shfl_xor(fl, off);
+                mts = max(mts, (u64)__shfl_xor((unsigned long long)mts, off));
+            }
+            if (lane == 0) {
+                const u32 nokeys = F.counters[CNT_NOKEYS];
+                for (int k = 0; k < CNT_TS_SAVE; k++)
+                    __hip_atomic_store(&F.counters[k], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&F.counters[CNT_NOKEYS], nokeys, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&F.counters[CNT_FLAGS], fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&F.counters[CNT_BAD], nbad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&F.counters[CNT_OK], nok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // the timestamp the fallback restores, then this call's (same thread: in order)
+                *(u64*)&F.counters[CNT_TS_SAVE] = *F.commit_ts;
+                if (mts) atomicMax((unsigned long long*)F.commit_ts, (unsigned long long)mts);
+                s_flags = fl;  // the call's figures in LDS: no global re-read below
+                s_bad = nbad;
+                s_ok = nok;
+            }
+        }
+        __syncthreads();
+    } else {
+        if (tid == 0) s_flags = fp_cnt(F, CNT_FLAGS);
+        __syncthreads();
+    }
+    // fp_dupcheck (eager claims: fp_commit found the repeats)
+    const bool dupcheck = (s_flags & FL_NONMONO) && !F.eager;
+    if (dupcheck) {
         for (u32 i = tid; i < n; i += FP_TAIL_THREADS) fp_dupcheck_one(F, i);
-    __syncthreads();
-    if (tid == 0) s_flags = fp_cnt(F, CNT_FLAGS);
+        __syncthreads();
+        if (tid == 0) s_flags = fp_cnt(F, CNT_FLAGS);
+    }
     __syncthreads();
     const u32 flags = s_flags;
     // fp_chains, fp_chains_fin
@@ -958,6 +1066,10 @@ __global__ __launch_bounds__(FP_TAIL_THREADS) void fp_tail(Tables T, FastArgs F)
             if (n_ok) atomicAdd(&F.counters[CNT_OK], n_ok);
             if (n_bad) atomicAdd(&F.counters[CNT_BAD], n_bad);
             if (mts) atomicMax((unsigned long long*)F.commit_ts, (unsigned long long)mts);
+            if (F.small) {
+                if (n_ok) atomicAdd(&s_ok, n_ok);
+                if (n_bad) atomicAdd(&s_bad, n_bad);
+            }
         }
         __syncthreads();
         for (u32 i = tid; i < n; i += FP_TAIL_THREADS) {
@@ -968,7 +1080,7 @@ __global__ __launch_bounds__(FP_TAIL_THREADS) void fp_tail(Tables T, FastArgs F)
     __syncthreads();
     // fp_run
     if (tid == 0) {
-        s_bad = fp_cnt(F, CNT_BAD);
+        if (!F.small) s_bad = fp_cnt(F, CNT_BAD);  // (small: kept in LDS)
         fp_run_one(T, F, flags, s_bad);
         s_run = F.counters[CNT_RUN];
     }
@@ -976,12 +1088,12 @@ __global__ __launch_bounds__(FP_TAIL_THREADS) void fp_tail(Tables T, FastArgs F)
     const u32 bad = s_bad;
     // fp_index (first launch): clear the claims, the tiles' accepted count and
     // timestamp, then the ids when the call stands without failures
-    if (flags & FL_NONMONO)
+    if ((flags & FL_NONMONO) && !F.eager)
         for (u32 i = tid; i < n; i += FP_TAIL_THREADS) {
             const u32 g = F.gpos[i];
             if (g != NONE32) F.gtab[g] = 0;
         }
-    if (w == 0) {
+    if (w == 0 && !F.small) {  // (small: folded with the flags above)
         u64 mts = 0, nok = 0;
         for (u32 k = lane; k < ntiles; k += 64) {
             mts = max(mts, F.tile_idr[TILE_WORDS * k + 4]);
@@ -1001,8 +1113,9 @@ __global__ __launch_bounds__(FP_TAIL_THREADS) void fp_tail(Tables T, FastArgs F)
         if (w == 0)
             for (u32 k0 = 0; k0 < ntiles; k0 += 64) fp_fold_idr(T, F, k0, ntiles);
         const u64 row0 = T.base[BASE_ROWS];
-        for (u32 i = tid; i < n; i += FP_TAIL_THREADS)
-            if (F.fres[i] == TBGPU_CREATE_TRANSFER_OK) xidx_insert(T, fp_key(F, i), (u32)(row0 + i));
+        if (!F.eager)
+            for (u32 i = tid; i < n; i += FP_TAIL_THREADS)
+                if (F.fres[i] == TBGPU_CREATE_TRANSFER_OK) xidx_insert(T, fp_key(F, i), (u32)(row0 + i));
     }
     // fp_mask, scan3, fp_fix, fp_index (fixed): each thread takes a contiguous range,
     // so its ranks are the workgroup's exclusive prefix plus a running count
@@ -1028,16 +1141,64 @@ __global__ __launch_bounds__(FP_TAIL_THREADS) void fp_tail(Tables T, FastArgs F)
         if (!F.dry) {
             if (w == 0)
                 for (u32 k0 = 0; k0 < ntiles; k0 += 64) fp_fold_idr(T, F, k0, ntiles);
-            for (u32 i = i0; i < i1; i++)
-                if (F.fres[i] == TBGPU_CREATE_TRANSFER_OK) xidx_insert(T, fp_key(F, i), F.rows[i]);
+            if (!F.eager)
+                for (u32 i = i0; i < i1; i++)
+                    if (F.fres[i] == TBGPU_CREATE_TRANSFER_OK) xidx_insert(T, fp_key(F, i), F.rows[i]);
         }
     }
     __syncthreads();
     // fp_advance
-    if (tid == 0 && stands) {
-        T.base[BASE_REPLIES] += fp_cnt(F, CNT_BAD);
-        if (!F.dry) T.base[BASE_ROWS] += fp_cnt(F, CNT_OK);
+    __shared__ u64 s_base[4];  // (small) the device cursors after the call, for the report
+    if (tid == 0) {
+        if (F.small) {
+            // the cursors once, updated in registers (the report reads them from LDS)
+            u64 b[4];
+            for (int k = 0; k < 4; k++) b[k] = T.base[k];
+            if (stands) {
+                b[BASE_REPLIES] += s_bad;
+                if (!F.dry) b[BASE_ROWS] += s_ok;
+                T.base[BASE_REPLIES] = b[BASE_REPLIES];
+                T.base[BASE_ROWS] = b[BASE_ROWS];
+            }
+            for (int k = 0; k < 4; k++) s_base[k] = b[k];
+            s_fix = F.counters[CNT_FIX];  // (this thread's own store in fp_run_one)
+        } else if (stands) {
+            T.base[BASE_REPLIES] += fp_cnt(F, CNT_BAD);
+            if (!F.dry) T.base[BASE_ROWS] += fp_cnt(F, CNT_OK);
+        }
     }
+    if (!F.small) return;
+    // each batch's reply count (its failures, final after the chains; none without them)
+    if (stands && bad != 0)
+        for (u32 i = tid; i < n; i += FP_TAIL_THREADS)
+            if (F.fres[i] != TBGPU_CREATE_TRANSFER_OK) atomicAdd(&F.batch_counts[fp_batch_of(F.b_start, F.nb, i)], 1u);
+    __syncthreads();
+    if (!rp.out) return;
+    // k_report: the call's end stored into pinned host memory.  The counter words the host
+    // reads come from LDS (flags, accepted, failed, run, fix; the rest 0), the cursors
+    // too; reply counts are all 0 without failures.  Without replies to copy, wave 0 alone
+    // stores the report, fences its own stores and then the sequence word: no barrier.
+    const u64 total = rp.out_replies ? s_base[BASE_REPLIES] : 0;
+    const bool all = total != 0 || bad != 0;
+    auto word = [&](u32 k) -> u32 {
+        if (k < RPT_BASE) {
+            return k == CNT_FLAGS ? s_flags : k == CNT_OK ? s_ok : k == CNT_BAD ? s_bad : k == CNT_RUN ? s_run
+                 : k == CNT_FIX ? s_fix : 0u;
+        }
+        if (k < RPT_COUNTS) return ((const u32*)s_base)[k - RPT_BASE];
+        return bad ? __hip_atomic_load(&F.batch_counts[k - RPT_COUNTS], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                   : 0u;
+    };
+    if (all || w == 0) {
+        const u32 stride = all ? FP_TAIL_THREADS : 64;
+        for (u32 k = tid; k < RPT_COUNTS + rp.nb; k += stride) rp.out[k] = word(k);
+        for (u64 j = tid; j < total; j += stride) rp.out_replies[j] = rp.replies[j];
+        // the call's sequence number last, once every store above is visible to the
+        // host: the host polls it instead of waiting for the launch's completion signal
+        __threadfence_system();
+    }
+    if (all) __syncthreads();
+    if (tid == 0 && rp.seq_out) __hip_atomic_store(rp.seq_out, rp.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Exact inverse of fp_commit's effects, before the general path redoes the call:
@@ -1047,6 +1208,9 @@ __global__ void fp_undo(Tables T, FastArgs F) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) *F.commit_ts = *(const u64*)&F.counters[CNT_TS_SAVE];
     if (F.dry || i >= F.n) return;
+    // every eager claim of the call (each took a slot that was empty before it; all go
+    // together, so no other id's probe sequence runs through them): the index as before
+    if (F.eager && F.gpos[i] != NONE32) T.xidx[F.gpos[i]] = 0;
     if (F.fres[i] != TBGPU_CREATE_TRANSFER_OK) return;
     const Transfer& t = F.ev[i];
     const u32 ds = acc_row(T, t.debit_account_id);
@@ -1070,8 +1234,12 @@ void fp_launch_prep(const FastArgs& F, hipStream_t stream, const BlockInline& bi
     HIP_CHECK(hipGetLastError());
 }
 
-void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream) {
-    fp_commit<<<(F.n + FP_THREADS - 1) / FP_THREADS, FP_THREADS, 0, stream>>>(T, F);
+void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream, const BlockInline& bi) {
+    if (F.small) {
+        fp_commit_small<<<(F.n + FP_SMALL_TILE - 1) / FP_SMALL_TILE, FP_SMALL_TILE, 0, stream>>>(T, F, bi);
+    } else {
+        fp_commit<<<(F.n + FP_THREADS - 1) / FP_THREADS, FP_THREADS, 0, stream>>>(T, F);
+    }
     HIP_CHECK(hipGetLastError());
 }
 
@@ -1094,8 +1262,9 @@ void fp_launch_fix(const Tables& T, const FastArgs& F, u8* mask, uint4* ranks, S
     HIP_CHECK(hipGetLastError());
 }
 
-void fp_launch_tail(const Tables& T, const FastArgs& F, hipStream_t stream) {
-    fp_tail<<<1, FP_TAIL_THREADS, 0, stream>>>(T, F);
+void fp_launch_tail(const Tables& T, const FastArgs& F, hipStream_t stream, const BlockInline& bi,
+                    const TailReport& rp) {
+    fp_tail<<<1, FP_TAIL_THREADS, 0, stream>>>(T, F, bi, rp);
     HIP_CHECK(hipGetLastError());
 }
 
@@ -1110,3 +1279,4 @@ void fp_launch_undo(const Tables& T, const FastArgs& F, hipStream_t stream) {
 }
 
 u64 fp_tiles(u64 n) { return (n + FP_THREADS - 1) / FP_THREADS; }
+u32 fp_tile_events() { return FP_THREADS; }

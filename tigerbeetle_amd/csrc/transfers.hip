@@ -1165,6 +1165,7 @@ __global__ void tr_side_build(TrArgs C, EvalState S, u32 kmax, const uint4* pair
     const uint4 pr1 = ev ? pairs[i + 1] : make_uint4(0, 0, 0, 0);
     const u8 sr = ev ? C.sres[i] : 0;
     const u16 fl = ev ? C.core[i].flags : 0;
+    const u8 af = ev ? C.core[i].aflags : 0;
     const u32 ds = ev ? C.dslot[i] : NONE32, cs = ev ? C.cslot[i] : NONE32;
     const u32 pd = ev ? C.pp_dslot[i] : NONE32, pc = ev ? C.pp_cslot[i] : NONE32;
     const bool pv = sr == SRES_DYN && (fl & (TF_POST | TF_VOID));
@@ -1212,8 +1213,12 @@ __global__ void tr_side_build(TrArgs C, EvalState S, u32 kmax, const uint4* pair
         skey[s + 1] = c;
         sval[s] = s;
         sval[s + 1] = s + 1;
-        C.sd.sev[s] = i;
-        C.sd.sev[s + 1] = i | (1u << 31);
+        // (a regular transfer's own sides: whether their balance decides its outcome)
+        const bool reg = !pv && sr == SRES_DYN && d != invalid;
+        const bool sd = reg && ((af & AF_DNEC) || (fl & TF_BDR));
+        const bool sc = reg && (((af >> 4) & AF_CNED) || (fl & TF_BCR));
+        C.sd.sev[s] = i | (sd ? SQ_SENS : 0u);
+        C.sd.sev[s + 1] = i | (1u << 31) | (sc ? SQ_SENS : 0u);
         C.sd.scand[s] = C.sd.scand[s + 1] = (pv && j < k) ? cand[j] : NONE32;
     }
 }
@@ -1234,7 +1239,7 @@ __global__ void tr_side_pos(TrArgs C, const u32* sval_s, u64 m) {
     // loads before stores (they may alias for the compiler: see tr_side_build)
     const u32 s = sval_s[q];
     const u32 ev = C.sd.sev[s];
-    const u32 i = ev & 0x7FFFFFFFu;
+    const u32 i = ev & SQ_EV;
     const u32 so = C.sd.soff[i], cs = C.cs[i], ce = C.ce[i];
     const bool doom = C.ctl && (C.ctl[ce] & TBGPU_CTL_DOOM);
     C.sd.spos[s] = (u32)q;
@@ -1484,7 +1489,7 @@ __global__ __launch_bounds__(256) void tr_advance(Tables T, TrArgs C, const uint
 __global__ void tr_walk_prep(TrArgs C, u64 m, u32 start, u32* sstart, u32* cfail) {
     const u64 q = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (q < m) {
-        const u32 ev = C.sd.sq_ev[q] & 0x7FFFFFFFu;
+        const u32 ev = C.sd.sq_ev[q] & SQ_EV;
         if (ev >= start) {
             C.sd.sq_ok[q] = 0;
             C.sd.sq_dpend[q] = 0;
@@ -1508,9 +1513,9 @@ __global__ void tr_walk_prep(TrArgs C, u64 m, u32 start, u32* sstart, u32* cfail
 __global__ void tr_walk_init(TrArgs C, u64 m, u32 start, const u32* sstart, const Bal4* bb, Bal4* wbal) {
     const u64 q = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= m) return;
-    if ((C.sd.sq_ev[q] & 0x7FFFFFFFu) < start) return;
+    if ((C.sd.sq_ev[q] & SQ_EV) < start) return;
     const u32 s0 = sstart[q];
-    if (q == s0 || (C.sd.sq_ev[q - 1] & 0x7FFFFFFFu) < start) wbal[s0] = bb[q];
+    if (q == s0 || (C.sd.sq_ev[q - 1] & SQ_EV) < start) wbal[s0] = bb[q];
 }
 
 struct WalkArgs {

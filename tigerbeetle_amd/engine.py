@@ -219,7 +219,7 @@ class Engine:
 
     def create_transfers(self, timestamp: int, events: np.ndarray) -> np.ndarray:
         events = np.ascontiguousarray(events, dtype=TRANSFER_DTYPE)
-        out = np.zeros(max(len(events), 1), dtype=RESULT_DTYPE)
+        out = np.empty(max(len(events), 1), dtype=RESULT_DTYPE)  # (the first n are written)
         n = self._L.tbgpu_create_transfers(self._h, timestamp, _ptr(events), len(events), _ptr(out))
         return out[:n].copy()
 

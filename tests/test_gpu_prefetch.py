@@ -102,3 +102,47 @@ def test_state_machine_prefetch_then_commit():
         assert_state_equal(sm.engine, orc)
     finally:
         sm.engine.close()
+
+
+def test_prepared_commit_gate_released_expired_and_cancelled():
+    """A prefetch prepares the commit (its launches wait behind a gate for the commit's
+    timestamp).  Whatever happens between prefetch and commit the replies and the state
+    equal the oracle's: the commit right away (the gate lets the prepared launches
+    through), the commit after the gate's 10-ms budget (nothing went through: an
+    ordinary call), another call in between (a lookup releases the gate), a second
+    prefetch (releases the first), and a prefetch followed by a different call only."""
+    import time
+    w = workload.config1(transfer_count=8190 * 8, account_count=600, seed=6)
+    orc, gpu = oracle.Oracle(len(w.accounts), len(w.transfers)), _engine(w)
+    try:
+        ats, tts = w.timestamps()
+        for be in (orc, gpu):
+            be.create_accounts_batches(ats, w.account_counts, w.accounts)
+        bs = _batches(w)
+        q = [1, 2, 3]  # account ids
+        got, want = [], []
+        for b, ev in enumerate(bs):
+            mode = b % 5
+            if mode == 0:
+                gpu.prefetch_transfers(ev)
+                gpu.prefetch_wait()
+            elif mode == 1:
+                gpu.prefetch_transfers(ev)
+                time.sleep(0.03)  # past the gate's budget
+            elif mode == 2:
+                gpu.prefetch_transfers(ev)
+                assert len(gpu.lookup_accounts(q)) == 3  # releases the gate
+            elif mode == 3:
+                gpu.prefetch_transfers(bs[(b + 1) % len(bs)])
+                gpu.prefetch_transfers(ev)  # releases the first preparation
+            # mode 4: no prefetch at all
+            got.append(gpu.create_transfers(int(tts[b]), ev))
+            res, rc, _ = orc.create_transfers_batches(tts[b:b + 1], w.transfer_counts[b:b + 1], ev)
+            want.append(res[:int(rc[0])].copy())
+        # a prefetch no commit follows, then a lookup and the end of the engine
+        gpu.prefetch_transfers(bs[0])
+        assert len(gpu.lookup_accounts(q)) == 3
+        assert_results_equal(got, want, "create_transfers")
+        assert_state_equal(gpu, orc)
+    finally:
+        gpu.close()

@@ -376,6 +376,17 @@ struct tbgpu_ctx {
     // whether the last fast attempt's ids did not rise (FL_NONMONO): the next attempt then
     // claims its ids eagerly in fp_commit (FastArgs::eager)
     bool ids_nonmono = false;
+    // The prepared drop-in commit (tbgpu_prefetch_transfers with a small fast call ahead):
+    // pinned words the gate kernel polls -- [GW_GO] the commit's sequence number (or
+    // | GATE_CANCEL_BIT), [GW_TS..+1] its timestamp, [GW_ACK] the sequence number of a
+    // gate that let nothing through -- and the device word the gated kernels read.
+    u32* h_gate = nullptr;
+    u32* h_gate_dev = nullptr;
+    u32* gate_status = nullptr;
+    bool gate_pending = false;  // a prepared commit is enqueued and not yet released or cancelled
+    bool gate_arm = false;      // try_fast: gate the kernels it launches on gate_status
+    u32 gate_seq = 0, gate_n = 0;
+    u64 gate_budget = 0;        // wall-clock ticks a gate waits before letting nothing through
     u32 last_passes = 8;  // passes the last fixed point took (sizes the next pass group)
     bool long_segments = false;  // this call has an account segment too long for the fused scan
     // fixed-point pass counters, a ring of PC_RING words: changes per pass (the gate
@@ -443,6 +454,19 @@ struct tbgpu_ctx {
     char err[256] = {0};
 };
 
+enum { GW_GO = 0, GW_TS = 2, GW_ACK = 4, GW_WORDS = 8 };
+constexpr u32 GATE_CANCEL_BIT = 0x80000000u;
+
+// Release a prepared commit that will not be committed (any other call on the ctx): its
+// gate then lets nothing through, and the work behind it on the stream goes on.
+static void gate_cancel(tbgpu_ctx* c) {
+    if (!c->gate_pending) return;
+    c->gate_pending = false;
+    c->spec_pending = false;
+    c->tail_reported = false;
+    __atomic_store_n(&c->h_gate[GW_GO], c->gate_seq | GATE_CANCEL_BIT, __ATOMIC_RELEASE);
+}
+
 // Entry guard (tbgpu.h "Concurrency"): a ctx serves one caller at a time, except that
 // the router's send side (tbgpu_route_stats / _prepare / _scatter / _scatter_packed /
 // _unpack / _unpack_packed: the route stream and buffers of their own) may run on one
@@ -450,11 +474,14 @@ struct tbgpu_ctx {
 // entry on the same thread is allowed; overlapping calls otherwise abort.
 struct CallGuard {
     std::recursive_mutex& mu;
-    CallGuard(tbgpu_ctx* c, bool route) : mu(route ? c->route_mu : c->call_mu) {
+    // keep_gate: the entry points that complete a prepared commit (prefetch_wait, the
+    // commit itself); every other call on the engine stream releases it first
+    CallGuard(tbgpu_ctx* c, bool route, bool keep_gate = false) : mu(route ? c->route_mu : c->call_mu) {
         HIP_CHECK(hipSetDevice(c->device));
         if (!mu.try_lock())
             tbgpu_fatal("ctx", route ? "concurrent router calls on one ctx" : "concurrent calls on one ctx", __FILE__,
                         __LINE__);
+        if (!route && !keep_gate) gate_cancel(c);
     }
     ~CallGuard() { mu.unlock(); }
 };
@@ -569,6 +596,14 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     // (+1: the small calls' sequence word, fp_tail's last store)
     HIP_CHECK(hipHostMalloc((void**)&c->h_report, (RPT_COUNTS + c->bmax + 1) * sizeof(u32), HOST_COHERENT));
     HIP_CHECK(hipHostMalloc((void**)&c->h_res, c->nmax * 8 + 8, HOST_COHERENT));
+    HIP_CHECK(hipHostMalloc((void**)&c->h_gate, GW_WORDS * sizeof(u32), HOST_COHERENT));
+    memset(c->h_gate, 0, GW_WORDS * sizeof(u32));
+    HIP_CHECK(hipHostGetDevicePointer((void**)&c->h_gate_dev, c->h_gate, 0));
+    {
+        int khz = 0;  // the wall clock the gate times its wait with
+        HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
+        c->gate_budget = (u64)std::max(khz, 1) * 10;  // 10 ms
+    }
     HIP_CHECK(hipHostGetDevicePointer((void**)&c->h_res_dev, c->h_res, 0));
     HIP_CHECK(hipHostGetDevicePointer((void**)&c->h_report_dev, c->h_report, 0));
     HIP_CHECK(hipHostMalloc((void**)&c->h_counts, c->bmax * sizeof(u32), hipHostMallocDefault));
@@ -664,6 +699,7 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     c->T.idr = dalloc<u64>(4, &B);
     c->T.xrun = dalloc<u64>(8, &B);
     c->T.big = dalloc<u32>(4, &B);
+    c->gate_status = dalloc<u32>(1, &B);
     c->T.hcount = c->T.big + 1;        // [1] entries, [2] refused
     c->T.hash_limit = c->aidx_cap / 2;  // load <= 0.5
     c->T.base = dalloc<u64>(4, &B);
@@ -715,6 +751,7 @@ extern "C" void tbgpu_reset(tbgpu_ctx* c) {
 
 extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     if (!c) return;
+    gate_cancel(c);  // (a prepared commit's gate lets nothing through; the sync below then ends)
     if (c->ht_calls) {
         static const char* what[8] = {"guard", "ev0 recorded", "batch block", "fp_commit launched",
                                       "fp_tail launched", "ev1 recorded", "end seen", "returned"};
@@ -733,7 +770,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
                     (void*)c->ro_bcount, (void*)c->ro_spart, (void*)c->rd_claim, (void*)c->rd_first,
                     (void*)c->rd_slot})
         if (p) { guard_release(p); (void)hipFree(p); }
-    void* ptrs[] = {c->T.dense, c->T.acc, c->T.aidx, c->T.xrows, c->T.xful, c->T.xidx, c->T.hrows, c->T.commit_ts, c->T.idr, c->T.xrun, c->T.big, c->ev_buf,
+    void* ptrs[] = {c->T.dense, c->T.acc, c->T.aidx, c->T.xrows, c->T.xful, c->T.xidx, c->T.hrows, c->T.commit_ts, c->T.idr, c->T.xrun, c->T.big, c->gate_status, c->ev_buf,
                     c->b_start, c->ts, c->cs, c->ce, c->sres, c->dslot, c->cslot, c->pre_e, c->pre_p,
                     c->pp_dslot, c->pp_cslot, c->gslot, c->pslot, c->prev_id, c->pend_last, c->pend_first, c->prev_pend,
                     c->gclaim, c->gcnt_id, c->gcnt_pd, c->gmem, c->gbeg, c->gend, c->gfill, c->pfill, c->pbeg, c->skey, c->sval, c->skey_s,
@@ -760,6 +797,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     }
     if (c->h_counters) (void)hipHostFree(c->h_counters);
     if (c->h_report) (void)hipHostFree(c->h_report);
+    if (c->h_gate) (void)hipHostFree(c->h_gate);
     if (c->h_counts) (void)hipHostFree(c->h_counts);
     if (c->h_stage_start) (void)hipHostFree(c->h_stage_start);
     if (c->h_base) (void)hipHostFree(c->h_base);
@@ -1024,6 +1062,7 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_crea
     F.tile = F.small ? FP_SMALL_TILE : fp_tile_events();
     static const bool no_eager = getenv("TBGPU_NO_EAGER") != nullptr;  // A/B timing: fp_dupcheck + inserts
     F.eager = (c->ids_nonmono && !F.dry && !no_eager) ? 1u : 0u;
+    F.gate = c->gate_arm ? c->gate_status : nullptr;
     const BlockInline bi = take_block(c);
     prof_mark(c, PH_PREP);
     if (!F.small) fp_launch_prep(F, s, bi);
@@ -2109,8 +2148,128 @@ extern "C" int tbgpu_copy_to_device(tbgpu_ctx* c, void* dst_device, const void* 
     return 0;
 }
 
+// The prepared drop-in commit's gate: one lane waits for the commit call's word in
+// pinned host memory (bounded: budget wall-clock ticks), then writes the call's batch
+// block (one batch of n events at the timestamp the call brought) and the reply cursor's
+// reset, and its verdict for the gated kernels behind it on the stream; a gate that lets
+// nothing through (cancelled, or the call did not come in time) also tells the host.
+__global__ void k_gate(const u32* go, const u64* ts_word, u32* ack, u32 seq, u32 n, u32* block, u32 ts_off, u64* base,
+                       u32* status, u64 budget) {
+    if (threadIdx.x != 0) return;
+    const u64 t0 = wall_clock64();
+    u32 verdict = GATE_OFF;
+    for (;;) {
+        const u32 v = __hip_atomic_load(go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (v == seq) {
+            verdict = GATE_GO;
+            break;
+        }
+        if (v == (seq | GATE_CANCEL_BIT) || wall_clock64() - t0 > budget) break;
+        __builtin_amdgcn_s_sleep(16);
+    }
+    if (verdict == GATE_GO) {
+        const u64 ts = __hip_atomic_load(ts_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        block[0] = 0;
+        block[1] = n;
+        *(u64*)(block + ts_off) = ts;
+        base[BASE_REPLIES] = 0;
+    } else {
+        __hip_atomic_store(ack, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    *status = verdict;
+}
+
+// tbgpu_prefetch_transfers, when the commit that follows will be a one-batch fast call
+// (fp_commit_small + fp_tail): everything but the timestamp is known, so both launches
+// are enqueued now behind k_gate, and the commit call only writes its timestamp and
+// sequence number into pinned memory: no launch on its critical path.  Any other call
+// releases the gate (gate_cancel), and a gate that waits past its budget lets nothing
+// through; the commit then runs as an ordinary prefetched call.
+static void prepare_gated(tbgpu_ctx* c, u32 n) {
+    static const bool off = getenv("TBGPU_NO_GATE") != nullptr;  // A/B timing
+    static const bool no_tail = getenv("TBGPU_NO_TAIL") != nullptr, no_small = getenv("TBGPU_NO_SMALL") != nullptr;
+    if (off || no_tail || no_small || n == 0 || n > FP_TAIL_MAX || c->prof || c->rt_dry ||
+        (c->opt.flags & TBGPU_OPT_FORCE_GENERAL) || spec_disabled() || !fast_due(c) || c->rows_hi + n > c->xrow_cap)
+        return;
+    ensure_h_rc(c, 1);
+    c->rt_ev_ts = nullptr;
+    c->rt_ctl = nullptr;
+    c->blk_words = 0;  // the gate writes the block
+    c->b_ts = (u64*)(c->b_start + batch_ts_offset(1));
+    const u32 seq = ++c->call_seq;
+    c->h_gate[GW_ACK] = 0;
+    __atomic_store_n(&c->h_gate[GW_GO], 0u, __ATOMIC_RELEASE);
+    k_gate<<<1, 64, 0, c->stream>>>(c->h_gate_dev + GW_GO, (const u64*)(c->h_gate_dev + GW_TS), c->h_gate_dev + GW_ACK,
+                                    seq, n, c->b_start, (u32)batch_ts_offset(1), c->T.base, c->gate_status,
+                                    c->gate_budget);
+    HIP_CHECK(hipGetLastError());
+    c->tail_rp = TailReport{c->h_report_dev, 1, (const u64*)c->res_buf, c->h_res_dev,
+                            c->h_report_dev + RPT_COUNTS + c->bmax, seq};
+    c->tail_reported = false;
+    c->gate_arm = true;
+    const bool launched = try_fast(c, (const Transfer*)c->pf_buf, n, 1, (tbgpu_create_transfers_result_t*)c->res_buf,
+                                   /*spec=*/true);
+    c->gate_arm = false;
+    if (!launched || !c->tail_reported)
+        tbgpu_fatal("prefetch", "a prepared commit did not take the small fast launches", __FILE__, __LINE__);
+    c->gate_pending = true;
+    c->gate_seq = seq;
+    c->gate_n = n;
+}
+
+// The commit of a prepared call: release the gate with the timestamp, then wait for
+// fp_tail's sequence word (or the gate's note that it let nothing through).  Returns
+// false when the call must run as an ordinary one (the gate let nothing through, or the
+// fast attempt fell back: its effects are undone by spec_settle's fp_undo).
+static bool commit_gated(tbgpu_ctx* c, u64 timestamp, tbgpu_create_transfers_result_t* results, u32* count_out) {
+    c->gate_pending = false;
+    const u32 seq = c->gate_seq, n = c->gate_n;
+    memcpy(c->h_gate + GW_TS, &timestamp, sizeof timestamp);
+    __atomic_store_n(&c->h_gate[GW_GO], seq, __ATOMIC_RELEASE);
+    ht_mark(c, 4);
+    const volatile u32* seqw = c->h_report + RPT_COUNTS + c->bmax;
+    bool go = true;
+    for (u32 k = 0;; k++) {
+        if (__atomic_load_n(seqw, __ATOMIC_ACQUIRE) == seq) break;
+        if (__atomic_load_n(&c->h_gate[GW_ACK], __ATOMIC_ACQUIRE) == seq) {
+            go = false;
+            break;
+        }
+        if ((k & 1023) == 1023 && hipStreamQuery(c->stream) != hipErrorNotReady) {
+            wait_stream(c->stream);  // (reports a failure)
+            go = __atomic_load_n(seqw, __ATOMIC_ACQUIRE) == seq;
+            break;
+        }
+    }
+    ht_mark(c, 6);
+    c->tail_reported = false;
+    if (!go) {
+        c->spec_pending = false;
+        return false;
+    }
+    memcpy(c->h_counters, c->h_report, CNT_COUNT * sizeof(u32));
+    memcpy(c->h_base, c->h_report + RPT_BASE, 4 * sizeof(u64));
+    memcpy(c->h_rc, c->h_report + RPT_COUNTS, sizeof(u32));
+    if (!spec_settle(c)) return false;
+    const std::vector<u32> starts = {0u, n};
+    copy_results_to_batches(c, 1, starts, &n, (u8*)results);
+    c->n_rows = c->h_base[BASE_ROWS];
+    c->n_hist = c->h_base[BASE_HIST];
+    c->rows_hi = c->n_rows;
+    c->slow_chunks = 0;
+    c->stats.events = n;
+    c->stats.iterations = 1;
+    c->stats.sorts = 0;
+    c->stats.path = 1;
+    c->stats.device_ms = 0;  // (no call events around a prepared commit)
+    c->stats_lazy = false;
+    for (double& v : c->stats.phase_ms) v = 0;
+    *count_out = c->h_rc[0];
+    return true;
+}
+
 extern "C" int tbgpu_prefetch_transfers(tbgpu_ctx* c, const tbgpu_transfer_t* events, uint32_t count) {
-    CallGuard guard_(c, false);
+    CallGuard guard_(c, false);  // (releases an earlier prepared commit)
     c->pf_valid = false;
     if (count > TBGPU_BATCH_MAX) return -22;
     // behind the previous commit on the ctx's stream (that commit has returned: its
@@ -2120,11 +2279,12 @@ extern "C" int tbgpu_prefetch_transfers(tbgpu_ctx* c, const tbgpu_transfer_t* ev
     c->pf_src = events;
     c->pf_n = count;
     c->pf_valid = true;
+    prepare_gated(c, count);
     return 0;
 }
 
 extern "C" int tbgpu_prefetch_wait(tbgpu_ctx* c) {
-    CallGuard guard_(c, false);
+    CallGuard guard_(c, false, /*keep_gate=*/true);
     if (c->pf_valid) wait_event(c->pf_ev);
     return 0;
 }
@@ -2136,12 +2296,27 @@ extern "C" uint32_t tbgpu_create_transfers(tbgpu_ctx* c, uint64_t timestamp, con
         c->ht0 = std::chrono::steady_clock::now();
         c->ht_calls++;
     }
-    CallGuard guard_(c, false);
+    CallGuard guard_(c, false, /*keep_gate=*/true);
     ht_mark(c, 0);
     uint32_t rc = 0;
     const uint64_t ts = timestamp;
     uint32_t out;
-    if (c->pf_valid && c->pf_src == (const void*)events && c->pf_n == count) {
+    const bool prepared = c->pf_valid && c->pf_src == (const void*)events && c->pf_n == count;
+    if (prepared && c->gate_pending && c->gate_n == count) {
+        c->pf_valid = false;
+        if (commit_gated(c, timestamp, results, &out)) {
+            ht_mark(c, 7);
+            c->ht_on = false;
+            return out;
+        }
+        // the gate let nothing through, or the attempt fell back: an ordinary call
+        out = (uint32_t)transfers_batches(c, 1, &ts, &count, (const Transfer*)c->pf_buf, true, results, false, &rc);
+        ht_mark(c, 7);
+        c->ht_on = false;
+        return out;
+    }
+    gate_cancel(c);
+    if (prepared) {
         // prefetched: the events are in HBM already (the copy is ahead on the stream)
         c->pf_valid = false;
         out = (uint32_t)transfers_batches(c, 1, &ts, &count, (const Transfer*)c->pf_buf, true, results, false, &rc);

@@ -34,7 +34,12 @@ struct FastArgs {
     // fp_dupcheck, no inserts after; the fix moves a slot to its row's rank, a broken
     // chain withdraws its members' claims (XIDX_TOMB), a fallback clears every claim.
     u32 eager;
+    // A prepared drop-in commit (tbgpu_prefetch_transfers): the kernels were enqueued
+    // behind k_gate, which writes GATE_GO here once the commit call has come (with its
+    // timestamp), or GATE_OFF; both kernels do nothing unless GO.  Null: ungated.
+    const u32* gate;
 };
+constexpr u32 GATE_GO = 1, GATE_OFF = 2;
 // per tile: max lo, max hi, min lo, min hi of the accepted ids; max accepted timestamp;
 // accepted count; (fp_commit_small) failures and FL_* flags
 constexpr u32 TILE_WORDS = 8;

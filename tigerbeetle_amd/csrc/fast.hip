@@ -345,6 +345,7 @@ __device__ __forceinline__ void fp_commit_body(const Tables& T, FastArgs F, cons
 #if defined(FP_LDS_EVENTS)
     __shared__ uint4 s_stage[TILE / 64][STAGE_RECS * 8];
 #endif
+    if (SMALL && F.gate && *F.gate != GATE_GO) return;  // a prepared commit that did not come
     const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const u32 tile = blockIdx.x;
     const u32 i = tile * TILE + tid;
@@ -994,6 +995,7 @@ __device__ __forceinline__ u32 fp_cnt(const FastArgs& F, int k) {
 }
 
 __global__ __launch_bounds__(FP_TAIL_THREADS) void fp_tail(Tables T, FastArgs F, BlockInline bi, TailReport rp) {
+    if (F.gate && *F.gate != GATE_GO) return;  // a prepared commit that did not come
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6, n = F.n;
     const u32 ntiles = (n + F.tile - 1) / F.tile;
     __shared__ u32 s_flags, s_bad, s_run, s_ok, s_fix;

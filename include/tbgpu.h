@@ -295,8 +295,15 @@ uint32_t tbgpu_create_transfers(tbgpu_ctx* ctx, uint64_t timestamp,
  * callback's point).  The next tbgpu_create_transfers with the same `events` pointer
  * and `count` commits from the staged copy (no copy inside the commit); any other
  * create call (accounts, transfers, batches, device and routed forms), an import,
- * tbgpu_reset and tbgpu_open discard it.  As in the reference, the prepare's body must not change
- * between prefetch and commit.  Returns 0, or -22 when count exceeds a batch. */
+ * tbgpu_reset and tbgpu_open discard it.
+ * When that commit will be a one-batch fast call, the prefetch also prepares it: its
+ * launches are enqueued behind a gate kernel that waits (at most 10 ms) for the
+ * commit's timestamp in pinned memory, so the commit itself launches nothing.  Any
+ * call on the ctx other than tbgpu_prefetch_wait and that commit releases the gate
+ * (the prepared launches then do nothing); a commit after the gate's wait ran out is an
+ * ordinary prefetched call.  Results never depend on which of these happened.
+ * As in the reference, the prepare's body must not change between prefetch and commit.
+ * Returns 0, or -22 when count exceeds a batch. */
 int tbgpu_prefetch_transfers(tbgpu_ctx* ctx, const tbgpu_transfer_t* events, uint32_t count);
 int tbgpu_prefetch_wait(tbgpu_ctx* ctx);
 

@@ -111,6 +111,9 @@ def _make(spec):
         return ShardWorkload(seed, world, steps, B)
     if kind == "mixr":
         return random_u128_ids(ShardWorkload(seed, world, steps, B), seed)
+    if kind == "mixw":  # wider: 128-event batches over 8 ledgers of 1000 accounts
+        return random_u128_ids(ShardWorkload(seed, world, steps, B, batch=128, ledgers=8, accounts_per_ledger=1000),
+                               seed)
     if kind == "mixa":
         from tests.shard_backends import with_account_recreates
         return with_account_recreates(ShardWorkload(seed, world, steps, B), seed)
@@ -241,6 +244,14 @@ def test_general_step_random_u128_ids(world):
     commit, tensor collectives), bit-exact against the single state machine."""
     stats = _check(("mixr", 71 + world, world, 3, 2), world, device_step=True)
     assert stats["steps"] > 0 and stats["dry_rounds"] > 0
+
+
+def test_general_step_same_id_imported_to_two_shards():
+    """A committed id requested by post/voids routed to two other shards in one round:
+    its holder answers one row per request (4 ranks, 8 ledgers: the case the 2- and
+    3-rank mixes did not reach; found by profiles/general_rehearsal.py)."""
+    stats = _check(("mixw", 12, 4, 4, 2), 4)
+    assert stats["imports"] > 0
 
 
 @pytest.mark.parametrize("spec", [("mix", 81, 2, 3, 2), ("mixr", 82, 3, 2, 2)])

@@ -180,6 +180,7 @@ class ShardedStateMachine:
         self._worker = None       # the pipelined stream's commit thread
         self.timing = {"eligibility_ms": 0.0, "order_ms": 0.0, "partition_ms": 0.0, "exchange_ms": 0.0,
                        "commit_ms": 0.0, "replies_ms": 0.0}
+        self.gtiming = {}         # the general step's phases (shard_vec.round_vec), when timed
         self.stats = {"steps": 0, "splits": 0, "dry_rounds": 0, "cross_chains": 0, "imports": 0,
                       "preruns": 0, "serial_fallbacks": 0, "device_fallbacks": 0}
 

@@ -188,6 +188,7 @@ def round_vec(sm, glob, T, my_events, replies, start):
     W, me = sm.world, sm.rank
     g0, i0 = start
     P0 = (g0 << 32) | i0
+    mark = _phase_clock(sm)
     # ---- 1. my remaining events, in global order
     evs, Gs, Is = [], [], []
     for g in sorted(my_events):
@@ -214,6 +215,7 @@ def round_vec(sm, glob, T, my_events, replies, start):
         cstart[1:] = (G[1:] != G[:-1]) | ~linked[:-1]
     chain = P[segment_first(cstart, n)] if n else np.zeros(0, np.int64)
 
+    mark("order")
     # ---- 2. directory
     xlo, xhi = E["id_lo"], E["id_hi"]
     plo, phi = E["pending_id_lo"], E["pending_id_hi"]
@@ -248,6 +250,7 @@ def round_vec(sm, glob, T, my_events, replies, start):
     p_h = np.full(n, ANY, np.int64)
     p_p = np.full(n, INF, np.int64)
     p_t[r1], p_h[r1], p_p[r1] = mine_t[len(r0):], mine_h[len(r0):], mine_p[len(r0):]
+    mark("directory")
 
     # ---- 3. routing of my events (shard.py _round, rule for rule)
     def same_chain(pos):
@@ -289,6 +292,7 @@ def round_vec(sm, glob, T, my_events, replies, start):
         route = np.where(route == ANY, np.repeat(fill, np.diff(np.append(seg, n))), route)
     # post/voids whose id is committed on another shard: that row, imported
     imp = pv & (id_t == EXISTS) & (id_h != route)
+    mark("routing")
 
     # ---- 4. the earliest hazard over all ranks splits the step
     hz = int(chain[np.nonzero(hazard)[0]].min()) if hazard.any() else INF
@@ -303,6 +307,7 @@ def round_vec(sm, glob, T, my_events, replies, start):
         stop = min_over_ranks(comm, nxt)
     loc = P < stop
     _do_imports(sm, xlo[imp], xhi[imp], id_h[imp], route[imp])
+    mark("split_imports")
 
     # ---- 5. events to their owners (global order kept per source)
     dest = route[loc]
@@ -336,6 +341,7 @@ def round_vec(sm, glob, T, my_events, replies, start):
     if me == 0:
         sm.stats["cross_chains"] += len(span_keys)
 
+    mark("exchange")
     # ---- 6. commit (dry rounds while chains span shards)
     in_span = np.isin(mC, span_keys)
     mG, mI = mP >> 32, mP & 0xFFFFFFFF
@@ -396,6 +402,7 @@ def round_vec(sm, glob, T, my_events, replies, start):
                                    "(its break depends on no other chain: an engine invariant failed)")
         brk = nb
 
+    mark("commit")
     # ---- 7. replies to their sources
     rp, rg, ri = mP[mask], mG[mask], mI[mask]
     bad = res != 0
@@ -410,9 +417,27 @@ def round_vec(sm, glob, T, my_events, replies, start):
         m = np.sort(ids)[-1]
         top = (int(m["hi"]) << 64) | int(m["lo"])
     sm.max_id = max(sm.max_id, sm.comm.allreduce_max(top))
+    mark("replies")
     if stop == INF:
         return None
     return (int(stop) >> 32, int(stop) & 0xFFFFFFFF)
+
+
+def _phase_clock(sm):
+    """Wall time (and this thread's CPU time, "cpu_" keys) of the general step's phases
+    into sm.gtiming (ms) when sm.timed.  The phases end in a host value (every device call of the step returns host arrays), so
+    the marks need no device synchronisation."""
+    if not sm.timed:
+        return lambda name: None
+    import time
+    t = [time.perf_counter(), time.thread_time()]
+
+    def mark(name):
+        now, cpu = time.perf_counter(), time.thread_time()
+        sm.gtiming[name] = sm.gtiming.get(name, 0.0) + (now - t[0]) * 1e3
+        sm.gtiming["cpu_" + name] = sm.gtiming.get("cpu_" + name, 0.0) + (cpu - t[1]) * 1e3
+        t[0], t[1] = now, cpu
+    return mark
 
 
 def _do_imports(sm, lo, hi, holder, dest):
@@ -431,9 +456,10 @@ def _do_imports(sm, lo, hi, holder, dest):
         q = np.zeros(len(rows), dtype=U128_DTYPE)
         q["lo"], q["hi"] = rows[:, 0].view(np.uint64), rows[:, 1].view(np.uint64)
         found = sm.backend.lookup_transfers(q)
-        if len(found) != len(np.unique(_hl(q["lo"], q["hi"]))):
-            raise RuntimeError("sharded commit: the directory names a shard that does not hold the transfer")
         fk = _hl(found["id_lo"], found["id_hi"])
+        # the same id may be requested for several destinations (one row per request)
+        if not np.isin(_hl(q["lo"], q["hi"]), fk).all():
+            raise RuntimeError("sharded commit: the directory names a shard that does not hold the transfer")
         fo = np.argsort(fk, kind="stable")
         rows_by_q = found[fo[np.searchsorted(fk[fo], _hl(q["lo"], q["hi"]))]]
         for d in range(W):

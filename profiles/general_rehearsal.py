@@ -8,7 +8,7 @@ them.  The ranks are threads of one process, so the host phases share one interp
 lock: their wall times are upper bounds of what separate processes would take; the
 CPU times ("cpu_" keys) are each thread's own work.
 
-    python profiles/general_rehearsal.py [--worlds 2 4] [--batch 8190] [--batches 2] [--steps 4]
+    python profiles/general_rehearsal.py [--worlds 2 4] [--batch 8190] [--batches 2] [--steps 4] [--windows 0 4096]
 """
 import argparse
 import json
@@ -22,7 +22,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def run(world, batch, bpr, steps, seed):
+def run(world, batch, bpr, steps, seed, window=None):
     import torch
 
     from tests.shard_workload import ShardWorkload, random_u128_ids
@@ -46,6 +46,8 @@ def run(world, batch, bpr, steps, seed):
             comm = Comm(rank, world, device=dev)
             comm.dist = ThreadDist(group, rank)
             sm = ShardedStateMachine(eng, comm)
+            if window is not None:
+                sm.round_window = window
             sm.create_accounts(w.account_batches if rank == 0 else [])
             walls = []
             for s in range(steps):
@@ -79,7 +81,7 @@ def run(world, batch, bpr, steps, seed):
     phases = {k: round(float(np.mean([o["g"].get(k, 0.0) for o in outs])) / timed, 3) for k in keys}
     host = sum(v for k, v in phases.items() if not k.startswith("cpu_") and k != "commit")
     host_cpu = sum(v for k, v in phases.items() if k.startswith("cpu_") and k != "cpu_commit")
-    return {"world": world, "events_per_step": per_step, "batch": batch, "batches_per_rank": bpr,
+    return {"world": world, "events_per_step": per_step, "round_window": window, "batch": batch, "batches_per_rank": bpr,
             "timed_steps": timed, "ms_per_step": round(wall, 3),
             "events_per_s": round(per_step / (wall * 1e-3), 1),
             "phases_ms_per_step": phases, "host_wall_ms_per_step": round(host, 3),
@@ -95,9 +97,12 @@ def main():
     ap.add_argument("--batches", type=int, default=2)
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--windows", type=int, nargs="+", default=[None],
+                    help="ShardedStateMachine.round_window values (0: the whole step per round)")
     a = ap.parse_args()
     for world in a.worlds:
-        print(json.dumps(run(world, a.batch, a.batches, a.steps, a.seed + world)), flush=True)
+        for win in a.windows:
+            print(json.dumps(run(world, a.batch, a.batches, a.steps, a.seed + world, win)), flush=True)
 
 
 if __name__ == "__main__":

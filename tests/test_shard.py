@@ -41,7 +41,7 @@ def _backend(kind, w, rank=0, world=1):
 
 
 def _worker(rank, world, port, out_dir, spec, kind="oracle", device_step=False, max_rounds=None, vectorized=True,
-            skew_dry_rank=None):
+            skew_dry_rank=None, window=None):
     import torch.distributed as dist
     from tigerbeetle_amd.shard import Comm, ShardedStateMachine
     if skew_dry_rank == rank:
@@ -55,6 +55,8 @@ def _worker(rank, world, port, out_dir, spec, kind="oracle", device_step=False, 
         if max_rounds is not None:
             sm.max_rounds = max_rounds
         sm.vectorized = vectorized
+        if window is not None:
+            sm.round_window = window
         acc_replies = sm.create_accounts(w.account_batches if rank == 0 else [])
         replies = []
         if device_step == "stream":
@@ -122,11 +124,12 @@ def _make(spec):
     return config4_small(seed, world, steps, B)
 
 
-def _check(spec, world, kind="oracle", device_step=False, max_rounds=None, vectorized=True, skew_dry_rank=None):
+def _check(spec, world, kind="oracle", device_step=False, max_rounds=None, vectorized=True, skew_dry_rank=None,
+           window=None):
     import torch.multiprocessing as mp
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(world, _free_port(), d, spec, kind, device_step, max_rounds, vectorized,
-                                skew_dry_rank),
+                                skew_dry_rank, window),
                  nprocs=world, join=True)
         outs = [pickle.load(open(os.path.join(d, f"r{r}.pkl"), "rb")) for r in range(world)]
     return verify(_make(spec), outs, world)
@@ -252,6 +255,15 @@ def test_general_step_same_id_imported_to_two_shards():
     3-rank mixes did not reach; found by profiles/general_rehearsal.py)."""
     stats = _check(("mixw", 12, 4, 4, 2), 4)
     assert stats["imports"] > 0
+
+
+@pytest.mark.parametrize("window", [1, 37])
+def test_general_step_round_window(window):
+    """Rounds bounded by a window of events (ShardedStateMachine.round_window, cut at
+    the chain the window ends in, or after the round's first chain): the same replies
+    and state as the single state machine, over more rounds."""
+    stats = _check(("mixr", 75 + window, 3, 3, 2), 3, device_step=True, window=window)
+    assert stats["steps"] > 3 * 6
 
 
 @pytest.mark.parametrize("spec", [("mix", 81, 2, 3, 2), ("mixr", 82, 3, 2, 2)])

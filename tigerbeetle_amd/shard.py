@@ -173,6 +173,8 @@ class ShardedStateMachine:
         self.commit_timestamp = 0
         self.max_id = 0         # every transfer id seen so far is <= this (the fast step's id filter)
         self.max_rounds = MAX_ROUNDS
+        # events of the general step's round window (shard_vec.window_cut); 0: the whole step
+        self.round_window = 4096
         self.limit_ids: set[int] = set()  # ids of accounts created with a balance limit flag
         self.amount_bound = 0.0  # >= the sum of every transfer amount routed: bounds every balance
         self.timed = False       # accumulate per-phase wall times of the device step (with syncs)

@@ -180,6 +180,44 @@ def _directory_host(sm, R: np.ndarray):
 
 
 # ----------------------------------------------------------------- round --
+def window_cut(sm, glob, my_events, g0, i0) -> int:
+    """Collective when the window ends inside a batch.  The global position where this
+    round stops at the latest: about sm.round_window events after (g0, i0), moved back
+    to the start of the chain it falls in (chains never cross a batch; the batch's
+    owner knows its chains), or past that chain when it is the round's first.  A round
+    only commits its prefix before the first hazard, so its routing needs no events
+    beyond this point; the window bounds the host work of the rounds that hazards
+    make many.  INF: the rest of the step fits the window."""
+    left = sm.round_window
+    if not left:
+        return INF
+    g, i = g0, i0
+    while g < len(glob):
+        if left <= 0:
+            return g << 32
+        c = glob[g][2]
+        if c - i > left:
+            break
+        left -= c - i
+        g, i = g + 1, 0
+    else:
+        return INF
+    iw = i + left
+    prop = INF
+    if glob[g][0] == sm.rank:
+        linked = (my_events[g]["flags"] & LINKED) != 0
+        s = iw
+        while s > 0 and linked[s - 1]:
+            s -= 1
+        if g == g0 and s <= i0:  # the window's first chain: cut after it
+            e = iw
+            while e < c - 1 and linked[e]:
+                e += 1
+            s = e + 1
+        prop = (g << 32) | s if s < c else (g + 1) << 32
+    return min_over_ranks(sm.comm, prop)
+
+
 def round_vec(sm, glob, T, my_events, replies, start):
     """ShardedStateMachine._round over arrays: the same routing, splits, dry rounds
     and commit; returns None when the round committed every remaining event, else the
@@ -189,17 +227,20 @@ def round_vec(sm, glob, T, my_events, replies, start):
     g0, i0 = start
     P0 = (g0 << 32) | i0
     mark = _phase_clock(sm)
-    # ---- 1. my remaining events, in global order
+    # ---- 1. my remaining events of the round's window, in global order
+    wcut = window_cut(sm, glob, my_events, g0, i0)
+    wg, wi = (wcut >> 32, wcut & 0xFFFFFFFF) if wcut != INF else (INF, 0)
     evs, Gs, Is = [], [], []
     for g in sorted(my_events):
-        if g < g0:
+        if g < g0 or g > wg:
             continue
         b = my_events[g]
         lo = i0 if g == g0 else 0
-        if lo < len(b):
-            evs.append(b[lo:])
-            Gs.append(np.full(len(b) - lo, g, np.int64))
-            Is.append(np.arange(lo, len(b), dtype=np.int64))
+        hi = wi if g == wg else len(b)
+        if lo < hi:
+            evs.append(b[lo:hi])
+            Gs.append(np.full(hi - lo, g, np.int64))
+            Is.append(np.arange(lo, hi, dtype=np.int64))
     E = np.concatenate(evs) if evs else np.zeros(0, TRANSFER_DTYPE)
     G = np.concatenate(Gs) if Gs else np.zeros(0, np.int64)
     I = np.concatenate(Is) if Is else np.zeros(0, np.int64)
@@ -305,6 +346,7 @@ def round_vec(sm, glob, T, my_events, replies, start):
             after = np.nonzero((chain != c) & (P > P0))[0]
             nxt = int(P[after[0]]) if len(after) else int(((P[chain == c][-1] >> 32) + 1) << 32)
         stop = min_over_ranks(comm, nxt)
+    stop = min(stop, wcut)
     loc = P < stop
     _do_imports(sm, xlo[imp], xhi[imp], id_h[imp], route[imp])
     mark("split_imports")

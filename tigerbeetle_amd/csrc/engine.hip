@@ -1282,7 +1282,12 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
     const bool chains = true;  // whether the call has chains is on the device: scan with the chain part
     static const bool no_incr = getenv("TBGPU_NO_INCR") != nullptr;  // A/B timing: every event every pass
     u32 p = 0;                  // next pass to enqueue
-    u32 group = std::max<u32>(2, std::min<u32>(c->last_passes, PASS_GROUP_MAX));
+    // the first group: the last fixed point's passes plus a margin.  A pass past
+    // convergence returns at once (≈3 µs a launch); a second group costs the host round
+    // trip, the first group's gated epilogue run as no-ops and a second one launched
+    // just in time (≈250 µs of a config-3 chunk in profiles/r05/kernel_trace_config3.csv)
+    static const u32 margin = getenv("TBGPU_PASS_MARGIN") ? (u32)atoi(getenv("TBGPU_PASS_MARGIN")) : 3u;
+    u32 group = std::max<u32>(2, std::min<u32>(c->last_passes + margin, PASS_GROUP_MAX));
     if (c->opt.flags & TBGPU_OPT_WALK_EARLY) group = 2;  // (tests) the walk after the first two passes
     u32 done_at = NONE32;
     for (;;) {

@@ -1,8 +1,10 @@
 """Compare timing variants of the engine library (build.build_variant) on the
 bench workload: each variant runs in fresh processes with TBGPU_LIB pointing at
 its library.  Usage (GPU box, repo root):
-    python3 profiles/variants.py NAME ... [-- bench args]
-where build/var_NAME/libtbgpu.so was built beforehand; 'base' is the product library."""
+    python3 profiles/variants.py NAME[=DEFINE+DEFINE..] ... [-- bench args]
+'base' is the product library; any other NAME is tigerbeetle_amd/build/var_NAME/libtbgpu.so,
+built here from its DEFINEs when missing (the variant builds stay off the pushed tree:
+.gpurunignore)."""
 import json
 import os
 import subprocess
@@ -16,13 +18,17 @@ if "--" in argv:
     argv, bench_args = argv[:k], argv[k + 1:]
 reps = int(os.environ.get("REPS", "3"))
 for spec in argv:
-    name = spec
+    name, _, defs = spec.partition("=")
     lib = os.path.join(ROOT, "tigerbeetle_amd", "build", "var_" + name, "libtbgpu.so")
     env = dict(os.environ)
     if name != "base":
         if not os.path.exists(lib):
-            print(name, "missing", lib, flush=True)
-            continue
+            if not defs:
+                print(name, "missing", lib, "(give NAME=DEFINE+DEFINE to build it)", flush=True)
+                continue
+            sys.path.insert(0, ROOT)
+            from tigerbeetle_amd.build import build_variant
+            build_variant(name, defs.split("+"))
         env["TBGPU_LIB"] = lib
     vals, commits, idx, app = [], [], [], []
     for _ in range(reps):

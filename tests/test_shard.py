@@ -41,7 +41,7 @@ def _backend(kind, w, rank=0, world=1):
 
 
 def _worker(rank, world, port, out_dir, spec, kind="oracle", device_step=False, max_rounds=None, vectorized=True,
-            skew_dry_rank=None, window=None):
+            skew_dry_rank=None, window=None, shard_stops=True):
     import torch.distributed as dist
     from tigerbeetle_amd.shard import Comm, ShardedStateMachine
     if skew_dry_rank == rank:
@@ -57,6 +57,7 @@ def _worker(rank, world, port, out_dir, spec, kind="oracle", device_step=False, 
         sm.vectorized = vectorized
         if window is not None:
             sm.round_window = window
+        sm.shard_stops = shard_stops
         acc_replies = sm.create_accounts(w.account_batches if rank == 0 else [])
         replies = []
         if device_step == "stream":
@@ -125,11 +126,11 @@ def _make(spec):
 
 
 def _check(spec, world, kind="oracle", device_step=False, max_rounds=None, vectorized=True, skew_dry_rank=None,
-           window=None):
+           window=None, shard_stops=True):
     import torch.multiprocessing as mp
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(world, _free_port(), d, spec, kind, device_step, max_rounds, vectorized,
-                                skew_dry_rank, window),
+                                skew_dry_rank, window, shard_stops),
                  nprocs=world, join=True)
         outs = [pickle.load(open(os.path.join(d, f"r{r}.pkl"), "rb")) for r in range(world)]
     return verify(_make(spec), outs, world)
@@ -255,6 +256,51 @@ def test_general_step_same_id_imported_to_two_shards():
     3-rank mixes did not reach; found by profiles/general_rehearsal.py)."""
     stats = _check(("mixw", 12, 4, 4, 2), 4)
     assert stats["imports"] > 0
+
+
+@pytest.mark.parametrize("shard_stops", [True, False])
+def test_general_step_per_shard_stops(shard_stops):
+    """Rounds with a stop per shard (ShardStops: hazards, chains, shared keys and effect
+    shards) and with one stop for all: both bit-exact, the first in fewer rounds."""
+    stats = _check(("mixw", 14, 4, 3, 2), 4, window=200, shard_stops=shard_stops)
+    assert stats["steps"] > 3
+
+
+def test_shard_stops_rules():
+    """ShardStops._solve on hand-made rounds (positions 0..; two shards)."""
+    from tigerbeetle_amd.shard_vec import EF_ALL, EF_NONE, INF, ShardStops
+    P = np.arange(8, dtype=np.int64)
+    C = P.copy()
+    z = np.zeros(8, np.int64)
+    ef = np.array([0, 1, 0, 1, 0, 1, 0, 1])
+    H = np.zeros(8, bool)
+    H[2] = True  # a hazard on shard 0: shard 0 waits from 2 on, shard 1 goes on
+    w = ShardStops._solve(2, P, C, ef, H, z, z, INF)
+    assert w.tolist() == [False, False, True, False, True, False, True, False]
+    # a chain over 3 and 4 (shard 1 and 0): it waits whole, and shard 1 from 3 on
+    C2 = C.copy()
+    C2[4] = 3
+    w = ShardStops._solve(2, P, C2, ef, H, z, z, INF)
+    assert w.tolist() == [False, False, True, True, True, True, True, True]
+    # a later event sharing a key with a waiting one waits (5 on shard 1 names 2's id)
+    kx = z.copy()
+    kx[2] = 77
+    kp = z.copy()
+    kp[5] = 77
+    w = ShardStops._solve(2, P, C, ef, H, kx, kp, INF)
+    assert w.tolist() == [False, False, True, False, True, True, True, True]
+    # an event that may change state anywhere stops every shard once it waits
+    ef2 = ef.copy()
+    ef2[2] = EF_ALL
+    w = ShardStops._solve(2, P, C, ef2, H, z, z, INF)
+    assert w.tolist() == [False, False, True, True, True, True, True, True]
+    # one that cannot change state stops no shard
+    ef2[2] = EF_NONE
+    w = ShardStops._solve(2, P, C, ef2, H, z, z, INF)
+    assert w.tolist() == [False, False, True, False, False, False, False, False]
+    # the window
+    w = ShardStops._solve(2, P, C, ef, np.zeros(8, bool), z, z, 6)
+    assert w.tolist() == [False] * 6 + [True] * 2
 
 
 @pytest.mark.parametrize("window", [1, 37])

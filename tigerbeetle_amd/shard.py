@@ -175,6 +175,9 @@ class ShardedStateMachine:
         self.max_rounds = MAX_ROUNDS
         # events of the general step's round window (shard_vec.window_cut); 0: the whole step
         self.round_window = 4096
+        # the general step's rounds stop each shard at its own first waiting event
+        # (shard_vec.ShardStops); False: one stop for all, at the first hazard
+        self.shard_stops = True
         self.limit_ids: set[int] = set()  # ids of accounts created with a balance limit flag
         self.amount_bound = 0.0  # >= the sum of every transfer amount routed: bounds every balance
         self.timed = False       # accumulate per-phase wall times of the device step (with syncs)
@@ -285,11 +288,12 @@ class ShardedStateMachine:
         my_events = {gidx[(self.rank, j)]: b for j, b in enumerate(batches)}
         replies = {g: [] for g in my_events}
         start = (0, 0)  # resume point (global batch, index) after a hazard split
+        done = {g: np.zeros(len(b), dtype=bool) for g, b in my_events.items()}  # committed in a round
         while True:
             self.stats["steps"] += 1
             if self.vectorized:
                 from .shard_vec import round_vec
-                split = round_vec(self, glob, T, my_events, replies, start)
+                split = round_vec(self, glob, T, my_events, replies, start, done)
             else:
                 split = self._round(glob, T, my_events, replies, start)
             if split is None:

@@ -218,10 +218,13 @@ def window_cut(sm, glob, my_events, g0, i0) -> int:
     return min_over_ranks(sm.comm, prop)
 
 
-def round_vec(sm, glob, T, my_events, replies, start):
+def round_vec(sm, glob, T, my_events, replies, start, done=None):
     """ShardedStateMachine._round over arrays: the same routing, splits, dry rounds
     and commit; returns None when the round committed every remaining event, else the
-    (global batch, index) to resume from."""
+    (global batch, index) to resume from.  `done` (per global batch of this rank: which
+    events committed in earlier rounds) enables per-shard stops (shard_stops): then a
+    round commits, on each shard, its events before that shard's stop, and the resume
+    point is the first event not done anywhere."""
     comm = sm.comm
     W, me = sm.world, sm.rank
     g0, i0 = start
@@ -238,9 +241,13 @@ def round_vec(sm, glob, T, my_events, replies, start):
         lo = i0 if g == g0 else 0
         hi = wi if g == wg else len(b)
         if lo < hi:
-            evs.append(b[lo:hi])
-            Gs.append(np.full(hi - lo, g, np.int64))
-            Is.append(np.arange(lo, hi, dtype=np.int64))
+            idx = np.arange(lo, hi, dtype=np.int64)
+            if done is not None:
+                idx = idx[~done[g][lo:hi]]
+            if len(idx):
+                evs.append(b[idx])
+                Gs.append(np.full(len(idx), g, np.int64))
+                Is.append(idx)
     E = np.concatenate(evs) if evs else np.zeros(0, TRANSFER_DTYPE)
     G = np.concatenate(Gs) if Gs else np.zeros(0, np.int64)
     I = np.concatenate(Is) if Is else np.zeros(0, np.int64)
@@ -253,7 +260,7 @@ def round_vec(sm, glob, T, my_events, replies, start):
     # that ends it, within one batch (execute, src/state_machine.zig:1018-1035)
     cstart = np.ones(n, dtype=bool)
     if n > 1:
-        cstart[1:] = (G[1:] != G[:-1]) | ~linked[:-1]
+        cstart[1:] = (G[1:] != G[:-1]) | (I[1:] != I[:-1] + 1) | ~linked[:-1]
     chain = P[segment_first(cstart, n)] if n else np.zeros(0, np.int64)
 
     mark("order")
@@ -335,10 +342,20 @@ def round_vec(sm, glob, T, my_events, replies, start):
     imp = pv & (id_t == EXISTS) & (id_h != route)
     mark("routing")
 
-    # ---- 4. the earliest hazard over all ranks splits the step
-    hz = int(chain[np.nonzero(hazard)[0]].min()) if hazard.any() else INF
-    stop = min_over_ranks(comm, hz)
+    # ---- 4. the earliest hazard over all ranks splits the step (per-shard stops: each
+    # shard stops at its own first event that must wait)
+    stops = None
+    if done is not None and sm.shard_stops:
+        # the effect shard (ShardStops)
+        ef = np.where(led != 0, own, np.where(~pv | (p_t == PEND_NONE), EF_NONE,
+                                              np.where(p_t == PEND, p_h, EF_ALL)))
+        stops = ShardStops(sm, P, chain, ef, hazard, _key_hash(xlo, xhi, xval), _key_hash(plo, phi, pval), wcut)
+        stop = INF if stops.any_commits() else P0
+    else:
+        hz = int(chain[np.nonzero(hazard)[0]].min()) if hazard.any() else INF
+        stop = min_over_ranks(comm, hz)
     if stop <= P0:
+        stops = None
         sm.stats["serial_fallbacks"] += 1
         nxt = INF
         if n and P[0] == P0:
@@ -347,7 +364,7 @@ def round_vec(sm, glob, T, my_events, replies, start):
             nxt = int(P[after[0]]) if len(after) else int(((P[chain == c][-1] >> 32) + 1) << 32)
         stop = min_over_ranks(comm, nxt)
     stop = min(stop, wcut)
-    loc = P < stop
+    loc = P < stop if stops is None else stops.committed(P)
     _do_imports(sm, xlo[imp], xhi[imp], id_h[imp], route[imp])
     mark("split_imports")
 
@@ -436,6 +453,8 @@ def round_vec(sm, glob, T, my_events, replies, start):
                 span_keys, span_last = span_keys[keep], span_last[keep]
                 in_span = np.isin(mC, span_keys)
                 stop = min(stop, cut)
+                if stops is not None:
+                    stops.cut(cut)
                 sm.stats["serial_fallbacks"] += 1
                 brk, rounds = {}, 0
                 continue
@@ -460,9 +479,127 @@ def round_vec(sm, glob, T, my_events, replies, start):
         top = (int(m["hi"]) << 64) | int(m["lo"])
     sm.max_id = max(sm.max_id, sm.comm.allreduce_max(top))
     mark("replies")
+    if done is not None:
+        ok = P < stop if stops is None else stops.committed(P)
+        for g in np.unique(G[ok]).tolist():
+            done[g][I[ok & (G == g)]] = True
+    if stops is not None:
+        stop = stops.resume()
     if stop == INF:
         return None
     return (int(stop) >> 32, int(stop) & 0xFFFFFFFF)
+
+
+def _key_hash(lo, hi, valid) -> np.ndarray:
+    """A nonzero 64-bit hash of each valid u128 key (0: none).  Used only to find events
+    that share a key; a collision makes the stops more conservative, never wrong."""
+    with np.errstate(over="ignore"):
+        h = lo.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+        h ^= hi.astype(np.uint64) * np.uint64(0xC2B2AE3D27D4EB4F)
+        h ^= h >> np.uint64(29)
+    h = (h | np.uint64(1)).view(np.int64)
+    return np.where(valid, h, 0)
+
+
+EF_NONE, EF_ALL = -3, -4    # effect shard of an event that cannot change state / whose shard is open
+
+
+class ShardStops:
+    """Collective (one all-gather).  Per-shard stops of a round: which events of the
+    round's window wait, chosen so that each shard still applies its state changes in
+    global order.  Every rank gathers the round's events (position, chain, effect shard,
+    hazard, id and pending-id key hashes) and computes the same answer: the smallest
+    closed set of waiting events that holds
+
+    - every hazard (its outcome needs an earlier uncommitted event of another shard);
+    - whole chains (linked events commit together, src/state_machine.zig:1018-1035);
+    - events that share a key (id or pending id, in either role) in global order: a later
+      one waits while an earlier one does (an earlier post/void must not see a pending
+      created after it; a later repeat of an id must see the first one);
+    - every event at or after the stop of its *effect shard*: the only shard where it can
+      change state.  That is its ledger's owner (a transfer routed anywhere else fails:
+      `exists*`, or accounts / pending of another ledger), nothing for a transfer with
+      ledger 0 (it fails), and for a post/void with ledger 0 its pending's holder
+      (committed, or the first occurrence in the step: if that one fails, the occurrence
+      that holds the pending next round is an earlier hazard, which stopped its own
+      shard before this event), nothing when no pending precedes it (it fails; a later
+      event with that id waits with it, by the keys), or every shard for a pending
+      hazard (its pending may come from a later repeat of an id whose first occurrence
+      had no shard).  A shard's stop is the earliest chain start among the waiting events
+      it is the effect shard of.
+
+    Everything else an event reads is on its own shard or committed (the routing sends a
+    post/void to its pending's holder and a repeat of an id to the holder or into a
+    hazard), so the results are those of the global order: each shard applies the
+    state-changing events it commits in increasing position, round after round; a
+    waiting event that lands on another shard later can only fail there.  Fixed point
+    over the stops (each only falls, to a chain start); past 64 iterations every event
+    from the earliest waiting one on waits (the single stop of a round without them)."""
+
+    def __init__(self, sm, P, chain, ef, hazard, kx, kp, wcut):
+        rows = np.stack([P, chain, ef, hazard.astype(np.int64), kx, kp], axis=1) if len(P) else \
+            np.zeros((0, 6), np.int64)
+        A, _ = gather_rows(sm.comm, rows)
+        A = A[np.argsort(A[:, 0], kind="stable")]
+        self.P = A[:, 0]
+        self.wcut = wcut
+        self.wait = self._solve(sm.world, A[:, 0], A[:, 1], A[:, 2], A[:, 3] != 0, A[:, 4], A[:, 5], wcut)
+
+    @staticmethod
+    def _solve(W, P, C, EF, H, kx, kp, wcut):
+        n = len(P)
+        if not n:
+            return np.zeros(0, bool)
+        _, cidx = np.unique(C, return_inverse=True)
+        nch = int(cidx.max()) + 1
+        ke = np.concatenate([np.nonzero(kx)[0], np.nonzero(kp)[0]])
+        kk = np.concatenate([kx[kx != 0], kp[kp != 0]])
+        o = np.lexsort((P[ke], kk))
+        ke, kk = ke[o], kk[o]
+        kfirst = np.ones(len(kk), dtype=bool)
+        kfirst[1:] = kk[1:] != kk[:-1]
+        kgid = np.cumsum(kfirst) - 1
+        nk = int(kgid[-1]) + 1 if len(kgid) else 0
+        kP = P[ke]
+        one = EF >= 0
+        S = np.full(W, wcut, np.int64)
+        wait = H | (P >= wcut)
+        for _ in range(64):
+            smin = S.min()
+            w = wait | (one & (P >= S[np.where(one, EF, 0)])) | ((EF == EF_ALL) & (P >= smin))
+            w = np.bincount(cidx, weights=w, minlength=nch)[cidx] > 0
+            if nk:
+                fd = np.full(nk, INF, np.int64)
+                wk = w[ke]
+                np.minimum.at(fd, kgid[wk], kP[wk])
+                w[ke[kP > fd[kgid]]] = True
+                w = np.bincount(cidx, weights=w, minlength=nch)[cidx] > 0
+            S2 = S.copy()
+            np.minimum.at(S2, EF[w & one], C[w & one])
+            allw = w & (EF == EF_ALL)
+            if allw.any():
+                np.minimum(S2, C[allw].min(), out=S2)
+            if np.array_equal(S2, S) and np.array_equal(w, wait):
+                return w
+            S, wait = S2, w
+        first = P[wait].min() if wait.any() else wcut
+        return P >= first
+
+    def any_commits(self) -> bool:
+        return bool((~self.wait).any())
+
+    def committed(self, P) -> np.ndarray:
+        if not len(P):
+            return np.zeros(0, bool)
+        return ~self.wait[np.searchsorted(self.P, P)]
+
+    def cut(self, pos: int) -> None:
+        self.wait |= self.P >= pos
+        self.wcut = min(self.wcut, pos)
+
+    def resume(self) -> int:
+        """The first position not committed (INF: the step is done)."""
+        return min(int(self.P[self.wait].min()) if self.wait.any() else INF, self.wcut)
 
 
 def _phase_clock(sm):

@@ -8,7 +8,7 @@ them.  The ranks are threads of one process, so the host phases share one interp
 lock: their wall times are upper bounds of what separate processes would take; the
 CPU times ("cpu_" keys) are each thread's own work.
 
-    python profiles/general_rehearsal.py [--worlds 2 4] [--batch 8190] [--batches 2] [--steps 4] [--windows 0 4096]
+    python profiles/general_rehearsal.py [--worlds 2 4] [--batch 8190] [--batches 2] [--steps 4] [--windows 0 4096] [--stops 1 0]
 """
 import argparse
 import json
@@ -22,7 +22,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def run(world, batch, bpr, steps, seed, window=None):
+def run(world, batch, bpr, steps, seed, window=None, stops=True):
     import torch
 
     from tests.shard_workload import ShardWorkload, random_u128_ids
@@ -48,6 +48,7 @@ def run(world, batch, bpr, steps, seed, window=None):
             sm = ShardedStateMachine(eng, comm)
             if window is not None:
                 sm.round_window = window
+            sm.shard_stops = stops
             sm.create_accounts(w.account_batches if rank == 0 else [])
             walls = []
             for s in range(steps):
@@ -81,7 +82,7 @@ def run(world, batch, bpr, steps, seed, window=None):
     phases = {k: round(float(np.mean([o["g"].get(k, 0.0) for o in outs])) / timed, 3) for k in keys}
     host = sum(v for k, v in phases.items() if not k.startswith("cpu_") and k != "commit")
     host_cpu = sum(v for k, v in phases.items() if k.startswith("cpu_") and k != "cpu_commit")
-    return {"world": world, "events_per_step": per_step, "round_window": window, "batch": batch, "batches_per_rank": bpr,
+    return {"world": world, "events_per_step": per_step, "round_window": window, "shard_stops": stops, "batch": batch, "batches_per_rank": bpr,
             "timed_steps": timed, "ms_per_step": round(wall, 3),
             "events_per_s": round(per_step / (wall * 1e-3), 1),
             "phases_ms_per_step": phases, "host_wall_ms_per_step": round(host, 3),
@@ -97,12 +98,15 @@ def main():
     ap.add_argument("--batches", type=int, default=2)
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--stops", type=int, nargs="+", default=[1],
+                    help="ShardedStateMachine.shard_stops values (1: per-shard stops, 0: one stop)")
     ap.add_argument("--windows", type=int, nargs="+", default=[None],
                     help="ShardedStateMachine.round_window values (0: the whole step per round)")
     a = ap.parse_args()
     for world in a.worlds:
         for win in a.windows:
-            print(json.dumps(run(world, a.batch, a.batches, a.steps, a.seed + world, win)), flush=True)
+            for st in a.stops:
+                print(json.dumps(run(world, a.batch, a.batches, a.steps, a.seed + world, win, bool(st))), flush=True)
 
 
 if __name__ == "__main__":

@@ -175,9 +175,11 @@ class ShardedStateMachine:
         self.max_rounds = MAX_ROUNDS
         # events of the general step's round window (shard_vec.window_cut); 0: the whole step
         self.round_window = 4096
-        # the general step's rounds stop each shard at its own first waiting event
-        # (shard_vec.ShardStops); False: one stop for all, at the first hazard
-        self.shard_stops = True
+        # True: the general step's rounds stop each shard at its own first waiting event
+        # (shard_vec.ShardStops); False: one stop for all, at the first hazard.  Off by
+        # default: on the flag-heavy mix it saves 8-10 % of the rounds and costs more in
+        # its gather and solve (profiles/r05/general_rehearsal.txt)
+        self.shard_stops = False
         self.limit_ids: set[int] = set()  # ids of accounts created with a balance limit flag
         self.amount_bound = 0.0  # >= the sum of every transfer amount routed: bounds every balance
         self.timed = False       # accumulate per-phase wall times of the device step (with syncs)

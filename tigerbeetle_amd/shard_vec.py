@@ -550,35 +550,46 @@ class ShardStops:
         n = len(P)
         if not n:
             return np.zeros(0, bool)
-        _, cidx = np.unique(C, return_inverse=True)
-        nch = int(cidx.max()) + 1
+        wait = H | (P >= wcut)
+        if not wait.any():
+            return wait
+        # chains are runs of consecutive positions: their starts rise along P
+        cidx = np.zeros(n, np.int64)
+        np.cumsum(C[1:] != C[:-1], out=cidx[1:])
+        nch = int(cidx[-1]) + 1
+        # keys held by two or more of the round's records (a single record orders nothing)
         ke = np.concatenate([np.nonzero(kx)[0], np.nonzero(kp)[0]])
         kk = np.concatenate([kx[kx != 0], kp[kp != 0]])
-        o = np.lexsort((P[ke], kk))
-        ke, kk = ke[o], kk[o]
-        kfirst = np.ones(len(kk), dtype=bool)
-        kfirst[1:] = kk[1:] != kk[:-1]
-        kgid = np.cumsum(kfirst) - 1
-        nk = int(kgid[-1]) + 1 if len(kgid) else 0
+        _, kinv, kcnt = np.unique(kk, return_inverse=True, return_counts=True)
+        multi = kcnt[kinv] > 1
+        ke, kinv = ke[multi], kinv[multi]
         kP = P[ke]
+        nk = len(kcnt)
         one = EF >= 0
+        efi = np.where(one, EF, 0)
+        allm = EF == EF_ALL
         S = np.full(W, wcut, np.int64)
-        wait = H | (P >= wcut)
-        for _ in range(64):
-            smin = S.min()
-            w = wait | (one & (P >= S[np.where(one, EF, 0)])) | ((EF == EF_ALL) & (P >= smin))
+
+        def close(w):
             w = np.bincount(cidx, weights=w, minlength=nch)[cidx] > 0
-            if nk:
-                fd = np.full(nk, INF, np.int64)
+            if len(ke):
                 wk = w[ke]
-                np.minimum.at(fd, kgid[wk], kP[wk])
-                w[ke[kP > fd[kgid]]] = True
-                w = np.bincount(cidx, weights=w, minlength=nch)[cidx] > 0
+                if wk.any():
+                    fd = np.full(nk, INF, np.int64)
+                    np.minimum.at(fd, kinv[wk], kP[wk])
+                    later = kP > fd[kinv]
+                    if later.any():
+                        w[ke[later]] = True
+                        w = np.bincount(cidx, weights=w, minlength=nch)[cidx] > 0
+            return w
+
+        for _ in range(64):
+            w = close(wait | (one & (P >= S[efi])) | (allm & (P >= S.min())))
             S2 = S.copy()
-            np.minimum.at(S2, EF[w & one], C[w & one])
-            allw = w & (EF == EF_ALL)
-            if allw.any():
-                np.minimum(S2, C[allw].min(), out=S2)
+            m = w & one
+            np.minimum.at(S2, EF[m], C[m])
+            if (w & allm).any():
+                np.minimum(S2, C[w & allm].min(), out=S2)
             if np.array_equal(S2, S) and np.array_equal(w, wait):
                 return w
             S, wait = S2, w

@@ -646,6 +646,8 @@ typedef struct tbgpu_stats {
     double   phase_ms[8];
     uint64_t walks;           /* chunks, since init, whose fixed point reached its
                                  pass budget and was walked in execute's order    */
+    uint64_t index_rebuilds;  /* transfer-id index rebuilds since init: withdrawn
+                                 claims of non-rising ids left tombstones          */
 } tbgpu_stats;
 void tbgpu_last_stats(tbgpu_ctx* ctx, tbgpu_stats* out);
 /* Enable per-phase HIP-event timing (adds a few event records per call). */

@@ -209,6 +209,48 @@ def test_random_id_order():
     _parity(w)
 
 
+def test_withdrawn_id_claims_rebuild_the_index():
+    """Random ids (eager claims in fp_commit) in linked pairs whose second member fails
+    four times in five: each broken pair withdraws its first member's claim, leaving a
+    tombstone in the transfer-id index.  Past 1/16 of the slots the engine rebuilds the
+    index from the stored rows (xidx_tombs_check); replies, state and lookups still
+    match the oracle."""
+    from tigerbeetle_amd.types import TransferFlags
+    w = workload.config1(transfer_count=40 * 256, account_count=300, seed=31, batch=256, id_order="random")
+    rng = np.random.default_rng(31)
+    t = w.transfers
+    for i in range(0, len(t) - 1, 2):
+        t[i]["flags"] |= np.uint16(int(TransferFlags.linked))
+        if rng.random() < 0.8:
+            t[i + 1]["credit_account_id_lo"] ^= np.uint64(0x5A5A)  # no such account
+    orc = oracle.Oracle(len(w.accounts), len(w.transfers))
+    gpu = _engine(transfers_max=1 << 13, history_max=1 << 10, events_per_call_max=1 << 12)
+    try:
+        oa, ot = run_workload(orc, w)
+        ga, gt = run_workload(gpu, w, split=1)
+        assert_results_equal(gt, ot, "create_transfers")
+        assert_state_equal(gpu, orc)
+        assert gpu.stats().index_rebuilds > 0, gpu.stats().index_rebuilds
+        # every id through the rebuilt index: the stored ones found, the withdrawn not
+        q = t[["id_lo", "id_hi"]]
+        ids = [(int(h) << 64) | int(lo) for lo, h in zip(q["id_lo"], q["id_hi"])]
+        for c0 in range(0, len(ids), 4096):
+            got = gpu.lookup_transfers(ids[c0:c0 + 4096])
+            want = orc.lookup_transfers(ids[c0:c0 + 4096])
+            assert got.tobytes() == want.tobytes(), (c0, len(got), len(want))
+        # later calls still claim and find ids after the rebuild
+        w2 = workload.config1(transfer_count=4 * 256, account_count=300, seed=32, batch=256, id_order="random")
+        t2 = w2.transfers
+        t2[100] = t[0]  # an id seen before the rebuild (stored or withdrawn)
+        ts = int(orc.commit_timestamp()) + 10_000
+        for b in range(4):
+            ev = np.ascontiguousarray(t2[b * 256:(b + 1) * 256])
+            assert gpu.create_transfers(ts + b * 1000, ev).tobytes() == orc.create_transfers(ts + b * 1000, ev).tobytes()
+        assert_state_equal(gpu, orc)
+    finally:
+        gpu.close()
+
+
 def test_fast_path_with_failures():
     """Static failures, unknown accounts and re-submitted ids stay on the fast path:
     rows are re-placed at their ranks (fp_fix) and the replies are exact."""

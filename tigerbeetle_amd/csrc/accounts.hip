@@ -408,6 +408,14 @@ __global__ void import_transfers(Tables T, const Transfer* rows, u32 n, u64 row_
     }
 }
 
+// The transfer-id index rebuilt from the stored rows (xidx_tombs_check, engine.hip):
+// every row outside the sorted run, whose rows are found by search, not by the index.
+__global__ void k_rehash_xidx(Tables T, u64 n) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n || (r >= T.xrun[0] && r < T.xrun[1])) return;
+    xidx_insert(T, T.xrows[r].id, (u32)r);
+}
+
 // tbgpu_open: the account index from the dense rows (ac_apply's insert).
 __global__ void k_rebuild_aidx(Tables T, u64 n) {
     const u64 row = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -541,6 +549,10 @@ void launch_set_balances(const Tables& T, u128 id, Bal4 b, int* status, hipStrea
 }
 void launch_get_posted(const Tables& T, u128 id, int* status, hipStream_t stream) {
     k_get_posted<<<1, 1, 0, stream>>>(T, id, status);
+}
+
+void launch_rehash_xidx(const Tables& T, u64 n, hipStream_t s) {
+    if (n) k_rehash_xidx<<<(u32)((n + 255) / 256), 256, 0, s>>>(T, n);
 }
 
 void launch_import_transfers(const Tables& T, const Transfer* rows, u32 n, u64 row_base, hipStream_t stream) {

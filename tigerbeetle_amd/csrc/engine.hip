@@ -421,6 +421,7 @@ struct tbgpu_ctx {
     u64* h_res_dev = nullptr;
     u64 h_rc_cap = 0;
     u64 rows_hi = 0;           // upper bound of T.base[BASE_ROWS] (n_rows + events enqueued since)
+    u64 eager_events = 0;      // events of eager-claim attempts since the last tombstone check
     // tbgpu_prefetch_transfers: one batch staged in HBM ahead of its commit
     u8* pf_buf = nullptr;          // TBGPU_BATCH_MAX * 128 bytes
     const void* pf_src = nullptr;  // the caller's buffer it was copied from
@@ -700,7 +701,7 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     c->T.xrun = dalloc<u64>(8, &B);
     c->T.big = dalloc<u32>(4, &B);
     c->gate_status = dalloc<u32>(1, &B);
-    c->T.hcount = c->T.big + 1;        // [1] entries, [2] refused
+    c->T.hcount = c->T.big + 1;        // [1] entries, [2] refused, [3] transfer-id tombstones
     c->T.hash_limit = c->aidx_cap / 2;  // load <= 0.5
     c->T.base = dalloc<u64>(4, &B);
     c->T.shard_world = o.shard_world >= 2 ? o.shard_world : 0;
@@ -1062,6 +1063,7 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_crea
     F.tile = F.small ? FP_SMALL_TILE : fp_tile_events();
     static const bool no_eager = getenv("TBGPU_NO_EAGER") != nullptr;  // A/B timing: fp_dupcheck + inserts
     F.eager = (c->ids_nonmono && !F.dry && !no_eager) ? 1u : 0u;
+    if (F.eager) c->eager_events += n;
     F.gate = c->gate_arm ? c->gate_status : nullptr;
     const BlockInline bi = take_block(c);
     prof_mark(c, PH_PREP);
@@ -1687,12 +1689,36 @@ static bool spec_settle(tbgpu_ctx* c) {
     return false;
 }
 
+// Withdrawn eager claims leave tombstones in the transfer-id index (XIDX_TOMB), which no
+// insert reuses.  Stored rows keep the load at or below 0.5; tombstones could fill the
+// rest over a long life, and a probe needs an empty slot to end.  So every 1/8 of the
+// slots' worth of eager-claim events the count is read (one round trip), and past 1/16
+// of the slots the index is rebuilt from the stored rows outside the sorted run: the load
+// stays below 0.5 + 1/16 + 1/8.  Never with a prepared commit queued (its gate would
+// hold the stream): the entry points call it before they prepare one.
+static void xidx_tombs_check(tbgpu_ctx* c) {
+    const u64 slots = c->T.xidx_mask + 1;
+    if (c->eager_events <= slots / 8) return;
+    c->eager_events = 0;
+    hipStream_t s = c->stream;
+    u32 tombs = 0;
+    d2h(c, &tombs, c->T.hcount + 2, sizeof(u32), s);
+    if (tombs <= slots / 16) return;
+    u64 rows = 0;
+    d2h(c, &rows, c->T.base + BASE_ROWS, sizeof(u64), s);
+    HIP_CHECK(hipMemsetAsync(c->T.xidx, 0, slots * sizeof(u32), s));
+    HIP_CHECK(hipMemsetAsync(c->T.hcount + 2, 0, sizeof(u32), s));
+    launch_rehash_xidx(c->T, rows, s);
+    c->stats.index_rebuilds++;
+}
+
 static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t* timestamps, const uint32_t* counts,
                                   const Transfer* ev_src, bool src_device, tbgpu_create_transfers_result_t* results,
                                   bool dst_device, uint32_t* result_counts, const uint64_t* ev_ts_host = nullptr,
                                   const uint8_t* ctl_host = nullptr, bool routed_device = false) {
     HIP_CHECK(hipSetDevice(c->device));
     entry_flush(c->stream);
+    xidx_tombs_check(c);
     c->stats_lazy = false;
     static const bool no_call_events = getenv("TBGPU_NO_CALL_EVENTS") != nullptr;  // experiment
     const bool call_events = !no_call_events || c->prof;
@@ -2277,6 +2303,7 @@ extern "C" int tbgpu_prefetch_transfers(tbgpu_ctx* c, const tbgpu_transfer_t* ev
     CallGuard guard_(c, false);  // (releases an earlier prepared commit)
     c->pf_valid = false;
     if (count > TBGPU_BATCH_MAX) return -22;
+    xidx_tombs_check(c);
     // behind the previous commit on the ctx's stream (that commit has returned: its
     // kernels no longer read the slot); a DMA engine moves it while the caller goes on
     h2d(c, c->pf_buf, events, (u64)count * 128, c->stream);
@@ -2938,6 +2965,8 @@ extern "C" int tbgpu_open(tbgpu_ctx* c, const void* image, uint64_t size) {
         launch_import_transfers(c->T, c->T.xrows + off, k, off, s);  // rows in place: index + key range
     }
     h2d(c, c->T.commit_ts, &h.commit_ts, sizeof(u64), s);
+    HIP_CHECK(hipMemsetAsync(c->T.hcount + 2, 0, sizeof(u32), s));  // a fresh index: no tombstones
+    c->eager_events = 0;
     u32 refused = 0;
     d2h(c, &refused, c->T.hcount + 1, sizeof(u32), s);
     if (refused) tbgpu_fatal("open", "account index full after the capacity check", __FILE__, __LINE__);

@@ -855,7 +855,10 @@ __device__ void fp_chains_one(const Tables& T, const FastArgs& F, u32 i, u32& n_
     } else {
         n_bad++;
         if (!F.small) atomicAdd(&F.batch_counts[b], 1u);  // (small: fp_tail counts each batch's replies)
-        if (F.eager && F.gpos[i] != NONE32) T.xidx[F.gpos[i]] = XIDX_TOMB;  // its claim withdrawn
+        if (F.eager && F.gpos[i] != NONE32) {  // its claim withdrawn
+            T.xidx[F.gpos[i]] = XIDX_TOMB;
+            atomicAdd(&T.hcount[2], 1u);  // (xidx_tombs_check)
+        }
     }
 }
 

@@ -162,6 +162,7 @@ void launch_lookup_accounts(const Tables& T, const u128* ids, u32 n, Account* ou
 void launch_lookup_transfers(const Tables& T, const u128* ids, u32 n, Transfer* out, u8* found, hipStream_t stream);
 void launch_set_balances(const Tables& T, u128 id, Bal4 b, int* status, hipStream_t stream);
 void launch_import_transfers(const Tables& T, const Transfer* rows, u32 n, u64 row_base, hipStream_t stream);
+void launch_rehash_xidx(const Tables& T, u64 n, hipStream_t stream);
 void launch_get_posted(const Tables& T, u128 id, int* status, hipStream_t stream);
 void launch_rebuild_accounts(const Tables& T, u64 n, hipStream_t stream);
 // ledger shards: other shards' accounts into / out of the directory

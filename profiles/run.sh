@@ -12,7 +12,8 @@
 #   pmc:C[:ORDER]       kernel trace + PMC passes of config C's bench    OUT/pmcC[_ORDER]/ (+ traffic.json)
 #                       step (profiles/collect.sh), ids in ORDER
 #   hostpath            the drop-in call's kernel timeline               OUT/hostpath/
-#   fuzz:FIRST:COUNT[:big]  the on-demand fuzz sweep                     OUT/fuzz_FIRST.txt
+#   fuzz:FIRST:COUNT[:big|:random]  the on-demand fuzz sweep (full-size batches, or
+#                       random u128 ids)                                 OUT/fuzz_FIRST[MODE].txt
 #   passes:C            pass trace of config C (TBGPU_TRACE_PASSES=1)    OUT/passes_configC.json
 #   ab:V1,V2[:A,B..]    timing variants (profiles/variants.py; `base` is the product library,
 #                       others build/var_NAME built beforehand), REPS alternations
@@ -65,10 +66,11 @@ step() {
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/hostpath/kt" -o kt --output-format csv -- \
         python3 -u "$ROOT/profiles/hostpath_trace.py" > "$ROOT/$OUT/hostpath/kt.log" 2>&1) ;;
     fuzz)
-      local first=${rest%%:*} r2=${rest#*:} count big=""
-      count=${r2%%:*}; [ "$r2" != "$count" ] && big=1
-      TB_FUZZ_BIG=$big TB_FUZZ_STRESS=$first:$count timeout -k 10 900 python3 -u -m pytest -x -q -s --timeout 880 \
-        --timeout-method thread tests/test_gpu_fuzz.py -k stress > "$OUT/fuzz_$first.txt" 2>&1 ;;
+      local first=${rest%%:*} r2=${rest#*:} count mode="" big="" rnd=""
+      count=${r2%%:*}; [ "$r2" != "$count" ] && mode=${r2#*:}
+      case $mode in big) big=1;; random) rnd=1;; esac
+      TB_FUZZ_BIG=$big TB_FUZZ_RANDOM=$rnd TB_FUZZ_STRESS=$first:$count timeout -k 10 900 python3 -u -m pytest -x -q -s \
+        --timeout 880 --timeout-method thread tests/test_gpu_fuzz.py -k stress > "$OUT/fuzz_$first$mode.txt" 2>&1 ;;
     passes)
       TBGPU_TRACE_PASSES=1 timeout -k 10 300 python3 -u bench.py --config "$rest" --steps 1 --warmup 0 $Q \
         > "$OUT/passes_config$rest.json" 2> "$OUT/passes_config$rest.err" ;;

@@ -32,7 +32,7 @@ def _mutate(w, rng, rate):
         k = int(rng.integers(0, 11))
         j = int(rng.integers(0, i)) if i else 0
         if k == 0:
-            t[i]["id_lo"] = t[j]["id_lo"]                       # repeated id
+            t[i]["id_lo"], t[i]["id_hi"] = t[j]["id_lo"], t[j]["id_hi"]  # repeated id
         elif k == 1:
             t[i]["debit_account_id_lo"] = 10_000 + i            # unknown account
         elif k == 2:
@@ -48,7 +48,7 @@ def _mutate(w, rng, rate):
         elif k in (6, 7) and pend:
             p = pend[int(rng.integers(0, len(pend)))]
             t[i]["flags"] = np.uint16(int(TF.post_pending_transfer if k == 6 else TF.void_pending_transfer))
-            t[i]["pending_id_lo"] = t[p]["id_lo"]
+            t[i]["pending_id_lo"], t[i]["pending_id_hi"] = t[p]["id_lo"], t[p]["id_hi"]
             t[i]["amount_lo"] = 0 if rng.random() < 0.5 else max(1, int(t[p]["amount_lo"]) // 2)
             t[i]["ledger"] = 0
             t[i]["code"] = 0
@@ -56,10 +56,13 @@ def _mutate(w, rng, rate):
             t[i]["flags"] |= np.uint16(int(TF.balancing_debit if rng.random() < 0.5 else TF.balancing_credit))
         elif k == 9:
             t[i]["timeout"] = 1                                 # timeout without pending
+        elif i:
+            t[i]["id_lo"], t[i]["id_hi"] = t[i - 1]["id_lo"], t[i - 1]["id_hi"]  # adjacent repeat
         else:
-            t[i]["id_lo"] = t[i - 1]["id_lo"] if i else 0       # adjacent repeat / id zero
+            t[i]["id_lo"], t[i]["id_hi"] = 0, 0                 # id zero
     if rng.random() < 0.5:
-        t[-1]["id_lo"] = t[int(rng.integers(0, n - 1))]["id_lo"]  # the call's last event repeats an id
+        j = int(rng.integers(0, n - 1))
+        t[-1]["id_lo"], t[-1]["id_hi"] = t[j]["id_lo"], t[j]["id_hi"]  # the call's last event repeats an id
     w.transfers = t
     return w
 
@@ -99,6 +102,22 @@ def test_fuzz_mutations(seed):
         _check(w, force_general=True, walk_early=True)
 
 
+@pytest.mark.parametrize("seed", range(48))
+def test_fuzz_random_ids(seed):
+    """The same mutations on random u128 ids (benchmark --id-order=random), committed batch
+    by batch: from the second call on the fast path claims ids eagerly in fp_commit
+    (repeats inside a call, withdrawn claims of broken chains, fallbacks that clear them)."""
+    rng = np.random.default_rng(5000 + seed)
+    nb = int(rng.integers(3, 7))
+    batch = int(rng.integers(50, 700))
+    w = workload.config1(transfer_count=nb * batch, account_count=int(rng.integers(3, 40)), seed=seed,
+                         batch=batch, id_order="random")
+    w = _mutate(w, rng, [0.0005, 0.005, 0.03, 0.15][seed % 4])
+    _check(w, split=1)
+    if seed % 4 == 0:
+        _check(w)
+
+
 STRESS = os.environ.get("TB_FUZZ_STRESS")  # "first:count": a wider sweep on demand (profiles/r04/fuzz_stress.sh)
 
 
@@ -108,16 +127,17 @@ def test_fuzz_stress_sweep():
     (the passes, the side sort and the headroom scan this sweep is for)."""
     first, count = (int(x) for x in STRESS.split(":"))
     big = os.environ.get("TB_FUZZ_BIG") == "1"  # full-size batches, more accounts
+    order = "random" if os.environ.get("TB_FUZZ_RANDOM") == "1" else "sequential"  # random u128 ids
     for seed in range(first, first + count):
         rng = np.random.default_rng(1000 + seed)
         nb = int(rng.integers(2, 6))
         batch = int(rng.integers(500, 8191)) if big else int(rng.integers(50, 700))
         w = workload.config1(transfer_count=nb * batch, account_count=int(rng.integers(3, 300 if big else 40)),
-                             seed=seed, batch=batch)
+                             seed=seed, batch=batch, id_order=order)
         w = _mutate(w, rng, [0.0005, 0.005, 0.03, 0.15][seed % 4])
         _check(w)
         _check(w, force_general=True)
-        if seed % 5 == 0:
+        if seed % 5 == 0 or order == "random":
             _check(w, split=1)
         if seed % 7 == 0:
             _check(w, force_general=True, walk_early=True)

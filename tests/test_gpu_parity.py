@@ -251,6 +251,45 @@ def test_withdrawn_id_claims_rebuild_the_index():
         gpu.close()
 
 
+def test_eager_claim_of_a_broken_chain_is_not_an_existing_id():
+    """Random ids, eager claims (the ctx saw non-rising ids in its first call): the second
+    call, 1M events in one streamed call (≈2000 tiles of fp_commit, more than the chip
+    holds at once), starts with an event linked to a partner that fails, so its claim is
+    withdrawn after fp_commit; the call's last events repeat its id.  If their tiles
+    classify after the first tile claimed the id and stored its optimistic row, a probe
+    that compared this call's claimed rows would answer `exists` (fp_classify probes only
+    rows committed before the call, xidx_committed); the sequential answer is `ok` for
+    the first repeat (the first event failed) and `exists_with_different_amount` for the
+    second."""
+    from tigerbeetle_amd.types import TransferFlags
+    nb = 1 + 122
+    w = workload.config1(transfer_count=nb * 8190, account_count=500, seed=41, id_order="random")
+    t = w.transfers
+    a = 8190  # the second call's first event
+    t[a]["flags"] |= np.uint16(int(TransferFlags.linked))
+    t[a + 1]["credit_account_id_lo"] ^= np.uint64(0x77)  # no such account: the chain breaks
+    last = len(t) - 1
+    for b in (last - 2, last):
+        t[b]["id_lo"], t[b]["id_hi"] = t[a]["id_lo"], t[a]["id_hi"]
+    t[last]["amount_lo"] += np.uint64(1)
+    orc = oracle.Oracle(len(w.accounts), len(w.transfers))
+    gpu = _engine(transfers_max=1 << 21, events_per_call_max=1 << 20)  # the second call is one chunk
+    try:
+        ats, tts = w.timestamps()
+        for be in (orc, gpu):
+            be.create_accounts_batches(ats, w.account_counts, w.accounts)
+        got, want = [], []
+        for b0, b1 in ((0, 1), (1, nb)):
+            e0, e1 = b0 * 8190, b1 * 8190
+            for be, out in ((gpu, got), (orc, want)):
+                res, rc, _ = be.create_transfers_batches(tts[b0:b1], w.transfer_counts[b0:b1], t[e0:e1])
+                out.append(res[:int(rc.sum())].copy())
+        assert_results_equal(got, want, "create_transfers")
+        assert_state_equal(gpu, orc)
+    finally:
+        gpu.close()
+
+
 def test_fast_path_with_failures():
     """Static failures, unknown accounts and re-submitted ids stay on the fast path:
     rows are re-placed at their ranks (fp_fix) and the replies are exact."""

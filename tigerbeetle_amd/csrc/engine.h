@@ -184,7 +184,8 @@ constexpr u32 SIDE_CANDS = 3;
 struct Sides {
     u32 m;            // sides of the chunk
     u32* soff;        // [n + 1] first side (unsorted id) of each event
-    u32* sev;         // [m] unsorted: event | side << 31 (0 debit, 1 credit) | SQ_SENS (bit 30)
+    u32* sev;         // [m] unsorted: event | side << 31 (0 debit, 1 credit) | SQ_SENS | SQ_FIRST
+    u32* scs;         // [m] unsorted: the side's sq_cs word (written by tr_side_build)
     u32* scand;       // [m] unsorted: the candidate pending of a post/void pair (pref encoding), else NONE32
     u32* spos;        // [m] sorted position of unsorted side s
     const u32* skey_s;  // [m] sorted keys (account row; >= invalid: no account)
@@ -203,8 +204,9 @@ constexpr u32 SQ_STANDALONE = 1u << 31, SQ_DOOM = 1u << 30, SQ_CS = (1u << 30) -
 // headroom pass -- a debit side of an account with debits_must_not_exceed_credits or of
 // a balancing_debit transfer, a credit side likewise (eval_balances_narrow reads nothing
 // else of a balance; post/void and static failures read none).  The headroom scan marks
-// an event due only through such a side.  Events fit 29 bits (events_per_call_max).
-constexpr u32 SQ_SENS = 1u << 30, SQ_EV = (1u << 30) - 1;
+// an event due only through such a side.  Bit 29: the side belongs to its event's first
+// pair (its sorted position goes to epos).  Events fit 29 bits (events_per_call_max).
+constexpr u32 SQ_SENS = 1u << 30, SQ_FIRST = 1u << 29, SQ_EV = (1u << 29) - 1;
 
 struct SideScanArgs {
     const u32* skey;  // sorted side keys (account row; >= invalid for inert)

@@ -283,7 +283,7 @@ struct tbgpu_ctx {
     EvalState st[2];
     u64 scap = 0, side_m = 0;  // side capacity, sides of the last fixed point
     u32 *skey, *sval, *skey_s, *sval_s, *spos;
-    u32 *soff, *sev, *scand, *sq_ev, *sq_cs;
+    u32 *soff, *sev, *scs, *scand, *sq_ev, *sq_cs;
     EvCore* core = nullptr;
     u32* tstart = nullptr;
     uint2* epos = nullptr;
@@ -539,6 +539,7 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     c->tstart = dalloc<u32>(m / side_scan_fused_tile() + 2, &B);
     c->epos = dalloc<uint2>(nmax + 1, &B);
     c->sev = dalloc<u32>(m, &B);
+    c->scs = dalloc<u32>(m, &B);
     c->scand = dalloc<u32>(m, &B);
     c->sq_ev = dalloc<u32>(m, &B);
     c->sq_cs = dalloc<u32>(m, &B);
@@ -775,7 +776,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
                     c->b_start, c->ts, c->cs, c->ce, c->sres, c->dslot, c->cslot, c->pre_e, c->pre_p,
                     c->pp_dslot, c->pp_cslot, c->gslot, c->pslot, c->prev_id, c->pend_last, c->pend_first, c->prev_pend,
                     c->gclaim, c->gcnt_id, c->gcnt_pd, c->gmem, c->gbeg, c->gend, c->gfill, c->pfill, c->pbeg, c->skey, c->sval, c->skey_s,
-                    c->soff, c->core, c->tstart, c->epos, c->sev, c->scand, c->sq_ev, c->sq_cs, c->sq_ok, c->sq_dpend, c->sq_dpost, c->gkey_s,
+                    c->soff, c->core, c->tstart, c->epos, c->sev, c->scs, c->scand, c->sq_ev, c->sq_cs, c->sq_ok, c->sq_dpend, c->sq_dpost, c->gkey_s,
                     c->gsorted,
                     c->sval_s, c->spos, c->bb, c->bh, c->ss.keys_tmp, c->ss.vals_tmp, c->ss.hist, c->side_tiles,
                     c->sc.tile_sums, c->fres, c->mask, c->ranks, c->res_buf, c->counts, c->counters, c->status,
@@ -1000,7 +1001,7 @@ static TrArgs make_tr_args(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb) {
     C.gfill = c->gfill; C.pfill = c->pfill; C.pbeg = c->pbeg;
     C.glist = c->gkey_s;  // scratch (free before the sides are built)
     C.plist = c->skey;
-    C.sd.soff = c->soff; C.sd.sev = c->sev; C.sd.scand = c->scand; C.sd.spos = c->spos; C.sd.skey_s = c->skey_s;
+    C.sd.soff = c->soff; C.sd.sev = c->sev; C.sd.scs = c->scs; C.sd.scand = c->scand; C.sd.spos = c->spos; C.sd.skey_s = c->skey_s;
     C.sd.sq_ev = c->sq_ev; C.sd.sq_cs = c->sq_cs; C.sd.sq_ok = c->sq_ok; C.sd.sq_dpend = c->sq_dpend;
     C.sd.sq_dpost = c->sq_dpost;
     C.sd.tstart = c->tstart;

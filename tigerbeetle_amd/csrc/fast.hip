@@ -107,13 +107,34 @@ __device__ __forceinline__ u64 aidx_probe_from(const Tables& T, u64 h, u128 id) 
     }
 }
 
-__device__ __forceinline__ u32 xidx_probe_from(const Tables& T, u64 h, u128 id) {
+// The rows a probe may compare: committed before this call (row < row_base).  A slot
+// that names a row of this call is an eager claim (FastArgs::eager), whose row may or
+// may not be stored yet: the claim itself decides a repeat (fp_claim_is_dup), so a probe
+// of the pre-call state walks past it like a tombstone.
+__device__ __forceinline__ bool xidx_committed(const Tables& T, u32 r1, u64 row_base, u128 id) {
+    return r1 != XIDX_TOMB && r1 - 1 < row_base && T.xrows[r1 - 1].id == id;
+}
+
+__device__ __forceinline__ u32 xidx_probe_from(const Tables& T, u64 h, u128 id, u64 row_base) {
     for (;;) {
         h = (h + XIDX_STEP) & T.xidx_mask;
         const u32 r1 = T.xidx[h];
         if (r1 == 0) return NONE32;
-        if (r1 != XIDX_TOMB && T.xrows[r1 - 1].id == id) return r1 - 1;
+        if (xidx_committed(T, r1, row_base, id)) return r1 - 1;
     }
+}
+
+// xidx_probe (engine.h) over the pre-call state only (see xidx_committed).
+__device__ __forceinline__ u32 xidx_probe_pre(const Tables& T, u128 id, u64 row_base) {
+    if (xidx_maybe_present(T, id)) {
+        const u64 h = xidx_hash(id) & T.xidx_mask;
+        const u32 r1 = T.xidx[h];
+        if (r1 != 0) {
+            const u32 r = xidx_committed(T, r1, row_base, id) ? r1 - 1 : xidx_probe_from(T, h, id, row_base);
+            if (r != NONE32) return r;
+        }
+    }
+    return xrun_maybe(T, id) ? xrun_find(T, id) : NONE32;
 }
 
 // Eager claim of accepted event i's id (FastArgs::eager) at its optimistic row: the
@@ -139,7 +160,7 @@ __device__ __forceinline__ bool fp_claim_is_dup(const Tables& T, const FastArgs&
 }
 
 __device__ __forceinline__ u8 fp_classify_guarded(const Tables& T, const FastArgs& F, const Transfer& t, u32 i,
-                                                  u64 ts, u32* dslot_out, u32* cslot_out);
+                                                  u64 ts, u64 row_base, u32* dslot_out, u32* cslot_out);
 
 // Result of one event against the pre-call state, or FRES_SLOW.  The debit and
 // credit account rows, the transfer-id slot and the duplicate claim are all
@@ -147,10 +168,10 @@ __device__ __forceinline__ u8 fp_classify_guarded(const Tables& T, const FastArg
 // precedence of the resulting checks is ordered), so one event costs about one
 // memory round trip instead of four.
 __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, const Transfer& t, u32 i, u64 ts,
-                                          u32* dslot_out, u32* cslot_out) {
+                                          u64 row_base, u32* dslot_out, u32* cslot_out) {
     const u16 f = t.flags;
     if (f & (TF_BDR | TF_BCR | TF_POST | TF_VOID) || *T.big)
-        return fp_classify_guarded(T, F, t, i, ts, dslot_out, cslot_out);
+        return fp_classify_guarded(T, F, t, i, ts, row_base, dslot_out, cslot_out);
     // speculative first-slot reads (hash tables at load <= 0.5: usually the hit).
     // The 32-byte account index entries carry ledger and flags, so the rows
     // themselves are only touched by the balance atomics.
@@ -199,7 +220,7 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
     if (!ledger_owned(T, t.ledger)) return FRES_SLOW;  // another shard's ledger (the general path refuses it)
     if ((A.flags | B.flags) & (AF_DNEC | AF_CNED | AF_HISTORY)) return FRES_SLOW;  // limits / history
     if (x_r1 != 0) {
-        const u32 pre = (x_r1 != XIDX_TOMB && T.xrows[x_r1 - 1].id == t.id) ? x_r1 - 1 : xidx_probe_from(T, hx, t.id);
+        const u32 pre = xidx_committed(T, x_r1, row_base, t.id) ? x_r1 - 1 : xidx_probe_from(T, hx, t.id, row_base);
         if (pre != NONE32) return fp_exists(t, T.xrows[pre]);
     }
     if (xrun_maybe(T, t.id)) {  // the sorted run (an id replayed from an earlier call)
@@ -219,7 +240,7 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
 // The static checks that precede what makes an event ineligible (their results
 // are exact); otherwise FRES_SLOW.
 __device__ __forceinline__ u8 fp_classify_guarded(const Tables& T, const FastArgs& F, const Transfer& t, u32 i,
-                                                       u64 ts, u32* dslot_out, u32* cslot_out) {
+                                                       u64 ts, u64 row_base, u32* dslot_out, u32* cslot_out) {
     const u16 f = t.flags;
     if (t.timestamp != 0) return TBGPU_CREATE_TRANSFER_TIMESTAMP_MUST_BE_ZERO;
     if (f & 0xFFC0u) return TBGPU_CREATE_TRANSFER_RESERVED_FLAG;
@@ -257,7 +278,7 @@ __device__ __forceinline__ u8 fp_classify_guarded(const Tables& T, const FastArg
     if ((dfl | cfl) & (AF_DNEC | AF_CNED | AF_HISTORY)) return FRES_SLOW;  // limits / history
     const Account& dr = T.acc[ds];
     const Account& cr = T.acc[cs];
-    const u32 pre = xidx_probe(T, t.id);
+    const u32 pre = xidx_probe_pre(T, t.id, row_base);
     if (pre != NONE32) return fp_exists(t, T.xrows[pre]);
     // an id repeated within the call is caught by fp_dupcheck, as on the unguarded path
     // overflow impossible: amount < 2^64 and the touched balances' high words < 2^62
@@ -502,7 +523,7 @@ __device__ __forceinline__ void fp_commit_body(const Tables& T, FastArgs F, cons
         u32 ds = NONE32, cs = NONE32;
         if (lk && i - bs == nbatch - 1) r = TBGPU_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN;  // checked first (:1024)
         else if (myctl & TBGPU_CTL_SKIP) r = TBGPU_CREATE_TRANSFER_LINKED_EVENT_FAILED;    // broken on another shard
-        else r = fp_classify(T, F, t, i, ts, &ds, &cs);
+        else r = fp_classify(T, F, t, i, ts, row_base, &ds, &cs);
         own_ok = r == TBGPU_CREATE_TRANSFER_OK;
         if (F.eager) {
             u32 slot = NONE32;

@@ -1168,6 +1168,7 @@ __global__ void tr_side_build(TrArgs C, EvalState S, u32 kmax, const uint4* pair
     const u8 af = ev ? C.core[i].aflags : 0;
     const u32 ds = ev ? C.dslot[i] : NONE32, cs = ev ? C.cslot[i] : NONE32;
     const u32 pd = ev ? C.pp_dslot[i] : NONE32, pc = ev ? C.pp_cslot[i] : NONE32;
+    const u32 ecs = ev ? C.cs[i] : 0u, ece = ev ? C.ce[i] : 0u;
     const bool pv = sr == SRES_DYN && (fl & (TF_POST | TF_VOID));
     u32 cand[SIDE_CANDS], cd[SIDE_CANDS], cc[SIDE_CANDS];
     u32 k = 1;
@@ -1194,6 +1195,9 @@ __global__ void tr_side_build(TrArgs C, EvalState S, u32 kmax, const uint4* pair
     const u32 s0 = 2 * (pr.x + pr.y + pr.z);
     C.sd.soff[i] = s0;
     if (i == C.n) return;
+    // the sorted chain word of every side of the event (tr_side_pos copies it in order)
+    const bool doom = C.ctl && (C.ctl[ece] & TBGPU_CTL_DOOM);
+    const u32 cw = ecs | (ecs == ece ? SQ_STANDALONE : 0u) | (doom ? SQ_DOOM : 0u);
     const u32 slots = (2 * (pr1.x + pr1.y + pr1.z) - s0) / 2;  // tr_side_count's bound
     if (k > slots) {  // (the bound holds by construction: a broken one is a device error)
         atomicOr(&C.counters[CNT_FLAGS], (u32)FL_ERROR);
@@ -1217,8 +1221,10 @@ __global__ void tr_side_build(TrArgs C, EvalState S, u32 kmax, const uint4* pair
         const bool reg = !pv && sr == SRES_DYN && d != invalid;
         const bool sd = reg && ((af & AF_DNEC) || (fl & TF_BDR));
         const bool sc = reg && (((af >> 4) & AF_CNED) || (fl & TF_BCR));
-        C.sd.sev[s] = i | (sd ? SQ_SENS : 0u);
-        C.sd.sev[s + 1] = i | (1u << 31) | (sc ? SQ_SENS : 0u);
+        const u32 first = j == 0 ? SQ_FIRST : 0u;
+        C.sd.sev[s] = i | first | (sd ? SQ_SENS : 0u);
+        C.sd.sev[s + 1] = i | first | (1u << 31) | (sc ? SQ_SENS : 0u);
+        C.sd.scs[s] = C.sd.scs[s + 1] = cw;
         C.sd.scand[s] = C.sd.scand[s + 1] = (pv && j < k) ? cand[j] : NONE32;
     }
 }
@@ -1236,16 +1242,15 @@ __global__ void tr_side_pos(TrArgs C, const u32* sval_s, u64 m) {
     start = wave_min(start);
     if (start != NONE32 && q == start) atomicMin(&C.sd.tstart[q / C.sd.tile], start);
     if (q >= m) return;
-    // loads before stores (they may alias for the compiler: see tr_side_build)
+    // loads before stores (they may alias for the compiler: see tr_side_build); the
+    // side's words were written by tr_side_build in unsorted order (two gathers here
+    // instead of the event's offset, chain bounds and control byte)
     const u32 s = sval_s[q];
-    const u32 ev = C.sd.sev[s];
-    const u32 i = ev & SQ_EV;
-    const u32 so = C.sd.soff[i], cs = C.cs[i], ce = C.ce[i];
-    const bool doom = C.ctl && (C.ctl[ce] & TBGPU_CTL_DOOM);
+    const u32 ev = C.sd.sev[s], cw = C.sd.scs[s];
     C.sd.spos[s] = (u32)q;
     C.sd.sq_ev[q] = ev;
-    if (s - so < 2) ((u32*)&C.sd.epos[i])[ev >> 31] = (u32)q;
-    C.sd.sq_cs[q] = cs | (cs == ce ? SQ_STANDALONE : 0u) | (doom ? SQ_DOOM : 0u);
+    if (ev & SQ_FIRST) ((u32*)&C.sd.epos[ev & SQ_EV])[ev >> 31] = (u32)q;
+    C.sd.sq_cs[q] = cw;
 }
 
 // Write event i's side records (sorted order) for its outcome: the debit and credit

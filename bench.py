@@ -151,6 +151,7 @@ def query_phase(eng, w, acc_n, torch, dev, count=100, batch=1024):
 
 
 HOST_WARMUP = 8  # untimed drop-in calls before each timed set (first-call allocations, page faults)
+HOST_PY = 40     # of each drop-in set, the calls made through the Python wrapper (the rest from C)
 
 
 def host_path(eng, w, tts, counts, b0, nbs, torch):
@@ -178,34 +179,43 @@ def host_path(eng, w, tts, counts, b0, nbs, torch):
 
     def pct(x):
         x = np.asarray(x)
+        if not len(x):
+            return None
         return {"p50": round(float(np.percentile(x, 50)), 1), "p99": round(float(np.percentile(x, 99)), 1),
                 "max": round(float(x.max()), 1)}
 
-    lat, dev_us, ev_single = [], [], 0
-    for k in range(single):
+    # Timed from C (tbgpu_bench_host_calls: the call as the Zig shim makes it, no Python
+    # around it) on the first HOST_C of each set, then a sample through the Python
+    # wrapper (engine.create_transfers) for comparison
+    py_n = lambda k: HOST_PY if k >= HOST_PY + 2 * HOST_WARMUP + 8 else 0
+    c_single, c_pre = single - py_n(single), prefetched - py_n(prefetched)
+
+    def c_calls(mode, g0, k):
+        ev = view[int(offs[g0]) - o0:int(offs[g0 + k]) - o0]
+        com, pre = eng.bench_host_calls(mode, tts[g0:g0 + k], counts[g0:g0 + k], ev)
+        return com[HOST_WARMUP:], pre[HOST_WARMUP:], int(offs[g0 + k] - offs[g0 + HOST_WARMUP])
+
+    lat, _, ev_single = c_calls(0, b0, c_single)
+    py_lat, dev_us = [], []
+    for k in range(c_single, single):
         ev = batch(b0 + k)
         t0 = time.perf_counter()
         eng.create_transfers(int(tts[b0 + k]), ev)
-        if k >= HOST_WARMUP:
-            lat.append((time.perf_counter() - t0) * 1e6)
+        if k >= c_single + HOST_WARMUP:
+            py_lat.append((time.perf_counter() - t0) * 1e6)
             dev_us.append(eng.stats().device_ms * 1e3)  # HIP events around the call on the engine stream
-            ev_single += len(ev)
-    lat = np.array(lat)
     p0 = b0 + single
-    pre_us, com_us, both_us, ev_pre = [], [], [], 0
-    for k in range(prefetched):
+    com_us, pre_us, ev_pre = c_calls(1, p0, c_pre)
+    both_us = com_us + pre_us
+    py_com = []
+    for k in range(c_pre, prefetched):
         ev = batch(p0 + k)
-        t0 = time.perf_counter()
         eng.prefetch_transfers(ev)
         eng.prefetch_wait()
         t1 = time.perf_counter()
         eng.create_transfers(int(tts[p0 + k]), ev)
-        t2 = time.perf_counter()
-        if k >= HOST_WARMUP:
-            pre_us.append((t1 - t0) * 1e6)
-            com_us.append((t2 - t1) * 1e6)
-            both_us.append((t2 - t0) * 1e6)
-            ev_pre += len(ev)
+        if k >= c_pre + HOST_WARMUP:
+            py_com.append((time.perf_counter() - t1) * 1e6)
     s0 = p0 + prefetched
     ev = view[int(offs[s0]) - o0:]
     t0 = time.perf_counter()
@@ -216,8 +226,10 @@ def host_path(eng, w, tts, counts, b0, nbs, torch):
                       "latency_us": pct(lat),
                       "slowest_calls": [int(x) + HOST_WARMUP for x in np.argsort(lat)[::-1][:3]],
                       "device_us": pct(dev_us),
+                      "python_wrapper_latency_us": pct(py_lat),
                       "transfers_per_s": round(ev_single / (lat.sum() * 1e-6), 1),
-                      "entry": "tbgpu_create_transfers (one batch per call, pinned host buffers)"},
+                      "entry": "tbgpu_create_transfers (one batch per call, pinned host buffers), timed from C "
+                               "(tbgpu_bench_host_calls); python_wrapper_*: the same call through engine.py"},
            "streamed": {"batches": streamed, "transfers": len(ev), "seconds": round(el, 6),
                         "transfers_per_s": round(len(ev) / el, 1),
                         "entry": "tbgpu_create_transfers_batches (host buffers, H2D inside the call)"}}
@@ -225,6 +237,7 @@ def host_path(eng, w, tts, counts, b0, nbs, torch):
         out["prefetched"] = {"calls": len(com_us), "warmup_calls": HOST_WARMUP,
                              "commit_latency_us": pct(com_us), "prefetch_latency_us": pct(pre_us),
                              "prefetch_plus_commit_us": pct(both_us),
+                             "python_wrapper_commit_latency_us": pct(py_com),
                              "commit_transfers_per_s": round(ev_pre / (np.sum(com_us) * 1e-6), 1),
                              "entry": "tbgpu_prefetch_transfers + tbgpu_prefetch_wait, then tbgpu_create_transfers "
                                       "(the batch staged in HBM before the commit)"}

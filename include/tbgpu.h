@@ -585,6 +585,16 @@ int tbgpu_bench_generate_transfers(int device, uint64_t first_id, uint64_t count
                                    uint32_t ledger0, uint32_t ledgers, uint32_t ledger_stride,
                                    uint32_t accounts_per_ledger, void* out_device);
 
+/* The drop-in call timed from C, as the Zig shim issues it (bench.py host_path):
+ * `calls` consecutive batches (batch k: counts[k] events at the running offset of
+ * `events`, committed at timestamps[k]); mode 0 one tbgpu_create_transfers per batch,
+ * mode 1 tbgpu_prefetch_transfers + tbgpu_prefetch_wait and then the commit of the same
+ * batch.  Wall time per commit (and per prefetch, when prefetch_us is not NULL) in
+ * microseconds.  Replies go to `results` (room for the largest batch).  0, or -22. */
+int tbgpu_bench_host_calls(tbgpu_ctx* ctx, int mode, uint32_t calls, const tbgpu_transfer_t* events,
+                           const uint32_t* counts, const uint64_t* timestamps,
+                           tbgpu_create_transfers_result_t* results, double* commit_us, double* prefetch_us);
+
 /* Test harness `setup` action (src/state_machine.zig:1892-1908): overwrite an
  * existing account's four balances.  Returns 0, or -1 if the account is missing. */
 int tbgpu_test_set_balances(tbgpu_ctx* ctx, tbgpu_uint128_t id,

@@ -3057,3 +3057,31 @@ extern "C" int tbgpu_last_error(tbgpu_ctx* c, char* buf, uint32_t len) {
     snprintf(buf, len, "%s", c ? c->err : "no ctx");
     return (int)strlen(buf);
 }
+
+// The drop-in call timed from C (bench.py host_path): what the Zig shim's call costs,
+// without a host-language wrapper around it.  Batch k is counts[k] events at the running
+// offset of `events`, committed at timestamps[k]; mode 0: tbgpu_create_transfers per
+// batch; mode 1: tbgpu_prefetch_transfers + tbgpu_prefetch_wait, then
+// tbgpu_create_transfers of the same batch, as the replica runs them.
+extern "C" int tbgpu_bench_host_calls(tbgpu_ctx* c, int mode, uint32_t calls, const tbgpu_transfer_t* events,
+                                      const uint32_t* counts, const uint64_t* timestamps,
+                                      tbgpu_create_transfers_result_t* results, double* commit_us,
+                                      double* prefetch_us) {
+    using clk = std::chrono::steady_clock;
+    u64 off = 0;
+    for (uint32_t k = 0; k < calls; k++) {
+        const tbgpu_transfer_t* ev = events + off;
+        const auto t0 = clk::now();
+        if (mode == 1) {
+            if (tbgpu_prefetch_transfers(c, ev, counts[k]) != 0) return -22;
+            tbgpu_prefetch_wait(c);
+        }
+        const auto t1 = clk::now();
+        tbgpu_create_transfers(c, timestamps[k], ev, counts[k], results);
+        const auto t2 = clk::now();
+        commit_us[k] = std::chrono::duration<double, std::micro>(t2 - t1).count();
+        if (prefetch_us) prefetch_us[k] = std::chrono::duration<double, std::micro>(t1 - t0).count();
+        off += counts[k];
+    }
+    return 0;
+}

@@ -94,6 +94,8 @@ def lib():
     L.tbgpu_prefetch_transfers.argtypes = [vp, vp, u32]
     L.tbgpu_prefetch_wait.restype = ctypes.c_int
     L.tbgpu_prefetch_wait.argtypes = [vp]
+    L.tbgpu_bench_host_calls.restype = ctypes.c_int
+    L.tbgpu_bench_host_calls.argtypes = [vp, ctypes.c_int, u32, vp, vp, vp, vp, vp, vp]
     L.tbgpu_test_set_balances.restype = ctypes.c_int
     L.tbgpu_test_set_balances.argtypes = [vp, U128, U128, U128, U128, U128]
     for name in ("tbgpu_account_count", "tbgpu_transfer_count", "tbgpu_history_count", "tbgpu_commit_timestamp"):
@@ -244,6 +246,23 @@ class Engine:
             raise ValueError("prefetch_transfers needs the contiguous event array create_transfers will get")
         if self._L.tbgpu_prefetch_transfers(self._h, _ptr(events), len(events)) != 0:
             raise ValueError("prefetch_transfers: more events than a batch")
+
+    def bench_host_calls(self, mode: int, timestamps, counts, events):
+        """tbgpu_bench_host_calls: the drop-in call timed from C (mode 0 one
+        tbgpu_create_transfers per batch, 1 prefetch + wait + commit).  Returns the per-call
+        commit and prefetch wall times in microseconds."""
+        ts = np.ascontiguousarray(timestamps, dtype=np.uint64)
+        cs = np.ascontiguousarray(counts, dtype=np.uint32)
+        if events.dtype != TRANSFER_DTYPE or not events.flags["C_CONTIGUOUS"]:
+            raise ValueError("bench_host_calls needs contiguous TRANSFER_DTYPE events")
+        out = np.zeros(max(int(cs.max()) if len(cs) else 1, 1), dtype=RESULT_DTYPE)
+        com = np.zeros(len(cs), dtype=np.float64)
+        pre = np.zeros(len(cs), dtype=np.float64)
+        rc = self._L.tbgpu_bench_host_calls(self._h, int(mode), len(cs), _ptr(events), _ptr(cs), _ptr(ts), _ptr(out),
+                                            _ptr(com), _ptr(pre))
+        if rc != 0:
+            raise ValueError(f"bench_host_calls: {rc}")
+        return com, pre
 
     def prefetch_wait(self) -> None:
         """The prefetch's completion (the reference's prefetch callback point)."""

@@ -427,7 +427,10 @@ enum {
     CNT_NSIMPLE = 22,   // general path: events on the per-pass simple list (tr_lists)
     CNT_NCOMPLEX = 23,  // general path: events on the per-pass complex list
     CNT_ALL = 24,       // general path: the pass at which every event is evaluated (Dirty::all)
-    CNT_COUNT = 25,
+    CNT_STICKY = 25,    // FL_ERROR / FL_FOREIGN raised by a chunk's apply kernels: no chunk's reset
+                        // clears it (the host reads a pass group's counters before its apply
+                        // kernels run, and this word with the call's end)
+    CNT_COUNT = 26,
 };
 // A call's report in host memory (k_report, or fp_tail's last phase): counters, then the
 // device cursors, then the reply count of each batch (words).

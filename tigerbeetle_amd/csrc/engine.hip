@@ -446,6 +446,7 @@ struct tbgpu_ctx {
     u8* ximp = nullptr;          // per stored row: 1 = imported from another shard
     hipEvent_t ev0, ev1;
     hipEvent_t ev_side, ev_lists;  // fixed_point's side count and work-list lengths landed
+    hipEvent_t ev_group;           // a pass group's counters landed (before its apply kernels ran)
     // phase profiler: consecutive marks on the ctx stream; segment k belongs to
     // the phase opened by mark k.
     bool prof = false;
@@ -682,6 +683,7 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     HIP_CHECK(hipEventCreate(&c->ev1));
     HIP_CHECK(hipEventCreateWithFlags(&c->ev_side, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&c->ev_lists, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&c->ev_group, hipEventDisableTiming));
     c->accounts_max = o.accounts_max;
     c->aidx_cap = pow2_at_least(2 * o.hashed_max);  // ids outside the direct-mapped directory
     c->xrow_cap = o.transfers_max;
@@ -739,6 +741,7 @@ extern "C" void tbgpu_reset(tbgpu_ctx* c) {
     HIP_CHECK(hipMemsetAsync(c->T.xrun, 0, 8 * sizeof(u64), c->stream));                 // empty run
     HIP_CHECK(hipMemsetAsync(c->T.big, 0, 4 * sizeof(u32), c->stream));  // the guard and the index occupancy
     HIP_CHECK(hipMemsetAsync(c->T.base, 0, 4 * sizeof(u64), c->stream));
+    HIP_CHECK(hipMemsetAsync(c->counters, 0, CNT_COUNT * sizeof(u32), c->stream));  // CNT_STICKY included
     if (c->T.dense_n) HIP_CHECK(hipMemsetAsync(c->T.dense, 0, c->T.dense_n * sizeof(u64), c->stream));
     if (c->ximp) HIP_CHECK(hipMemsetAsync(c->ximp, 0, c->xrow_cap, c->stream));
     HIP_CHECK(hipMemsetAsync(c->f_gtab, 0, c->f_gcap * sizeof(u32), c->stream));  // fast path's claim table
@@ -816,6 +819,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
     (void)hipEventDestroy(c->ev1);
     (void)hipEventDestroy(c->ev_side);
     (void)hipEventDestroy(c->ev_lists);
+    (void)hipEventDestroy(c->ev_group);
     (void)hipStreamDestroy(c->stream);
     (void)hipStreamDestroy(c->route_stream);
     delete c;
@@ -1326,6 +1330,13 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
         const u32 p0 = p;
         p += group;
         tr_launch_converged(chg, PC_RING, p0, p, c->counters, c->counters + EPI_WORD, s);
+        // the group's counters come back now, and the host decides on them while the
+        // apply kernels run (gated on the convergence word): a converged chunk's next
+        // chunk is enqueued behind them without the GPU idling through the host's wake-up.
+        // The apply kernels' own errors land in CNT_STICKY, read with the call's end.
+        HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, (PC_OFF + PC_RING) * sizeof(u32), hipMemcpyDeviceToHost,
+                                 s));
+        HIP_CHECK(hipEventRecord(c->ev_group, s));
         if (narrow && !c->long_segments) {
             // the Bal4 balances of the converged state (tr_apply's history rows, bs_final)
             SideScanArgs SF = SA;
@@ -1334,13 +1345,13 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
             SF.cfail_alt = c->st[1].cfail;
             SF.cfail_clear = nullptr;
             SF.epi = c->counters + EPI_WORD;
-            side_scan_fused(SF, m, inv_acc, c->tstart, c->counters + CNT_LONG, c->T.acc, c->bb, s);
+            // (its long-segment word is the sticky one: the passes' narrow scans, over the
+            // same windows, would have met such a segment first, so this is an error)
+            side_scan_fused(SF, m, inv_acc, c->tstart, c->counters + CNT_STICKY, c->T.acc, c->bb, s);
         }
         epilogue(m);
         prof_mark(c, PH_END);
-        HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, (PC_OFF + PC_RING) * sizeof(u32), hipMemcpyDeviceToHost,
-                                 s));
-        wait_stream(s);
+        wait_event(c->ev_group);
         if (c->h_counters[CNT_FLAGS] & FL_FOREIGN)
             tbgpu_fatal("create_transfers", "a transfer of a ledger another shard owns (ledger shard ctx)", __FILE__,
                         __LINE__);
@@ -1845,6 +1856,10 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
             memcpy(c->h_counters, c->h_report, CNT_COUNT * sizeof(u32));
             memcpy(c->h_base, c->h_report + RPT_BASE, 4 * sizeof(u64));
             memcpy(c->h_rc + b0, c->h_report + RPT_COUNTS, nb * sizeof(u32));
+            if (c->h_counters[CNT_STICKY])  // an apply kernel's error in any chunk of the call
+                tbgpu_fatal("create_transfers", (c->h_counters[CNT_STICKY] & FL_FOREIGN) ?
+                            "a transfer of a ledger another shard owns (ledger shard ctx)" :
+                            "device error in the apply kernels (table capacity)", __FILE__, __LINE__);
             if (!spec_settle(c))  // the speculative fast attempt fell back: redo the call
                 return transfers_batches(c, nb_total, timestamps, counts, ev_src, src_device, results, dst_device,
                                          result_counts, ev_ts_host, ctl_host, routed_device);

@@ -1332,7 +1332,10 @@ __global__ void tr_apply(Tables T, TrArgs C, EvalState S, const u8* __restrict__
     const u64 row_base = T.base[BASE_ROWS], hist_base = T.base[BASE_HIST];
     const uint4 tot = rk[C.n];
     if (!C.dry && (row_base + tot.x > T.xrow_cap || hist_base + tot.z > T.hist_cap)) {
-        if (i == 0) atomicOr(&C.counters[CNT_FLAGS], (u32)FL_ERROR);
+        if (i == 0) {
+            atomicOr(&C.counters[CNT_FLAGS], (u32)FL_ERROR);
+            atomicOr(&C.counters[CNT_STICKY], (u32)FL_ERROR);
+        }
         return;
     }
     const u8 r = fres[i];
@@ -1356,6 +1359,7 @@ __global__ void tr_apply(Tables T, TrArgs C, EvalState S, const u8* __restrict__
     } else {
         if (C.dslot[i] == ROW_FOREIGN || C.cslot[i] == ROW_FOREIGN) {  // (never: evaluate_one flagged it)
             atomicOr(&C.counters[CNT_FLAGS], (u32)FL_FOREIGN);
+            atomicOr(&C.counters[CNT_STICKY], (u32)FL_FOREIGN);
             return;
         }
         // the accounts' history flags are in the event's core (classify): the rows are
@@ -1757,7 +1761,7 @@ __global__ void tr_prep(TrArgs C, u32* cfail0, u32* pc, u32 ring) {
             pc[ring + k] = NONE32;
         }
         if (k == 0) pc[2 * ring] = 1;  // an open gate (the full scans after a headroom fixed point, the walk)
-        if (k < CNT_COUNT) C.counters[k] = 0;
+        if (k < CNT_COUNT && k != CNT_STICKY) C.counters[k] = 0;
     }
 }
 

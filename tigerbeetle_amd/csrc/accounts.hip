@@ -273,15 +273,29 @@ constexpr int AF_THREADS = 256;
 
 __global__ __launch_bounds__(AF_THREADS) void ac_fast_check(Tables T, AcArgs C, u64 row_base) {
     const u64 t = (u64)blockIdx.x * AF_THREADS + threadIdx.x;
-    const u32 e = (u32)(t >> 3), ch = (u32)(t & 7);
+    const u32 e = (u32)(t >> 3), ch = (u32)(t & 7), lane = threadIdx.x & 63;
+    // The wave's 8 events are nearly always in one batch: one uniform binary search for
+    // its first event, issued before the event loads, and lanes past a batch boundary
+    // walk on (a search per event made every wave wait for seven dependent loads)
+    const u32 e0 = __builtin_amdgcn_readfirstlane(e);
+    u32 b = e0 < C.n ? ac_batch_of(C.b_start, C.nb, e0) : 0u;
     bool bad = false;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (e < C.n) v = ((const uint4*)&C.ev[e])[ch];
+    // the previous event's id: from the lanes 8 below (chunk 0 of event e - 1), or, for
+    // the wave's first event, from memory
+    const u32 px = __shfl(v.x, lane - 8), py = __shfl(v.y, lane - 8), pz = __shfl(v.z, lane - 8),
+              pw = __shfl(v.w, lane - 8);
     if (e < C.n) {
-        uint4 v = ((const uint4*)&C.ev[e])[ch];
         switch (ch) {
         case 0: {  // id: not 0 / maxInt (:1204-1205), absent, above the previous event's
             const u128 id = ((u128)(((u64)v.w << 32) | v.z) << 64) | (((u64)v.y << 32) | v.x);
             bad = id == 0 || id == U128_MAX;
-            if (!bad && e > 0) bad = !(id > C.ev[e - 1].id);
+            if (!bad && e > 0) {
+                const u128 prev = lane >= 8 ? ((u128)(((u64)pw << 32) | pz) << 64) | (((u64)py << 32) | px)
+                                            : C.ev[e - 1].id;
+                bad = !(id > prev);
+            }
             if (!bad) {
                 if (dense_has(T, id)) bad = T.dense[dense_slot(T, id)] != 0;
                 else bad = acc_probe(T.aidx, T.aidx_mask, id) != NONE32;
@@ -298,7 +312,7 @@ __global__ __launch_bounds__(AF_THREADS) void ac_fast_check(Tables T, AcArgs C, 
             const u32 code = v.y & 0xFFFFu, flags = v.y >> 16;
             bad = v.x == 0 || code == 0 || (v.z | v.w) != 0 || (flags & (0xFFF0u | AF_LINKED)) != 0 ||
                   ((flags & AF_DNEC) && (flags & AF_CNED));
-            const u32 b = ac_batch_of(C.b_start, C.nb, e);
+            while (b + 1 < C.nb && C.b_start[b + 1] <= e) b++;
             const u32 bs = C.b_start[b], nbatch = C.b_start[b + 1] - bs;
             const u64 ts = C.b_ts[b] - nbatch + (e - bs) + 1;
             v.z = (u32)ts;

@@ -266,9 +266,15 @@ __global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const
 //                  one lane probes the directory / index and compares the id with
 //                  the previous event's.  Anything else raises FL_SLOW (one atomic
 //                  per wave), and the host redoes the call on the general path
-//                  (rows past n_accounts are free space, nothing else was written).
-//   ac_fast_index  gated on a clean check: the index slot (CAS on its row word),
-//                  the directory entry, zero reply counts, commit_timestamp.
+//                  (rows past n_accounts are free space; the directory entries the
+//                  check wrote are cleared by ac_fast_index first).
+//                  An id of the direct-mapped directory whose entry is empty gets
+//                  its entry right there (ids rise through the call, so no two events
+//                  write one entry).
+//   ac_fast_index  on a clean check: the index slot of every hashed id (CAS on its row
+//                  word; none when every id is in the directory, FL_AC_HASHED clear),
+//                  zero reply counts, commit_timestamp.  On a failed check: the
+//                  directory entries the check wrote are cleared again.
 constexpr int AF_THREADS = 256;
 
 __global__ __launch_bounds__(AF_THREADS) void ac_fast_check(Tables T, AcArgs C, u64 row_base) {
@@ -286,6 +292,9 @@ __global__ __launch_bounds__(AF_THREADS) void ac_fast_check(Tables T, AcArgs C, 
     // the wave's first event, from memory
     const u32 px = __shfl(v.x, lane - 8), py = __shfl(v.y, lane - 8), pz = __shfl(v.z, lane - 8),
               pw = __shfl(v.w, lane - 8);
+    // the event's ledger and flags (chunk 7, seven lanes up), for its directory entry
+    const u32 q7x = __shfl(v.x, lane + 7), q7y = __shfl(v.y, lane + 7);
+    bool hashed = false;
     if (e < C.n) {
         switch (ch) {
         case 0: {  // id: not 0 / maxInt (:1204-1205), absent, above the previous event's
@@ -297,8 +306,14 @@ __global__ __launch_bounds__(AF_THREADS) void ac_fast_check(Tables T, AcArgs C, 
                 bad = !(id > prev);
             }
             if (!bad) {
-                if (dense_has(T, id)) bad = T.dense[dense_slot(T, id)] != 0;
-                else bad = acc_probe(T.aidx, T.aidx_mask, id) != NONE32;
+                if (dense_has(T, id)) {
+                    u64& d = T.dense[dense_slot(T, id)];
+                    bad = d != 0;
+                    if (!bad) d = dense_entry((u32)(row_base + e), q7x, (u16)(q7y >> 16));
+                } else {
+                    hashed = true;
+                    bad = acc_probe(T.aidx, T.aidx_mask, id) != NONE32;
+                }
             }
             break;
         }
@@ -324,19 +339,31 @@ __global__ __launch_bounds__(AF_THREADS) void ac_fast_check(Tables T, AcArgs C, 
         }
         ((uint4*)&T.acc[row_base + e])[ch] = v;
     }
-    if (__ballot(bad) && wave_leader()) atomicOr(&C.counters[CNT_FLAGS], (u32)FL_SLOW);
+    const u32 fl = (__ballot(bad) ? (u32)FL_SLOW : 0u) | (__ballot(hashed) ? (u32)FL_AC_HASHED : 0u);
+    if (fl && wave_leader()) atomicOr(&C.counters[CNT_FLAGS], fl);
 }
 
 __global__ __launch_bounds__(AF_THREADS) void ac_fast_index(Tables T, AcArgs C, u64 row_base) {
-    if (C.counters[CNT_FLAGS] & FL_SLOW) return;
+    const u32 flags = C.counters[CNT_FLAGS];
     const u32 i = blockIdx.x * AF_THREADS + threadIdx.x;
-    if (i < C.n) {
+    if (flags & FL_SLOW) {
+        // the call goes to the general path: the directory entries the check wrote go
+        if (i < C.n) {
+            const u128 id = C.ev[i].id;
+            if (dense_has(T, id)) {
+                u64& d = T.dense[dense_slot(T, id)];
+                if (d != 0 && dense_row(d) == (u32)(row_base + i)) d = 0;
+            }
+        }
+        return;
+    }
+    if (i < C.n && (flags & FL_AC_HASHED)) {
         const u32 row = (u32)(row_base + i);
         const uint4 k = ((const uint4*)&T.acc[row])[0];
         const uint4 m = ((const uint4*)&T.acc[row])[7];
         const u128 id = ((u128)(((u64)k.w << 32) | k.z) << 64) | (((u64)k.y << 32) | k.x);
-        const u16 code = (u16)(m.y & 0xFFFFu), flags = (u16)(m.y >> 16);
-        if (!acc_insert(T, id, row, m.x, flags, code)) atomicOr(&C.counters[CNT_FLAGS], (u32)FL_CAPACITY);
+        const u16 code = (u16)(m.y & 0xFFFFu), af = (u16)(m.y >> 16);
+        if (!acc_insert(T, id, row, m.x, af, code)) atomicOr(&C.counters[CNT_FLAGS], (u32)FL_CAPACITY);
     }
     if (blockIdx.x == 0) {
         // replies: none; commit_timestamp: the latest event's (every event is accepted)

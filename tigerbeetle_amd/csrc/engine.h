@@ -452,4 +452,5 @@ enum {
     FL_CAPACITY = 1u << 12,   // create_accounts: accounts_max reached (ac_apply wrote nothing past it)
     FL_WIDE = 1u << 14,       // general path: an amount >= 2^64 or a balance near 2^128 (no headroom passes)
     FL_FOREIGN = 1u << 13,    // ledger shard: a transfer on a ledger another shard owns reached its balances
+    FL_AC_HASHED = 1u << 15,  // create_accounts' clean call: some id is outside the direct-mapped directory
 };

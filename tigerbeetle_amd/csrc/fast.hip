@@ -115,11 +115,22 @@ __device__ __forceinline__ bool xidx_committed(const Tables& T, u32 r1, u64 row_
     return r1 != XIDX_TOMB && r1 - 1 < row_base && T.xrows[r1 - 1].id == id;
 }
 
-__device__ __forceinline__ u32 xidx_probe_from(const Tables& T, u64 h, u128 id, u64 row_base) {
+// A slot this call claimed was empty before the call, so no committed row with the id
+// lies past it (linear probing): the probe ends there, as at an empty slot.  `*end` is
+// where it ended: the slot an eager claim of the id starts at (the occupied slots before
+// it hold other ids, and stay occupied through the call).
+__device__ __forceinline__ bool xidx_ends_probe(u32 r1, u64 row_base) {
+    return r1 == 0 || (r1 != XIDX_TOMB && r1 - 1 >= row_base);
+}
+
+__device__ __forceinline__ u32 xidx_probe_from(const Tables& T, u64 h, u128 id, u64 row_base, u64* end = nullptr) {
     for (;;) {
         h = (h + XIDX_STEP) & T.xidx_mask;
         const u32 r1 = T.xidx[h];
-        if (r1 == 0) return NONE32;
+        if (xidx_ends_probe(r1, row_base)) {
+            if (end) *end = h;
+            return NONE32;
+        }
         if (xidx_committed(T, r1, row_base, id)) return r1 - 1;
     }
 }
@@ -143,8 +154,7 @@ __device__ __forceinline__ u32 xidx_probe_pre(const Tables& T, u128 id, u64 row_
 // call's rows (>= row_base: event row - row_base, whose id is read from the events)
 // with the same id is a repeat within the call: returns true (nothing claimed).
 __device__ __forceinline__ bool fp_claim_is_dup(const Tables& T, const FastArgs& F, u128 id, u64 row_base, u32 i,
-                                                u32* slot) {
-    u64 h = xidx_hash(id) & T.xidx_mask;
+                                                u64 h, u32* slot) {
     for (;;) {
         const u32 prev = atomicCAS(&T.xidx[h], 0u, (u32)(row_base + i) + 1);
         if (prev == 0) {
@@ -168,8 +178,9 @@ __device__ __forceinline__ u8 fp_classify_guarded(const Tables& T, const FastArg
 // precedence of the resulting checks is ordered), so one event costs about one
 // memory round trip instead of four.
 __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, const Transfer& t, u32 i, u64 ts,
-                                          u64 row_base, u32* dslot_out, u32* cslot_out) {
+                                          u64 row_base, u32* dslot_out, u32* cslot_out, u64* xend) {
     const u16 f = t.flags;
+    *xend = xidx_hash(t.id) & T.xidx_mask;  // (the guarded form's claims start at the id's slot)
     if (f & (TF_BDR | TF_BCR | TF_POST | TF_VOID) || *T.big)
         return fp_classify_guarded(T, F, t, i, ts, row_base, dslot_out, cslot_out);
     // speculative first-slot reads (hash tables at load <= 0.5: usually the hit).
@@ -219,8 +230,8 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
     if (t.ledger != A.ledger) return TBGPU_CREATE_TRANSFER_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
     if (!ledger_owned(T, t.ledger)) return FRES_SLOW;  // another shard's ledger (the general path refuses it)
     if ((A.flags | B.flags) & (AF_DNEC | AF_CNED | AF_HISTORY)) return FRES_SLOW;  // limits / history
-    if (x_r1 != 0) {
-        const u32 pre = xidx_committed(T, x_r1, row_base, t.id) ? x_r1 - 1 : xidx_probe_from(T, hx, t.id, row_base);
+    if (maybe && !xidx_ends_probe(x_r1, row_base)) {
+        const u32 pre = xidx_committed(T, x_r1, row_base, t.id) ? x_r1 - 1 : xidx_probe_from(T, hx, t.id, row_base, xend);
         if (pre != NONE32) return fp_exists(t, T.xrows[pre]);
     }
     if (xrun_maybe(T, t.id)) {  // the sorted run (an id replayed from an earlier call)
@@ -521,13 +532,14 @@ __device__ __forceinline__ void fp_commit_body(const Tables& T, FastArgs F, cons
     if (valid) {
         id = t.id;
         u32 ds = NONE32, cs = NONE32;
+        u64 xend = xidx_hash(t.id) & T.xidx_mask;  // where an eager claim starts (fp_classify)
         if (lk && i - bs == nbatch - 1) r = TBGPU_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN;  // checked first (:1024)
         else if (myctl & TBGPU_CTL_SKIP) r = TBGPU_CREATE_TRANSFER_LINKED_EVENT_FAILED;    // broken on another shard
-        else r = fp_classify(T, F, t, i, ts, row_base, &ds, &cs);
+        else r = fp_classify(T, F, t, i, ts, row_base, &ds, &cs, &xend);
         own_ok = r == TBGPU_CREATE_TRANSFER_OK;
         if (F.eager) {
             u32 slot = NONE32;
-            if (own_ok && fp_claim_is_dup(T, F, t.id, row_base, i, &slot)) {
+            if (own_ok && fp_claim_is_dup(T, F, t.id, row_base, i, xend, &slot)) {
                 r = FRES_SLOW;  // an id repeated within the call: the fixed point decides it
                 own_ok = false;
             }

@@ -25,7 +25,7 @@ struct Tables {
     u64 aidx_mask;     // capacity - 1 (power of two)
     Transfer* xrows;   // stored transfers, append-only, commit order
     u8* xful;          // posted groove by pending row: 0 none, 1 posted, 2 voided
-    u32* xidx;         // transfer id -> row + 1 (the key is read from xrows)
+    u64* xidx;         // transfer id -> slot: row + 1 (low word; 0 empty) | key fingerprint << 32
     u64 xidx_mask;
     History* hrows;    // account-history groove rows, append-only
     u64* commit_ts;    // device copy of StateMachine.commit_timestamp (atomicMax)
@@ -388,14 +388,25 @@ __device__ __forceinline__ u32 xrun_find(const Tables& T, u128 id) {
 // A slot whose claim was withdrawn (fast.hip's eager claims: a chain of the call broke,
 // or its event failed a later check): probes walk past it, inserts never reuse it.
 constexpr u32 XIDX_TOMB = 0xFFFFFFFFu;
+// A slot is 8 bytes: row + 1 in the low word (0: empty), in the high word 32 bits of the
+// id's hash independent of the slot's own: a probe reads a row (its 128 bytes, for the
+// key) only when the fingerprint matches, so colliding ids of random order cost one slot
+// read each instead of a slot and a row.
+__device__ __forceinline__ u32 xidx_fp(u128 id) {
+    return (u32)(mix64((u64)(id >> 64) * 0x9E3779B97F4A7C15ull ^ (u64)id) >> 32);
+}
+__device__ __forceinline__ u64 xidx_slot(u128 id, u32 row) { return ((u64)xidx_fp(id) << 32) | (row + 1); }
+__device__ __forceinline__ u32 xidx_r1(u64 e) { return (u32)e; }
 
 __device__ __forceinline__ u32 xidx_probe(const Tables& T, u128 id) {
     if (xidx_maybe_present(T, id)) {  // else outside the hashed ids' key range
+        const u32 fp = xidx_fp(id);
         u64 h = xidx_hash(id) & T.xidx_mask;
         for (;;) {
-            const u32 r1 = T.xidx[h];
+            const u64 e = T.xidx[h];
+            const u32 r1 = xidx_r1(e);
             if (r1 == 0) break;
-            if (r1 != XIDX_TOMB && T.xrows[r1 - 1].id == id) return r1 - 1;
+            if (r1 != XIDX_TOMB && (u32)(e >> 32) == fp && T.xrows[r1 - 1].id == id) return r1 - 1;
             h = (h + XIDX_STEP) & T.xidx_mask;
         }
     }
@@ -405,7 +416,9 @@ __device__ __forceinline__ u32 xidx_probe(const Tables& T, u128 id) {
 // Inserts never compare keys: a call inserts ids that are absent and distinct.
 __device__ __forceinline__ void xidx_insert(const Tables& T, u128 id, u32 row) {
     u64 h = xidx_hash(id) & T.xidx_mask;
-    while (atomicCAS(&T.xidx[h], 0u, row + 1) != 0) h = (h + XIDX_STEP) & T.xidx_mask;
+    const u64 v = xidx_slot(id, row);
+    while (atomicCAS((unsigned long long*)&T.xidx[h], 0ull, (unsigned long long)v) != 0)
+        h = (h + XIDX_STEP) & T.xidx_mask;
 }
 
 // Counter words (device u32[16]) used for host decisions.

@@ -696,7 +696,7 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     c->T.aidx_mask = c->aidx_cap - 1;
     c->T.xrows = dalloc<Transfer>(c->xrow_cap, &B);
     c->T.xful = dalloc<u8>(c->xrow_cap, &B);
-    c->T.xidx = dalloc_hot<u32>(c->xidx_cap, &B);
+    c->T.xidx = dalloc_hot<u64>(c->xidx_cap, &B);
     c->T.xidx_mask = c->xidx_cap - 1;
     c->T.hrows = dalloc<History>(c->hist_cap, &B);
     c->T.commit_ts = dalloc<u64>(2, &B);
@@ -734,7 +734,7 @@ extern "C" void tbgpu_reset(tbgpu_ctx* c) {
     c->pf_valid = false;
     HIP_CHECK(hipMemsetAsync(c->T.aidx, 0, c->aidx_cap * sizeof(AccIdx), c->stream));
     HIP_CHECK(hipMemsetAsync(c->T.xful, 0, c->xrow_cap, c->stream));
-    HIP_CHECK(hipMemsetAsync(c->T.xidx, 0, c->xidx_cap * sizeof(u32), c->stream));
+    HIP_CHECK(hipMemsetAsync(c->T.xidx, 0, c->xidx_cap * sizeof(u64), c->stream));
     HIP_CHECK(hipMemsetAsync(c->T.commit_ts, 0, 2 * sizeof(u64), c->stream));
     HIP_CHECK(hipMemsetAsync(c->T.idr, 0, 2 * sizeof(u64), c->stream));                  // max = 0
     HIP_CHECK(hipMemsetAsync(c->T.idr + 2, 0xFF, 2 * sizeof(u64), c->stream));           // min = ~0
@@ -1718,7 +1718,7 @@ static void xidx_tombs_check(tbgpu_ctx* c) {
     if (tombs <= slots / 16) return;
     u64 rows = 0;
     d2h(c, &rows, c->T.base + BASE_ROWS, sizeof(u64), s);
-    HIP_CHECK(hipMemsetAsync(c->T.xidx, 0, slots * sizeof(u32), s));
+    HIP_CHECK(hipMemsetAsync(c->T.xidx, 0, slots * sizeof(u64), s));
     HIP_CHECK(hipMemsetAsync(c->T.hcount + 2, 0, sizeof(u32), s));
     launch_rehash_xidx(c->T, rows, s);
     c->stats.index_rebuilds++;

@@ -111,27 +111,29 @@ __device__ __forceinline__ u64 aidx_probe_from(const Tables& T, u64 h, u128 id) 
 // that names a row of this call is an eager claim (FastArgs::eager), whose row may or
 // may not be stored yet: the claim itself decides a repeat (fp_claim_is_dup), so a probe
 // of the pre-call state walks past it like a tombstone.
-__device__ __forceinline__ bool xidx_committed(const Tables& T, u32 r1, u64 row_base, u128 id) {
-    return r1 != XIDX_TOMB && r1 - 1 < row_base && T.xrows[r1 - 1].id == id;
+__device__ __forceinline__ bool xidx_committed(const Tables& T, u64 e, u64 row_base, u128 id) {
+    const u32 r1 = xidx_r1(e);
+    return r1 != XIDX_TOMB && r1 - 1 < row_base && (u32)(e >> 32) == xidx_fp(id) && T.xrows[r1 - 1].id == id;
 }
 
 // A slot this call claimed was empty before the call, so no committed row with the id
 // lies past it (linear probing): the probe ends there, as at an empty slot.  `*end` is
 // where it ended: the slot an eager claim of the id starts at (the occupied slots before
 // it hold other ids, and stay occupied through the call).
-__device__ __forceinline__ bool xidx_ends_probe(u32 r1, u64 row_base) {
+__device__ __forceinline__ bool xidx_ends_probe(u64 e, u64 row_base) {
+    const u32 r1 = xidx_r1(e);
     return r1 == 0 || (r1 != XIDX_TOMB && r1 - 1 >= row_base);
 }
 
 __device__ __forceinline__ u32 xidx_probe_from(const Tables& T, u64 h, u128 id, u64 row_base, u64* end = nullptr) {
     for (;;) {
         h = (h + XIDX_STEP) & T.xidx_mask;
-        const u32 r1 = T.xidx[h];
-        if (xidx_ends_probe(r1, row_base)) {
+        const u64 e = T.xidx[h];
+        if (xidx_ends_probe(e, row_base)) {
             if (end) *end = h;
             return NONE32;
         }
-        if (xidx_committed(T, r1, row_base, id)) return r1 - 1;
+        if (xidx_committed(T, e, row_base, id)) return xidx_r1(e) - 1;
     }
 }
 
@@ -139,9 +141,9 @@ __device__ __forceinline__ u32 xidx_probe_from(const Tables& T, u64 h, u128 id, 
 __device__ __forceinline__ u32 xidx_probe_pre(const Tables& T, u128 id, u64 row_base) {
     if (xidx_maybe_present(T, id)) {
         const u64 h = xidx_hash(id) & T.xidx_mask;
-        const u32 r1 = T.xidx[h];
-        if (r1 != 0) {
-            const u32 r = xidx_committed(T, r1, row_base, id) ? r1 - 1 : xidx_probe_from(T, h, id, row_base);
+        const u64 e = T.xidx[h];
+        if (xidx_r1(e) != 0) {
+            const u32 r = xidx_committed(T, e, row_base, id) ? xidx_r1(e) - 1 : xidx_probe_from(T, h, id, row_base);
             if (r != NONE32) return r;
         }
     }
@@ -155,13 +157,16 @@ __device__ __forceinline__ u32 xidx_probe_pre(const Tables& T, u128 id, u64 row_
 // with the same id is a repeat within the call: returns true (nothing claimed).
 __device__ __forceinline__ bool fp_claim_is_dup(const Tables& T, const FastArgs& F, u128 id, u64 row_base, u32 i,
                                                 u64 h, u32* slot) {
+    const u64 mine = xidx_slot(id, (u32)(row_base + i));
+    const u32 fp = (u32)(mine >> 32);
     for (;;) {
-        const u32 prev = atomicCAS(&T.xidx[h], 0u, (u32)(row_base + i) + 1);
-        if (prev == 0) {
+        const u64 pe = atomicCAS((unsigned long long*)&T.xidx[h], 0ull, (unsigned long long)mine);
+        const u32 prev = xidx_r1(pe);
+        if (pe == 0) {
             *slot = (u32)h;
             return false;
         }
-        if (prev != XIDX_TOMB && prev - 1 >= row_base && F.ev[prev - 1 - row_base].id == id) {
+        if (prev != XIDX_TOMB && prev - 1 >= row_base && (u32)(pe >> 32) == fp && F.ev[prev - 1 - row_base].id == id) {
             *slot = NONE32;
             return true;
         }
@@ -199,9 +204,9 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
         if (dd) EA = T.dense[dense_slot(T, t.debit_account_id)]; else A = T.aidx[hd];
         if (dc) EB = T.dense[dense_slot(T, t.credit_account_id)]; else B = T.aidx[hc];
     }
-    const bool maybe = xidx_maybe_present(T, t.id);
+    const bool maybe = !(FP_ABLATE & ABL_IDS) && xidx_maybe_present(T, t.id);  // (ABL_IDS: timing only)
     const u64 hx = xidx_hash(t.id) & T.xidx_mask;
-    const u32 x_r1 = maybe ? T.xidx[hx] : 0u;
+    const u64 x_r1 = maybe ? T.xidx[hx] : 0ull;
     if (t.timestamp != 0) return TBGPU_CREATE_TRANSFER_TIMESTAMP_MUST_BE_ZERO;
     if (f & 0xFFC0u) return TBGPU_CREATE_TRANSFER_RESERVED_FLAG;
     if (t.id == 0) return TBGPU_CREATE_TRANSFER_ID_MUST_NOT_BE_ZERO;
@@ -231,7 +236,8 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
     if (!ledger_owned(T, t.ledger)) return FRES_SLOW;  // another shard's ledger (the general path refuses it)
     if ((A.flags | B.flags) & (AF_DNEC | AF_CNED | AF_HISTORY)) return FRES_SLOW;  // limits / history
     if (maybe && !xidx_ends_probe(x_r1, row_base)) {
-        const u32 pre = xidx_committed(T, x_r1, row_base, t.id) ? x_r1 - 1 : xidx_probe_from(T, hx, t.id, row_base, xend);
+        const u32 pre = xidx_committed(T, x_r1, row_base, t.id) ? xidx_r1(x_r1) - 1
+                                                                 : xidx_probe_from(T, hx, t.id, row_base, xend);
         if (pre != NONE32) return fp_exists(t, T.xrows[pre]);
     }
     if (xrun_maybe(T, t.id)) {  // the sorted run (an id replayed from an earlier call)
@@ -390,8 +396,11 @@ __device__ __forceinline__ void fp_commit_body(const Tables& T, FastArgs F, cons
             F.b_start = s_blk;
             F.b_ts = (const u64*)(s_blk + ((F.nb + 2) & ~1u));  // batch_ts_offset
         }
-        if (tid == 0) s_flags = 0;
     }
+    // the tile's FL_* flags gather in LDS (a per-wave atomic on the call's flag word
+    // serialized at the memory side: 128k waves of random ids each raising
+    // FL_NONMONO, half of config 4's waves raising FL_FCHAIN), then one atomic per tile
+    if (tid == 0) s_flags = 0;
     const u64 row_base = T.base[BASE_ROWS];  // device cursor: no host round trip between calls
     // When this call's rows will extend the id index's sorted run if every event is
     // accepted with rising ids (the benchmark's case: fp_run), nothing needs the id
@@ -519,7 +528,7 @@ __device__ __forceinline__ void fp_commit_body(const Tables& T, FastArgs F, cons
         plk = (F.ev[i - 1].flags & TF_LINKED) && !(F.ctl && (F.ctl[i - 1] & TBGPU_CTL_CHAIN_END));
     plk = plk && valid && i > bs;
     const bool member = lk || plk || (myctl & TBGPU_CTL_DOOM);
-    if (__ballot(member) && lane == 0) atomicOr(SMALL ? &s_flags : &F.counters[CNT_FLAGS], (u32)FL_FCHAIN);
+    if (__ballot(member) && lane == 0) atomicOr(&s_flags, (u32)FL_FCHAIN);
     bool own_ok = false;
 #if defined(FP_NT_ROWS)  // timing variant: rows written with non-temporal stores
 #define STORE_ROW() do { if (!(FP_ABLATE & ABL_ROWS)) { \
@@ -539,7 +548,7 @@ __device__ __forceinline__ void fp_commit_body(const Tables& T, FastArgs F, cons
         own_ok = r == TBGPU_CREATE_TRANSFER_OK;
         if (F.eager) {
             u32 slot = NONE32;
-            if (own_ok && fp_claim_is_dup(T, F, t.id, row_base, i, xend, &slot)) {
+            if (own_ok && !(FP_ABLATE & ABL_IDS) && fp_claim_is_dup(T, F, t.id, row_base, i, xend, &slot)) {
                 r = FRES_SLOW;  // an id repeated within the call: the fixed point decides it
                 own_ok = false;
             }
@@ -571,7 +580,7 @@ __device__ __forceinline__ void fp_commit_body(const Tables& T, FastArgs F, cons
             t.timestamp = ts;
             STORE_ROW();
         } else if (r == FRES_SLOW) {
-            atomicOr(SMALL ? &s_flags : &F.counters[CNT_FLAGS], (u32)FL_SLOW);
+            atomicOr(&s_flags, (u32)FL_SLOW);
         } else if (r != FRES_CHAIN && !SMALL) {
             atomicAdd(&F.batch_counts[b], 1u);  // (SMALL: fp_tail counts each batch's replies)
         }
@@ -595,7 +604,7 @@ __device__ __forceinline__ void fp_commit_body(const Tables& T, FastArgs F, cons
             }
         }
         const bool up = !valid || i == 0 || hi > phi || (hi == phi && lo > plo);
-        if (__ballot(!up) && lane == 0) atomicOr(SMALL ? &s_flags : &F.counters[CNT_FLAGS], (u32)FL_NONMONO);
+        if (__ballot(!up) && lane == 0) atomicOr(&s_flags, (u32)FL_NONMONO);
     }
     const u64 okm = __ballot(ok), badm = __ballot(bad);
     u64 mts = ok ? ts : 0;
@@ -641,8 +650,11 @@ __device__ __forceinline__ void fp_commit_body(const Tables& T, FastArgs F, cons
             if (SMALL) {
                 F.tile_idr[TILE_WORDS * tile + 6] = nbad;
                 F.tile_idr[TILE_WORDS * tile + 7] = s_flags;
-            } else if (nbad) {
-                atomicAdd(&F.counters[CNT_BAD], nbad);
+            } else {
+                if (nbad) atomicAdd(&F.counters[CNT_BAD], nbad);
+                const u32 fl = s_flags;  // (skipped when an earlier tile raised them already)
+                if (fl && (__hip_atomic_load(&F.counters[CNT_FLAGS], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & fl) != fl)
+                    atomicOr(&F.counters[CNT_FLAGS], fl);
             }
         }
     }
@@ -889,7 +901,7 @@ __device__ void fp_chains_one(const Tables& T, const FastArgs& F, u32 i, u32& n_
         n_bad++;
         if (!F.small) atomicAdd(&F.batch_counts[b], 1u);  // (small: fp_tail counts each batch's replies)
         if (F.eager && F.gpos[i] != NONE32) {  // its claim withdrawn
-            T.xidx[F.gpos[i]] = XIDX_TOMB;
+            T.xidx[F.gpos[i]] = XIDX_TOMB;  // (the fingerprint goes too: a tombstone matches nothing)
             atomicAdd(&T.hcount[2], 1u);  // (xidx_tombs_check)
         }
     }
@@ -989,7 +1001,7 @@ __device__ __forceinline__ void fp_fix_one(const FastArgs& F, const Tables& T, u
     t.timestamp = F.ev_ts ? F.ev_ts[i] : F.b_ts[b] - (F.b_start[b + 1] - bs) + (i - bs) + 1;
     T.xrows[row] = t;
     F.rows[i] = row;
-    if (F.eager) T.xidx[F.gpos[i]] = row + 1;  // the claim follows its row
+    if (F.eager) T.xidx[F.gpos[i]] = xidx_slot(t.id, row);  // the claim follows its row
 }
 
 __global__ void fp_fix(FastArgs F, Tables T, const uint4* rk) {

@@ -658,6 +658,8 @@ typedef struct tbgpu_stats {
                                  pass budget and was walked in execute's order    */
     uint64_t index_rebuilds;  /* transfer-id index rebuilds since init: withdrawn
                                  claims of non-rising ids left tombstones          */
+    uint64_t h64_redos;       /* general-path chunks, since init, redone in the
+                                 u128 form after a 64-bit headroom left +-2^63    */
 } tbgpu_stats;
 void tbgpu_last_stats(tbgpu_ctx* ctx, tbgpu_stats* out);
 /* Enable per-phase HIP-event timing (adds a few event records per call). */

@@ -1,0 +1,16 @@
+# The general path's 64-bit headroom form: GPU tests of the general path, then config 3
+# with and without it (TBGPU_NO_H64=1), alternating.  OUT=gpurun_out/<dir>.
+set -e
+OUT=${1:-gpurun_out/h64}
+mkdir -p $OUT
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+    tests/test_gpu_parity.py tests/test_gpu_general.py tests/test_gpu_golden.py tests/test_gpu_fuzz.py \
+    > $OUT/tests.txt 2>&1
+A="--config 3 --steps 5 --warmup 1 --no-cpu --no-queries --no-host"
+for r in 1 2 3; do
+  for v in on off; do
+    if [ $v = off ]; then export TBGPU_NO_H64=1; else unset TBGPU_NO_H64; fi
+    timeout -k 10 200 python bench.py $A > $OUT/c3_${v}_$r.json 2> $OUT/c3_${v}_$r.err
+    echo "$v $r $(python -c "import json;d=json.load(open('$OUT/c3_${v}_$r.json'));print(d['value'],d['ms_per_step'],d['roofline'].get('phase_ms_per_step'))")"
+  done
+done

@@ -160,6 +160,47 @@ commit lookup_accounts
         gpu.close()
 
 
+def _h64_table(last_amount: int) -> str:
+    """Eight accounts just under 2^61 (the 64-bit headroom form's entry bound) whose
+    balancing debits pile their headroom onto A9 inside one call: A9's figures leave
+    +-2^63 during the fixed point.  (No transfer takes an account across 2^61 before the
+    call's fixed point: the fast path's attempt, undone, would set the guard bit.)"""
+    top = (1 << 61) - 1
+    lines = [f"account A{k} 0 0 0 0 _ _ _ _ L1 C1 _ _ _ _ _ ok" for k in range(1, 11)]
+    lines.append("commit create_accounts")
+    lines += [f"setup A{k} 0 0 0 {top}" for k in range(1, 9)]
+    lines += [f"transfer T{k} A{k} A9 0 _ _ _ _ _ L1 C1 _ _ _ _ BDR _ _ _ ok" for k in range(1, 9)]
+    lines.append("transfer T9 A9 A10 5 _ _ _ _ _ L1 C1 _ _ _ _ _ _ _ _ ok")
+    lines.append(f"transfer T10 A10 A9 {last_amount} _ _ _ _ _ L1 C1 _ _ _ _ _ _ _ _ ok")
+    lines.append("commit create_transfers")
+    lines += [f"lookup_account A{k} 0 {top} 0 {top}" for k in range(1, 9)]
+    lines.append(f"lookup_account A9 0 5 0 {8 * top + last_amount}")
+    lines.append(f"lookup_account A10 0 {last_amount} 0 5")
+    lines.append("commit lookup_accounts")
+    return "\n".join(lines)
+
+
+@pytest.mark.parametrize("big_amount", [False, True], ids=["h64-redo", "wide64"])
+def test_h64_headroom_overflow_redoes_the_chunk(big_amount):
+    """A chunk in the 64-bit headroom form (amounts < 2^40, balances < 2^61) whose
+    balancing transfers carry one account's figures past +-2^63 raises FL_H64_OVER,
+    applies nothing and is redone in the u128 form, with the oracle's results.  With an
+    amount >= 2^40 in the call the chunk never takes the 64-bit form."""
+    from table import check
+    text = _h64_table(1 << 40 if big_amount else 1)
+    orc = oracle.Oracle(64, 64)
+    try:
+        check(orc, text)
+    finally:
+        orc.close()
+    gpu = _engine()
+    try:
+        check(gpu, text)
+        assert gpu.stats().h64_redos == (0 if big_amount else 1), gpu.stats().h64_redos
+    finally:
+        gpu.close()
+
+
 @pytest.mark.parametrize("order", ["increasing", "random"])
 def test_guarded_fast_path_many_calls(order):
     """Once any balance's high word reaches 2^62 every event takes the guarded

@@ -409,6 +409,7 @@ __global__ void k_set_balances(Tables T, u128 id, Bal4 b, int* status) {
     const u64 lim = 1ull << 62;
     if ((u64)(b.dp >> 64) >= lim || (u64)(b.dpo >> 64) >= lim || (u64)(b.cp >> 64) >= lim || (u64)(b.cpo >> 64) >= lim)
         atomicOr(T.big, 1u);
+    if ((b.dp | b.dpo | b.cp | b.cpo) >> 61) atomicOr(T.big, 2u);
     *status = 0;
 }
 __global__ void k_get_posted(Tables T, u128 id, int* status) {
@@ -511,6 +512,7 @@ __global__ void k_scan_big(Tables T, u64 n) {
     if ((u64)(a.debits_pending >> 64) >= lim || (u64)(a.debits_posted >> 64) >= lim ||
         (u64)(a.credits_pending >> 64) >= lim || (u64)(a.credits_posted >> 64) >= lim)
         atomicOr(T.big, 1u);
+    if ((a.debits_pending | a.debits_posted | a.credits_pending | a.credits_posted) >> 61) atomicOr(T.big, 2u);
 }
 
 }  // namespace

@@ -85,7 +85,8 @@ __device__ __forceinline__ SE load_elem(const SideScanArgs& A, u64 q, u32 invali
     const bool eval_ok = A.sq_ok[q] & 1;
     if (!eval_ok) return e;
     const bool fin = side_final(A, q);
-    const u128 dpe = A.sq_dpend[q], dpo = A.sq_dpost[q];
+    u128 dpe, dpo;
+    side_deltas(A, q, dpe, dpo);
     const bool credit = A.sq_ev[q] >> 31;
     if (fin) {
         if (credit) { e.F.cp = dpe; e.F.cpo = dpo; } else { e.F.dp = dpe; e.F.dpo = dpo; }
@@ -204,13 +205,17 @@ __global__ void bs_final(SideScanArgs A, u64 m, u32 invalid, const Bal4* __restr
         --p;
         if (A.skey[p] != key || (A.sq_cs[p] & SQ_CS) != cs) break;
         if ((A.sq_ok[p] & 1) && !side_final(A, p)) {
-            if (A.sq_ev[p] >> 31) { tot.cp -= A.sq_dpend[p]; tot.cpo -= A.sq_dpost[p]; }
-            else { tot.dp -= A.sq_dpend[p]; tot.dpo -= A.sq_dpost[p]; }
+            u128 dpe, dpo;
+            side_deltas(A, p, dpe, dpo);
+            if (A.sq_ev[p] >> 31) { tot.cp -= dpe; tot.cpo -= dpo; }
+            else { tot.dp -= dpe; tot.dpo -= dpo; }
         }
     }
     if (side_final(A, q)) {
-        if (A.sq_ev[q] >> 31) { tot.cp += A.sq_dpend[q]; tot.cpo += A.sq_dpost[q]; }
-        else { tot.dp += A.sq_dpend[q]; tot.dpo += A.sq_dpost[q]; }
+        u128 dpe, dpo;
+        side_deltas(A, q, dpe, dpo);
+        if (A.sq_ev[q] >> 31) { tot.cp += dpe; tot.cpo += dpo; }
+        else { tot.dp += dpe; tot.dpo += dpo; }
     }
     Account& a = acc[key];
     a.debits_pending = tot.dp;
@@ -221,6 +226,7 @@ __global__ void bs_final(SideScanArgs A, u64 m, u32 invalid, const Bal4* __restr
     if ((u64)(tot.dp >> 64) >= lim || (u64)(tot.dpo >> 64) >= lim || (u64)(tot.cp >> 64) >= lim ||
         (u64)(tot.cpo >> 64) >= lim)
         atomicOr(big, 1u);
+    if ((tot.dp | tot.dpo | tot.cp | tot.cpo) >> 61) atomicOr(big, 2u);  // (the 64-bit headroom passes' guard)
 }
 
 // --------------------------------------------------------- fused scan ----
@@ -316,7 +322,8 @@ __device__ __forceinline__ void side_contrib(const SideScanArgs& A, u64 q, Bal4&
     zero(F);
     zero(H);
     if (!(A.sq_ok[q] & 1)) return;
-    const u128 dpe = A.sq_dpend[q], dpo = A.sq_dpost[q];
+    u128 dpe, dpo;
+    side_deltas(A, q, dpe, dpo);
     const bool fin = (A.probe & 1) ? true : side_final(A, q), credit = A.sq_ev[q] >> 31;
     const u128 pe = credit ? 0 : dpe, po = credit ? 0 : dpo, ce = credit ? dpe : 0, co = credit ? dpo : 0;
     if (fin) { F.dp = pe; F.dpo = po; F.cp = ce; F.cpo = co; }
@@ -537,6 +544,10 @@ __host__ __device__ __forceinline__ u32 resolve_blocks_n(u32 n_complex) {
     return (n_complex + NF_THREADS - 1) / NF_THREADS;
 }
 
+// H64: the 64-bit form (side_scan_fused_h64): the figures and deltas are stored as 64-bit
+// two's complement (exact: FL_WIDE64 clear bounds every headroom of the chunk within
+// +-2^63), read sign-extended and scanned as before.
+template <bool H64>
 __global__ __launch_bounds__(NF_THREADS) void bs_fused_narrow(SideScanArgs A, u64 m, u32 invalid,
                                                               const u32* __restrict__ tstart, u32 ntiles,
                                                               u32* long_flag, const Account* __restrict__ acc) {
@@ -577,9 +588,16 @@ __global__ __launch_bounds__(NF_THREADS) void bs_fused_narrow(SideScanArgs A, u6
         c[k] = in ? A.sq_cs[q] : SQ_STANDALONE;
         ev[k] = in ? A.sq_ev[q] : 0;
         okw[k] = in ? A.sq_ok[q] : 0;
-        dpe[k] = in ? A.sq_dpend[q] : 0;
-        dpo[k] = in ? A.sq_dpost[q] : 0;
-        old[k] = (!all && in) ? A.bh[q] : 0;
+        if (H64) {
+            const ulonglong2 d = in ? ((const ulonglong2*)A.sq_d64)[q] : ulonglong2{0, 0};
+            dpe[k] = sext64(d.x);
+            dpo[k] = sext64(d.y);
+            old[k] = (!all && in) ? sext64(A.bh64[q]) : 0;
+        } else {
+            dpe[k] = in ? A.sq_dpend[q] : 0;
+            dpo[k] = in ? A.sq_dpost[q] : 0;
+            old[k] = (!all && in) ? A.bh[q] : 0;
+        }
     }
     const u32 prev0 = (qa < b0 && qa > a0) ? A.skey[qa - 1] : invalid;
     u32 cf[NF_IPT];
@@ -636,12 +654,13 @@ __global__ __launch_bounds__(NF_THREADS) void bs_fused_narrow(SideScanArgs A, u6
             u128 out = credit ? r_hc[k] : r_hd[k];
             if (!(e[k].fl & 1)) out += credit ? run.hc : run.hd;
             out += h;
+            if (H64 && !fits64(out)) atomicOr(A.over, (u32)FL_H64_OVER);  // the chunk is redone in u128
             if (all) {
-                A.bh[q] = out;
-            } else if (old[k] != out) {
+                if (H64) A.bh64[q] = (u64)out; else A.bh[q] = out;
+            } else if (H64 ? (u64)old[k] != (u64)out : old[k] != out) {
                 // a balance moved: its event is due this pass (with its chain) when this
                 // balance can decide its outcome (SQ_SENS); otherwise only the figure moves
-                A.bh[q] = out;
+                if (H64) A.bh64[q] = (u64)out; else A.bh[q] = out;
                 if ((ev[k] & SQ_SENS) || A.all_sides) {
                     A.dt.ev[par * A.dt.n + (ev[k] & SQ_EV)] = pq;
                     if (!(c[k] & SQ_STANDALONE)) A.dt.chain[par * A.dt.n + (c[k] & SQ_CS)] = pq;
@@ -667,8 +686,17 @@ void side_scan_fused_narrow(const SideScanArgs& A, u64 m, u32 invalid, const u32
                             const Account* acc, hipStream_t stream) {
     if (m == 0) return;
     const u32 ntiles = (u32)((m + BF_TILE - 1) / BF_TILE);
-    bs_fused_narrow<<<resolve_blocks_n(A.n_complex) + ntiles, NF_THREADS, 0, stream>>>(A, m, invalid, tstart, ntiles,
-                                                                                     long_flag, acc);
+    bs_fused_narrow<false><<<resolve_blocks_n(A.n_complex) + ntiles, NF_THREADS, 0, stream>>>(A, m, invalid, tstart,
+                                                                                            ntiles, long_flag, acc);
+    HIP_CHECK(hipGetLastError());
+}
+
+void side_scan_fused_h64(const SideScanArgs& A, u64 m, u32 invalid, const u32* tstart, u32* long_flag,
+                         const Account* acc, hipStream_t stream) {
+    if (m == 0) return;
+    const u32 ntiles = (u32)((m + BF_TILE - 1) / BF_TILE);
+    bs_fused_narrow<true><<<resolve_blocks_n(A.n_complex) + ntiles, NF_THREADS, 0, stream>>>(A, m, invalid, tstart,
+                                                                                           ntiles, long_flag, acc);
     HIP_CHECK(hipGetLastError());
 }
 

@@ -33,8 +33,9 @@ struct Tables {
     // [3] min hi.  An id outside it is absent without a probe (the LSM key-range
     // short-circuit of src/lsm/tree.zig:289-300, why sequential ids are cheap).
     u64* idr;
-    // Set once any balance high word reaches 2^62: until then a call of < 2^32
-    // events with amounts < 2^64 cannot overflow a u128 sum (fast.hip).
+    // Bit 0 set once any balance high word reaches 2^62: until then a call of < 2^32
+    // events with amounts < 2^64 cannot overflow a u128 sum (fast.hip).  Bit 1 once any
+    // balance reaches 2^61 (the general path's 64-bit headroom passes, FL_WIDE64).
     u32* big;
     // Account index occupancy: [0] hash-index entries reserved so far, [1] nonzero once
     // an insert was refused because `hash_limit` (half the slots: load <= 0.5, so every
@@ -194,6 +195,12 @@ struct Sides {
     u8* sq_ok;        // [m] sorted, per pass: the side's effect is evaluated-ok
     u128* sq_dpend;   // [m] sorted, per pass: its delta on the *_pending balance
     u128* sq_dpost;   // [m] sorted, per pass: its delta on the *_posted balance
+    // The compact form of the deltas (a chunk in 64-bit headroom form, FL_WIDE64 clear):
+    // [2m] (pending, posted) per side as 64-bit two's complement, in sq_dpend's memory;
+    // null when the chunk keeps the u128 form.  One form per chunk (the host decides it
+    // before tr_side_rec writes the first records).
+    u64* sq_d64;
+    u32* over;        // the flag word FL_H64_OVER goes to (a compact delta that does not fit)
     u32* tstart;      // [m / tile + 1] first account start in each fused-scan window (NONE32: none)
     uint2* epos;      // [n] sorted positions of each event's first side pair (debit, credit)
     u32 tile;         // the fused scan's window (sides)
@@ -215,6 +222,7 @@ struct SideScanArgs {
     const u8* sq_ok;
     const u128* sq_dpend;
     const u128* sq_dpost;
+    const u64* sq_d64;  // the compact form (Sides::sq_d64), or null
     const u32* cfail; // per-chain first failure of the state scanned
     u32* cfail_clear; // the next state's cfail, reset by the scan (NONE32), or null
     u32 n;            // events (cfail_clear length)
@@ -231,9 +239,27 @@ struct SideScanArgs {
     // headroom passes (side_scan_fused_narrow): the side's one balance figure its
     // evaluation reads, or null (the Bal4 passes)
     u128* bh;
+    u64* bh64;        // the 64-bit headroom passes' figure (side_scan_fused_h64), or null
+    u32* over;        // the flag word FL_H64_OVER goes to (a figure outside +-2^63)
     u32 all_sides;    // headroom passes: a moved balance marks its event whatever SQ_SENS says
                       // (TBGPU_NO_SENS=1, A/B timing)
 };
+
+// A 64-bit two's complement value as the u128 it stands for.
+__device__ __forceinline__ u128 sext64(u64 v) { return (u128)(__int128)(long long)v; }
+__device__ __forceinline__ bool fits64(u128 v) { return sext64((u64)v) == v; }
+
+// Sorted side q's deltas (pending, posted), from whichever form the chunk keeps.
+__device__ __forceinline__ void side_deltas(const SideScanArgs& A, u64 q, u128& dpe, u128& dpo) {
+    if (A.sq_d64) {
+        const ulonglong2 v = ((const ulonglong2*)A.sq_d64)[q];
+        dpe = sext64(v.x);
+        dpo = sext64(v.y);
+    } else {
+        dpe = A.sq_dpend[q];
+        dpo = A.sq_dpost[q];
+    }
+}
 
 // final-ok of a sorted side: evaluated-ok and its chain persisted
 __device__ __forceinline__ bool side_final(const SideScanArgs& A, u64 q) {
@@ -256,6 +282,11 @@ u32 side_scan_fused_tile();
 // debits_posted - credits_pending - credits_posted (a credit side), modulo 2^128, in A.bh.
 void side_scan_fused_narrow(const SideScanArgs& A, u64 m, u32 invalid, const u32* tstart, u32* long_flag,
                             const Account* acc, hipStream_t stream);
+// The same in 64-bit form (FL_WIDE64 clear: every headroom of the chunk lies within
+// +-2^63, so it and every delta are exact as 64-bit two's complement): A.bh64 per side,
+// the deltas from A.sq_d64 -- 8 + 16 bytes per side where the u128 form moves 16 + 32.
+void side_scan_fused_h64(const SideScanArgs& A, u64 m, u32 invalid, const u32* tstart, u32* long_flag,
+                         const Account* acc, hipStream_t stream);
 void side_final_balances(const SideScanArgs& A, u64 m, u32 invalid, const Bal4* bb, Account* acc, u32* big,
                          hipStream_t stream);
 
@@ -466,4 +497,22 @@ enum {
     FL_WIDE = 1u << 14,       // general path: an amount >= 2^64 or a balance near 2^128 (no headroom passes)
     FL_FOREIGN = 1u << 13,    // ledger shard: a transfer on a ledger another shard owns reached its balances
     FL_AC_HASHED = 1u << 15,  // create_accounts' clean call: some id is outside the direct-mapped directory
+    FL_WIDE64 = 1u << 16,     // general path: an amount >= 2^40 or a balance >= 2^61 (no 64-bit headroom passes)
+    FL_H64_OVER = 1u << 17,   // general path: a headroom or delta of a 64-bit-form chunk left +-2^63 (redo it in u128)
 };
+
+// Sorted side q's deltas written in the chunk's form (SideScanArgs side_deltas reads them).
+// `check`: whether a delta that does not fit raises FL_H64_OVER -- every evaluation's
+// record (the headroom passes' amounts fit while their figures do; the walk reads full
+// balances).  The initial state's records are not checked: a balancing transfer of
+// amount 0 starts at maxInt(u64), which every 64-bit-form pass 0 replaces (its amount is
+// clamped to a headroom within +-2^63) and rewrites.
+__device__ __forceinline__ void side_deltas_put(const Sides& sd, u64 q, u128 dpe, u128 dpo, bool check = true) {
+    if (sd.sq_d64) {
+        if (check && (!fits64(dpe) || !fits64(dpo))) atomicOr(sd.over, (u32)FL_H64_OVER);
+        ((ulonglong2*)sd.sq_d64)[q] = ulonglong2{(unsigned long long)(u64)dpe, (unsigned long long)(u64)dpo};
+    } else {
+        sd.sq_dpend[q] = dpe;
+        sd.sq_dpost[q] = dpo;
+    }
+}

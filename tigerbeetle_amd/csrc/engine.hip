@@ -294,6 +294,7 @@ struct tbgpu_ctx {
     u32 *d_ev, *d_chain, *d_slot, *d_win;  // the passes' dirty stamps (engine.h Dirty)
     Bal4* bb = nullptr;
     u128* bh = nullptr;  // headroom passes: one balance figure per side (balances.hip)
+    u64* sd64 = nullptr; // the current chunk's compact side deltas (Sides::sq_d64), or null
     SortScratch ss{};
     void* side_tiles = nullptr;
     Scan3Scratch sc{};
@@ -1181,7 +1182,7 @@ static void walk(tbgpu_ctx* c, const TrArgs& C, u32 n, EvalState& D, const u32* 
         HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)one, 1, 1, s));
         SideScanArgs SA{};
         SA.skey = c->skey_s; SA.sq_ev = c->sq_ev; SA.sq_cs = c->sq_cs; SA.sq_ok = c->sq_ok;
-        SA.sq_dpend = c->sq_dpend; SA.sq_dpost = c->sq_dpost; SA.n = n;
+        SA.sq_dpend = c->sq_dpend; SA.sq_dpost = c->sq_dpost; SA.sq_d64 = c->sd64; SA.n = n;
         SA.cfail = D.cfail;
         SA.cfail_clear = nullptr;
         SA.gate = PassGate{one, c->counters + CNT_RESORT, 0, 1};
@@ -1216,8 +1217,11 @@ static void walk(tbgpu_ctx* c, const TrArgs& C, u32 n, EvalState& D, const u32* 
 // the group converges they run right behind it instead of after the round trip.
 // Returns the converged state.
 template <typename Epi>
-static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilogue) {
+static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C0, u32 n, Epi&& epilogue, bool allow_h64 = true) {
     hipStream_t s = c->stream;
+    TrArgs C = C0;  // (its side deltas' form is decided below, once classify's flags are back)
+    C.sd.sq_d64 = nullptr;
+    c->sd64 = nullptr;
     const u64 g = C.gmask + 1;
     const u32 inv_acc = (u32)c->accounts_max;  // side keys are account rows
     const int bits_acc = log2u(c->accounts_max + 1);
@@ -1249,7 +1253,7 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
     HIP_CHECK(hipMemcpyAsync(c->h_base + 7, c->counters + CNT_FLAGS, sizeof(u32), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipEventRecord(c->ev_lists, s));
 
-    auto build_sides = [&](const EvalState& S) {
+    auto build_sides = [&](const EvalState& S, bool records = true) {
         prof_mark(c, PH_SORT);
         for (u32 kmax : {SIDE_CANDS, 1u}) {
             if (!counted) count_sides(kmax);
@@ -1266,10 +1270,10 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
         if (m > c->scap) tbgpu_fatal("create_transfers", "side capacity", __FILE__, __LINE__);
         radix_sort_pairs(c->skey, c->sval, c->skey_s, c->sval_s, m, bits_acc, c->ss, s);
         tr_launch_side_pos(C, c->sval_s, m, s);
-        tr_launch_side_rec(C, S, s);
+        if (records) tr_launch_side_rec(C, S, s);
         c->stats.sorts++;
     };
-    build_sides(c->st[0]);
+    build_sides(c->st[0], false);  // (its side records once the deltas' form is known)
     wait_event(c->ev_lists);  // (long landed: the sort is queued behind it)
     memcpy(n_list, c->h_base + 6, sizeof n_list);
     u32 cflags = 0;
@@ -1279,10 +1283,28 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
     // one full scan behind the converged group, for the apply kernels.
     static const bool no_narrow = getenv("TBGPU_NO_HEADROOM") != nullptr;  // A/B timing
     const bool narrow = !(cflags & FL_WIDE) && !no_narrow;
+    // ... in 64-bit form when every amount is < 2^40, every committed balance < 2^61
+    // (FL_WIDE64 clear) and the chunk has at most 2^20 events: every headroom of the
+    // chunk then lies within +-2^63 (the committed ones within +-2^62, and the chunk moves
+    // one by less than 2^20 * 2^40; a balancing amount never exceeds the headroom it
+    // draws on), so the figures and the side deltas are exact as 64-bit two's
+    // complement, and a pass moves half the bytes per side.
+    static const bool no_h64 = getenv("TBGPU_NO_H64") != nullptr;  // A/B timing
+    // A figure can still leave +-2^63 when balancing transfers pile several accounts'
+    // headroom onto one: the scan (or a Bal4 pass's delta) raises FL_H64_OVER, the group
+    // applies nothing, and the chunk is redone from its start in the u128 form.
+    const bool h64 = allow_h64 && narrow && !c->long_segments && !(cflags & FL_WIDE64) && n <= (1u << 20) && !no_h64;
+    if (h64) {
+        c->sd64 = (u64*)c->sq_dpend;  // [2m] u64 in the u128 array's memory
+        C.sd.sq_d64 = c->sd64;
+        C.sd.over = c->counters + CNT_FLAGS;
+    }
+    tr_launch_side_rec(C, c->st[0], s);
 
     SideScanArgs SA{};
     SA.skey = c->skey_s; SA.sq_ev = c->sq_ev; SA.sq_cs = c->sq_cs; SA.sq_ok = c->sq_ok;
-    SA.sq_dpend = c->sq_dpend; SA.sq_dpost = c->sq_dpost; SA.n = n;
+    SA.sq_dpend = c->sq_dpend; SA.sq_dpost = c->sq_dpost; SA.sq_d64 = c->sd64; SA.n = n;
+    SA.over = c->counters + CNT_FLAGS;
     SA.dt = C.dt;
     SA.lst_complex = c->lst_complex;
     SA.gslot = c->gslot; SA.pslot = c->pslot; SA.cs = c->cs; SA.ce = c->ce;
@@ -1311,15 +1333,20 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
             SA.gate = G;
             const bool hr = narrow && !c->long_segments;
             TrArgs CE = C;
-            CE.bh = hr ? c->bh : nullptr;
+            CE.bh = hr && !h64 ? c->bh : nullptr;
+            CE.bh64 = hr && h64 ? (const u64*)c->bh : nullptr;
             if (c->long_segments) {
                 side_scan(SA, m, inv_acc, chains, c->side_tiles, c->T.acc, c->bb, s);
             } else if (hr) {
                 SideScanArgs SN = SA;
                 SN.bh = c->bh;
+                SN.bh64 = (u64*)c->bh;
                 static const bool no_sens = getenv("TBGPU_NO_SENS") != nullptr;  // A/B timing
                 SN.all_sides = no_sens ? 1u : 0u;
-                side_scan_fused_narrow(SN, m, inv_acc, c->tstart, c->counters + CNT_LONG, c->T.acc, s);
+                if (h64)
+                    side_scan_fused_h64(SN, m, inv_acc, c->tstart, c->counters + CNT_LONG, c->T.acc, s);
+                else
+                    side_scan_fused_narrow(SN, m, inv_acc, c->tstart, c->counters + CNT_LONG, c->T.acc, s);
             } else {
                 side_scan_fused(SA, m, inv_acc, c->tstart, c->counters + CNT_LONG, c->T.acc, c->bb, s);
             }
@@ -1352,6 +1379,10 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
         epilogue(m);
         prof_mark(c, PH_END);
         wait_event(c->ev_group);
+        if (c->h_counters[CNT_FLAGS] & FL_H64_OVER) {
+            c->stats.h64_redos++;
+            return fixed_point(c, C0, n, epilogue, false);
+        }
         if (c->h_counters[CNT_FLAGS] & FL_FOREIGN)
             tbgpu_fatal("create_transfers", "a transfer of a ledger another shard owns (ledger shard ctx)", __FILE__,
                         __LINE__);
@@ -1366,6 +1397,12 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
                     c->h_counters[CNT_RESORT]);
         }
         const u32 lng = c->h_counters[CNT_LONG];
+        if (lng && h64) {
+            // the three-launch Bal4 scan from here on reads full balances, which the
+            // 64-bit records need not hold: the chunk again, in the u128 form
+            c->long_segments = true;
+            return fixed_point(c, C0, n, epilogue, false);
+        }
         if (lng) {
             // pass r's fused scan met an account segment longer than its window: redo
             // it, and the rest of the call, with the three-launch scan
@@ -1395,6 +1432,15 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C, u32 n, Epi&& epilog
         if (p >= budget) {
             // past the pass budget: the last pass (p - 1) wrote st[p & 1]; walk on from its front
             walk(c, C, n, c->st[p & 1], c->pc + PC_RING + p % PC_RING, m, build_sides);
+            if (h64) {  // the walk's Bal4 deltas of a 64-bit-form chunk
+                HIP_CHECK(hipMemcpyAsync(c->h_counters + CNT_FLAGS, c->counters + CNT_FLAGS, sizeof(u32),
+                                         hipMemcpyDeviceToHost, s));
+                wait_stream(s);
+                if (c->h_counters[CNT_FLAGS] & FL_H64_OVER) {
+                    c->stats.h64_redos++;
+                    return fixed_point(c, C0, n, epilogue, false);
+                }
+            }
             HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)(c->counters + EPI_WORD), (p & 1) ? 2 : 1, 1, s));
             epilogue(m);
             c->stats.iterations = p;
@@ -1511,7 +1557,7 @@ static bool run_transfers_chunk(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb,
         if (!c->rt_dry) {
             SideScanArgs SA{};
             SA.skey = c->skey_s; SA.sq_ev = c->sq_ev; SA.sq_cs = c->sq_cs; SA.sq_ok = c->sq_ok;
-            SA.sq_dpend = c->sq_dpend; SA.sq_dpost = c->sq_dpost; SA.n = n;
+            SA.sq_dpend = c->sq_dpend; SA.sq_dpost = c->sq_dpost; SA.sq_d64 = c->sd64; SA.n = n;
             SA.cfail = c->st[0].cfail;
             SA.cfail_alt = c->st[1].cfail;
             SA.epi = C.epi;

@@ -186,7 +186,7 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
                                           u64 row_base, u32* dslot_out, u32* cslot_out, u64* xend) {
     const u16 f = t.flags;
     *xend = xidx_hash(t.id) & T.xidx_mask;  // (the guarded form's claims start at the id's slot)
-    if (f & (TF_BDR | TF_BCR | TF_POST | TF_VOID) || *T.big)
+    if (f & (TF_BDR | TF_BCR | TF_POST | TF_VOID) || (*T.big & 1))
         return fp_classify_guarded(T, F, t, i, ts, row_base, dslot_out, cslot_out);
     // speculative first-slot reads (hash tables at load <= 0.5: usually the hit).
     // The 32-byte account index entries carry ledger and flags, so the rows
@@ -694,6 +694,7 @@ __device__ __forceinline__ void fp_commit_body(const Tables& T, FastArgs F, cons
     for (int k = 0; k < PER; k++) {
         if (!wp[k]) continue;
         const u64 c = (u64)cv[k] + (old[k] + av[k] < old[k] ? 1 : 0);
+        if (!(old[k] >> 61) && ((old[k] + av[k]) >> 61 || c)) atomicOr(T.big, 2u);  // crossed 2^61
         if (c) {
             const u64 hi = atomicAdd((unsigned long long*)&wp[k][1], (unsigned long long)c);
             if (hi + c >= (1ull << 62)) atomicOr(T.big, 1u);  // later calls must prove no overflow
@@ -842,6 +843,7 @@ __device__ __forceinline__ bool fp_linked(const FastArgs& F, u32 j) {
 __device__ __forceinline__ void add_u128_small(const Tables& T, u128* p, u64 a) {
     u64* w = (u64*)p;
     const u64 old = atomicAdd((unsigned long long*)&w[0], (unsigned long long)a);
+    if (!(old >> 61) && ((old + a) >> 61 || old + a < old)) atomicOr(T.big, 2u);  // crossed 2^61
     if (old + a < old) {
         const u64 hi = atomicAdd((unsigned long long*)&w[1], 1ull);
         if (hi + 1 >= (1ull << 62)) atomicOr(T.big, 1u);

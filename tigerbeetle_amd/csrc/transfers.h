@@ -64,6 +64,7 @@ struct TrArgs {
     u32* lst_complex;
     Dirty dt;             // dirty tracking of the passes (engine.h)
     const u128* bh;       // headroom passes: the side's balance figure (balances.hip), or null (Bal4)
+    const u64* bh64;      // 64-bit headroom passes (side_scan_fused_h64): the same figure, or null
     u32 debug;            // diagnostics: count changed events by kind (TBGPU_TRACE_PASSES)
     u32 sparse;           // a pass whose previous pass changed fewer than n >> sparse events checks
                           // each event's due stamp before issuing its loads (0: never)

@@ -200,9 +200,11 @@ __device__ __forceinline__ u32 classify_one(const Tables& T, const TrArgs& C, u3
             pre_e = xidx_probe(T, t.id);
             pre_p = xidx_probe(T, t.pending_id);
             if ((u64)(t.amount >> 64) != 0) fl |= FL_WIDE;
+            if (t.amount >> 40) fl |= FL_WIDE64;
             if (pre_p != NONE32) {
                 const Transfer& p = T.xrows[pre_p];
                 if ((u64)(p.amount >> 64) != 0) fl |= FL_WIDE;
+                if (p.amount >> 40) fl |= FL_WIDE64;
                 u32 lg;
                 u16 af;
                 ppd = acc_find(T, p.debit_account_id, &lg, &af);
@@ -250,6 +252,7 @@ __device__ __forceinline__ u32 classify_one(const Tables& T, const TrArgs& C, u3
             if (f & (TF_BDR | TF_BCR)) fl |= FL_BALANCING;
             if (f & TF_PENDING) fl |= FL_PENDING;
             if ((u64)(t.amount >> 64) != 0) fl |= FL_WIDE;
+            if (t.amount >> 40) fl |= FL_WIDE64;
             if ((dfl | cfl) & (AF_DNEC | AF_CNED)) fl |= FL_LIMITS;
             if ((dfl | cfl) & AF_HISTORY) fl |= FL_HISTORY;
         }
@@ -284,7 +287,8 @@ __device__ __forceinline__ u32 classify_one(const Tables& T, const TrArgs& C, u3
 __global__ void tr_classify(Tables T, TrArgs C) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     u32 fl = block_or(i < C.n ? classify_one(T, C, i) : 0u);
-    if (i == 0 && *T.big) fl |= FL_WIDE;  // a committed balance near 2^128
+    if (i == 0 && (*T.big & 1)) fl |= FL_WIDE;    // a committed balance near 2^128
+    if (i == 0 && (*T.big & 2)) fl |= FL_WIDE64;  // a committed balance >= 2^61
     if (threadIdx.x == 0 && fl) atomicOr(&C.counters[CNT_FLAGS], fl);
 }
 
@@ -588,7 +592,8 @@ __device__ __forceinline__ bool fin_ok(const TrArgs& C, const EvalState& S, u32 
 // (everything before it is final: each event depends only on earlier ones).  An
 // accepted post/void whose balance effect sits under the wrong side keys (its
 // pending resolved to an event with other accounts) asks the host to re-sort.
-__device__ __forceinline__ bool write_sides(const TrArgs& C, u32 i, bool pv, bool ok, u32 pref, u128 dpe, u128 dpo);
+__device__ __forceinline__ bool write_sides(const TrArgs& C, u32 i, bool pv, bool ok, u32 pref, u128 dpe, u128 dpo,
+                                            bool check = true);
 
 // A sparse pass (tr_eval_lists: few events changed in the previous one) checks the
 // event's due stamps before anything else, so that an event that is not due costs one
@@ -636,7 +641,10 @@ __device__ __forceinline__ bool evaluate_one(const Tables& T, const TrArgs& C, c
     if ((C.probe & 1) && (k.flags & (TF_POST | TF_VOID))) return false;
     Bal4 bd, bc;
     u128 hd = 0, hc = 0;
-    if (C.bh) {
+    if (C.bh64) {
+        hd = sext64(C.bh64[ep.x]);
+        hc = sext64(C.bh64[ep.y]);
+    } else if (C.bh) {
         hd = C.bh[ep.x];
         hc = C.bh[ep.y];
     } else {
@@ -665,7 +673,7 @@ __device__ __forceinline__ bool evaluate_one(const Tables& T, const TrArgs& C, c
                 res = TBGPU_CREATE_TRANSFER_LINKED_EVENT_FAILED;
             } else {
                 u128 amount = 0;
-                res = C.bh ? eval_balances_narrow(k, hd, hc, &amount) : eval_balances(k, bd, bc, &amount);
+                res = (C.bh || C.bh64) ? eval_balances_narrow(k, hd, hc, &amount) : eval_balances(k, bd, bc, &amount);
                 if (res == TBGPU_CREATE_TRANSFER_OK) {
                     amt = amount;
                     if (k.flags & TF_PENDING) dpe = amount; else dpo = amount;
@@ -936,7 +944,9 @@ __device__ __forceinline__ bool eval_simple_one(const TrArgs& C, const EvalState
     }
     u128 amount = 0;
     u8 res;
-    if (C.bh) {
+    if (C.bh64) {
+        res = eval_balances_narrow(e, sext64(C.bh64[ep.x]), sext64(C.bh64[ep.y]), &amount);
+    } else if (C.bh) {
         res = eval_balances_narrow(e, C.bh[ep.x], C.bh[ep.y], &amount);
     } else {
         const Bal4 bd = bb[ep.x], bc = bb[ep.y];
@@ -956,8 +966,8 @@ __device__ __forceinline__ bool eval_simple_one(const TrArgs& C, const EvalState
     if (changed) {
         const u128 dpe = ok && (e.flags & TF_PENDING) ? amt : 0, dpo = ok && !(e.flags & TF_PENDING) ? amt : 0;
         C.sd.sq_ok[ep.x] = C.sd.sq_ok[ep.y] = ok ? 1 : 0;
-        C.sd.sq_dpend[ep.x] = C.sd.sq_dpend[ep.y] = dpe;
-        C.sd.sq_dpost[ep.x] = C.sd.sq_dpost[ep.y] = dpo;
+        side_deltas_put(C.sd, ep.x, dpe, dpo);
+        side_deltas_put(C.sd, ep.y, dpe, dpo);
         mark_changed(C, i, q);
     }
     return changed;
@@ -1256,12 +1266,13 @@ __global__ void tr_side_pos(TrArgs C, const u32* sval_s, u64 m) {
 // Write event i's side records (sorted order) for its outcome: the debit and credit
 // sides of a transfer, or of the candidate pair of a post/void that it resolved to.
 // Returns false when an accepted post/void's pending is not among its candidates.
-__device__ __forceinline__ bool write_sides(const TrArgs& C, u32 i, bool pv, bool ok, u32 pref, u128 dpe, u128 dpo) {
+__device__ __forceinline__ bool write_sides(const TrArgs& C, u32 i, bool pv, bool ok, u32 pref, u128 dpe, u128 dpo,
+                                            bool check) {
     if (!pv) {  // one side pair
         const uint2 ep = C.sd.epos[i];
         C.sd.sq_ok[ep.x] = C.sd.sq_ok[ep.y] = ok ? 1 : 0;
-        C.sd.sq_dpend[ep.x] = C.sd.sq_dpend[ep.y] = ok ? dpe : 0;
-        C.sd.sq_dpost[ep.x] = C.sd.sq_dpost[ep.y] = ok ? dpo : 0;
+        side_deltas_put(C.sd, ep.x, ok ? dpe : 0, ok ? dpo : 0, check);
+        side_deltas_put(C.sd, ep.y, ok ? dpe : 0, ok ? dpo : 0, check);
         return true;
     }
     const u32 s0 = C.sd.soff[i], s1 = C.sd.soff[i + 1];
@@ -1271,8 +1282,8 @@ __device__ __forceinline__ bool write_sides(const TrArgs& C, u32 i, bool pv, boo
         found |= pv && act;
         const u32 q0 = C.sd.spos[s], q1 = C.sd.spos[s + 1];
         C.sd.sq_ok[q0] = C.sd.sq_ok[q1] = act ? 1 : 0;
-        C.sd.sq_dpend[q0] = C.sd.sq_dpend[q1] = act ? dpe : 0;
-        C.sd.sq_dpost[q0] = C.sd.sq_dpost[q1] = act ? dpo : 0;
+        side_deltas_put(C.sd, q0, act ? dpe : 0, act ? dpo : 0, check);
+        side_deltas_put(C.sd, q1, act ? dpe : 0, act ? dpo : 0, check);
     }
     return found;
 }
@@ -1282,7 +1293,7 @@ __global__ void tr_side_rec(TrArgs C, EvalState S) {
     if (i >= C.n) return;
     u128 dpe, dpo;
     state_deltas(C, S, i, &dpe, &dpo);
-    write_sides(C, i, is_post_void(C, i), S.ok[i] & 1, S.pref[i], dpe, dpo);
+    write_sides(C, i, is_post_void(C, i), S.ok[i] & 1, S.pref[i], dpe, dpo, /*check=*/false);
 }
 
 // ---------------------------------------------------------------- apply ----
@@ -1501,8 +1512,7 @@ __global__ void tr_walk_prep(TrArgs C, u64 m, u32 start, u32* sstart, u32* cfail
         const u32 ev = C.sd.sq_ev[q] & SQ_EV;
         if (ev >= start) {
             C.sd.sq_ok[q] = 0;
-            C.sd.sq_dpend[q] = 0;
-            C.sd.sq_dpost[q] = 0;
+            side_deltas_put(C.sd, q, 0, 0);
         }
         const u32 key = C.sd.skey_s[q];
         u64 lo = 0, hi = q;  // first position with this key
@@ -1842,7 +1852,8 @@ namespace {
 __global__ void tr_converged(const u32* ring, u32 ring_len, u32 p0, u32 p1, const u32* counters, u32* epi) {
     if (threadIdx.x != 0) return;
     u32 e = 0;
-    if (counters[CNT_RESORT] == 0 && counters[CNT_LONG] == 0)
+    // (a 64-bit-form chunk whose figures left +-2^63 applies nothing: the host redoes it)
+    if (counters[CNT_RESORT] == 0 && counters[CNT_LONG] == 0 && !(counters[CNT_FLAGS] & FL_H64_OVER))
         for (u32 q = p0; q < p1; q++)
             if (ring[(q + 1) % ring_len] == 0) {
                 e = 1 + ((q + 1) & 1);

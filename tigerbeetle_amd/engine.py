@@ -42,7 +42,8 @@ class Options(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [("events", ctypes.c_uint64), ("iterations", ctypes.c_uint32), ("path", ctypes.c_uint32),
                 ("sorts", ctypes.c_uint64), ("device_ms", ctypes.c_double), ("phase_ms", ctypes.c_double * 8),
-                ("walks", ctypes.c_uint64), ("index_rebuilds", ctypes.c_uint64)]
+                ("walks", ctypes.c_uint64), ("index_rebuilds", ctypes.c_uint64),
+                ("h64_redos", ctypes.c_uint64)]
 
 PHASES = ("upload", "classify", "sort", "scan", "evaluate", "apply", "index", "prep")
 

@@ -49,7 +49,8 @@ constexpr u32 FP_SMALL_TILE = 64;
 // calls of at most FP_TAIL_MAX events run fp_launch_tail (one workgroup) instead of
 // fp_launch_index + fp_launch_fix + fp_launch_advance
 constexpr u32 FP_TAIL_THREADS = 1024, FP_TAIL_MAX = 16384;
-enum { ABL_DUP = 1, ABL_BALANCES = 2, ABL_ROWS = 4, ABL_LOOKBACK = 8, ABL_EVENT = 16, ABL_PROBE = 32, ABL_IDS = 64 };
+enum { ABL_DUP = 1, ABL_BALANCES = 2, ABL_ROWS = 4, ABL_LOOKBACK = 8, ABL_EVENT = 16, ABL_PROBE = 32, ABL_IDS = 64,
+       ABL_XREAD = 128, ABL_CLAIM_STORE = 256 };
 // Timing-only ablations exist only in variant builds (build.build_variant with
 // FP_ABLATE=<mask>, profiles/ablate.py): the product library compiles them out, so no
 // environment setting can make it skip work.

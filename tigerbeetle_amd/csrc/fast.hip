@@ -204,7 +204,7 @@ __device__ __forceinline__ u8 fp_classify(const Tables& T, const FastArgs& F, co
         if (dd) EA = T.dense[dense_slot(T, t.debit_account_id)]; else A = T.aidx[hd];
         if (dc) EB = T.dense[dense_slot(T, t.credit_account_id)]; else B = T.aidx[hc];
     }
-    const bool maybe = !(FP_ABLATE & ABL_IDS) && xidx_maybe_present(T, t.id);  // (ABL_IDS: timing only)
+    const bool maybe = !(FP_ABLATE & (ABL_IDS | ABL_XREAD)) && xidx_maybe_present(T, t.id);  // (ABL_*: timing only)
     const u64 hx = xidx_hash(t.id) & T.xidx_mask;
     const u64 x_r1 = maybe ? T.xidx[hx] : 0ull;
     if (t.timestamp != 0) return TBGPU_CREATE_TRANSFER_TIMESTAMP_MUST_BE_ZERO;
@@ -548,7 +548,12 @@ __device__ __forceinline__ void fp_commit_body(const Tables& T, FastArgs F, cons
         own_ok = r == TBGPU_CREATE_TRANSFER_OK;
         if (F.eager) {
             u32 slot = NONE32;
-            if (own_ok && !(FP_ABLATE & ABL_IDS) && fp_claim_is_dup(T, F, t.id, row_base, i, xend, &slot)) {
+            if (FP_ABLATE & ABL_CLAIM_STORE) {  // timing only: the claim as a plain store, no repeat check
+                if (own_ok) {
+                    T.xidx[xend] = xidx_slot(t.id, (u32)(row_base + i));
+                    slot = (u32)xend;
+                }
+            } else if (own_ok && !(FP_ABLATE & ABL_IDS) && fp_claim_is_dup(T, F, t.id, row_base, i, xend, &slot)) {
                 r = FRES_SLOW;  // an id repeated within the call: the fixed point decides it
                 own_ok = false;
             }

@@ -7,7 +7,7 @@ timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method threa
     tests/test_gpu_parity.py tests/test_gpu_general.py tests/test_gpu_golden.py tests/test_gpu_fuzz.py \
     > $OUT/tests.txt 2>&1
 A="--config 3 --steps 5 --warmup 1 --no-cpu --no-queries --no-host"
-for r in 1 2 3; do
+for r in 1; do
   for v in on off; do
     if [ $v = off ]; then export TBGPU_NO_H64=1; else unset TBGPU_NO_H64; fi
     timeout -k 10 200 python bench.py $A > $OUT/c3_${v}_$r.json 2> $OUT/c3_${v}_$r.err

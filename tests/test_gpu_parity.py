@@ -201,6 +201,14 @@ def test_h64_headroom_overflow_redoes_the_chunk(big_amount):
         gpu.close()
 
 
+def test_h64_long_segments_keep_the_form():
+    """Zipf-hot accounts on the general path: their segments outgrow the fused scan's
+    window, so the passes switch to the three-launch Bal4 scan, which reads the chunk's
+    64-bit delta records (no redo: no balance nears 2^62)."""
+    st = _parity(workload.config2(transfer_count=100_000, account_count=20_000, seed=5), force_general=True)
+    assert st.h64_redos == 0, st.h64_redos
+
+
 @pytest.mark.parametrize("order", ["increasing", "random"])
 def test_guarded_fast_path_many_calls(order):
     """Once any balance's high word reaches 2^62 every event takes the guarded

@@ -178,6 +178,10 @@ __global__ __launch_bounds__(BS_THREADS) void bs_down(SideScanArgs A, u64 m, u32
             out.cpo = a.credits_posted;
             if (!(e.fl & 1)) out = add(out, run.F);
             if (HAS_H && !(e.fl & 2)) out = add(out, run.H);
+            // a 64-bit-form chunk's Bal4 passes (a long segment, the walk): a balance past
+            // 2^62 could give a headroom, or a balancing amount, past what its 64-bit
+            // records hold -- the chunk is redone in the u128 form
+            if (A.over && ((out.dp | out.dpo | out.cp | out.cpo) >> 62)) atomicOr(A.over, (u32)FL_H64_OVER);
             bb[q] = out;
         }
         run = combine<HAS_H>(run, e);

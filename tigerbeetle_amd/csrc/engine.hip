@@ -1183,6 +1183,7 @@ static void walk(tbgpu_ctx* c, const TrArgs& C, u32 n, EvalState& D, const u32* 
         SideScanArgs SA{};
         SA.skey = c->skey_s; SA.sq_ev = c->sq_ev; SA.sq_cs = c->sq_cs; SA.sq_ok = c->sq_ok;
         SA.sq_dpend = c->sq_dpend; SA.sq_dpost = c->sq_dpost; SA.sq_d64 = c->sd64; SA.n = n;
+        SA.over = c->sd64 ? c->counters + CNT_FLAGS : nullptr;  // (the walk's Bal4 scans of a 64-bit-form chunk)
         SA.cfail = D.cfail;
         SA.cfail_clear = nullptr;
         SA.gate = PassGate{one, c->counters + CNT_RESORT, 0, 1};
@@ -1291,8 +1292,9 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C0, u32 n, Epi&& epilo
     // complement, and a pass moves half the bytes per side.
     static const bool no_h64 = getenv("TBGPU_NO_H64") != nullptr;  // A/B timing
     // A figure can still leave +-2^63 when balancing transfers pile several accounts'
-    // headroom onto one: the scan (or a Bal4 pass's delta) raises FL_H64_OVER, the group
-    // applies nothing, and the chunk is redone from its start in the u128 form.
+    // headroom onto one: the scan (a Bal4 pass of a long segment or the walk: a balance
+    // past 2^62, or a delta that does not fit) raises FL_H64_OVER, the group applies
+    // nothing, and the chunk is redone from its start in the u128 form.
     const bool h64 = allow_h64 && narrow && !c->long_segments && !(cflags & FL_WIDE64) && n <= (1u << 20) && !no_h64;
     if (h64) {
         c->sd64 = (u64*)c->sq_dpend;  // [2m] u64 in the u128 array's memory
@@ -1304,7 +1306,7 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C0, u32 n, Epi&& epilo
     SideScanArgs SA{};
     SA.skey = c->skey_s; SA.sq_ev = c->sq_ev; SA.sq_cs = c->sq_cs; SA.sq_ok = c->sq_ok;
     SA.sq_dpend = c->sq_dpend; SA.sq_dpost = c->sq_dpost; SA.sq_d64 = c->sd64; SA.n = n;
-    SA.over = c->counters + CNT_FLAGS;
+    SA.over = h64 ? c->counters + CNT_FLAGS : nullptr;
     SA.dt = C.dt;
     SA.lst_complex = c->lst_complex;
     SA.gslot = c->gslot; SA.pslot = c->pslot; SA.cs = c->cs; SA.ce = c->ce;
@@ -1397,12 +1399,6 @@ static EvalState* fixed_point(tbgpu_ctx* c, const TrArgs& C0, u32 n, Epi&& epilo
                     c->h_counters[CNT_RESORT]);
         }
         const u32 lng = c->h_counters[CNT_LONG];
-        if (lng && h64) {
-            // the three-launch Bal4 scan from here on reads full balances, which the
-            // 64-bit records need not hold: the chunk again, in the u128 form
-            c->long_segments = true;
-            return fixed_point(c, C0, n, epilogue, false);
-        }
         if (lng) {
             // pass r's fused scan met an account segment longer than its window: redo
             // it, and the rest of the call, with the three-launch scan

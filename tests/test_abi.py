@@ -2,6 +2,8 @@
 import ctypes
 import re
 
+import pytest
+
 from tigerbeetle_amd import engine
 from tigerbeetle_amd.types import ACCOUNT_DTYPE, HISTORY_DTYPE, TRANSFER_DTYPE
 
@@ -99,22 +101,25 @@ def test_init_without_gpu_fails_loudly():
         engine.Engine()
 
 
-def test_stats_struct_matches_the_python_mirror(tmp_path):
-    """tbgpu_stats as the C compiler lays it out (include/tbgpu.h) against engine.Stats,
-    the ctypes mirror the Python host reads it through: size and every field's offset."""
+@pytest.mark.parametrize("ctype,mirror", [("tbgpu_stats", "Stats"), ("tbgpu_options", "Options")])
+def test_structs_match_the_python_mirrors(tmp_path, ctype, mirror):
+    """tbgpu_stats / tbgpu_options as the C compiler lays them out (include/tbgpu.h)
+    against the ctypes mirrors the Python host passes and reads: size and every field's
+    offset."""
     import os
     import subprocess
-    fields = [name for name, _ in engine.Stats._fields_]
+    M = getattr(engine, mirror)
+    fields = [name for name, _ in M._fields_]
     src = tmp_path / "stats.c"
     src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "tbgpu.h"\nint main(void) {\n'
-                   '    printf("size %zu\\n", sizeof(tbgpu_stats));\n'
-                   + "".join(f'    printf("{f} %zu\\n", offsetof(tbgpu_stats, {f}));\n' for f in fields)
+                   f'    printf("size %zu\\n", sizeof({ctype}));\n'
+                   + "".join(f'    printf("{f} %zu\\n", offsetof({ctype}, {f}));\n' for f in fields)
                    + "    return 0;\n}\n")
     exe = tmp_path / "stats"
     inc = os.path.join(os.path.dirname(engine.HEADER))
     subprocess.run(["gcc", "-std=c11", "-I", inc, str(src), "-o", str(exe)], check=True)
     out = dict(line.split() for line in subprocess.run([str(exe)], check=True, capture_output=True,
                                                        text=True).stdout.splitlines())
-    assert int(out["size"]) == ctypes.sizeof(engine.Stats)
+    assert int(out["size"]) == ctypes.sizeof(M)
     for f in fields:
-        assert int(out[f]) == getattr(engine.Stats, f).offset, f
+        assert int(out[f]) == getattr(M, f).offset, f

@@ -74,7 +74,7 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def pmc_traffic(config: int, accounts: int, kernel=None, id_order: str = "sequential"):
+def pmc_traffic(config: int, accounts: int, kernel=None, id_order: str = "sequential", routed: bool = False):
     """HBM bytes per launch from the newest committed rocprofv3 PMC summary of THIS
     workload (profiles/rNN/traffic*.json, written by profiles/collect.sh +
     summarize.py on the same bench command and tagged with its config and account
@@ -90,7 +90,7 @@ def pmc_traffic(config: int, accounts: int, kernel=None, id_order: str = "sequen
         except (OSError, KeyError, ValueError, TypeError):
             continue
         if meta.get("config") != config or meta.get("accounts") != accounts or \
-                meta.get("id_order", "sequential") != id_order:
+                meta.get("id_order", "sequential") != id_order or bool(meta.get("routed", False)) != routed:
             continue
         rel = os.path.relpath(f, ROOT)
         ev = meta["events_per_step"]
@@ -103,8 +103,8 @@ def pmc_traffic(config: int, accounts: int, kernel=None, id_order: str = "sequen
         else:
             continue
         return round(per), f"{rel}: 2xFETCH_SIZE+WRITE_SIZE, {what} ({per / ev:.1f} B/transfer)"
-    return None, (f"no rocprofv3 PMC summary of config {config} with {accounts} accounts"
-                  f"{'' if id_order == 'sequential' else ', ' + id_order + ' ids'} under profiles/")
+    return None, (f"no rocprofv3 PMC summary of config {config}{' (routed)' if routed else ''} with {accounts} "
+                  f"accounts{'' if id_order == 'sequential' else ', ' + id_order + ' ids'} under profiles/")
 
 
 def query_phase(eng, w, acc_n, torch, dev, count=100, batch=1024):
@@ -152,6 +152,7 @@ def query_phase(eng, w, acc_n, torch, dev, count=100, batch=1024):
 
 HOST_WARMUP = 8  # untimed drop-in calls before each timed set (first-call allocations, page faults)
 HOST_PY = 40     # of each drop-in set, the calls made through the Python wrapper (the rest from C)
+STAGE_GAP_US = 200.0  # host_path `staged`: the journal write + replication round trip between prepare and commit
 
 
 def host_path(eng, w, tts, counts, b0, nbs, torch):
@@ -164,12 +165,16 @@ def host_path(eng, w, tts, counts, b0, nbs, torch):
       (tbgpu_prefetch_transfers, then its wait: the replica commits only after the
       prefetch callback, src/vsr/replica.zig:3384-3415): the commit's own latency, and
       prefetch + commit;
+    - `staged`: the primary's whole sequence for one op: tbgpu_stage_transfers at
+      StateMachine.prepare (src/vsr/replica.zig:5159-5167), a busy-wait standing for the
+      journal write and the replication round trip (STAGE_GAP_US), then prefetch (the
+      body found in HBM) + its wait and the commit back to back (:3137-3152);
     - `streamed`: tbgpu_create_transfers_batches over many batches from host memory.
     Reported beside the metric, never as `value` (which is HBM-resident)."""
     from tigerbeetle_amd.types import TRANSFER_DTYPE
-    single, prefetched, streamed = nbs
+    single, prefetched, staged, streamed = nbs
     offs = np.concatenate([[0], np.cumsum(counts.astype(np.int64))])
-    o0, o1 = int(offs[b0]), int(offs[b0 + single + prefetched + streamed])
+    o0, o1 = int(offs[b0]), int(offs[b0 + single + prefetched + staged + streamed])
     pinned = torch.empty((o1 - o0) * 128, dtype=torch.uint8, pin_memory=True)
     view = pinned.numpy().view(TRANSFER_DTYPE)
     view[:] = w.transfers[o0:o1]
@@ -216,7 +221,21 @@ def host_path(eng, w, tts, counts, b0, nbs, torch):
         eng.create_transfers(int(tts[p0 + k]), ev)
         if k >= c_pre + HOST_WARMUP:
             py_com.append((time.perf_counter() - t1) * 1e6)
-    s0 = p0 + prefetched
+    g0 = p0 + prefetched
+    st_out = None
+    if staged:
+        ev_g = view[int(offs[g0]) - o0:int(offs[g0 + staged]) - o0]
+        st_us, spre_us, scom_us = eng.bench_host_staged(tts[g0:g0 + staged], counts[g0:g0 + staged], ev_g, STAGE_GAP_US)
+        st_us, spre_us, scom_us = st_us[HOST_WARMUP:], spre_us[HOST_WARMUP:], scom_us[HOST_WARMUP:]
+        ev_st = int(offs[g0 + staged] - offs[g0 + HOST_WARMUP])
+        st_out = {"calls": len(scom_us), "warmup_calls": HOST_WARMUP, "gap_us": STAGE_GAP_US,
+                  "stage_latency_us": pct(st_us), "prefetch_latency_us": pct(spre_us),
+                  "commit_latency_us": pct(scom_us), "prefetch_plus_commit_us": pct(spre_us + scom_us),
+                  "transfers_per_s_prefetch_plus_commit": round(ev_st / (np.sum(spre_us + scom_us) * 1e-6), 1),
+                  "entry": "tbgpu_stage_transfers (at prepare), a busy-wait of gap_us, then "
+                           "tbgpu_prefetch_transfers_staged + tbgpu_prefetch_wait and tbgpu_create_transfers, "
+                           "timed from C (tbgpu_bench_host_staged)"}
+    s0 = g0 + staged
     ev = view[int(offs[s0]) - o0:]
     t0 = time.perf_counter()
     eng.create_transfers_batches(tts[s0:s0 + streamed], counts[s0:s0 + streamed], ev)
@@ -241,6 +260,8 @@ def host_path(eng, w, tts, counts, b0, nbs, torch):
                              "commit_transfers_per_s": round(ev_pre / (np.sum(com_us) * 1e-6), 1),
                              "entry": "tbgpu_prefetch_transfers + tbgpu_prefetch_wait, then tbgpu_create_transfers "
                                       "(the batch staged in HBM before the commit)"}
+    if st_out:
+        out["staged"] = st_out
     return out
 
 
@@ -417,6 +438,11 @@ def routed_bench(args, rank, world, local_rank, torch, dist, backend="nccl"):
         cpu = cpu_baseline_leg(args, acc_n, acc_n, ats_c, w.account_counts, w.accounts, tts_c, counts, w.transfers)
     if rank == 0:
         fp_gbps = per_step * COMMIT_BYTES_PER_TRANSFER / (fp_ms * 1e-3) / 1e9 if fp_ms > 0 else 0.0
+        # the owner commit's fp_commit from the PMC passes of this same routed command
+        # (profiles/run.sh pmc:4:routed); per launch like `achieved`
+        traffic, traffic_src = pmc_traffic(4, acc_n, kernel="fp_commit", routed=True) if world == 1 else \
+            (None, "PMC passes are taken on one GPU (a one-rank routed group); the N-rank launch is not profiled")
+        traffic_gbps = traffic / (fp_ms * 1e-3) / 1e9 if traffic and fp_ms > 0 else None
         e2e = value / world * ALGO_BYTES_PER_TRANSFER / 1e9
         a2a_bytes = per_step * ssm.wire_bytes_per_event * (world - 1) / world  # leaving each rank per step
         line = {
@@ -451,7 +477,10 @@ def routed_bench(args, rank, world, local_rank, torch, dist, backend="nccl"):
                        "dry_rounds": ssm.stats["dry_rounds"] - st0["dry_rounds"],
                        "fallbacks": ssm.stats["device_fallbacks"] - st0["device_fallbacks"]},
             "roofline": {"bound": "hbm", "achieved": round(fp_gbps, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(fp_gbps / HBM_PEAK_GBPS, 5), "traffic": None,
+                         "frac": round(fp_gbps / HBM_PEAK_GBPS, 5), "traffic": traffic,
+                         "traffic_source": traffic_src,
+                         "traffic_achieved": round(traffic_gbps, 2) if traffic_gbps else None,
+                         "traffic_frac": round(traffic_gbps / HBM_PEAK_GBPS, 5) if traffic_gbps else None,
                          "kernel": "fp_commit (the owner commit)",
                          "basis": f"{COMMIT_BYTES_PER_TRANSFER} B/transfer x {per_step} transfers per launch / "
                                   f"fp_commit launch time ({fp_ms:.4f} ms, HIP events on the engine stream, "
@@ -680,9 +709,9 @@ def main():
     B, K, W = args.batches_per_step, args.steps, args.warmup
     if (world > 1 or args.routed) and args.config == 4 and not args.unrouted:
         return routed_bench(args, rank, world, local_rank, torch, dist, backend)
-    host_nb = (0, 0, 0) if (args.no_host or world > 1 or args.config == 5) else \
-        ((args.host_batches or 136, args.host_batches or 136, (args.host_batches or 64) * 4) if args.config != 3
-         else (16, 16, 48))
+    host_nb = (0, 0, 0, 0) if (args.no_host or world > 1 or args.config == 5) else \
+        ((args.host_batches or 136, args.host_batches or 136, args.host_batches or 136, (args.host_batches or 64) * 4)
+         if args.config != 3 else (16, 16, 16, 48))
     n_batches = (K + W) * B + sum(host_nb)
     n_transfers = n_batches * BATCH_MAX
     t_gen = time.time()
@@ -804,13 +833,13 @@ def main():
     iters = []
     sorts = []
     paths = []
-    step_commit_ms = []  # per step: the dominant launch's HIP-event time (fp_commit on the fast path)
+    step_phase_ms = []  # per step: every phase's HIP-event time (the dominant one's spread is reported)
     non_ok = 0
     t0 = time.perf_counter()
     for k in range(W, W + K):
         non_ok += step(k)
         st = eng.stats()
-        step_commit_ms.append(st.phase_ms[1])
+        step_phase_ms.append(np.array(st.phase_ms[:8], dtype=np.float64))
         phase += np.array(st.phase_ms[:8])
         dev_ms += st.device_ms
         iters.append(st.iterations)
@@ -844,6 +873,7 @@ def main():
     # over the call's device time (HIP events around the call on the engine stream).
     names = list(PHASES)
     dom = int(np.argmax(phase[:len(names)]))
+    step_dom_ms = [float(p[dom]) for p in step_phase_ms]  # the dominant phase, step by step
     phase_ms_per_step = {names[i]: round(phase[i] / K, 4) for i in range(len(names))}
     e2e_gbps = value / world * ALGO_BYTES_PER_TRANSFER / 1e9
     if w is not None:
@@ -886,10 +916,10 @@ def main():
         "end_to_end": {"achieved": round(e2e_gbps, 2), "frac": round(e2e_gbps / HBM_PEAK_GBPS, 5),
                        "basis": f"{ALGO_BYTES_PER_TRANSFER} B/transfer x per-GPU committed transfers/s"},
         "dominant_phase": names[dom],
-        "dominant_ms_per_step": {"min": round(min(step_commit_ms), 4),
-                                 "median": round(float(np.median(step_commit_ms)), 4),
-                                 "max": round(max(step_commit_ms), 4),
-                                 "first": round(step_commit_ms[0], 4), "last": round(step_commit_ms[-1], 4)},
+        "dominant_ms_per_step": {"phase": names[dom], "min": round(min(step_dom_ms), 4),
+                                 "median": round(float(np.median(step_dom_ms)), 4),
+                                 "max": round(max(step_dom_ms), 4),
+                                 "first": round(step_dom_ms[0], 4), "last": round(step_dom_ms[-1], 4)},
         "phase_ms_per_step": phase_ms_per_step,
         "device_ms_per_step": round(dev_ms / K, 4),
     }

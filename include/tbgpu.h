@@ -307,6 +307,28 @@ uint32_t tbgpu_create_transfers(tbgpu_ctx* ctx, uint64_t timestamp,
 int tbgpu_prefetch_transfers(tbgpu_ctx* ctx, const tbgpu_transfer_t* events, uint32_t count);
 int tbgpu_prefetch_wait(tbgpu_ctx* ctx);
 
+/* StateMachine.prepare for create_transfers (src/state_machine.zig:503-512, called by
+ * the primary from primary_pipeline_prepare, src/vsr/replica.zig:5159-5167, before the
+ * prepare is journaled and replicated; the op is prefetched and committed once a quorum
+ * has it, src/vsr/replica.zig:3137-3152).  Starts the body's host-to-device copy into
+ * one of TBGPU_STAGE_SLOTS slots in HBM, keyed by `key`, and returns: the copy runs on a
+ * stream of its own while the prepare is replicated.  `key` identifies the body's
+ * content: the shim passes the message header's checksum_body, which the prepare keeps
+ * from its request (the body is not changed between the two, :5193-5211).  Staging the
+ * same key again does nothing.  It never releases a pending prepared commit.  A slot is
+ * reused oldest-first (slots a prefetch took before the others); the body must not
+ * change while its copy runs (until tbgpu_prefetch_transfers_staged of it returns, or
+ * the next stage call).  Backups never call prepare: their prefetch copies as
+ * tbgpu_prefetch_transfers does.  Returns 0, or -22 when count exceeds a batch. */
+#define TBGPU_STAGE_SLOTS 8u /* constants.pipeline_prepare_queue_max */
+int tbgpu_stage_transfers(tbgpu_ctx* ctx, tbgpu_uint128_t key, const tbgpu_transfer_t* events, uint32_t count);
+/* tbgpu_prefetch_transfers for a body that may have been staged: when a slot holds
+ * `key` with `count` events, the prefetch copies nothing and only prepares the commit
+ * from that slot (tbgpu_prefetch_wait then waits for the staged copy, normally long
+ * done); otherwise it is tbgpu_prefetch_transfers.  Results are the same either way. */
+int tbgpu_prefetch_transfers_staged(tbgpu_ctx* ctx, tbgpu_uint128_t key, const tbgpu_transfer_t* events,
+                                    uint32_t count);
+
 /* Streaming form: `batch_count` consecutive commits of create_transfers, with
  * identical results to calling tbgpu_create_transfers once per batch in order.
  * Batch b has `counts[b]` events starting after the previous batch's events and
@@ -594,6 +616,13 @@ int tbgpu_bench_generate_transfers(int device, uint64_t first_id, uint64_t count
 int tbgpu_bench_host_calls(tbgpu_ctx* ctx, int mode, uint32_t calls, const tbgpu_transfer_t* events,
                            const uint32_t* counts, const uint64_t* timestamps,
                            tbgpu_create_transfers_result_t* results, double* commit_us, double* prefetch_us);
+/* The primary's sequence for one op (bench): tbgpu_stage_transfers, a busy-wait of
+ * gap_us standing for the replication round trip, then tbgpu_prefetch_transfers_staged
+ * + tbgpu_prefetch_wait and tbgpu_create_transfers, timed per call from C. */
+int tbgpu_bench_host_staged(tbgpu_ctx* ctx, uint32_t calls, const tbgpu_transfer_t* events,
+                            const uint32_t* counts, const uint64_t* timestamps,
+                            tbgpu_create_transfers_result_t* results, double gap_us, double* stage_us,
+                            double* prefetch_us, double* commit_us);
 
 /* Test harness `setup` action (src/state_machine.zig:1892-1908): overwrite an
  * existing account's four balances.  Returns 0, or -1 if the account is missing. */
@@ -627,16 +656,20 @@ int tbgpu_get_posted(tbgpu_ctx* ctx, tbgpu_uint128_t pending_id);
  * state the ctx owns -- accounts, stored transfers, the posted groove, account
  * history, commit_timestamp -- as one self-describing image in a caller buffer
  * (the replica hands it to its grid / superblock).  Layout: a 64-B header
- * {magic "TBGPUCK1", version 1, counts, commit_timestamp, checksum of the rest},
- * then Account[n_accounts], Transfer[n_rows], posted u8[n_rows], imported
- * u8[n_rows], AccountHistoryGrooveValue[n_history].  The indexes are derived
- * state, rebuilt on open. */
+ * {magic "TBGPUCK1", version, shard, counts, commit_timestamp, checksum of the
+ * rest}, then Account[n_accounts], Transfer[n_rows], posted u8[n_rows], imported
+ * u8[n_rows], AccountHistoryGrooveValue[n_history], and for a ledger shard the
+ * other shards' directory entries.  Version 1: an unsharded ctx; version 3: a
+ * ledger shard (shard_world << 16 | shard_rank in `shard`); version 2: a legacy
+ * shard image without its shard, still accepted by any shard ctx.  The indexes are
+ * derived state, rebuilt on open. */
 uint64_t tbgpu_checkpoint_size(tbgpu_ctx* ctx);
 /* Returns the bytes written, or 0 when `capacity` is too small. */
 uint64_t tbgpu_checkpoint(tbgpu_ctx* ctx, void* out, uint64_t capacity);
 /* Replaces the ctx's state by the image's.  Returns 0, -22 (EINVAL) for a bad
- * magic/version/size/checksum, -28 (ENOSPC) when the image exceeds the ctx's
- * capacities. */
+ * magic/version/size/checksum or an image of another shard or kind, -95
+ * (EOPNOTSUPP) for a version-1 image offered to a ledger-shard ctx, -28 (ENOSPC)
+ * when the image exceeds the ctx's capacities. */
 int tbgpu_open(tbgpu_ctx* ctx, const void* image, uint64_t size);
 
 /* StateMachine.commit_timestamp (src/state_machine.zig:375). */

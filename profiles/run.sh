@@ -10,7 +10,8 @@
 #   config:C[:A,B..]    bench.py --config C plus arguments A B ..        OUT/bench_configC[_tag].json
 #                       (commas stand for spaces: config:1:--id-order,random)
 #   pmc:C[:ORDER]       kernel trace + PMC passes of config C's bench    OUT/pmcC[_ORDER]/ (+ traffic.json)
-#                       step (profiles/collect.sh), ids in ORDER
+#                       step (profiles/collect.sh), ids in ORDER; pmc:4:routed: the routed step
+#                       on a one-rank group                              OUT/pmc4_routed/
 #   hostpath            the drop-in call's kernel timeline               OUT/hostpath/
 #   fuzz:FIRST:COUNT[:big|:random]  the on-demand fuzz sweep (full-size batches, or
 #                       random u128 ids)                                 OUT/fuzz_FIRST[MODE].txt
@@ -54,12 +55,15 @@ step() {
       timeout -k 10 600 python3 -u bench.py --config "$c" ${a//,/ } > "$OUT/bench_config$c$tag.json" \
         2> "$OUT/bench_config$c$tag.err" ;;
     pmc)
-      local c=${rest%%:*} order=sequential
+      local c=${rest%%:*} order=sequential routed="" extra=""
       [ "$rest" != "$c" ] && order=${rest#*:}
-      local d=$OUT/pmc$c; [ "$order" != sequential ] && d=${d}_$order
+      # pmc:4:routed profiles the routed step on a one-rank group (the scaling family's N = 1)
+      [ "$order" = routed ] && { order=sequential; routed=1; extra="--routed"; }
+      local d=$OUT/pmc$c; [ "$order" != sequential ] && d=${d}_$order; [ -n "$routed" ] && d=${d}_routed
       local steps="--steps 2 --warmup 1"
-      TB_CONFIG=$c TB_ACCOUNTS=$(accounts_of "$c") TB_CALLS=3 TB_ID_ORDER=$order EVENTS_PER_LAUNCH=$(events_of "$c") \
-        bash profiles/collect.sh "$d" --config "$c" --id-order "$order" $steps $Q > "$d.log" 2>&1 ;;
+      TB_CONFIG=$c TB_ACCOUNTS=$(accounts_of "$c") TB_CALLS=3 TB_ID_ORDER=$order TB_ROUTED=$routed \
+        EVENTS_PER_LAUNCH=$(events_of "$c") \
+        bash profiles/collect.sh "$d" --config "$c" --id-order "$order" $extra $steps $Q > "$d.log" 2>&1 ;;
     hostpath)
       mkdir -p "$OUT/hostpath"
       timeout -k 10 300 python3 -u profiles/hostpath_trace.py > "$OUT/hostpath/plain.txt" 2>&1 || return 1

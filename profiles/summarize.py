@@ -76,6 +76,7 @@ if ev:
             tot += 2 * sum(f) * 1024 + sum(w) * 1024 * len(f) / len(w)
     res["_meta"] = {"config": int(os.environ.get("TB_CONFIG", "2")), "accounts": int(os.environ.get("TB_ACCOUNTS", "1000000")),
                     "id_order": os.environ.get("TB_ID_ORDER", "sequential"),
+                    "routed": bool(os.environ.get("TB_ROUTED")),
                     "steps": int(os.environ.get("TB_CALLS", "3")), "events_per_step": ev,
                     "commit_traffic_bytes": tot}
     if len(sys.argv) > 3:

@@ -129,7 +129,7 @@ def test_ledger_shard_checkpoint_round_trip():
             e.create_transfers_batches(np.array([n + 403 + r], np.uint64), np.array([400], np.uint32), t)
         for r, e in enumerate(engines):
             image = e.checkpoint()
-            assert image[8:12].view(np.uint32)[0] == 2  # version 2: a shard's image
+            assert image[8:12].view(np.uint32)[0] == 3  # version 3: a shard's image, naming its shard
             assert image[12:16].view(np.uint32)[0] == (world << 16 | r)
             wrong = other if r == 0 else _shard_engine(n, world, 0)
             try:
@@ -142,6 +142,20 @@ def test_ledger_shard_checkpoint_round_trip():
             try:
                 assert fresh.open(image) == 0
                 assert np.array_equal(fresh.checkpoint(), image), "restored shard image differs"
+                # a legacy version-2 image (round 5's first trees: no shard in the
+                # header) still opens into a shard ctx and comes back as version 3
+                legacy = image.copy()
+                legacy[8:12].view(np.uint32)[0] = 2
+                legacy[12:16].view(np.uint32)[0] = 0
+                again = _shard_engine(n, world, r)
+                try:
+                    assert again.open(legacy) == 0
+                    assert np.array_equal(again.checkpoint(), image), "legacy image restored differently"
+                finally:
+                    again.close()
+                bad = legacy.copy()
+                bad[12:16].view(np.uint32)[0] = world << 16 | r  # a version 2 never named a shard
+                assert fresh.open(bad) == -22
                 # an image whose hashed ids exceed the ctx's account index is refused
                 small = _shard_engine(n, world, r, hashed_max=64)
                 try:
@@ -151,7 +165,9 @@ def test_ledger_shard_checkpoint_round_trip():
             finally:
                 fresh.close()
         plain_img = plain.checkpoint()
-        assert engines[0].open(plain_img) == -22, "a shard ctx accepted an unsharded image"
+        # -95: a version-1 image cannot be told from an old shard image without foreign
+        # accounts, so a shard ctx refuses it with its own code
+        assert engines[0].open(plain_img) == -95, "a shard ctx accepted an unsharded image"
     finally:
         for e in engines + [other, plain]:
             e.close()

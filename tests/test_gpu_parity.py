@@ -738,6 +738,71 @@ def test_pinned_host_events_read_in_place():
         gpu.close()
 
 
+@pytest.mark.parametrize("order", ["shuffled_directory", "random_u128"])
+def test_create_accounts_unordered_ids(order):
+    """The clean call with ids that do not rise (the benchmark's --id-order=random /
+    reversed, IdPermutation, src/testing/id.zig:28-48): ac_fast_dup claims every id in a
+    call-local table.  Clean shuffled calls stay on the two-pass path; a repeat within
+    the call (adjacent or far apart), an existing id and an invalid field each hand the
+    call to the general path; every reply and row equals the oracle's, and the claim
+    table is left clean for the calls after (and for create_transfers' own use of it)."""
+    rng = np.random.default_rng(21)
+    calls, used = [], 0
+
+    def fresh(n):
+        nonlocal used
+        a = workload.make_accounts(np.arange(used + 1, used + 1 + n, dtype=np.uint64),
+                                   ledger=rng.integers(1, 3, n).astype(np.uint32))
+        used += n
+        if order == "random_u128":
+            a["id_lo"] = rng.integers(1, 1 << 63, n, dtype=np.uint64)
+            a["id_hi"] = rng.integers(1, 1 << 63, n, dtype=np.uint64)
+        else:
+            a = a[rng.permutation(n)]
+        return np.ascontiguousarray(a)
+
+    calls.append(fresh(4000))                     # clean, unordered
+    c = fresh(3000)
+    c[2999] = c[17]                               # a repeat far apart
+    calls.append(c)
+    calls.append(fresh(2500))                     # clean again (the claims were cleared)
+    c = fresh(1800)
+    c[901] = c[900]                               # an adjacent repeat
+    calls.append(c)
+    c = fresh(1500)
+    c[40] = calls[0][1234]                        # an existing id
+    calls.append(c)
+    c = fresh(1200)
+    c[5]["ledger"] = 0                            # an invalid field
+    calls.append(c)
+    calls.append(fresh(8190))                     # a full clean batch
+    orc, gpu = oracle.Oracle(40000, 30000), _engine(accounts_max=40000, transfers_max=30000)
+    try:
+        ts = 0
+        for c in calls:
+            ts += 1 + len(c)
+            want = orc.create_accounts(ts, c)
+            got = gpu.create_accounts(ts, c)
+            assert got.tobytes() == want.tobytes(), (got[:5], want[:5])
+        # transfers between the created accounts, after the account calls used the table
+        accs = np.concatenate(calls)
+        t = np.zeros(6000, dtype=workload.TRANSFER_DTYPE)
+        t["id_lo"] = rng.permutation(6000).astype(np.uint64) + 1
+        pick = rng.integers(0, len(accs), (6000, 2))
+        t["debit_account_id_lo"], t["debit_account_id_hi"] = accs["id_lo"][pick[:, 0]], accs["id_hi"][pick[:, 0]]
+        t["credit_account_id_lo"], t["credit_account_id_hi"] = accs["id_lo"][pick[:, 1]], accs["id_hi"][pick[:, 1]]
+        t["ledger"] = accs["ledger"][pick[:, 0]]
+        t["code"] = 1
+        t["amount_lo"] = 3
+        ts += 6001
+        assert gpu.create_transfers(ts, t).tobytes() == orc.create_transfers(ts, t).tobytes()
+        assert_state_equal(gpu, orc)
+        q = [int(a["id_lo"]) | (int(a["id_hi"]) << 64) for a in accs[::61]]
+        assert gpu.lookup_accounts(q).tobytes() == orc.lookup_accounts(q).tobytes()
+    finally:
+        gpu.close()
+
+
 @pytest.mark.parametrize("dense", [True, False], ids=["directory", "hashed"])
 def test_create_accounts_clean_and_dirty_calls(dense):
     """create_accounts' two-pass clean call (accounts.hip ac_fast_*: rising ids, every

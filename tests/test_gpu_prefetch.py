@@ -146,3 +146,124 @@ def test_prepared_commit_gate_released_expired_and_cancelled():
         assert_state_equal(gpu, orc)
     finally:
         gpu.close()
+
+
+@pytest.mark.parametrize("mix,pinned,depth", [("config1", False, 3), ("config1", True, 3), ("config1", True, 11),
+                                               ("config3", False, 3), ("config3", False, 11)])
+def test_staged_bodies_commit_in_order(mix, pinned, depth):
+    """StateMachine.prepare stages each body (tbgpu_stage_transfers) a pipeline's depth
+    ahead of its commit, as the primary does (src/vsr/replica.zig:5159-5167, then
+    :3137-3152): op k is staged, then op k - depth is prefetched from its slot and
+    committed.  Depth 3 stays inside the 8 slots; depth 11 overruns them, so the oldest
+    bodies are evicted and their prefetch copies them again.  Both replies and state
+    equal the oracle's, for page-locked and pageable bodies and on the general path."""
+    import torch
+    w = workload.config1(transfer_count=8190 * 14, account_count=700, seed=11) if mix == "config1" else \
+        workload.config3(batches=14, batch=1200, account_count=300, seed=12)
+    orc = oracle.Oracle(len(w.accounts), len(w.transfers))
+    gpu = _engine(w, pinned_input=pinned)
+    try:
+        ats, tts = w.timestamps()
+        for be in (orc, gpu):
+            be.create_accounts_batches(ats, w.account_counts, w.accounts)
+        bs = _batches(w)
+        if pinned:
+            from tigerbeetle_amd.types import TRANSFER_DTYPE
+            keep = []
+            for b, ev in enumerate(bs):
+                t = torch.empty(max(len(ev), 1) * 128, dtype=torch.uint8, pin_memory=True)
+                v = t.numpy().view(TRANSFER_DTYPE)[:len(ev)]
+                v[:] = ev
+                keep.append(t)
+                bs[b] = v
+        got, want = [], []
+        key = lambda b: (0xB0D1 << 64) | (b * 7919 + 1)  # any content key, one per body
+        for k in range(len(bs) + depth):
+            if k < len(bs):
+                gpu.stage_transfers(key(k), bs[k])
+            b = k - depth
+            if b < 0:
+                continue
+            gpu.prefetch_transfers_staged(key(b), bs[b])
+            gpu.prefetch_wait()
+            got.append(gpu.create_transfers(int(tts[b]), bs[b]))
+            res, rc, _ = orc.create_transfers_batches(tts[b:b + 1], w.transfer_counts[b:b + 1], bs[b])
+            want.append(res[:int(rc[0])].copy())
+        assert_results_equal(got, want, "create_transfers")
+        assert_state_equal(gpu, orc)
+    finally:
+        gpu.close()
+
+
+def test_stage_key_mismatch_and_interleaved_calls():
+    """A prefetch whose key no slot holds (or whose count differs) copies its body; a
+    stage call between a prefetch and its commit does not release the prepared commit
+    and does not disturb it; a lookup in between does release it.  Replies equal the
+    oracle's throughout."""
+    w = workload.config1(transfer_count=8190 * 6, account_count=500, seed=13)
+    orc, gpu = oracle.Oracle(len(w.accounts), len(w.transfers)), _engine(w)
+    try:
+        ats, tts = w.timestamps()
+        for be in (orc, gpu):
+            be.create_accounts_batches(ats, w.account_counts, w.accounts)
+        bs = _batches(w)
+        got, want = [], []
+        for b, ev in enumerate(bs):
+            if b == 0:
+                gpu.stage_transfers(100, ev[:-1])      # same key, another count: not this body
+                gpu.prefetch_transfers_staged(100, ev)
+            elif b == 1:
+                gpu.prefetch_transfers_staged(555, ev)  # never staged
+            else:
+                gpu.stage_transfers(200 + b, ev)
+                gpu.prefetch_transfers_staged(200 + b, ev)
+                if b == 3:
+                    gpu.stage_transfers(900, bs[0])     # staging between prefetch and commit
+                if b == 4:
+                    assert len(gpu.lookup_accounts([1, 2])) == 2  # releases the gate
+            gpu.prefetch_wait()
+            got.append(gpu.create_transfers(int(tts[b]), ev))
+            res, rc, _ = orc.create_transfers_batches(tts[b:b + 1], w.transfer_counts[b:b + 1], ev)
+            want.append(res[:int(rc[0])].copy())
+        assert_results_equal(got, want, "create_transfers")
+        assert_state_equal(gpu, orc)
+    finally:
+        gpu.close()
+
+
+def test_prepared_commit_with_failures_writes_only_its_replies():
+    """A prepared (gated) commit whose batch has fast-path failures -- ids committed by
+    an earlier batch (`exists`, `exists_with_different_*`) and static failures -- writes
+    exactly its sparse replies and leaves the caller's buffer past them untouched
+    (the whole event count used to be copied)."""
+    import ctypes
+    from tigerbeetle_amd.types import RESULT_DTYPE
+    w = workload.config1(transfer_count=8190 * 3, account_count=400, seed=14)
+    orc, gpu = oracle.Oracle(len(w.accounts), len(w.transfers) * 2), _engine(w)
+    try:
+        ats, tts = w.timestamps()
+        for be in (orc, gpu):
+            be.create_accounts_batches(ats, w.account_counts, w.accounts)
+        bs = _batches(w)
+        bad = bs[2].copy()
+        rng = np.random.default_rng(3)
+        pick = rng.choice(len(bad), 40, replace=False)
+        bad["id_lo"][pick[:20]] = bs[0]["id_lo"][pick[:20]]      # committed by batch 0
+        bad["amount_lo"][pick[10:20]] += 1                       # ... with another amount
+        bad["credit_account_id_lo"][pick[20:30]] = bad["debit_account_id_lo"][pick[20:30]]
+        bad["code"][pick[30:]] = 0
+        bodies = [bs[0], bs[1], np.ascontiguousarray(bad)]
+        for b, ev in enumerate(bodies):
+            gpu.prefetch_transfers(ev)
+            gpu.prefetch_wait()
+            out = np.full(len(ev) + 8, 0xABABABABABABABAB, dtype=np.uint64).view(RESULT_DTYPE)
+            n = gpu._L.tbgpu_create_transfers(gpu._h, int(tts[b]), ev.ctypes.data_as(ctypes.c_void_p), len(ev),
+                                              out.ctypes.data_as(ctypes.c_void_p))
+            res, rc, _ = orc.create_transfers_batches(tts[b:b + 1], np.array([len(ev)], np.uint32), ev)
+            assert n == int(rc[0]), (b, n, int(rc[0]))
+            assert out[:n].tobytes() == res[:n].tobytes(), b
+            assert (out[n:].view(np.uint64) == 0xABABABABABABABAB).all(), f"batch {b}: replies past the count written"
+        assert n == 40
+        assert_state_equal(gpu, orc)
+    finally:
+        gpu.close()

@@ -258,23 +258,31 @@ __global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const
 
 // ---------------------------------------------- the clean call in two passes --
 // The benchmark's create_accounts call (src/tigerbeetle/benchmark_load.zig:209-247):
-// ids rising through the call, no chain, no existing id, every field valid.  Then
-// every event is ok, its row is n_accounts + i and its timestamp T_b - n_b + k + 1
-// (execute, :1033-1035; create_account, :1198-1225), so the call is two passes:
+// no repeated id, no chain, no existing id, every field valid.  Then every event is
+// ok, its row is n_accounts + i and its timestamp T_b - n_b + k + 1 (execute,
+// :1033-1035; create_account, :1198-1225), so the call is two passes (three when its
+// ids do not rise):
 //   ac_fast_check  8 lanes per account, 16 bytes each: the lane's fields checked,
 //                  the chunk stored to the optimistic row (the timestamp patched in);
 //                  one lane probes the directory / index and compares the id with
-//                  the previous event's.  Anything else raises FL_SLOW (one atomic
-//                  per wave), and the host redoes the call on the general path
-//                  (rows past n_accounts are free space; the directory entries the
-//                  check wrote are cleared by ac_fast_index first).
+//                  the previous event's (ids that do not rise raise FL_NONMONO).
+//                  Anything else raises FL_SLOW (one atomic per wave), and the host
+//                  redoes the call on the general path (rows past n_accounts are free
+//                  space; the directory entries the check wrote are cleared by
+//                  ac_fast_index first).
 //                  An id of the direct-mapped directory whose entry is empty gets
-//                  its entry right there (ids rise through the call, so no two events
-//                  write one entry).
+//                  its entry right there (two events writing one entry have one id:
+//                  rising ids never do, and ac_fast_dup finds them otherwise).
+//   ac_fast_dup    only with FL_NONMONO (--id-order=random / reversed, the benchmark's
+//                  IdPermutation, src/testing/id.zig:28-48): every id claims a slot of
+//                  a call-local table by CAS (event + 1); a claim that meets an earlier
+//                  claim of the same id (read from the events, which nothing writes)
+//                  is a repeat: FL_SLOW.
 //   ac_fast_index  on a clean check: the index slot of every hashed id (CAS on its row
 //                  word; none when every id is in the directory, FL_AC_HASHED clear),
 //                  zero reply counts, commit_timestamp.  On a failed check: the
-//                  directory entries the check wrote are cleared again.
+//                  directory entries the check wrote are cleared again.  Either way
+//                  the call-local claims are cleared.
 constexpr int AF_THREADS = 256;
 
 __global__ __launch_bounds__(AF_THREADS) void ac_fast_check(Tables T, AcArgs C, u64 row_base) {
@@ -294,7 +302,7 @@ __global__ __launch_bounds__(AF_THREADS) void ac_fast_check(Tables T, AcArgs C, 
               pw = __shfl(v.w, lane - 8);
     // the event's ledger and flags (chunk 7, seven lanes up), for its directory entry
     const u32 q7x = __shfl(v.x, lane + 7), q7y = __shfl(v.y, lane + 7);
-    bool hashed = false;
+    bool hashed = false, nonmono = false;
     if (e < C.n) {
         switch (ch) {
         case 0: {  // id: not 0 / maxInt (:1204-1205), absent, above the previous event's
@@ -303,7 +311,7 @@ __global__ __launch_bounds__(AF_THREADS) void ac_fast_check(Tables T, AcArgs C, 
             if (!bad && e > 0) {
                 const u128 prev = lane >= 8 ? ((u128)(((u64)pw << 32) | pz) << 64) | (((u64)py << 32) | px)
                                             : C.ev[e - 1].id;
-                bad = !(id > prev);
+                nonmono = !(id > prev);  // (a repeat is possible: ac_fast_dup looks)
             }
             if (!bad) {
                 if (dense_has(T, id)) {
@@ -339,13 +347,40 @@ __global__ __launch_bounds__(AF_THREADS) void ac_fast_check(Tables T, AcArgs C, 
         }
         ((uint4*)&T.acc[row_base + e])[ch] = v;
     }
-    const u32 fl = (__ballot(bad) ? (u32)FL_SLOW : 0u) | (__ballot(hashed) ? (u32)FL_AC_HASHED : 0u);
+    const u32 fl = (__ballot(bad) ? (u32)FL_SLOW : 0u) | (__ballot(hashed) ? (u32)FL_AC_HASHED : 0u) |
+                   (__ballot(nonmono) ? (u32)FL_NONMONO : 0u);
     if (fl && wave_leader()) atomicOr(&C.counters[CNT_FLAGS], fl);
+}
+
+__global__ __launch_bounds__(AF_THREADS) void ac_fast_dup(AcArgs C) {
+    const u32 flags = C.counters[CNT_FLAGS];
+    if (!(flags & FL_NONMONO)) return;  // ids rise through the call: none repeats
+    const u32 i = blockIdx.x * AF_THREADS + threadIdx.x;
+    bool dup = false;
+    if (i < C.n) {
+        const u128 id = C.ev[i].id;
+        u64 h = hash128(id) & C.fmask;
+        for (;;) {
+            const u32 prev = atomicCAS(&C.ftab[h], 0u, i + 1);
+            if (prev == 0) {
+                C.fpos[i] = (u32)h;
+                break;
+            }
+            if (C.ev[prev - 1].id == id) {
+                C.fpos[i] = NONE32;
+                dup = true;
+                break;
+            }
+            h = (h + 1) & C.fmask;
+        }
+    }
+    if (__ballot(dup) && wave_leader()) atomicOr(&C.counters[CNT_FLAGS], (u32)FL_SLOW);
 }
 
 __global__ __launch_bounds__(AF_THREADS) void ac_fast_index(Tables T, AcArgs C, u64 row_base) {
     const u32 flags = C.counters[CNT_FLAGS];
     const u32 i = blockIdx.x * AF_THREADS + threadIdx.x;
+    if ((flags & FL_NONMONO) && i < C.n && C.fpos[i] != NONE32) C.ftab[C.fpos[i]] = 0;  // (all-zero again)
     if (flags & FL_SLOW) {
         // the call goes to the general path: the directory entries the check wrote go
         if (i < C.n) {
@@ -565,6 +600,7 @@ void ac_launch_mask(const Tables& T, const AcArgs& C, const u8* res, const u8* o
 void ac_launch_fast(const Tables& T, const AcArgs& C, u64 row_base, hipStream_t stream) {
     const u64 lanes = 8ull * C.n;
     ac_fast_check<<<(u32)((lanes + AF_THREADS - 1) / AF_THREADS), AF_THREADS, 0, stream>>>(T, C, row_base);
+    ac_fast_dup<<<(u32)((C.n + AF_THREADS - 1) / AF_THREADS), AF_THREADS, 0, stream>>>(C);
     ac_fast_index<<<(u32)((std::max(C.n, C.nb) + AF_THREADS - 1) / AF_THREADS), AF_THREADS, 0, stream>>>(T, C, row_base);
     HIP_CHECK(hipGetLastError());
 }

@@ -429,6 +429,27 @@ struct tbgpu_ctx {
     u32 pf_n = 0;
     bool pf_valid = false;
     hipEvent_t pf_ev = nullptr;    // recorded behind the copy
+    const u8* pf_dev = nullptr;    // where the prefetched body is in HBM: pf_buf, or a stage slot
+    int pf_slot = -1;              // the stage slot it is (-1: pf_buf)
+    // tbgpu_stage_transfers (StateMachine.prepare): bodies copied into HBM at prepare
+    // time, one slot per prepare the pipeline may hold, keyed by the caller's content key;
+    // the copies run on a stream of their own, so staging never waits behind (or releases)
+    // a prepared commit's gate on the engine stream.  Allocated on first use.
+    struct StageSlot {
+        u8* d = nullptr;           // TBGPU_BATCH_MAX * 128 bytes in HBM
+        u8* h = nullptr;           // page-locked shadow for a pageable source (first need)
+        const u8* h_dev = nullptr;
+        u64 key_lo = 0, key_hi = 0;
+        u32 n = 0;
+        bool valid = false;
+        bool used = false;         // a prefetch has taken it (the first to reuse)
+        u64 seq = 0;               // staging order
+        hipEvent_t staged = nullptr;    // behind its copy (stage stream)
+        hipEvent_t released = nullptr; // behind the last launch that read it (engine stream)
+        bool release_recorded = false;
+    } stg[TBGPU_STAGE_SLOTS];
+    hipStream_t stage_stream = nullptr;
+    u64 stage_seq = 0;
     // account-transfers index (query.hip), allocated by the first compaction
     u32 *q_key = nullptr, *q_val = nullptr, *q_tkey = nullptr, *q_tval = nullptr;
     SortScratch q_ss{};
@@ -816,6 +837,14 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
         }
     for (hipEvent_t e : c->prof_pool) (void)hipEventDestroy(e);
     if (c->pf_ev) (void)hipEventDestroy(c->pf_ev);
+    if (c->stage_stream) (void)hipStreamSynchronize(c->stage_stream);
+    for (auto& S : c->stg) {
+        if (S.d) { guard_release(S.d); (void)hipFree(S.d); }
+        if (S.h) (void)hipHostFree(S.h);
+        if (S.staged) (void)hipEventDestroy(S.staged);
+        if (S.released) (void)hipEventDestroy(S.released);
+    }
+    if (c->stage_stream) (void)hipStreamDestroy(c->stage_stream);
     (void)hipEventDestroy(c->ev0);
     (void)hipEventDestroy(c->ev1);
     (void)hipEventDestroy(c->ev_side);
@@ -1865,17 +1894,18 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         if (b1 == nb_total) {
             // the call's end: counters, cursors and reply counts in one copy, with the
             // replies, and one wait
-            if (!c->tail_reported) {  // (fp_tail stored it already: a small call)
+            const bool tail_done = c->tail_reported;  // fp_tail stored the report already: a small call
+            c->tail_reported = false;
+            if (!tail_done) {
                 const u32 rb = std::max<u32>((RPT_COUNTS + nb + 255) / 256,
                                              dst_device ? 1u : std::min<u32>(n / 256, 1024));
                 k_report<<<rb, 256, 0, c->stream>>>(c->counters, c->T.base, c->counts, nb, c->h_report_dev,
                                                     (const u64*)c->res_buf, dst_device ? nullptr : c->h_res_dev);
                 HIP_CHECK(hipGetLastError());
             }
-            c->tail_reported = false;
-            if (call_events || !c->tail_reported) HIP_CHECK(hipEventRecord(c->ev1, c->stream));
+            if (call_events || !tail_done) HIP_CHECK(hipEventRecord(c->ev1, c->stream));
             ht_mark(c, 5);
-            if (c->tail_reported && !c->prof) {
+            if (tail_done && !c->prof) {
                 // a small call: fp_tail's last store is its sequence word in pinned host
                 // memory, after everything it reported; spin on it (no completion signal,
                 // no wake-up), and only past a bound wait for the launch as any other call
@@ -2296,7 +2326,7 @@ static void prepare_gated(tbgpu_ctx* c, u32 n) {
                             c->h_report_dev + RPT_COUNTS + c->bmax, seq};
     c->tail_reported = false;
     c->gate_arm = true;
-    const bool launched = try_fast(c, (const Transfer*)c->pf_buf, n, 1, (tbgpu_create_transfers_result_t*)c->res_buf,
+    const bool launched = try_fast(c, (const Transfer*)c->pf_dev, n, 1, (tbgpu_create_transfers_result_t*)c->res_buf,
                                    /*spec=*/true);
     c->gate_arm = false;
     if (!launched || !c->tail_reported)
@@ -2340,8 +2370,9 @@ static bool commit_gated(tbgpu_ctx* c, u64 timestamp, tbgpu_create_transfers_res
     memcpy(c->h_base, c->h_report + RPT_BASE, 4 * sizeof(u64));
     memcpy(c->h_rc, c->h_report + RPT_COUNTS, sizeof(u32));
     if (!spec_settle(c)) return false;
+    // the call's replies only (none when every event is ok): the count fp_tail reported
     const std::vector<u32> starts = {0u, n};
-    copy_results_to_batches(c, 1, starts, &n, (u8*)results);
+    copy_results_to_batches(c, 1, starts, c->h_rc, (u8*)results);
     c->n_rows = c->h_base[BASE_ROWS];
     c->n_hist = c->h_base[BASE_HIST];
     c->rows_hi = c->n_rows;
@@ -2368,14 +2399,136 @@ extern "C" int tbgpu_prefetch_transfers(tbgpu_ctx* c, const tbgpu_transfer_t* ev
     HIP_CHECK(hipEventRecord(c->pf_ev, c->stream));
     c->pf_src = events;
     c->pf_n = count;
+    c->pf_dev = c->pf_buf;
+    c->pf_slot = -1;
     c->pf_valid = true;
     prepare_gated(c, count);
     return 0;
 }
 
+// ---- staging at prepare (tbgpu_stage_transfers) --------------------------------------
+//
+// The replica hands every request body to StateMachine.prepare when it makes the prepare
+// (src/vsr/replica.zig:5159-5167 -> src/state_machine.zig:503), before the journal write
+// and the replication round trip; it prefetches and commits that op only once a quorum
+// has it (src/vsr/replica.zig:3137-3152), back to back.  Staging the body's copy at
+// prepare takes the copy out of that back-to-back sequence: prefetch then finds the
+// body in HBM and only enqueues the prepared commit.
+
+static void stage_init(tbgpu_ctx* c) {
+    if (c->stage_stream) return;
+    HIP_CHECK(hipSetDevice(c->device));
+    HIP_CHECK(hipStreamCreateWithFlags(&c->stage_stream, hipStreamNonBlocking));
+    for (auto& S : c->stg) {
+        S.d = dalloc<u8>((u64)TBGPU_BATCH_MAX * 128, &c->bytes);
+        HIP_CHECK(hipEventCreateWithFlags(&S.staged, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&S.released, hipEventDisableTiming));
+    }
+}
+
+static int stage_find(tbgpu_ctx* c, tbgpu_uint128_t key, u32 n) {
+    for (int k = 0; k < (int)TBGPU_STAGE_SLOTS; k++) {
+        const auto& S = c->stg[k];
+        if (S.valid && S.key_lo == key.lo && S.key_hi == key.hi && S.n == n) return k;
+    }
+    return -1;
+}
+
+extern "C" int tbgpu_stage_transfers(tbgpu_ctx* c, tbgpu_uint128_t key, const tbgpu_transfer_t* events,
+                                     uint32_t count) {
+    CallGuard guard_(c, false, /*keep_gate=*/true);  // (a prepared commit may be pending)
+    if (count > TBGPU_BATCH_MAX) return -22;
+    if (count == 0) return 0;
+    stage_init(c);
+    if (stage_find(c, key, count) >= 0) return 0;  // the same content is staged already
+    // the slot: a free one, else the oldest a prefetch has taken, else the oldest; never
+    // the one the pending prefetch reads
+    int pick = -1;
+    for (int pass = 0; pass < 3 && pick < 0; pass++) {
+        u64 best = ~0ull;
+        for (int k = 0; k < (int)TBGPU_STAGE_SLOTS; k++) {
+            const auto& S = c->stg[k];
+            if (c->pf_valid && c->pf_slot == k) continue;
+            const bool fits = pass == 0 ? !S.valid : pass == 1 ? S.used : true;
+            if (fits && S.seq < best) {
+                best = S.seq;
+                pick = k;
+            }
+        }
+    }
+    auto& S = c->stg[pick];
+    S.valid = false;
+    // the slot's last readers (a commit on the engine stream) come before its new copy
+    if (S.release_recorded) HIP_CHECK(hipStreamWaitEvent(c->stage_stream, S.released, 0));
+    const u64 bytes = (u64)count * 128;
+    const void* src = (c->opt.flags & TBGPU_OPT_PINNED_INPUT) ? pinned_device_ptr(events, bytes) : nullptr;
+    if (!src) {
+        // a pageable body: through the slot's page-locked shadow (its previous copy out of
+        // the shadow has run: staged)
+        if (!S.h) {
+            HIP_CHECK(hipHostMalloc((void**)&S.h, (u64)TBGPU_BATCH_MAX * 128, hipHostMallocMapped | hipHostMallocCoherent));
+            void* d = nullptr;
+            HIP_CHECK(hipHostGetDevicePointer(&d, S.h, 0));
+            S.h_dev = (const u8*)d;
+        } else {
+            HIP_CHECK(hipEventSynchronize(S.staged));
+        }
+        memcpy(S.h, events, bytes);
+        src = S.h_dev;
+    }
+    if (sdma_h2d()) HIP_CHECK(hipMemcpyAsync(S.d, src == S.h_dev ? (const void*)S.h : (const void*)events, bytes,
+                                             hipMemcpyHostToDevice, c->stage_stream));
+    else copy_in(S.d, src, bytes, c->stage_stream);
+    HIP_CHECK(hipEventRecord(S.staged, c->stage_stream));
+    S.key_lo = key.lo;
+    S.key_hi = key.hi;
+    S.n = count;
+    S.used = false;
+    S.seq = ++c->stage_seq;
+    S.valid = true;
+    return 0;
+}
+
+extern "C" int tbgpu_prefetch_transfers_staged(tbgpu_ctx* c, tbgpu_uint128_t key, const tbgpu_transfer_t* events,
+                                               uint32_t count) {
+    CallGuard guard_(c, false);  // (releases an earlier prepared commit)
+    if (count > TBGPU_BATCH_MAX) return -22;
+    const int k = c->stage_stream ? stage_find(c, key, count) : -1;
+    if (k < 0) return tbgpu_prefetch_transfers(c, events, count);  // not staged: copy it now
+    c->pf_valid = false;
+    xidx_tombs_check(c);
+    auto& S = c->stg[k];
+    // the engine stream waits for the slot's copy only while it still runs (a finished
+    // copy needs no cross-queue dependency)
+    if (hipEventQuery(S.staged) != hipSuccess) HIP_CHECK(hipStreamWaitEvent(c->stream, S.staged, 0));
+    c->pf_src = events;
+    c->pf_n = count;
+    c->pf_dev = S.d;
+    c->pf_slot = k;
+    c->pf_valid = true;
+    S.used = true;
+    prepare_gated(c, count);
+    // the prepared launches read the slot; a commit that does not take them records the
+    // release again behind its own launches (stage_release)
+    HIP_CHECK(hipEventRecord(S.released, c->stream));
+    S.release_recorded = true;
+    return 0;
+}
+
+// a commit (or anything else) read stage slot k on the engine stream: its next copy
+// comes after that
+static void stage_release(tbgpu_ctx* c, int k) {
+    if (k < 0) return;
+    HIP_CHECK(hipEventRecord(c->stg[k].released, c->stream));
+    c->stg[k].release_recorded = true;
+}
+
 extern "C" int tbgpu_prefetch_wait(tbgpu_ctx* c) {
     CallGuard guard_(c, false, /*keep_gate=*/true);
-    if (c->pf_valid) wait_event(c->pf_ev);
+    if (c->pf_valid) {
+        if (c->pf_slot >= 0) wait_event(c->stg[c->pf_slot].staged);
+        else wait_event(c->pf_ev);
+    }
     return 0;
 }
 
@@ -2400,7 +2553,8 @@ extern "C" uint32_t tbgpu_create_transfers(tbgpu_ctx* c, uint64_t timestamp, con
             return out;
         }
         // the gate let nothing through, or the attempt fell back: an ordinary call
-        out = (uint32_t)transfers_batches(c, 1, &ts, &count, (const Transfer*)c->pf_buf, true, results, false, &rc);
+        out = (uint32_t)transfers_batches(c, 1, &ts, &count, (const Transfer*)c->pf_dev, true, results, false, &rc);
+        stage_release(c, c->pf_slot);
         ht_mark(c, 7);
         c->ht_on = false;
         return out;
@@ -2409,7 +2563,8 @@ extern "C" uint32_t tbgpu_create_transfers(tbgpu_ctx* c, uint64_t timestamp, con
     if (prepared) {
         // prefetched: the events are in HBM already (the copy is ahead on the stream)
         c->pf_valid = false;
-        out = (uint32_t)transfers_batches(c, 1, &ts, &count, (const Transfer*)c->pf_buf, true, results, false, &rc);
+        out = (uint32_t)transfers_batches(c, 1, &ts, &count, (const Transfer*)c->pf_dev, true, results, false, &rc);
+        stage_release(c, c->pf_slot);
     } else {
         c->pf_valid = false;
         out = (uint32_t)transfers_batches(c, 1, &ts, &count, (const Transfer*)events, false, results, false, &rc);
@@ -2456,6 +2611,9 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
     C.counters = c->counters;
     C.ts_part = c->ac_part;
     C.counts_out = c->counts;
+    C.ftab = c->f_gtab;  // (the fast path's claim table: all-zero between calls, >= 2n slots)
+    C.fpos = c->f_gpos;
+    C.fmask = std::min<u64>(c->f_gcap, pow2_at_least(2ull * n)) - 1;
     static const bool no_fast = getenv("TBGPU_NO_AC_FAST") != nullptr;  // A/B timing of the general path
     if (!no_fast && !(c->opt.flags & TBGPU_OPT_FORCE_GENERAL) && c->n_accounts + n <= c->accounts_max &&
         !c->T.shard_world) {
@@ -2873,11 +3031,14 @@ extern "C" uint64_t tbgpu_get_account_history_device(tbgpu_ctx* c, uint32_t coun
 
 namespace {
 constexpr u64 CK_MAGIC = 0x314B435550474254ull;  // "TBGPUCK1"
-// version 1: one state machine; version 2: a ledger shard's image, which also lists
+// version 1: one state machine; version 3: a ledger shard's image, which also lists
 // the other shards' accounts its directory knows (n_foreign ForeignAccount records,
 // sorted by id, after the history rows) and names its shard: `shard` = world << 16 |
 // rank.  An image opens only into a ctx of the same kind and, for a shard, the same
-// world and rank.
+// world and rank.  Version 2 is the shard image of round 5's first trees, which did not
+// name its shard (`shard` 0): it still opens into any shard ctx.  A shard ctx refuses a
+// version-1 image with -95 (those trees wrote a shard image without foreign accounts as
+// version 1, which cannot be told apart from an unsharded image).
 struct CkHeader {
     u64 magic;
     u32 version, shard;
@@ -2945,7 +3106,7 @@ extern "C" uint64_t tbgpu_checkpoint(tbgpu_ctx* c, void* out, uint64_t capacity)
     }
     CkHeader h{};
     h.magic = CK_MAGIC;
-    h.version = c->T.shard_world ? 2 : 1;
+    h.version = c->T.shard_world ? 3 : 1;
     h.shard = c->T.shard_world ? (c->T.shard_world << 16 | c->T.shard_rank) : 0;
     h.n_foreign = nf;
     h.n_accounts = na;
@@ -2962,12 +3123,14 @@ extern "C" int tbgpu_open(tbgpu_ctx* c, const void* image, uint64_t size) {
     if (size < sizeof(CkHeader)) return -22;
     CkHeader h;
     memcpy(&h, image, sizeof h);
-    if (h.magic != CK_MAGIC || (h.version != 1 && h.version != 2)) return -22;
+    if (h.magic != CK_MAGIC || h.version < 1 || h.version > 3) return -22;
     if (h.version == 1 && (h.n_foreign != 0 || h.shard != 0)) return -22;
+    if (h.version == 2 && h.shard != 0) return -22;
     // a ledger shard's image only into the ctx of the same shard, and an unsharded one
     // only into an unsharded ctx
-    if (h.version == 1 && c->T.shard_world) return -22;
-    if (h.version == 2 && (!c->T.shard_world || h.shard != (c->T.shard_world << 16 | c->T.shard_rank))) return -22;
+    if (h.version == 1 && c->T.shard_world) return -95;
+    if (h.version != 1 && !c->T.shard_world) return -22;
+    if (h.version == 3 && h.shard != (c->T.shard_world << 16 | c->T.shard_rank)) return -22;
     if (size != sizeof(CkHeader) + ck_payload_bytes(h.n_accounts, h.n_rows, h.n_hist, h.n_foreign)) return -22;
     const u8* p = (const u8*)image + sizeof(CkHeader);
     if (ck_checksum(p, size - sizeof(CkHeader)) != h.checksum) return -22;
@@ -3138,6 +3301,40 @@ extern "C" int tbgpu_bench_host_calls(tbgpu_ctx* c, int mode, uint32_t calls, co
         const auto t2 = clk::now();
         commit_us[k] = std::chrono::duration<double, std::micro>(t2 - t1).count();
         if (prefetch_us) prefetch_us[k] = std::chrono::duration<double, std::micro>(t1 - t0).count();
+        off += counts[k];
+    }
+    return 0;
+}
+
+// The replica's sequence for one op on the primary, timed from C (bench.py host_path
+// `staged`): tbgpu_stage_transfers at prepare, a busy-wait of `gap_us` standing for the
+// journal write and the replication round trip, then prefetch (staged) + its wait and
+// the commit back to back (src/vsr/replica.zig:3137-3152).  The key is the call's index
+// (a stand-in for the header's checksum_body).
+extern "C" int tbgpu_bench_host_staged(tbgpu_ctx* c, uint32_t calls, const tbgpu_transfer_t* events,
+                                       const uint32_t* counts, const uint64_t* timestamps,
+                                       tbgpu_create_transfers_result_t* results, double gap_us, double* stage_us,
+                                       double* prefetch_us, double* commit_us) {
+    using clk = std::chrono::steady_clock;
+    auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    u64 off = 0;
+    for (uint32_t k = 0; k < calls; k++) {
+        const tbgpu_transfer_t* ev = events + off;
+        const tbgpu_uint128_t key{0x5354414745ull, (u64)k + 1};
+        const auto t0 = clk::now();
+        if (tbgpu_stage_transfers(c, key, ev, counts[k]) != 0) return -22;
+        const auto t1 = clk::now();
+        while (us(t1, clk::now()) < gap_us) {
+        }
+        const auto t2 = clk::now();
+        if (tbgpu_prefetch_transfers_staged(c, key, ev, counts[k]) != 0) return -22;
+        tbgpu_prefetch_wait(c);
+        const auto t3 = clk::now();
+        tbgpu_create_transfers(c, timestamps[k], ev, counts[k], results);
+        const auto t4 = clk::now();
+        stage_us[k] = us(t0, t1);
+        prefetch_us[k] = us(t2, t3);
+        commit_us[k] = us(t3, t4);
         off += counts[k];
     }
     return 0;

@@ -1267,7 +1267,11 @@ __global__ void fp_undo(Tables T, FastArgs F) {
     if (F.dry || i >= F.n) return;
     // every eager claim of the call (each took a slot that was empty before it; all go
     // together, so no other id's probe sequence runs through them): the index as before
-    if (F.eager && F.gpos[i] != NONE32) T.xidx[F.gpos[i]] = 0;
+    if (F.eager && F.gpos[i] != NONE32) {
+        // a claim fp_chains withdrew is a tombstone it counted: uncount it with the slot
+        if ((u32)T.xidx[F.gpos[i]] == XIDX_TOMB) atomicSub(&T.hcount[2], 1u);
+        T.xidx[F.gpos[i]] = 0;
+    }
     if (F.fres[i] != TBGPU_CREATE_TRANSFER_OK) return;
     const Transfer& t = F.ev[i];
     const u32 ds = acc_row(T, t.debit_account_id);

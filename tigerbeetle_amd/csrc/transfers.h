@@ -137,9 +137,15 @@ struct AcArgs {
     u64 gmask;
     u32* counters;
     u32* counts_out;  // per-batch reply counts (the clean two-pass call writes zeros)
+    // the clean call with ids that do not rise (random u128 ids): a call-local claim
+    // table (event + 1 per slot, all-zero between calls: the fast path's transfer-id
+    // claim table) finds a repeated id, and each event's claimed slot to clear again
+    u32* ftab;
+    u32* fpos;
+    u64 fmask;
 };
 // The clean call (accounts.hip ac_fast_*): raises FL_SLOW in counters[CNT_FLAGS] and
-// changes nothing visible when the call is not clean (ids rising, all fields valid,
+// changes nothing visible when the call is not clean (no repeated id, all fields valid,
 // no chain, no existing id); otherwise commits it.  The caller ensures row capacity.
 void ac_launch_fast(const Tables& T, const AcArgs& C, u64 row_base, hipStream_t stream);
 void ac_launch_classify(const Tables& T, const AcArgs& C, hipStream_t stream);

@@ -97,6 +97,12 @@ def lib():
     L.tbgpu_prefetch_wait.argtypes = [vp]
     L.tbgpu_bench_host_calls.restype = ctypes.c_int
     L.tbgpu_bench_host_calls.argtypes = [vp, ctypes.c_int, u32, vp, vp, vp, vp, vp, vp]
+    L.tbgpu_stage_transfers.restype = ctypes.c_int
+    L.tbgpu_stage_transfers.argtypes = [vp, U128, vp, u32]
+    L.tbgpu_prefetch_transfers_staged.restype = ctypes.c_int
+    L.tbgpu_prefetch_transfers_staged.argtypes = [vp, U128, vp, u32]
+    L.tbgpu_bench_host_staged.restype = ctypes.c_int
+    L.tbgpu_bench_host_staged.argtypes = [vp, u32, vp, vp, vp, vp, ctypes.c_double, vp, vp, vp]
     L.tbgpu_test_set_balances.restype = ctypes.c_int
     L.tbgpu_test_set_balances.argtypes = [vp, U128, U128, U128, U128, U128]
     for name in ("tbgpu_account_count", "tbgpu_transfer_count", "tbgpu_history_count", "tbgpu_commit_timestamp"):
@@ -247,6 +253,39 @@ class Engine:
             raise ValueError("prefetch_transfers needs the contiguous event array create_transfers will get")
         if self._L.tbgpu_prefetch_transfers(self._h, _ptr(events), len(events)) != 0:
             raise ValueError("prefetch_transfers: more events than a batch")
+
+    def stage_transfers(self, key: int, events: np.ndarray) -> None:
+        """StateMachine.prepare for create_transfers (tbgpu_stage_transfers): the body's
+        copy to HBM starts now, keyed by `key` (the shim's checksum_body); a later
+        prefetch_transfers(events, key=key) finds it there.  `events` must stay unchanged
+        until that prefetch."""
+        if events.dtype != TRANSFER_DTYPE or not events.flags["C_CONTIGUOUS"]:
+            raise ValueError("stage_transfers needs a contiguous TRANSFER_DTYPE array")
+        if self._L.tbgpu_stage_transfers(self._h, u128(key), _ptr(events), len(events)) != 0:
+            raise ValueError("stage_transfers: more events than a batch")
+
+    def prefetch_transfers_staged(self, key: int, events: np.ndarray) -> None:
+        """tbgpu_prefetch_transfers_staged: prefetch of a body that may have been staged
+        under `key` (then nothing is copied); create_transfers on the same array commits it."""
+        if events.dtype != TRANSFER_DTYPE or not events.flags["C_CONTIGUOUS"]:
+            raise ValueError("prefetch_transfers_staged needs the contiguous event array create_transfers will get")
+        if self._L.tbgpu_prefetch_transfers_staged(self._h, u128(key), _ptr(events), len(events)) != 0:
+            raise ValueError("prefetch_transfers_staged: more events than a batch")
+
+    def bench_host_staged(self, timestamps, counts, events, gap_us: float):
+        """tbgpu_bench_host_staged: stage, a gap of gap_us, prefetch (staged) + wait,
+        commit, per batch, timed from C.  Returns (stage, prefetch, commit) microseconds."""
+        ts = np.ascontiguousarray(timestamps, dtype=np.uint64)
+        cs = np.ascontiguousarray(counts, dtype=np.uint32)
+        if events.dtype != TRANSFER_DTYPE or not events.flags["C_CONTIGUOUS"]:
+            raise ValueError("bench_host_staged needs contiguous TRANSFER_DTYPE events")
+        out = np.zeros(max(int(cs.max()) if len(cs) else 1, 1), dtype=RESULT_DTYPE)
+        st, pre, com = (np.zeros(len(cs), dtype=np.float64) for _ in range(3))
+        rc = self._L.tbgpu_bench_host_staged(self._h, len(cs), _ptr(events), _ptr(cs), _ptr(ts), _ptr(out),
+                                             float(gap_us), _ptr(st), _ptr(pre), _ptr(com))
+        if rc != 0:
+            raise ValueError(f"bench_host_staged: {rc}")
+        return st, pre, com
 
     def bench_host_calls(self, mode: int, timestamps, counts, events):
         """tbgpu_bench_host_calls: the drop-in call timed from C (mode 0 one

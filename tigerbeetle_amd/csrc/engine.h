@@ -467,6 +467,9 @@ enum {
     CNT_GCUR = 8,       // general path: id-group ranges reserved so far
     CNT_PCUR = 9,       // general path: pending-group ranges reserved so far
     CNT_TS_SAVE = 12,   // fast path: commit_timestamp before the call (u64 in words 12-13)
+    CNT_TICKET = 14,    // fast path (small call): fp_commit_small's finished tiles (the last one resets it)
+    CNT_TAILSEQ = 15,   // fast path (small call): the sequence number whose end fp_commit_small's last
+                        // tile stored itself (fp_tail then has nothing to do)
     CNT_DBG = 16,       // diagnostics (words 16-21): changed events by kind, summed over a call's passes
     CNT_NSIMPLE = 22,   // general path: events on the per-pass simple list (tr_lists)
     CNT_NCOMPLEX = 23,  // general path: events on the per-pass complex list

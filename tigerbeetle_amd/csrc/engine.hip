@@ -445,8 +445,6 @@ struct tbgpu_ctx {
         bool used = false;         // a prefetch has taken it (the first to reuse)
         u64 seq = 0;               // staging order
         hipEvent_t staged = nullptr;    // behind its copy (stage stream)
-        hipEvent_t released = nullptr; // behind the last launch that read it (engine stream)
-        bool release_recorded = false;
     } stg[TBGPU_STAGE_SLOTS];
     hipStream_t stage_stream = nullptr;
     u64 stage_seq = 0;
@@ -479,7 +477,6 @@ struct tbgpu_ctx {
 };
 
 enum { GW_GO = 0, GW_TS = 2, GW_ACK = 4, GW_WORDS = 8 };
-constexpr u32 GATE_CANCEL_BIT = 0x80000000u;
 
 // Release a prepared commit that will not be committed (any other call on the ctx): its
 // gate then lets nothing through, and the work behind it on the stream goes on.
@@ -842,7 +839,6 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
         if (S.d) { guard_release(S.d); (void)hipFree(S.d); }
         if (S.h) (void)hipHostFree(S.h);
         if (S.staged) (void)hipEventDestroy(S.staged);
-        if (S.released) (void)hipEventDestroy(S.released);
     }
     if (c->stage_stream) (void)hipStreamDestroy(c->stage_stream);
     (void)hipEventDestroy(c->ev0);
@@ -1099,13 +1095,21 @@ static bool try_fast(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 nb, tbgpu_crea
     static const bool no_eager = getenv("TBGPU_NO_EAGER") != nullptr;  // A/B timing: fp_dupcheck + inserts
     F.eager = (c->ids_nonmono && !F.dry && !no_eager) ? 1u : 0u;
     if (F.eager) c->eager_events += n;
-    F.gate = c->gate_arm ? c->gate_status : nullptr;
+    GateArgs ga{};
+    if (c->gate_arm) {  // a prepared commit (prepare_gated): the tiles wait for the commit call
+        F.gate = c->gate_status;
+        F.gate_seq = c->gate_seq;
+        ga = GateArgs{c->h_gate_dev + GW_GO, (const u64*)(c->h_gate_dev + GW_TS), c->h_gate_dev + GW_ACK, c->gate_budget};
+    }
     const BlockInline bi = take_block(c);
     prof_mark(c, PH_PREP);
     if (!F.small) fp_launch_prep(F, s, bi);
     prof_mark(c, PH_CLASSIFY);
     F.ev_copy = c->ev_in_host ? (Transfer*)c->ev_buf : nullptr;
-    fp_launch_commit(c->T, F, s, F.small ? bi : BlockInline{});
+    // the simple small call ends in fp_commit_small's last tile (TBGPU_NO_FUSE: A/B timing)
+    static const bool no_fuse = getenv("TBGPU_NO_FUSE") != nullptr;
+    F.fuse = (F.small && c->tail_rp.out && c->tail_rp.seq_out && !no_fuse) ? 1u : 0u;
+    fp_launch_commit(c->T, F, s, F.small ? bi : BlockInline{}, F.small ? c->tail_rp : TailReport{}, ga);
     ht_mark(c, 3);
     if (F.ev_copy) {  // the later launches read fp_commit's HBM copy of the events
         F.ev = F.ev_copy;
@@ -2267,43 +2271,14 @@ extern "C" int tbgpu_copy_to_device(tbgpu_ctx* c, void* dst_device, const void* 
     return 0;
 }
 
-// The prepared drop-in commit's gate: one lane waits for the commit call's word in
-// pinned host memory (bounded: budget wall-clock ticks), then writes the call's batch
-// block (one batch of n events at the timestamp the call brought) and the reply cursor's
-// reset, and its verdict for the gated kernels behind it on the stream; a gate that lets
-// nothing through (cancelled, or the call did not come in time) also tells the host.
-__global__ void k_gate(const u32* go, const u64* ts_word, u32* ack, u32 seq, u32 n, u32* block, u32 ts_off, u64* base,
-                       u32* status, u64 budget) {
-    if (threadIdx.x != 0) return;
-    const u64 t0 = wall_clock64();
-    u32 verdict = GATE_OFF;
-    for (;;) {
-        const u32 v = __hip_atomic_load(go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (v == seq) {
-            verdict = GATE_GO;
-            break;
-        }
-        if (v == (seq | GATE_CANCEL_BIT) || wall_clock64() - t0 > budget) break;
-        __builtin_amdgcn_s_sleep(16);
-    }
-    if (verdict == GATE_GO) {
-        const u64 ts = __hip_atomic_load(ts_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        block[0] = 0;
-        block[1] = n;
-        *(u64*)(block + ts_off) = ts;
-        base[BASE_REPLIES] = 0;
-    } else {
-        __hip_atomic_store(ack, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    *status = verdict;
-}
-
 // tbgpu_prefetch_transfers, when the commit that follows will be a one-batch fast call
 // (fp_commit_small + fp_tail): everything but the timestamp is known, so both launches
-// are enqueued now behind k_gate, and the commit call only writes its timestamp and
-// sequence number into pinned memory: no launch on its critical path.  Any other call
-// releases the gate (gate_cancel), and a gate that waits past its budget lets nothing
-// through; the commit then runs as an ordinary prefetched call.
+// are enqueued now, and fp_commit_small classifies the batch against the pre-call state
+// at once; its tiles then wait (fp_gate_wait) for the commit call, which only writes its
+// timestamp and sequence number into pinned memory: no launch, and only the state
+// changes and the call's end, on its critical path.  Any other call releases the gate
+// (gate_cancel), and tiles that wait past the budget change nothing; the commit then
+// runs as an ordinary prefetched call.
 static void prepare_gated(tbgpu_ctx* c, u32 n) {
     static const bool off = getenv("TBGPU_NO_GATE") != nullptr;  // A/B timing
     static const bool no_tail = getenv("TBGPU_NO_TAIL") != nullptr, no_small = getenv("TBGPU_NO_SMALL") != nullptr;
@@ -2318,10 +2293,7 @@ static void prepare_gated(tbgpu_ctx* c, u32 n) {
     const u32 seq = ++c->call_seq;
     c->h_gate[GW_ACK] = 0;
     __atomic_store_n(&c->h_gate[GW_GO], 0u, __ATOMIC_RELEASE);
-    k_gate<<<1, 64, 0, c->stream>>>(c->h_gate_dev + GW_GO, (const u64*)(c->h_gate_dev + GW_TS), c->h_gate_dev + GW_ACK,
-                                    seq, n, c->b_start, (u32)batch_ts_offset(1), c->T.base, c->gate_status,
-                                    c->gate_budget);
-    HIP_CHECK(hipGetLastError());
+    c->gate_seq = seq;
     c->tail_rp = TailReport{c->h_report_dev, 1, (const u64*)c->res_buf, c->h_res_dev,
                             c->h_report_dev + RPT_COUNTS + c->bmax, seq};
     c->tail_reported = false;
@@ -2422,7 +2394,6 @@ static void stage_init(tbgpu_ctx* c) {
     for (auto& S : c->stg) {
         S.d = dalloc<u8>((u64)TBGPU_BATCH_MAX * 128, &c->bytes);
         HIP_CHECK(hipEventCreateWithFlags(&S.staged, hipEventDisableTiming));
-        HIP_CHECK(hipEventCreateWithFlags(&S.released, hipEventDisableTiming));
     }
 }
 
@@ -2458,8 +2429,11 @@ extern "C" int tbgpu_stage_transfers(tbgpu_ctx* c, tbgpu_uint128_t key, const tb
     }
     auto& S = c->stg[pick];
     S.valid = false;
-    // the slot's last readers (a commit on the engine stream) come before its new copy
-    if (S.release_recorded) HIP_CHECK(hipStreamWaitEvent(c->stage_stream, S.released, 0));
+    // Nothing reads the slot any more: a slot is read only by the launches of a commit
+    // of its body, which have read it when that commit returns (a prepared commit's
+    // sequence word is the last store of its last launch that reads the events; an
+    // ordinary call waits for its launches; a released gate lets them read nothing),
+    // and the slot of the prefetch still pending was not picked.
     const u64 bytes = (u64)count * 128;
     const void* src = (c->opt.flags & TBGPU_OPT_PINNED_INPUT) ? pinned_device_ptr(events, bytes) : nullptr;
     if (!src) {
@@ -2508,19 +2482,7 @@ extern "C" int tbgpu_prefetch_transfers_staged(tbgpu_ctx* c, tbgpu_uint128_t key
     c->pf_valid = true;
     S.used = true;
     prepare_gated(c, count);
-    // the prepared launches read the slot; a commit that does not take them records the
-    // release again behind its own launches (stage_release)
-    HIP_CHECK(hipEventRecord(S.released, c->stream));
-    S.release_recorded = true;
     return 0;
-}
-
-// a commit (or anything else) read stage slot k on the engine stream: its next copy
-// comes after that
-static void stage_release(tbgpu_ctx* c, int k) {
-    if (k < 0) return;
-    HIP_CHECK(hipEventRecord(c->stg[k].released, c->stream));
-    c->stg[k].release_recorded = true;
 }
 
 extern "C" int tbgpu_prefetch_wait(tbgpu_ctx* c) {
@@ -2554,7 +2516,6 @@ extern "C" uint32_t tbgpu_create_transfers(tbgpu_ctx* c, uint64_t timestamp, con
         }
         // the gate let nothing through, or the attempt fell back: an ordinary call
         out = (uint32_t)transfers_batches(c, 1, &ts, &count, (const Transfer*)c->pf_dev, true, results, false, &rc);
-        stage_release(c, c->pf_slot);
         ht_mark(c, 7);
         c->ht_on = false;
         return out;
@@ -2564,7 +2525,6 @@ extern "C" uint32_t tbgpu_create_transfers(tbgpu_ctx* c, uint64_t timestamp, con
         // prefetched: the events are in HBM already (the copy is ahead on the stream)
         c->pf_valid = false;
         out = (uint32_t)transfers_batches(c, 1, &ts, &count, (const Transfer*)c->pf_dev, true, results, false, &rc);
-        stage_release(c, c->pf_slot);
     } else {
         c->pf_valid = false;
         out = (uint32_t)transfers_batches(c, 1, &ts, &count, (const Transfer*)events, false, results, false, &rc);

@@ -34,12 +34,26 @@ struct FastArgs {
     // fp_dupcheck, no inserts after; the fix moves a slot to its row's rank, a broken
     // chain withdraws its members' claims (XIDX_TOMB), a fallback clears every claim.
     u32 eager;
-    // A prepared drop-in commit (tbgpu_prefetch_transfers): the kernels were enqueued
-    // behind k_gate, which writes GATE_GO here once the commit call has come (with its
-    // timestamp), or GATE_OFF; both kernels do nothing unless GO.  Null: ungated.
-    const u32* gate;
+    // A prepared drop-in commit (tbgpu_prefetch_transfers): fp_commit_small is enqueued at
+    // prefetch time and classifies every event against the pre-call state right away
+    // (reads only; the timestamp enters only the last check, overflows_timeout, which is
+    // patched after); then each tile waits for the commit call's word in pinned memory
+    // (gate_go: gate_seq, or gate_seq | GATE_CANCEL_BIT; the timestamp in gate_ts), and
+    // the tiles agree on one verdict through the device word `gate` (tagged gate_seq << 2 |
+    // GATE_GO / GATE_OFF, set by the first tile to decide; an OFF winner also stores
+    // gate_seq into gate_ack).  Nothing changes state before GO.  fp_tail does nothing
+    // unless the tag is GO.  Null: ungated.
+    u32* gate;
+    u32 gate_seq;
+    // fp_commit_small's last tile ends a simple small call itself (no failure, no chain,
+    // no repeat check left, the rows taken by the sorted run or already claimed): the
+    // counters, cursors and the report with its sequence word, so the host's wait ends
+    // there; fp_tail, enqueued behind it as always, then returns at once.
+    u32 fuse;
 };
 constexpr u32 GATE_GO = 1, GATE_OFF = 2;
+constexpr u32 GATE_CANCEL_BIT = 0x80000000u;
+__host__ __device__ inline u32 gate_tag(u32 seq, u32 verdict) { return (seq << 2) | verdict; }
 // per tile: max lo, max hi, min lo, min hi of the accepted ids; max accepted timestamp;
 // accepted count; (fp_commit_small) failures and FL_* flags
 constexpr u32 TILE_WORDS = 8;
@@ -74,7 +88,17 @@ struct BlockInline {
     u32 w[BLOCK_INLINE_WORDS];
 };
 void fp_launch_prep(const FastArgs& F, hipStream_t stream, const BlockInline& bi = BlockInline{});
-void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream, const BlockInline& bi = BlockInline{});
+struct TailReport;
+// The prepared commit's words in pinned memory (FastArgs::gate), fp_commit_small's own
+// argument (fp_commit's arguments stay as they are: their size is its SGPR budget).
+struct GateArgs {
+    const u32* go;
+    const u64* ts;
+    u32* ack;
+    u64 budget;  // wall-clock ticks a tile waits before deciding OFF
+};
+void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream, const BlockInline& bi,
+                      const TailReport& rp, const GateArgs& ga = GateArgs{});
 void fp_launch_index(const Tables& T, const FastArgs& F, hipStream_t stream);
 void fp_launch_fix(const Tables& T, const FastArgs& F, u8* mask, uint4* ranks, Scan3Scratch& sc, hipStream_t stream);
 void fp_launch_undo(const Tables& T, const FastArgs& F, hipStream_t stream);

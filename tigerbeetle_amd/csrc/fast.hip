@@ -359,7 +359,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 #ifndef FP_WAVES_PER_EU
-#define FP_WAVES_PER_EU 5  // 3..5 measured alike, 7..8 slower (profiles/micro/README.md)
+#define FP_WAVES_PER_EU 6  // 6: 24 waves per CU, the LDS limit (+5-7 % over 5, profiles/r06/ab_waves.txt); 7..8 slower
 #endif
 // One tile of TILE events per workgroup.  Rows are stored optimistically at
 // row_base + event (every event accepted, the benchmark's case); failures are
@@ -369,8 +369,51 @@ __device__ __forceinline__ void wave_lds_sync() {
 // (its batch block comes in the kernel arguments, and the tile's flags and failure
 // count go to its tile record instead of the call's counters, which fp_tail sets
 // from the records: nothing here needs them reset first).
+__device__ void fp_small_tail(const Tables& T, const FastArgs& F, const BlockInline& bi, const TailReport& rp);
+
+// A prepared commit's gate, in each tile (one wave; lane 0 polls): the commit call's
+// timestamp once the tiles agree on GO, or ~0 when they agree on OFF (cancelled, or no
+// commit within the budget).  The first tile to decide sets the tagged verdict word by
+// CAS; the others follow it, so either every tile runs or none does.
+__device__ __forceinline__ u64 fp_gate_wait(const FastArgs& F, const GateArgs& G) {
+    u64 ts = ~0ull;
+    if ((threadIdx.x & 63) == 0) {
+        const u32 seq = F.gate_seq, tag_go = gate_tag(seq, GATE_GO), tag_off = gate_tag(seq, GATE_OFF);
+        const u64 t0 = wall_clock64();
+        u32 v = 0;
+        for (;;) {
+            // relaxed loads: an acquire at system scope invalidates the caches, which 128
+            // spinning tiles would do to each other's loads (and to the classify still
+            // running in other tiles) at every turn.  The timestamp is read after GO was
+            // seen, from the same coherent host memory the host wrote it to before GO.
+            u32 d = __hip_atomic_load(F.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (d == tag_go || d == tag_off) {
+                v = d;
+                break;
+            }
+            const u32 go = __hip_atomic_load(G.go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            u32 want = 0;
+            if (go == seq) want = tag_go;
+            else if (go == (seq | GATE_CANCEL_BIT) || wall_clock64() - t0 > G.budget) want = tag_off;
+            if (want) {
+                if (__hip_atomic_compare_exchange_strong(F.gate, &d, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)) {
+                    v = want;
+                    if (want == tag_off) __hip_atomic_store(G.ack, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                continue;  // another tile decided first: follow it
+            }
+            __builtin_amdgcn_s_sleep(4);
+        }
+        if (v == tag_go) ts = __hip_atomic_load(G.ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    return __shfl((unsigned long long)ts, 0);
+}
+
 template <int TILE, bool SMALL>
-__device__ __forceinline__ void fp_commit_body(const Tables& T, FastArgs F, const BlockInline& bi) {
+__device__ __forceinline__ void fp_commit_body(const Tables& T, FastArgs F, const BlockInline& bi,
+                                               const TailReport& rp = TailReport{}, const GateArgs& G = GateArgs{}) {
     constexpr int AGG = 4 * TILE;  // LDS aggregation table (2x the sides of a tile)
     __shared__ u64 s_maxts[TILE / 64];
     __shared__ u32 s_cnt[TILE / 64][2];
@@ -383,7 +426,8 @@ __device__ __forceinline__ void fp_commit_body(const Tables& T, FastArgs F, cons
 #if defined(FP_LDS_EVENTS)
     __shared__ uint4 s_stage[TILE / 64][STAGE_RECS * 8];
 #endif
-    if (SMALL && F.gate && *F.gate != GATE_GO) return;  // a prepared commit that did not come
+    // a prepared commit (SMALL only): classify now, change state once the commit has come
+    const bool gated = SMALL && F.gate != nullptr;
     const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const u32 tile = blockIdx.x;
     const u32 i = tile * TILE + tid;
@@ -454,7 +498,13 @@ __device__ __forceinline__ void fp_commit_body(const Tables& T, FastArgs F, cons
     const u32 i0 = __builtin_amdgcn_readfirstlane(wbase);
     Transfer t{};
     u32 bs = 0, nbatch = 0;
-    if (i0 < F.n) {
+    if (gated) {  // one batch; its timestamp comes with the commit (fp_gate_wait)
+        if (valid) {
+            b = 0;
+            bs = 0;
+            nbatch = F.n;
+        }
+    } else if (i0 < F.n) {
         const u32 b0 = fp_batch_of(F.b_start, F.nb, i0);
         const u32 s0 = F.b_start[b0], e0 = F.b_start[b0 + 1];
         const u64 t0 = F.ev_ts ? 0 : F.b_ts[b0];
@@ -538,13 +588,40 @@ __device__ __forceinline__ void fp_commit_body(const Tables& T, FastArgs F, cons
 #else
 #define STORE_ROW() do { if (!(FP_ABLATE & ABL_ROWS)) T.xrows[row_base + i] = t; } while (0)
 #endif
+    u32 ds = NONE32, cs = NONE32;
+    u64 xend = 0;  // where an eager claim starts (fp_classify)
+#define FP_CLASSIFY()                                                                                                \
+    do {                                                                                                             \
+        id = t.id;                                                                                                   \
+        xend = xidx_hash(t.id) & T.xidx_mask;                                                                        \
+        if (lk && i - bs == nbatch - 1) r = TBGPU_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN; /* checked first (:1024) */ \
+        else if (myctl & TBGPU_CTL_SKIP) r = TBGPU_CREATE_TRANSFER_LINKED_EVENT_FAILED; /* broken on another shard */  \
+        else r = fp_classify(T, F, t, i, ts, row_base, &ds, &cs, &xend);                                             \
+    } while (0)
+    if (SMALL && valid) FP_CLASSIFY();  // (gated: ts 0 until the commit)
+    if (gated) {
+        // everything above only read the pre-call state (the previous commit's launches
+        // are done: they precede these on the stream); state changes only after GO
+        const u64 T0 = fp_gate_wait(F, G);
+        if (T0 == ~0ull) return;  // the commit did not come: nothing was changed
+        if (tile == 0 && tid == 0) {
+            // the batch block and the reply cursor for the launches after this one
+            ((u32*)F.b_start)[0] = 0;
+            ((u32*)F.b_start)[1] = F.n;
+            *(u64*)F.b_ts = T0;
+            T.base[BASE_REPLIES] = 0;
+        }
+        if (valid) {
+            ts = T0 - F.n + i + 1;
+            // overflows_timeout, the last check of create_transfer (:1323-1325) and the only
+            // one that reads the timestamp: classify ran with 0, where it never fires
+            if (r == TBGPU_CREATE_TRANSFER_OK && t.timeout != 0 && sum_overflows64(ts, (u64)t.timeout * NS_PER_S))
+                r = TBGPU_CREATE_TRANSFER_OVERFLOWS_TIMEOUT;
+        }
+    }
     if (valid) {
-        id = t.id;
-        u32 ds = NONE32, cs = NONE32;
-        u64 xend = xidx_hash(t.id) & T.xidx_mask;  // where an eager claim starts (fp_classify)
-        if (lk && i - bs == nbatch - 1) r = TBGPU_CREATE_TRANSFER_LINKED_EVENT_CHAIN_OPEN;  // checked first (:1024)
-        else if (myctl & TBGPU_CTL_SKIP) r = TBGPU_CREATE_TRANSFER_LINKED_EVENT_FAILED;    // broken on another shard
-        else r = fp_classify(T, F, t, i, ts, row_base, &ds, &cs, &xend);
+        if (!SMALL) FP_CLASSIFY();
+#undef FP_CLASSIFY
         own_ok = r == TBGPU_CREATE_TRANSFER_OK;
         if (F.eager) {
             u32 slot = NONE32;
@@ -705,6 +782,20 @@ __device__ __forceinline__ void fp_commit_body(const Tables& T, FastArgs F, cons
             if (hi + c >= (1ull << 62)) atomicOr(T.big, 1u);  // later calls must prove no overflow
         }
     }
+    if constexpr (SMALL) {
+        if (F.fuse) {
+            // the last tile to finish (one wave per tile: its fence covers its record)
+            static_assert(!SMALL || TILE == 64, "one wave per small tile");
+            const u32 ntiles = (F.n + TILE - 1) / TILE;
+            __threadfence();
+            u32 t = 0;
+            if (lane == 0) t = atomicAdd(&F.counters[CNT_TICKET], 1u);
+            t = __shfl(t, 0);
+            if (t != ntiles - 1) return;
+            __threadfence();  // (acquire: the other tiles' records)
+            fp_small_tail(T, F, bi, rp);
+        }
+    }
 }
 
 __global__ __launch_bounds__(FP_THREADS) __attribute__((amdgpu_waves_per_eu(FP_WAVES_PER_EU)))
@@ -712,8 +803,9 @@ void fp_commit(Tables T, FastArgs F) {
     fp_commit_body<FP_THREADS, false>(T, F, BlockInline{});
 }
 
-__global__ __launch_bounds__(FP_SMALL_TILE) void fp_commit_small(Tables T, FastArgs F, BlockInline bi) {
-    fp_commit_body<FP_SMALL_TILE, true>(T, F, bi);
+__global__ __launch_bounds__(FP_SMALL_TILE) void fp_commit_small(Tables T, FastArgs F, BlockInline bi, TailReport rp,
+                                                                 GateArgs G) {
+    fp_commit_body<FP_SMALL_TILE, true>(T, F, bi, rp, G);
 }
 
 // Only when the call's ids were not increasing: claim every accepted id once.
@@ -1037,6 +1129,114 @@ __global__ void fp_prep(FastArgs F, BlockInline bi) {
     if (k < F.nb) F.batch_counts[k] = 0;
 }
 
+// The simple small call's end, by fp_commit_small's last tile (one wave, F.fuse): the
+// tiles' records say no event failed, none is a chain member and no repeat check is
+// left (ids rising, or claimed eagerly), and either the rows extend the sorted run or
+// their ids are claimed already: then fp_tail's phases reduce to counters, the run's
+// bounds or the key range, the cursors and the report, done here in one round of loads
+// and one of stores, and the host's wait ends without the kernel boundary and fp_tail's
+// launch.  Otherwise nothing is written (fp_tail does the whole tail, as without F.fuse).
+__device__ void fp_small_tail(const Tables& T, const FastArgs& F, const BlockInline& bi, const TailReport& rp) {
+    const u32 lane = threadIdx.x & 63, n = F.n;
+    const u32 ntiles = (n + F.tile - 1) / F.tile;
+    auto ld64 = [](const u64* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    // one round of loads: the tiles' records (every lane), and in lane 0 what the run
+    // decision and the cursors need
+    u32 fl = 0, nbad = 0, nok = 0;
+    u64 mts = 0;
+    for (u32 k = lane; k < ntiles; k += 64) {
+        const u64* r = F.tile_idr + TILE_WORDS * k;
+        mts = max(mts, ld64(r + 4));
+        nok += (u32)ld64(r + 5);
+        nbad += (u32)ld64(r + 6);
+        fl |= (u32)ld64(r + 7);
+    }
+    u64 xr[6] = {0, 0, 0, 0, 0, 0}, b[4] = {0, 0, 0, 0}, cts = 0;
+    u128 first = 0, last = 0;
+    if (lane == 0) {
+        for (int k = 0; k < 6; k++) xr[k] = ld64(T.xrun + k);
+        for (int k = 0; k < 4; k++) b[k] = ld64(T.base + k);
+        cts = ld64(F.commit_ts);
+        first = F.ev[0].id;
+        last = F.ev[n - 1].id;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        nbad += __shfl_xor(nbad, off);
+        nok += __shfl_xor(nok, off);
+        fl |= __shfl_xor(fl, off);
+        mts = max(mts, (u64)__shfl_xor((unsigned long long)mts, off));
+    }
+    // what fp_tail would decide (fp_run_one), without writing anything yet
+    u32 take = 0, ok = 0;
+    if (lane == 0) {
+        const bool simple = !(fl & (FL_SLOW | FL_ERROR | FL_FCHAIN)) && nbad == 0 && (!(fl & FL_NONMONO) || F.eager);
+        if (simple && !F.eager && n && !(fl & FL_NONMONO)) {
+            const bool empty = xr[0] == xr[1];
+            take = (empty || (xr[1] == b[BASE_ROWS] && first > (((u128)xr[5] << 64) | xr[4]))) ? 1u : 0u;
+        }
+        ok = simple && (take || F.eager) && rp.out && rp.seq_out && !F.dry ? 1u : 0u;
+    }
+    ok = __shfl(ok, 0);
+    take = __shfl(take, 0);
+    if (!ok) {
+        if (lane == 0) __hip_atomic_store(&F.counters[CNT_TICKET], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;  // fp_tail ends the call
+    }
+    // the stores: fp_prep's (the batch block, the reply counts), the counters, the run or
+    // the key range, the cursors
+    if (lane < bi.words) bi.block[lane] = bi.w[lane];
+    for (u32 k = lane; k < F.nb; k += 64) F.batch_counts[k] = 0;
+    if (!take) {  // (eager: the claims are the index inserts) the tiles' id ranges into T.idr
+        for (u32 k0 = 0; k0 < ntiles; k0 += 64) fp_fold_idr(T, F, k0, ntiles);
+    }
+    if (lane == 0) {
+        const u32 nokeys = F.counters[CNT_NOKEYS];
+        for (int k = 0; k < CNT_TS_SAVE; k++) F.counters[k] = 0;
+        F.counters[CNT_NOKEYS] = nokeys;
+        F.counters[CNT_FLAGS] = fl;
+        F.counters[CNT_OK] = nok;
+        F.counters[CNT_RUN] = take;
+        *(u64*)&F.counters[CNT_TS_SAVE] = cts;
+        if (mts > cts) *F.commit_ts = mts;
+        if (take) {
+            u64* r = T.xrun;
+            if (xr[0] == xr[1]) {
+                r[0] = b[BASE_ROWS];
+                r[2] = (u64)first;
+                r[3] = (u64)(first >> 64);
+            }
+            r[1] = b[BASE_ROWS] + n;
+            r[4] = (u64)last;
+            r[5] = (u64)(last >> 64);
+        }
+        if ((bi.words && bi.reset_replies) || F.gate) b[BASE_REPLIES] = 0;  // (a prepared commit's starts at 0)
+        b[BASE_ROWS] += nok;
+        T.base[BASE_REPLIES] = b[BASE_REPLIES];
+        T.base[BASE_ROWS] = b[BASE_ROWS];
+    }
+    for (int k = 0; k < 4; k++) b[k] = __shfl(b[k], 0);  // (lane 0's cursors, for the report)
+    // the report (k_report's words: flags, accepted, run; the cursors; no replies), then
+    // the sequence word once the report is visible to the host
+    for (u32 k = lane; k < RPT_COUNTS + rp.nb; k += 64) {
+        u32 v = 0;
+        if (k == CNT_FLAGS) v = fl;
+        else if (k == CNT_OK) v = nok;
+        else if (k == CNT_RUN) v = take;
+        else if (k >= RPT_BASE && k < RPT_COUNTS) {
+            const u32 w = k - RPT_BASE;
+            const u64 bw = (w >> 1) == 0 ? b[0] : (w >> 1) == 1 ? b[1] : (w >> 1) == 2 ? b[2] : b[3];
+            v = (w & 1) ? (u32)(bw >> 32) : (u32)bw;
+        }
+        rp.out[k] = v;
+    }
+    __threadfence_system();
+    if (lane == 0) {
+        __hip_atomic_store(&F.counters[CNT_TAILSEQ], rp.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&F.counters[CNT_TICKET], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(rp.seq_out, rp.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // Small calls (n <= FP_TAIL_MAX, e.g. one drop-in batch of 8190): everything after
 // fp_commit in ONE workgroup, the launches of fp_launch_index, fp_launch_fix and
 // fp_launch_advance run as phases separated by barriers.  A batch of 8190 events
@@ -1050,7 +1250,9 @@ __device__ __forceinline__ u32 fp_cnt(const FastArgs& F, int k) {
 }
 
 __global__ __launch_bounds__(FP_TAIL_THREADS) void fp_tail(Tables T, FastArgs F, BlockInline bi, TailReport rp) {
-    if (F.gate && *F.gate != GATE_GO) return;  // a prepared commit that did not come
+    if (F.gate && __hip_atomic_load(F.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gate_tag(F.gate_seq, GATE_GO))
+        return;  // a prepared commit that did not come
+    if (F.fuse && fp_cnt(F, CNT_TAILSEQ) == rp.seq) return;  // fp_commit_small's last tile ended the call
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6, n = F.n;
     const u32 ntiles = (n + F.tile - 1) / F.tile;
     __shared__ u32 s_flags, s_bad, s_run, s_ok, s_fix;
@@ -1295,9 +1497,10 @@ void fp_launch_prep(const FastArgs& F, hipStream_t stream, const BlockInline& bi
     HIP_CHECK(hipGetLastError());
 }
 
-void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream, const BlockInline& bi) {
+void fp_launch_commit(const Tables& T, const FastArgs& F, hipStream_t stream, const BlockInline& bi,
+                      const TailReport& rp, const GateArgs& ga) {
     if (F.small) {
-        fp_commit_small<<<(F.n + FP_SMALL_TILE - 1) / FP_SMALL_TILE, FP_SMALL_TILE, 0, stream>>>(T, F, bi);
+        fp_commit_small<<<(F.n + FP_SMALL_TILE - 1) / FP_SMALL_TILE, FP_SMALL_TILE, 0, stream>>>(T, F, bi, rp, ga);
     } else {
         fp_commit<<<(F.n + FP_THREADS - 1) / FP_THREADS, FP_THREADS, 0, stream>>>(T, F);
     }

@@ -198,9 +198,12 @@ def test_staged_bodies_commit_in_order(mix, pinned, depth):
 def test_stage_key_mismatch_and_interleaved_calls():
     """A prefetch whose key no slot holds (or whose count differs) copies its body; a
     stage call between a prefetch and its commit does not release the prepared commit
-    and does not disturb it; a lookup in between does release it.  Replies equal the
-    oracle's throughout."""
-    w = workload.config1(transfer_count=8190 * 6, account_count=500, seed=13)
+    and does not disturb it (its own prepared commit queues behind, and is dropped when
+    the next prefetch names another body); a lookup in between does release it; staged
+    commits whose gates ran out (the commit came after the budget) take the ordinary
+    path.  Replies equal the oracle's throughout."""
+    import time
+    w = workload.config1(transfer_count=8190 * 8, account_count=500, seed=13)
     orc, gpu = oracle.Oracle(len(w.accounts), len(w.transfers)), _engine(w)
     try:
         ats, tts = w.timestamps()
@@ -214,6 +217,13 @@ def test_stage_key_mismatch_and_interleaved_calls():
                 gpu.prefetch_transfers_staged(100, ev)
             elif b == 1:
                 gpu.prefetch_transfers_staged(555, ev)  # never staged
+            elif b == 5:
+                for k in range(3):  # three prepared commits queued ...
+                    gpu.stage_transfers(500 + b + k, bs[b + k])
+                time.sleep(0.05)    # ... whose gates all run out before the commits come
+                gpu.prefetch_transfers_staged(500 + b, ev)
+            elif b in (6, 7):
+                gpu.prefetch_transfers_staged(500 + b, ev)
             else:
                 gpu.stage_transfers(200 + b, ev)
                 gpu.prefetch_transfers_staged(200 + b, ev)

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <vector>
 
@@ -387,6 +388,19 @@ struct tbgpu_ctx {
     bool gate_pending = false;  // a prepared commit is enqueued and not yet released or cancelled
     bool gate_arm = false;      // try_fast: gate the kernels it launches on gate_status
     u32 gate_seq = 0, gate_n = 0;
+    // Prepared commits of staged bodies (tbgpu_stage_transfers), enqueued at prepare
+    // time behind the current one, in commit order: each classifies its batch once the
+    // commits before it have run, then waits for its own commit call.
+    struct Prepared {
+        u32 seq, n;
+        int slot;
+        u64 key_lo, key_hi;
+        FastArgs F;
+        TailReport rp;
+    };
+    std::deque<Prepared> pq;
+    u64 pq_events = 0;  // their events (rows they may take)
+    u32 gate_last = 0;  // the newest prepared commit's sequence number (a cancel covers it and all before)
     u64 gate_budget = 0;        // wall-clock ticks a gate waits before letting nothing through
     u32 last_passes = 8;  // passes the last fixed point took (sizes the next pass group)
     bool long_segments = false;  // this call has an account segment too long for the fused scan
@@ -480,12 +494,26 @@ enum { GW_GO = 0, GW_TS = 2, GW_ACK = 4, GW_WORDS = 8 };
 
 // Release a prepared commit that will not be committed (any other call on the ctx): its
 // gate then lets nothing through, and the work behind it on the stream goes on.
+// The queued ones behind it go too (their batches were classified against a state the
+// released commit would have left).  The word only ever grows: a release is the next
+// sequence number, a cancel covers every sequence number up to the newest prepared.
 static void gate_cancel(tbgpu_ctx* c) {
-    if (!c->gate_pending) return;
-    c->gate_pending = false;
-    c->spec_pending = false;
-    c->tail_reported = false;
-    __atomic_store_n(&c->h_gate[GW_GO], c->gate_seq | GATE_CANCEL_BIT, __ATOMIC_RELEASE);
+    if (!c->gate_pending && c->pq.empty()) return;
+    if (c->gate_pending) {
+        c->gate_pending = false;
+        c->spec_pending = false;
+        c->tail_reported = false;
+    }
+    c->pq.clear();
+    c->pq_events = 0;
+    __atomic_store_n(&c->h_gate[GW_GO], c->gate_last | GATE_CANCEL_BIT, __ATOMIC_RELEASE);
+}
+
+// The next call sequence number (31 bits, never 0: the gate word's top bit marks a cancel).
+static u32 next_seq(tbgpu_ctx* c) {
+    c->call_seq = (c->call_seq + 1) & ~GATE_CANCEL_BIT;
+    if (c->call_seq == 0) c->call_seq = 1;
+    return c->call_seq;
 }
 
 // Entry guard (tbgpu.h "Concurrency"): a ctx serves one caller at a time, except that
@@ -675,6 +703,8 @@ extern "C" void tbgpu_set_profiling(tbgpu_ctx* c, int enable) {
     c->prof_phase.clear();
 }
 
+static void stage_init(tbgpu_ctx* c);
+
 extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     *out = nullptr;
     tbgpu_options o{};
@@ -722,7 +752,7 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     c->T.idr = dalloc<u64>(4, &B);
     c->T.xrun = dalloc<u64>(8, &B);
     c->T.big = dalloc<u32>(4, &B);
-    c->gate_status = dalloc<u32>(1, &B);
+    c->gate_status = dalloc<u32>(4, &B);  // the prepared commit's verdict, and its timestamp at [2..3]
     c->T.hcount = c->T.big + 1;        // [1] entries, [2] refused, [3] transfer-id tombstones
     c->T.hash_limit = c->aidx_cap / 2;  // load <= 0.5
     c->T.base = dalloc<u64>(4, &B);
@@ -743,6 +773,7 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     }
     c->T.dense = dalloc_hot<u64>(c->T.dense_n, &B);
     alloc_scratch(c, o.events_per_call_max);
+    stage_init(c);
     tbgpu_reset(c);
     *out = c;
     return 0;
@@ -1886,7 +1917,7 @@ static uint64_t transfers_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_
         c->tail_reported = false;
         if (b1 == nb_total)
             c->tail_rp = TailReport{c->h_report_dev, nb, (const u64*)c->res_buf, dst_device ? nullptr : c->h_res_dev,
-                                    c->h_report_dev + RPT_COUNTS + c->bmax, ++c->call_seq};
+                                    c->h_report_dev + RPT_COUNTS + c->bmax, next_seq(c)};
         const bool stood = run_transfers_chunk(c, ev, n, nb, rdev, try_fast_path,
                                                /*split=*/!c->rt_dry && nb > general_chunk_batches(), spec);
         c->ev_in_host = false;
@@ -2279,33 +2310,65 @@ extern "C" int tbgpu_copy_to_device(tbgpu_ctx* c, void* dst_device, const void* 
 // changes and the call's end, on its critical path.  Any other call releases the gate
 // (gate_cancel), and tiles that wait past the budget change nothing; the commit then
 // runs as an ordinary prefetched call.
-static void prepare_gated(tbgpu_ctx* c, u32 n) {
+static bool prepare_ok(const tbgpu_ctx* c, u32 n) {
     static const bool off = getenv("TBGPU_NO_GATE") != nullptr;  // A/B timing
     static const bool no_tail = getenv("TBGPU_NO_TAIL") != nullptr, no_small = getenv("TBGPU_NO_SMALL") != nullptr;
-    if (off || no_tail || no_small || n == 0 || n > FP_TAIL_MAX || c->prof || c->rt_dry ||
-        (c->opt.flags & TBGPU_OPT_FORCE_GENERAL) || spec_disabled() || !fast_due(c) || c->rows_hi + n > c->xrow_cap)
-        return;
-    ensure_h_rc(c, 1);
+    return !(off || no_tail || no_small || n == 0 || n > FP_TAIL_MAX || c->prof || c->rt_dry ||
+             (c->opt.flags & TBGPU_OPT_FORCE_GENERAL) || spec_disabled() || !fast_due(c));
+}
+
+// Enqueue a prepared commit of n events at `ev` (in HBM) with sequence number `seq`: the
+// current commit's host state (spec_F, tail_rp, ...) is left describing it.
+static void prepare_launch(tbgpu_ctx* c, const Transfer* ev, u32 n, u32 seq) {
     c->rt_ev_ts = nullptr;
     c->rt_ctl = nullptr;
-    c->blk_words = 0;  // the gate writes the block
+    c->blk_words = 0;  // the gated tiles write the block
     c->b_ts = (u64*)(c->b_start + batch_ts_offset(1));
-    const u32 seq = ++c->call_seq;
-    c->h_gate[GW_ACK] = 0;
-    __atomic_store_n(&c->h_gate[GW_GO], 0u, __ATOMIC_RELEASE);
     c->gate_seq = seq;
     c->tail_rp = TailReport{c->h_report_dev, 1, (const u64*)c->res_buf, c->h_res_dev,
                             c->h_report_dev + RPT_COUNTS + c->bmax, seq};
     c->tail_reported = false;
     c->gate_arm = true;
-    const bool launched = try_fast(c, (const Transfer*)c->pf_dev, n, 1, (tbgpu_create_transfers_result_t*)c->res_buf,
-                                   /*spec=*/true);
+    const bool launched = try_fast(c, ev, n, 1, (tbgpu_create_transfers_result_t*)c->res_buf, /*spec=*/true);
     c->gate_arm = false;
     if (!launched || !c->tail_reported)
         tbgpu_fatal("prefetch", "a prepared commit did not take the small fast launches", __FILE__, __LINE__);
+    c->gate_last = seq;
+}
+
+static void prepare_gated(tbgpu_ctx* c, u32 n) {
+    if (!prepare_ok(c, n) || c->rows_hi + n > c->xrow_cap) return;
+    ensure_h_rc(c, 1);
+    prepare_launch(c, (const Transfer*)c->pf_dev, n, next_seq(c));
     c->gate_pending = true;
-    c->gate_seq = seq;
     c->gate_n = n;
+}
+
+// tbgpu_stage_transfers: the staged body's commit prepared at once, behind the current
+// and the queued ones (no host round trip: the engine stream may be held by a gate).
+static void stage_prepare(tbgpu_ctx* c, int k, u32 n) {
+    const u64 ahead = c->pq_events + (c->gate_pending ? c->gate_n : 0);
+    if (!prepare_ok(c, n) || c->pq.size() + 2 > TBGPU_STAGE_SLOTS || c->h_rc_cap < 1 ||
+        c->rows_hi + ahead + n > c->xrow_cap)
+        return;
+    auto& S = c->stg[k];
+    // the current prepared commit's host state, kept
+    const FastArgs sF = c->spec_F;
+    const bool sP = c->spec_pending, sT = c->tail_reported;
+    const TailReport sR = c->tail_rp;
+    const u32 sG = c->gate_seq;
+    const tbgpu_stats sS = c->stats;
+    if (hipEventQuery(S.staged) != hipSuccess) HIP_CHECK(hipStreamWaitEvent(c->stream, S.staged, 0));
+    const u32 seq = next_seq(c);
+    prepare_launch(c, (const Transfer*)S.d, n, seq);
+    c->pq.push_back(tbgpu_ctx::Prepared{seq, n, k, S.key_lo, S.key_hi, c->spec_F, c->tail_rp});
+    c->pq_events += n;
+    c->spec_F = sF;
+    c->spec_pending = sP;
+    c->tail_reported = sT;
+    c->tail_rp = sR;
+    c->gate_seq = sG;
+    c->stats = sS;
 }
 
 // The commit of a prepared call: release the gate with the timestamp, then wait for
@@ -2336,11 +2399,13 @@ static bool commit_gated(tbgpu_ctx* c, u64 timestamp, tbgpu_create_transfers_res
     c->tail_reported = false;
     if (!go) {
         c->spec_pending = false;
+        gate_cancel(c);  // the queued commits classified against the state this one would have left
         return false;
     }
     memcpy(c->h_counters, c->h_report, CNT_COUNT * sizeof(u32));
     memcpy(c->h_base, c->h_report + RPT_BASE, 4 * sizeof(u64));
     memcpy(c->h_rc, c->h_report + RPT_COUNTS, sizeof(u32));
+    if (c->h_counters[CNT_FLAGS] & (FL_SLOW | FL_ERROR)) gate_cancel(c);  // (before the undo waits behind them)
     if (!spec_settle(c)) return false;
     // the call's replies only (none when every event is ok): the count fp_tail reported
     const std::vector<u32> starts = {0u, n};
@@ -2413,20 +2478,27 @@ extern "C" int tbgpu_stage_transfers(tbgpu_ctx* c, tbgpu_uint128_t key, const tb
     stage_init(c);
     if (stage_find(c, key, count) >= 0) return 0;  // the same content is staged already
     // the slot: a free one, else the oldest a prefetch has taken, else the oldest; never
-    // the one the pending prefetch reads
+    // the one the pending prefetch reads or one a queued prepared commit will read
     int pick = -1;
-    for (int pass = 0; pass < 3 && pick < 0; pass++) {
-        u64 best = ~0ull;
-        for (int k = 0; k < (int)TBGPU_STAGE_SLOTS; k++) {
-            const auto& S = c->stg[k];
-            if (c->pf_valid && c->pf_slot == k) continue;
-            const bool fits = pass == 0 ? !S.valid : pass == 1 ? S.used : true;
-            if (fits && S.seq < best) {
-                best = S.seq;
-                pick = k;
+    for (int round = 0; round < 2 && pick < 0; round++) {
+        if (round == 1) gate_cancel(c);  // every slot is spoken for: the queued commits go
+        for (int pass = 0; pass < 3 && pick < 0; pass++) {
+            u64 best = ~0ull;
+            for (int k = 0; k < (int)TBGPU_STAGE_SLOTS; k++) {
+                const auto& S = c->stg[k];
+                if (c->pf_valid && c->pf_slot == k) continue;
+                bool queued = false;
+                for (const auto& p : c->pq) queued |= p.slot == k;
+                if (queued) continue;
+                const bool fits = pass == 0 ? !S.valid : pass == 1 ? S.used : true;
+                if (fits && S.seq < best) {
+                    best = S.seq;
+                    pick = k;
+                }
             }
         }
     }
+    if (pick < 0) tbgpu_fatal("stage", "no stage slot", __FILE__, __LINE__);
     auto& S = c->stg[pick];
     S.valid = false;
     // Nothing reads the slot any more: a slot is read only by the launches of a commit
@@ -2460,13 +2532,36 @@ extern "C" int tbgpu_stage_transfers(tbgpu_ctx* c, tbgpu_uint128_t key, const tb
     S.used = false;
     S.seq = ++c->stage_seq;
     S.valid = true;
+    stage_prepare(c, pick, count);
     return 0;
 }
 
 extern "C" int tbgpu_prefetch_transfers_staged(tbgpu_ctx* c, tbgpu_uint128_t key, const tbgpu_transfer_t* events,
                                                uint32_t count) {
-    CallGuard guard_(c, false);  // (releases an earlier prepared commit)
+    CallGuard guard_(c, false, /*keep_gate=*/true);
     if (count > TBGPU_BATCH_MAX) return -22;
+    if (!c->gate_pending && !c->pq.empty() && c->pq.front().key_lo == key.lo && c->pq.front().key_hi == key.hi &&
+        c->pq.front().n == count) {
+        // its commit was prepared when it was staged: it becomes the current one
+        const tbgpu_ctx::Prepared p = c->pq.front();
+        c->pq.pop_front();
+        c->pq_events -= p.n;
+        c->pf_src = events;
+        c->pf_n = count;
+        c->pf_dev = c->stg[p.slot].d;
+        c->pf_slot = p.slot;
+        c->pf_valid = true;
+        c->stg[p.slot].used = true;
+        c->gate_pending = true;
+        c->gate_seq = p.seq;
+        c->gate_n = p.n;
+        c->spec_F = p.F;
+        c->spec_pending = true;
+        c->tail_rp = p.rp;
+        c->tail_reported = true;
+        return 0;
+    }
+    gate_cancel(c);  // (what is queued is not what commits next)
     const int k = c->stage_stream ? stage_find(c, key, count) : -1;
     if (k < 0) return tbgpu_prefetch_transfers(c, events, count);  // not staged: copy it now
     c->pf_valid = false;

@@ -373,30 +373,40 @@ __device__ void fp_small_tail(const Tables& T, const FastArgs& F, const BlockInl
 
 // A prepared commit's gate, in each tile (one wave; lane 0 polls): the commit call's
 // timestamp once the tiles agree on GO, or ~0 when they agree on OFF (cancelled, or no
-// commit within the budget).  The first tile to decide sets the tagged verdict word by
-// CAS; the others follow it, so either every tile runs or none does.
+// commit within the budget).  Tile 0 alone polls the host's word (128 tiles reading
+// pinned memory in a loop slowed the whole call down), and publishes the timestamp in
+// device memory, then the verdict, tagged with the call's sequence number, by CAS; the
+// other tiles poll that device word.  Any tile whose budget runs out first sets OFF by
+// the same CAS, so either every tile runs or none does.
 __device__ __forceinline__ u64 fp_gate_wait(const FastArgs& F, const GateArgs& G) {
     u64 ts = ~0ull;
     if ((threadIdx.x & 63) == 0) {
         const u32 seq = F.gate_seq, tag_go = gate_tag(seq, GATE_GO), tag_off = gate_tag(seq, GATE_OFF);
+        const bool poller = blockIdx.x == 0;
+        u64* ts_dev = (u64*)(F.gate + 2);  // (8-byte aligned: the gate words are u32[4])
         const u64 t0 = wall_clock64();
         u32 v = 0;
         for (;;) {
-            // relaxed loads: an acquire at system scope invalidates the caches, which 128
-            // spinning tiles would do to each other's loads (and to the classify still
-            // running in other tiles) at every turn.  The timestamp is read after GO was
-            // seen, from the same coherent host memory the host wrote it to before GO.
             u32 d = __hip_atomic_load(F.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (d == tag_go || d == tag_off) {
                 v = d;
                 break;
             }
-            const u32 go = __hip_atomic_load(G.go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             u32 want = 0;
-            if (go == seq) want = tag_go;
-            else if (go == (seq | GATE_CANCEL_BIT) || wall_clock64() - t0 > G.budget) want = tag_off;
+            u64 t_go = 0;
+            if (poller) {
+                const u32 go = __hip_atomic_load(G.go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (go == seq) {
+                    want = tag_go;
+                    t_go = __hip_atomic_load(G.ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(ts_dev, t_go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else if ((go & GATE_CANCEL_BIT) && ((go - seq) & ~GATE_CANCEL_BIT) < (GATE_CANCEL_BIT >> 1)) {
+                    want = tag_off;  // a cancel of every prepared commit up to a sequence >= ours
+                }
+            }
+            if (!want && wall_clock64() - t0 > G.budget) want = tag_off;
             if (want) {
-                if (__hip_atomic_compare_exchange_strong(F.gate, &d, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                if (__hip_atomic_compare_exchange_strong(F.gate, &d, want, __ATOMIC_RELEASE, __ATOMIC_RELAXED,
                                                          __HIP_MEMORY_SCOPE_AGENT)) {
                     v = want;
                     if (want == tag_off) __hip_atomic_store(G.ack, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -404,9 +414,13 @@ __device__ __forceinline__ u64 fp_gate_wait(const FastArgs& F, const GateArgs& G
                 }
                 continue;  // another tile decided first: follow it
             }
-            __builtin_amdgcn_s_sleep(4);
+            if (poller) __builtin_amdgcn_s_sleep(2);
+            else __builtin_amdgcn_s_sleep(8);
         }
-        if (v == tag_go) ts = __hip_atomic_load(G.ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (v == tag_go) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (the poller's timestamp store before its CAS)
+            ts = __hip_atomic_load(ts_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     return __shfl((unsigned long long)ts, 0);
 }

@@ -257,6 +257,11 @@ enum {
                                           are read in place and uploads skip the staging
                                           ring.  Without it every host buffer is copied
                                           through the ctx's page-locked ring. */
+    TBGPU_OPT_DENSE_INDEXES = 1u << 3, /* size the account and transfer-id hash indexes at
+                                          load <= 1/2 (2 slots per id of capacity) instead of
+                                          the default <= 1/8 (8 slots, while an index stays
+                                          within 1 GiB / 8 GiB): a quarter of the memory, a
+                                          second probe more often (random u128 ids) */
 };
 
 /* Replaces StateMachine.init/deinit (src/state_machine.zig:418-451).

@@ -273,7 +273,8 @@ def test_withdrawn_id_claims_rebuild_the_index():
         if rng.random() < 0.8:
             t[i + 1]["credit_account_id_lo"] ^= np.uint64(0x5A5A)  # no such account
     orc = oracle.Oracle(len(w.accounts), len(w.transfers))
-    gpu = _engine(transfers_max=1 << 13, history_max=1 << 10, events_per_call_max=1 << 12)
+    # (load <= 1/2: the tombstones reach 1/16 of the slots within the workload)
+    gpu = _engine(transfers_max=1 << 13, history_max=1 << 10, events_per_call_max=1 << 12, dense_indexes=True)
     try:
         oa, ot = run_workload(orc, w)
         ga, gt = run_workload(gpu, w, split=1)

@@ -734,9 +734,22 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     HIP_CHECK(hipEventCreateWithFlags(&c->ev_lists, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&c->ev_group, hipEventDisableTiming));
     c->accounts_max = o.accounts_max;
-    c->aidx_cap = pow2_at_least(2 * o.hashed_max);  // ids outside the direct-mapped directory
+    // ids outside the direct-mapped directory, at load <= 1/8 while the index stays within
+    // 1 GiB (a probe's first slot then nearly always decides it: one dependent load for a
+    // random u128 id), else <= 1/2 (TBGPU_OPT_DENSE_INDEXES, or TBGPU_AIDX_LOAD2 for A/B
+    // timing: <= 1/2 always)
+    static const bool load2 = getenv("TBGPU_AIDX_LOAD2") != nullptr;
+    c->aidx_cap = pow2_at_least(2 * o.hashed_max);
+    if (!load2 && !(o.flags & TBGPU_OPT_DENSE_INDEXES) && c->aidx_cap * 4 * sizeof(AccIdx) <= (1ull << 30))
+        c->aidx_cap *= 4;
     c->xrow_cap = o.transfers_max;
+    // the transfer-id index at load <= 1/8 while it stays within 8 GiB (random u128 ids:
+    // an eager claim's first CAS then nearly always takes its slot), else <= 1/2
+    // (TBGPU_OPT_DENSE_INDEXES, or TBGPU_XIDX_LOAD2 for A/B timing: <= 1/2 always)
+    static const bool xload2 = getenv("TBGPU_XIDX_LOAD2") != nullptr;
+    const bool dense_ix = (o.flags & TBGPU_OPT_DENSE_INDEXES) != 0;
     c->xidx_cap = pow2_at_least(2 * o.transfers_max);
+    if (!xload2 && !dense_ix && c->xidx_cap * 4 * sizeof(u64) <= (8ull << 30)) c->xidx_cap *= 4;
     c->hist_cap = o.history_max;
     u64& B = c->bytes;
     ZeroOn zero_on(c->stream);
@@ -754,7 +767,7 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     c->T.big = dalloc<u32>(4, &B);
     c->gate_status = dalloc<u32>(4, &B);  // the prepared commit's verdict, and its timestamp at [2..3]
     c->T.hcount = c->T.big + 1;        // [1] entries, [2] refused, [3] transfer-id tombstones
-    c->T.hash_limit = c->aidx_cap / 2;  // load <= 0.5
+    c->T.hash_limit = pow2_at_least(2 * o.hashed_max) / 2;  // hashed_max (rounded up): load <= 0.5 at most
     c->T.base = dalloc<u64>(4, &B);
     c->T.shard_world = o.shard_world >= 2 ? o.shard_world : 0;
     c->T.shard_rank = o.shard_world >= 2 ? o.shard_rank : 0;

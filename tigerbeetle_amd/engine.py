@@ -51,6 +51,7 @@ PHASES = ("upload", "classify", "sort", "scan", "evaluate", "apply", "index", "p
 OPT_FORCE_GENERAL = 1
 OPT_WALK_EARLY = 2  # include/tbgpu.h TBGPU_OPT_WALK_EARLY (tests)
 OPT_PINNED_INPUT = 4  # include/tbgpu.h TBGPU_OPT_PINNED_INPUT: host event buffers are page-locked
+OPT_DENSE_INDEXES = 8  # include/tbgpu.h TBGPU_OPT_DENSE_INDEXES: hash indexes at load <= 1/2
 
 
 def header_symbols() -> list[str]:
@@ -182,7 +183,8 @@ class Engine:
     def __init__(self, device: int = 0, accounts_max: int = 1 << 16, transfers_max: int = 1 << 20,
                  history_max: int = 1 << 16, events_per_call_max: int = 1 << 17, force_general: bool = False,
                  dense_block_span: int = 0, walk_early: bool = False, pinned_input: bool = False,
-                 directory_max: int = 0, hashed_max: int = 0, shard_world: int = 0, shard_rank: int = 0):
+                 directory_max: int = 0, hashed_max: int = 0, shard_world: int = 0, shard_rank: int = 0,
+                 dense_indexes: bool = False):
         """dense_block_span = S > 0: account ids of the form (b << 32) | k with 1 <= k <= S
         (e.g. ledger-major numbering) are looked up in the direct-mapped directory, one
         8-byte read; other ids use the hash index.  0: the directory covers ids
@@ -194,7 +196,7 @@ class Engine:
         opt = Options(device=device, accounts_max=accounts_max, transfers_max=transfers_max,
                       history_max=history_max, events_per_call_max=events_per_call_max,
                       flags=(OPT_FORCE_GENERAL if force_general else 0) | (OPT_WALK_EARLY if walk_early else 0)
-                      | (OPT_PINNED_INPUT if pinned_input else 0),
+                      | (OPT_PINNED_INPUT if pinned_input else 0) | (OPT_DENSE_INDEXES if dense_indexes else 0),
                       dense_block_span=dense_block_span, directory_max=directory_max, hashed_max=hashed_max,
                       shard_world=shard_world, shard_rank=shard_rank)
         self.device = device

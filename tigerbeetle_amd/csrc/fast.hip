@@ -395,7 +395,9 @@ __device__ __forceinline__ u64 fp_gate_wait(const FastArgs& F, const GateArgs& G
             u32 want = 0;
             u64 t_go = 0;
             if (poller) {
-                const u32 go = __hip_atomic_load(G.go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                // (relaxed: the host wrote the timestamp before GO, and the timestamp is read
+                // only after GO was seen, from the same coherent host memory)
+                const u32 go = __hip_atomic_load(G.go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (go == seq) {
                     want = tag_go;
                     t_go = __hip_atomic_load(G.ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -406,7 +408,12 @@ __device__ __forceinline__ u64 fp_gate_wait(const FastArgs& F, const GateArgs& G
             }
             if (!want && wall_clock64() - t0 > G.budget) want = tag_off;
             if (want) {
-                if (__hip_atomic_compare_exchange_strong(F.gate, &d, want, __ATOMIC_RELEASE, __ATOMIC_RELAXED,
+                // The timestamp's sc1 store has completed before the verdict's CAS, and the
+                // other tiles read it with an sc1 load after seeing the verdict: the
+                // hand-off of MI355X_MICROARCH.md's sc1 forms, without the release's L2
+                // write-back or the acquire's L1 invalidate (≈1.7 µs each)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (__hip_atomic_compare_exchange_strong(F.gate, &d, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                          __HIP_MEMORY_SCOPE_AGENT)) {
                     v = want;
                     if (want == tag_off) __hip_atomic_store(G.ack, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -417,10 +424,7 @@ __device__ __forceinline__ u64 fp_gate_wait(const FastArgs& F, const GateArgs& G
             if (poller) __builtin_amdgcn_s_sleep(2);
             else __builtin_amdgcn_s_sleep(8);
         }
-        if (v == tag_go) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (the poller's timestamp store before its CAS)
-            ts = __hip_atomic_load(ts_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (v == tag_go) ts = __hip_atomic_load(ts_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     return __shfl((unsigned long long)ts, 0);
 }
@@ -470,7 +474,8 @@ __device__ __forceinline__ void fp_commit_body(const Tables& T, FastArgs F, cons
 #if defined(FP_KEYS_ALWAYS)  // timing variant: the copies as before
         keys = true;
 #endif
-        if (tile == 0 && tid == 0) F.counters[CNT_NOKEYS] = keys ? 0u : 1u;  // (fp_tail keeps it)
+        if (tile == 0 && tid == 0)  // (fp_tail keeps it; an sc1 store: the last small tile reads it)
+            __hip_atomic_store(&F.counters[CNT_NOKEYS], keys ? 0u : 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 #if defined(FP_LDS_EVENTS)
     // The wave's 64 events as coalesced 16-byte loads (lane k of load j holds chunk
@@ -729,7 +734,7 @@ __device__ __forceinline__ void fp_commit_body(const Tables& T, FastArgs F, cons
         if (lane < 4) {
             u64 v = s_idr[0][lane];
             for (int w = 1; w < TILE / 64; w++) v = lane < 2 ? max(v, s_idr[w][lane]) : min(v, s_idr[w][lane]);
-            F.tile_idr[TILE_WORDS * tile + lane] = v;
+            __hip_atomic_store(&F.tile_idr[TILE_WORDS * tile + lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (lane == 0) {
             u32 nok = 0, nbad = 0;
@@ -741,11 +746,14 @@ __device__ __forceinline__ void fp_commit_body(const Tables& T, FastArgs F, cons
             }
             // accepted count and commit timestamp: folded by fp_index (one atomic per
             // tile on one address would serialize 16k tiles at the memory side)
-            F.tile_idr[TILE_WORDS * tile + 4] = maxts;
-            F.tile_idr[TILE_WORDS * tile + 5] = nok;
+            // (sc1 stores: the last small tile reads the records with sc1 loads, fp_small_tail)
+            __hip_atomic_store(&F.tile_idr[TILE_WORDS * tile + 4], maxts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&F.tile_idr[TILE_WORDS * tile + 5], (u64)nok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (SMALL) {
-                F.tile_idr[TILE_WORDS * tile + 6] = nbad;
-                F.tile_idr[TILE_WORDS * tile + 7] = s_flags;
+                __hip_atomic_store(&F.tile_idr[TILE_WORDS * tile + 6], (u64)nbad, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&F.tile_idr[TILE_WORDS * tile + 7], (u64)s_flags, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
             } else {
                 if (nbad) atomicAdd(&F.counters[CNT_BAD], nbad);
                 const u32 fl = s_flags;  // (skipped when an earlier tile raised them already)
@@ -800,13 +808,17 @@ __device__ __forceinline__ void fp_commit_body(const Tables& T, FastArgs F, cons
         if (F.fuse) {
             // the last tile to finish (one wave per tile: its fence covers its record)
             static_assert(!SMALL || TILE == 64, "one wave per small tile");
+            // Every tile's record (and tile 0's CNT_NOKEYS) went out as sc1 stores; the
+            // wave waits for them, then takes its ticket (an agent-scope atomic), and the
+            // tile whose ticket is last reads the records with sc1 loads: the counter
+            // hand-off of MI355X_MICROARCH.md's sc1 forms (no release or acquire fence:
+            // ≈3.5 µs each way as __threadfence)
             const u32 ntiles = (F.n + TILE - 1) / TILE;
-            __threadfence();
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             u32 t = 0;
-            if (lane == 0) t = atomicAdd(&F.counters[CNT_TICKET], 1u);
+            if (lane == 0) t = __hip_atomic_fetch_add(&F.counters[CNT_TICKET], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             t = __shfl(t, 0);
             if (t != ntiles - 1) return;
-            __threadfence();  // (acquire: the other tiles' records)
             fp_small_tail(T, F, bi, rp);
         }
     }
@@ -884,7 +896,8 @@ __device__ __forceinline__ void fp_fold_idr(const Tables& T, const FastArgs& F, 
     const u32 k = k0 + (threadIdx.x & 63);
     u64 r[4] = {0, 0, ~0ull, ~0ull};
     if (k < ntiles)
-        for (int w = 0; w < 4; w++) r[w] = F.tile_idr[TILE_WORDS * k + w];
+        for (int w = 0; w < 4; w++)  // (sc1 loads: fp_small_tail reads records of this launch's tiles)
+            r[w] = __hip_atomic_load(&F.tile_idr[TILE_WORDS * k + w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int off = 32; off > 0; off >>= 1) {
         r[0] = max(r[0], (u64)__shfl_xor((unsigned long long)r[0], off));
         r[1] = max(r[1], (u64)__shfl_xor((unsigned long long)r[1], off));
@@ -1204,7 +1217,7 @@ __device__ void fp_small_tail(const Tables& T, const FastArgs& F, const BlockInl
         for (u32 k0 = 0; k0 < ntiles; k0 += 64) fp_fold_idr(T, F, k0, ntiles);
     }
     if (lane == 0) {
-        const u32 nokeys = F.counters[CNT_NOKEYS];
+        const u32 nokeys = __hip_atomic_load(&F.counters[CNT_NOKEYS], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         for (int k = 0; k < CNT_TS_SAVE; k++) F.counters[k] = 0;
         F.counters[CNT_NOKEYS] = nokeys;
         F.counters[CNT_FLAGS] = fl;
@@ -1241,9 +1254,12 @@ __device__ void fp_small_tail(const Tables& T, const FastArgs& F, const BlockInl
             const u64 bw = (w >> 1) == 0 ? b[0] : (w >> 1) == 1 ? b[1] : (w >> 1) == 2 ? b[2] : b[3];
             v = (w & 1) ? (u32)(bw >> 32) : (u32)bw;
         }
-        rp.out[k] = v;
+        __hip_atomic_store(&rp.out[k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    __threadfence_system();
+    // the report's system-scope stores (past every cache, into coherent host memory) are
+    // complete before the sequence word goes out: no L2 write-back of the rows the tiles
+    // stored on this XCD (a system-scope release fence would make one)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) {
         __hip_atomic_store(&F.counters[CNT_TAILSEQ], rp.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&F.counters[CNT_TICKET], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -79,11 +79,15 @@ def test_prefetch_of_another_body_is_not_used():
         gpu.close()
 
 
-def test_state_machine_prefetch_then_commit():
+@pytest.mark.parametrize("role,mix", [("backup", "config3"), ("primary", "config3"), ("primary", "config1")])
+def test_state_machine_prefetch_then_commit(role, mix):
     """The host mirror: prefetch(create_transfers, body) then commit(body) as the
-    replica drives it, against the oracle."""
+    replica drives it, against the oracle.  A primary also prepares every body two ops
+    ahead of its commit (StateMachine.prepare stages it, src/vsr/replica.zig:5159-5167);
+    a backup never prepares."""
     from tigerbeetle_amd.state_machine import StateMachine
-    w = workload.config3(batches=3, batch=1500, account_count=200, seed=9)
+    w = workload.config3(batches=3, batch=1500, account_count=200, seed=9) if mix == "config3" else \
+        workload.config1(transfer_count=8190 * 5, account_count=500, seed=19)
     orc = oracle.Oracle(len(w.accounts), len(w.transfers))
     sm = StateMachine(engine=_engine(w))
     try:
@@ -91,8 +95,14 @@ def test_state_machine_prefetch_then_commit():
         orc.create_accounts_batches(ats, w.account_counts, w.accounts)
         sm.engine.create_accounts_batches(ats, w.account_counts, w.accounts)
         sm.commit_timestamp = int(ats[-1])
+        bodies = [ev.tobytes() for ev in _batches(w)]
+        if role == "primary":
+            for body in bodies[:2]:
+                sm.prepare(Operation.create_transfers, body)
         for b, ev in enumerate(_batches(w)):
-            body = ev.tobytes()
+            body = bodies[b]
+            if role == "primary" and b + 2 < len(bodies):
+                sm.prepare(Operation.create_transfers, bodies[b + 2])
             done = []
             sm.prefetch(lambda _: done.append(True), b + 1, Operation.create_transfers, body)
             assert done

@@ -8,6 +8,8 @@ lookups to the HIP engine (libtbgpu.so).  Inputs and outputs are raw message bod
 """
 from __future__ import annotations
 
+import hashlib
+
 import numpy as np
 
 from .engine import Engine
@@ -26,11 +28,27 @@ class StateMachine:
         self.prepare_timestamp = 0
         self.commit_timestamp = 0
         self._prefetched = None  # the create_transfers body prefetch staged (its array view)
+        self._staged = {}        # content key -> the staged body's array (alive while its copy may run)
 
-    # src/state_machine.zig:503-512
+    @staticmethod
+    def body_key(input: bytes) -> int:
+        """The body's content key (the Zig shim passes the header's checksum_body; the
+        mirror has no header, so a 128-bit hash of the same bytes)."""
+        return int.from_bytes(hashlib.blake2b(input, digest_size=16).digest(), "little")
+
+    # src/state_machine.zig:503-512; the primary calls it from primary_pipeline_prepare
+    # (src/vsr/replica.zig:5159-5167), before the prepare is replicated: a create_transfers
+    # body is staged in HBM then and its commit prepared (tbgpu_stage_transfers)
     def prepare(self, operation: Operation, input: bytes) -> None:
         if operation in (Operation.create_accounts, Operation.create_transfers):
             self.prepare_timestamp += len(input) // 128
+        if operation == Operation.create_transfers and input:
+            key = self.body_key(input)
+            events = np.frombuffer(input, dtype=TRANSFER_DTYPE)
+            self.engine.stage_transfers(key, events)
+            self._staged[key] = events
+            while len(self._staged) > 16:
+                self._staged.pop(next(iter(self._staged)))
 
     # src/state_machine.zig:930-955: the LSM compaction beat; here the account-transfers
     # index folds in the rows committed since the previous beat.
@@ -39,15 +57,18 @@ class StateMachine:
         callback(self)
 
     # src/state_machine.zig:514-655 — the tables are HBM-resident, so prefetch has only
-    # the batch's host-to-device copy left to do: create_transfers stages it
-    # (tbgpu_prefetch_transfers) and the commit of the same body skips its copy.  The
-    # callback runs once the copy has landed (the reference delivers it asynchronously
-    # via the grid's next tick).
+    # the batch's host-to-device copy left to do, and none when prepare staged the body:
+    # create_transfers finds it by its content key (tbgpu_prefetch_transfers_staged;
+    # a backup, which never prepares, copies it now) and the commit of the same body
+    # skips its copy.  The callback runs once the copy has landed (the reference delivers
+    # it asynchronously via the grid's next tick).
     def prefetch(self, callback, op: int, operation: Operation, input: bytes) -> None:
         if operation == Operation.create_transfers and input:
             self._prefetched = np.frombuffer(input, dtype=TRANSFER_DTYPE)
-            self.engine.prefetch_transfers(self._prefetched)
+            key = self.body_key(input)
+            self.engine.prefetch_transfers_staged(key, self._prefetched)
             self.engine.prefetch_wait()
+            self._staged.pop(key, None)
         callback(self)
 
     # src/state_machine.zig:894-928

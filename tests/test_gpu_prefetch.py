@@ -287,3 +287,71 @@ def test_prepared_commit_with_failures_writes_only_its_replies():
         assert_state_equal(gpu, orc)
     finally:
         gpu.close()
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_staged_random_schedules(seed):
+    """Random schedules of the drop-in entry points, as a primary, a backup and other
+    callers would interleave them: staging up to 6 bodies ahead (tbgpu_stage_transfers,
+    each queuing its prepared commit), staged and plain prefetches, commits with and
+    without a prefetch, lookups and streamed calls in between (each releases whatever
+    is prepared), bodies staged twice or never committed, a gap past the gates' budget.
+    Mixes with failures, chains, two-phase transfers and (seeds 3-4) random u128 ids.
+    Every reply and the final state equal the oracle's."""
+    import time
+    from tigerbeetle_amd.types import TRANSFER_DTYPE
+    rng = np.random.default_rng(100 + seed)
+    if seed % 2:
+        w = workload.config3(batches=24, batch=int(rng.integers(300, 1500)), account_count=300, seed=seed)
+    else:
+        w = workload.config1(transfer_count=24 * 1200, account_count=400, seed=seed, batch=1200,
+                             id_order="random" if seed >= 3 else "sequential")
+    orc = oracle.Oracle(len(w.accounts), len(w.transfers) + 1024)
+    gpu = _engine(w, pinned_input=seed >= 3)
+    try:
+        ats, tts = w.timestamps()
+        for be in (orc, gpu):
+            be.create_accounts_batches(ats, w.account_counts, w.accounts)
+        bs = _batches(w)
+        if seed >= 3:  # page-locked bodies (the copy kernels read them in place)
+            import torch
+            keep = []
+            for b, ev in enumerate(bs):
+                t = torch.empty(max(len(ev), 1) * 128, dtype=torch.uint8, pin_memory=True)
+                v = t.numpy().view(TRANSFER_DTYPE)[:len(ev)]
+                v[:] = ev
+                keep.append(t)
+                bs[b] = v
+        key = lambda b: (seed << 96) | (b * 2654435761 + 7)
+        staged = 0  # bodies staged so far (in commit order)
+        got, want = [], []
+        for b, ev in enumerate(bs):
+            # stage ahead, as prepares arrive
+            ahead = int(rng.integers(0, 7))
+            while staged < min(len(bs), b + 1 + ahead):
+                gpu.stage_transfers(key(staged), bs[staged])
+                if rng.random() < 0.1:
+                    gpu.stage_transfers(key(staged), bs[staged])  # the same body again: nothing new
+                staged += 1
+            r = rng.random()
+            if r < 0.03:
+                time.sleep(0.03)  # past the gates' budget
+            elif r < 0.08:
+                q = [int(w.accounts["id_lo"][k]) | (int(w.accounts["id_hi"][k]) << 64) for k in range(3)]
+                assert len(gpu.lookup_accounts(q)) == 3  # releases what is prepared
+            elif r < 0.11 and b + 1 < len(bs):
+                gpu.stage_transfers(key(10_000 + b), bs[b + 1][:-1])  # a body that never commits
+            mode = rng.random()
+            if mode < 0.7:
+                gpu.prefetch_transfers_staged(key(b), ev)
+                gpu.prefetch_wait()
+            elif mode < 0.85:
+                gpu.prefetch_transfers(ev)
+                gpu.prefetch_wait()
+            got.append(gpu.create_transfers(int(tts[b]), ev))
+            res, rc, _ = orc.create_transfers_batches(tts[b:b + 1], w.transfer_counts[b:b + 1], ev)
+            want.append(res[:int(rc[0])].copy())
+        assert_results_equal(got, want, "create_transfers")
+        assert_state_equal(gpu, orc)
+    finally:
+        gpu.close()

@@ -8,6 +8,7 @@
 #include "common.h"
 #include "engine.h"
 #include "transfers.h"
+#include "fast.h"
 
 namespace {
 
@@ -260,8 +261,7 @@ __global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const
 // The benchmark's create_accounts call (src/tigerbeetle/benchmark_load.zig:209-247):
 // no repeated id, no chain, no existing id, every field valid.  Then every event is
 // ok, its row is n_accounts + i and its timestamp T_b - n_b + k + 1 (execute,
-// :1033-1035; create_account, :1198-1225), so the call is two passes (three when its
-// ids do not rise):
+// :1033-1035; create_account, :1198-1225), so the call is two passes:
 //   ac_fast_check  8 lanes per account, 16 bytes each: the lane's fields checked,
 //                  the chunk stored to the optimistic row (the timestamp patched in);
 //                  one lane probes the directory / index and compares the id with
@@ -270,14 +270,12 @@ __global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const
 //                  redoes the call on the general path (rows past n_accounts are free
 //                  space; the directory entries the check wrote are cleared by
 //                  ac_fast_index first).
-//                  An id of the direct-mapped directory whose entry is empty gets
-//                  its entry right there (two events writing one entry have one id:
-//                  rising ids never do, and ac_fast_dup finds them otherwise).
-//   ac_fast_dup    only with FL_NONMONO (--id-order=random / reversed, the benchmark's
-//                  IdPermutation, src/testing/id.zig:28-48): every id claims a slot of
-//                  a call-local table by CAS (event + 1); a claim that meets an earlier
-//                  claim of the same id (read from the events, which nothing writes)
-//                  is a repeat: FL_SLOW.
+//                  An id of the direct-mapped directory claims its entry by CAS; a
+//                  hashed id claims a slot of a call-local table by CAS (event + 1),
+//                  and a claim that meets an earlier claim of the same id is a
+//                  repeat.  Either way a repeated id inside the call (the benchmark's
+//                  IdPermutation orders, src/testing/id.zig:28-48, can put one
+//                  anywhere) raises FL_SLOW in the same pass.
 //   ac_fast_index  on a clean check: the index slot of every hashed id (CAS on its row
 //                  word; none when every id is in the directory, FL_AC_HASHED clear),
 //                  zero reply counts, commit_timestamp.  On a failed check: the
@@ -285,8 +283,15 @@ __global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const
 //                  the call-local claims are cleared.
 constexpr int AF_THREADS = 256;
 
-__global__ __launch_bounds__(AF_THREADS) void ac_fast_check(Tables T, AcArgs C, u64 row_base) {
+__global__ __launch_bounds__(AF_THREADS) void ac_fast_check(Tables T, AcArgs C, u64 row_base, BlockInline bi) {
     const u64 t = (u64)blockIdx.x * AF_THREADS + threadIdx.x;
+    __shared__ u32 s_blk[BLOCK_INLINE_WORDS];
+    if (bi.words) {  // a small call's batch block, from the arguments (no upload launch)
+        if (threadIdx.x < bi.words) s_blk[threadIdx.x] = bi.w[threadIdx.x];
+        __syncthreads();
+        C.b_start = s_blk;
+        C.b_ts = (const u64*)(s_blk + ((C.nb + 2) & ~1u));  // batch_ts_offset
+    }
     const u32 e = (u32)(t >> 3), ch = (u32)(t & 7), lane = threadIdx.x & 63;
     // The wave's 8 events are nearly always in one batch: one uniform binary search for
     // its first event, issued before the event loads, and lanes past a batch boundary
@@ -303,6 +308,7 @@ __global__ __launch_bounds__(AF_THREADS) void ac_fast_check(Tables T, AcArgs C, 
     // the event's ledger and flags (chunk 7, seven lanes up), for its directory entry
     const u32 q7x = __shfl(v.x, lane + 7), q7y = __shfl(v.y, lane + 7);
     bool hashed = false, nonmono = false;
+    u32 slot = NONE32;  // (the event's claim in the call-local table)
     if (e < C.n) {
         switch (ch) {
         case 0: {  // id: not 0 / maxInt (:1204-1205), absent, above the previous event's
@@ -311,18 +317,31 @@ __global__ __launch_bounds__(AF_THREADS) void ac_fast_check(Tables T, AcArgs C, 
             if (!bad && e > 0) {
                 const u128 prev = lane >= 8 ? ((u128)(((u64)pw << 32) | pz) << 64) | (((u64)py << 32) | px)
                                             : C.ev[e - 1].id;
-                nonmono = !(id > prev);  // (a repeat is possible: ac_fast_dup looks)
+                nonmono = !(id > prev);  // (a repeat is possible: the claims below find it)
             }
             if (!bad) {
                 if (dense_has(T, id)) {
-                    u64& d = T.dense[dense_slot(T, id)];
-                    bad = d != 0;
-                    if (!bad) d = dense_entry((u32)(row_base + e), q7x, (u16)(q7y >> 16));
+                    // an existing account or an earlier event of the call holds the entry:
+                    // one CAS decides between two events of one id
+                    const u64 want = dense_entry((u32)(row_base + e), q7x, (u16)(q7y >> 16));
+                    bad = atomicCAS((unsigned long long*)&T.dense[dense_slot(T, id)], 0ull,
+                                    (unsigned long long)want) != 0ull;
                 } else {
                     hashed = true;
                     bad = acc_probe(T.aidx, T.aidx_mask, id) != NONE32;
+                    // a repeat inside the call: every hashed id claims a slot of the
+                    // call-local table by CAS (event + 1); a claim that meets an earlier
+                    // claim of the same id (read from the events, which nothing writes)
+                    // is a repeat
+                    for (u64 h = hash128(id) & C.fmask; !bad;) {
+                        const u32 prev = atomicCAS(&C.ftab[h], 0u, e + 1);
+                        if (prev == 0) { slot = (u32)h; break; }
+                        bad = C.ev[prev - 1].id == id;
+                        h = (h + 1) & C.fmask;
+                    }
                 }
             }
+            C.fpos[e] = slot;
             break;
         }
         case 1: case 2: case 3: case 4:  // balances must be zero (:1208-1211)
@@ -347,40 +366,37 @@ __global__ __launch_bounds__(AF_THREADS) void ac_fast_check(Tables T, AcArgs C, 
         }
         ((uint4*)&T.acc[row_base + e])[ch] = v;
     }
+    // The flags once per workgroup, and only the bits not raised yet: with random ids
+    // every wave raises FL_AC_HASHED | FL_NONMONO, and one atomic per wave on the one
+    // flags word serialised at L2 (10k random ids: 1252 atomics; the kernel took 22.6 us
+    // with them, 11.3 us without)
+    __shared__ u32 s_fl;
+    if (threadIdx.x == 0) s_fl = 0;
+    __syncthreads();
     const u32 fl = (__ballot(bad) ? (u32)FL_SLOW : 0u) | (__ballot(hashed) ? (u32)FL_AC_HASHED : 0u) |
                    (__ballot(nonmono) ? (u32)FL_NONMONO : 0u);
-    if (fl && wave_leader()) atomicOr(&C.counters[CNT_FLAGS], fl);
-}
-
-__global__ __launch_bounds__(AF_THREADS) void ac_fast_dup(AcArgs C) {
-    const u32 flags = C.counters[CNT_FLAGS];
-    if (!(flags & FL_NONMONO)) return;  // ids rise through the call: none repeats
-    const u32 i = blockIdx.x * AF_THREADS + threadIdx.x;
-    bool dup = false;
-    if (i < C.n) {
-        const u128 id = C.ev[i].id;
-        u64 h = hash128(id) & C.fmask;
-        for (;;) {
-            const u32 prev = atomicCAS(&C.ftab[h], 0u, i + 1);
-            if (prev == 0) {
-                C.fpos[i] = (u32)h;
-                break;
-            }
-            if (C.ev[prev - 1].id == id) {
-                C.fpos[i] = NONE32;
-                dup = true;
-                break;
-            }
-            h = (h + 1) & C.fmask;
-        }
+    if (fl && wave_leader()) atomicOr(&s_fl, fl);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_fl) {
+        const u32 seen = __hip_atomic_load(&C.fast_words[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((seen & s_fl) != s_fl) atomicOr(&C.fast_words[0], s_fl);
     }
-    if (__ballot(dup) && wave_leader()) atomicOr(&C.counters[CNT_FLAGS], (u32)FL_SLOW);
 }
 
-__global__ __launch_bounds__(AF_THREADS) void ac_fast_index(Tables T, AcArgs C, u64 row_base) {
-    const u32 flags = C.counters[CNT_FLAGS];
+__global__ __launch_bounds__(AF_THREADS) void ac_fast_index(Tables T, AcArgs C, u64 row_base, BlockInline bi) {
+    const u32 flags = C.fast_words[0];
     const u32 i = blockIdx.x * AF_THREADS + threadIdx.x;
-    if ((flags & FL_NONMONO) && i < C.n && C.fpos[i] != NONE32) C.ftab[C.fpos[i]] = 0;  // (all-zero again)
+    __shared__ u32 s_blk[BLOCK_INLINE_WORDS];
+    if (bi.words) {  // a small call's batch block: to memory (the general path reads it there)
+        if (threadIdx.x < bi.words) {
+            s_blk[threadIdx.x] = bi.w[threadIdx.x];
+            if (blockIdx.x == 0) bi.block[threadIdx.x] = bi.w[threadIdx.x];
+        }
+        __syncthreads();
+        C.b_start = s_blk;
+        C.b_ts = (const u64*)(s_blk + ((C.nb + 2) & ~1u));  // batch_ts_offset
+    }
+    if (i < C.n && C.fpos[i] != NONE32) C.ftab[C.fpos[i]] = 0;  // (all-zero again)
     if (flags & FL_SLOW) {
         // the call goes to the general path: the directory entries the check wrote go
         if (i < C.n) {
@@ -390,25 +406,43 @@ __global__ __launch_bounds__(AF_THREADS) void ac_fast_index(Tables T, AcArgs C, 
                 if (d != 0 && dense_row(d) == (u32)(row_base + i)) d = 0;
             }
         }
-        return;
-    }
-    if (i < C.n && (flags & FL_AC_HASHED)) {
-        const u32 row = (u32)(row_base + i);
-        const uint4 k = ((const uint4*)&T.acc[row])[0];
-        const uint4 m = ((const uint4*)&T.acc[row])[7];
-        const u128 id = ((u128)(((u64)k.w << 32) | k.z) << 64) | (((u64)k.y << 32) | k.x);
-        const u16 code = (u16)(m.y & 0xFFFFu), af = (u16)(m.y >> 16);
-        if (!acc_insert(T, id, row, m.x, af, code)) atomicOr(&C.counters[CNT_FLAGS], (u32)FL_CAPACITY);
-    }
-    if (blockIdx.x == 0) {
-        // replies: none; commit_timestamp: the latest event's (every event is accepted)
-        u64 mts = 0;
-        for (u32 b = threadIdx.x; b < C.nb; b += AF_THREADS) {
-            C.counts_out[b] = 0;
-            if (C.b_start[b + 1] > C.b_start[b]) mts = max(mts, C.b_ts[b]);
+    } else {
+        if (i < C.n && (flags & FL_AC_HASHED)) {
+            const u32 row = (u32)(row_base + i);
+            const uint4 k = ((const uint4*)&T.acc[row])[0];
+            const uint4 m = ((const uint4*)&T.acc[row])[7];
+            const u128 id = ((u128)(((u64)k.w << 32) | k.z) << 64) | (((u64)k.y << 32) | k.x);
+            const u16 code = (u16)(m.y & 0xFFFFu), af = (u16)(m.y >> 16);
+            if (!acc_insert(T, id, row, m.x, af, code)) atomicOr(&C.fast_words[0], (u32)FL_CAPACITY);
         }
-        mts = wave_max_u64(mts);
-        if (wave_leader() && mts) atomicMax((unsigned long long*)T.commit_ts, (unsigned long long)mts);
+        if (blockIdx.x == 0) {
+            // replies: none; commit_timestamp: the latest event's (every event is accepted)
+            u64 mts = 0;
+            for (u32 b = threadIdx.x; b < C.nb; b += AF_THREADS) {
+                C.counts_out[b] = 0;
+                if (C.b_start[b + 1] > C.b_start[b]) mts = max(mts, C.b_ts[b]);
+            }
+            mts = wave_max_u64(mts);
+            if (wave_leader() && mts) atomicMax((unsigned long long*)T.commit_ts, (unsigned long long)mts);
+        }
+    }
+    // The call's flags to the host from the last workgroup to finish (instead of a copy
+    // after the kernel: a blit launch of 4.2 us and its gap).  Each
+    // wave waits for its own memory operations (FL_CAPACITY's atomic among them), the
+    // workgroup then takes a ticket, and the last one reads the final word: the counter
+    // hand-off of MI355X_MICROARCH.md's sc1 forms.  The kernel's end makes the host
+    // store visible to the host's wait on the stream.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const u32 t = __hip_atomic_fetch_add(&C.fast_words[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == gridDim.x - 1) {
+            const u32 f = __hip_atomic_load(&C.fast_words[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(C.flags_out, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            // all-zero again for the next call (every workgroup has read the flags)
+            __hip_atomic_store(&C.fast_words[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&C.fast_words[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -597,11 +631,11 @@ void ac_launch_mask(const Tables& T, const AcArgs& C, const u8* res, const u8* o
     ac_mask<<<GRID(C.n)>>>(T, C, res, ok, cfail, fres, mask, gate);
     ac_ts_fold<<<1, 1024, 0, stream>>>(C.ts_part, (C.n + 255) / 256, T.commit_ts, gate);
 }
-void ac_launch_fast(const Tables& T, const AcArgs& C, u64 row_base, hipStream_t stream) {
+void ac_launch_fast(const Tables& T, const AcArgs& C, u64 row_base, const BlockInline& bi, hipStream_t stream) {
     const u64 lanes = 8ull * C.n;
-    ac_fast_check<<<(u32)((lanes + AF_THREADS - 1) / AF_THREADS), AF_THREADS, 0, stream>>>(T, C, row_base);
-    ac_fast_dup<<<(u32)((C.n + AF_THREADS - 1) / AF_THREADS), AF_THREADS, 0, stream>>>(C);
-    ac_fast_index<<<(u32)((std::max(C.n, C.nb) + AF_THREADS - 1) / AF_THREADS), AF_THREADS, 0, stream>>>(T, C, row_base);
+    ac_fast_check<<<(u32)((lanes + AF_THREADS - 1) / AF_THREADS), AF_THREADS, 0, stream>>>(T, C, row_base, bi);
+    ac_fast_index<<<(u32)((std::max(C.n, C.nb) + AF_THREADS - 1) / AF_THREADS), AF_THREADS, 0, stream>>>(T, C, row_base,
+                                                                                                      bi);
     HIP_CHECK(hipGetLastError());
 }
 void ac_launch_apply(const Tables& T, const AcArgs& C, const u8* ok, const u8* fres, const uint4* rk, u64 row_base,

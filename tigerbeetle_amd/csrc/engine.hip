@@ -385,6 +385,7 @@ struct tbgpu_ctx {
     u32* h_gate = nullptr;
     u32* h_gate_dev = nullptr;
     u32* gate_status = nullptr;
+    u32* ac_fast_words = nullptr;  // the clean create_accounts call's flags and ticket (all-zero between calls)
     bool gate_pending = false;  // a prepared commit is enqueued and not yet released or cancelled
     bool gate_arm = false;      // try_fast: gate the kernels it launches on gate_status
     u32 gate_seq = 0, gate_n = 0;
@@ -643,8 +644,9 @@ static void alloc_scratch(tbgpu_ctx* c, u64 nmax) {
     // never reads a previous call's staged block and the host never reads a report the
     // device has not written back.
     constexpr unsigned HOST_COHERENT = hipHostMallocMapped | hipHostMallocCoherent;
-    // (+1: the small calls' sequence word, fp_tail's last store)
-    HIP_CHECK(hipHostMalloc((void**)&c->h_report, (RPT_COUNTS + c->bmax + 1) * sizeof(u32), HOST_COHERENT));
+    // (+1: the small calls' sequence word, fp_tail's last store; +1: the clean
+    // create_accounts call's flags, ac_fast_index's last store)
+    HIP_CHECK(hipHostMalloc((void**)&c->h_report, (RPT_COUNTS + c->bmax + 2) * sizeof(u32), HOST_COHERENT));
     HIP_CHECK(hipHostMalloc((void**)&c->h_res, c->nmax * 8 + 8, HOST_COHERENT));
     HIP_CHECK(hipHostMalloc((void**)&c->h_gate, GW_WORDS * sizeof(u32), HOST_COHERENT));
     memset(c->h_gate, 0, GW_WORDS * sizeof(u32));
@@ -766,6 +768,7 @@ extern "C" int tbgpu_init(tbgpu_ctx** out, const tbgpu_options* options) {
     c->T.xrun = dalloc<u64>(8, &B);
     c->T.big = dalloc<u32>(4, &B);
     c->gate_status = dalloc<u32>(4, &B);  // the prepared commit's verdict, and its timestamp at [2..3]
+    c->ac_fast_words = dalloc<u32>(2, &B);
     c->T.hcount = c->T.big + 1;        // [1] entries, [2] refused, [3] transfer-id tombstones
     c->T.hash_limit = pow2_at_least(2 * o.hashed_max) / 2;  // hashed_max (rounded up): load <= 0.5 at most
     c->T.base = dalloc<u64>(4, &B);
@@ -838,7 +841,7 @@ extern "C" void tbgpu_deinit(tbgpu_ctx* c) {
                     (void*)c->ro_bcount, (void*)c->ro_spart, (void*)c->rd_claim, (void*)c->rd_first,
                     (void*)c->rd_slot})
         if (p) { guard_release(p); (void)hipFree(p); }
-    void* ptrs[] = {c->T.dense, c->T.acc, c->T.aidx, c->T.xrows, c->T.xful, c->T.xidx, c->T.hrows, c->T.commit_ts, c->T.idr, c->T.xrun, c->T.big, c->gate_status, c->ev_buf,
+    void* ptrs[] = {c->T.dense, c->T.acc, c->T.aidx, c->T.xrows, c->T.xful, c->T.xidx, c->T.hrows, c->T.commit_ts, c->T.idr, c->T.xrun, c->T.big, c->gate_status, c->ac_fast_words, c->ev_buf,
                     c->b_start, c->ts, c->cs, c->ce, c->sres, c->dslot, c->cslot, c->pre_e, c->pre_p,
                     c->pp_dslot, c->pp_cslot, c->gslot, c->pslot, c->prev_id, c->pend_last, c->pend_first, c->prev_pend,
                     c->gclaim, c->gcnt_id, c->gcnt_pd, c->gmem, c->gbeg, c->gend, c->gfill, c->pfill, c->pbeg, c->skey, c->sval, c->skey_s,
@@ -2667,6 +2670,7 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
                                tbgpu_create_accounts_result_t* results_dev, u32* counts_host) {
     hipStream_t s = c->stream;
     if (n == 0) {
+        c->blk_words = 0;  // (no kernel reads the batch block)
         std::fill(counts_host, counts_host + nb, 0u);
         return;
     }
@@ -2686,12 +2690,20 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
     if (!no_fast && !(c->opt.flags & TBGPU_OPT_FORCE_GENERAL) && c->n_accounts + n <= c->accounts_max &&
         !c->T.shard_world) {
         // the clean call (accounts.hip ac_fast_*): one round trip decides whether it stood
-        HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)(c->counters + CNT_FLAGS), 0, 1, s));
-        ac_launch_fast(c->T, C, c->n_accounts, s);
-        HIP_CHECK(hipMemcpyAsync(c->h_counters, c->counters, CNT_COUNT * sizeof(u32), hipMemcpyDeviceToHost, s));
+        // (two launches: the batch block in their arguments when it is small, the flags
+        // in words of their own that the last workgroup zeroes again, the outcome stored
+        // to the host by that workgroup)
+        volatile u32* flags_host = c->h_report + RPT_COUNTS + c->bmax + 1;
+        *flags_host = FL_SLOW | FL_ERROR;  // (a kernel that never stored it reads as failed)
+        C.fast_words = c->ac_fast_words;
+        C.flags_out = c->h_report_dev + RPT_COUNTS + c->bmax + 1;
+        const BlockInline bi = take_block(c);
+        ac_launch_fast(c->T, C, c->n_accounts, bi, s);
         wait_stream(s);
-        if (!(c->h_counters[CNT_FLAGS] & FL_SLOW)) {
-            if (c->h_counters[CNT_FLAGS] & FL_CAPACITY)
+        const u32 flags = *flags_host;
+        if (flags & FL_ERROR) tbgpu_fatal("create_accounts", "the clean call reported no outcome", __FILE__, __LINE__);
+        if (!(flags & FL_SLOW)) {
+            if (flags & FL_CAPACITY)
                 tbgpu_fatal("create_accounts", "account index full (hashed_max exceeded)", __FILE__, __LINE__);
             std::fill(counts_host, counts_host + nb, 0u);
             c->n_accounts += n;
@@ -2700,6 +2712,7 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
         }
         // not clean: nothing visible changed (rows past n_accounts are free); the general path below
     }
+    flush_block(c);  // (when the fast call did not take it)
     HIP_CHECK(hipMemsetAsync(c->counters, 0, CNT_COUNT * sizeof(u32), s));
     HIP_CHECK(hipMemsetAsync(c->gclaim, 0, g * sizeof(u32), s));
     HIP_CHECK(hipMemsetAsync(c->gcnt_id, 0, g * sizeof(u32), s));
@@ -2780,7 +2793,7 @@ static uint64_t accounts_batches(tbgpu_ctx* c, uint32_t nb_total, const uint64_t
     for (u32 b0 = 0; b0 < nb_total;) {
         const u32 b1 = chunk_end(c, counts, b0, nb_total);
         const u32 nb = b1 - b0;
-        upload_batches(c, timestamps + b0, counts + b0, nb, starts);
+        upload_batches(c, timestamps + b0, counts + b0, nb, starts, false, /*allow_inline=*/true);
         const u32 n = starts[nb];
         const Account* ev = events + ev_off;
         if (!device) {

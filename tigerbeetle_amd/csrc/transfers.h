@@ -137,17 +137,25 @@ struct AcArgs {
     u64 gmask;
     u32* counters;
     u32* counts_out;  // per-batch reply counts (the clean two-pass call writes zeros)
-    // the clean call with ids that do not rise (random u128 ids): a call-local claim
-    // table (event + 1 per slot, all-zero between calls: the fast path's transfer-id
-    // claim table) finds a repeated id, and each event's claimed slot to clear again
+    // the clean call's repeats of a hashed id: a call-local claim table (event + 1 per
+    // slot, all-zero between calls: the fast path's transfer-id claim table) finds a
+    // repeated id, and each event's claimed slot to clear again
     u32* ftab;
     u32* fpos;
     u64 fmask;
+    // the clean call's outcome: its flags and ac_fast_index's ticket in fast_words[0..1]
+    // (a pair of its own, all-zero between calls: the last workgroup reads and resets
+    // them), the flags stored to flags_out (page-locked host memory, its device address)
+    u32* fast_words;
+    u32* flags_out;
 };
 // The clean call (accounts.hip ac_fast_*): raises FL_SLOW in counters[CNT_FLAGS] and
 // changes nothing visible when the call is not clean (no repeated id, all fields valid,
 // no chain, no existing id); otherwise commits it.  The caller ensures row capacity.
-void ac_launch_fast(const Tables& T, const AcArgs& C, u64 row_base, hipStream_t stream);
+// A small call's batch block travels in the kernels' arguments (fast.h BlockInline:
+// ac_fast_check reads it there, ac_fast_index writes it for the general path).
+struct BlockInline;
+void ac_launch_fast(const Tables& T, const AcArgs& C, u64 row_base, const BlockInline& bi, hipStream_t stream);
 void ac_launch_classify(const Tables& T, const AcArgs& C, hipStream_t stream);
 void ac_launch_group_sort(const AcArgs& C, u32 invalid, int bits, u32* k_in, u32* v_in, u32* k_out, u32* v_out,
                           SortScratch& ss, hipStream_t stream);

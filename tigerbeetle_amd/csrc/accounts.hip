@@ -87,7 +87,7 @@ __global__ void ac_mono(AcArgs C) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     bool down = false;
     if (i > 0 && i < C.n) down = !(C.ev[i].id > C.ev[i - 1].id);
-    if (__syncthreads_or(down) && threadIdx.x == 0) atomicOr(&C.counters[CNT_FLAGS], (u32)FL_NONMONO);
+    if (__syncthreads_or(down) && threadIdx.x == 0) raise_flags(&C.counters[CNT_FLAGS], (u32)FL_NONMONO);
 }
 
 __global__ void ac_classify(Tables T, AcArgs C) {
@@ -96,7 +96,7 @@ __global__ void ac_classify(Tables T, AcArgs C) {
     u32 fl = 0;
     if (i < C.n) fl = ac_classify_one(T, C, i, dup_check);
     fl = wave_or_u32(fl);  // one flag atomic per wave, not per chain member
-    if (fl && wave_leader()) atomicOr(&C.counters[CNT_FLAGS], fl);
+    if (wave_leader()) raise_flags(&C.counters[CNT_FLAGS], fl);
 }
 
 __global__ void ac_group1(AcArgs C) {
@@ -377,10 +377,7 @@ __global__ __launch_bounds__(AF_THREADS) void ac_fast_check(Tables T, AcArgs C, 
                    (__ballot(nonmono) ? (u32)FL_NONMONO : 0u);
     if (fl && wave_leader()) atomicOr(&s_fl, fl);
     __syncthreads();
-    if (threadIdx.x == 0 && s_fl) {
-        const u32 seen = __hip_atomic_load(&C.fast_words[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((seen & s_fl) != s_fl) atomicOr(&C.fast_words[0], s_fl);
-    }
+    if (threadIdx.x == 0) raise_flags(&C.fast_words[0], s_fl);
 }
 
 __global__ __launch_bounds__(AF_THREADS) void ac_fast_index(Tables T, AcArgs C, u64 row_base, BlockInline bi) {

@@ -290,6 +290,17 @@ void side_scan_fused_h64(const SideScanArgs& A, u64 m, u32 invalid, const u32* t
 void side_final_balances(const SideScanArgs& A, u64 m, u32 invalid, const Bal4* bb, Account* acc, u32* big,
                          hipStream_t stream);
 
+// FL_* bits raised on a flags word the whole grid shares: the atomic only when a bit
+// is missing.  Same-address atomics serialise at L2; one per workgroup of a large grid
+// whose workgroups all raise the same bits cost ~9 ns each (a 10k-account check: 11 us).
+__device__ __forceinline__ void raise_flags(u32* w, u32 fl) {
+#ifdef TBGPU_PLAIN_RAISE  // (timing variant: one atomic per caller)
+    if (fl) atomicOr(w, fl);
+#else
+    if (fl && (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & fl) != fl) atomicOr(w, fl);
+#endif
+}
+
 // Device probes shared by the kernels.  acc_probe returns the account ROW.
 __device__ __forceinline__ u32 acc_probe(const AccIdx* __restrict__ aidx, u64 mask, u128 id) {
     const u64 lo = (u64)id, hi = (u64)(id >> 64);

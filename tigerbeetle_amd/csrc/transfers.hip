@@ -289,7 +289,7 @@ __global__ void tr_classify(Tables T, TrArgs C) {
     u32 fl = block_or(i < C.n ? classify_one(T, C, i) : 0u);
     if (i == 0 && (*T.big & 1)) fl |= FL_WIDE;    // a committed balance near 2^128
     if (i == 0 && (*T.big & 2)) fl |= FL_WIDE64;  // a committed balance >= 2^61
-    if (threadIdx.x == 0 && fl) atomicOr(&C.counters[CNT_FLAGS], fl);
+    if (threadIdx.x == 0) raise_flags(&C.counters[CNT_FLAGS], fl);
 }
 
 // Single-member id groups record their member; multi-member groups need a sort.
@@ -303,7 +303,7 @@ __global__ void tr_group1(TrArgs C) {
         if (p != NONE32 && C.gcnt_pd[p] >= 2) fl |= FL_MULTI_PEND;
     }
     fl = block_or(fl);
-    if (threadIdx.x == 0 && fl) atomicOr(&C.counters[CNT_FLAGS], fl);
+    if (threadIdx.x == 0) raise_flags(&C.counters[CNT_FLAGS], fl);
 }
 
 // Sort keys for grouping: events by id slot (kind 0) or post/voids by pending slot (kind 1).
@@ -1020,6 +1020,8 @@ __global__ __launch_bounds__(EV_THREADS) void tr_eval_lists(Tables T, TrArgs C, 
     const u32 c = block_sum(changed ? 1u : 0u);
     const u32 f = block_min(changed ? i : NONE32);
     if (threadIdx.x == 0 && c) {
+        // (one of ~960 workgroups' two same-address atomics at the end of an early pass:
+        // measured free, profiles/r06/ab_pass_atomics_config3.txt)
         atomicAdd(chg, c);
         atomicMin(front, f);
     }

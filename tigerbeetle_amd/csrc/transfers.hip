@@ -91,12 +91,10 @@ __device__ __forceinline__ u32 gtab_find_or_insert(const TrArgs& C, u128 key, u3
     const u32 claim = ((i << 1) | kindbit) + 1;
     u64 h = hash128(key) & C.gmask;
     for (;;) {
-        u32 cur = C.gclaim[h];
-        if (cur == 0) {
-            const u32 prev = atomicCAS(&C.gclaim[h], 0u, claim);
-            if (prev == 0) return (u32)h;
-            cur = prev;
-        }
+        // the CAS itself reads the slot (a load first cost a round trip more for the
+        // usual empty slot)
+        const u32 cur = atomicCAS(&C.gclaim[h], 0u, claim);
+        if (cur == 0) return (u32)h;
         const u32 ci = (cur - 1) >> 1;
         const u128 ck = ((cur - 1) & 1) ? C.ev[ci].pending_id : C.ev[ci].id;
         if (ck == key) return (u32)h;

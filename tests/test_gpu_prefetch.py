@@ -355,3 +355,28 @@ def test_staged_random_schedules(seed):
         assert_state_equal(gpu, orc)
     finally:
         gpu.close()
+
+
+def test_new_ctx_after_another_on_recycled_memory():
+    """Contexts one after another, each with the same sizes (so the allocator tends to
+    hand a new ctx the memory of the last one): a ctx's prepared-commit verdict word,
+    its clean create_accounts ticket and its small calls' sequence word are matched
+    against values every ctx repeats (sequence numbers restart at 1), so a new ctx must
+    not read the previous one's.  Each ctx's stream has other timestamps."""
+    for k in range(4):
+        w = workload.config1(transfer_count=12_000, account_count=600, seed=20 + k)
+        orc, gpu = oracle.Oracle(len(w.accounts), len(w.transfers)), _engine(w)
+        try:
+            ats, tts = w.timestamps(start=1_000_000 * k)
+            for be in (orc, gpu):
+                be.create_accounts_batches(ats, w.account_counts, w.accounts)
+            got, want = [], []
+            for b, ev in enumerate(_batches(w)):
+                gpu.prefetch_transfers(ev)
+                got.append(gpu.create_transfers(int(tts[b]), ev))
+                res, rc, _ = orc.create_transfers_batches(tts[b:b + 1], w.transfer_counts[b:b + 1], ev)
+                want.append(res[:int(rc[0])].copy())
+            assert_results_equal(got, want, "create_transfers")
+            assert_state_equal(gpu, orc)
+        finally:
+            gpu.close()

@@ -811,7 +811,13 @@ extern "C" void tbgpu_reset(tbgpu_ctx* c) {
     if (c->T.dense_n) HIP_CHECK(hipMemsetAsync(c->T.dense, 0, c->T.dense_n * sizeof(u64), c->stream));
     if (c->ximp) HIP_CHECK(hipMemsetAsync(c->ximp, 0, c->xrow_cap, c->stream));
     HIP_CHECK(hipMemsetAsync(c->f_gtab, 0, c->f_gcap * sizeof(u32), c->stream));  // fast path's claim table
+    // Words matched against values a new ctx repeats (sequence numbers restart at 1,
+    // the clean accounts call's ticket at 0): a recycled allocation must not hold a
+    // previous ctx's prepared-commit verdict or ticket
+    HIP_CHECK(hipMemsetAsync(c->gate_status, 0, 4 * sizeof(u32), c->stream));
+    HIP_CHECK(hipMemsetAsync(c->ac_fast_words, 0, 2 * sizeof(u32), c->stream));
     wait_stream(c->stream);
+    c->h_report[RPT_COUNTS + c->bmax] = 0;  // (the small calls' sequence word: never 0)
     c->n_accounts = c->n_rows = c->n_hist = 0;
     c->n_foreign = 0;
     c->rows_hi = 0;

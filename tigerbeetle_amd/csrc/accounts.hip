@@ -12,13 +12,17 @@
 
 namespace {
 
-__device__ __forceinline__ u32 ac_batch_of(const u32* __restrict__ b_start, u32 nb, u32 i) {
+template <class Start>
+__device__ __forceinline__ u32 ac_batch_of_f(Start start, u32 nb, u32 i) {
     u32 lo = 0, hi = nb;
     while (hi - lo > 1) {
         const u32 mid = (lo + hi) >> 1;
-        if (b_start[mid] <= i) lo = mid; else hi = mid;
+        if (start(mid) <= i) lo = mid; else hi = mid;
     }
     return lo;
+}
+__device__ __forceinline__ u32 ac_batch_of(const u32* __restrict__ b_start, u32 nb, u32 i) {
+    return ac_batch_of_f([&](u32 k) { return b_start[k]; }, nb, i);
 }
 
 __device__ __forceinline__ u32 ac_gtab_insert(const AcArgs& C, u128 key, u32 i) {
@@ -261,7 +265,8 @@ __global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const
 // The benchmark's create_accounts call (src/tigerbeetle/benchmark_load.zig:209-247):
 // no repeated id, no chain, no existing id, every field valid.  Then every event is
 // ok, its row is n_accounts + i and its timestamp T_b - n_b + k + 1 (execute,
-// :1033-1035; create_account, :1198-1225), so the call is two passes:
+// :1033-1035; create_account, :1198-1225), so the call is two passes (three when its
+// ids do not rise):
 //   ac_fast_check  8 lanes per account, 16 bytes each: the lane's fields checked,
 //                  the chunk stored to the optimistic row (the timestamp patched in);
 //                  one lane probes the directory / index and compares the id with
@@ -270,12 +275,14 @@ __global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const
 //                  redoes the call on the general path (rows past n_accounts are free
 //                  space; the directory entries the check wrote are cleared by
 //                  ac_fast_index first).
-//                  An id of the direct-mapped directory claims its entry by CAS; a
-//                  hashed id claims a slot of a call-local table by CAS (event + 1),
-//                  and a claim that meets an earlier claim of the same id is a
-//                  repeat.  Either way a repeated id inside the call (the benchmark's
-//                  IdPermutation orders, src/testing/id.zig:28-48, can put one
-//                  anywhere) raises FL_SLOW in the same pass.
+//                  An id of the direct-mapped directory whose entry is empty gets
+//                  its entry right there (two events writing one entry have one id:
+//                  rising ids never do, and ac_fast_dup finds them otherwise).
+//   ac_fast_dup    only with FL_NONMONO (--id-order=random / reversed, the benchmark's
+//                  IdPermutation, src/testing/id.zig:28-48; otherwise it returns at
+//                  once): every id claims a slot of a call-local table by CAS (event +
+//                  1); a claim that meets an earlier claim of the same id (read from the
+//                  events, which nothing writes) is a repeat: FL_SLOW.
 //   ac_fast_index  on a clean check: the index slot of every hashed id (CAS on its row
 //                  word; none when every id is in the directory, FL_AC_HASHED clear),
 //                  zero reply counts, commit_timestamp.  On a failed check: the
@@ -283,21 +290,30 @@ __global__ void ac_apply(Tables T, AcArgs C, const u8* ok, const u8* fres, const
 //                  the call-local claims are cleared.
 constexpr int AF_THREADS = 256;
 
+// INL: a small call, whose batch block comes in the arguments (no upload launch) and is
+// copied to LDS, and whose flags are gathered per workgroup.  The other form is the
+// plain kernel: its batch block in memory, no LDS, no barrier (one kernel for both took
+// 96 us for 1M accounts against 66).
+template <bool INL>
 __global__ __launch_bounds__(AF_THREADS) void ac_fast_check(Tables T, AcArgs C, u64 row_base, BlockInline bi) {
     const u64 t = (u64)blockIdx.x * AF_THREADS + threadIdx.x;
-    __shared__ u32 s_blk[BLOCK_INLINE_WORDS];
-    if (bi.words) {  // a small call's batch block, from the arguments (no upload launch)
+    __shared__ u32 s_blk[INL ? BLOCK_INLINE_WORDS : 1];
+    constexpr bool inl = INL;
+    if constexpr (INL) {
         if (threadIdx.x < bi.words) s_blk[threadIdx.x] = bi.w[threadIdx.x];
         __syncthreads();
-        C.b_start = s_blk;
-        C.b_ts = (const u64*)(s_blk + ((C.nb + 2) & ~1u));  // batch_ts_offset
     }
+    const u32 ts_off = (C.nb + 2) & ~1u;  // batch_ts_offset
+    auto bstart = [&](u32 k) -> u32 { return inl ? s_blk[k] : C.b_start[k]; };
+    auto bts = [&](u32 b) -> u64 {
+        return inl ? ((u64)s_blk[ts_off + 2 * b + 1] << 32 | s_blk[ts_off + 2 * b]) : C.b_ts[b];
+    };
     const u32 e = (u32)(t >> 3), ch = (u32)(t & 7), lane = threadIdx.x & 63;
     // The wave's 8 events are nearly always in one batch: one uniform binary search for
     // its first event, issued before the event loads, and lanes past a batch boundary
     // walk on (a search per event made every wave wait for seven dependent loads)
     const u32 e0 = __builtin_amdgcn_readfirstlane(e);
-    u32 b = e0 < C.n ? ac_batch_of(C.b_start, C.nb, e0) : 0u;
+    u32 b = e0 < C.n ? ac_batch_of_f(bstart, C.nb, e0) : 0u;
     bool bad = false;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (e < C.n) v = ((const uint4*)&C.ev[e])[ch];
@@ -308,7 +324,6 @@ __global__ __launch_bounds__(AF_THREADS) void ac_fast_check(Tables T, AcArgs C, 
     // the event's ledger and flags (chunk 7, seven lanes up), for its directory entry
     const u32 q7x = __shfl(v.x, lane + 7), q7y = __shfl(v.y, lane + 7);
     bool hashed = false, nonmono = false;
-    u32 slot = NONE32;  // (the event's claim in the call-local table)
     if (e < C.n) {
         switch (ch) {
         case 0: {  // id: not 0 / maxInt (:1204-1205), absent, above the previous event's
@@ -317,31 +332,21 @@ __global__ __launch_bounds__(AF_THREADS) void ac_fast_check(Tables T, AcArgs C, 
             if (!bad && e > 0) {
                 const u128 prev = lane >= 8 ? ((u128)(((u64)pw << 32) | pz) << 64) | (((u64)py << 32) | px)
                                             : C.ev[e - 1].id;
-                nonmono = !(id > prev);  // (a repeat is possible: the claims below find it)
+                nonmono = !(id > prev);  // (a repeat is possible: ac_fast_dup looks)
             }
             if (!bad) {
                 if (dense_has(T, id)) {
-                    // an existing account or an earlier event of the call holds the entry:
-                    // one CAS decides between two events of one id
-                    const u64 want = dense_entry((u32)(row_base + e), q7x, (u16)(q7y >> 16));
-                    bad = atomicCAS((unsigned long long*)&T.dense[dense_slot(T, id)], 0ull,
-                                    (unsigned long long)want) != 0ull;
+                    // plain accesses: a CAS per account executes at the memory side (1M
+                    // accounts took 0.164 ms with one, 0.091 ms without); two events of
+                    // one id are a repeat, which ac_fast_dup finds
+                    u64& d = T.dense[dense_slot(T, id)];
+                    bad = d != 0;
+                    if (!bad) d = dense_entry((u32)(row_base + e), q7x, (u16)(q7y >> 16));
                 } else {
                     hashed = true;
                     bad = acc_probe(T.aidx, T.aidx_mask, id) != NONE32;
-                    // a repeat inside the call: every hashed id claims a slot of the
-                    // call-local table by CAS (event + 1); a claim that meets an earlier
-                    // claim of the same id (read from the events, which nothing writes)
-                    // is a repeat
-                    for (u64 h = hash128(id) & C.fmask; !bad;) {
-                        const u32 prev = atomicCAS(&C.ftab[h], 0u, e + 1);
-                        if (prev == 0) { slot = (u32)h; break; }
-                        bad = C.ev[prev - 1].id == id;
-                        h = (h + 1) & C.fmask;
-                    }
                 }
             }
-            C.fpos[e] = slot;
             break;
         }
         case 1: case 2: case 3: case 4:  // balances must be zero (:1208-1211)
@@ -354,9 +359,9 @@ __global__ __launch_bounds__(AF_THREADS) void ac_fast_check(Tables T, AcArgs C, 
             const u32 code = v.y & 0xFFFFu, flags = v.y >> 16;
             bad = v.x == 0 || code == 0 || (v.z | v.w) != 0 || (flags & (0xFFF0u | AF_LINKED)) != 0 ||
                   ((flags & AF_DNEC) && (flags & AF_CNED));
-            while (b + 1 < C.nb && C.b_start[b + 1] <= e) b++;
-            const u32 bs = C.b_start[b], nbatch = C.b_start[b + 1] - bs;
-            const u64 ts = C.b_ts[b] - nbatch + (e - bs) + 1;
+            while (b + 1 < C.nb && bstart(b + 1) <= e) b++;
+            const u32 bs = bstart(b), nbatch = bstart(b + 1) - bs;
+            const u64 ts = bts(b) - nbatch + (e - bs) + 1;
             v.z = (u32)ts;
             v.w = (u32)(ts >> 32);
             break;
@@ -366,34 +371,69 @@ __global__ __launch_bounds__(AF_THREADS) void ac_fast_check(Tables T, AcArgs C, 
         }
         ((uint4*)&T.acc[row_base + e])[ch] = v;
     }
-    // The flags once per workgroup, and only the bits not raised yet: with random ids
-    // every wave raises FL_AC_HASHED | FL_NONMONO, and one atomic per wave on the one
-    // flags word serialised at L2 (10k random ids: 1252 atomics; the kernel took 22.6 us
-    // with them, 11.3 us without)
-    __shared__ u32 s_fl;
-    if (threadIdx.x == 0) s_fl = 0;
-    __syncthreads();
+    // Only the bits not raised yet (raise_flags): with random ids every wave raises
+    // FL_AC_HASHED | FL_NONMONO, and one atomic per wave on the one flags word
+    // serialised at L2 (10k random ids: 1252 atomics; the kernel took 22.6 us with them,
+    // 11.3 us without).  A small call gathers them per workgroup first (raise_flags per
+    // wave, its load's round trip at every wave's end: 0.059 ms for the call against
+    // 0.042); a large one per wave (no barrier).
     const u32 fl = (__ballot(bad) ? (u32)FL_SLOW : 0u) | (__ballot(hashed) ? (u32)FL_AC_HASHED : 0u) |
                    (__ballot(nonmono) ? (u32)FL_NONMONO : 0u);
-    if (fl && wave_leader()) atomicOr(&s_fl, fl);
-    __syncthreads();
-    if (threadIdx.x == 0) raise_flags(&C.fast_words[0], s_fl);
+    if constexpr (INL) {
+        __shared__ u32 s_fl;
+        if (threadIdx.x == 0) s_fl = 0;
+        __syncthreads();
+        if (fl && wave_leader()) atomicOr(&s_fl, fl);
+        __syncthreads();
+        if (threadIdx.x == 0) raise_flags(&C.fast_words[0], s_fl);
+    } else {
+        if (wave_leader()) raise_flags(&C.fast_words[0], fl);
+    }
+}
+
+__global__ __launch_bounds__(AF_THREADS) void ac_fast_dup(AcArgs C) {
+    if (!(C.fast_words[0] & FL_NONMONO)) return;  // ids rise through the call: none repeats
+    const u32 i = blockIdx.x * AF_THREADS + threadIdx.x;
+    bool dup = false;
+    if (i < C.n) {
+        const u128 id = C.ev[i].id;
+        u64 h = hash128(id) & C.fmask;
+        for (;;) {
+            const u32 prev = atomicCAS(&C.ftab[h], 0u, i + 1);
+            if (prev == 0) {
+                C.fpos[i] = (u32)h;
+                break;
+            }
+            if (C.ev[prev - 1].id == id) {
+                C.fpos[i] = NONE32;
+                dup = true;
+                break;
+            }
+            h = (h + 1) & C.fmask;
+        }
+    }
+    // (one flag atomic per workgroup at most, and none once the bit is up)
+    if (__syncthreads_or(dup) && threadIdx.x == 0) raise_flags(&C.fast_words[0], (u32)FL_SLOW);
 }
 
 __global__ __launch_bounds__(AF_THREADS) void ac_fast_index(Tables T, AcArgs C, u64 row_base, BlockInline bi) {
     const u32 flags = C.fast_words[0];
     const u32 i = blockIdx.x * AF_THREADS + threadIdx.x;
     __shared__ u32 s_blk[BLOCK_INLINE_WORDS];
-    if (bi.words) {  // a small call's batch block: to memory (the general path reads it there)
+    const bool inl = bi.words != 0;
+    if (inl) {  // a small call's batch block: to memory (the general path reads it there)
         if (threadIdx.x < bi.words) {
             s_blk[threadIdx.x] = bi.w[threadIdx.x];
             if (blockIdx.x == 0) bi.block[threadIdx.x] = bi.w[threadIdx.x];
         }
         __syncthreads();
-        C.b_start = s_blk;
-        C.b_ts = (const u64*)(s_blk + ((C.nb + 2) & ~1u));  // batch_ts_offset
     }
-    if (i < C.n && C.fpos[i] != NONE32) C.ftab[C.fpos[i]] = 0;  // (all-zero again)
+    const u32 ts_off = (C.nb + 2) & ~1u;  // batch_ts_offset
+    auto bstart = [&](u32 k) -> u32 { return inl ? s_blk[k] : C.b_start[k]; };
+    auto bts = [&](u32 b) -> u64 {
+        return inl ? ((u64)s_blk[ts_off + 2 * b + 1] << 32 | s_blk[ts_off + 2 * b]) : C.b_ts[b];
+    };
+    if ((flags & FL_NONMONO) && i < C.n && C.fpos[i] != NONE32) C.ftab[C.fpos[i]] = 0;  // (all-zero again)
     if (flags & FL_SLOW) {
         // the call goes to the general path: the directory entries the check wrote go
         if (i < C.n) {
@@ -417,7 +457,7 @@ __global__ __launch_bounds__(AF_THREADS) void ac_fast_index(Tables T, AcArgs C, 
             u64 mts = 0;
             for (u32 b = threadIdx.x; b < C.nb; b += AF_THREADS) {
                 C.counts_out[b] = 0;
-                if (C.b_start[b + 1] > C.b_start[b]) mts = max(mts, C.b_ts[b]);
+                if (bstart(b + 1) > bstart(b)) mts = max(mts, bts(b));
             }
             mts = wave_max_u64(mts);
             if (wave_leader() && mts) atomicMax((unsigned long long*)T.commit_ts, (unsigned long long)mts);
@@ -429,6 +469,10 @@ __global__ __launch_bounds__(AF_THREADS) void ac_fast_index(Tables T, AcArgs C, 
     // workgroup then takes a ticket, and the last one reads the final word: the counter
     // hand-off of MI355X_MICROARCH.md's sc1 forms.  The kernel's end makes the host
     // store visible to the host's wait on the stream.
+    // Only for small grids (flags_out set): the tickets are returning atomics on one
+    // word, ~12 ns each at the memory side, so 3907 workgroups (1M accounts) paid 47 us;
+    // a large call's host copies the flags after the kernel instead.
+    if (!C.flags_out) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -628,11 +672,15 @@ void ac_launch_mask(const Tables& T, const AcArgs& C, const u8* res, const u8* o
     ac_mask<<<GRID(C.n)>>>(T, C, res, ok, cfail, fres, mask, gate);
     ac_ts_fold<<<1, 1024, 0, stream>>>(C.ts_part, (C.n + 255) / 256, T.commit_ts, gate);
 }
+u32 ac_fast_index_grid(const AcArgs& C) { return (u32)((std::max(C.n, C.nb) + AF_THREADS - 1) / AF_THREADS); }
 void ac_launch_fast(const Tables& T, const AcArgs& C, u64 row_base, const BlockInline& bi, hipStream_t stream) {
     const u64 lanes = 8ull * C.n;
-    ac_fast_check<<<(u32)((lanes + AF_THREADS - 1) / AF_THREADS), AF_THREADS, 0, stream>>>(T, C, row_base, bi);
-    ac_fast_index<<<(u32)((std::max(C.n, C.nb) + AF_THREADS - 1) / AF_THREADS), AF_THREADS, 0, stream>>>(T, C, row_base,
-                                                                                                      bi);
+    if (bi.words)
+        ac_fast_check<true><<<(u32)((lanes + AF_THREADS - 1) / AF_THREADS), AF_THREADS, 0, stream>>>(T, C, row_base, bi);
+    else
+        ac_fast_check<false><<<(u32)((lanes + AF_THREADS - 1) / AF_THREADS), AF_THREADS, 0, stream>>>(T, C, row_base, bi);
+    ac_fast_dup<<<(u32)((C.n + AF_THREADS - 1) / AF_THREADS), AF_THREADS, 0, stream>>>(C);
+    ac_fast_index<<<ac_fast_index_grid(C), AF_THREADS, 0, stream>>>(T, C, row_base, bi);
     HIP_CHECK(hipGetLastError());
 }
 void ac_launch_apply(const Tables& T, const AcArgs& C, const u8* ok, const u8* fres, const uint4* rk, u64 row_base,

@@ -2702,11 +2702,16 @@ static void run_accounts_chunk(tbgpu_ctx* c, const Account* ev, u32 n, u32 nb,
         volatile u32* flags_host = c->h_report + RPT_COUNTS + c->bmax + 1;
         *flags_host = FL_SLOW | FL_ERROR;  // (a kernel that never stored it reads as failed)
         C.fast_words = c->ac_fast_words;
-        C.flags_out = c->h_report_dev + RPT_COUNTS + c->bmax + 1;
+        const bool ticket = ac_fast_index_grid(C) <= AC_TICKET_GRID_MAX;
+        C.flags_out = ticket ? c->h_report_dev + RPT_COUNTS + c->bmax + 1 : nullptr;
         const BlockInline bi = take_block(c);
         ac_launch_fast(c->T, C, c->n_accounts, bi, s);
+        if (!ticket) {  // (into ordinary page-locked memory: a copy into the coherent report took longer)
+            HIP_CHECK(hipMemcpyAsync(c->h_counters, c->ac_fast_words, sizeof(u32), hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipMemsetAsync(c->ac_fast_words, 0, 2 * sizeof(u32), s));
+        }
         wait_stream(s);
-        const u32 flags = *flags_host;
+        const u32 flags = ticket ? *flags_host : c->h_counters[0];
         if (flags & FL_ERROR) tbgpu_fatal("create_accounts", "the clean call reported no outcome", __FILE__, __LINE__);
         if (!(flags & FL_SLOW)) {
             if (flags & FL_CAPACITY)

@@ -144,8 +144,9 @@ struct AcArgs {
     u32* fpos;
     u64 fmask;
     // the clean call's outcome: its flags and ac_fast_index's ticket in fast_words[0..1]
-    // (a pair of its own, all-zero between calls: the last workgroup reads and resets
-    // them), the flags stored to flags_out (page-locked host memory, its device address)
+    // (a pair of its own, all-zero between calls); for a small call (flags_out set) the
+    // last workgroup stores the flags to flags_out (page-locked host memory, its device
+    // address) and zeroes the pair, otherwise the host copies and zeroes them
     u32* fast_words;
     u32* flags_out;
 };
@@ -156,6 +157,8 @@ struct AcArgs {
 // ac_fast_check reads it there, ac_fast_index writes it for the general path).
 struct BlockInline;
 void ac_launch_fast(const Tables& T, const AcArgs& C, u64 row_base, const BlockInline& bi, hipStream_t stream);
+u32 ac_fast_index_grid(const AcArgs& C);
+constexpr u32 AC_TICKET_GRID_MAX = 64;  // ac_fast_index grids up to this size report by ticket
 void ac_launch_classify(const Tables& T, const AcArgs& C, hipStream_t stream);
 void ac_launch_group_sort(const AcArgs& C, u32 invalid, int bits, u32* k_in, u32* v_in, u32* k_out, u32* v_out,
                           SortScratch& ss, hipStream_t stream);

@@ -6,7 +6,7 @@ OUT=${1:?}; REPS=${2:?}; shift 2
 mkdir -p "$OUT"
 for rep in $(seq 1 "$REPS"); do
   for spec in "$@"; do
-    tag=${spec:-default}
+    tag=${spec:-default}; tag=${tag//\//_}
     env $spec timeout -k 10 300 python3 -u bench.py --config 3 --steps 5 --warmup 2 --no-cpu --no-queries --no-host \
       --no-subconfigs > "$OUT/$tag.$rep.json" 2> "$OUT/$tag.$rep.err" || exit 1
     python3 -c "
